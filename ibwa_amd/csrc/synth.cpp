@@ -1,0 +1,282 @@
+// synth.cpp -- deterministic synthetic genome + read generator.
+//
+// SURVEY.md §8(d) fixes the synthetic workload: a GRCh37-sized genome (24
+// contigs with the chr1..22/X/Y lengths, seeded repeat families, N runs)
+// and 100 bp reads with 1 % substitutions and 5 % of reads carrying one
+// 1-3 bp indel, qualities 'I'.  Every random draw comes from splitmix64
+// keyed by (seed, stream, index) so the output is identical for any thread
+// count and on any host -- no libc / numpy RNG anywhere.
+//
+// N handling mirrors the reference packer: bns_fasta2bntseq (bntseq.c:180-224)
+// replaces every ambiguous base, in file order, by lrand48()&3 after
+// srand48(11).  ibwa_pack_nt4() restates that with the POSIX 48-bit LCG so
+// the repo-owned index builder produces the same .pac as `bwa index`.
+#include <cstdint>
+#include <cstring>
+#include <cstdlib>
+#include <vector>
+#include <thread>
+#include <algorithm>
+
+namespace {
+
+inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+// counter-based draw: value #idx of stream `stream` under `seed`
+inline uint64_t draw(uint64_t seed, uint64_t stream, uint64_t idx) {
+  return splitmix64(splitmix64(seed * 0x100000001B3ull ^ stream) + idx);
+}
+inline double unif(uint64_t r) { return (r >> 11) * (1.0 / 9007199254740992.0); }
+
+const char kACGT[4] = {'A', 'C', 'G', 'T'};
+
+// GRCh37 primary assembly lengths, chr1..22, X, Y (hg19 .fai)
+const uint64_t kGRCh37[24] = {
+    249250621, 243199373, 198022430, 191154276, 180915260, 171115067,
+    159138663, 146364022, 141213431, 135534747, 135006516, 133851895,
+    115169878, 107349540, 102531392, 90354753,  81195210,  78077248,
+    59128983,  63025520,  48129895,  51304566,  155270560, 59373566};
+
+inline char comp(char b) {
+  return b == 'A' ? 'T' : b == 'C' ? 'G' : b == 'G' ? 'C' : b == 'T' ? 'A' : 'N';
+}
+
+struct Family {
+  uint64_t off;  // offset of consensus in the family pool
+  uint32_t len;
+  double div;    // per-copy divergence
+};
+
+}  // namespace
+
+extern "C" {
+
+// Fill `lens[24]` with GRCh37 contig lengths scaled by num/den (min 1000).
+// Returns the total length.
+uint64_t ibwa_synth_grch37_lengths(uint64_t num, uint64_t den, uint64_t *lens) {
+  uint64_t tot = 0;
+  for (int i = 0; i < 24; ++i) {
+    uint64_t l = kGRCh37[i] * num / den;
+    if (l < 1000) l = 1000;
+    lens[i] = l;
+    tot += l;
+  }
+  return tot;
+}
+
+// Generate an ASCII genome into `out` (total = sum(lens) bytes, no newlines).
+//   repeat_frac : fraction of bases covered by mutated copies of repeat families
+//   n_frac      : approx. fraction of bases in N runs (telomeres + one internal gap per contig)
+// Deterministic in (seed, lens, params) regardless of n_threads.
+void ibwa_synth_genome(uint64_t seed, int n_contigs, const uint64_t *lens,
+                       double repeat_frac, double n_frac, int n_families,
+                       char *out, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  uint64_t total = 0;
+  for (int c = 0; c < n_contigs; ++c) total += lens[c];
+  // 1. unique background, GC ~41 %; parallel over 1 Mb chunks
+  const uint64_t CH = 1u << 20;
+  uint64_t n_chunks = (total + CH - 1) / CH;
+  auto bg = [&](int t) {
+    for (uint64_t ch = t; ch < n_chunks; ch += n_threads) {
+      uint64_t b = ch * CH, e = std::min(total, b + CH);
+      for (uint64_t i = b; i < e; ++i) {
+        uint64_t r = draw(seed, 1, i);
+        double u = unif(r);
+        // P(A)=P(T)=0.295, P(C)=P(G)=0.205
+        out[i] = u < 0.295 ? 'A' : u < 0.5 ? 'C' : u < 0.705 ? 'G' : 'T';
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t) th.emplace_back(bg, t);
+    for (auto &x : th) x.join();
+  }
+  // 2. repeat families: consensus lengths 300..6000, divergence 2..20 %
+  if (n_families < 1) n_families = 1;
+  std::vector<Family> fam(n_families);
+  uint64_t pool_len = 0;
+  for (int f = 0; f < n_families; ++f) {
+    uint64_t r = draw(seed, 2, f);
+    // skew toward short elements (Alu-like ~300 bp are the most common)
+    double u = unif(r);
+    fam[f].len = (uint32_t)(300 + (uint64_t)(u * u * 5700));
+    fam[f].div = 0.02 + 0.18 * unif(draw(seed, 3, f));
+    fam[f].off = pool_len;
+    pool_len += fam[f].len;
+  }
+  std::vector<char> pool(pool_len);
+  for (uint64_t i = 0; i < pool_len; ++i) pool[i] = kACGT[draw(seed, 4, i) & 3];
+  // copies placed per contig, deterministically; each contig is one task
+  std::vector<uint64_t> coff(n_contigs + 1, 0);
+  for (int c = 0; c < n_contigs; ++c) coff[c + 1] = coff[c] + lens[c];
+  auto rep = [&](int t) {
+    for (int c = t; c < n_contigs; c += n_threads) {
+      uint64_t L = lens[c], base = coff[c];
+      uint64_t target = (uint64_t)(repeat_frac * L), covered = 0, k = 0;
+      uint64_t stream = 100 + (uint64_t)c * 4;
+      while (covered < target && k < (1ull << 40)) {
+        uint64_t r0 = draw(seed, stream, k * 4 + 0);
+        uint64_t r1 = draw(seed, stream, k * 4 + 1);
+        ++k;
+        const Family &F = fam[r0 % n_families];
+        if (F.len >= L) continue;
+        uint64_t pos = r1 % (L - F.len);
+        bool rc = (r0 >> 40) & 1;
+        for (uint32_t j = 0; j < F.len; ++j) {
+          uint64_t rr = draw(seed, stream + 1, (k << 13) ^ j ^ (pos << 20));
+          char b = rc ? comp(pool[F.off + F.len - 1 - j]) : pool[F.off + j];
+          if (unif(rr) < F.div) b = kACGT[(rr >> 3) & 3];
+          out[base + pos + j] = b;
+        }
+        covered += F.len;
+      }
+      // a few microsatellites (tandem repeats), 0.5 % of the contig
+      uint64_t ms_target = L / 200, ms_cov = 0, m = 0;
+      while (ms_cov < ms_target && m < (1ull << 32)) {
+        uint64_t r = draw(seed, stream + 2, m++);
+        uint32_t unit = 1 + (r & 5);             // 1..6
+        uint32_t rl = 20 + ((r >> 8) % 180);     // 20..199 bp
+        if (rl + 8 >= L) break;
+        uint64_t pos = (r >> 20) % (L - rl);
+        char motif[8];
+        for (uint32_t q = 0; q < unit; ++q) motif[q] = kACGT[(r >> (40 + 2 * q)) & 3];
+        for (uint32_t j = 0; j < rl; ++j) out[base + pos + j] = motif[j % unit];
+        ms_cov += rl;
+      }
+      // N runs: 10 kb telomeres (scaled) + one internal gap
+      uint64_t tel = std::min<uint64_t>(10000, (uint64_t)(n_frac * L / 4));
+      uint64_t gap = (uint64_t)(n_frac * L) > 2 * tel ? (uint64_t)(n_frac * L) - 2 * tel : 0;
+      if (n_frac > 0) {
+        for (uint64_t j = 0; j < tel && j < L; ++j) out[base + j] = 'N';
+        for (uint64_t j = 0; j < tel && j < L; ++j) out[base + L - 1 - j] = 'N';
+        if (gap > 0 && L > gap + 2 * tel) {
+          uint64_t gpos = tel + draw(seed, stream + 3, 0) % (L - gap - 2 * tel);
+          for (uint64_t j = 0; j < gap; ++j) out[base + gpos + j] = 'N';
+        }
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t) th.emplace_back(rep, t);
+    for (auto &x : th) x.join();
+  }
+}
+
+// POSIX drand48 family: X' = (a X + c) mod 2^48; srand48(s): X = s<<16 | 0x330E;
+// lrand48() = X' >> 17.  Used to restate bntseq.c:181,224 exactly.
+static inline uint64_t lcg48(uint64_t x) {
+  return (0x5DEECE66Dull * x + 0xBull) & ((1ull << 48) - 1);
+}
+
+// Pack ASCII to 2-bit codes (one byte per base, 0..3) the way `bwa index`
+// builds .pac: nst_nt4_table (bntseq.c:39-56) then N -> lrand48()&3 in order.
+// Returns the number of ambiguous bases replaced.
+uint64_t ibwa_pack_nt4(const char *ascii, uint64_t n, uint8_t *codes) {
+  uint64_t x = (11ull << 16) | 0x330E, n_amb = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    int c;
+    switch (ascii[i]) {
+      case 'A': case 'a': c = 0; break;
+      case 'C': case 'c': c = 1; break;
+      case 'G': case 'g': c = 2; break;
+      case 'T': case 't': c = 3; break;
+      default: c = 4;
+    }
+    if (c == 4) {
+      x = lcg48(x);
+      c = (int)((x >> 17) & 3);
+      ++n_amb;
+    }
+    codes[i] = (uint8_t)c;
+  }
+  return n_amb;
+}
+
+// Draw `n_reads` single-end reads of length `len` from `ascii` (length n,
+// contigs concatenated; reads never span a contig boundary or an N).
+//   sub_rate   : i.i.d. substitution probability (uniform alternative base)
+//   indel_frac : fraction of reads carrying one 1-3 bp indel in [10, len-10)
+// Output: `seqs` (n_reads*len ASCII bases, fixed stride len), `pos` (0-based
+// leftmost genome coordinate), `strand` (0 fwd / 1 rev).  Deterministic in
+// (seed, index) for any thread count.
+void ibwa_synth_reads(uint64_t seed, const char *ascii, uint64_t n, int n_contigs,
+                      const uint64_t *lens, uint64_t n_reads, int len, double sub_rate,
+                      double indel_frac, char *seqs, uint64_t *pos, uint8_t *strand,
+                      int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  std::vector<uint64_t> coff(n_contigs + 1, 0);
+  for (int c = 0; c < n_contigs; ++c) coff[c + 1] = coff[c] + lens[c];
+  const int span = len + 3;
+  auto work = [&](int t) {
+    std::vector<char> win(span + 8), rd(len + 8);
+    for (uint64_t r = t; r < n_reads; r += n_threads) {
+      uint64_t k = 0;
+      for (;;) {
+        uint64_t x = draw(seed, 10, r * 64 + k++);
+        uint64_t p = x % (n > (uint64_t)span ? n - span : 1);
+        int ci = (int)(std::upper_bound(coff.begin(), coff.end(), p) - coff.begin()) - 1;
+        if (p + span > coff[ci + 1]) continue;
+        bool ok = true;
+        for (int j = 0; j < span; ++j) {
+          char b = ascii[p + j];
+          if (b != 'A' && b != 'C' && b != 'G' && b != 'T') { ok = false; break; }
+        }
+        if (!ok && k < 4096) continue;
+        pos[r] = p;
+        break;
+      }
+      uint64_t p = pos[r];
+      uint64_t y = draw(seed, 11, r);
+      bool rc = y & 1;
+      strand[r] = rc;
+      // optional indel
+      int ilen = 0, ipos = 0, is_ins = 0;
+      if (unif(draw(seed, 12, r)) < indel_frac && len > 24) {
+        uint64_t z = draw(seed, 13, r);
+        ilen = 1 + (int)(z % 3);
+        ipos = 10 + (int)((z >> 8) % (uint64_t)(len - 20));
+        is_ins = (z >> 20) & 1;
+      }
+      // build the read from the forward reference window
+      int wi = 0;
+      for (int j = 0; j < len; ++j) {
+        if (ilen && j == ipos) {
+          if (is_ins) {
+            for (int q = 0; q < ilen && j < len; ++q, ++j)
+              rd[j] = kACGT[draw(seed, 14, r * 8 + q) & 3];
+            if (j >= len) break;
+          } else {
+            wi += ilen;  // deletion: skip reference bases
+          }
+        }
+        rd[j] = ascii[p + wi++];
+      }
+      // substitutions
+      for (int j = 0; j < len; ++j) {
+        uint64_t s = draw(seed, 15, r * 1024 + j);
+        if (unif(s) < sub_rate) {
+          int c = (int)(std::find(kACGT, kACGT + 4, rd[j]) - kACGT);
+          if (c < 4) rd[j] = kACGT[(c + 1 + (int)((s >> 7) % 3)) & 3];
+        }
+      }
+      char *o = seqs + r * (uint64_t)len;
+      if (rc) {
+        for (int j = 0; j < len; ++j) o[j] = comp(rd[len - 1 - j]);
+      } else {
+        memcpy(o, rd.data(), len);
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < n_threads; ++t) th.emplace_back(work, t);
+  for (auto &x : th) x.join();
+}
+
+}  // extern "C"

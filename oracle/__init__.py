@@ -1,0 +1,261 @@
+"""oracle -- TEST INFRASTRUCTURE ONLY.
+
+CPU restatement of the reference `ibwa aln` hot path, used by tests/,
+``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg as the checker
+(or the timed CPU baseline).  The shipped product (ibwa_amd/, include/) never
+imports it.  Parity of this restatement is pinned against golden vectors made
+by the compiled reference (tests/golden/, tools/make_golden.py).
+"""
+import ctypes
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_ref", "liboracle.so")
+REF_BIN = os.path.join(HERE, "_ref", "ibwa_ref")
+REF_LIB = os.path.join(HERE, "_ref", "libibwa_ref.so")
+
+MODE_GAPE, MODE_COMPREAD, MODE_LOGGAP, MODE_NONSTOP = 0x01, 0x02, 0x04, 0x10
+MODE_BAM, MODE_BAM_SE, MODE_BAM_READ1, MODE_BAM_READ2, MODE_IL13 = 0x20, 0x40, 0x80, 0x100, 0x200
+
+
+class GapOpt(ctypes.Structure):
+    """gap_opt_t (bwtaln.h:105-115) -- also the 64-byte .sai header."""
+    _fields_ = [(n, ctypes.c_int) for n in ("s_mm", "s_gapo", "s_gape", "mode", "indel_end_skip",
+                                            "max_del_occ", "max_entries")] + \
+               [("fnr", ctypes.c_float)] + \
+               [(n, ctypes.c_int) for n in ("max_diff", "max_gapo", "max_gape", "max_seed_diff",
+                                            "seed_len", "n_threads", "max_top2", "trim_qual")]
+
+
+assert ctypes.sizeof(GapOpt) == 64
+
+ALN_DTYPE = np.dtype([("info", "<u4"), ("k", "<u4"), ("l", "<u4"), ("score", "<i4")])  # bwtaln.h:34-38
+
+
+def build(quiet=True):
+    """Compile the restatement (gcc) -- building the checker, not using it."""
+    kw = {"stdout": subprocess.DEVNULL} if quiet else {}
+    subprocess.run(["make", "-C", HERE, "oracle"], check=True, **kw)
+
+
+def build_ref(quiet=True):
+    """Compile the reference from /root/reference into oracle/_ref (build container only)."""
+    if not os.path.isdir("/root/reference"):
+        return False
+    kw = {"stdout": subprocess.DEVNULL, "stderr": subprocess.DEVNULL} if quiet else {}
+    subprocess.run(["make", "-C", HERE, "ref", "-j8"], check=True, **kw)
+    return True
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        c = ctypes
+        L.or_bwt_load.restype = c.c_void_p
+        L.or_bwt_load.argtypes = [c.c_char_p]
+        L.or_bwt_wrap.restype = c.c_void_p
+        L.or_bwt_wrap.argtypes = [c.c_uint32, c.POINTER(c.c_uint32), c.c_void_p, c.c_uint64]
+        L.or_bwt_free.argtypes = [c.c_void_p]
+        L.or_occ.restype = c.c_uint32
+        L.or_occ.argtypes = [c.c_void_p, c.c_uint32, c.c_int]
+        L.or_occ4.argtypes = [c.c_void_p, c.c_uint32, c.POINTER(c.c_uint32)]
+        L.or_cal_maxdiff.restype = c.c_int
+        L.or_cal_maxdiff.argtypes = [c.c_int, c.c_double, c.c_double]
+        L.or_gap_init_opt.argtypes = [c.POINTER(GapOpt)]
+        L.or_cal_sa_reg_gap.restype = c.c_int64
+        L.or_cal_sa_reg_gap.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p,
+                                        c.c_void_p, c.POINTER(GapOpt), c.c_int, c.c_void_p,
+                                        c.POINTER(c.c_void_p), c.c_void_p]
+        L.or_free.argtypes = [c.c_void_p]
+        if hasattr(L, "or_aln_local_core"):
+            L.or_aln_local_core.restype = c.c_int
+            L.or_aln_local_core.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
+                                            c.POINTER(c.c_int), c.c_int, c.c_void_p]
+        _lib = L
+    return _lib
+
+
+class Bwt:
+    """An index loaded by the restatement of bwt_restore_bwt (bwtio.c:51)."""
+
+    def __init__(self, path=None, primary=None, L2=None, words=None):
+        L = lib()
+        if path is not None:
+            self.h = L.or_bwt_load(path.encode())
+            if not self.h:
+                raise IOError(path)
+            self._keep = None
+        else:
+            self._keep = np.ascontiguousarray(words, dtype=np.uint32)
+            arr = (ctypes.c_uint32 * 4)(*[int(x) for x in L2])
+            self.h = L.or_bwt_wrap(int(primary), arr, self._keep.ctypes.data, self._keep.size)
+
+    def occ4(self, k):
+        out = (ctypes.c_uint32 * 4)()
+        lib().or_occ4(self.h, k & 0xFFFFFFFF, out)
+        return tuple(out)
+
+    def __del__(self):
+        try:
+            lib().or_bwt_free(self.h)
+        except Exception:
+            pass
+
+
+def default_opt():
+    o = GapOpt()
+    lib().or_gap_init_opt(ctypes.byref(o))
+    return o
+
+
+def parse_aln_args(argv):
+    """Restates bwa_aln's getopt loop (bwtaln.c:249-284).  Returns (opt, rest)."""
+    import getopt
+    o = default_opt()
+    opte = -1
+    opts, rest = getopt.getopt(argv, "n:o:e:i:d:l:k:cLR:m:t:NM:O:E:q:f:b012IB:")
+    for k, v in opts:
+        if k == "-n":
+            if "." in v:
+                o.fnr, o.max_diff = float(v), -1
+            else:
+                o.max_diff, o.fnr = int(v), -1.0
+        elif k == "-o": o.max_gapo = int(v)
+        elif k == "-e": opte = int(v)
+        elif k == "-M": o.s_mm = int(v)
+        elif k == "-O": o.s_gapo = int(v)
+        elif k == "-E": o.s_gape = int(v)
+        elif k == "-d": o.max_del_occ = int(v)
+        elif k == "-i": o.indel_end_skip = int(v)
+        elif k == "-l": o.seed_len = int(v)
+        elif k == "-k": o.max_seed_diff = int(v)
+        elif k == "-m": o.max_entries = int(v)
+        elif k == "-t": o.n_threads = int(v)
+        elif k == "-L": o.mode |= MODE_LOGGAP
+        elif k == "-R": o.max_top2 = int(v)
+        elif k == "-q": o.trim_qual = int(v)
+        elif k == "-c": o.mode &= ~MODE_COMPREAD
+        elif k == "-N": o.mode |= MODE_NONSTOP; o.max_top2 = 0x7fffffff
+        elif k == "-b": o.mode |= MODE_BAM
+        elif k == "-0": o.mode |= MODE_BAM_SE
+        elif k == "-1": o.mode |= MODE_BAM_READ1
+        elif k == "-2": o.mode |= MODE_BAM_READ2
+        elif k == "-I": o.mode |= MODE_IL13
+        elif k == "-B": o.mode |= int(v) << 24
+    if opte > 0:
+        o.max_gape = opte
+        o.mode &= ~MODE_GAPE
+    return o, rest
+
+
+_NT4 = np.full(256, 4, dtype=np.uint8)
+for _c, _v in zip(b"ACGTacgt", [0, 1, 2, 3, 0, 1, 2, 3]):
+    _NT4[_c] = _v
+_NT4[ord("-")] = 5  # bntseq.c:39-56
+
+
+def read_fastq_records(path):
+    """Minimal kseq_read (kseq.h:156): name = first token, seq/qual printable chars."""
+    recs = []
+    with open(path, "rb") as f:
+        lines = f.read().split(b"\n")
+    i = 0
+    while i < len(lines):
+        h = lines[i]
+        if not h or h[:1] not in (b"@", b">"):
+            i += 1
+            continue
+        name = h[1:].split()[0].decode()
+        seq = lines[i + 1].strip()
+        qual = b""
+        i += 2
+        if i < len(lines) and lines[i][:1] == b"+":
+            qual = lines[i + 1].strip()
+            i += 2
+        recs.append((name, seq, qual))
+    return recs
+
+
+def encode_reads(recs, mode, trim_qual):
+    """Restates bwa_read_seq (bwaseqio.c:145-208) for FASTQ input.
+
+    Returns (seq_concat uint8, offsets uint64, lens uint32): seq is the
+    bwa_seq_t.seq array -- codes of the (trimmed) read, reversed.
+    """
+    is_64 = mode & MODE_IL13
+    l_bc = (mode >> 24) & 0xff
+    out, offs, lens = [], [], []
+    off = 0
+    for name, seq, qual in recs:
+        if is_64 and qual:
+            qual = bytes(q - 31 for q in qual)
+        if len(seq) <= l_bc:
+            continue
+        if l_bc:
+            seq = seq[l_bc:]
+            if qual:
+                qual = qual[l_bc:]
+        codes = _NT4[np.frombuffer(seq, dtype=np.uint8)]
+        L = len(codes)
+        if qual and trim_qual >= 1:  # bwa_trim_read (bwaseqio.c:74-87)
+            s = mx = 0
+            max_l = L - 1
+            for l in range(L - 1, 35 - 2, -1):  # l >= BWA_MIN_RDLEN - 1
+                s += trim_qual - (qual[l] - 33)
+                if s < 0:
+                    break
+                if s > mx:
+                    mx, max_l = s, l
+            L = max_l + 1
+        out.append(codes[:L][::-1].copy())
+        offs.append(off)
+        lens.append(L)
+        off += L
+    seqs = np.concatenate(out) if out else np.zeros(0, np.uint8)
+    return seqs, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
+
+
+def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False):
+    """Run the restated bwa_cal_sa_reg_gap.  Returns (n_aln int32[n], alns ALN_DTYPE[...], touches)."""
+    L = lib()
+    n = len(lens)
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    n_aln = np.zeros(n, dtype=np.int32)
+    tch = np.zeros(n, dtype=np.uint32) if touches else None
+    ptr = ctypes.c_void_p()
+    tot = L.or_cal_sa_reg_gap(bwt0.h, bwt1.h, n, seqs.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                              ctypes.byref(opt), n_threads, n_aln.ctypes.data, ctypes.byref(ptr),
+                              tch.ctypes.data if touches else None)
+    buf = ctypes.string_at(ptr.value, max(tot, 0) * 16)
+    L.or_free(ptr)
+    alns = np.frombuffer(buf, dtype=ALN_DTYPE).copy()
+    return n_aln, alns, tch
+
+
+def sai_bytes(opt, n_aln, alns, batch=0x40000):
+    """bwtaln.c:192,227-231: 64 B gap_opt_t header, then per read int32 n_aln + n_aln x 16 B."""
+    parts = [bytes(opt)]
+    p = 0
+    for n in n_aln:
+        parts.append(struct.pack("<i", int(n)))
+        if n:
+            parts.append(alns[p:p + n].tobytes())
+            p += n
+    return b"".join(parts)
+
+
+def sai_body_equal(a, b):
+    """Compare .sai files, masking header bytes 52..55 (gap_opt_t.n_threads)."""
+    return a[:52] == b[:52] and a[56:64] == b[56:64] and a[64:] == b[64:]

@@ -1,0 +1,607 @@
+/*
+ * ibwa_oracle.c -- TEST INFRASTRUCTURE ONLY (checker + CPU baseline).
+ *
+ * A plain-C restatement of the reference aln hot path.  Each function names
+ * the reference lines it follows.  It is pinned against the golden .sai /
+ * Occ fixtures produced by the compiled reference (tests/golden/), and it is
+ * the `cpu_baseline` kind "port" in bench.py.  The shipped product never
+ * links, loads or calls it.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "ibwa_oracle.h"
+
+#define OCC_INTERVAL 128 /* bwt.h:34 */
+#define THREAD_BLOCK 1024 /* bwtaln.c:16 */
+
+/* ---------------- index (bwtio.c:51-70, bwt.h:56-63) ---------------- */
+
+or_bwt_t *or_bwt_load(const char *fn)
+{
+	FILE *fp = fopen(fn, "rb");
+	or_bwt_t *b;
+	long sz;
+	if (!fp) return 0;
+	b = (or_bwt_t*)calloc(1, sizeof(*b));
+	fseek(fp, 0, SEEK_END);
+	sz = ftell(fp);
+	b->bwt_size = (uint32_t)((sz - 20) >> 2);
+	b->bwt = (uint32_t*)malloc((size_t)b->bwt_size * 4);
+	fseek(fp, 0, SEEK_SET);
+	if (fread(&b->primary, 4, 1, fp) != 1 || fread(b->L2 + 1, 4, 4, fp) != 4 ||
+	    fread(b->bwt, 4, b->bwt_size, fp) != b->bwt_size) {
+		fclose(fp); free(b->bwt); free(b); return 0;
+	}
+	fclose(fp);
+	b->L2[0] = 0;
+	b->seq_len = b->L2[4];
+	b->owns = 1;
+	return b;
+}
+
+or_bwt_t *or_bwt_wrap(uint32_t primary, const uint32_t L2_1to4[4], uint32_t *words, uint64_t n_words)
+{
+	or_bwt_t *b = (or_bwt_t*)calloc(1, sizeof(*b));
+	b->primary = primary;
+	b->L2[0] = 0;
+	memcpy(b->L2 + 1, L2_1to4, 16);
+	b->seq_len = b->L2[4];
+	b->bwt_size = (uint32_t)n_words;
+	b->bwt = words;
+	b->owns = 0;
+	return b;
+}
+
+void or_bwt_free(or_bwt_t *b)
+{
+	if (!b) return;
+	if (b->owns) free(b->bwt);
+	free(b);
+}
+
+void or_free(void *p) { free(p); }
+
+/* ---------------- rank queries (bwt.c:81-214) ---------------- */
+
+/* number of symbol c among the 2-bit bases of y (bwt.c:81-88) */
+static inline int cnt2(uint64_t y, int c)
+{
+	y = ((c & 2) ? y : ~y) >> 1 & ((c & 1) ? y : ~y) & 0x5555555555555555ull;
+	return __builtin_popcountll(y);
+}
+
+/* 4 bytes of per-symbol counts for one 16-base word (bwt.c:36-45,153-155) */
+static inline uint32_t cnt4(uint32_t w)
+{
+	uint32_t x = 0;
+	int i;
+	for (i = 0; i < 16; ++i) x += 1u << (((w >> (30 - 2 * i)) & 3) << 3);
+	return x;
+}
+
+static inline const uint32_t *occ_intv(const or_bwt_t *b, uint32_t k) { return b->bwt + (k / OCC_INTERVAL) * 12; }
+
+/* Occ(c, k): bwt.c:90-113 -- count of c in BWT[0..k] with $ removed */
+static uint32_t occ_t(const or_bwt_t *b, uint32_t k, int c, uint32_t *t)
+{
+	uint32_t n, j, i;
+	const uint32_t *p;
+	if (k == b->seq_len) return b->L2[c + 1] - b->L2[c];
+	if (k == (uint32_t)-1) return 0;
+	++*t;
+	if (k >= b->primary) --k;
+	p = occ_intv(b, k);
+	n = p[c];
+	p += 4;
+	j = k >> 5 << 5;
+	for (i = k / OCC_INTERVAL * OCC_INTERVAL; i < j; i += 32, p += 2)
+		n += cnt2((uint64_t)p[0] << 32 | p[1], c);
+	n += cnt2(((uint64_t)p[0] << 32 | p[1]) & ~((1ull << ((~k & 31) << 1)) - 1), c);
+	if (c == 0) n -= ~k & 31; /* masked bases read as A */
+	return n;
+}
+
+uint32_t or_occ(const or_bwt_t *b, uint32_t k, int c) { uint32_t t = 0; return occ_t(b, k, c, &t); }
+
+/* bwt.c:116-151 */
+static void twoocc_t(const or_bwt_t *b, uint32_t k, uint32_t l, int c, uint32_t *ok, uint32_t *ol, uint32_t *t)
+{
+	uint32_t _k, _l;
+	if (k == l) { *ok = *ol = occ_t(b, k, c, t); return; }
+	_k = k >= b->primary ? k - 1 : k;
+	_l = l >= b->primary ? l - 1 : l;
+	if (_l / OCC_INTERVAL != _k / OCC_INTERVAL || k == (uint32_t)-1 || l == (uint32_t)-1) {
+		*ok = occ_t(b, k, c, t);
+		*ol = occ_t(b, l, c, t);
+	} else {
+		/* same interval: one block serves both ends */
+		uint32_t m, n, i, j;
+		const uint32_t *p;
+		++*t;
+		k = _k; l = _l;
+		p = occ_intv(b, k);
+		n = p[c];
+		p += 4;
+		j = k >> 5 << 5;
+		for (i = k / OCC_INTERVAL * OCC_INTERVAL; i < j; i += 32, p += 2)
+			n += cnt2((uint64_t)p[0] << 32 | p[1], c);
+		m = n;
+		n += cnt2(((uint64_t)p[0] << 32 | p[1]) & ~((1ull << ((~k & 31) << 1)) - 1), c);
+		if (c == 0) n -= ~k & 31;
+		*ok = n;
+		j = l >> 5 << 5;
+		for (; i < j; i += 32, p += 2)
+			m += cnt2((uint64_t)p[0] << 32 | p[1], c);
+		m += cnt2(((uint64_t)p[0] << 32 | p[1]) & ~((1ull << ((~l & 31) << 1)) - 1), c);
+		if (c == 0) m -= ~l & 31;
+		*ol = m;
+	}
+}
+
+/* bwt.c:157-174 */
+static void occ4_t(const or_bwt_t *b, uint32_t k, uint32_t cnt[4], uint32_t *t)
+{
+	uint32_t i, j, x;
+	const uint32_t *p;
+	if (k == (uint32_t)-1) { memset(cnt, 0, 16); return; }
+	++*t;
+	if (k >= b->primary) --k;
+	p = occ_intv(b, k);
+	memcpy(cnt, p, 16);
+	p += 4;
+	j = k >> 4 << 4;
+	for (i = k / OCC_INTERVAL * OCC_INTERVAL, x = 0; i < j; i += 16, ++p) x += cnt4(*p);
+	x += cnt4(*p & ~((1U << ((~k & 15) << 1)) - 1)) - (~k & 15);
+	cnt[0] += x & 0xff; cnt[1] += x >> 8 & 0xff; cnt[2] += x >> 16 & 0xff; cnt[3] += x >> 24;
+}
+
+void or_occ4(const or_bwt_t *b, uint32_t k, uint32_t cnt[4]) { uint32_t t = 0; occ4_t(b, k, cnt, &t); }
+
+/* bwt.c:177-214 */
+static void twoocc4_t(const or_bwt_t *b, uint32_t k, uint32_t l, uint32_t ck[4], uint32_t cl[4], uint32_t *t)
+{
+	uint32_t _k, _l;
+	if (k == l) { occ4_t(b, k, ck, t); memcpy(cl, ck, 16); return; }
+	_k = k >= b->primary ? k - 1 : k;
+	_l = l >= b->primary ? l - 1 : l;
+	if (_l / OCC_INTERVAL != _k / OCC_INTERVAL || k == (uint32_t)-1 || l == (uint32_t)-1) {
+		occ4_t(b, k, ck, t);
+		occ4_t(b, l, cl, t);
+	} else {
+		uint32_t i, j, x, y;
+		const uint32_t *p;
+		++*t;
+		k = _k; l = _l;
+		p = occ_intv(b, k);
+		memcpy(ck, p, 16);
+		p += 4;
+		j = k >> 4 << 4;
+		for (i = k / OCC_INTERVAL * OCC_INTERVAL, x = 0; i < j; i += 16, ++p) x += cnt4(*p);
+		y = x;
+		x += cnt4(*p & ~((1U << ((~k & 15) << 1)) - 1)) - (~k & 15);
+		j = l >> 4 << 4;
+		for (; i < j; i += 16, ++p) y += cnt4(*p);
+		y += cnt4(*p & ~((1U << ((~l & 15) << 1)) - 1)) - (~l & 15);
+		memcpy(cl, ck, 16);
+		ck[0] += x & 0xff; ck[1] += x >> 8 & 0xff; ck[2] += x >> 16 & 0xff; ck[3] += x >> 24;
+		cl[0] += y & 0xff; cl[1] += y >> 8 & 0xff; cl[2] += y >> 16 & 0xff; cl[3] += y >> 24;
+	}
+}
+
+void or_2occ4(const or_bwt_t *b, uint32_t k, uint32_t l, uint32_t ck[4], uint32_t cl[4])
+{
+	uint32_t t = 0;
+	twoocc4_t(b, k, l, ck, cl, &t);
+}
+
+/* bwt.c:235-250: continue an exact backward search over str[0..len-1] */
+static int match_exact_alt(const or_bwt_t *b, int len, const uint8_t *str, uint32_t *k0, uint32_t *l0, uint32_t *t)
+{
+	int i;
+	uint32_t k = *k0, l = *l0, ok, ol;
+	for (i = len - 1; i >= 0; --i) {
+		int c = str[i];
+		if (c > 3) return 0;
+		twoocc_t(b, k - 1, l, c, &ok, &ol, t);
+		k = b->L2[c] + ok + 1;
+		l = b->L2[c] + ol;
+		if (k > l) return 0;
+	}
+	*k0 = k; *l0 = l;
+	return (int)(l - k + 1);
+}
+
+/* ---------------- options (bwtaln.c:21-51) ---------------- */
+
+void or_gap_init_opt(or_gap_opt_t *o)
+{
+	memset(o, 0, sizeof(*o));
+	o->s_mm = 3; o->s_gapo = 11; o->s_gape = 4;
+	o->max_diff = -1; o->max_gapo = 1; o->max_gape = 6;
+	o->indel_end_skip = 5; o->max_del_occ = 10; o->max_entries = 2000000;
+	o->mode = OR_MODE_GAPE | OR_MODE_COMPREAD;
+	o->seed_len = 32; o->max_seed_diff = 2;
+	o->fnr = 0.04f;
+	o->n_threads = 1;
+	o->max_top2 = 30;
+	o->trim_qual = 0;
+}
+
+/* smallest k with Poisson(l*err) upper tail < thres (bwtaln.c:39-51) */
+int or_cal_maxdiff(int l, double err, double thres)
+{
+	double elambda = exp(-l * err);
+	double sum, y = 1.0;
+	int k, x = 1;
+	for (k = 1, sum = elambda; k < 1000; ++k) {
+		y *= l * err;
+		x *= k;
+		sum += elambda * y / x;
+		if (1.0 - sum < thres) return k;
+	}
+	return 2;
+}
+
+/* ---------------- widths (bwtaln.c:54-78) ---------------- */
+
+typedef struct { uint32_t w; int bid; } width_t;
+
+static void cal_width(const or_bwt_t *b, int len, const uint8_t *str, width_t *width, uint32_t *t)
+{
+	uint32_t k = 0, l = b->seq_len, ok, ol;
+	int i, bid = 0;
+	for (i = 0; i < len; ++i) {
+		int c = str[i];
+		if (c < 4) {
+			twoocc_t(b, k - 1, l, c, &ok, &ol, t);
+			k = b->L2[c] + ok + 1;
+			l = b->L2[c] + ol;
+		}
+		if (k > l || c > 3) { k = 0; l = b->seq_len; ++bid; }
+		width[i].w = l - k + 1;
+		width[i].bid = bid;
+	}
+	width[len].w = 0;
+	width[len].bid = ++bid;
+}
+
+/* ---------------- bucketed LIFO priority stack (bwtgap.c:13-79) ---------------- */
+
+typedef struct {
+	uint32_t k, l;
+	int i, a, state, n_mm, n_gapo, n_gape, last_diff_pos, score;
+} entry_t;
+
+typedef struct { int n, m; entry_t *e; } bucket_t;
+typedef struct { int n_stacks, best, n_entries; bucket_t *b; } gstack_t;
+
+#define SCORE(m, o, e, p) ((m) * (p)->s_mm + (o) * (p)->s_gapo + (e) * (p)->s_gape)
+#define ST_M 0
+#define ST_I 1
+#define ST_D 2
+
+static gstack_t *gs_init(int md, int go, int ge, const or_gap_opt_t *o)
+{
+	gstack_t *s = (gstack_t*)calloc(1, sizeof(*s));
+	int i;
+	s->n_stacks = SCORE(md + 1, go + 1, ge + 1, o);
+	s->b = (bucket_t*)calloc(s->n_stacks, sizeof(bucket_t));
+	for (i = 0; i < s->n_stacks; ++i) { s->b[i].m = 4; s->b[i].e = (entry_t*)calloc(4, sizeof(entry_t)); }
+	return s;
+}
+
+static void gs_free(gstack_t *s)
+{
+	int i;
+	for (i = 0; i < s->n_stacks; ++i) free(s->b[i].e);
+	free(s->b); free(s);
+}
+
+static void gs_reset(gstack_t *s)
+{
+	int i;
+	for (i = 0; i < s->n_stacks; ++i) s->b[i].n = 0;
+	s->best = s->n_stacks;
+	s->n_entries = 0;
+}
+
+/* bwtgap.c:45-64.  last_diff_pos: a non-diff push keeps the value already in
+ * its slot, which for positive penalties is always the just-popped parent's
+ * (SURVEY §7); we pass the parent's value explicitly ("inherit"). */
+static void gs_push(gstack_t *s, int a, int i, uint32_t k, uint32_t l, int n_mm, int n_gapo, int n_gape,
+                    int state, int ldp, const or_gap_opt_t *o)
+{
+	int score = SCORE(n_mm, n_gapo, n_gape, o);
+	bucket_t *q;
+	entry_t *p;
+	if (score < 0 || score >= s->n_stacks) { fprintf(stderr, "[oracle] score %d out of range\n", score); abort(); }
+	q = s->b + score;
+	if (q->n == q->m) { q->m <<= 1; q->e = (entry_t*)realloc(q->e, q->m * sizeof(entry_t)); }
+	p = q->e + q->n;
+	p->k = k; p->l = l; p->i = i & 0xffff; p->a = a; p->state = state;
+	p->n_mm = n_mm & 0xff; p->n_gapo = n_gapo & 0xff; p->n_gape = n_gape & 0xff;
+	p->last_diff_pos = ldp;
+	p->score = score & 0x7ff; /* info = score<<21 keeps 11 bits */
+	++q->n;
+	++s->n_entries;
+	if (s->best > score) s->best = score;
+}
+
+static void gs_pop(gstack_t *s, entry_t *e)
+{
+	bucket_t *q = s->b + s->best;
+	*e = q->e[q->n - 1];
+	--q->n;
+	--s->n_entries;
+	if (q->n == 0 && s->n_entries) {
+		int i;
+		for (i = s->best + 1; i < s->n_stacks; ++i) if (s->b[i].n) break;
+		s->best = i;
+	} else if (s->n_entries == 0) s->best = s->n_stacks;
+}
+
+/* bwtgap.c:81-91 */
+static void gap_shadow(int x, uint32_t max, int last_diff_pos, width_t *w)
+{
+	int i, j;
+	for (i = j = 0; i < last_diff_pos; ++i) {
+		if (w[i].w > (uint32_t)x) w[i].w -= x;
+		else if (w[i].w == (uint32_t)x) { w[i].bid = 1; w[i].w = max - (++j); }
+	}
+}
+
+static int int_log2(uint32_t v) /* bwtgap.c:93-102 */
+{
+	int c = 0;
+	if (v & 0xffff0000u) { v >>= 16; c |= 16; }
+	if (v & 0xff00) { v >>= 8; c |= 8; }
+	if (v & 0xf0) { v >>= 4; c |= 4; }
+	if (v & 0xc) { v >>= 2; c |= 2; }
+	if (v & 0x2) c |= 1;
+	return c;
+}
+
+typedef struct { or_aln1_t *a; int n, m; } alnv_t;
+
+/* bwtgap.c:104-264 */
+static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq[2], width_t *w[2],
+                      width_t *seed_w[2], const or_gap_opt_t *opt, alnv_t *out, gstack_t *stack, uint32_t *t)
+{
+	int best_score = SCORE(opt->max_diff + 1, opt->max_gapo + 1, opt->max_gape + 1, opt);
+	int best_diff = opt->max_diff + 1, max_diff = opt->max_diff;
+	int best_cnt = 0, j, nN;
+	out->n = 0;
+	for (j = nN = 0; j < len; ++j) if (seq[0][j] > 3) ++nN;
+	if (nN > max_diff) return;
+
+	gs_reset(stack);
+	gs_push(stack, 0, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
+	gs_push(stack, 1, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
+
+	while (stack->n_entries) {
+		entry_t e;
+		int a, i, m, m_seed = 0, hit, allow_diff, allow_M, tmp;
+		uint32_t k, l, ck[4], cl[4], occ;
+		const or_bwt_t *bwt;
+		const uint8_t *str;
+		const width_t *sw = 0;
+		width_t *width;
+
+		if (stack->n_entries > opt->max_entries) break;
+		gs_pop(stack, &e);
+		k = e.k; l = e.l;
+		a = e.a; i = e.i;
+		if (!(opt->mode & OR_MODE_NONSTOP) && (uint32_t)e.score > (uint32_t)(best_score + opt->s_mm)) break;
+
+		m = max_diff - (e.n_mm + e.n_gapo);
+		if (opt->mode & OR_MODE_GAPE) m -= e.n_gape;
+		if (m < 0) continue;
+		bwt = bwts[1 - a]; str = seq[a]; width = w[a];
+		if (seed_w) {
+			sw = seed_w[a];
+			m_seed = opt->max_seed_diff - (e.n_mm + e.n_gapo);
+			if (opt->mode & OR_MODE_GAPE) m_seed -= e.n_gape;
+		}
+		if (i > 0 && m < width[i - 1].bid) continue;
+
+		hit = 0;
+		if (i == 0) hit = 1;
+		else if (m == 0 && (e.state == ST_M || (opt->mode & OR_MODE_GAPE) || e.n_gape == opt->max_gape)) {
+			if (match_exact_alt(bwt, i, str, &k, &l, t)) hit = 1;
+			else continue;
+		}
+		if (hit) {
+			int score = SCORE(e.n_mm, e.n_gapo, e.n_gape, opt), do_add = 1;
+			if (out->n == 0) {
+				best_score = score;
+				best_diff = e.n_mm + e.n_gapo;
+				if (opt->mode & OR_MODE_GAPE) best_diff += e.n_gape;
+				if (!(opt->mode & OR_MODE_NONSTOP))
+					max_diff = (best_diff + 1 > opt->max_diff) ? opt->max_diff : best_diff + 1;
+			}
+			if (score == best_score) best_cnt = (int)((uint32_t)best_cnt + (l - k + 1));
+			else if (best_cnt > opt->max_top2) break;
+			if (e.n_gapo) {
+				for (j = 0; j < out->n; ++j) if (out->a[j].k == k && out->a[j].l == l) break;
+				if (j < out->n) do_add = 0;
+			}
+			if (do_add) {
+				or_aln1_t *p;
+				gap_shadow(l - k + 1, bwt->seq_len, e.last_diff_pos, width);
+				if (out->n == out->m) {
+					out->m = out->m ? out->m << 1 : 4;
+					out->a = (or_aln1_t*)realloc(out->a, out->m * sizeof(or_aln1_t));
+				}
+				p = out->a + out->n++;
+				memset(p, 0, sizeof(*p));
+				p->n_mm = e.n_mm; p->n_gapo = e.n_gapo; p->n_gape = e.n_gape; p->a = a;
+				p->k = k; p->l = l; p->score = score;
+			}
+			continue;
+		}
+
+		--i;
+		twoocc4_t(bwt, k - 1, l, ck, cl, t);
+		occ = l - k + 1;
+		allow_diff = allow_M = 1;
+		if (i > 0) {
+			int ii = i - (len - opt->seed_len);
+			if (width[i - 1].bid > m - 1) allow_diff = 0;
+			else if (width[i - 1].bid == m - 1 && width[i].bid == m - 1 && width[i - 1].w == width[i].w) allow_M = 0;
+			if (seed_w && ii > 0) {
+				if (sw[ii - 1].bid > m_seed - 1) allow_diff = 0;
+				else if (sw[ii - 1].bid == m_seed - 1 && sw[ii].bid == m_seed - 1 && sw[ii - 1].w == sw[ii].w) allow_M = 0;
+			}
+		}
+		tmp = (opt->mode & OR_MODE_LOGGAP) ? int_log2(e.n_gape + e.n_gapo) / 2 + 1 : e.n_gapo + e.n_gape;
+		if (allow_diff && i >= opt->indel_end_skip + tmp && len - i >= opt->indel_end_skip + tmp) {
+			if (e.state == ST_M) {
+				if (e.n_gapo < opt->max_gapo) {
+					gs_push(stack, a, i, k, l, e.n_mm, e.n_gapo + 1, e.n_gape, ST_I, i, opt);
+					for (j = 0; j != 4; ++j) {
+						uint32_t kk = bwt->L2[j] + ck[j] + 1, ll = bwt->L2[j] + cl[j];
+						if (kk <= ll) gs_push(stack, a, i + 1, kk, ll, e.n_mm, e.n_gapo + 1, e.n_gape, ST_D, i + 1, opt);
+					}
+				}
+			} else if (e.state == ST_I) {
+				if (e.n_gape < opt->max_gape)
+					gs_push(stack, a, i, k, l, e.n_mm, e.n_gapo, e.n_gape + 1, ST_I, i, opt);
+			} else if (e.state == ST_D) {
+				if (e.n_gape < opt->max_gape) {
+					if (e.n_gape + e.n_gapo < max_diff || occ < (uint32_t)opt->max_del_occ) {
+						for (j = 0; j != 4; ++j) {
+							uint32_t kk = bwt->L2[j] + ck[j] + 1, ll = bwt->L2[j] + cl[j];
+							if (kk <= ll) gs_push(stack, a, i + 1, kk, ll, e.n_mm, e.n_gapo, e.n_gape + 1, ST_D, i + 1, opt);
+						}
+					}
+				}
+			}
+		}
+		if (allow_diff && allow_M) {
+			for (j = 1; j <= 4; ++j) {
+				int c = (str[i] + j) & 3;
+				int is_mm = (j != 4 || str[i] > 3);
+				uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
+				if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm + is_mm, e.n_gapo, e.n_gape, ST_M,
+				                      is_mm ? i : e.last_diff_pos, opt);
+			}
+		} else if (str[i] < 4) {
+			int c = str[i] & 3;
+			uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
+			if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm, e.n_gapo, e.n_gape, ST_M, e.last_diff_pos, opt);
+		}
+	}
+	(void)best_diff;
+}
+
+/* ---------------- batch driver (bwtaln.c:80-140, 151-156, 199-218) ---------------- */
+
+typedef struct {
+	const or_bwt_t *bwt[2];
+	int64_t n_seqs;
+	const uint8_t *seq;
+	const uint64_t *off;
+	const uint32_t *len;
+	const or_gap_opt_t *opt;
+	or_gap_opt_t base;  /* batch-level local_opt (bwtaln.c:86-93) */
+	int max_len;
+	int32_t *n_aln;
+	or_aln1_t **per_read;
+	uint32_t *touches;
+	int64_t next;  /* dynamic claim of THREAD_BLOCK reads (bwtaln.c:100-113) */
+	pthread_mutex_t lock;
+} batch_t;
+
+static void *worker(void *data)
+{
+	batch_t *B = (batch_t*)data;
+	const or_gap_opt_t *opt = B->opt;
+	or_gap_opt_t local = B->base;
+	gstack_t *stack = gs_init(local.max_diff, local.max_gapo, local.max_gape, &local);
+	width_t *w[2], *sw[2];
+	uint8_t *rseq = (uint8_t*)malloc(B->max_len + 1);
+	alnv_t out = {0, 0, 0};
+	w[0] = (width_t*)calloc(B->max_len + 1, sizeof(width_t));
+	w[1] = (width_t*)calloc(B->max_len + 1, sizeof(width_t));
+	sw[0] = (width_t*)calloc(opt->seed_len + 1, sizeof(width_t));
+	sw[1] = (width_t*)calloc(opt->seed_len + 1, sizeof(width_t));
+	for (;;) {
+		int64_t b0, b1, r;
+		pthread_mutex_lock(&B->lock);
+		b0 = B->next; B->next += THREAD_BLOCK;
+		pthread_mutex_unlock(&B->lock);
+		if (b0 >= B->n_seqs) break;
+		b1 = b0 + THREAD_BLOCK < B->n_seqs ? b0 + THREAD_BLOCK : B->n_seqs;
+		for (r = b0; r < b1; ++r) {
+			int L = (int)B->len[r], j;
+			const uint8_t *seq[2];
+			uint32_t t = 0;
+			seq[0] = B->seq + B->off[r];
+			/* rseq = complement(seq) under COMPREAD, else seq (bwaseqio.c:189-192) */
+			for (j = 0; j < L; ++j) {
+				int c = seq[0][j];
+				rseq[j] = (opt->mode & OR_MODE_COMPREAD) && c < 4 ? 3 - c : c;
+			}
+			seq[1] = rseq;
+			cal_width(B->bwt[0], L, seq[0], w[0], &t);
+			cal_width(B->bwt[1], L, seq[1], w[1], &t);
+			if (opt->fnr > 0.0) local.max_diff = or_cal_maxdiff(L, 0.02, opt->fnr);
+			local.seed_len = opt->seed_len < L ? opt->seed_len : 0x7fffffff;
+			if (L > opt->seed_len) {
+				cal_width(B->bwt[0], opt->seed_len, seq[0] + (L - opt->seed_len), sw[0], &t);
+				cal_width(B->bwt[1], opt->seed_len, seq[1] + (L - opt->seed_len), sw[1], &t);
+			}
+			match_gap(B->bwt, L, seq, w, L <= opt->seed_len ? 0 : sw, &local, &out, stack, &t);
+			B->n_aln[r] = out.n;
+			if (out.n) {
+				B->per_read[r] = (or_aln1_t*)malloc(out.n * sizeof(or_aln1_t));
+				memcpy(B->per_read[r], out.a, out.n * sizeof(or_aln1_t));
+			} else B->per_read[r] = 0;
+			if (B->touches) B->touches[r] = t;
+		}
+	}
+	free(out.a); free(rseq);
+	free(w[0]); free(w[1]); free(sw[0]); free(sw[1]);
+	gs_free(stack);
+	return 0;
+}
+
+int64_t or_cal_sa_reg_gap(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_seqs,
+                          const uint8_t *seq, const uint64_t *off, const uint32_t *len,
+                          const or_gap_opt_t *opt, int n_threads,
+                          int32_t *n_aln, or_aln1_t **alns_out, uint32_t *touches_out)
+{
+	batch_t B;
+	int64_t i, tot = 0, p = 0;
+	int t;
+	pthread_t *tid;
+	memset(&B, 0, sizeof(B));
+	B.bwt[0] = bwt0; B.bwt[1] = bwt1;
+	B.n_seqs = n_seqs; B.seq = seq; B.off = off; B.len = len; B.opt = opt;
+	B.n_aln = n_aln; B.touches = touches_out;
+	B.per_read = (or_aln1_t**)calloc(n_seqs > 0 ? n_seqs : 1, sizeof(or_aln1_t*));
+	pthread_mutex_init(&B.lock, 0);
+	for (i = 0; i < n_seqs; ++i) if ((int)len[i] > B.max_len) B.max_len = (int)len[i];
+	B.base = *opt;
+	if (opt->fnr > 0.0) B.base.max_diff = or_cal_maxdiff(B.max_len, 0.02, opt->fnr);
+	if (B.base.max_diff < B.base.max_gapo) B.base.max_gapo = B.base.max_diff;
+	if (n_threads < 1) n_threads = 1;
+	tid = (pthread_t*)calloc(n_threads, sizeof(pthread_t));
+	for (t = 0; t < n_threads; ++t) pthread_create(&tid[t], 0, worker, &B);
+	for (t = 0; t < n_threads; ++t) pthread_join(tid[t], 0);
+	free(tid);
+	for (i = 0; i < n_seqs; ++i) tot += n_aln[i];
+	*alns_out = (or_aln1_t*)malloc((tot ? tot : 1) * sizeof(or_aln1_t));
+	for (i = 0; i < n_seqs; ++i) {
+		if (n_aln[i]) memcpy(*alns_out + p, B.per_read[i], n_aln[i] * sizeof(or_aln1_t));
+		p += n_aln[i];
+		free(B.per_read[i]);
+	}
+	free(B.per_read);
+	pthread_mutex_destroy(&B.lock);
+	return tot;
+}

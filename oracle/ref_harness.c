@@ -1,0 +1,82 @@
+/*
+ * ref_harness.c -- TEST INFRASTRUCTURE ONLY (see oracle/README.md).
+ *
+ * A thin driver linked against the reference sources compiled in place from
+ * /root/reference by oracle/Makefile (outputs go to oracle/_ref/ only).  It
+ * is used to (1) produce golden fixtures in this container and (2) time the
+ * reference CPU path as bench.py's `cpu_baseline` (kind "reference").
+ * Nothing in the shipped product links or loads this file.
+ *
+ * Commands mirror main.cpp:45-59 for the two commands we need:
+ *   ibwa_ref index [-a is|bwtsw] <in.fa>   -> bwa_index   (bwtindex.c:42)
+ *   ibwa_ref aln [opts] <prefix> <in.fq>   -> bwa_aln     (bwtaln.c:243)
+ *   ibwa_ref occ4 <prefix.bwt> k...        -> bwt_occ4    (bwt.c:157)  (KAT)
+ *   ibwa_ref sw <ref_seq> <read_seq>       -> aln_local_core (stdaln.c:529)
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+#include "bwt.h"
+#include "bwtaln.h"
+#include "stdaln.h"
+
+int bwa_index(int argc, char *argv[]);
+int bwa_aln(int argc, char *argv[]);
+extern unsigned char nst_nt4_table[256];
+
+static int cmd_occ4(int argc, char *argv[])
+{
+	int i;
+	bwt_t *bwt;
+	if (argc < 3) return 1;
+	bwt = bwt_restore_bwt(argv[1]);
+	for (i = 2; i < argc; ++i) {
+		bwtint_t k = (bwtint_t)strtoul(argv[i], 0, 0), c4[4];
+		bwt_occ4(bwt, k, c4);
+		printf("%u\t%u\t%u\t%u\t%u\n", k, c4[0], c4[1], c4[2], c4[3]);
+	}
+	bwt_destroy(bwt);
+	return 0;
+}
+
+/* sw <ref> <read> : both as ACGTN strings; prints score, path_len and the path */
+static int cmd_sw(int argc, char *argv[])
+{
+	int l1, l2, i, path_len = 0, score, n_cigar = 0;
+	unsigned char *s1, *s2;
+	path_t *path;
+	uint32_t *cigar;
+	AlnParam ap = aln_param_bwa;
+	if (argc < 3) return 1;
+	l1 = strlen(argv[1]); l2 = strlen(argv[2]);
+	s1 = (unsigned char*)malloc(l1 + 1); s2 = (unsigned char*)malloc(l2 + 1);
+	for (i = 0; i < l1; ++i) s1[i] = nst_nt4_table[(int)argv[1][i]];
+	for (i = 0; i < l2; ++i) s2[i] = nst_nt4_table[(int)argv[2][i]];
+	path = (path_t*)calloc(l1 + l2 + 2, sizeof(path_t));
+	score = aln_local_core(s1, l1, s2, l2, &ap, path, &path_len, 1, 0);
+	printf("%d\t%d", score, path_len);
+	if (score >= 0 && path_len > 0) {
+		cigar = aln_path2cigar32(path, path_len, &n_cigar);
+		printf("\t%d,%d\t%d,%d\t", path[path_len-1].i, path[path_len-1].j, path[0].i, path[0].j);
+		for (i = 0; i < n_cigar; ++i) printf("%u%c", cigar[i]>>4, "MIDS"[cigar[i]&0xf]);
+		free(cigar);
+	}
+	printf("\n");
+	free(path); free(s1); free(s2);
+	return 0;
+}
+
+int main(int argc, char *argv[])
+{
+	if (argc < 2) {
+		fprintf(stderr, "usage: ibwa_ref index|aln|occ4|sw ...\n");
+		return 1;
+	}
+	if (strcmp(argv[1], "index") == 0) return bwa_index(argc - 1, argv + 1);
+	if (strcmp(argv[1], "aln") == 0) return bwa_aln(argc - 1, argv + 1);
+	if (strcmp(argv[1], "occ4") == 0) return cmd_occ4(argc - 1, argv + 1);
+	if (strcmp(argv[1], "sw") == 0) return cmd_sw(argc - 1, argv + 1);
+	fprintf(stderr, "unknown command %s\n", argv[1]);
+	return 1;
+}
