@@ -1,0 +1,392 @@
+// aln.hip -- the aln hot path on gfx950: one read per lane.
+//
+// Why a lane, not a wavefront, per read: every backward-search step is a
+// dependent random 64 B fetch into a 1.5 GB table, so throughput is set by
+// the number of independent chains in flight (Little's law: ~8 TB/s x ~2 us
+// / 64 B = ~250k outstanding fetches).  One read per wave would give 8k
+// chains on 256 CUs; one read per lane gives 64x that.
+//
+//   k_width  : bwt_cal_width x4 per read (bwtaln.c:54-78, called :123-130),
+//              the two strands (and the two seeds) advanced in lockstep so
+//              each lane keeps two fetches in flight.
+//   k_search : bwt_match_gap (bwtgap.c:104-264) with the bucketed LIFO
+//              priority stack of bwtgap.c:13-79 kept per lane in HBM as
+//              per-bucket linked lists.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "engine.h"
+#include "occ.h"
+
+namespace ibwa {
+
+namespace {
+
+constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_NONSTOP = 0x10;
+constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
+
+// All six 16 B loads of a rank-query pair are issued unconditionally so that
+// the compiler can put every fetch of a step in flight before the first wait.
+struct Fetch {
+  uint4 ck, bk, sk, cl, bl, sl;
+  uint32_t offk, offl;
+  bool kneg;
+};
+
+__device__ __forceinline__ void fetch_pair(const IndexView &ix, uint32_t k, uint32_t l, Fetch &f) {
+  f.kneg = (k == 0xFFFFFFFFu);
+  uint32_t kk = f.kneg ? 0u : bwt_kk(ix, k);
+  uint32_t ll = bwt_kk(ix, l);
+  const uint4 *pk = ix.blk + (size_t)(kk >> 7) * 4;
+  const uint4 *pl = ix.blk + (size_t)(ll >> 7) * 4;
+  f.offk = kk & 127;
+  f.offl = ll & 127;
+  f.ck = pk[0];
+  f.bk = pk[1 + (f.offk >> 6)];
+  f.sk = pk[3];
+  f.cl = pl[0];
+  f.bl = pl[1 + (f.offl >> 6)];
+  f.sl = pl[3];
+}
+
+__device__ __forceinline__ uint32_t occ_c(const uint4 &cnt, const uint4 &bs, const uint4 &sb, uint32_t off,
+                                          uint32_t c) {
+  uint32_t q = off >> 5, w0, w1, m0, m1;
+  chunk_words(bs, q, w0, w1);
+  chunk_masks(off & 31, m0, m1);
+  return sel4(cnt, c) + sub_byte(sb, q, c) + count1(w0, w1, m0, m1, c);
+}
+
+// bwt_2occ(k-1, l, c) from a fetch made with (k-1, l)
+__device__ __forceinline__ void occ2_from(const Fetch &f, uint32_t c, uint32_t &ok, uint32_t &ol) {
+  ok = f.kneg ? 0u : occ_c(f.ck, f.bk, f.sk, f.offk, c);
+  ol = occ_c(f.cl, f.bl, f.sl, f.offl, c);
+}
+
+__device__ __forceinline__ void occ4x2_from(const Fetch &f, uint32_t ck[4], uint32_t cl[4]) {
+  if (f.kneg) {
+    ck[0] = ck[1] = ck[2] = ck[3] = 0;
+  } else {
+    occ4_from(f.ck, f.bk, f.sk, f.offk, ck);
+  }
+  occ4_from(f.cl, f.bl, f.sl, f.offl, cl);
+}
+
+__device__ __forceinline__ uint32_t strand_base(uint32_t c, int a, bool comp) {
+  // seq[1] = rseq = complement of seq under COMPREAD (bwaseqio.c:189-192)
+  return (a == 1 && comp && c < 4) ? 3u - c : c;
+}
+
+// two bwt_cal_width chains in lockstep: str on ixa -> wa, strand-1 str on ixb -> wb
+__device__ void width_pair(const IndexView &ixa, const IndexView &ixb, int L, const uint8_t *s, bool comp,
+                           uint2 *wa, uint2 *wb) {
+  uint32_t ka = 0, la = ixa.seq_len, kb = 0, lb = ixb.seq_len;
+  uint32_t bida = 0, bidb = 0;
+  for (int i = 0; i < L; ++i) {
+    uint32_t ca = s[i];
+    uint32_t cb = strand_base(ca, 1, comp);
+    Fetch fa, fb;
+    fetch_pair(ixa, ka - 1, la, fa);
+    fetch_pair(ixb, kb - 1, lb, fb);
+    if (ca < 4) {
+      uint32_t ok, ol;
+      occ2_from(fa, ca, ok, ol);
+      ka = ixa.L2[ca] + ok + 1;
+      la = ixa.L2[ca] + ol;
+    }
+    if (ka > la || ca > 3) { ka = 0; la = ixa.seq_len; ++bida; }
+    wa[i] = make_uint2(la - ka + 1, bida);
+    if (cb < 4) {
+      uint32_t ok, ol;
+      occ2_from(fb, cb, ok, ol);
+      kb = ixb.L2[cb] + ok + 1;
+      lb = ixb.L2[cb] + ol;
+    }
+    if (kb > lb || cb > 3) { kb = 0; lb = ixb.seq_len; ++bidb; }
+    wb[i] = make_uint2(lb - kb + 1, bidb);
+  }
+  wa[L] = make_uint2(0u, bida + 1);
+  wb[L] = make_uint2(0u, bidb + 1);
+}
+
+__global__ void __launch_bounds__(256) k_width(AlnArgs A) {
+  const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= A.n) return;
+  const int64_t r = A.ids ? A.ids[lane] : lane;
+  const int L = (int)A.len[r];
+  const uint8_t *s = A.seq + A.off[r];
+  const bool comp = A.o.mode & MODE_COMPREAD;
+  uint2 *w0 = A.wbuf + (uint64_t)lane * A.wstride;
+  uint2 *w1 = w0 + A.wlen1;
+  uint2 *sw0 = w1 + A.wlen1;
+  uint2 *sw1 = sw0 + (A.o.seed_len + 1);
+  width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1);
+  if (L > A.o.seed_len) width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1);
+}
+
+__device__ __forceinline__ int int_log2(uint32_t v) {  // bwtgap.c:93-102
+  return v ? 31 - __builtin_clz(v) : 0;
+}
+
+// bwt_match_exact_alt (bwt.c:235-250) over str[0..i-1] from (k, l)
+__device__ __forceinline__ bool match_exact_alt(const IndexView &ix, int i, const uint8_t *s, int a, bool comp,
+                                                uint32_t &k0, uint32_t &l0) {
+  uint32_t k = k0, l = l0;
+  for (int j = i - 1; j >= 0; --j) {
+    uint32_t c = strand_base(s[j], a, comp);
+    if (c > 3) return false;
+    Fetch f;
+    fetch_pair(ix, k - 1, l, f);
+    uint32_t ok, ol;
+    occ2_from(f, c, ok, ol);
+    k = ix.L2[c] + ok + 1;
+    l = ix.L2[c] + ol;
+    if (k > l) return false;
+  }
+  k0 = k;
+  l0 = l;
+  return true;
+}
+
+__global__ void __launch_bounds__(256) k_search(AlnArgs A) {
+  const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= A.n) return;
+  const AlnOpt &o = A.o;
+  const int64_t r = A.ids ? A.ids[lane] : lane;
+  const int len = (int)A.len[r];
+  const uint8_t *s = A.seq + A.off[r];
+  const bool comp = o.mode & MODE_COMPREAD;
+  uint2 *wbase = A.wbuf + (uint64_t)lane * A.wstride;
+  uint2 *W[2] = {wbase, wbase + A.wlen1};
+  const uint2 *SW[2] = {wbase + 2 * A.wlen1, wbase + 2 * A.wlen1 + (o.seed_len + 1)};
+  const bool seeded = len > o.seed_len;  // bwtaln.c:127,132
+  uint32_t *heads = A.heads + (uint64_t)lane * o.n_stacks;
+  uint4 *ent = A.ent + (uint64_t)lane * A.cap;
+  uint32_t *prv = A.prev + (uint64_t)lane * A.cap;
+  uint4 *out = A.aln + (uint64_t)lane * A.aln_cap;
+  uint32_t status = 0;
+  int n_aln = 0;
+
+  // per-read local_opt (bwtaln.c:125-126)
+  const int opt_max_diff = o.fnr_pos ? (int)A.maxdiff_tab[len] : o.max_diff;
+  const int seed_len = o.seed_len;  // only read when seeded
+  int best_score = (opt_max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape;
+  int max_diff = opt_max_diff;
+  int best_cnt = 0;
+
+  // bwtgap.c:116-122: too many N
+  {
+    int nN = 0;
+    for (int j = 0; j < len; ++j) nN += s[j] > 3;
+    if (nN > max_diff) {
+      A.n_aln[lane] = 0;
+      A.status[lane] = 0;
+      return;
+    }
+  }
+  for (int b = 0; b < o.n_stacks; ++b) heads[b] = NIL;
+  int best = o.n_stacks, n_entries = 0;
+  uint32_t bump = 0, free_head = NIL;  // slots: bump allocator + free list threaded through prv[]
+  bool dead = false;
+
+  auto push = [&](int a, int i, uint32_t k, uint32_t l, int n_mm, int n_gapo, int n_gape, int state, int ldp) {
+    n_mm &= 0xff; n_gapo &= 0xff; n_gape &= 0xff;  // 8-bit fields (bwtgap.h:9)
+    int score = n_mm * o.s_mm + n_gapo * o.s_gapo + n_gape * o.s_gape;
+    if (score < 0 || score >= o.n_stacks) { status |= ST_BAD_SCORE; dead = true; return; }
+    uint32_t slot;
+    if (free_head != NIL) {
+      slot = free_head;
+      free_head = prv[slot];
+    } else {
+      if (bump >= A.cap) { status |= ST_STACK_OVERFLOW; dead = true; return; }
+      slot = bump++;
+    }
+    ent[slot] = make_uint4(k, l, (uint32_t)(i & 0xffff) | ((uint32_t)ldp << 16),
+                           (uint32_t)a | (uint32_t)state << 1 | (uint32_t)n_mm << 8 | (uint32_t)n_gapo << 16 |
+                               (uint32_t)n_gape << 24);
+    prv[slot] = heads[score];
+    heads[score] = slot;
+    ++n_entries;
+    if (best > score) best = score;
+  };
+
+  push(0, len, 0, A.ix[0].seq_len, 0, 0, 0, STATE_M, 0);
+  push(1, len, 0, A.ix[0].seq_len, 0, 0, 0, STATE_M, 0);
+
+  while (n_entries && !dead) {
+    if (n_entries > o.max_entries) break;
+    // gap_pop (bwtgap.c:66-79): top of the lowest non-empty bucket
+    uint32_t slot = heads[best];
+    const uint4 e = ent[slot];
+    const uint32_t pv = prv[slot];
+    heads[best] = pv;
+    if (slot + 1 == bump) {
+      bump = slot;
+    } else {
+      prv[slot] = free_head;
+      free_head = slot;
+    }
+    --n_entries;
+    if (pv == NIL) {
+      if (n_entries) {
+        int b = best + 1;
+        while (b < o.n_stacks && heads[b] == NIL) ++b;
+        best = b;
+      } else {
+        best = o.n_stacks;
+      }
+    }
+    uint32_t k = e.x, l = e.y;
+    int i = (int)(e.z & 0xffff), ldp = (int)(e.z >> 16);
+    const int a = (int)(e.w & 1), state = (int)((e.w >> 1) & 3);
+    const int e_mm = (int)((e.w >> 8) & 0xff), e_go = (int)((e.w >> 16) & 0xff), e_ge = (int)(e.w >> 24);
+    const int e_score = (e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape) & 0x7ff;  // info>>21
+    if (!(o.mode & MODE_NONSTOP) && (uint32_t)e_score > (uint32_t)(best_score + o.s_mm)) break;
+
+    int m = max_diff - (e_mm + e_go);
+    if (o.mode & MODE_GAPE) m -= e_ge;
+    if (m < 0) continue;
+    const IndexView &ix = A.ix[1 - a];
+    uint2 *width = W[a];
+    const uint2 *sw = SW[a];
+    int m_seed = 0;
+    if (seeded) {
+      m_seed = o.max_seed_diff - (e_mm + e_go);
+      if (o.mode & MODE_GAPE) m_seed -= e_ge;
+    }
+    if (i > 0 && m < (int)width[i - 1].y) continue;
+
+    bool hit = false;
+    if (i == 0) {
+      hit = true;
+    } else if (m == 0 && (state == STATE_M || (o.mode & MODE_GAPE) || e_ge == o.max_gape)) {
+      if (match_exact_alt(ix, i, s, a, comp, k, l)) hit = true;
+      else continue;
+    }
+    if (hit) {
+      const int score = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
+      bool do_add = true;
+      if (n_aln == 0) {
+        best_score = score;
+        int best_diff = e_mm + e_go;
+        if (o.mode & MODE_GAPE) best_diff += e_ge;
+        if (!(o.mode & MODE_NONSTOP)) max_diff = (best_diff + 1 > opt_max_diff) ? opt_max_diff : best_diff + 1;
+      }
+      if (score == best_score) best_cnt = (int)((uint32_t)best_cnt + (l - k + 1));
+      else if (best_cnt > o.max_top2) break;
+      if (e_go) {
+        for (int j = 0; j < n_aln && j < (int)A.aln_cap; ++j) {
+          uint4 h = out[j];
+          if (h.y == k && h.z == l) { do_add = false; break; }
+        }
+      }
+      if (do_add) {
+        // gap_shadow (bwtgap.c:81-91) on this strand's width array
+        const uint32_t x = l - k + 1, mx = ix.seq_len;
+        uint32_t jj = 0;
+        for (int q = 0; q < ldp; ++q) {
+          uint2 w = width[q];
+          if (w.x > x) { w.x -= x; width[q] = w; }
+          else if (w.x == x) { ++jj; width[q] = make_uint2(mx - jj, 1u); }
+        }
+        if (n_aln >= (int)A.aln_cap) { status |= ST_ALN_OVERFLOW; dead = true; break; }
+        out[n_aln++] = make_uint4((uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24, k,
+                                  l, (uint32_t)score);
+      }
+      continue;
+    }
+
+    --i;
+    uint32_t cnt_k[4], cnt_l[4];
+    {
+      Fetch f;
+      fetch_pair(ix, k - 1, l, f);
+      occ4x2_from(f, cnt_k, cnt_l);
+    }
+    const uint32_t occ = l - k + 1;
+    bool allow_diff = true, allow_M = true;
+    if (i > 0) {
+      const uint2 w_im1 = width[i - 1], w_i = width[i];
+      const int ii = i - (len - seed_len);
+      if ((int)w_im1.y > m - 1) allow_diff = false;
+      else if ((int)w_im1.y == m - 1 && (int)w_i.y == m - 1 && w_im1.x == w_i.x) allow_M = false;
+      if (seeded && ii > 0) {
+        const uint2 s_im1 = sw[ii - 1], s_i = sw[ii];
+        if ((int)s_im1.y > m_seed - 1) allow_diff = false;
+        else if ((int)s_im1.y == m_seed - 1 && (int)s_i.y == m_seed - 1 && s_im1.x == s_i.x) allow_M = false;
+      }
+    }
+    const int tmp = (o.mode & MODE_LOGGAP) ? int_log2((uint32_t)(e_ge + e_go)) / 2 + 1 : e_go + e_ge;
+    if (allow_diff && i >= o.indel_end_skip + tmp && len - i >= o.indel_end_skip + tmp) {
+      if (state == STATE_M) {
+        if (e_go < o.max_gapo) {
+          push(a, i, k, l, e_mm, e_go + 1, e_ge, STATE_I, i);
+          for (int j = 0; j != 4; ++j) {
+            uint32_t kk = ix.L2[j] + cnt_k[j] + 1, ll = ix.L2[j] + cnt_l[j];
+            if (kk <= ll) push(a, i + 1, kk, ll, e_mm, e_go + 1, e_ge, STATE_D, i + 1);
+          }
+        }
+      } else if (state == STATE_I) {
+        if (e_ge < o.max_gape) push(a, i, k, l, e_mm, e_go, e_ge + 1, STATE_I, i);
+      } else if (state == STATE_D) {
+        if (e_ge < o.max_gape) {
+          if (e_ge + e_go < max_diff || occ < (uint32_t)o.max_del_occ) {
+            for (int j = 0; j != 4; ++j) {
+              uint32_t kk = ix.L2[j] + cnt_k[j] + 1, ll = ix.L2[j] + cnt_l[j];
+              if (kk <= ll) push(a, i + 1, kk, ll, e_mm, e_go, e_ge + 1, STATE_D, i + 1);
+            }
+          }
+        }
+      }
+    }
+    const uint32_t ci = strand_base(s[i], a, comp);
+    if (allow_diff && allow_M) {
+      for (int j = 1; j <= 4; ++j) {
+        const uint32_t c = (ci + j) & 3;
+        const int is_mm = (j != 4 || ci > 3);
+        uint32_t kk = ix.L2[c] + cnt_k[c] + 1, ll = ix.L2[c] + cnt_l[c];
+        if (kk <= ll) push(a, i, kk, ll, e_mm + is_mm, e_go, e_ge, STATE_M, is_mm ? i : ldp);
+      }
+    } else if (ci < 4) {
+      const uint32_t c = ci & 3;
+      uint32_t kk = ix.L2[c] + cnt_k[c] + 1, ll = ix.L2[c] + cnt_l[c];
+      if (kk <= ll) push(a, i, kk, ll, e_mm, e_go, e_ge, STATE_M, ldp);
+    }
+  }
+  A.n_aln[lane] = n_aln;
+  A.status[lane] = status;
+}
+
+__global__ void __launch_bounds__(256) k_occ4(IndexView ix, int64_t n, const uint32_t *k, uint32_t *cnt) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  uint32_t o[4];
+  occ4(ix, k[t], o);
+  cnt[4 * t + 0] = o[0];
+  cnt[4 * t + 1] = o[1];
+  cnt[4 * t + 2] = o[2];
+  cnt[4 * t + 3] = o[3];
+}
+
+}  // namespace
+
+hipError_t launch_width(const AlnArgs &a, int block, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  uint64_t grid = (a.n + block - 1) / block;
+  hipLaunchKernelGGL(k_width, dim3((unsigned)grid), dim3(block), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_search(const AlnArgs &a, int block, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  uint64_t grid = (a.n + block - 1) / block;
+  hipLaunchKernelGGL(k_search, dim3((unsigned)grid), dim3(block), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_occ4(const IndexView &ix, int64_t n, const uint32_t *k, uint32_t *cnt, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_occ4, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, n, k, cnt);
+  return hipGetLastError();
+}
+
+}  // namespace ibwa

@@ -1,0 +1,313 @@
+// aln_main.cpp -- `ibwa-amd aln [options] <prefix> <in.fq>`: the reference's
+// aln command (bwtaln.c:243-328, bwa_aln_core :173-241) with the per-batch
+// pthread fan-out replaced by the GPU engine (include/ibwa_aln.h).
+//
+// Kept from the reference: the getopt option set and semantics, gap_opt_t
+// written raw as the 64-byte .sai header, 0x40000-read batches, read
+// encoding (bwaseqio.c:145-208: barcode strip, -I, -q trimming, reverse /
+// reverse-complement), and the per-read `int32 n_aln + n_aln x 16 B` records
+// in input order.  Added: -G INT (number of GPUs; a batch is split into
+// contiguous slices that keep the batch-level max length, bwtaln.c:89-93).
+// Reading the next batch overlaps the GPU work on the current one.
+#include <ctype.h>
+#include <getopt.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ibwa_aln.h"
+
+namespace {
+
+const int kBatch = 0x40000;  // bwtaln.c:193
+const int kMinRdLen = 35;    // BWA_MIN_RDLEN, bwtaln.h:23
+
+unsigned char nt4[256];
+
+void init_nt4() {  // nst_nt4_table (bntseq.c:39-56)
+  memset(nt4, 4, sizeof nt4);
+  nt4[(int)'A'] = nt4[(int)'a'] = 0;
+  nt4[(int)'C'] = nt4[(int)'c'] = 1;
+  nt4[(int)'G'] = nt4[(int)'g'] = 2;
+  nt4[(int)'T'] = nt4[(int)'t'] = 3;
+  nt4[(int)'-'] = 5;
+}
+
+// Buffered gz reader with the record semantics of kseq_read (kseq.h:156-195).
+struct SeqReader {
+  gzFile fp = nullptr;
+  std::vector<char> buf = std::vector<char>(1 << 20);
+  int begin = 0, end = 0;
+  bool eof = false;
+  int last_char = 0;
+  std::string name, seq, qual;
+
+  bool open(const char *fn) {
+    fp = strcmp(fn, "-") ? gzopen(fn, "r") : gzdopen(fileno(stdin), "r");
+    if (fp) gzbuffer(fp, 1 << 20);
+    return fp != nullptr;
+  }
+  ~SeqReader() {
+    if (fp) gzclose(fp);
+  }
+  int getc_() {
+    if (begin >= end) {
+      if (eof) return -1;
+      end = gzread(fp, buf.data(), (unsigned)buf.size());
+      begin = 0;
+      if (end <= 0) { eof = true; end = 0; return -1; }
+    }
+    return (unsigned char)buf[begin++];
+  }
+  // returns seq length, -1 at EOF, -2 on a truncated quality string
+  int read() {
+    int c;
+    if (last_char == 0) {
+      while ((c = getc_()) != -1 && c != '>' && c != '@') {}
+      if (c == -1) return -1;
+      last_char = c;
+    }
+    name.clear(); seq.clear(); qual.clear();
+    bool got = false;
+    while ((c = getc_()) != -1 && !isspace(c)) { name.push_back((char)c); got = true; }
+    if (c == -1 && !got) return -1;
+    if (c != '\n') while ((c = getc_()) != -1 && c != '\n') {}  // comment
+    while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@')
+      if (isgraph(c)) seq.push_back((char)c);
+    if (c == '>' || c == '@') last_char = c;
+    if (c != '+') return (int)seq.size();
+    while ((c = getc_()) != -1 && c != '\n') {}
+    if (c == -1) return -2;
+    while ((c = getc_()) != -1 && qual.size() < seq.size())
+      if (c >= 33 && c <= 127) qual.push_back((char)c);
+    last_char = 0;
+    if (seq.size() != qual.size()) return -2;
+    return (int)seq.size();
+  }
+};
+
+struct Batch {
+  std::vector<uint8_t> seq;
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> len;
+  int max_len = 0;
+  int64_t n() const { return (int64_t)len.size(); }
+};
+
+// bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input
+bool read_batch(SeqReader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
+  b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0;
+  const bool is_64 = mode & IBWA_MODE_IL13;
+  const int l_bc = (unsigned)mode >> 24;
+  if (l_bc > 15) {
+    fprintf(stderr, "[bwa_read_seq] the maximum barcode length is 15.\n");
+    return false;
+  }
+  int l;
+  while ((int)b.len.size() < kBatch && (l = rd.read()) >= 0) {
+    std::string &s = rd.seq, &q = rd.qual;
+    if (is_64 && !q.empty())
+      for (auto &ch : q) ch = (char)(ch - 31);
+    if ((int)s.size() <= l_bc) continue;
+    if (l_bc) {
+      s.erase(0, l_bc);
+      if (!q.empty()) q.erase(0, l_bc);
+    }
+    int len = (int)s.size(), full = len;
+    *n_tot += full;
+    if (!q.empty() && trim_qual >= 1) {  // bwa_trim_read (bwaseqio.c:74-87)
+      int sc = 0, mx = 0, max_l = len - 1;
+      for (int p = len - 1; p >= kMinRdLen - 1; --p) {
+        sc += trim_qual - ((unsigned char)q[p] - 33);
+        if (sc < 0) break;
+        if (sc > mx) { mx = sc; max_l = p; }
+      }
+      len = max_l + 1;
+      *n_trimmed += full - len;
+    }
+    b.off.push_back(b.seq.size());
+    b.len.push_back((uint32_t)len);
+    if (len > b.max_len) b.max_len = len;
+    for (int j = len - 1; j >= 0; --j) b.seq.push_back(nt4[(unsigned char)s[j]]);  // seq := reverse(read)
+  }
+  return !b.len.empty();
+}
+
+void usage(const ibwa_gap_opt_t *o) {
+  fprintf(stderr, "\nUsage:   ibwa-amd aln [options] <prefix> <in.fq>\n\n");
+  fprintf(stderr, "Options: -n NUM    max #diff (int) or missing prob under 0.02 err rate (float) [%.2f]\n", o->fnr);
+  fprintf(stderr, "         -o INT    maximum number or fraction of gap opens [%d]\n", o->max_gapo);
+  fprintf(stderr, "         -e INT    maximum number of gap extensions, -1 for disabling long gaps [-1]\n");
+  fprintf(stderr, "         -i INT    do not put an indel within INT bp towards the ends [%d]\n", o->indel_end_skip);
+  fprintf(stderr, "         -d INT    maximum occurrences for extending a long deletion [%d]\n", o->max_del_occ);
+  fprintf(stderr, "         -l INT    seed length [%d]\n", o->seed_len);
+  fprintf(stderr, "         -k INT    maximum differences in the seed [%d]\n", o->max_seed_diff);
+  fprintf(stderr, "         -m INT    maximum entries in the queue [%d]\n", o->max_entries);
+  fprintf(stderr, "         -t INT    number of host threads (recorded in the .sai header) [%d]\n", o->n_threads);
+  fprintf(stderr, "         -G INT    number of GPUs [1]\n");
+  fprintf(stderr, "         -M INT    mismatch penalty [%d]\n", o->s_mm);
+  fprintf(stderr, "         -O INT    gap open penalty [%d]\n", o->s_gapo);
+  fprintf(stderr, "         -E INT    gap extension penalty [%d]\n", o->s_gape);
+  fprintf(stderr, "         -R INT    stop searching when there are >INT equally best hits [%d]\n", o->max_top2);
+  fprintf(stderr, "         -q INT    quality threshold for read trimming down to %dbp [%d]\n", kMinRdLen, o->trim_qual);
+  fprintf(stderr, "         -f FILE   file to write output to instead of stdout\n");
+  fprintf(stderr, "         -B INT    length of barcode\n");
+  fprintf(stderr, "         -c        input sequences are in the color space\n");
+  fprintf(stderr, "         -L        log-scaled gap penalty for long deletions\n");
+  fprintf(stderr, "         -N        non-iterative mode: search for all n-difference hits (slooow)\n");
+  fprintf(stderr, "         -I        the input is in the Illumina 1.3+ FASTQ-like format\n\n");
+}
+
+int die(const char *what) {
+  fprintf(stderr, "[ibwa-amd aln] %s: %s\n", what, ibwa_last_error());
+  return 1;
+}
+
+}  // namespace
+
+int main(int argc, char *argv[]) {
+  if (argc < 2 || strcmp(argv[1], "aln") != 0) {
+    fprintf(stderr, "Usage: ibwa-amd aln [options] <prefix> <in.fq>\n");
+    return 1;
+  }
+  --argc; ++argv;
+  init_nt4();
+  ibwa_gap_opt_t opt;
+  ibwa_gap_init_opt(&opt);
+  int opte = -1, n_gpus = 1, c;
+  const char *fn_out = nullptr;
+  // bwtaln.c:249-284 (+ -G)
+  while ((c = getopt(argc, argv, "n:o:e:i:d:l:k:cLR:m:t:NM:O:E:q:f:b012IB:G:")) >= 0) {
+    switch (c) {
+      case 'n':
+        if (strstr(optarg, ".")) opt.fnr = (float)atof(optarg), opt.max_diff = -1;
+        else opt.max_diff = atoi(optarg), opt.fnr = -1.0f;
+        break;
+      case 'o': opt.max_gapo = atoi(optarg); break;
+      case 'e': opte = atoi(optarg); break;
+      case 'M': opt.s_mm = atoi(optarg); break;
+      case 'O': opt.s_gapo = atoi(optarg); break;
+      case 'E': opt.s_gape = atoi(optarg); break;
+      case 'd': opt.max_del_occ = atoi(optarg); break;
+      case 'i': opt.indel_end_skip = atoi(optarg); break;
+      case 'l': opt.seed_len = atoi(optarg); break;
+      case 'k': opt.max_seed_diff = atoi(optarg); break;
+      case 'm': opt.max_entries = atoi(optarg); break;
+      case 't': opt.n_threads = atoi(optarg); break;
+      case 'L': opt.mode |= IBWA_MODE_LOGGAP; break;
+      case 'R': opt.max_top2 = atoi(optarg); break;
+      case 'q': opt.trim_qual = atoi(optarg); break;
+      case 'c': opt.mode &= ~IBWA_MODE_COMPREAD; break;
+      case 'N': opt.mode |= IBWA_MODE_NONSTOP; opt.max_top2 = 0x7fffffff; break;
+      case 'f': fn_out = optarg; break;
+      case 'b': opt.mode |= IBWA_MODE_BAM; break;
+      case '0': opt.mode |= IBWA_MODE_BAM_SE; break;
+      case '1': opt.mode |= IBWA_MODE_BAM_READ1; break;
+      case '2': opt.mode |= IBWA_MODE_BAM_READ2; break;
+      case 'I': opt.mode |= IBWA_MODE_IL13; break;
+      case 'B': opt.mode |= atoi(optarg) << 24; break;
+      case 'G': n_gpus = atoi(optarg); break;
+      default: return 1;
+    }
+  }
+  if (opte > 0) {
+    opt.max_gape = opte;
+    opt.mode &= ~IBWA_MODE_GAPE;
+  }
+  if (optind + 2 > argc) {
+    usage(&opt);
+    return 1;
+  }
+  if (opt.mode & IBWA_MODE_BAM) {
+    fprintf(stderr, "[ibwa-amd aln] BAM input (-b) is not supported yet; convert to FASTQ\n");
+    return 1;
+  }
+  if (opt.fnr > 0.0f) {  // bwtaln.c:317-324
+    for (int i = 17, k = 0; i <= 250; ++i) {
+      int l = ibwa_cal_maxdiff(i, 0.02, opt.fnr);
+      if (l != k) fprintf(stderr, "[bwa_aln] %dbp reads: max_diff = %d\n", i, l);
+      k = l;
+    }
+  }
+  const std::string prefix = argv[optind];
+  SeqReader rd;
+  if (!rd.open(argv[optind + 1])) {
+    fprintf(stderr, "[ibwa-amd aln] cannot open %s\n", argv[optind + 1]);
+    return 1;
+  }
+  FILE *out = fn_out ? fopen(fn_out, "wb") : stdout;
+  if (!out) {
+    fprintf(stderr, "[ibwa-amd aln] cannot write %s\n", fn_out);
+    return 1;
+  }
+  if (n_gpus < 1) n_gpus = 1;
+  std::vector<ibwa_ctx_t *> ctx(n_gpus, nullptr);
+  for (int g = 0; g < n_gpus; ++g) {
+    if (ibwa_ctx_create(g, &ctx[g])) return die("ibwa_ctx_create");
+    if (g == 0) {
+      if (ibwa_ctx_load_bwt_file(ctx[0], 0, (prefix + ".bwt").c_str())) return die("load .bwt");
+      if (ibwa_ctx_load_bwt_file(ctx[0], 1, (prefix + ".rbwt").c_str())) return die("load .rbwt");
+    } else if (ibwa_ctx_clone_index(ctx[g], ctx[0])) {
+      return die("replicate index");
+    }
+  }
+  fwrite(&opt, sizeof opt, 1, out);  // bwtaln.c:192
+
+  Batch cur, nxt;
+  long n_trim = 0, n_tot = 0;
+  int64_t tot_seqs = 0;
+  bool have = read_batch(rd, opt.mode, opt.trim_qual, cur, &n_trim, &n_tot);
+  while (have) {
+    auto t0 = std::chrono::steady_clock::now();
+    const int64_t n = cur.n();
+    tot_seqs += n;
+    if (opt.trim_qual >= 1 && n_tot)
+      fprintf(stderr, "[bwa_read_seq] %.1f%% bases are trimmed.\n", 100.0f * n_trim / n_tot);
+    n_trim = n_tot = 0;
+    fprintf(stderr, "[bwa_aln_core] calculate SA coordinate... ");
+    std::vector<std::vector<int32_t>> g_naln(n_gpus);
+    std::vector<ibwa_aln1_t *> g_aln(n_gpus, nullptr);
+    std::vector<int> g_rc(n_gpus, 0);
+    std::vector<std::thread> th;
+    const int64_t per = (n + n_gpus - 1) / n_gpus;
+    for (int g = 0; g < n_gpus; ++g) {
+      th.emplace_back([&, g]() {
+        int64_t b = std::min<int64_t>(n, g * per), e = std::min<int64_t>(n, b + per);
+        g_naln[g].resize(e - b);
+        int64_t tot = 0;
+        g_rc[g] = ibwa_aln_batch(ctx[g], &opt, e - b, cur.seq.data(), cur.off.data() + b, cur.len.data() + b,
+                                 cur.max_len, g_naln[g].data(), &g_aln[g], &tot);
+      });
+    }
+    // overlap: parse the next batch while the GPUs work
+    bool more = read_batch(rd, opt.mode, opt.trim_qual, nxt, &n_trim, &n_tot);
+    for (auto &t : th) t.join();
+    for (int g = 0; g < n_gpus; ++g)
+      if (g_rc[g]) return die("aln");
+    double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, "%.2f sec\n", sec);
+    fprintf(stderr, "[bwa_aln_core] write to the disk... ");
+    for (int g = 0; g < n_gpus; ++g) {  // bwtaln.c:227-231, input order
+      const ibwa_aln1_t *p = g_aln[g];
+      for (int32_t k : g_naln[g]) {
+        fwrite(&k, 4, 1, out);
+        if (k) fwrite(p, sizeof(ibwa_aln1_t), k, out);
+        p += k;
+      }
+      ibwa_free(g_aln[g]);
+    }
+    fprintf(stderr, "0.00 sec\n");
+    fprintf(stderr, "[bwa_aln_core] %lld sequences have been processed.\n", (long long)tot_seqs);
+    std::swap(cur, nxt);
+    have = more;
+  }
+  if (out != stdout) fclose(out);
+  for (auto *x : ctx) ibwa_ctx_destroy(x);
+  return 0;
+}

@@ -1,0 +1,55 @@
+// engine.h -- internal device/host interface of the aln engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "occ.h"
+
+namespace ibwa {
+
+constexpr uint32_t NIL = 0xFFFFFFFFu;
+constexpr uint32_t ST_STACK_OVERFLOW = 1u;  // per-lane stack capacity exceeded -> retry pass
+constexpr uint32_t ST_ALN_OVERFLOW = 2u;    // per-read hit slots exceeded      -> retry pass
+constexpr uint32_t ST_BAD_SCORE = 4u;       // score outside [0, n_stacks): invalid options
+
+// Batch-level `local_opt` of bwa_cal_sa_reg_gap (bwtaln.c:86-93) as the kernels see it.
+struct AlnOpt {
+  int s_mm, s_gapo, s_gape, mode;
+  int indel_end_skip, max_del_occ, max_entries;
+  int fnr_pos;    // opt->fnr > 0: max_diff is per read length (maxdiff_tab)
+  int max_diff;   // opt->max_diff when !fnr_pos
+  int max_gapo;   // already clamped to the batch max_diff (bwtaln.c:92)
+  int max_gape, max_seed_diff, seed_len, max_top2;
+  int n_stacks;   // gap_init_stack size (bwtgap.c:18)
+};
+
+struct AlnArgs {
+  IndexView ix[2];           // ix[0] = .bwt, ix[1] = .rbwt
+  const uint8_t *seq;        // bwa_seq_t.seq arrays (read reversed), concatenated
+  const uint64_t *off;
+  const uint32_t *len;
+  const int64_t *ids;        // lane -> read id (nullptr: identity)
+  int64_t n;                 // lanes in this launch
+  const int16_t *maxdiff_tab;  // [len] -> bwa_cal_maxdiff(len, 0.02, fnr)
+  uint2 *wbuf;               // per-lane width arrays {w, bid}
+  uint64_t wstride;          // entries per lane
+  uint32_t wlen1;            // batch max_len + 1
+  uint32_t *heads;           // per-lane bucket heads [n_stacks]
+  uint4 *ent;                // per-lane stack entries [cap]
+  uint32_t *prev;            // per-lane links [cap]
+  uint32_t cap;
+  uint4 *aln;                // per-lane hits [aln_cap] (bwt_aln1_t as uint4)
+  int32_t *n_aln;            // per lane
+  uint32_t aln_cap;
+  uint32_t *status;          // per lane ST_* flags
+  AlnOpt o;
+};
+
+hipError_t relayout_reference_bwt(const uint32_t *d_ref, uint64_t n_words, uint64_t n_blocks, uint4 *d_out,
+                                  hipStream_t st);
+hipError_t pack_blocks(const uint32_t *d_sym, uint64_t n_sym_words, const uint4 *d_block_base, uint64_t n_blocks,
+                       uint4 *d_out, hipStream_t st);
+hipError_t launch_width(const AlnArgs &a, int block, hipStream_t st);
+hipError_t launch_search(const AlnArgs &a, int block, hipStream_t st);
+hipError_t launch_occ4(const IndexView &ix, int64_t n, const uint32_t *k, uint32_t *cnt, hipStream_t st);
+
+}  // namespace ibwa

@@ -1,0 +1,506 @@
+// engine.hip -- host side of the C ABI in include/ibwa_aln.h.
+//
+// Replaces, per batch, the pthread fan-out of bwa_aln_core (bwtaln.c:199-218)
+// and the per-thread scratch of bwa_cal_sa_reg_gap (bwtaln.c:88-97, 139) with
+// one HIP launch grid over the batch and HBM-resident per-lane scratch.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "ibwa_aln.h"
+
+using namespace ibwa;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                                    \
+  do {                                                                                               \
+    hipError_t e_ = (x);                                                                             \
+    if (e_ != hipSuccess) return fail(IBWA_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+  } while (0)
+
+// A growable device buffer.
+struct DBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) return fail(IBWA_EHIP, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+    cap = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T *as() const { return (T *)p; }
+};
+
+}  // namespace
+
+struct ibwa_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  // index
+  DBuf idx[2];
+  IndexView ix[2] = {};
+  bool loaded[2] = {false, false};
+  // staged batch
+  DBuf d_seq, d_off, d_len;
+  int64_t n = 0;
+  uint64_t seq_bytes = 0;
+  int max_len = 0;
+  // scratch + outputs
+  DBuf d_wbuf, d_heads, d_ent, d_prev, d_aln, d_naln, d_status, d_tab, d_ids;
+  DBuf r_aln, r_naln, r_status;  // retry pass outputs
+  // results of the last run (host)
+  std::vector<int32_t> h_naln;
+  std::vector<uint32_t> h_status;
+  std::vector<uint4> h_aln;      // n * aln_cap slots
+  std::vector<int64_t> retry_ids;
+  std::vector<std::vector<uint4>> retry_alns;
+  uint32_t aln_cap_used = 0;
+  // tuning
+  uint32_t stack_cap = 4096, aln_cap = 8;
+  int block = 256;
+  int64_t lanes_per_chunk = 1 << 18;
+  ibwa_run_stats_t stats = {};
+};
+
+extern "C" {
+
+const char *ibwa_last_error(void) { return g_err.c_str(); }
+void ibwa_free(void *p) { free(p); }
+
+void ibwa_gap_init_opt(ibwa_gap_opt_t *o) {  // bwtaln.c:21-37
+  memset(o, 0, sizeof(*o));
+  o->s_mm = 3; o->s_gapo = 11; o->s_gape = 4;
+  o->max_diff = -1; o->max_gapo = 1; o->max_gape = 6;
+  o->indel_end_skip = 5; o->max_del_occ = 10; o->max_entries = 2000000;
+  o->mode = IBWA_MODE_GAPE | IBWA_MODE_COMPREAD;
+  o->seed_len = 32; o->max_seed_diff = 2;
+  o->fnr = 0.04f;
+  o->n_threads = 1;
+  o->max_top2 = 30;
+  o->trim_qual = 0;
+}
+
+int ibwa_cal_maxdiff(int l, double err, double thres) {  // bwtaln.c:39-51
+  double elambda = exp(-l * err);
+  double sum, y = 1.0;
+  int k, x = 1;
+  for (k = 1, sum = elambda; k < 1000; ++k) {
+    y *= l * err;
+    x *= k;
+    sum += elambda * y / x;
+    if (1.0 - sum < thres) return k;
+  }
+  return 2;
+}
+
+int ibwa_ctx_create(int device, ibwa_ctx_t **out) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return fail(IBWA_EHIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= n) return fail(IBWA_EINVAL, "device %d out of range (%d devices)", device, n);
+  HIPCHK(hipSetDevice(device));
+  ibwa_ctx *c = new ibwa_ctx();
+  c->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (auto &x : c->ev) HIPCHK(hipEventCreate(&x));
+  *out = c;
+  return 0;
+}
+
+void ibwa_ctx_destroy(ibwa_ctx_t *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
+                  &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
+                  &c->r_status})
+    b->release();
+  for (auto &x : c->ev) (void)hipEventDestroy(x);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int ibwa_ctx_set_tuning(ibwa_ctx_t *c, int stack_cap, int aln_cap, int block) {
+  if (stack_cap > 0) c->stack_cap = stack_cap;
+  if (aln_cap > 0) c->aln_cap = aln_cap;
+  if (block > 0) {
+    if (block % 64 || block > 256) return fail(IBWA_EINVAL, "block must be a multiple of 64 and <= 256");
+    c->block = block;
+  }
+  return 0;
+}
+
+int ibwa_ctx_load_bwt(ibwa_ctx_t *c, int strand, uint32_t primary, const uint32_t L2[4], const uint32_t *bwt,
+                      uint64_t bwt_size) {
+  if (strand < 0 || strand > 1) return fail(IBWA_EINVAL, "strand must be 0 (.bwt) or 1 (.rbwt)");
+  HIPCHK(hipSetDevice(c->device));
+  const uint32_t seq_len = L2[3];
+  const uint64_t n_blocks = ((uint64_t)seq_len + 127) / 128 + 1;
+  // expected reference size: 4 words per 128 symbols (+1 final count block) + ceil(n/16) words
+  const uint64_t expect = ((uint64_t)seq_len + 127) / 128 * 4 + 4 + ((uint64_t)seq_len + 15) / 16;
+  if (bwt_size != expect)
+    return fail(IBWA_EINVAL, "bwt_size %llu does not match seq_len %u (expected %llu)", (unsigned long long)bwt_size,
+                seq_len, (unsigned long long)expect);
+  DBuf tmp;
+  if (int rc = tmp.ensure(bwt_size * 4)) return rc;
+  if (int rc = c->idx[strand].ensure(n_blocks * 64)) { tmp.release(); return rc; }
+  HIPCHK(hipMemcpyAsync(tmp.p, bwt, bwt_size * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(relayout_reference_bwt(tmp.as<uint32_t>(), bwt_size, n_blocks, c->idx[strand].as<uint4>(), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  tmp.release();
+  IndexView &ix = c->ix[strand];
+  ix.blk = c->idx[strand].as<uint4>();
+  ix.primary = primary;
+  ix.seq_len = seq_len;
+  ix.L2[0] = 0;
+  for (int j = 0; j < 4; ++j) ix.L2[j + 1] = L2[j];
+  c->loaded[strand] = true;
+  return 0;
+}
+
+int ibwa_ctx_load_bwt_file(ibwa_ctx_t *c, int strand, const char *path) {  // bwtio.c:51-70
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return fail(IBWA_EIO, "cannot open %s", path);
+  fseek(fp, 0, SEEK_END);
+  long sz = ftell(fp);
+  fseek(fp, 0, SEEK_SET);
+  if (sz < 20) { fclose(fp); return fail(IBWA_EIO, "%s: too short", path); }
+  uint64_t n_words = (uint64_t)(sz - 20) >> 2;
+  uint32_t primary, L2[4];
+  std::vector<uint32_t> buf(n_words);
+  bool ok = fread(&primary, 4, 1, fp) == 1 && fread(L2, 4, 4, fp) == 4 && fread(buf.data(), 4, n_words, fp) == n_words;
+  fclose(fp);
+  if (!ok) return fail(IBWA_EIO, "%s: short read", path);
+  return ibwa_ctx_load_bwt(c, strand, primary, L2, buf.data(), n_words);
+}
+
+int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
+  for (int s = 0; s < 2; ++s) {
+    if (!src->loaded[s]) return fail(IBWA_ENOINDEX, "source index not loaded");
+    HIPCHK(hipSetDevice(dst->device));
+    uint64_t bytes = ((uint64_t)src->ix[s].seq_len + 127) / 128 * 64 + 64;
+    if (int rc = dst->idx[s].ensure(bytes)) return rc;
+    if (src->device == dst->device) {
+      HIPCHK(hipMemcpyAsync(dst->idx[s].p, src->idx[s].p, bytes, hipMemcpyDeviceToDevice, dst->stream));
+    } else {
+      HIPCHK(hipMemcpyPeerAsync(dst->idx[s].p, dst->device, src->idx[s].p, src->device, bytes, dst->stream));
+    }
+    HIPCHK(hipStreamSynchronize(dst->stream));
+    dst->ix[s] = src->ix[s];
+    dst->ix[s].blk = dst->idx[s].as<uint4>();
+    dst->loaded[s] = true;
+  }
+  return 0;
+}
+
+int ibwa_batch_stage(ibwa_ctx_t *c, int64_t n, const uint8_t *seq, const uint64_t *off, const uint32_t *len) {
+  if (n < 0) return fail(IBWA_EINVAL, "n < 0");
+  HIPCHK(hipSetDevice(c->device));
+  uint64_t bytes = 0;
+  int max_len = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (len[i] > 65535) return fail(IBWA_EINVAL, "read %lld: length %u > 65535 is not supported", (long long)i, len[i]);
+    bytes = std::max<uint64_t>(bytes, off[i] + len[i]);
+    max_len = std::max<int>(max_len, (int)len[i]);
+  }
+  if (int rc = c->d_seq.ensure(bytes + 16)) return rc;
+  if (int rc = c->d_off.ensure(n * 8 + 8)) return rc;
+  if (int rc = c->d_len.ensure(n * 4 + 4)) return rc;
+  if (bytes) HIPCHK(hipMemcpyAsync(c->d_seq.p, seq, bytes, hipMemcpyHostToDevice, c->stream));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(c->d_off.p, off, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_len.p, len, n * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->n = n;
+  c->seq_bytes = bytes;
+  c->max_len = max_len;
+  return 0;
+}
+
+static int check_opt(const ibwa_gap_opt_t *o) {
+  if (o->s_mm <= 0 || o->s_gapo <= 0 || o->s_gape <= 0)
+    return fail(IBWA_EINVAL,
+                "zero/negative penalties (-M %d -O %d -E %d) are unsupported: the reference reads uninitialised "
+                "stack slots (bwtgap.c:60) or crashes on them",
+                o->s_mm, o->s_gapo, o->s_gape);
+  if (o->seed_len < 0 || o->max_gape < 0 || o->max_gapo < 0) return fail(IBWA_EINVAL, "negative option");
+  return 0;
+}
+
+// Runs one pass of (width, search) over `lanes` reads.  ids == nullptr: reads base..base+lanes-1.
+static int run_pass(ibwa_ctx *c, AlnArgs A, int64_t base, int64_t lanes, const int64_t *d_ids, float *ms_w,
+                    float *ms_s) {
+  (void)base;
+  A.n = lanes;
+  A.ids = d_ids;
+  HIPCHK(hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(launch_width(A, c->block, c->stream));
+  HIPCHK(hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(launch_search(A, c->block, c->stream));
+  HIPCHK(hipEventRecord(c->ev[2], c->stream));
+  HIPCHK(hipEventSynchronize(c->ev[2]));
+  float a = 0, b = 0;
+  HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+  HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+  *ms_w += a;
+  *ms_s += b;
+  return 0;
+}
+
+int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!c->loaded[0] || !c->loaded[1]) return fail(IBWA_ENOINDEX, "load both .bwt and .rbwt first");
+  if (c->ix[0].seq_len != c->ix[1].seq_len) return fail(IBWA_EINVAL, ".bwt and .rbwt lengths differ");
+  if (int rc = check_opt(opt)) return rc;
+  HIPCHK(hipSetDevice(c->device));
+  memset(&c->stats, 0, sizeof(c->stats));
+  const int64_t n = c->n;
+  const int max_len = std::max(batch_max_len, c->max_len);
+
+  // batch-level local_opt (bwtaln.c:86-93)
+  AlnOpt o = {};
+  o.s_mm = opt->s_mm; o.s_gapo = opt->s_gapo; o.s_gape = opt->s_gape; o.mode = opt->mode;
+  o.indel_end_skip = opt->indel_end_skip; o.max_del_occ = opt->max_del_occ; o.max_entries = opt->max_entries;
+  o.fnr_pos = opt->fnr > 0.0f;
+  int batch_md = o.fnr_pos ? ibwa_cal_maxdiff(max_len, 0.02, opt->fnr) : opt->max_diff;
+  o.max_diff = opt->max_diff;
+  o.max_gapo = batch_md < opt->max_gapo ? batch_md : opt->max_gapo;
+  o.max_gape = opt->max_gape; o.max_seed_diff = opt->max_seed_diff; o.seed_len = opt->seed_len;
+  o.max_top2 = opt->max_top2;
+  o.n_stacks = (batch_md + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape;
+  if (o.n_stacks <= 0 || o.n_stacks > (1 << 20)) return fail(IBWA_EINVAL, "invalid stack size %d", o.n_stacks);
+
+  // per-length max_diff table
+  std::vector<int16_t> tab(max_len + 1);
+  for (int l = 0; l <= max_len; ++l) tab[l] = (int16_t)(o.fnr_pos ? ibwa_cal_maxdiff(l, 0.02, opt->fnr) : opt->max_diff);
+  if (int rc = c->d_tab.ensure(tab.size() * 2)) return rc;
+  HIPCHK(hipMemcpyAsync(c->d_tab.p, tab.data(), tab.size() * 2, hipMemcpyHostToDevice, c->stream));
+
+  AlnArgs A = {};
+  A.ix[0] = c->ix[0];
+  A.ix[1] = c->ix[1];
+  A.seq = c->d_seq.as<uint8_t>();
+  A.off = c->d_off.as<uint64_t>();
+  A.len = c->d_len.as<uint32_t>();
+  A.maxdiff_tab = c->d_tab.as<int16_t>();
+  A.wlen1 = (uint32_t)max_len + 1;
+  A.wstride = 2ull * A.wlen1 + 2ull * ((uint64_t)std::max(opt->seed_len, 0) + 1);
+  A.o = o;
+
+  // first pass, in chunks of lanes_per_chunk reads
+  const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), c->lanes_per_chunk);
+  A.cap = c->stack_cap;
+  A.aln_cap = c->aln_cap;
+  if (int rc = c->d_wbuf.ensure(chunk * A.wstride * 8)) return rc;
+  if (int rc = c->d_heads.ensure(chunk * (uint64_t)o.n_stacks * 4)) return rc;
+  if (int rc = c->d_ent.ensure(chunk * (uint64_t)A.cap * 16)) return rc;
+  if (int rc = c->d_prev.ensure(chunk * (uint64_t)A.cap * 4)) return rc;
+  if (int rc = c->d_aln.ensure(std::max<int64_t>(n, 1) * (uint64_t)A.aln_cap * 16)) return rc;
+  if (int rc = c->d_naln.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
+  if (int rc = c->d_status.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
+  A.wbuf = c->d_wbuf.as<uint2>();
+  A.heads = c->d_heads.as<uint32_t>();
+  A.ent = c->d_ent.as<uint4>();
+  A.prev = c->d_prev.as<uint32_t>();
+  float ms_w = 0, ms_s = 0;
+  for (int64_t b0 = 0; b0 < n; b0 += chunk) {
+    int64_t lanes = std::min(chunk, n - b0);
+    // lane-indexed inputs and outputs: shift the base pointers to this chunk
+    AlnArgs B = A;
+    B.off = A.off + b0;
+    B.len = A.len + b0;
+    B.aln = c->d_aln.as<uint4>() + b0 * A.aln_cap;
+    B.n_aln = c->d_naln.as<int32_t>() + b0;
+    B.status = c->d_status.as<uint32_t>() + b0;
+    if (int rc = run_pass(c, B, b0, lanes, nullptr, &ms_w, &ms_s)) return rc;
+    c->stats.n_launch_width++;
+    c->stats.n_launch_search++;
+  }
+  c->stats.ms_width = ms_w;
+  c->stats.ms_search = ms_s;
+  c->aln_cap_used = A.aln_cap;
+
+  // results + overflow detection
+  c->h_naln.resize(n);
+  c->h_status.resize(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_status.data(), c->d_status.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  c->retry_ids.clear();
+  c->retry_alns.clear();
+  for (int64_t i = 0; i < n; ++i) {
+    if (c->h_status[i] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "read %lld: score outside the stack range", (long long)i);
+    if (c->h_status[i]) c->retry_ids.push_back(i);
+  }
+  // retry pass: larger stacks / hit arrays for the few reads that overflowed
+  std::vector<int64_t> todo = c->retry_ids;
+  uint64_t cap = std::max<uint64_t>((uint64_t)c->stack_cap * 16, 65536);
+  uint32_t acap = std::max<uint32_t>(c->aln_cap * 64, 4096);
+  std::vector<std::vector<uint4>> found(todo.size());
+  std::vector<int64_t> where(todo.size());
+  for (size_t j = 0; j < todo.size(); ++j) where[j] = (int64_t)j;
+  float ms_r = 0;
+  while (!todo.empty()) {
+    // live entries never exceed max_entries + 9 (one expansion after the last check)
+    const uint64_t need_cap = std::min<uint64_t>(cap, (uint64_t)opt->max_entries + 16);
+    // keep each retry chunk within ~16 GiB of stack scratch
+    int64_t per = std::max<int64_t>(1, (int64_t)((16ull << 30) / (need_cap * 20 + acap * 16 + A.wstride * 8 + 64)));
+    std::vector<int64_t> next;
+    std::vector<int64_t> next_where;
+    for (size_t b0 = 0; b0 < todo.size(); b0 += per) {
+      int64_t lanes = std::min<int64_t>(per, (int64_t)todo.size() - (int64_t)b0);
+      AlnArgs B = A;
+      B.cap = (uint32_t)need_cap;
+      B.aln_cap = acap;
+      if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
+      if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
+      if (int rc = c->d_heads.ensure(lanes * (uint64_t)o.n_stacks * 4)) return rc;
+      if (int rc = c->d_ent.ensure(lanes * need_cap * 16)) return rc;
+      if (int rc = c->d_prev.ensure(lanes * need_cap * 4)) return rc;
+      if (int rc = c->r_aln.ensure(lanes * (uint64_t)acap * 16)) return rc;
+      if (int rc = c->r_naln.ensure(lanes * 4)) return rc;
+      if (int rc = c->r_status.ensure(lanes * 4)) return rc;
+      HIPCHK(hipMemcpyAsync(c->d_ids.p, todo.data() + b0, lanes * 8, hipMemcpyHostToDevice, c->stream));
+      B.wbuf = c->d_wbuf.as<uint2>();
+      B.heads = c->d_heads.as<uint32_t>();
+      B.ent = c->d_ent.as<uint4>();
+      B.prev = c->d_prev.as<uint32_t>();
+      B.aln = c->r_aln.as<uint4>();
+      B.n_aln = c->r_naln.as<int32_t>();
+      B.status = c->r_status.as<uint32_t>();
+      float a = 0, b = 0;
+      if (int rc = run_pass(c, B, 0, lanes, c->d_ids.as<int64_t>(), &a, &b)) return rc;
+      ms_r += a + b;
+      std::vector<int32_t> rn(lanes);
+      std::vector<uint32_t> rs(lanes);
+      std::vector<uint4> ra(lanes * (uint64_t)acap);
+      HIPCHK(hipMemcpyAsync(rn.data(), c->r_naln.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(ra.data(), c->r_aln.p, lanes * (uint64_t)acap * 16, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      for (int64_t j = 0; j < lanes; ++j) {
+        int64_t slot = where[b0 + j];
+        if (rs[j] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "score outside the stack range");
+        if (rs[j]) {
+          next.push_back(todo[b0 + j]);
+          next_where.push_back(slot);
+          continue;
+        }
+        found[slot].assign(ra.begin() + j * acap, ra.begin() + j * acap + rn[j]);
+      }
+    }
+    if (!next.empty()) {
+      if (cap >= (uint64_t)opt->max_entries + 16 && acap >= (1u << 20))
+        return fail(IBWA_EOVERFLOW, "read %lld overflowed the large-capacity pass", (long long)next[0]);
+      cap *= 16;
+      acap = std::min<uint32_t>(acap * 16, 1u << 20);
+    }
+    todo.swap(next);
+    where.swap(next_where);
+  }
+  c->retry_alns.swap(found);
+  c->stats.ms_retry = ms_r;
+  c->stats.n_retry = (int64_t)c->retry_ids.size();
+  c->stats.ms_total =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}
+
+int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total) {
+  const int64_t n = c->n;
+  const uint32_t cap = c->aln_cap_used;
+  c->h_aln.resize(std::max<int64_t>(n, 1) * cap);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(c->h_aln.data(), c->d_aln.p, n * (uint64_t)cap * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  // patch in retried reads
+  std::vector<int32_t> cnt(c->h_naln.begin(), c->h_naln.end());
+  for (size_t j = 0; j < c->retry_ids.size(); ++j) cnt[c->retry_ids[j]] = (int32_t)c->retry_alns[j].size();
+  int64_t tot = 0;
+  for (int64_t i = 0; i < n; ++i) tot += cnt[i];
+  ibwa_aln1_t *o = (ibwa_aln1_t *)malloc(std::max<int64_t>(tot, 1) * sizeof(ibwa_aln1_t));
+  if (!o) return fail(IBWA_EINVAL, "out of host memory");
+  size_t rj = 0;
+  int64_t p = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint4 *src;
+    if (rj < c->retry_ids.size() && c->retry_ids[rj] == i) {
+      src = c->retry_alns[rj].data();
+      ++rj;
+    } else {
+      src = c->h_aln.data() + i * cap;
+    }
+    memcpy(o + p, src, (size_t)cnt[i] * 16);
+    p += cnt[i];
+    if (n_aln) n_aln[i] = cnt[i];
+  }
+  *aln = o;
+  if (n_total) *n_total = tot;
+  return 0;
+}
+
+int ibwa_batch_stats(const ibwa_ctx_t *c, ibwa_run_stats_t *st) {
+  *st = c->stats;
+  return 0;
+}
+
+int ibwa_aln_batch(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int64_t n, const uint8_t *seq, const uint64_t *off,
+                   const uint32_t *len, int batch_max_len, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total) {
+  if (int rc = ibwa_batch_stage(c, n, seq, off, len)) return rc;
+  if (int rc = ibwa_batch_run(c, opt, batch_max_len)) return rc;
+  return ibwa_batch_fetch(c, n_aln, aln, n_total);
+}
+
+int ibwa_occ4(ibwa_ctx_t *c, int strand, int64_t n, const uint32_t *k, uint32_t *cnt) {
+  if (!c->loaded[strand]) return fail(IBWA_ENOINDEX, "index not loaded");
+  HIPCHK(hipSetDevice(c->device));
+  DBuf dk, dc;
+  if (int rc = dk.ensure(n * 4 + 4)) return rc;
+  if (int rc = dc.ensure(n * 16 + 16)) { dk.release(); return rc; }
+  HIPCHK(hipMemcpyAsync(dk.p, k, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(launch_occ4(c->ix[strand], n, dk.as<uint32_t>(), dc.as<uint32_t>(), c->stream));
+  HIPCHK(hipMemcpyAsync(cnt, dc.p, n * 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dk.release();
+  dc.release();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+"""Python binding (ctypes) of the C ABI in include/ibwa_aln.h.
+
+This is plumbing for tests and bench.py; the product interface is the C ABI
+and the `ibwa-amd aln` CLI.  Every call goes to libibwa_amd.so on a gfx950
+device; there is no CPU path here -- if the library or the device is missing
+the call raises.
+"""
+import ctypes
+import os
+import struct
+
+import numpy as np
+
+from . import _native
+
+c = ctypes
+
+
+class GapOpt(c.Structure):
+    """gap_opt_t (bwtaln.h:105-115) == ibwa_gap_opt_t; also the 64-byte .sai header."""
+    _fields_ = [(n, c.c_int) for n in ("s_mm", "s_gapo", "s_gape", "mode", "indel_end_skip",
+                                       "max_del_occ", "max_entries")] + \
+               [("fnr", c.c_float)] + \
+               [(n, c.c_int) for n in ("max_diff", "max_gapo", "max_gape", "max_seed_diff",
+                                       "seed_len", "n_threads", "max_top2", "trim_qual")]
+
+
+class RunStats(c.Structure):
+    _fields_ = [("ms_width", c.c_double), ("ms_search", c.c_double), ("ms_retry", c.c_double),
+                ("ms_total", c.c_double), ("n_retry", c.c_int64), ("n_launch_width", c.c_int64),
+                ("n_launch_search", c.c_int64)]
+
+
+assert c.sizeof(GapOpt) == 64
+ALN_DTYPE = np.dtype([("info", "<u4"), ("k", "<u4"), ("l", "<u4"), ("score", "<i4")])  # bwt_aln1_t
+
+MODE_GAPE, MODE_COMPREAD, MODE_LOGGAP, MODE_NONSTOP = 0x01, 0x02, 0x04, 0x10
+MODE_BAM, MODE_BAM_SE, MODE_BAM_READ1, MODE_BAM_READ2, MODE_IL13 = 0x20, 0x40, 0x80, 0x100, 0x200
+
+# every exported symbol declared in include/ibwa_aln.h: name -> (restype, argtypes)
+_vp, _i, _i64, _u32, _u64 = c.c_void_p, c.c_int, c.c_int64, c.c_uint32, c.c_uint64
+CAPI = {
+    "ibwa_last_error": (c.c_char_p, []),
+    "ibwa_free": (None, [_vp]),
+    "ibwa_gap_init_opt": (None, [c.POINTER(GapOpt)]),
+    "ibwa_cal_maxdiff": (_i, [_i, c.c_double, c.c_double]),
+    "ibwa_ctx_create": (_i, [_i, c.POINTER(_vp)]),
+    "ibwa_ctx_destroy": (None, [_vp]),
+    "ibwa_ctx_load_bwt": (_i, [_vp, _i, _u32, c.POINTER(_u32), _vp, _u64]),
+    "ibwa_ctx_load_bwt_file": (_i, [_vp, _i, c.c_char_p]),
+    "ibwa_ctx_clone_index": (_i, [_vp, _vp]),
+    "ibwa_aln_batch": (_i, [_vp, c.POINTER(GapOpt), _i64, _vp, _vp, _vp, _i, _vp, c.POINTER(_vp),
+                            c.POINTER(_i64)]),
+    "ibwa_batch_stage": (_i, [_vp, _i64, _vp, _vp, _vp]),
+    "ibwa_batch_run": (_i, [_vp, c.POINTER(GapOpt), _i]),
+    "ibwa_batch_fetch": (_i, [_vp, _vp, c.POINTER(_vp), c.POINTER(_i64)]),
+    "ibwa_batch_stats": (_i, [_vp, c.POINTER(RunStats)]),
+    "ibwa_ctx_set_tuning": (_i, [_vp, _i, _i, _i]),
+    "ibwa_occ4": (_i, [_vp, _i, _i64, _vp, _vp]),
+}
+
+
+def declare(L):
+    for name, (res, args) in CAPI.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+_declared = False
+
+
+def lib():
+    global _declared
+    L = _native.lib()
+    if not _declared:
+        declare(L)
+        _declared = True
+    return L
+
+
+class IbwaError(RuntimeError):
+    pass
+
+
+def _chk(rc):
+    if rc != 0:
+        raise IbwaError(f"ibwa error {rc}: {lib().ibwa_last_error().decode()}")
+
+
+def default_opt():
+    o = GapOpt()
+    lib().ibwa_gap_init_opt(c.byref(o))
+    return o
+
+
+def read_bwt_file(path):
+    """bwt_restore_bwt (bwtio.c:51-70): -> (primary, L2[1..4], words uint32)."""
+    with open(path, "rb") as f:
+        primary, = struct.unpack("<I", f.read(4))
+        L2 = struct.unpack("<4I", f.read(16))
+        words = np.frombuffer(f.read(), dtype=np.uint32)
+    return primary, L2, words
+
+
+class Engine:
+    """One device context (one GPU) with both FM-indexes resident in HBM."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = c.c_void_p()
+        _chk(L.ibwa_ctx_create(device, c.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().ibwa_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_index_files(self, prefix):
+        _chk(lib().ibwa_ctx_load_bwt_file(self.h, 0, (prefix + ".bwt").encode()))
+        _chk(lib().ibwa_ctx_load_bwt_file(self.h, 1, (prefix + ".rbwt").encode()))
+
+    def load_index(self, strand, primary, L2, words):
+        words = np.ascontiguousarray(words, dtype=np.uint32)
+        arr = (c.c_uint32 * 4)(*[int(x) for x in L2])
+        _chk(lib().ibwa_ctx_load_bwt(self.h, strand, int(primary), arr, words.ctypes.data, words.size))
+
+    def set_tuning(self, stack_cap=0, aln_cap=0, block=0):
+        _chk(lib().ibwa_ctx_set_tuning(self.h, stack_cap, aln_cap, block))
+
+    def stage(self, seqs, offs, lens):
+        self._keep = (np.ascontiguousarray(seqs, dtype=np.uint8), np.ascontiguousarray(offs, dtype=np.uint64),
+                      np.ascontiguousarray(lens, dtype=np.uint32))
+        s, o, l = self._keep
+        _chk(lib().ibwa_batch_stage(self.h, l.size, s.ctypes.data, o.ctypes.data, l.ctypes.data))
+        self.n = l.size
+
+    def run(self, opt, batch_max_len=0):
+        _chk(lib().ibwa_batch_run(self.h, c.byref(opt), batch_max_len))
+
+    def fetch(self):
+        n_aln = np.zeros(self.n, dtype=np.int32)
+        ptr = c.c_void_p()
+        tot = c.c_int64()
+        _chk(lib().ibwa_batch_fetch(self.h, n_aln.ctypes.data, c.byref(ptr), c.byref(tot)))
+        buf = c.string_at(ptr.value, tot.value * 16)
+        lib().ibwa_free(ptr)
+        return n_aln, np.frombuffer(buf, dtype=ALN_DTYPE).copy()
+
+    def stats(self):
+        st = RunStats()
+        _chk(lib().ibwa_batch_stats(self.h, c.byref(st)))
+        return st
+
+    def aln(self, seqs, offs, lens, opt, batch_max_len=0):
+        """bwa_cal_sa_reg_gap over one batch -> (n_aln[n], alns ALN_DTYPE)."""
+        self.stage(seqs, offs, lens)
+        self.run(opt, batch_max_len)
+        return self.fetch()
+
+    def occ4(self, strand, ks):
+        ks = np.ascontiguousarray(ks, dtype=np.uint32)
+        out = np.zeros((ks.size, 4), dtype=np.uint32)
+        _chk(lib().ibwa_occ4(self.h, strand, ks.size, ks.ctypes.data, out.ctypes.data))
+        return out

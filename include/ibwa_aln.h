@@ -1,0 +1,128 @@
+/*
+ * ibwa_aln.h -- C ABI of the MI355X `ibwa aln` engine (libibwa_amd.so).
+ *
+ * Plain pointers and sizes only.  Each entry point names the reference
+ * interface it replaces.  The drop-in that keeps the reference's own types
+ * (`bwa_cal_sa_reg_gap` itself) is in ibwa_bwa_compat.h.
+ *
+ * Error convention: functions return 0 on success and a negative IBWA_E*
+ * code on failure; ibwa_last_error() gives a message.  There is no CPU
+ * fallback: without a usable gfx950 device every compute call fails.
+ */
+#ifndef IBWA_ALN_H
+#define IBWA_ALN_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+	IBWA_OK = 0,
+	IBWA_EHIP = -1,      /* HIP runtime error (no device, OOM, launch failure) */
+	IBWA_EINVAL = -2,    /* bad argument / unsupported option combination */
+	IBWA_ENOINDEX = -3,  /* index not loaded */
+	IBWA_EIO = -4,       /* file I/O */
+	IBWA_EOVERFLOW = -5  /* a read exceeded even the large-capacity retry pass */
+};
+
+/* gap_opt_t (bwtaln.h:105-115); also the raw 64-byte .sai header (bwtaln.c:192) */
+typedef struct {
+	int s_mm, s_gapo, s_gape;
+	int mode; /* bits 24-31: barcode length */
+	int indel_end_skip, max_del_occ, max_entries;
+	float fnr;
+	int max_diff, max_gapo, max_gape;
+	int max_seed_diff, seed_len;
+	int n_threads;
+	int max_top2;
+	int trim_qual;
+} ibwa_gap_opt_t;
+
+/* bwt_aln1_t (bwtaln.h:34-38): one SA interval hit, 16 bytes, the .sai record */
+typedef struct {
+	uint32_t n_mm:8, n_gapo:8, n_gape:8, a:1;
+	uint32_t k, l;
+	int score;
+} ibwa_aln1_t;
+
+#define IBWA_MODE_GAPE     0x01 /* bwtaln.h:95-103 */
+#define IBWA_MODE_COMPREAD 0x02
+#define IBWA_MODE_LOGGAP   0x04
+#define IBWA_MODE_NONSTOP  0x10
+#define IBWA_MODE_BAM      0x20
+#define IBWA_MODE_BAM_SE   0x40
+#define IBWA_MODE_BAM_READ1 0x80
+#define IBWA_MODE_BAM_READ2 0x100
+#define IBWA_MODE_IL13     0x200
+
+typedef struct ibwa_ctx ibwa_ctx_t;
+
+const char *ibwa_last_error(void);
+void ibwa_free(void *p);
+
+/* gap_init_opt (bwtaln.c:21-37) */
+void ibwa_gap_init_opt(ibwa_gap_opt_t *opt);
+/* bwa_cal_maxdiff (bwtaln.c:39-51) */
+int ibwa_cal_maxdiff(int len, double err, double thres);
+
+/* One engine per GPU (device ordinal).  Owns a HIP stream and device buffers. */
+int ibwa_ctx_create(int device, ibwa_ctx_t **out);
+void ibwa_ctx_destroy(ibwa_ctx_t *ctx);
+
+/*
+ * Make an FM-index device-resident (replaces the host residency of
+ * bwt_restore_bwt, bwtio.c:51-70, as used by bwa_aln_core bwtaln.c:184-189).
+ * strand 0 = prefix.bwt, 1 = prefix.rbwt.  `bwt` is the reference's
+ * interleaved array (bwt_t.bwt, bwt_size words); L2 = bwt_t.L2[1..4].
+ */
+int ibwa_ctx_load_bwt(ibwa_ctx_t *ctx, int strand, uint32_t primary, const uint32_t L2[4],
+                      const uint32_t *bwt, uint64_t bwt_size);
+int ibwa_ctx_load_bwt_file(ibwa_ctx_t *ctx, int strand, const char *path);
+/* Copy the index of another context (same process) device-to-device (xGMI peer copy when possible). */
+int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src);
+
+/*
+ * Batched aln over flat arrays -- the body of bwa_cal_sa_reg_gap
+ * (bwtaln.c:80-140) for one batch of n_seqs reads.
+ *   seq/off/len : bwa_seq_t.seq of read i (the read reversed, codes 0..5,
+ *                 bwaseqio.c:183-191) at seq[off[i] .. off[i]+len[i])
+ *   batch_max_len: 0, or the max read length of the *whole* reference batch
+ *                 when this call processes only a slice of it (bwtaln.c:89-93
+ *                 derive max_diff / max_gapo / stack size from it)
+ *   n_aln       : out, per read hit count
+ *   aln         : out, malloc'd concatenation of hits in read order (ibwa_free)
+ */
+int ibwa_aln_batch(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt, int64_t n_seqs, const uint8_t *seq,
+                   const uint64_t *off, const uint32_t *len, int batch_max_len, int32_t *n_aln,
+                   ibwa_aln1_t **aln, int64_t *n_total);
+
+/*
+ * Device-resident form used for measurement: stage a batch into HBM once,
+ * run the kernels (inputs already resident), then fetch the results.
+ */
+int ibwa_batch_stage(ibwa_ctx_t *ctx, int64_t n_seqs, const uint8_t *seq, const uint64_t *off,
+                     const uint32_t *len);
+int ibwa_batch_run(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt, int batch_max_len);
+int ibwa_batch_fetch(ibwa_ctx_t *ctx, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total);
+
+typedef struct {
+	double ms_width;       /* width kernel, HIP events on the engine stream */
+	double ms_search;      /* search kernel (first pass) */
+	double ms_retry;       /* large-capacity retry pass (0 if none) */
+	double ms_total;       /* ibwa_batch_run wall, device-synchronised */
+	int64_t n_retry;       /* reads re-run in the large-capacity pass */
+	int64_t n_launch_width, n_launch_search;
+} ibwa_run_stats_t;
+int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
+
+/* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */
+int ibwa_ctx_set_tuning(ibwa_ctx_t *ctx, int stack_cap, int aln_cap, int block);
+
+/* Device Occ KAT: bwt_occ4 (bwt.c:157) for n positions k[] on strand s -> cnt[4*n] */
+int ibwa_occ4(ibwa_ctx_t *ctx, int strand, int64_t n, const uint32_t *k, uint32_t *cnt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

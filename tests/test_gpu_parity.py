@@ -1,0 +1,74 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's goldens.
+
+Bit-exact for every .sai of the option matrix (tools/make_golden.py) and for
+bwt_occ4 KATs; plus engine-vs-oracle on larger seeded read sets.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from ibwa_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+
+
+def _eopt(o):
+    e = E.GapOpt()
+    for f, _ in E.GapOpt._fields_:
+        setattr(e, f, getattr(o, f))
+    return e
+
+
+def test_occ4_kats_gpu(golden_dir, gpu_engine):
+    for s, which in enumerate(["bwt", "rbwt"]):
+        rows = [list(map(int, l.split())) for l in open(os.path.join(golden_dir, f"kat_occ4_{which}.tsv"))]
+        ks = np.array([r[0] for r in rows], dtype=np.uint32)
+        got = gpu_engine.occ4(s, ks)
+        assert (got == np.array([r[1:] for r in rows], dtype=np.uint32)).all(), which
+
+
+def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine):
+    bad = []
+    for key, m in sorted(sai_manifest.items()):
+        opt, _ = oracle.parse_aln_args(m["argv"])
+        recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+        seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+        n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+        got = oracle.sai_bytes(opt, n_aln, alns)
+        exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+        if not oracle.sai_body_equal(got, exp):
+            bad.append(key)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("stack_cap,aln_cap", [(16, 1), (64, 2)])
+def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap, aln_cap):
+    """Tiny per-lane capacities force most reads through the large-capacity retry pass."""
+    try:
+        gpu_engine.set_tuning(stack_cap=stack_cap, aln_cap=aln_cap)
+        for key in ["r150.default", "mixed.N", "r100.default"]:
+            m = sai_manifest[key]
+            opt, _ = oracle.parse_aln_args(m["argv"])
+            recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+            seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+            n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+            assert gpu_engine.stats().n_retry > 0
+            exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+            assert oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp), key
+    finally:
+        gpu_engine.set_tuning(stack_cap=4096, aln_cap=8)
+
+
+def test_empty_batch(gpu_engine):
+    n_aln, alns = gpu_engine.aln(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                                 E.default_opt())
+    assert n_aln.size == 0 and alns.size == 0
+
+
+def test_rejects_zero_penalty(gpu_engine):
+    o = E.default_opt()
+    o.s_gapo = 0  # the reference aborts on -O 0
+    with pytest.raises(E.IbwaError):
+        gpu_engine.aln(np.zeros(36, np.uint8), np.zeros(1, np.uint64), np.full(1, 36, np.uint32), o)

@@ -1,0 +1,51 @@
+"""The CPU restatement (oracle/) against the compiled reference's own outputs.
+
+Pins the oracle before it is trusted: every golden .sai (option matrix x read
+sets, tools/make_golden.py) must be byte-identical after masking the
+n_threads header field, and bwt_occ4 must match the reference's KATs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+
+def test_occ4_kats(golden_dir, oracle_index):
+    for which, b in zip(["bwt", "rbwt"], oracle_index):
+        for line in open(os.path.join(golden_dir, f"kat_occ4_{which}.tsv")):
+            k, *cnt = map(int, line.split())
+            assert b.occ4(k) == tuple(cnt), (which, k)
+
+
+def _load(golden_dir, m):
+    opt, _ = oracle.parse_aln_args(m["argv"])
+    recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+    return opt, oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_sai_goldens(golden_dir, sai_manifest, oracle_index, threads):
+    b0, b1 = oracle_index
+    for key, m in sorted(sai_manifest.items()):
+        opt, (seqs, offs, lens) = _load(golden_dir, m)
+        n_aln, alns, _ = oracle.cal_sa_reg_gap(b0, b1, seqs, offs, lens, opt, n_threads=threads)
+        got = oracle.sai_bytes(opt, n_aln, alns)
+        exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+        assert oracle.sai_body_equal(got, exp), key
+
+
+def test_maxdiff_table():
+    # bwtaln.c:317-324 prints these breakpoints for the default fnr 0.04
+    L = oracle.lib()
+    md = [L.or_cal_maxdiff(l, 0.02, 0.04) for l in range(17, 251)]
+    assert md[0] == 2 and md[100 - 17] == 5 and md[150 - 17] == 6 and md[37 - 17] == 2 and md[38 - 17] == 3
+
+
+def test_touch_counts_positive(golden_dir, sai_manifest, oracle_index):
+    b0, b1 = oracle_index
+    opt, (seqs, offs, lens) = _load(golden_dir, sai_manifest["r100.n0"])
+    _, _, t = oracle.cal_sa_reg_gap(b0, b1, seqs, offs, lens, opt, touches=True)
+    # -n 0 on 100 bp: 2 full + 2 seed widths (264 steps) plus exact tails
+    assert 250 < t.mean() < 500
