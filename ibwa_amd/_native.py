@@ -42,8 +42,13 @@ def _declare(L):
     L.ibwa_synth_reads.argtypes = [c.c_uint64, c.c_void_p, c.c_uint64, c.c_int, u64p, c.c_uint64,
                                    c.c_int, c.c_double, c.c_double, c.c_void_p, c.c_void_p,
                                    c.c_void_p, c.c_int]
-    try:
-        from ._native_decl import declare_extra
-        declare_extra(L)
-    except ImportError:
-        pass
+    declare_host_helpers(L)
+
+
+def declare_host_helpers(L):
+    c = ctypes
+    L.ibwa_pack_nt4_mt.restype = c.c_uint64
+    L.ibwa_pack_nt4_mt.argtypes = [c.c_void_p, c.c_uint64, c.c_void_p, c.c_int]
+    L.ibwa_encode_reads_fixed.restype = None
+    L.ibwa_encode_reads_fixed.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_void_p, c.c_void_p, c.c_void_p,
+                                          c.c_int]

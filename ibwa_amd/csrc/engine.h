@@ -51,5 +51,8 @@ hipError_t pack_blocks(const uint32_t *d_sym, uint64_t n_sym_words, const uint4 
 hipError_t launch_width(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_search(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_occ4(const IndexView &ix, int64_t n, const uint32_t *k, uint32_t *cnt, hipStream_t st);
+hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_t *primary, uint32_t totals[4],
+                        uint32_t *sa_sample, uint32_t sa_intv, int *rounds, hipStream_t st);
+hipError_t reverse_text(uint8_t *T, uint64_t n, hipStream_t st);
 
 }  // namespace ibwa

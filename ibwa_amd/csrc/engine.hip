@@ -88,6 +88,10 @@ struct ibwa_ctx {
   std::vector<int64_t> retry_ids;
   std::vector<std::vector<uint4>> retry_alns;
   uint32_t aln_cap_used = 0;
+  // sampled suffix arrays kept by ibwa_ctx_build_index
+  DBuf sa_s[2];
+  uint32_t sa_intv = 0;
+  int build_rounds[2] = {0, 0};
   // tuning
   uint32_t stack_cap = 4096, aln_cap = 8;
   int block = 256;
@@ -146,7 +150,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
-                  &c->r_status})
+                  &c->r_status, &c->sa_s[0], &c->sa_s[1]})
     b->release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(c->stream);
@@ -223,6 +227,91 @@ int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
     dst->ix[s].blk = dst->idx[s].as<uint4>();
     dst->loaded[s] = true;
   }
+  return 0;
+}
+
+int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa_intv) {
+  if (n == 0 || n >= 0xFFFFFFFEull) return fail(IBWA_EINVAL, "text length %llu outside [1, 2^32-2)", (unsigned long long)n);
+  if (sa_intv < 0) return fail(IBWA_EINVAL, "sa_intv < 0");
+  HIPCHK(hipSetDevice(c->device));
+  DBuf T;
+  if (int rc = T.ensure(n)) return rc;
+  HIPCHK(hipMemcpyAsync(T.p, codes, n, hipMemcpyHostToDevice, c->stream));
+  for (int s = 0; s < 2; ++s) {
+    c->loaded[s] = false;
+    if (s == 1) HIPCHK(reverse_text(T.as<uint8_t>(), n, c->stream));  // .rpac (bwtmisc.c:160-185)
+    const uint64_t n_blocks = (n + 127) / 128 + 1;
+    if (int rc = c->idx[s].ensure(n_blocks * 64)) { T.release(); return rc; }
+    uint32_t *sa_out = nullptr;
+    if (sa_intv > 0) {
+      if (int rc = c->sa_s[s].ensure(((n + sa_intv) / sa_intv) * 4)) { T.release(); return rc; }
+      sa_out = c->sa_s[s].as<uint32_t>();
+    }
+    uint32_t primary = 0, tot[4] = {0, 0, 0, 0};
+    hipError_t e = build_strand(T.as<uint8_t>(), n, c->idx[s].as<uint4>(), &primary, tot, sa_out, (uint32_t)sa_intv,
+                                &c->build_rounds[s], c->stream);
+    if (e != hipSuccess) {
+      T.release();
+      return fail(IBWA_EHIP, "suffix sort (strand %d): %s", s, hipGetErrorString(e));
+    }
+    IndexView &ix = c->ix[s];
+    ix.blk = c->idx[s].as<uint4>();
+    ix.primary = primary;
+    ix.seq_len = (uint32_t)n;
+    ix.L2[0] = 0;
+    ix.L2[1] = tot[0];
+    ix.L2[2] = tot[0] + tot[1];
+    ix.L2[3] = tot[0] + tot[1] + tot[2];
+    ix.L2[4] = tot[0] + tot[1] + tot[2] + tot[3];
+    if (ix.L2[4] != n) { T.release(); return fail(IBWA_EHIP, "index build: symbol total %u != n", ix.L2[4]); }
+    c->loaded[s] = true;
+  }
+  c->sa_intv = (uint32_t)sa_intv;
+  T.release();
+  return 0;
+}
+
+int ibwa_ctx_bwt_info(const ibwa_ctx_t *c, int strand, uint32_t *primary, uint32_t L2[4], uint64_t *bwt_size) {
+  if (strand < 0 || strand > 1 || !c->loaded[strand]) return fail(IBWA_ENOINDEX, "index not loaded");
+  const IndexView &ix = c->ix[strand];
+  if (primary) *primary = ix.primary;
+  if (L2) for (int j = 0; j < 4; ++j) L2[j] = ix.L2[j + 1];
+  const uint64_t n = ix.seq_len;
+  if (bwt_size) *bwt_size = (n + 127) / 128 * 4 + 4 + (n + 15) / 16;
+  return 0;
+}
+
+int ibwa_ctx_export_bwt(const ibwa_ctx_t *c, int strand, uint32_t *words, uint64_t cap) {
+  uint64_t need = 0;
+  if (int rc = ibwa_ctx_bwt_info(c, strand, nullptr, nullptr, &need)) return rc;
+  if (cap < need) return fail(IBWA_EINVAL, "export buffer too small (%llu < %llu)", (unsigned long long)cap,
+                              (unsigned long long)need);
+  HIPCHK(hipSetDevice(c->device));
+  const uint64_t n = c->ix[strand].seq_len, nb = (n + 127) / 128;
+  std::vector<uint4> blk((nb + 1) * 4);
+  HIPCHK(hipMemcpy(blk.data(), c->idx[strand].p, blk.size() * 16, hipMemcpyDeviceToHost));
+  // bwt_bwtupdate_core (bwtmisc.c:122-144): [4 counts][<=8 words] per 128 symbols, then final counts
+  uint64_t k = 0;
+  for (uint64_t b = 0; b < nb; ++b) {
+    const uint4 *p = &blk[b * 4];
+    words[k++] = p[0].x; words[k++] = p[0].y; words[k++] = p[0].z; words[k++] = p[0].w;
+    const uint32_t w8[8] = {p[1].x, p[1].y, p[1].z, p[1].w, p[2].x, p[2].y, p[2].z, p[2].w};
+    const uint64_t nw = std::min<uint64_t>(8, (n - b * 128 + 15) / 16);
+    for (uint64_t q = 0; q < nw; ++q) words[k++] = w8[q];
+  }
+  const IndexView &ix = c->ix[strand];
+  for (int j = 0; j < 4; ++j) words[k++] = ix.L2[j + 1] - ix.L2[j];
+  return k == need ? 0 : fail(IBWA_EINVAL, "internal: exported %llu words, expected %llu", (unsigned long long)k,
+                              (unsigned long long)need);
+}
+
+int ibwa_ctx_export_sa(const ibwa_ctx_t *c, int strand, uint32_t *out, uint64_t cap) {
+  if (strand < 0 || strand > 1 || !c->loaded[strand] || !c->sa_intv) return fail(IBWA_ENOINDEX, "no sampled SA");
+  const uint64_t n = c->ix[strand].seq_len, n_sa = (n + c->sa_intv) / c->sa_intv;
+  if (cap < n_sa) return fail(IBWA_EINVAL, "export buffer too small");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(out, c->sa_s[strand].p, n_sa * 4, hipMemcpyDeviceToHost));
+  out[0] = 0xFFFFFFFFu;  // bwt.c:66
   return 0;
 }
 

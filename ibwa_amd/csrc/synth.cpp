@@ -199,6 +199,89 @@ uint64_t ibwa_pack_nt4(const char *ascii, uint64_t n, uint8_t *codes) {
   return n_amb;
 }
 
+// jump the 48-bit LCG ahead by k steps: compose the affine map x -> a x + c
+static uint64_t lcg48_skip(uint64_t x, uint64_t k) {
+  const uint64_t M = (1ull << 48) - 1;
+  uint64_t A = 1, C = 0, a = 0x5DEECE66Dull, c = 0xBull;
+  while (k) {
+    if (k & 1) { A = (A * a) & M; C = (C * a + c) & M; }
+    c = (c * a + c) & M;  // (a,c)∘(a,c) = (a^2, a c + c)
+    a = (a * a) & M;
+    k >>= 1;
+  }
+  return (A * x + C) & M;
+}
+
+static inline int nt4_of(char ch) {
+  switch (ch) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+  }
+}
+
+// Multithreaded ibwa_pack_nt4: identical output (each chunk jumps the LCG
+// ahead by the number of ambiguous bases before it).
+uint64_t ibwa_pack_nt4_mt(const char *ascii, uint64_t n, uint8_t *codes, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  const uint64_t CH = 1ull << 24, nch = (n + CH - 1) / CH;
+  std::vector<uint64_t> namb(nch + 1, 0);
+  auto count = [&](int t) {
+    for (uint64_t ch = t; ch < nch; ch += n_threads) {
+      uint64_t b = ch * CH, e = std::min(n, b + CH), k = 0;
+      for (uint64_t i = b; i < e; ++i) k += nt4_of(ascii[i]) == 4;
+      namb[ch + 1] = k;
+    }
+  };
+  auto fill = [&](int t) {
+    for (uint64_t ch = t; ch < nch; ch += n_threads) {
+      uint64_t b = ch * CH, e = std::min(n, b + CH);
+      uint64_t x = lcg48_skip((11ull << 16) | 0x330E, namb[ch]);
+      for (uint64_t i = b; i < e; ++i) {
+        int c = nt4_of(ascii[i]);
+        if (c == 4) { x = lcg48(x); c = (int)((x >> 17) & 3); }
+        codes[i] = (uint8_t)c;
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t) th.emplace_back(count, t);
+    for (auto &x : th) x.join();
+  }
+  for (uint64_t ch = 0; ch < nch; ++ch) namb[ch + 1] += namb[ch];
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t) th.emplace_back(fill, t);
+    for (auto &x : th) x.join();
+  }
+  return namb[nch];
+}
+
+// Fixed-length ASCII reads -> bwa_seq_t.seq layout (codes, read reversed;
+// bwaseqio.c:183-191): seq[i*len .. i*len+len), off[i] = i*len, lens[i] = len.
+void ibwa_encode_reads_fixed(const char *ascii, uint64_t n, int len, uint8_t *seq, uint64_t *off, uint32_t *lens,
+                             int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  auto work = [&](int t) {
+    for (uint64_t r = t; r < n; r += n_threads) {
+      const char *s = ascii + r * (uint64_t)len;
+      uint8_t *o = seq + r * (uint64_t)len;
+      for (int j = 0; j < len; ++j) {
+        char ch = s[len - 1 - j];
+        o[j] = ch == '-' ? 5 : (uint8_t)nt4_of(ch);
+      }
+      off[r] = r * (uint64_t)len;
+      lens[r] = (uint32_t)len;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < n_threads; ++t) th.emplace_back(work, t);
+  for (auto &x : th) x.join();
+}
+
 // Draw `n_reads` single-end reads of length `len` from `ascii` (length n,
 // contigs concatenated; reads never span a contig boundary or an N).
 //   sub_rate   : i.i.d. substitution probability (uniform alternative base)

@@ -57,6 +57,10 @@ CAPI = {
     "ibwa_batch_stats": (_i, [_vp, c.POINTER(RunStats)]),
     "ibwa_ctx_set_tuning": (_i, [_vp, _i, _i, _i]),
     "ibwa_occ4": (_i, [_vp, _i, _i64, _vp, _vp]),
+    "ibwa_ctx_build_index": (_i, [_vp, _vp, _u64, _i]),
+    "ibwa_ctx_bwt_info": (_i, [_vp, _i, c.POINTER(_u32), c.POINTER(_u32), c.POINTER(_u64)]),
+    "ibwa_ctx_export_bwt": (_i, [_vp, _i, _vp, _u64]),
+    "ibwa_ctx_export_sa": (_i, [_vp, _i, _vp, _u64]),
 }
 
 
@@ -165,6 +169,31 @@ class Engine:
         self.stage(seqs, offs, lens)
         self.run(opt, batch_max_len)
         return self.fetch()
+
+    def build_index(self, codes, sa_intv=0):
+        """On-device `bwa index` (BWT part) from 2-bit codes (uint8, N already replaced)."""
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        _chk(lib().ibwa_ctx_build_index(self.h, codes.ctypes.data, codes.size, sa_intv))
+
+    def bwt_info(self, strand):
+        p = c.c_uint32()
+        L2 = (c.c_uint32 * 4)()
+        sz = c.c_uint64()
+        _chk(lib().ibwa_ctx_bwt_info(self.h, strand, c.byref(p), L2, c.byref(sz)))
+        return p.value, tuple(L2), sz.value
+
+    def export_bwt(self, strand):
+        """-> (primary, L2[1..4], words) in the reference .bwt layout."""
+        primary, L2, sz = self.bwt_info(strand)
+        words = np.zeros(sz, dtype=np.uint32)
+        _chk(lib().ibwa_ctx_export_bwt(self.h, strand, words.ctypes.data, sz))
+        return primary, L2, words
+
+    def export_sa(self, strand, intv):
+        n = self.bwt_info(strand)[1][3]
+        out = np.zeros((n + intv) // intv, dtype=np.uint32)
+        _chk(lib().ibwa_ctx_export_sa(self.h, strand, out.ctypes.data, out.size))
+        return out
 
     def occ4(self, strand, ks):
         ks = np.ascontiguousarray(ks, dtype=np.uint32)

@@ -119,6 +119,24 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 /* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */
 int ibwa_ctx_set_tuning(ibwa_ctx_t *ctx, int stack_cap, int aln_cap, int block);
 
+/*
+ * On-device index construction (bwa_index, bwtindex.c:42-186, for the BWT
+ * part): `codes` is the packed reference (.pac content, one 2-bit code per
+ * byte, N already replaced as bns_fasta2bntseq does -- see ibwa_pack_nt4),
+ * n < 2^32 - 1.  Builds .bwt (text) and .rbwt (reversed text, bwtmisc.c:160)
+ * straight into HBM; the result is bit-identical to `bwa index`.
+ * sa_intv > 0 also keeps the sampled suffix arrays (.sa/.rsa, bwt_cal_sa).
+ */
+int ibwa_ctx_build_index(ibwa_ctx_t *ctx, const uint8_t *codes, uint64_t n, int sa_intv);
+/* Geometry of a resident index: primary, L2[1..4], and bwt_size (reference words). */
+int ibwa_ctx_bwt_info(const ibwa_ctx_t *ctx, int strand, uint32_t *primary, uint32_t L2[4], uint64_t *bwt_size);
+/* Export a resident index in the reference's interleaved .bwt word layout
+ * (bwt_dump_bwt, bwtio.c:7-15, after bwt_bwtupdate_core): words[bwt_size]. */
+int ibwa_ctx_export_bwt(const ibwa_ctx_t *ctx, int strand, uint32_t *words, uint64_t cap);
+/* Export the sampled SA kept by ibwa_ctx_build_index: out[(n+intv)/intv] with out[0] = (u32)-1
+ * (bwt.c:56-66); entries 1.. are what bwt_dump_sa writes. */
+int ibwa_ctx_export_sa(const ibwa_ctx_t *ctx, int strand, uint32_t *out, uint64_t cap);
+
 /* Device Occ KAT: bwt_occ4 (bwt.c:157) for n positions k[] on strand s -> cnt[4*n] */
 int ibwa_occ4(ibwa_ctx_t *ctx, int strand, int64_t n, const uint32_t *k, uint32_t *cnt);
 
