@@ -48,6 +48,76 @@ __device__ __forceinline__ void fetch_pair(const IndexView &ix, uint32_t k, uint
   f.sl = pl[3];
 }
 
+// Predicated fetch: no loads when !run; the l-end reuses the k-end block's
+// counts when both ends fall in one 128-symbol block (bwt.c:125's fast path).
+__device__ __forceinline__ void fetch_pair_p(const IndexView &ix, uint32_t k, uint32_t l, bool run, Fetch &f) {
+  f.kneg = (k == 0xFFFFFFFFu);
+  uint32_t kk = f.kneg ? 0u : bwt_kk(ix, k);
+  uint32_t ll = bwt_kk(ix, l);
+  const bool same = !f.kneg && (kk >> 7) == (ll >> 7);
+  const uint4 *pk = ix.blk + (size_t)(kk >> 7) * 4;
+  const uint4 *pl = ix.blk + (size_t)(ll >> 7) * 4;
+  f.offk = kk & 127;
+  f.offl = ll & 127;
+  if (run && !f.kneg) {
+    f.ck = pk[0];
+    f.bk = pk[1 + (f.offk >> 6)];
+    f.sk = pk[3];
+  }
+  if (run) f.bl = pl[1 + (f.offl >> 6)];
+  if (run && !same) {
+    f.cl = pl[0];
+    f.sl = pl[3];
+  }
+  if (same) {
+    f.cl = f.ck;
+    f.sl = f.sk;
+  }
+}
+
+// Single-symbol rank pair: per end only the 16 B that bwt_2occ needs --
+// C[c], the 32-symbol chunk (8 B) and its sub-count word -- 3 loads, 4 VGPRs.
+struct Fetch1 {
+  uint32_t ck, sk, cl, sl;
+  uint2 wk, wl;
+  uint32_t offk, offl;
+  bool kneg;
+};
+
+__device__ __forceinline__ void fetch1(const IndexView &ix, uint32_t k, uint32_t l, uint32_t c, bool run,
+                                       Fetch1 &f) {
+  f.kneg = (k == 0xFFFFFFFFu);
+  const uint32_t kk = f.kneg ? 0u : bwt_kk(ix, k);
+  const uint32_t ll = bwt_kk(ix, l);
+  const uint32_t *pk = reinterpret_cast<const uint32_t *>(ix.blk + (size_t)(kk >> 7) * 4);
+  const uint32_t *pl = reinterpret_cast<const uint32_t *>(ix.blk + (size_t)(ll >> 7) * 4);
+  f.offk = kk & 127;
+  f.offl = ll & 127;
+  const uint32_t qk = f.offk >> 5, ql = f.offl >> 5;
+  if (run && !f.kneg) {
+    f.ck = pk[c];
+    f.wk = *reinterpret_cast<const uint2 *>(pk + 4 + 2 * qk);
+    f.sk = pk[11 + (qk ? qk : 1)];
+  }
+  if (run) {
+    f.cl = pl[c];
+    f.wl = *reinterpret_cast<const uint2 *>(pl + 4 + 2 * ql);
+    f.sl = pl[11 + (ql ? ql : 1)];
+  }
+}
+
+__device__ __forceinline__ uint32_t occ1_end(uint32_t cnt, uint32_t sub, uint2 w, uint32_t off, uint32_t c) {
+  const uint32_t q = off >> 5;
+  uint32_t m0, m1;
+  chunk_masks(off & 31, m0, m1);
+  return cnt + (q ? (sub >> (8 * c)) & 0xFFu : 0u) + count1(w.x, w.y, m0, m1, c);
+}
+
+__device__ __forceinline__ void occ2_from1(const Fetch1 &f, uint32_t c, uint32_t &ok, uint32_t &ol) {
+  ok = f.kneg ? 0u : occ1_end(f.ck, f.sk, f.wk, f.offk, c);
+  ol = occ1_end(f.cl, f.sl, f.wl, f.offl, c);
+}
+
 __device__ __forceinline__ uint32_t occ_c(const uint4 &cnt, const uint4 &bs, const uint4 &sb, uint32_t off,
                                           uint32_t c) {
   uint32_t q = off >> 5, w0, w1, m0, m1;
@@ -77,29 +147,29 @@ __device__ __forceinline__ uint32_t strand_base(uint32_t c, int a, bool comp) {
 }
 
 // two bwt_cal_width chains in lockstep: str on ixa -> wa, strand-1 str on ixb -> wb
-__device__ void width_pair(const IndexView &ixa, const IndexView &ixb, int L, const uint8_t *s, bool comp,
+__device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView ixb, int L, const uint8_t *s, bool comp,
                            uint2 *wa, uint2 *wb) {
   uint32_t ka = 0, la = ixa.seq_len, kb = 0, lb = ixb.seq_len;
   uint32_t bida = 0, bidb = 0;
   for (int i = 0; i < L; ++i) {
     uint32_t ca = s[i];
     uint32_t cb = strand_base(ca, 1, comp);
-    Fetch fa, fb;
-    fetch_pair(ixa, ka - 1, la, fa);
-    fetch_pair(ixb, kb - 1, lb, fb);
+    Fetch1 fa, fb;
+    fetch1(ixa, ka - 1, la, ca & 3, ca < 4, fa);
+    fetch1(ixb, kb - 1, lb, cb & 3, cb < 4, fb);
     if (ca < 4) {
       uint32_t ok, ol;
-      occ2_from(fa, ca, ok, ol);
-      ka = ixa.L2[ca] + ok + 1;
-      la = ixa.L2[ca] + ol;
+      occ2_from1(fa, ca, ok, ol);
+      ka = l2of(ixa, ca) + ok + 1;
+      la = l2of(ixa, ca) + ol;
     }
     if (ka > la || ca > 3) { ka = 0; la = ixa.seq_len; ++bida; }
     wa[i] = make_uint2(la - ka + 1, bida);
     if (cb < 4) {
       uint32_t ok, ol;
-      occ2_from(fb, cb, ok, ol);
-      kb = ixb.L2[cb] + ok + 1;
-      lb = ixb.L2[cb] + ol;
+      occ2_from1(fb, cb, ok, ol);
+      kb = l2of(ixb, cb) + ok + 1;
+      lb = l2of(ixb, cb) + ol;
     }
     if (kb > lb || cb > 3) { kb = 0; lb = ixb.seq_len; ++bidb; }
     wb[i] = make_uint2(lb - kb + 1, bidb);
@@ -134,12 +204,12 @@ __device__ __forceinline__ bool match_exact_alt(const IndexView &ix, int i, cons
   for (int j = i - 1; j >= 0; --j) {
     uint32_t c = strand_base(s[j], a, comp);
     if (c > 3) return false;
-    Fetch f;
-    fetch_pair(ix, k - 1, l, f);
+    Fetch1 f;
+    fetch1(ix, k - 1, l, c, true, f);
     uint32_t ok, ol;
-    occ2_from(f, c, ok, ol);
-    k = ix.L2[c] + ok + 1;
-    l = ix.L2[c] + ol;
+    occ2_from1(f, c, ok, ol);
+    k = l2of(ix, c) + ok + 1;
+    l = l2of(ix, c) + ol;
     if (k > l) return false;
   }
   k0 = k;
@@ -150,14 +220,15 @@ __device__ __forceinline__ bool match_exact_alt(const IndexView &ix, int i, cons
 __global__ void __launch_bounds__(256) k_search(AlnArgs A) {
   const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= A.n) return;
-  const AlnOpt &o = A.o;
+  const AlnOpt o = A.o;
+  const IndexView ixv0 = A.ix[0], ixv1 = A.ix[1];
   const int64_t r = A.ids ? A.ids[lane] : lane;
   const int len = (int)A.len[r];
   const uint8_t *s = A.seq + A.off[r];
   const bool comp = o.mode & MODE_COMPREAD;
   uint2 *wbase = A.wbuf + (uint64_t)lane * A.wstride;
-  uint2 *W[2] = {wbase, wbase + A.wlen1};
-  const uint2 *SW[2] = {wbase + 2 * A.wlen1, wbase + 2 * A.wlen1 + (o.seed_len + 1)};
+  uint2 *const W0 = wbase, *const W1 = wbase + A.wlen1;
+  const uint2 *const SW0 = wbase + 2 * A.wlen1, *const SW1 = wbase + 2 * A.wlen1 + (o.seed_len + 1);
   const bool seeded = len > o.seed_len;  // bwtaln.c:127,132
   uint32_t *heads = A.heads + (uint64_t)lane * o.n_stacks;
   uint4 *ent = A.ent + (uint64_t)lane * A.cap;
@@ -209,8 +280,8 @@ __global__ void __launch_bounds__(256) k_search(AlnArgs A) {
     if (best > score) best = score;
   };
 
-  push(0, len, 0, A.ix[0].seq_len, 0, 0, 0, STATE_M, 0);
-  push(1, len, 0, A.ix[0].seq_len, 0, 0, 0, STATE_M, 0);
+  push(0, len, 0, ixv0.seq_len, 0, 0, 0, STATE_M, 0);
+  push(1, len, 0, ixv0.seq_len, 0, 0, 0, STATE_M, 0);
 
   while (n_entries && !dead) {
     if (n_entries > o.max_entries) break;
@@ -245,9 +316,9 @@ __global__ void __launch_bounds__(256) k_search(AlnArgs A) {
     int m = max_diff - (e_mm + e_go);
     if (o.mode & MODE_GAPE) m -= e_ge;
     if (m < 0) continue;
-    const IndexView &ix = A.ix[1 - a];
-    uint2 *width = W[a];
-    const uint2 *sw = SW[a];
+    const IndexView ix = a ? ixv0 : ixv1;
+    uint2 *width = a ? W1 : W0;
+    const uint2 *sw = a ? SW1 : SW0;
     int m_seed = 0;
     if (seeded) {
       m_seed = o.max_seed_diff - (e_mm + e_go);
@@ -321,7 +392,7 @@ __global__ void __launch_bounds__(256) k_search(AlnArgs A) {
         if (e_go < o.max_gapo) {
           push(a, i, k, l, e_mm, e_go + 1, e_ge, STATE_I, i);
           for (int j = 0; j != 4; ++j) {
-            uint32_t kk = ix.L2[j] + cnt_k[j] + 1, ll = ix.L2[j] + cnt_l[j];
+            uint32_t kk = l2of(ix, j) + cnt_k[j] + 1, ll = l2of(ix, j) + cnt_l[j];
             if (kk <= ll) push(a, i + 1, kk, ll, e_mm, e_go + 1, e_ge, STATE_D, i + 1);
           }
         }
@@ -331,7 +402,7 @@ __global__ void __launch_bounds__(256) k_search(AlnArgs A) {
         if (e_ge < o.max_gape) {
           if (e_ge + e_go < max_diff || occ < (uint32_t)o.max_del_occ) {
             for (int j = 0; j != 4; ++j) {
-              uint32_t kk = ix.L2[j] + cnt_k[j] + 1, ll = ix.L2[j] + cnt_l[j];
+              uint32_t kk = l2of(ix, j) + cnt_k[j] + 1, ll = l2of(ix, j) + cnt_l[j];
               if (kk <= ll) push(a, i + 1, kk, ll, e_mm, e_go, e_ge + 1, STATE_D, i + 1);
             }
           }
@@ -343,12 +414,12 @@ __global__ void __launch_bounds__(256) k_search(AlnArgs A) {
       for (int j = 1; j <= 4; ++j) {
         const uint32_t c = (ci + j) & 3;
         const int is_mm = (j != 4 || ci > 3);
-        uint32_t kk = ix.L2[c] + cnt_k[c] + 1, ll = ix.L2[c] + cnt_l[c];
+        uint32_t kk = l2of(ix, c) + cnt_k[c] + 1, ll = l2of(ix, c) + cnt_l[c];
         if (kk <= ll) push(a, i, kk, ll, e_mm + is_mm, e_go, e_ge, STATE_M, is_mm ? i : ldp);
       }
     } else if (ci < 4) {
       const uint32_t c = ci & 3;
-      uint32_t kk = ix.L2[c] + cnt_k[c] + 1, ll = ix.L2[c] + cnt_l[c];
+      uint32_t kk = l2of(ix, c) + cnt_k[c] + 1, ll = l2of(ix, c) + cnt_l[c];
       if (kk <= ll) push(a, i, kk, ll, e_mm, e_go, e_ge, STATE_M, ldp);
     }
   }

@@ -44,12 +44,33 @@ struct AlnArgs {
   AlnOpt o;
 };
 
+// Kernel arguments of the exact-match path: only what it reads (fewer SGPRs).
+struct ExactArgs {
+  IndexView ix[2];
+  const uint8_t *seq;
+  const uint64_t *off;
+  const uint32_t *len;
+  int64_t n;
+  uint4 *aln;
+  int32_t *n_aln;
+  uint32_t *status;
+  uint32_t aln_cap;
+  int mode;
+  const uint2 *kt0, *kt1;  // K-mer interval tables of .bwt / .rbwt (kmer.hip), or null
+  int K;                   // K-mer length (0: no table)
+};
+
+hipError_t build_kmer_table(const IndexView &ix, int K, uint2 *table, uint2 *tmp, hipStream_t st);
+
 hipError_t relayout_reference_bwt(const uint32_t *d_ref, uint64_t n_words, uint64_t n_blocks, uint4 *d_out,
                                   hipStream_t st);
 hipError_t pack_blocks(const uint32_t *d_sym, uint64_t n_sym_words, const uint4 *d_block_base, uint64_t n_blocks,
                        uint4 *d_out, hipStream_t st);
 hipError_t launch_width(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_search(const AlnArgs &a, int block, hipStream_t st);
+hipError_t launch_exact(const AlnArgs &a, const uint2 *kt0, const uint2 *kt1, int K, uint4 *rec, uint32_t stride,
+                        unsigned long long *d_counter, int blocks, hipStream_t st);
+uint32_t exact_record_stride(int max_len);
 hipError_t launch_occ4(const IndexView &ix, int64_t n, const uint32_t *k, uint32_t *cnt, hipStream_t st);
 hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_t *primary, uint32_t totals[4],
                         uint32_t *sa_sample, uint32_t sa_intv, int *rounds, hipStream_t st);

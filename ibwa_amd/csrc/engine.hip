@@ -96,8 +96,44 @@ struct ibwa_ctx {
   uint32_t stack_cap = 4096, aln_cap = 8;
   int block = 256;
   int64_t lanes_per_chunk = 1 << 18;
+  int exact_path = 1;       // use k_exact when max_diff == 0
+  int exact_blocks = 2048;  // persistent grid of k_exact (set from the CU count)
+  DBuf d_counter, d_rec;
+  // K-mer interval tables for the exact-match path (kmer.hip)
+  DBuf kt[2];
+  int kmer_k = -1;  // requested K (-1: auto from the genome size, 0: off)
+  int kmer_K = 0;   // K of the built tables
+  bool kmer_valid = false;
   ibwa_run_stats_t stats = {};
 };
+
+namespace {
+// (Re)build the K-mer tables for the resident index if needed.
+int ensure_kmer(ibwa_ctx *c) {
+  if (c->kmer_valid) return 0;
+  int K = c->kmer_k;
+  if (K < 0) {  // auto: ~log4(n) symbols leave most K-mers unique; cap the table at 2 x 2 GiB
+    K = 1;
+    while (K < 14 && (1ull << (2 * (K + 1))) <= (uint64_t)c->ix[0].seq_len) ++K;
+  }
+  if (K > 16) K = 16;
+  c->kmer_K = 0;
+  if (K > 0) {
+    DBuf tmp;
+    if (int rc = tmp.ensure((1ull << (2 * (K - 1))) * 8)) return rc;
+    for (int s = 0; s < 2; ++s) {
+      if (int rc = c->kt[s].ensure((1ull << (2 * K)) * 8)) { tmp.release(); return rc; }
+      hipError_t e = build_kmer_table(c->ix[s], K, c->kt[s].as<uint2>(), tmp.as<uint2>(), c->stream);
+      if (e != hipSuccess) { tmp.release(); return fail(IBWA_EHIP, "K-mer table: %s", hipGetErrorString(e)); }
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    tmp.release();
+    c->kmer_K = K;
+  }
+  c->kmer_valid = true;
+  return 0;
+}
+}  // namespace
 
 extern "C" {
 
@@ -138,6 +174,9 @@ int ibwa_ctx_create(int device, ibwa_ctx_t **out) {
   HIPCHK(hipSetDevice(device));
   ibwa_ctx *c = new ibwa_ctx();
   c->device = device;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+    c->exact_blocks = cus * 8;  // 8 x 256-thread blocks per CU: 32 waves/CU when registers allow
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (auto &x : c->ev) HIPCHK(hipEventCreate(&x));
   *out = c;
@@ -150,11 +189,21 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
-                  &c->r_status, &c->sa_s[0], &c->sa_s[1]})
+                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec})
     b->release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
+  std::string k = key ? key : "";
+  if (k == "exact_path") c->exact_path = value != 0;
+  else if (k == "kmer_k" && value >= -1 && value <= 16) { c->kmer_k = (int)value; c->kmer_valid = false; }
+  else if (k == "exact_blocks" && value > 0) c->exact_blocks = (int)value;
+  else if (k == "lanes_per_chunk" && value > 0) c->lanes_per_chunk = value;
+  else return fail(IBWA_EINVAL, "unknown option %s", k.c_str());
+  return 0;
 }
 
 int ibwa_ctx_set_tuning(ibwa_ctx_t *c, int stack_cap, int aln_cap, int block) {
@@ -192,6 +241,7 @@ int ibwa_ctx_load_bwt(ibwa_ctx_t *c, int strand, uint32_t primary, const uint32_
   ix.L2[0] = 0;
   for (int j = 0; j < 4; ++j) ix.L2[j + 1] = L2[j];
   c->loaded[strand] = true;
+  c->kmer_valid = false;
   return 0;
 }
 
@@ -226,6 +276,7 @@ int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
     dst->ix[s] = src->ix[s];
     dst->ix[s].blk = dst->idx[s].as<uint4>();
     dst->loaded[s] = true;
+    dst->kmer_valid = false;
   }
   return 0;
 }
@@ -266,6 +317,7 @@ int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa
     if (ix.L2[4] != n) { T.release(); return fail(IBWA_EHIP, "index build: symbol total %u != n", ix.L2[4]); }
     c->loaded[s] = true;
   }
+  c->kmer_valid = false;
   c->sa_intv = (uint32_t)sa_intv;
   T.release();
   return 0;
@@ -409,6 +461,45 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   A.wlen1 = (uint32_t)max_len + 1;
   A.wstride = 2ull * A.wlen1 + 2ull * ((uint64_t)std::max(opt->seed_len, 0) + 1);
   A.o = o;
+
+  const bool exact_path = c->exact_path && !o.fnr_pos && opt->max_diff == 0 && opt->max_entries >= 2;
+  c->stats.path = exact_path ? 1 : 0;
+  if (exact_path) {
+    A.aln_cap = c->aln_cap;
+    A.n = n;
+    if (int rc = c->d_aln.ensure(std::max<int64_t>(n, 1) * (uint64_t)A.aln_cap * 16)) return rc;
+    if (int rc = c->d_naln.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
+    if (int rc = c->d_status.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
+    if (int rc = c->d_counter.ensure(64)) return rc;
+    A.aln = c->d_aln.as<uint4>();
+    A.n_aln = c->d_naln.as<int32_t>();
+    A.status = c->d_status.as<uint32_t>();
+    if (int rc = ensure_kmer(c)) return rc;
+    c->stats.kmer_k = c->kmer_K;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    const uint32_t stride = exact_record_stride(max_len);
+    if (int rc = c->d_rec.ensure(std::max<int64_t>(n, 1) * (uint64_t)stride * 16)) return rc;
+    HIPCHK(launch_exact(A, c->kt[0].as<uint2>(), c->kt[1].as<uint2>(), c->kmer_K, c->d_rec.as<uint4>(), stride,
+                        c->d_counter.as<unsigned long long>(), c->exact_blocks, c->stream));
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[1]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    c->stats.ms_search = ms;
+    c->stats.n_launch_search = 1;
+    c->aln_cap_used = A.aln_cap;
+    c->h_naln.resize(n);
+    c->h_status.assign(n, 0);
+    if (n) {
+      HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    c->retry_ids.clear();
+    c->retry_alns.clear();
+    c->stats.ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+  }
 
   // first pass, in chunks of lanes_per_chunk reads
   const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), c->lanes_per_chunk);

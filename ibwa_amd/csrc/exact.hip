@@ -1,0 +1,249 @@
+// exact.hip -- the exact-match path of `aln -n 0` (max_diff == 0).
+//
+// Why this path exists and is exact: with max_diff == 0 the search of
+// bwtgap.c:104-264 never expands an entry.  The two root entries (strand 1
+// popped first, LIFO) have m == 0, so each is either pruned by
+// `m < width[len-1].bid` (:155) or resolved by bwt_match_exact_alt
+// (:160-163).  width[len-1].bid == 0 exactly when the read occurs in the text
+// -- the condition under which the exact search succeeds -- so the width
+// pass (bwtaln.c:123-130) decides nothing the exact search does not, and
+// gap_shadow is a no-op (last_diff_pos == 0).  Any N makes nN > max_diff
+// (:116-122).  Hence: hits = [strand 1 exact, strand 0 exact] (each if
+// found), each {0,0,0,a,k,l,score 0} -- verified bit-exact against the
+// reference goldens and the CPU restatement (tests/).
+//
+// Two kernels:
+//   k_pack_reads : streaming pre-pass, one read per lane: 2-bit codes, N flag,
+//                  the two K-mer table indices and the first symbol word.
+//   k_exact      : persistent; one read per lane, both strands advanced in
+//                  lockstep; every loop iteration is exactly one memory round
+//                  trip for every lane (rank queries, table lookups, the next
+//                  16-symbol word and new read headers are all issued before
+//                  the single wait), lanes refilled from a per-wave chunk.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "engine.h"
+#include "occ.h"
+
+namespace ibwa {
+
+namespace {
+
+constexpr int MODE_COMPREAD = 0x02;
+constexpr int EXACT_CHUNK = 512;
+
+// Record of read r at rec + r * stride (uint4 units):
+//   [0] = {len | hasN << 16, kmer index strand 1, kmer index strand 0, first symbol word}
+//   [1..] = 2-bit codes of bwa_seq_t.seq, 16 per dword, position p at bits 2*(p&15) of dword p>>4
+// `first symbol word` is the dword holding position len-1-K (table used) or len-1.
+__global__ void __launch_bounds__(256) k_pack_reads(const uint8_t *__restrict__ seq, const uint64_t *__restrict__ off,
+                                                    const uint32_t *__restrict__ len, int64_t n, uint4 *__restrict__ rec,
+                                                    uint32_t stride, int K, int comp) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int L = (int)len[r];
+  const uint8_t *s = seq + off[r];
+  uint4 *R = rec + (uint64_t)r * stride;
+  uint32_t *W = reinterpret_cast<uint32_t *>(R + 1);
+  const bool use_tab = K > 0 && L >= K;
+  const int p0 = use_tab ? L - 1 - K : L - 1;
+  uint32_t nN = 0, xa = 0, xb = 0, w = 0, first = 0;
+  for (int j = 0; j < L; ++j) {
+    const uint32_t c = s[j];
+    nN += c > 3;
+    const uint32_t c2 = c & 3;
+    xa = (xa << 2) | (comp ? c2 ^ 3u : c2);
+    xb = (xb << 2) | c2;
+    w |= c2 << (2 * (j & 15));
+    if ((j & 15) == 15 || j == L - 1) {
+      W[j >> 4] = w;
+      if (p0 >= 0 && (p0 >> 4) == (j >> 4)) first = w;
+      w = 0;
+    }
+  }
+  const uint32_t kmask = K >= 16 ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
+  R[0] = make_uint4((uint32_t)L | (nN ? 1u << 16 : 0u), use_tab ? xa & kmask : 0u, use_tab ? xb & kmask : 0u, first);
+}
+
+struct EndLoad {
+  uint4 cnt;
+  uint2 w;
+  uint32_t sub;
+};
+
+// issue the loads of one rank-query end (no dependence on the symbol)
+__device__ __forceinline__ void load_end(const IndexView &ix, uint32_t kk, bool run, EndLoad &e) {
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(ix.blk + (size_t)(kk >> 7) * 4);
+  const uint32_t q = (kk & 127) >> 5;
+  if (run) {
+    e.cnt = *reinterpret_cast<const uint4 *>(p);
+    e.w = *reinterpret_cast<const uint2 *>(p + 4 + 2 * q);
+    e.sub = p[11 + (q ? q : 1)];
+  }
+}
+
+__device__ __forceinline__ uint32_t occ_end(const EndLoad &e, uint32_t kk, uint32_t c) {
+  const uint32_t off = kk & 127, q = off >> 5;
+  uint32_t m0, m1;
+  chunk_masks(off & 31, m0, m1);
+  return sel4(e.cnt, c) + (q ? (e.sub >> (8 * c)) & 0xFFu : 0u) + count1(e.w.x, e.w.y, m0, m1, c);
+}
+
+// one chain: (k, l) -> extension by c, from the two ends' loads
+__device__ __forceinline__ void extend(const IndexView &ix, uint32_t &k, uint32_t &l, uint32_t c, const EndLoad &ek,
+                                       uint32_t kk, bool kneg, const EndLoad &el, uint32_t ll) {
+  const uint32_t ok = kneg ? 0u : occ_end(ek, kk, c);
+  const uint32_t ol = occ_end(el, ll, c);
+  const uint32_t base = l2of(ix, c);
+  k = base + ok + 1;
+  l = base + ol;
+}
+
+__global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restrict__ rec, uint32_t stride,
+                                               unsigned long long *counter) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  const bool comp = A.mode & MODE_COMPREAD;
+  const IndexView ix0 = A.ix[0], ix1 = A.ix[1];
+  const int K = A.K;
+  int64_t cur = 0, cend = 0;  // wave-uniform chunk cursor
+  bool more = true;
+  // lane state: 0 idle, 1 header requested, 2 running
+  int st = 0;
+  int64_t r = 0;
+  int len = 0, p = 0;         // p: next position (both strands advance together)
+  uint32_t ka = 0, la = 0, kb = 0, lb = 0, ia = 0, ib = 0, bw = 0;
+  bool ra = false, rb = false, fa = false, fb = false, lk = false;
+  for (;;) {
+    // ---- claim reads for idle lanes (no memory traffic unless the chunk runs out)
+    unsigned long long need = __ballot(st == 0);
+    while (need && more) {
+      if (cur >= cend) {
+        int64_t base = 0;
+        if (lane == 0) base = (int64_t)atomicAdd(counter, (unsigned long long)EXACT_CHUNK);
+        base = __shfl(base, 0);
+        if (base >= A.n) { more = false; break; }
+        cur = base;
+        cend = base + EXACT_CHUNK < A.n ? base + EXACT_CHUNK : A.n;
+      }
+      const int rank = __popcll(need & lt_mask);
+      const int64_t avail = cend - cur;
+      if (st == 0 && rank < avail) {
+        r = cur + rank;
+        st = 1;
+      }
+      const int64_t cnt = __popcll(need);
+      cur += avail < cnt ? avail : cnt;
+      need = __ballot(st == 0);
+    }
+    if (__ballot(st != 0) == 0ull) break;
+
+    // ---- issue every load of this step
+    const bool hdr = st == 1;
+    const bool run = st == 2;
+    const bool look_a = run && lk && ra, look_b = run && lk && rb;
+    const bool step_a = run && !lk && ra, step_b = run && !lk && rb;
+    const uint32_t c = (bw >> (2 * (p & 15))) & 3;  // symbol of seq at p (valid when running and !lk)
+    const uint32_t ca = comp ? c ^ 3u : c, cb = c;
+    uint4 h = make_uint4(0, 0, 0, 0);
+    if (hdr) h = rec[(uint64_t)r * stride];
+    uint2 ta = make_uint2(0, 0), tb = make_uint2(0, 0);
+    if (look_a) ta = A.kt0[ia];
+    if (look_b) tb = A.kt1[ib];
+    const bool ka_neg = ka == 0, kb_neg = kb == 0;  // k - 1 == (u32)-1
+    const uint32_t kka = ka_neg ? 0u : bwt_kk(ix0, ka - 1), lla = bwt_kk(ix0, la);
+    const uint32_t kkb = kb_neg ? 0u : bwt_kk(ix1, kb - 1), llb = bwt_kk(ix1, lb);
+    EndLoad eak, eal, ebk, ebl;
+    load_end(ix0, kka, step_a && !ka_neg, eak);
+    load_end(ix0, lla, step_a, eal);
+    load_end(ix1, kkb, step_b && !kb_neg, ebk);
+    load_end(ix1, llb, step_b, ebl);
+    // next symbol word: crossing into a new 16-symbol word on the next step
+    uint32_t nbw = 0;
+    const bool need_word = run && !lk && (ra || rb) && (p & 15) == 0 && p > 0;
+    if (need_word) nbw = reinterpret_cast<const uint32_t *>(rec + (uint64_t)r * stride + 1)[(p - 1) >> 4];
+
+    // ---- consume
+    if (hdr) {
+      len = (int)(h.x & 0xFFFF);
+      const bool hasN = (h.x >> 16) & 1;
+      ia = h.y;
+      ib = h.z;
+      bw = h.w;
+      ka = kb = 0;
+      la = ix0.seq_len;
+      lb = ix1.seq_len;
+      p = len - 1;
+      fa = fb = hasN;  // nN > max_diff (= 0): no hit
+      ra = rb = !hasN && len > 0;
+      lk = ra && K > 0 && len >= K;
+      st = 2;
+    } else if (run) {
+      if (lk) {
+        if (look_a) { ka = ta.x; la = ta.y; if (ka > la) { ra = false; fa = true; } }
+        if (look_b) { kb = tb.x; lb = tb.y; if (kb > lb) { rb = false; fb = true; } }
+        p -= K;
+        lk = false;
+      } else {
+        if (step_a) {
+          extend(ix0, ka, la, ca, eak, kka, ka_neg, eal, lla);
+          if (ka > la) { ra = false; fa = true; }
+        }
+        if (step_b) {
+          extend(ix1, kb, lb, cb, ebk, kkb, kb_neg, ebl, llb);
+          if (kb > lb) { rb = false; fb = true; }
+        }
+        if (need_word) bw = nbw;
+        --p;
+      }
+    }
+    if (st == 2 && (p < 0 || (!ra && !rb))) {
+      // both chains finished: a chain that did not fail consumed every symbol
+      uint4 *out = A.aln + (uint64_t)r * A.aln_cap;
+      int nh = 0;
+      if (!fa) out[nh++] = make_uint4(1u << 24, ka, la, 0u);
+      if (!fb) out[nh++] = make_uint4(0u, kb, lb, 0u);
+      A.n_aln[r] = nh;
+      A.status[r] = 0;
+      st = 0;
+    }
+  }
+}
+
+}  // namespace
+
+uint32_t exact_record_stride(int max_len) {  // in uint4 units
+  return 1u + (uint32_t)((max_len + 63) / 64);
+}
+
+hipError_t launch_exact(const AlnArgs &a, const uint2 *kt0, const uint2 *kt1, int K, uint4 *rec, uint32_t stride,
+                        unsigned long long *d_counter, int blocks, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  const int comp = (a.o.mode & MODE_COMPREAD) ? 1 : 0;
+  hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a.seq, a.off, a.len, a.n,
+                     rec, stride, K, comp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  if (e != hipSuccess) return e;
+  ExactArgs x;
+  x.ix[0] = a.ix[0];
+  x.ix[1] = a.ix[1];
+  x.seq = a.seq;
+  x.off = a.off;
+  x.len = a.len;
+  x.n = a.n;
+  x.aln = a.aln;
+  x.n_aln = a.n_aln;
+  x.status = a.status;
+  x.aln_cap = a.aln_cap;
+  x.mode = a.o.mode;
+  x.kt0 = kt0;
+  x.kt1 = kt1;
+  x.K = K;
+  hipLaunchKernelGGL(k_exact, dim3(blocks), dim3(256), 0, st, x, rec, stride, d_counter);
+  return hipGetLastError();
+}
+
+}  // namespace ibwa

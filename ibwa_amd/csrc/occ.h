@@ -29,6 +29,11 @@ struct IndexView {
   uint32_t L2[5];
 };
 
+// L2[c] by selects: a dynamic index into the kernel-argument array would go through scratch
+__device__ __forceinline__ uint32_t l2of(const IndexView &ix, uint32_t c) {
+  return c == 0 ? ix.L2[0] : c == 1 ? ix.L2[1] : c == 2 ? ix.L2[2] : ix.L2[3];
+}
+
 __device__ __forceinline__ uint32_t bwt_kk(const IndexView &ix, uint32_t k) {
   return k >= ix.primary ? k - 1 : k;  // bwt.c:97
 }

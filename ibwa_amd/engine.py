@@ -28,7 +28,7 @@ class GapOpt(c.Structure):
 class RunStats(c.Structure):
     _fields_ = [("ms_width", c.c_double), ("ms_search", c.c_double), ("ms_retry", c.c_double),
                 ("ms_total", c.c_double), ("n_retry", c.c_int64), ("n_launch_width", c.c_int64),
-                ("n_launch_search", c.c_int64)]
+                ("n_launch_search", c.c_int64), ("path", c.c_int), ("kmer_k", c.c_int)]
 
 
 assert c.sizeof(GapOpt) == 64
@@ -56,6 +56,7 @@ CAPI = {
     "ibwa_batch_fetch": (_i, [_vp, _vp, c.POINTER(_vp), c.POINTER(_i64)]),
     "ibwa_batch_stats": (_i, [_vp, c.POINTER(RunStats)]),
     "ibwa_ctx_set_tuning": (_i, [_vp, _i, _i, _i]),
+    "ibwa_ctx_set_option": (_i, [_vp, c.c_char_p, c.c_long]),
     "ibwa_occ4": (_i, [_vp, _i, _i64, _vp, _vp]),
     "ibwa_ctx_build_index": (_i, [_vp, _vp, _u64, _i]),
     "ibwa_ctx_bwt_info": (_i, [_vp, _i, c.POINTER(_u32), c.POINTER(_u32), c.POINTER(_u64)]),
@@ -139,6 +140,9 @@ class Engine:
 
     def set_tuning(self, stack_cap=0, aln_cap=0, block=0):
         _chk(lib().ibwa_ctx_set_tuning(self.h, stack_cap, aln_cap, block))
+
+    def set_option(self, key, value):
+        _chk(lib().ibwa_ctx_set_option(self.h, key.encode(), int(value)))
 
     def stage(self, seqs, offs, lens):
         self._keep = (np.ascontiguousarray(seqs, dtype=np.uint8), np.ascontiguousarray(offs, dtype=np.uint64),

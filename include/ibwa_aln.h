@@ -113,8 +113,13 @@ typedef struct {
 	double ms_total;       /* ibwa_batch_run wall, device-synchronised */
 	int64_t n_retry;       /* reads re-run in the large-capacity pass */
 	int64_t n_launch_width, n_launch_search;
+	int path;              /* 0: width + gapped search; 1: exact-match path (max_diff == 0) */
+	int kmer_k;            /* K of the K-mer interval table the exact path used (0: none) */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
+
+/* Named engine options: "exact_path" (0/1, default 1), "exact_blocks", "lanes_per_chunk". */
+int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
 /* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */
 int ibwa_ctx_set_tuning(ibwa_ctx_t *ctx, int stack_cap, int aln_cap, int block);

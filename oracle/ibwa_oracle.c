@@ -498,6 +498,47 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 	(void)best_diff;
 }
 
+/* Occ-interval touches (SURVEY §8d counting rules) of the exact-match path the
+ * GPU takes for max_diff == 0: strand 1 = bwt_match_exact_alt(bwt0, rseq),
+ * strand 0 = bwt_match_exact_alt(bwt1, seq), none for reads with an N.  Used
+ * to price the GPU path's own algorithmic bytes (it skips bwt_cal_width). */
+/* one exact chain priced with a K-mer table: the first K steps are one lookup */
+static void exact_chain_touches(const or_bwt_t *b, int L, const uint8_t *str, int K, uint32_t *t)
+{
+	uint32_t k = 0, l = b->seq_len, dummy = 0;
+	if (K > 0 && L >= K) {
+		++*t;
+		if (!match_exact_alt(b, K, str + L - K, &k, &l, &dummy)) return;
+		L -= K;
+	}
+	match_exact_alt(b, L, str, &k, &l, t);
+}
+
+void or_exact_touches(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_seqs, const uint8_t *seq,
+                      const uint64_t *off, const uint32_t *len, int mode, int K, uint32_t *touches)
+{
+	int64_t r;
+	uint8_t *rseq = 0;
+	int cap = 0;
+	for (r = 0; r < n_seqs; ++r) {
+		int L = (int)len[r], j, nN = 0;
+		const uint8_t *s = seq + off[r];
+		uint32_t t = 0, k, l;
+		if (L + 1 > cap) { cap = L + 1; rseq = (uint8_t*)realloc(rseq, cap); }
+		for (j = 0; j < L; ++j) {
+			nN += s[j] > 3;
+			rseq[j] = (mode & OR_MODE_COMPREAD) && s[j] < 4 ? 3 - s[j] : s[j];
+		}
+		if (nN == 0) {
+			exact_chain_touches(bwt0, L, rseq, K, &t);
+			exact_chain_touches(bwt1, L, s, K, &t);
+		}
+		(void)k; (void)l;
+		touches[r] = t;
+	}
+	free(rseq);
+}
+
 /* ---------------- batch driver (bwtaln.c:80-140, 151-156, 199-218) ---------------- */
 
 typedef struct {

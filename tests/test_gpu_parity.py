@@ -29,7 +29,10 @@ def test_occ4_kats_gpu(golden_dir, gpu_engine):
         assert (got == np.array([r[1:] for r in rows], dtype=np.uint32)).all(), which
 
 
-def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine):
+@pytest.mark.parametrize("exact_path", [1, 0])
+def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path):
+    """exact_path=0 forces -n 0 through the general width + search kernels too."""
+    gpu_engine.set_option("exact_path", exact_path)
     bad = []
     for key, m in sorted(sai_manifest.items()):
         opt, _ = oracle.parse_aln_args(m["argv"])
@@ -40,6 +43,9 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine):
         exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
         if not oracle.sai_body_equal(got, exp):
             bad.append(key)
+        if m["argv"] == ["-n", "0"]:
+            assert gpu_engine.stats().path == exact_path, key
+    gpu_engine.set_option("exact_path", 1)
     assert not bad, bad
 
 

@@ -1,0 +1,88 @@
+"""Parity at sizes the golden fixtures do not reach (31 Mb genome built on device).
+
+* round trip: reads copied exactly from the genome must all be found by
+  `aln -n 0`, on the strand they were drawn from (strand 0 = forward);
+* GPU == CPU restatement on seeded reads for default gapped options, -n 0,
+  and a 150 bp / 2 % error set, including the overflow-retry path.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from ibwa_amd import _native
+from ibwa_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mid_genome():
+    L = _native.lib()
+    lens = (ctypes.c_uint64 * 24)()
+    tot = L.ibwa_synth_grch37_lengths(1, 100, lens)
+    ascii_ = np.empty(tot, dtype=np.uint8)
+    L.ibwa_synth_genome(77, 24, lens, 0.45, 0.01, 120, ascii_.ctypes.data, 8)
+    codes = np.empty(tot, dtype=np.uint8)
+    L.ibwa_pack_nt4_mt(ascii_.ctypes.data, tot, codes.ctypes.data, 8)
+    eng = E.Engine(0)
+    eng.build_index(codes)
+    p0, l0, w0 = eng.export_bwt(0)
+    p1, l1, w1 = eng.export_bwt(1)
+    b0 = oracle.Bwt(primary=p0, L2=l0, words=w0)
+    b1 = oracle.Bwt(primary=p1, L2=l1, words=w1)
+    yield ascii_, [int(x) for x in lens], eng, b0, b1
+    eng.close()
+
+
+def reads(ascii_, lens, seed, n, ln, sub, indel):
+    L = _native.lib()
+    c_lens = (ctypes.c_uint64 * 24)(*lens)
+    raw = np.empty(n * ln, dtype=np.uint8)
+    pos = np.empty(n, dtype=np.uint64)
+    strand = np.empty(n, dtype=np.uint8)
+    L.ibwa_synth_reads(seed, ascii_.ctypes.data, ascii_.size, 24, c_lens, n, ln, sub, indel, raw.ctypes.data,
+                       pos.ctypes.data, strand.ctypes.data, 8)
+    seq = np.empty(n * ln, dtype=np.uint8)
+    off = np.empty(n, dtype=np.uint64)
+    lns = np.empty(n, dtype=np.uint32)
+    L.ibwa_encode_reads_fixed(raw.ctypes.data, n, ln, seq.ctypes.data, off.ctypes.data, lns.ctypes.data, 8)
+    return seq, off, lns, strand, raw
+
+
+def eopt(argv):
+    o, _ = oracle.parse_aln_args(argv)
+    e = E.GapOpt()
+    for f, _ in E.GapOpt._fields_:
+        setattr(e, f, getattr(o, f))
+    return o, e
+
+
+def test_exact_reads_round_trip(mid_genome):
+    ascii_, lens, eng, _, _ = mid_genome
+    seq, off, lns, strand, raw = reads(ascii_, lens, 11, 200_000, 100, 0.0, 0.0)
+    has_n = (seq.reshape(-1, 100) > 3).any(axis=1)
+    _, e = eopt(["-n", "0"])
+    n_aln, alns = eng.aln(seq, off, lns, e)
+    assert (n_aln[~has_n] >= 1).all()
+    first = np.concatenate([[0], np.cumsum(n_aln)[:-1]])
+    a = (alns["info"] >> 24) & 1
+    # the drawing strand is always among the hits: strand 0 = forward = a 0
+    ok = np.zeros(len(n_aln), bool)
+    for j in range(2):
+        sel = n_aln > j
+        ok[sel] |= a[first[sel] + j] == strand[sel]
+    assert ok[~has_n].all()
+
+
+@pytest.mark.parametrize("argv,ln,sub,n", [([], 100, 0.01, 30_000), (["-n", "0"], 100, 0.01, 100_000),
+                                           ([], 150, 0.02, 8_000), (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000)])
+def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n):
+    ascii_, lens, eng, b0, b1 = mid_genome
+    seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
+    o, e = eopt(argv)
+    n_aln, alns = eng.aln(seq, off, lns, e)
+    rn, ra, _ = oracle.cal_sa_reg_gap(b0, b1, seq, off, lns, o, n_threads=8)
+    assert (n_aln == rn).all()
+    assert alns.tobytes() == ra.tobytes()
