@@ -58,6 +58,7 @@ struct ExactArgs {
   int mode;
   const uint2 *kt0, *kt1;  // K-mer interval tables of .bwt / .rbwt (kmer.hip), or null
   int K;                   // K-mer length (0: no table)
+  const uint4 *o64[2];     // bit-plane Occ layouts (occ64.hip)
 };
 
 hipError_t build_kmer_table(const IndexView &ix, int K, uint2 *table, uint2 *tmp, hipStream_t st);
@@ -68,8 +69,11 @@ hipError_t pack_blocks(const uint32_t *d_sym, uint64_t n_sym_words, const uint4 
                        uint4 *d_out, hipStream_t st);
 hipError_t launch_width(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_search(const AlnArgs &a, int block, hipStream_t st);
-hipError_t launch_exact(const AlnArgs &a, const uint2 *kt0, const uint2 *kt1, int K, uint4 *rec, uint32_t stride,
-                        unsigned long long *d_counter, int blocks, hipStream_t st);
+hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1, const uint2 *kt0,
+                        const uint2 *kt1, int K, uint4 *rec, uint32_t stride, unsigned long long *d_counter,
+                        int blocks, hipStream_t st);
+uint64_t occ64_blocks(uint32_t seq_len);
+hipError_t build_occ64(const IndexView &ix, uint4 *out, hipStream_t st);
 uint32_t exact_record_stride(int max_len);
 hipError_t launch_occ4(const IndexView &ix, int64_t n, const uint32_t *k, uint32_t *cnt, hipStream_t st);
 hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_t *primary, uint32_t totals[4],

@@ -99,8 +99,9 @@ struct ibwa_ctx {
   int exact_path = 1;       // use k_exact when max_diff == 0
   int exact_blocks = 2048;  // persistent grid of k_exact (set from the CU count)
   DBuf d_counter, d_rec;
+  bool naln_on_host = true;  // h_naln mirrors d_naln
   // K-mer interval tables for the exact-match path (kmer.hip)
-  DBuf kt[2];
+  DBuf kt[2], o64[2];
   int kmer_k = -1;  // requested K (-1: auto from the genome size, 0: off)
   int kmer_K = 0;   // K of the built tables
   bool kmer_valid = false;
@@ -112,12 +113,24 @@ namespace {
 int ensure_kmer(ibwa_ctx *c) {
   if (c->kmer_valid) return 0;
   int K = c->kmer_k;
-  if (K < 0) {  // auto: ~log4(n) symbols leave most K-mers unique; cap the table at 2 x 2 GiB
+  if (K < 0) {
+    // auto: K ~ log4(2n) (past that most K-mers are absent), up to 15 (2 x 8.6 GB for a
+    // human genome; K = 16 measured slower: 2 x 34 GB of randomly probed tables),
+    // and both tables within 40 % of the free HBM
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     K = 1;
-    while (K < 14 && (1ull << (2 * (K + 1))) <= (uint64_t)c->ix[0].seq_len) ++K;
+    while (K < 15 && (1ull << (2 * (K + 1))) <= 2ull * c->ix[0].seq_len &&
+           2ull * 8ull * (1ull << (2 * (K + 1))) <= (uint64_t)(0.4 * (double)free_b))
+      ++K;
   }
   if (K > 16) K = 16;
   c->kmer_K = 0;
+  // bit-plane Occ layouts (occ64.hip), 1 byte per BWT row and strand
+  for (int s = 0; s < 2; ++s) {
+    if (int rc = c->o64[s].ensure(occ64_blocks(c->ix[s].seq_len) * 64)) return rc;
+    HIPCHK(build_occ64(c->ix[s], c->o64[s].as<uint4>(), c->stream));
+  }
   if (K > 0) {
     DBuf tmp;
     if (int rc = tmp.ensure((1ull << (2 * (K - 1))) * 8)) return rc;
@@ -189,7 +202,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
-                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec})
+                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1]})
     b->release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(c->stream);
@@ -479,7 +492,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     const uint32_t stride = exact_record_stride(max_len);
     if (int rc = c->d_rec.ensure(std::max<int64_t>(n, 1) * (uint64_t)stride * 16)) return rc;
-    HIPCHK(launch_exact(A, c->kt[0].as<uint2>(), c->kt[1].as<uint2>(), c->kmer_K, c->d_rec.as<uint4>(), stride,
+    HIPCHK(launch_exact(A, c->o64[0].as<uint4>(), c->o64[1].as<uint4>(), c->kt[0].as<uint2>(),
+                        c->kt[1].as<uint2>(), c->kmer_K, c->d_rec.as<uint4>(), stride,
                         c->d_counter.as<unsigned long long>(), c->exact_blocks, c->stream));
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[1]));
@@ -489,11 +503,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->stats.n_launch_search = 1;
     c->aln_cap_used = A.aln_cap;
     c->h_naln.resize(n);
-    c->h_status.assign(n, 0);
-    if (n) {
-      HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
-    }
+    c->h_status.clear();
+    c->naln_on_host = false;  // results stay in HBM; ibwa_batch_fetch copies them
     c->retry_ids.clear();
     c->retry_alns.clear();
     c->stats.ms_total =
@@ -542,6 +553,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(hipMemcpyAsync(c->h_status.data(), c->d_status.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }
+  c->naln_on_host = true;
   c->retry_ids.clear();
   c->retry_alns.clear();
   for (int64_t i = 0; i < n; ++i) {
@@ -627,6 +639,12 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
   const uint32_t cap = c->aln_cap_used;
   c->h_aln.resize(std::max<int64_t>(n, 1) * cap);
   if (n) {
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->naln_on_host) {
+      c->h_naln.resize(n);
+      HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+      c->naln_on_host = true;
+    }
     HIPCHK(hipMemcpyAsync(c->h_aln.data(), c->d_aln.p, n * (uint64_t)cap * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }

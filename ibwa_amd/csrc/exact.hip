@@ -66,39 +66,32 @@ __global__ void __launch_bounds__(256) k_pack_reads(const uint8_t *__restrict__ 
   R[0] = make_uint4((uint32_t)L | (nN ? 1u << 16 : 0u), use_tab ? xa & kmask : 0u, use_tab ? xb & kmask : 0u, first);
 }
 
-struct EndLoad {
-  uint4 cnt;
-  uint2 w;
-  uint32_t sub;
-};
-
-// issue the loads of one rank-query end (no dependence on the symbol)
-__device__ __forceinline__ void load_end(const IndexView &ix, uint32_t kk, bool run, EndLoad &e) {
-  const uint32_t *p = reinterpret_cast<const uint32_t *>(ix.blk + (size_t)(kk >> 7) * 4);
-  const uint32_t q = (kk & 127) >> 5;
-  if (run) {
-    e.cnt = *reinterpret_cast<const uint4 *>(p);
-    e.w = *reinterpret_cast<const uint2 *>(p + 4 + 2 * q);
-    e.sub = p[11 + (q ? q : 1)];
-  }
+// bit-plane rank query (occ64.hip): {C[c], 0, P_lo[c], P_hi[c]} of the 64-row block of `row`
+__device__ __forceinline__ uint4 load64(const uint4 *o, uint32_t row, uint32_t c, bool run) {
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (run) v = o[(size_t)(row >> 6) * 4 + c];
+  return v;
 }
 
-__device__ __forceinline__ uint32_t occ_end(const EndLoad &e, uint32_t kk, uint32_t c) {
-  const uint32_t off = kk & 127, q = off >> 5;
-  uint32_t m0, m1;
-  chunk_masks(off & 31, m0, m1);
-  return sel4(e.cnt, c) + (q ? (e.sub >> (8 * c)) & 0xFFu : 0u) + count1(e.w.x, e.w.y, m0, m1, c);
+__device__ __forceinline__ uint32_t occ64(const uint4 &v, uint32_t row) {
+  const uint32_t o = row & 63;
+  const uint32_t mlo = o >= 31 ? 0xFFFFFFFFu : ((2u << o) - 1u);
+  const uint32_t mhi = o < 32 ? 0u : (o == 63 ? 0xFFFFFFFFu : ((2u << (o - 32)) - 1u));
+  return v.x + (uint32_t)__builtin_popcount(v.z & mlo) + (uint32_t)__builtin_popcount(v.w & mhi);
 }
 
-// one chain: (k, l) -> extension by c, from the two ends' loads
-__device__ __forceinline__ void extend(const IndexView &ix, uint32_t &k, uint32_t &l, uint32_t c, const EndLoad &ek,
-                                       uint32_t kk, bool kneg, const EndLoad &el, uint32_t ll) {
-  const uint32_t ok = kneg ? 0u : occ_end(ek, kk, c);
-  const uint32_t ol = occ_end(el, ll, c);
+// bwt_2occ + the interval update of bwt_match_exact_alt (bwt.c:243-245);
+// `vk` is the k-1 end's block, or a copy of `vl` when both ends share it
+__device__ __forceinline__ void extend64(const IndexView &ix, uint32_t &k, uint32_t &l, uint32_t c, const uint4 &vk,
+                                         const uint4 &vl) {
+  const uint32_t ok = k == 0 ? 0u : occ64(vk, k - 1);
+  const uint32_t ol = occ64(vl, l);
   const uint32_t base = l2of(ix, c);
   k = base + ok + 1;
   l = base + ol;
 }
+
+__device__ __forceinline__ bool share_block(uint32_t k, uint32_t l) { return k != 0 && ((k - 1) >> 6) == (l >> 6); }
 
 __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restrict__ rec, uint32_t stride,
                                                unsigned long long *counter) {
@@ -151,14 +144,11 @@ __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restr
     uint2 ta = make_uint2(0, 0), tb = make_uint2(0, 0);
     if (look_a) ta = A.kt0[ia];
     if (look_b) tb = A.kt1[ib];
-    const bool ka_neg = ka == 0, kb_neg = kb == 0;  // k - 1 == (u32)-1
-    const uint32_t kka = ka_neg ? 0u : bwt_kk(ix0, ka - 1), lla = bwt_kk(ix0, la);
-    const uint32_t kkb = kb_neg ? 0u : bwt_kk(ix1, kb - 1), llb = bwt_kk(ix1, lb);
-    EndLoad eak, eal, ebk, ebl;
-    load_end(ix0, kka, step_a && !ka_neg, eak);
-    load_end(ix0, lla, step_a, eal);
-    load_end(ix1, kkb, step_b && !kb_neg, ebk);
-    load_end(ix1, llb, step_b, ebl);
+    const bool sha = share_block(ka, la), shb = share_block(kb, lb);
+    const uint4 val = load64(A.o64[0], la, ca, step_a);
+    const uint4 vbl = load64(A.o64[1], lb, cb, step_b);
+    uint4 vak = load64(A.o64[0], ka - 1, ca, step_a && ka != 0 && !sha);
+    uint4 vbk = load64(A.o64[1], kb - 1, cb, step_b && kb != 0 && !shb);
     // next symbol word: crossing into a new 16-symbol word on the next step
     uint32_t nbw = 0;
     const bool need_word = run && !lk && (ra || rb) && (p & 15) == 0 && p > 0;
@@ -187,11 +177,13 @@ __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restr
         lk = false;
       } else {
         if (step_a) {
-          extend(ix0, ka, la, ca, eak, kka, ka_neg, eal, lla);
+          if (sha) vak = val;
+          extend64(ix0, ka, la, ca, vak, val);
           if (ka > la) { ra = false; fa = true; }
         }
         if (step_b) {
-          extend(ix1, kb, lb, cb, ebk, kkb, kb_neg, ebl, llb);
+          if (shb) vbk = vbl;
+          extend64(ix1, kb, lb, cb, vbk, vbl);
           if (kb > lb) { rb = false; fb = true; }
         }
         if (need_word) bw = nbw;
@@ -217,8 +209,9 @@ uint32_t exact_record_stride(int max_len) {  // in uint4 units
   return 1u + (uint32_t)((max_len + 63) / 64);
 }
 
-hipError_t launch_exact(const AlnArgs &a, const uint2 *kt0, const uint2 *kt1, int K, uint4 *rec, uint32_t stride,
-                        unsigned long long *d_counter, int blocks, hipStream_t st) {
+hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1, const uint2 *kt0,
+                        const uint2 *kt1, int K, uint4 *rec, uint32_t stride, unsigned long long *d_counter,
+                        int blocks, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   const int comp = (a.o.mode & MODE_COMPREAD) ? 1 : 0;
   hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a.seq, a.off, a.len, a.n,
@@ -242,6 +235,8 @@ hipError_t launch_exact(const AlnArgs &a, const uint2 *kt0, const uint2 *kt1, in
   x.kt0 = kt0;
   x.kt1 = kt1;
   x.K = K;
+  x.o64[0] = o64_0;
+  x.o64[1] = o64_1;
   hipLaunchKernelGGL(k_exact, dim3(blocks), dim3(256), 0, st, x, rec, stride, d_counter);
   return hipGetLastError();
 }
