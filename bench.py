@@ -233,7 +233,8 @@ def main():
                 # the general path runs the reference algorithm: its touches are the oracle's;
                 # the two kernels (width, search) are priced together
                 path_touches = touches
-                kname, k_ms = "k_width+k_search", (ms_w + ms_s) / launches
+                kname = "k_width+k_gapped" if path == 2 else "k_width+k_search"
+                k_ms = (ms_w + ms_s) / launches
             ach = path_touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9
             result["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": kname,
@@ -241,8 +242,10 @@ def main():
                                   "touches_per_read": path_touches, "bytes_per_touch": 64,
                                   "reference_touches_per_read": touches,
                                   "reference_equivalent_GBps": touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9}
+        stl = eng.stats()
         result["extra"] = {"index_build_s": build_s, "n_retry": int(n_retry), "parity_sample_ok": check_ok,
-                           "path": "exact" if path == 1 else "width+search",
+                           "n_stack_overflow": int(stl.n_stack_overflow), "n_aln_overflow": int(stl.n_aln_overflow),
+                           "path": {0: "width+search", 1: "exact", 2: "width+gapped"}.get(path, str(path)),
                            "k_width_ms": ms_w / launches, "k_search_ms": ms_s / launches,
                            "retry_ms": ms_r / launches}
         print(json.dumps(result), flush=True)

@@ -189,6 +189,11 @@ __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
   uint2 *w1 = w0 + A.wlen1;
   uint2 *sw0 = w1 + A.wlen1;
   uint2 *sw1 = sw0 + (A.o.seed_len + 1);
+  if (A.nN) {
+    uint32_t nN = 0;
+    for (int j = 0; j < L; ++j) nN += s[j] > 3;
+    A.nN[lane] = (uint16_t)(nN > 0xFFFFu ? 0xFFFFu : nN);
+  }
   width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1);
   if (L > A.o.seed_len) width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1);
 }

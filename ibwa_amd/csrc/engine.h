@@ -41,8 +41,40 @@ struct AlnArgs {
   int32_t *n_aln;            // per lane
   uint32_t aln_cap;
   uint32_t *status;          // per lane ST_* flags
+  uint16_t *nN;              // per lane N count (k_width output, may be null)
   AlnOpt o;
 };
+
+// Kernel arguments of the persistent gapped search (gapped.hip).
+struct GapArgs {
+  IndexView ix[2];
+  const uint4 *o64[2];       // bit-plane Occ blocks (occ64.hip)
+  const uint8_t *seq;
+  const uint64_t *off;
+  const uint32_t *len;
+  const int64_t *ids;        // read r of this launch -> input read (nullptr: identity)
+  int64_t n;
+  const int16_t *maxdiff_tab;
+  uint2 *wbuf;               // widths of read r at wbuf + r * wstride (k_width)
+  uint64_t wstride;
+  uint32_t wlen1;
+  const uint16_t *nN;        // per read N count (k_width)
+  uint4 *ent;                // per-lane primary stack regions, cap1 slots each
+  uint32_t cap1;
+  uint4 *pool;               // extension regions, cap2 slots each
+  uint32_t cap2;
+  unsigned long long *pool_next;
+  unsigned long long pool_n;
+  uint4 *aln;                // hits of read r at aln + r * aln_cap
+  int32_t *n_aln;
+  uint32_t aln_cap;
+  uint32_t *status;
+  AlnOpt o;
+};
+size_t gapped_lds_bytes(int n_stacks, int block, bool wide);
+// wide: 24-bit slot links (reads < 4096 bp), for the large-capacity retry pass
+hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int blocks, int block, bool wide,
+                         hipStream_t st);
 
 // Kernel arguments of the exact-match path: only what it reads (fewer SGPRs).
 struct ExactArgs {

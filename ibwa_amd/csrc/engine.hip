@@ -99,6 +99,15 @@ struct ibwa_ctx {
   int exact_path = 1;       // use k_exact when max_diff == 0
   int exact_blocks = 2048;  // persistent grid of k_exact (set from the CU count)
   DBuf d_counter, d_rec;
+  int n_cus = 256;
+  // persistent gapped search (gapped.hip)
+  int gapped_v2 = 1;
+  int gap_blocks_per_cu = 3;         // 134 VGPRs -> 3 waves per SIMD
+  uint32_t gap_cap1 = 8192;          // per-lane primary stack slots
+  uint64_t gap_pool_n = 8192;        // extension regions of 65535 - gap_cap1 slots
+  uint32_t gap_aln_cap = 64;         // hit slots per read
+  int64_t gap_reads_per_chunk = 1 << 22;
+  DBuf d_nN, d_pool;
   bool naln_on_host = true;  // h_naln mirrors d_naln
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
@@ -146,6 +155,28 @@ int ensure_kmer(ibwa_ctx *c) {
   c->kmer_valid = true;
   return 0;
 }
+// Kernel arguments of the persistent gapped search shared by the first and retry passes;
+// the caller fills the per-pass scratch and output pointers.
+GapArgs gap_args(const ibwa_ctx *c, const AlnArgs &A, const AlnOpt &o, int64_t b0, int64_t cnt) {
+  GapArgs G = {};
+  G.ix[0] = c->ix[0];
+  G.ix[1] = c->ix[1];
+  G.o64[0] = c->o64[0].as<uint4>();
+  G.o64[1] = c->o64[1].as<uint4>();
+  G.seq = A.seq;
+  G.off = A.off + b0;
+  G.len = A.len + b0;
+  G.ids = nullptr;
+  G.n = cnt;
+  G.maxdiff_tab = A.maxdiff_tab;
+  G.wbuf = c->d_wbuf.as<uint2>();
+  G.wstride = A.wstride;
+  G.wlen1 = A.wlen1;
+  G.nN = c->d_nN.as<uint16_t>();
+  G.pool_next = c->d_counter.as<unsigned long long>() + 1;
+  G.o = o;
+  return G;
+}
 }  // namespace
 
 extern "C" {
@@ -189,7 +220,10 @@ int ibwa_ctx_create(int device, ibwa_ctx_t **out) {
   c->device = device;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+  {
     c->exact_blocks = cus * 8;  // 8 x 256-thread blocks per CU: 32 waves/CU when registers allow
+    c->n_cus = cus;
+  }
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (auto &x : c->ev) HIPCHK(hipEventCreate(&x));
   *out = c;
@@ -202,7 +236,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
-                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1]})
+                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool})
     b->release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(c->stream);
@@ -215,6 +249,12 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "kmer_k" && value >= -1 && value <= 16) { c->kmer_k = (int)value; c->kmer_valid = false; }
   else if (k == "exact_blocks" && value > 0) c->exact_blocks = (int)value;
   else if (k == "lanes_per_chunk" && value > 0) c->lanes_per_chunk = value;
+  else if (k == "gapped_v2") c->gapped_v2 = value != 0;
+  else if (k == "gap_blocks_per_cu" && value > 0 && value <= 8) c->gap_blocks_per_cu = (int)value;
+  else if (k == "gap_cap1" && value >= 2 && value < 65535) c->gap_cap1 = (uint32_t)value;
+  else if (k == "gap_pool_n" && value >= 0) c->gap_pool_n = (uint64_t)value;
+  else if (k == "gap_aln_cap" && value > 0 && value <= 4096) c->gap_aln_cap = (uint32_t)value;
+  else if (k == "gap_reads_per_chunk" && value > 0) c->gap_reads_per_chunk = value;
   else return fail(IBWA_EINVAL, "unknown option %s", k.c_str());
   return 0;
 }
@@ -512,10 +552,73 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     return 0;
   }
 
+  // persistent gapped search (gapped.hip) when the options fit its entry bit fields
+  const bool v2 = c->gapped_v2 && batch_md + 1 <= 31 && o.max_gapo <= 7 && o.max_gape <= 15 &&
+                  gapped_lds_bytes(o.n_stacks, 64, true) <= 65536 && max_len <= 65535;
+  float ms_w = 0, ms_s = 0;
+  if (v2) {
+    if (int rc = ensure_kmer(c)) return rc;
+    c->stats.path = 2;
+    const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), c->gap_reads_per_chunk);
+    A.aln_cap = c->gap_aln_cap;
+    // LDS bucket heads: n_stacks u16 per lane, at most 64 KiB per workgroup
+    const int block = gapped_lds_bytes(o.n_stacks, 256, false) <= 65536 ? 256
+                      : gapped_lds_bytes(o.n_stacks, 128, false) <= 65536 ? 128 : 64;
+    const size_t lds = gapped_lds_bytes(o.n_stacks, block, false);
+    const int per_cu = std::max<int>(
+        1, std::min<int>(c->gap_blocks_per_cu * 256 / block, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
+    const int blocks = c->n_cus * per_cu;
+    const uint64_t lanes = (uint64_t)blocks * block;
+    const uint32_t cap1 = c->gap_cap1, cap2 = 65535u - cap1;
+    const uint64_t pool_n = c->gap_pool_n;
+    if (int rc = c->d_wbuf.ensure(chunk * A.wstride * 8)) return rc;
+    if (int rc = c->d_nN.ensure(chunk * 2 + 2)) return rc;
+    if (int rc = c->d_ent.ensure(lanes * cap1 * 16)) return rc;
+    if (int rc = c->d_pool.ensure(pool_n * cap2 * 16)) return rc;
+    if (int rc = c->d_aln.ensure(std::max<int64_t>(n, 1) * (uint64_t)A.aln_cap * 16)) return rc;
+    if (int rc = c->d_naln.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
+    if (int rc = c->d_status.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
+    if (int rc = c->d_counter.ensure(64)) return rc;
+    for (int64_t b0 = 0; b0 < n; b0 += chunk) {
+      const int64_t cnt = std::min(chunk, n - b0);
+      AlnArgs B = A;
+      B.n = cnt;
+      B.off = A.off + b0;
+      B.len = A.len + b0;
+      B.wbuf = c->d_wbuf.as<uint2>();
+      B.nN = c->d_nN.as<uint16_t>();
+      GapArgs G = gap_args(c, A, o, b0, cnt);
+      G.wbuf = B.wbuf;
+      G.nN = B.nN;
+      G.ent = c->d_ent.as<uint4>();
+      G.cap1 = cap1;
+      G.pool = c->d_pool.as<uint4>();
+      G.cap2 = cap2;
+      G.pool_n = pool_n;
+      G.aln = c->d_aln.as<uint4>() + b0 * A.aln_cap;
+      G.n_aln = c->d_naln.as<int32_t>() + b0;
+      G.aln_cap = A.aln_cap;
+      G.status = c->d_status.as<uint32_t>() + b0;
+      HIPCHK(hipEventRecord(c->ev[0], c->stream));
+      HIPCHK(launch_width(B, c->block, c->stream));
+      HIPCHK(hipEventRecord(c->ev[1], c->stream));
+      HIPCHK(launch_gapped(G, c->d_counter.as<unsigned long long>(), blocks, block, false, c->stream));
+      HIPCHK(hipEventRecord(c->ev[2], c->stream));
+      HIPCHK(hipEventSynchronize(c->ev[2]));
+      float a = 0, b = 0;
+      HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+      HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+      ms_w += a;
+      ms_s += b;
+      c->stats.n_launch_width++;
+      c->stats.n_launch_search++;
+    }
+  }
   // first pass, in chunks of lanes_per_chunk reads
   const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), c->lanes_per_chunk);
   A.cap = c->stack_cap;
-  A.aln_cap = c->aln_cap;
+  if (!v2) A.aln_cap = c->aln_cap;
+  if (!v2) {
   if (int rc = c->d_wbuf.ensure(chunk * A.wstride * 8)) return rc;
   if (int rc = c->d_heads.ensure(chunk * (uint64_t)o.n_stacks * 4)) return rc;
   if (int rc = c->d_ent.ensure(chunk * (uint64_t)A.cap * 16)) return rc;
@@ -527,7 +630,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   A.heads = c->d_heads.as<uint32_t>();
   A.ent = c->d_ent.as<uint4>();
   A.prev = c->d_prev.as<uint32_t>();
-  float ms_w = 0, ms_s = 0;
   for (int64_t b0 = 0; b0 < n; b0 += chunk) {
     int64_t lanes = std::min(chunk, n - b0);
     // lane-indexed inputs and outputs: shift the base pointers to this chunk
@@ -541,6 +643,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->stats.n_launch_width++;
     c->stats.n_launch_search++;
   }
+  }  // !v2
   c->stats.ms_width = ms_w;
   c->stats.ms_search = ms_s;
   c->aln_cap_used = A.aln_cap;
@@ -559,6 +662,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   for (int64_t i = 0; i < n; ++i) {
     if (c->h_status[i] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "read %lld: score outside the stack range", (long long)i);
     if (c->h_status[i]) c->retry_ids.push_back(i);
+    c->stats.n_stack_overflow += (c->h_status[i] & ST_STACK_OVERFLOW) != 0;
+    c->stats.n_aln_overflow += (c->h_status[i] & ST_ALN_OVERFLOW) != 0;
   }
   // retry pass: larger stacks / hit arrays for the few reads that overflowed
   std::vector<int64_t> todo = c->retry_ids;
@@ -568,9 +673,13 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   std::vector<int64_t> where(todo.size());
   for (size_t j = 0; j < todo.size(); ++j) where[j] = (int64_t)j;
   float ms_r = 0;
+  // first retry round: the persistent gapped kernel with 24-bit slot links and one
+  // large stack region per read (reads < 4096 bp); later rounds: the general kernels
+  bool wide_round = v2 && max_len < 4096;
   while (!todo.empty()) {
     // live entries never exceed max_entries + 9 (one expansion after the last check)
-    const uint64_t need_cap = std::min<uint64_t>(cap, (uint64_t)opt->max_entries + 16);
+    const uint64_t need_cap = wide_round ? std::min<uint64_t>((uint64_t)opt->max_entries + 64, 1u << 20)
+                                         : std::min<uint64_t>(cap, (uint64_t)opt->max_entries + 16);
     // keep each retry chunk within ~16 GiB of stack scratch
     int64_t per = std::max<int64_t>(1, (int64_t)((16ull << 30) / (need_cap * 20 + acap * 16 + A.wstride * 8 + 64)));
     std::vector<int64_t> next;
@@ -582,9 +691,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       B.aln_cap = acap;
       if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
       if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
-      if (int rc = c->d_heads.ensure(lanes * (uint64_t)o.n_stacks * 4)) return rc;
-      if (int rc = c->d_ent.ensure(lanes * need_cap * 16)) return rc;
-      if (int rc = c->d_prev.ensure(lanes * need_cap * 4)) return rc;
+      if (int rc = c->d_ent.ensure((lanes + 63) / 64 * 64 * need_cap * 16)) return rc;
+      if (!wide_round) {
+        if (int rc = c->d_heads.ensure(lanes * (uint64_t)o.n_stacks * 4)) return rc;
+        if (int rc = c->d_prev.ensure(lanes * need_cap * 4)) return rc;
+      }
       if (int rc = c->r_aln.ensure(lanes * (uint64_t)acap * 16)) return rc;
       if (int rc = c->r_naln.ensure(lanes * 4)) return rc;
       if (int rc = c->r_status.ensure(lanes * 4)) return rc;
@@ -597,7 +708,34 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       B.n_aln = c->r_naln.as<int32_t>();
       B.status = c->r_status.as<uint32_t>();
       float a = 0, b = 0;
-      if (int rc = run_pass(c, B, 0, lanes, c->d_ids.as<int64_t>(), &a, &b)) return rc;
+      if (wide_round) {
+        if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
+        if (int rc = c->d_counter.ensure(64)) return rc;
+        B.ids = c->d_ids.as<int64_t>();
+        B.n = lanes;
+        B.nN = c->d_nN.as<uint16_t>();
+        GapArgs G = gap_args(c, A, o, 0, lanes);
+        G.ids = B.ids;
+        G.ent = B.ent;
+        G.cap1 = (uint32_t)need_cap;
+        G.pool = nullptr;
+        G.cap2 = 0;
+        G.pool_n = 0;
+        G.aln = B.aln;
+        G.n_aln = B.n_aln;
+        G.aln_cap = acap;
+        G.status = B.status;
+        const int blk = 64;
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        HIPCHK(launch_width(B, c->block, c->stream));
+        HIPCHK(launch_gapped(G, c->d_counter.as<unsigned long long>(), (int)((lanes + blk - 1) / blk), blk, true,
+                             c->stream));
+        HIPCHK(hipEventRecord(c->ev[4], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[4]));
+        HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
+      } else {
+        if (int rc = run_pass(c, B, 0, lanes, c->d_ids.as<int64_t>(), &a, &b)) return rc;
+      }
       ms_r += a + b;
       std::vector<int32_t> rn(lanes);
       std::vector<uint32_t> rs(lanes);
@@ -616,6 +754,12 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         }
         found[slot].assign(ra.begin() + j * acap, ra.begin() + j * acap + rn[j]);
       }
+    }
+    if (wide_round) {
+      wide_round = false;  // what still overflows goes to the general kernels at the same capacities
+      todo.swap(next);
+      where.swap(next_where);
+      continue;
     }
     if (!next.empty()) {
       if (cap >= (uint64_t)opt->max_entries + 16 && acap >= (1u << 20))

@@ -113,8 +113,11 @@ typedef struct {
 	double ms_total;       /* ibwa_batch_run wall, device-synchronised */
 	int64_t n_retry;       /* reads re-run in the large-capacity pass */
 	int64_t n_launch_width, n_launch_search;
-	int path;              /* 0: width + gapped search; 1: exact-match path (max_diff == 0) */
+	int path;              /* 0: width + general search; 1: exact-match path (max_diff == 0);
+	                          2: width + persistent gapped search */
 	int kmer_k;            /* K of the K-mer interval table the exact path used (0: none) */
+	int64_t n_stack_overflow;  /* first-pass reads whose stack did not fit (re-run) */
+	int64_t n_aln_overflow;    /* first-pass reads whose hits did not fit (re-run) */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 

@@ -77,6 +77,7 @@ def lib():
                                         c.c_void_p, c.POINTER(GapOpt), c.c_int, c.c_void_p,
                                         c.POINTER(c.c_void_p), c.c_void_p]
         L.or_free.argtypes = [c.c_void_p]
+        L.or_set_stats.argtypes = [c.c_void_p]
         L.or_exact_touches.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p, c.c_void_p,
                                        c.c_int, c.c_int, c.c_void_p]
         if hasattr(L, "or_aln_local_core"):
@@ -227,10 +228,18 @@ def encode_reads(recs, mode, trim_qual):
     return seqs, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
 
 
-def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False):
-    """Run the restated bwa_cal_sa_reg_gap.  Returns (n_aln int32[n], alns ALN_DTYPE[...], touches)."""
+STATS_DTYPE = np.dtype([("pushes", "<u4"), ("pops", "<u4"), ("peak_entries", "<u4"), ("peak_bucket", "<u4"),
+                        ("n_aln", "<u4"), ("touches", "<u4")])
+
+
+def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False, stats=None):
+    """Run the restated bwa_cal_sa_reg_gap.  Returns (n_aln int32[n], alns ALN_DTYPE[...], touches).
+    `stats`: optional STATS_DTYPE[n] array filled with per-read search statistics."""
     L = lib()
     n = len(lens)
+    if stats is not None:
+        assert stats.dtype == STATS_DTYPE and stats.size >= n and stats.flags.c_contiguous
+        L.or_set_stats(ctypes.c_void_p(stats.ctypes.data))
     seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)

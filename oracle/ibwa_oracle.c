@@ -277,7 +277,12 @@ typedef struct {
 } entry_t;
 
 typedef struct { int n, m; entry_t *e; } bucket_t;
-typedef struct { int n_stacks, best, n_entries; bucket_t *b; } gstack_t;
+typedef struct { int n_stacks, best, n_entries; bucket_t *b; uint32_t pushes, pops, peak, peak_bucket; } gstack_t;
+
+/* per-read search statistics (test/bench instrumentation only) */
+typedef struct { uint32_t pushes, pops, peak_entries, peak_bucket, n_aln, touches; } or_stats_t;
+static or_stats_t *g_stats_next; /* consumed by the next or_cal_sa_reg_gap call */
+void or_set_stats(or_stats_t *buf) { g_stats_next = buf; }
 
 #define SCORE(m, o, e, p) ((m) * (p)->s_mm + (o) * (p)->s_gapo + (e) * (p)->s_gape)
 #define ST_M 0
@@ -307,6 +312,7 @@ static void gs_reset(gstack_t *s)
 	for (i = 0; i < s->n_stacks; ++i) s->b[i].n = 0;
 	s->best = s->n_stacks;
 	s->n_entries = 0;
+	s->pushes = s->pops = s->peak = s->peak_bucket = 0;
 }
 
 /* bwtgap.c:45-64.  last_diff_pos: a non-diff push keeps the value already in
@@ -329,11 +335,15 @@ static void gs_push(gstack_t *s, int a, int i, uint32_t k, uint32_t l, int n_mm,
 	++q->n;
 	++s->n_entries;
 	if (s->best > score) s->best = score;
+	++s->pushes;
+	if ((uint32_t)s->n_entries > s->peak) s->peak = s->n_entries;
+	if ((uint32_t)q->n > s->peak_bucket) s->peak_bucket = q->n;
 }
 
 static void gs_pop(gstack_t *s, entry_t *e)
 {
 	bucket_t *q = s->b + s->best;
+	++s->pops;
 	*e = q->e[q->n - 1];
 	--q->n;
 	--s->n_entries;
@@ -553,6 +563,7 @@ typedef struct {
 	int32_t *n_aln;
 	or_aln1_t **per_read;
 	uint32_t *touches;
+	or_stats_t *stats;
 	int64_t next;  /* dynamic claim of THREAD_BLOCK reads (bwtaln.c:100-113) */
 	pthread_mutex_t lock;
 } batch_t;
@@ -596,8 +607,14 @@ static void *worker(void *data)
 				cal_width(B->bwt[0], opt->seed_len, seq[0] + (L - opt->seed_len), sw[0], &t);
 				cal_width(B->bwt[1], opt->seed_len, seq[1] + (L - opt->seed_len), sw[1], &t);
 			}
+			stack->pushes = stack->pops = stack->peak = stack->peak_bucket = 0;
 			match_gap(B->bwt, L, seq, w, L <= opt->seed_len ? 0 : sw, &local, &out, stack, &t);
 			B->n_aln[r] = out.n;
+			if (B->stats) {
+				or_stats_t *st = B->stats + r;
+				st->pushes = stack->pushes; st->pops = stack->pops; st->peak_entries = stack->peak;
+				st->peak_bucket = stack->peak_bucket; st->n_aln = out.n; st->touches = t;
+			}
 			if (out.n) {
 				B->per_read[r] = (or_aln1_t*)malloc(out.n * sizeof(or_aln1_t));
 				memcpy(B->per_read[r], out.a, out.n * sizeof(or_aln1_t));
@@ -624,6 +641,8 @@ int64_t or_cal_sa_reg_gap(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_
 	B.bwt[0] = bwt0; B.bwt[1] = bwt1;
 	B.n_seqs = n_seqs; B.seq = seq; B.off = off; B.len = len; B.opt = opt;
 	B.n_aln = n_aln; B.touches = touches_out;
+	B.stats = g_stats_next;
+	g_stats_next = 0;
 	B.per_read = (or_aln1_t**)calloc(n_seqs > 0 ? n_seqs : 1, sizeof(or_aln1_t*));
 	pthread_mutex_init(&B.lock, 0);
 	for (i = 0; i < n_seqs; ++i) if ((int)len[i] > B.max_len) B.max_len = (int)len[i];

@@ -29,10 +29,12 @@ def test_occ4_kats_gpu(golden_dir, gpu_engine):
         assert (got == np.array([r[1:] for r in rows], dtype=np.uint32)).all(), which
 
 
-@pytest.mark.parametrize("exact_path", [1, 0])
-def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path):
-    """exact_path=0 forces -n 0 through the general width + search kernels too."""
+@pytest.mark.parametrize("exact_path,gapped_v2", [(1, 1), (0, 1), (1, 0), (0, 0)])
+def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path, gapped_v2):
+    """exact_path=0 forces -n 0 through the gapped search too; gapped_v2=0 selects the
+    general (retry-pass) kernels for every gapped option set."""
     gpu_engine.set_option("exact_path", exact_path)
+    gpu_engine.set_option("gapped_v2", gapped_v2)
     bad = []
     for key, m in sorted(sai_manifest.items()):
         opt, _ = oracle.parse_aln_args(m["argv"])
@@ -44,16 +46,24 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path):
         if not oracle.sai_body_equal(got, exp):
             bad.append(key)
         if m["argv"] == ["-n", "0"]:
-            assert gpu_engine.stats().path == exact_path, key
+            assert gpu_engine.stats().path == (1 if exact_path else 2 if gapped_v2 else 0), key
+        elif gapped_v2 and gpu_engine.stats().path != 2:
+            bad.append(key + ":path")
     gpu_engine.set_option("exact_path", 1)
+    gpu_engine.set_option("gapped_v2", 1)
     assert not bad, bad
 
 
-@pytest.mark.parametrize("stack_cap,aln_cap", [(16, 1), (64, 2)])
-def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap, aln_cap):
-    """Tiny per-lane capacities force most reads through the large-capacity retry pass."""
+@pytest.mark.parametrize("stack_cap,aln_cap,v2", [(16, 1, 0), (64, 2, 0), (16, 1, 1), (64, 2, 1)])
+def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap, aln_cap, v2):
+    """Tiny per-lane capacities force most reads through the large-capacity retry pass
+    (v2: tiny primary regions, an extension pool of 4 regions, tiny hit arrays)."""
     try:
         gpu_engine.set_tuning(stack_cap=stack_cap, aln_cap=aln_cap)
+        gpu_engine.set_option("gapped_v2", v2)
+        gpu_engine.set_option("gap_cap1", stack_cap)
+        gpu_engine.set_option("gap_pool_n", 4)
+        gpu_engine.set_option("gap_aln_cap", aln_cap)
         for key in ["r150.default", "mixed.N", "r100.default"]:
             m = sai_manifest[key]
             opt, _ = oracle.parse_aln_args(m["argv"])
@@ -65,6 +75,8 @@ def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap
             assert oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp), key
     finally:
         gpu_engine.set_tuning(stack_cap=4096, aln_cap=8)
+        for k, v in [("gapped_v2", 1), ("gap_cap1", 8192), ("gap_pool_n", 8192), ("gap_aln_cap", 64)]:
+            gpu_engine.set_option(k, v)
 
 
 def test_empty_batch(gpu_engine):

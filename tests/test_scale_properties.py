@@ -76,13 +76,25 @@ def test_exact_reads_round_trip(mid_genome):
     assert ok[~has_n].all()
 
 
-@pytest.mark.parametrize("argv,ln,sub,n", [([], 100, 0.01, 30_000), (["-n", "0"], 100, 0.01, 100_000),
-                                           ([], 150, 0.02, 8_000), (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000)])
-def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n):
+@pytest.mark.parametrize("argv,ln,sub,n,tune", [
+    ([], 100, 0.01, 30_000, {}), (["-n", "0"], 100, 0.01, 100_000, {}),
+    ([], 150, 0.02, 8_000, {}), (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {}),
+    # small primary stack regions: many reads spill into the extension pool, some overflow it
+    ([], 100, 0.02, 20_000, {"gap_cap1": 256, "gap_pool_n": 64}),
+    (["-n", "0"], 100, 0.01, 20_000, {"exact_path": 0}),
+    ([], 100, 0.01, 4_000, {"gapped_v2": 0})])
+def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
     o, e = eopt(argv)
-    n_aln, alns = eng.aln(seq, off, lns, e)
+    defaults = {"gap_cap1": 8192, "gap_pool_n": 8192, "exact_path": 1, "gapped_v2": 1}
+    try:
+        for k, v in tune.items():
+            eng.set_option(k, v)
+        n_aln, alns = eng.aln(seq, off, lns, e)
+    finally:
+        for k in tune:
+            eng.set_option(k, defaults[k])
     rn, ra, _ = oracle.cal_sa_reg_gap(b0, b1, seq, off, lns, o, n_threads=8)
     assert (n_aln == rn).all()
     assert alns.tobytes() == ra.tobytes()
