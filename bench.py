@@ -115,6 +115,7 @@ def main():
     ap.add_argument("--kmer-k", type=int, default=-1, help="K-mer table length for the exact path (-1 auto, 0 off)")
     ap.add_argument("--exact-path", type=int, default=1, help="use the exact-match kernel when max_diff == 0")
     ap.add_argument("--sweep-k", default="", help="comma list of K values to time after the main run")
+    ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -160,11 +161,22 @@ def main():
     for f, _ in E.GapOpt._fields_:
         setattr(opt, f, getattr(ropt, f))
 
+    for kv in args.opt:
+        k_, v_ = kv.split("=")
+        eng.set_option(k_, int(v_))
     eng.set_option("kmer_k", args.kmer_k)
     eng.set_option("exact_path", args.exact_path)
     eng.stage(seq, off, lns)
-    for _ in range(args.warmup):
+
+    def progress(tag):
+        st_ = eng.stats()
+        log(f"{tag}: total {st_.ms_total:.1f} ms (width {st_.ms_width:.1f}, search {st_.ms_search:.1f}, "
+            f"retry {st_.ms_retry:.1f} ms for {st_.n_retry} reads: {st_.n_stack_overflow} stack, "
+            f"{st_.n_aln_overflow} hit overflows)")
+
+    for w in range(args.warmup):
         eng.run(opt)
+        progress(f"warmup {w}")
     # timed region: inputs resident in HBM, results left in HBM
     ms_w = ms_s = ms_r = 0.0
     if dist is not None:
@@ -173,8 +185,9 @@ def main():
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipDeviceSynchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k_ in range(args.steps):
         eng.run(opt)
+        progress(f"step {k_}")
         st = eng.stats()
         ms_w += st.ms_width
         ms_s += st.ms_search

@@ -10,6 +10,7 @@ constexpr uint32_t NIL = 0xFFFFFFFFu;
 constexpr uint32_t ST_STACK_OVERFLOW = 1u;  // per-lane stack capacity exceeded -> retry pass
 constexpr uint32_t ST_ALN_OVERFLOW = 2u;    // per-read hit slots exceeded      -> retry pass
 constexpr uint32_t ST_BAD_SCORE = 4u;       // score outside [0, n_stacks): invalid options
+constexpr uint32_t ST_HEAVY = 8u;           // iteration budget of the first pass exceeded -> retry pass
 
 // Batch-level `local_opt` of bwa_cal_sa_reg_gap (bwtaln.c:86-93) as the kernels see it.
 struct AlnOpt {
@@ -54,24 +55,34 @@ struct GapArgs {
   const uint32_t *len;
   const int64_t *ids;        // read r of this launch -> input read (nullptr: identity)
   int64_t n;
+  int out_by_id;             // outputs indexed by ids[r] (else by r)
   const int16_t *maxdiff_tab;
   uint2 *wbuf;               // widths of read r at wbuf + r * wstride (k_width)
   uint64_t wstride;
   uint32_t wlen1;
   const uint16_t *nN;        // per read N count (k_width)
-  uint4 *ent;                // per-lane primary stack regions, cap1 slots each
+  uint4 *ent;                // per-lane static slot regions, cap1 slots each
   uint32_t cap1;
-  uint4 *pool;               // extension regions, cap2 slots each
-  uint32_t cap2;
-  unsigned long long *pool_next;
-  unsigned long long pool_n;
-  uint4 *aln;                // hits of read r at aln + r * aln_cap
+  uint32_t hit_slots;        // the last hit_slots static slots hold the read's hits
+  uint4 *pool;               // per-workgroup page pools: pages_per_block pages of 2^page_log2 slots
+  uint32_t page_log2;
+  int max_pages;             // pages a lane may hold
+  int pages_per_block;
+  uint4 *aln;                // hit stream (bwt_aln1_t as uint4), aln_total slots
+  unsigned long long aln_total;
+  unsigned long long *aln_next;  // stream fill counter (zeroed once per batch)
+  uint64_t *aln_off;         // per read: first hit in the stream
   int32_t *n_aln;
-  uint32_t aln_cap;
   uint32_t *status;
+  uint32_t *iters;           // optional: loop iterations per read (diagnostics)
+  unsigned long long *prof;  // optional: per-phase cycle counters [8] (diagnostics kernel)
+  uint32_t max_iters;        // iteration budget per read (0: none); over it -> ST_HEAVY
+  int lanes_per_wave;        // reads a wave runs at once (64; 1 for heavy reads)
+  int free_depth;            // LDS free-slot stack per read (wide kernel)
   AlnOpt o;
 };
-size_t gapped_lds_bytes(int n_stacks, int block, bool wide);
+size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int pages_per_block, int lanes_per_wave,
+                        int free_depth);
 // wide: 24-bit slot links (reads < 4096 bp), for the large-capacity retry pass
 hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int blocks, int block, bool wide,
                          hipStream_t st);

@@ -103,11 +103,18 @@ struct ibwa_ctx {
   // persistent gapped search (gapped.hip)
   int gapped_v2 = 1;
   int gap_blocks_per_cu = 3;         // 134 VGPRs -> 3 waves per SIMD
-  uint32_t gap_cap1 = 8192;          // per-lane primary stack slots
-  uint64_t gap_pool_n = 8192;        // extension regions of 65535 - gap_cap1 slots
-  uint32_t gap_aln_cap = 64;         // hit slots per read
+  uint32_t gap_cap1 = 8192;          // per-lane static slots (stack + hit area)
+  int gap_pages_per_block = 384;      // 128 KiB pages per 256-lane workgroup pool
+  uint32_t gap_hit_slots = 256;      // hits a read may hold in the first pass
   int64_t gap_reads_per_chunk = 1 << 22;
-  DBuf d_nN, d_pool;
+  uint32_t gap_iter_budget = 0;      // first-pass iterations per read before handing it to the retry pass
+  DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
+  bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
+  bool verbose = getenv("IBWA_VERBOSE") != nullptr;
+  bool prof_phases = getenv("IBWA_PROF_PHASES") != nullptr;  // diagnostics kernel variant
+  DBuf d_prof;
+  unsigned long long stream_len = 0;
+  std::vector<uint64_t> h_aoff;
   bool naln_on_host = true;  // h_naln mirrors d_naln
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
@@ -173,7 +180,8 @@ GapArgs gap_args(const ibwa_ctx *c, const AlnArgs &A, const AlnOpt &o, int64_t b
   G.wstride = A.wstride;
   G.wlen1 = A.wlen1;
   G.nN = c->d_nN.as<uint16_t>();
-  G.pool_next = c->d_counter.as<unsigned long long>() + 1;
+  G.aln_next = c->d_counter.as<unsigned long long>() + 1;
+  G.lanes_per_wave = 64;
   G.o = o;
   return G;
 }
@@ -236,7 +244,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
-                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool})
+                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof})
     b->release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(c->stream);
@@ -251,10 +259,11 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "lanes_per_chunk" && value > 0) c->lanes_per_chunk = value;
   else if (k == "gapped_v2") c->gapped_v2 = value != 0;
   else if (k == "gap_blocks_per_cu" && value > 0 && value <= 8) c->gap_blocks_per_cu = (int)value;
-  else if (k == "gap_cap1" && value >= 2 && value < 65535) c->gap_cap1 = (uint32_t)value;
-  else if (k == "gap_pool_n" && value >= 0) c->gap_pool_n = (uint64_t)value;
-  else if (k == "gap_aln_cap" && value > 0 && value <= 4096) c->gap_aln_cap = (uint32_t)value;
+  else if (k == "gap_cap1" && value >= 16 && value <= 65536) c->gap_cap1 = (uint32_t)value;
+  else if (k == "gap_pages_per_block" && value >= 1 && value <= 65536) c->gap_pages_per_block = (int)value;
+  else if (k == "gap_hit_slots" && value >= 1 && value <= 4096) c->gap_hit_slots = (uint32_t)value;
   else if (k == "gap_reads_per_chunk" && value > 0) c->gap_reads_per_chunk = value;
+  else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
   else return fail(IBWA_EINVAL, "unknown option %s", k.c_str());
   return 0;
 }
@@ -518,6 +527,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   const bool exact_path = c->exact_path && !o.fnr_pos && opt->max_diff == 0 && opt->max_entries >= 2;
   c->stats.path = exact_path ? 1 : 0;
   if (exact_path) {
+    c->stream_out = false;
     A.aln_cap = c->aln_cap;
     A.n = n;
     if (int rc = c->d_aln.ensure(std::max<int64_t>(n, 1) * (uint64_t)A.aln_cap * 16)) return rc;
@@ -554,31 +564,36 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
 
   // persistent gapped search (gapped.hip) when the options fit its entry bit fields
   const bool v2 = c->gapped_v2 && batch_md + 1 <= 31 && o.max_gapo <= 7 && o.max_gape <= 15 &&
-                  gapped_lds_bytes(o.n_stacks, 64, true) <= 65536 && max_len <= 65535;
+                  gapped_lds_bytes(o.n_stacks, 64, true, 0, 0, 1, 4096) <= 65536 && max_len <= 65535;
   float ms_w = 0, ms_s = 0;
+  c->stream_out = v2;
   if (v2) {
     if (int rc = ensure_kmer(c)) return rc;
     c->stats.path = 2;
     const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), c->gap_reads_per_chunk);
-    A.aln_cap = c->gap_aln_cap;
-    // LDS bucket heads: n_stacks u16 per lane, at most 64 KiB per workgroup
-    const int block = gapped_lds_bytes(o.n_stacks, 256, false) <= 65536 ? 256
-                      : gapped_lds_bytes(o.n_stacks, 128, false) <= 65536 ? 128 : 64;
-    const size_t lds = gapped_lds_bytes(o.n_stacks, block, false);
+    // LDS: bucket heads + free slots + page table per lane, the page bitmap per workgroup
+    const uint32_t LG = 13, P0 = c->gap_cap1;
+    const int max_pages = (int)std::min<uint32_t>(7, (65536u - P0) >> LG);
+    auto ppb_of = [&](int blk) { return std::max(1, c->gap_pages_per_block * blk / 256); };
+    auto lds_of = [&](int blk) { return gapped_lds_bytes(o.n_stacks, blk, false, max_pages, ppb_of(blk), 64, 0); };
+    const int block = lds_of(256) <= 65536 ? 256 : lds_of(128) <= 65536 ? 128 : 64;
+    const int ppb = ppb_of(block);
+    const size_t lds = lds_of(block);
     const int per_cu = std::max<int>(
         1, std::min<int>(c->gap_blocks_per_cu * 256 / block, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
     const int blocks = c->n_cus * per_cu;
     const uint64_t lanes = (uint64_t)blocks * block;
-    const uint32_t cap1 = c->gap_cap1, cap2 = 65535u - cap1;
-    const uint64_t pool_n = c->gap_pool_n;
+    const uint64_t aln_total = std::max<uint64_t>((uint64_t)n * 4, 1u << 20);
     if (int rc = c->d_wbuf.ensure(chunk * A.wstride * 8)) return rc;
     if (int rc = c->d_nN.ensure(chunk * 2 + 2)) return rc;
-    if (int rc = c->d_ent.ensure(lanes * cap1 * 16)) return rc;
-    if (int rc = c->d_pool.ensure(pool_n * cap2 * 16)) return rc;
-    if (int rc = c->d_aln.ensure(std::max<int64_t>(n, 1) * (uint64_t)A.aln_cap * 16)) return rc;
+    if (int rc = c->d_ent.ensure(lanes * P0 * 16)) return rc;
+    if (int rc = c->d_pool.ensure((uint64_t)blocks * ppb * (16ull << LG))) return rc;
+    if (int rc = c->d_aln.ensure(aln_total * 16)) return rc;
+    if (int rc = c->d_aoff.ensure(std::max<int64_t>(n, 1) * 8)) return rc;
     if (int rc = c->d_naln.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
     if (int rc = c->d_status.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
     if (int rc = c->d_counter.ensure(64)) return rc;
+    HIPCHK(hipMemsetAsync(c->d_counter.as<unsigned long long>() + 1, 0, 8, c->stream));
     for (int64_t b0 = 0; b0 < n; b0 += chunk) {
       const int64_t cnt = std::min(chunk, n - b0);
       AlnArgs B = A;
@@ -588,17 +603,28 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       B.wbuf = c->d_wbuf.as<uint2>();
       B.nN = c->d_nN.as<uint16_t>();
       GapArgs G = gap_args(c, A, o, b0, cnt);
-      G.wbuf = B.wbuf;
-      G.nN = B.nN;
       G.ent = c->d_ent.as<uint4>();
-      G.cap1 = cap1;
+      G.cap1 = P0;
+      G.hit_slots = std::min<uint32_t>(c->gap_hit_slots, P0 / 2);
       G.pool = c->d_pool.as<uint4>();
-      G.cap2 = cap2;
-      G.pool_n = pool_n;
-      G.aln = c->d_aln.as<uint4>() + b0 * A.aln_cap;
+      G.page_log2 = LG;
+      G.max_pages = max_pages;
+      G.pages_per_block = ppb;
+      G.aln = c->d_aln.as<uint4>();
+      G.aln_total = aln_total;
+      G.aln_off = c->d_aoff.as<uint64_t>() + b0;
       G.n_aln = c->d_naln.as<int32_t>() + b0;
-      G.aln_cap = A.aln_cap;
       G.status = c->d_status.as<uint32_t>() + b0;
+      G.max_iters = c->gap_iter_budget;
+      if (c->verbose) {
+        if (int rc = c->d_iters.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
+        G.iters = c->d_iters.as<uint32_t>() + b0;
+      }
+      if (c->prof_phases) {
+        if (int rc = c->d_prof.ensure(64)) return rc;
+        HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 64, c->stream));
+        G.prof = c->d_prof.as<unsigned long long>();
+      }
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
       HIPCHK(launch_width(B, c->block, c->stream));
       HIPCHK(hipEventRecord(c->ev[1], c->stream));
@@ -612,6 +638,26 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       ms_s += b;
       c->stats.n_launch_width++;
       c->stats.n_launch_search++;
+      if (c->verbose) {
+        std::vector<uint32_t> it(cnt);
+        HIPCHK(hipMemcpy(it.data(), G.iters, cnt * 4, hipMemcpyDeviceToHost));
+        uint64_t sum = 0;
+        uint32_t mx = 0;
+        for (uint32_t v : it) { sum += v; mx = std::max(mx, v); }
+        std::sort(it.begin(), it.end());
+        fprintf(stderr, "[ibwa_amd] k_gapped: %lld reads, %.3g lane-iterations (%.0f per read, p99 %u, p99.99 %u, "
+                "max %u), %.1f ms -> %.3g lane-iterations/s\n", (long long)cnt, (double)sum, (double)sum / cnt,
+                it[(size_t)(cnt * 0.99)], it[(size_t)(cnt * 0.9999)], mx, b, sum / (b * 1e-3));
+      }
+      if (c->prof_phases) {
+        unsigned long long pf[8];
+        HIPCHK(hipMemcpy(pf, c->d_prof.p, 64, hipMemcpyDeviceToHost));
+        const char *nm[8] = {"claim", "pop", "wait", "rest", " exact", " expand", " hit", " end"};
+        double tot = (double)(pf[0] + pf[1] + pf[2] + pf[3]);
+        fprintf(stderr, "[ibwa_amd] k_gapped phases (wave cycles, %d waves):", blocks * block / 64);
+        for (int q = 0; q < 8; ++q) fprintf(stderr, " %s %.1f%%", nm[q], tot > 0 ? 100.0 * pf[q] / tot : 0.0);
+        fprintf(stderr, "\n");
+      }
     }
   }
   // first pass, in chunks of lanes_per_chunk reads
@@ -651,7 +697,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   // results + overflow detection
   c->h_naln.resize(n);
   c->h_status.resize(n);
+  c->stream_len = 0;
   if (n) {
+    if (v2)
+      HIPCHK(hipMemcpyAsync(&c->stream_len, c->d_counter.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost,
+                            c->stream));
     HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_status.data(), c->d_status.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -664,6 +714,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (c->h_status[i]) c->retry_ids.push_back(i);
     c->stats.n_stack_overflow += (c->h_status[i] & ST_STACK_OVERFLOW) != 0;
     c->stats.n_aln_overflow += (c->h_status[i] & ST_ALN_OVERFLOW) != 0;
+    c->stats.n_heavy += (c->h_status[i] & ST_HEAVY) != 0;
   }
   // retry pass: larger stacks / hit arrays for the few reads that overflowed
   std::vector<int64_t> todo = c->retry_ids;
@@ -673,15 +724,19 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   std::vector<int64_t> where(todo.size());
   for (size_t j = 0; j < todo.size(); ++j) where[j] = (int64_t)j;
   float ms_r = 0;
-  // first retry round: the persistent gapped kernel with 24-bit slot links and one
-  // large stack region per read (reads < 4096 bp); later rounds: the general kernels
-  bool wide_round = v2 && max_len < 4096;
+  // first two retry rounds: the persistent gapped kernel with 24-bit slot links and one
+  // large static region per read (4 MiB, then 64 MiB; reads < 4096 bp); then the general kernels
+  int wide_rounds = v2 && max_len < 4096 ? 2 : 0;
   while (!todo.empty()) {
+    const bool wide_round = wide_rounds > 0;
+    const uint32_t wide_hits = 4096;
     // live entries never exceed max_entries + 9 (one expansion after the last check)
-    const uint64_t need_cap = wide_round ? std::min<uint64_t>((uint64_t)opt->max_entries + 64, 1u << 20)
-                                         : std::min<uint64_t>(cap, (uint64_t)opt->max_entries + 16);
-    // keep each retry chunk within ~16 GiB of stack scratch
-    int64_t per = std::max<int64_t>(1, (int64_t)((16ull << 30) / (need_cap * 20 + acap * 16 + A.wstride * 8 + 64)));
+    const uint64_t need_cap =
+        wide_round ? std::min<uint64_t>((uint64_t)opt->max_entries + 64 + wide_hits, wide_rounds == 2 ? 1u << 18 : 1u << 22)
+                   : std::min<uint64_t>(cap, (uint64_t)opt->max_entries + 16);
+    // keep each retry chunk within ~16 GiB (general kernels) / 48 GiB (gapped wide) of stack scratch
+    const uint64_t budget = (wide_round ? 48ull : 16ull) << 30;
+    int64_t per = std::max<int64_t>(1, (int64_t)(budget / (need_cap * 20 + acap * 16 + A.wstride * 8 + 64)));
     std::vector<int64_t> next;
     std::vector<int64_t> next_where;
     for (size_t b0 = 0; b0 < todo.size(); b0 += per) {
@@ -691,12 +746,14 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       B.aln_cap = acap;
       if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
       if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
-      if (int rc = c->d_ent.ensure((lanes + 63) / 64 * 64 * need_cap * 16)) return rc;
+      if (int rc = c->d_ent.ensure(lanes * need_cap * 16)) return rc;
       if (!wide_round) {
         if (int rc = c->d_heads.ensure(lanes * (uint64_t)o.n_stacks * 4)) return rc;
         if (int rc = c->d_prev.ensure(lanes * need_cap * 4)) return rc;
       }
-      if (int rc = c->r_aln.ensure(lanes * (uint64_t)acap * 16)) return rc;
+      const uint64_t r_total = wide_round ? (uint64_t)lanes * 64 + 65536 : (uint64_t)lanes * acap;
+      if (int rc = c->r_aln.ensure(r_total * 16)) return rc;
+      if (int rc = c->r_aoff.ensure(lanes * 8)) return rc;
       if (int rc = c->r_naln.ensure(lanes * 4)) return rc;
       if (int rc = c->r_status.ensure(lanes * 4)) return rc;
       HIPCHK(hipMemcpyAsync(c->d_ids.p, todo.data() + b0, lanes * 8, hipMemcpyHostToDevice, c->stream));
@@ -716,33 +773,54 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         B.nN = c->d_nN.as<uint16_t>();
         GapArgs G = gap_args(c, A, o, 0, lanes);
         G.ids = B.ids;
+        G.out_by_id = 0;
         G.ent = B.ent;
         G.cap1 = (uint32_t)need_cap;
+        G.hit_slots = wide_hits;
         G.pool = nullptr;
-        G.cap2 = 0;
-        G.pool_n = 0;
+        G.max_pages = 0;
+        G.pages_per_block = 0;
+        G.page_log2 = 13;
         G.aln = B.aln;
+        G.aln_total = r_total;
+        G.aln_next = c->d_counter.as<unsigned long long>() + 2;
+        G.aln_off = c->r_aoff.as<uint64_t>();
         G.n_aln = B.n_aln;
-        G.aln_cap = acap;
         G.status = B.status;
+        if (c->verbose) {
+          if (int rc = c->d_iters.ensure(lanes * 4)) return rc;
+          G.iters = c->d_iters.as<uint32_t>();
+        }
+        HIPCHK(hipMemsetAsync(G.aln_next, 0, 8, c->stream));
+        // one heavy read per wave: an iteration then costs only that read's path
         const int blk = 64;
+        G.lanes_per_wave = 1;
+        G.free_depth = 4096;  // 16 KiB of LDS per heavy read: freed slots are reused, not leaked
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
         HIPCHK(launch_width(B, c->block, c->stream));
-        HIPCHK(launch_gapped(G, c->d_counter.as<unsigned long long>(), (int)((lanes + blk - 1) / blk), blk, true,
-                             c->stream));
+        HIPCHK(launch_gapped(G, c->d_counter.as<unsigned long long>(), (int)lanes, blk, true, c->stream));
         HIPCHK(hipEventRecord(c->ev[4], c->stream));
         HIPCHK(hipEventSynchronize(c->ev[4]));
         HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
+        if (c->verbose) {
+          std::vector<uint32_t> it(lanes);
+          HIPCHK(hipMemcpy(it.data(), c->d_iters.p, lanes * 4, hipMemcpyDeviceToHost));
+          const uint32_t mx = *std::max_element(it.begin(), it.end());
+          fprintf(stderr, "[ibwa_amd]   wide launch: %lld reads, max %u iterations, %.1f ms (%.2f us/iteration)\n",
+                  (long long)lanes, mx, a, mx ? a * 1e3 / mx : 0.0);
+        }
       } else {
         if (int rc = run_pass(c, B, 0, lanes, c->d_ids.as<int64_t>(), &a, &b)) return rc;
       }
       ms_r += a + b;
       std::vector<int32_t> rn(lanes);
       std::vector<uint32_t> rs(lanes);
-      std::vector<uint4> ra(lanes * (uint64_t)acap);
+      std::vector<uint64_t> ro(lanes);
+      std::vector<uint4> ra(r_total);
       HIPCHK(hipMemcpyAsync(rn.data(), c->r_naln.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipMemcpyAsync(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipMemcpyAsync(ra.data(), c->r_aln.p, lanes * (uint64_t)acap * 16, hipMemcpyDeviceToHost, c->stream));
+      if (wide_round) HIPCHK(hipMemcpyAsync(ro.data(), c->r_aoff.p, lanes * 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(ra.data(), c->r_aln.p, r_total * 16, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       for (int64_t j = 0; j < lanes; ++j) {
         int64_t slot = where[b0 + j];
@@ -752,11 +830,15 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
           next_where.push_back(slot);
           continue;
         }
-        found[slot].assign(ra.begin() + j * acap, ra.begin() + j * acap + rn[j]);
+        const uint64_t first = wide_round ? (rn[j] ? ro[j] : 0) : (uint64_t)j * acap;
+        found[slot].assign(ra.begin() + first, ra.begin() + first + rn[j]);
       }
     }
+    if (c->verbose)
+      fprintf(stderr, "[ibwa_amd] retry round (%s, cap %llu): %zu reads, %zu still overflow, %.1f ms so far\n",
+              wide_round ? "gapped wide" : "general", (unsigned long long)need_cap, todo.size(), next.size(), ms_r);
     if (wide_round) {
-      wide_round = false;  // what still overflows goes to the general kernels at the same capacities
+      --wide_rounds;  // what still overflows goes to a larger round, then to the general kernels
       todo.swap(next);
       where.swap(next_where);
       continue;
@@ -781,7 +863,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
 int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total) {
   const int64_t n = c->n;
   const uint32_t cap = c->aln_cap_used;
-  c->h_aln.resize(std::max<int64_t>(n, 1) * cap);
+  // first-pass hits: per-read slots (n x cap), or the hit stream + per-read offsets
+  const uint64_t n_slots = c->stream_out ? c->stream_len : (uint64_t)n * cap;
+  c->h_aln.resize(std::max<uint64_t>(n_slots, 1));
   if (n) {
     HIPCHK(hipSetDevice(c->device));
     if (!c->naln_on_host) {
@@ -789,7 +873,11 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
       HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
       c->naln_on_host = true;
     }
-    HIPCHK(hipMemcpyAsync(c->h_aln.data(), c->d_aln.p, n * (uint64_t)cap * 16, hipMemcpyDeviceToHost, c->stream));
+    if (c->stream_out) {
+      c->h_aoff.resize(n);
+      HIPCHK(hipMemcpyAsync(c->h_aoff.data(), c->d_aoff.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (n_slots) HIPCHK(hipMemcpyAsync(c->h_aln.data(), c->d_aln.p, n_slots * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }
   // patch in retried reads
@@ -807,7 +895,7 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
       src = c->retry_alns[rj].data();
       ++rj;
     } else {
-      src = c->h_aln.data() + i * cap;
+      src = c->h_aln.data() + (c->stream_out ? (cnt[i] ? c->h_aoff[i] : 0) : i * cap);
     }
     memcpy(o + p, src, (size_t)cnt[i] * 16);
     p += cnt[i];

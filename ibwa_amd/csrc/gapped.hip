@@ -22,12 +22,20 @@
 // Entry (uint4): {k, l, i | last_diff_pos << 16,
 //                 prev(16) | n_mm(5) << 16 | n_gapo(3) << 21 | n_gape(4) << 24 | a << 28 | state << 29}
 // last_diff_pos: a non-diff push inherits the parent's.
-// Stack slots: a per-lane region of CAP1 slots, then one extension region
-// from a per-launch pool; a read that needs more (or options that do not fit
-// the bit fields) is re-run by the general kernels (aln.hip), exactly.
-// Slots are bump-allocated; a popped slot below the bump pointer goes on a
-// small per-lane free stack in LDS and is reused by the next pushes, so the
-// slots in use track the live entries (the reference's stack size).
+// Slot arena of a lane (16 B slots, addressed by a 16-bit (narrow) or 24-bit
+// (wide) slot number): a static region of P0 slots -- its last H slots hold
+// the read's hits, the rest the first stack entries -- followed by up to
+// max_pages pages of PG slots taken, only when the stack grows that far, from
+// its workgroup's page pool (a bitmap in LDS; pages go back when the read
+// ends).  Measured on a GRCh37-sized genome the live entries of a 100 bp read
+// have median 306, p99 14.5k, max 461k (tools/dfs_stats.py), so memory
+// follows the reads actually running instead of the worst case.  Stack slots
+// are bump-allocated; a popped slot below the bump pointer goes on a small
+// per-lane free stack in LDS and is reused by the next pushes, so the slots in
+// use track the live entries (the reference's stack size).  At read end the
+// hits are appended to a compact per-batch stream (one atomic per read).  A
+// read that needs more (or options that do not fit the bit fields) is re-run,
+// exactly, by the retry pass.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -42,8 +50,43 @@ namespace {
 
 constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_NONSTOP = 0x10;
 constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
-constexpr int GAP_CHUNK = 64;
-constexpr int FREE_DEPTH = 8;  // per-lane LDS stack of popped slots awaiting reuse
+// per-lane LDS stack of popped slots awaiting reuse (the retry pass's heavy reads get more)
+constexpr int NARROW_FREE_DEPTH = 8;
+constexpr int MAX_BUCKETS = 128;  // non-empty-bucket bitmask: four 32-bit registers
+
+// Non-empty score buckets as a 128-bit mask in four named registers (no array: scratch).
+struct BMask {
+  uint32_t m0, m1, m2, m3;
+};
+__device__ __forceinline__ void bm_set(BMask &m, int b) {
+  const uint32_t bit = 1u << (b & 31), w = (uint32_t)b >> 5;
+  m.m0 |= w == 0 ? bit : 0u;
+  m.m1 |= w == 1 ? bit : 0u;
+  m.m2 |= w == 2 ? bit : 0u;
+  m.m3 |= w == 3 ? bit : 0u;
+}
+__device__ __forceinline__ void bm_clr(BMask &m, int b) {
+  const uint32_t bit = 1u << (b & 31), w = (uint32_t)b >> 5;
+  m.m0 &= w == 0 ? ~bit : ~0u;
+  m.m1 &= w == 1 ? ~bit : ~0u;
+  m.m2 &= w == 2 ? ~bit : ~0u;
+  m.m3 &= w == 3 ? ~bit : ~0u;
+}
+__device__ __forceinline__ bool bm_has(const BMask &m, int b) {
+  const uint32_t w = (uint32_t)b >> 5;
+  const uint32_t x = w == 0 ? m.m0 : w == 1 ? m.m1 : w == 2 ? m.m2 : m.m3;
+  return (x >> (b & 31)) & 1u;
+}
+// lowest non-empty bucket >= from (MAX_BUCKETS if none)
+__device__ __forceinline__ int bm_next(const BMask &m, int from) {
+  const uint32_t w = (uint32_t)from >> 5, lo = ~0u << (from & 31);
+  const uint32_t x0 = w > 0 ? 0u : m.m0 & lo;
+  const uint32_t x1 = w > 1 ? 0u : (w == 1 ? m.m1 & lo : m.m1);
+  const uint32_t x2 = w > 2 ? 0u : (w == 2 ? m.m2 & lo : m.m2);
+  const uint32_t x3 = w > 3 ? 0u : (w == 3 ? m.m3 & lo : m.m3);
+  return x0 ? __builtin_ctz(x0) : x1 ? 32 + __builtin_ctz(x1) : x2 ? 64 + __builtin_ctz(x2)
+                                 : x3 ? 96 + __builtin_ctz(x3) : MAX_BUCKETS;
+}
 
 // The 64-row bit-plane block (occ64.hip): v[c] = {C[c], 0, P_lo[c], P_hi[c]}.  Four named
 // uint4 members, not an array: an array indexed by a runtime symbol is placed in scratch.
@@ -104,37 +147,77 @@ template <bool WIDE> struct Ent {
 
 }  // namespace
 
-// lane -> LDS heads: heads[b * blockDim + tid] (bank-friendly: lanes of a wave hit consecutive u16)
-template <bool WIDE>
+// LDS layout (per workgroup of NB lanes, lane-minor so a wave's accesses are consecutive):
+//   heads[n_stacks][LN] (H), free[free_depth][LN] (H), ptab[max_pages][LN] (u16), bitmap[ceil(NPB/32)] (u32)
+// with LN = the block's lanes that run reads (block / 64 * lanes_per_wave)
+size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int pages_per_block, int lanes_per_wave,
+                        int free_depth) {
+  const size_t ln = (size_t)block / 64 * lanes_per_wave;
+  const int fd = wide ? free_depth : NARROW_FREE_DEPTH;
+  size_t b = (size_t)(n_stacks + fd) * ln * (wide ? 4 : 2) + (size_t)max_pages * ln * 2;
+  b = (b + 3) & ~(size_t)3;
+  return b + (size_t)((pages_per_block + 31) / 32) * 4;
+}
+
+// PROF: per-wave cycle accounting of the loop's phases into A.prof[] (diagnostics build of
+// the same kernel): 0 claim, 1 pop, 2 wait for the loads, 3 rest, 4 exact step, 5 expansion,
+// 6 hit, 7 end of read.  Phases 4-7 are parts of 3, timed by the first active lane.
+template <bool WIDE, bool PROF>
 __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *counter) {
   using E = Ent<WIDE>;
   using H = typename E::Head;
   constexpr uint32_t NILH = E::NIL;
   extern __shared__ uint4 lds_raw[];
-  H *const lds_heads = reinterpret_cast<H *>(lds_raw);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   const int NB = blockDim.x;
+  // LDS lanes: the lanes that run reads; LDS index (x << nbl) + ltid (powers of two)
+  const int LNB = (NB >> 6) * A.lanes_per_wave;
+  const int nbl = 31 - __builtin_clz(LNB);
+  const int ltid = (tid >> 6) * A.lanes_per_wave + (lane < A.lanes_per_wave ? lane : 0);
   const AlnOpt o = A.o;
+  H *const lds_heads = reinterpret_cast<H *>(lds_raw);
+  H *const free_slots = lds_heads + o.n_stacks * LNB;  // free_slots[j * NB + tid]
+  const uint32_t FREE_DEPTH = WIDE ? (uint32_t)A.free_depth : (uint32_t)NARROW_FREE_DEPTH;
+  uint16_t *const ptab = reinterpret_cast<uint16_t *>(free_slots + FREE_DEPTH * LNB);  // ptab[((q) << nbl) + ltid]
+  uint32_t *const bitmap =
+      reinterpret_cast<uint32_t *>(ptab + ((A.max_pages * LNB + 1) & ~1));  // 4-byte aligned, still LDS
+  const int bm_words = (A.pages_per_block + 31) / 32;
+  for (int w = tid; w < bm_words; w += NB) {
+    const int lo = w * 32, hi = lo + 32 < A.pages_per_block ? lo + 32 : A.pages_per_block;
+    bitmap[w] = hi - lo >= 32 ? 0u : ~((1u << (hi - lo)) - 1u);  // bits past the pool stay taken
+  }
+  __syncthreads();
   const IndexView ixv0 = A.ix[0], ixv1 = A.ix[1];
   const bool comp = o.mode & MODE_COMPREAD;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + tid;
-  uint4 *const ent1 = A.ent + gtid * A.cap1;  // primary slot region
-  uint4 *ent2 = nullptr;                      // extension region (lazy)
+  const uint32_t P0 = A.cap1;                  // static slots per lane
+  const uint32_t HS = A.hit_slots;             // hits live in static slots [P0 - HS, P0)
+  const uint32_t LG = A.page_log2;             // page = 2^LG slots
+  // static region: one per lane that runs reads (lanes_per_wave of each wave)
+  uint4 *const ent1 = A.ent + ((gtid >> 6) * (uint64_t)A.lanes_per_wave + (uint64_t)(lane < A.lanes_per_wave ? lane : 0)) * P0;
+  uint4 *const pool = A.pool + (uint64_t)blockIdx.x * A.pages_per_block * (1ull << LG);
+  // highest stack slot + 1 (slot NILH is the list terminator)
+  const uint32_t slot_end = P0 + ((uint32_t)A.max_pages << LG) < NILH ? P0 + ((uint32_t)A.max_pages << LG) : NILH;
 
   int64_t cur = 0, cend = 0;
   bool more = true;
   // ---- lane state
-  int st = 0;  // 0 idle, 1 search (C valid or empty), 2 exact sub-search
-  int64_t r = 0;
+  int st = 0;  // 0 idle, 1 search (C valid or empty), 2 exact sub-search, 3 ended (retire)
+  uint32_t end_stat = 0;
+  int64_t r = 0, ro = 0;  // read of this launch, its output index
   int len = 0, opt_max_diff = 0, max_diff = 0, best_score = 0, n_aln = 0;
   int best_cnt = 0, n_entries = 0;
-  uint32_t bump = 0, status = 0, n_free = 0;
-  H *const free_slots = lds_heads + o.n_stacks * NB;  // free_slots[j * NB + tid]
+  uint32_t bump = 0, status = 0, n_free = 0, n_pages = 0, n_iter = 0;
+  // freed slots beyond the LDS stack: a list threaded through the slots themselves (x = next);
+  // fl_next is the head's successor once known (loaded with an iteration's other loads)
+  uint32_t fl_head = 0, fl_next = 0;
+  bool fl_known = true;
   bool seeded = false;
   const uint8_t *s = nullptr;
   const uint2 *W0 = nullptr, *W1 = nullptr, *SW0 = nullptr, *SW1 = nullptr;
+  BMask nonempty = {0u, 0u, 0u, 0u};
   uint4 C = make_uint4(0, 0, 0, 0);
   uint32_t C_slot = 0;
   int C_b = 0;
@@ -146,26 +229,71 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   uint4 xe = make_uint4(0, 0, 0, 0);  // the entry that went down the exact path
 
   auto slot_ptr = [&](uint32_t slot) __attribute__((always_inline)) -> uint4 * {
-    return slot < A.cap1 ? ent1 + slot : ent2 + (slot - A.cap1);
+    if (slot < P0) return ent1 + slot;
+    const uint32_t q = (slot - P0) >> LG;
+    return pool + ((uint64_t)ptab[((q) << nbl) + ltid] << LG) + ((slot - P0) & ((1u << LG) - 1u));
+  };
+  // the read is done: hits to the output stream, pages back to the pool
+  uint64_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0, pf7 = 0, t_rest = 0;
+  auto pnow = []() __attribute__((always_inline)) -> uint64_t {
+    uint64_t t = 0;
+    if (PROF) __asm__ volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+  };
+  auto pleader = [&]() __attribute__((always_inline)) -> bool {
+    return PROF && lane == __builtin_ctzll(__builtin_amdgcn_read_exec());
+  };
+  auto end_read = [&](uint32_t stat) __attribute__((always_inline)) {
+    const bool pl_ = pleader();
+    const uint64_t t0_ = pnow();
+    int na = stat ? 0 : n_aln;
+    if (na) {
+      const unsigned long long pos = atomicAdd(A.aln_next, (unsigned long long)na);
+      if (pos + (unsigned long long)na > A.aln_total) {
+        stat |= ST_ALN_OVERFLOW;
+        na = 0;
+      } else {
+        for (int j = 0; j < na; ++j) A.aln[pos + j] = ent1[P0 - 1 - j];
+        A.aln_off[ro] = pos;
+      }
+    }
+    A.n_aln[ro] = na;
+    A.status[ro] = stat;
+    if (A.iters) A.iters[ro] = n_iter;
+    for (uint32_t q = 0; q < n_pages; ++q) {
+      const uint32_t pg = ptab[((q) << nbl) + ltid];
+      atomicAnd(&bitmap[pg >> 5], ~(1u << (pg & 31)));
+    }
+    n_pages = 0;
+    st = 0;
+    if (pl_) pf7 += pnow() - t0_;
   };
 
   for (;;) {
+    uint64_t t_top = pnow();
+    if (PROF && t_rest) pf3 += t_top - t_rest;
+    // ------------------------------------------------ retire reads that ended last iteration
+    if (st == 3) end_read(end_stat);
     // ------------------------------------------------ claim + init new reads
-    unsigned long long need = __ballot(st == 0);
+    // lanes_per_wave < 64 (retry pass): a wave runs that many heavy reads, so each
+    // iteration executes only their paths
+    const int lpw = A.lanes_per_wave;
+    unsigned long long need = __ballot(st == 0 && lane < lpw);
     while (need && more) {
       if (cur >= cend) {
         int64_t base = 0;
-        if (lane == 0) base = (int64_t)atomicAdd(counter, (unsigned long long)GAP_CHUNK);
+        if (lane == 0) base = (int64_t)atomicAdd(counter, (unsigned long long)lpw);
         base = __shfl(base, 0);
         if (base >= A.n) { more = false; break; }
         cur = base;
-        cend = base + GAP_CHUNK < A.n ? base + GAP_CHUNK : A.n;
+        cend = base + lpw < A.n ? base + lpw : A.n;
       }
       const int rank = __popcll(need & lt_mask);
       const int64_t avail = cend - cur;
       if (st == 0 && rank < avail) {
         r = cur + rank;
         const int64_t rr = A.ids ? A.ids[r] : r;
+        ro = A.out_by_id ? rr : r;
         len = (int)A.len[rr];
         s = A.seq + A.off[rr];
         opt_max_diff = o.fnr_pos ? (int)A.maxdiff_tab[len] : o.max_diff;
@@ -181,17 +309,22 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         SW0 = wb + 2 * A.wlen1;
         SW1 = SW0 + (o.seed_len + 1);
         if ((int)A.nN[r] > max_diff) {  // bwtgap.c:116-122
-          A.n_aln[r] = 0;
-          A.status[r] = 0;
+          A.n_aln[ro] = 0;
+          A.status[ro] = 0;
         } else {
-          for (int b = 0; b < o.n_stacks; ++b) lds_heads[b * NB + tid] = (H)NILH;
           // roots (bwtgap.c:126-127): strand 0 then strand 1, both score 0 -> C = strand 1
           ent1[0] = E::make(0u, ixv0.seq_len, len, 0, NILH, 0, 0, 0, 0, STATE_M);
           C = E::make(0u, ixv0.seq_len, len, 0, 0u, 0, 0, 0, 1, STATE_M);
           ent1[1] = C;
-          lds_heads[0 * NB + tid] = 1;
+          lds_heads[ltid] = 1;
+          nonempty.m0 = 1u;
+          nonempty.m1 = nonempty.m2 = nonempty.m3 = 0u;
           bump = 2;
           n_free = 0;
+          fl_head = NILH;
+          fl_known = true;
+          n_pages = 0;
+          n_iter = 0;
           n_entries = 2;
           C_slot = 1;
           C_b = 0;
@@ -202,13 +335,21 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       }
       const int64_t cnt = __popcll(need);
       cur += avail < cnt ? avail : cnt;
-      need = __ballot(st == 0);
+      need = __ballot(st == 0 && lane < lpw);
     }
     if (__ballot(st != 0) == 0ull) break;
+    uint64_t t_pop = pnow();
+    pf0 += t_pop - t_top;
 
+    ++n_iter;
     // ------------------------------------------------ decide this iteration's work
     // search lanes pop C; exact lanes advance one symbol
     bool do_pop = false, finish = false;
+    if (A.max_iters && n_iter > A.max_iters && (st == 1 || st == 2)) {
+      status |= ST_HEAVY;  // a long search: the retry pass re-runs it from the start
+      st = 1;
+      n_entries = 0;
+    }
     uint4 e = make_uint4(0, 0, 0, 0);
     int a = 0, i = 0, ldp = 0, e_mm = 0, e_go = 0, e_ge = 0, state = 0, m = 0, m_seed = 0;
     if (st == 1) {
@@ -241,22 +382,27 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     uint32_t load_slot = 0;
     if (do_pop) {
       const uint32_t prev = E::prev(e);
-      lds_heads[C_b * NB + tid] = (H)prev;
+      lds_heads[((C_b) << nbl) + ltid] = (H)prev;
       --n_entries;
       if (C_slot + 1 == bump) {
         bump = C_slot;
       } else if (n_free < FREE_DEPTH) {
-        free_slots[n_free * NB + tid] = (H)C_slot;
+        free_slots[((n_free) << nbl) + ltid] = (H)C_slot;
         ++n_free;
+      } else {
+        reinterpret_cast<uint32_t *>(slot_ptr(C_slot))[0] = fl_head;
+        fl_next = fl_head;
+        fl_head = C_slot;
+        fl_known = true;
       }
       if (prev != NILH) {
         load_slot = prev;
         C_load = true;
       } else {
-        int b = C_b + 1;
-        while (b < o.n_stacks && lds_heads[b * NB + tid] == NILH) ++b;
+        bm_clr(nonempty, C_b);
+        const int b = bm_next(nonempty, C_b + 1);
         if (b < o.n_stacks) {
-          load_slot = lds_heads[b * NB + tid];
+          load_slot = lds_heads[((b) << nbl) + ltid];
           C_b = b;
           C_load = true;
         } else {
@@ -267,6 +413,8 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       if (C_load) C_slot = load_slot;
     }
 
+    uint64_t t_issue = pnow();
+    pf1 += t_issue - t_pop;
     // ------------------------------------------------ issue every load of this iteration
     const bool srch = do_pop && m >= 0;
     const IndexView ix = a ? ixv0 : ixv1;  // strand a searches bwt[1-a]
@@ -300,36 +448,60 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     // next candidate
     uint4 Cn = make_uint4(0, 0, 0, 0);
     if (do_pop && C_load) Cn = *slot_ptr(load_slot);
+    // successor of the free-list head, if a push took the previous head
+    uint32_t fl_ld = 0;
+    if (!fl_known) fl_ld = reinterpret_cast<const uint32_t *>(slot_ptr(fl_head))[0];
+    if (PROF) {
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      t_rest = pnow();
+      pf2 += t_rest - t_issue;
+    }
 
     // ------------------------------------------------ consume
+    if (!fl_known) {
+      fl_next = fl_ld;
+      fl_known = true;
+    }
     if (do_pop && C_load) {
       C = Cn;
       C_valid = true;
     }
     if (finish) {
-      A.n_aln[r] = n_aln;
-      A.status[r] = status;
-      st = 0;
+      end_stat = status;
+      st = 3;
       continue;
     }
     const uint32_t csym = (st == 2 ? xa : a) == 1 && comp && sym < 4 ? 3u - sym : sym;
+    // this iteration's rank queries, all four symbols: the children intervals (KK[c], LL[c])
+    // of (qk, ql) -- for the exact step, the exact first step and the expansion alike
+    uint4 KK = make_uint4(0, 0, 0, 0), LL = make_uint4(0, 0, 0, 0);
+    if (qrun) {
+      const uint4 cl4 = occ4_of(bl, ql);
+      const uint4 ck4 = qkneg ? make_uint4(0, 0, 0, 0)
+                              : make_uint4(occ_of(qshare ? bl.v0 : bk.v0, qk - 1),
+                                           occ_of(qshare ? bl.v1 : bk.v1, qk - 1),
+                                           occ_of(qshare ? bl.v2 : bk.v2, qk - 1),
+                                           occ_of(qshare ? bl.v3 : bk.v3, qk - 1));
+      KK = make_uint4(ixq.L2[0] + ck4.x + 1, ixq.L2[1] + ck4.y + 1, ixq.L2[2] + ck4.z + 1, ixq.L2[3] + ck4.w + 1);
+      LL = make_uint4(ixq.L2[0] + cl4.x, ixq.L2[1] + cl4.y, ixq.L2[2] + cl4.z, ixq.L2[3] + cl4.w);
+    }
 
     if (st == 2) {
       // one step of bwt_match_exact_alt (bwt.c:240-247)
+      const bool pl_ = pleader();
+      const uint64_t t0_ = pnow();
       bool fail = false;
       if (xj >= 0) {
         if (csym > 3) {
           fail = true;
         } else {
-          const uint32_t ok = qkneg ? 0u : pick4(occ4_of(qshare ? bl : bk, qk - 1), csym);
-          const uint32_t ol = pick4(occ4_of(bl, ql), csym);
-          const uint32_t base = l2of(ixq, csym);
-          xk = base + ok + 1;
-          xl = base + ol;
+          xk = pick4(KK, csym);
+          xl = pick4(LL, csym);
           if (xk > xl) fail = true;
           --xj;
         }
       }
+      if (pl_) pf4 += pnow() - t0_;
       if (fail) {
         st = 1;  // no hit (bwtgap.c:162): back to popping
       } else if (xj < 0) {
@@ -355,11 +527,8 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       // bwt_match_exact_alt over str[0..i-1] (bwtgap.c:160-163): the first step uses this
       // iteration's blocks; the rest run in sub-state 2
       if (csym > 3) continue;
-      const uint32_t ok = qkneg ? 0u : pick4(occ4_of(qshare ? bl : bk, qk - 1), csym);
-      const uint32_t ol = pick4(occ4_of(bl, ql), csym);
-      const uint32_t base = l2of(ix, csym);
-      xk = base + ok + 1;
-      xl = base + ol;
+      xk = pick4(KK, csym);
+      xl = pick4(LL, csym);
       if (xk > xl) continue;
       xj = i - 2;
       xa = a;
@@ -374,14 +543,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     }
     {
       // ---- expansion (bwtgap.c:200-258)
+      const bool pl_ = pleader();
+      const uint64_t t0_ = pnow();
       const int ni = i - 1;
-      // counts as uint4 + select: a dynamically indexed array would live in scratch
-      const uint4 ck4 = qkneg ? make_uint4(0, 0, 0, 0)
-                              : make_uint4(occ_of(qshare ? bl.v0 : bk.v0, qk - 1),
-                                           occ_of(qshare ? bl.v1 : bk.v1, qk - 1),
-                                           occ_of(qshare ? bl.v2 : bk.v2, qk - 1),
-                                           occ_of(qshare ? bl.v3 : bk.v3, qk - 1));
-      const uint4 cl4 = make_uint4(occ_of(bl.v0, ql), occ_of(bl.v1, ql), occ_of(bl.v2, ql), occ_of(bl.v3, ql));
       const uint32_t occ = l - k + 1;
       bool allow_diff = true, allow_M = true;
       if (ni > 0) {
@@ -393,29 +557,97 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           else if ((int)sw_lo.y == m_seed - 1 && (int)sw_hi.y == m_seed - 1 && sw_lo.x == sw_hi.x) allow_M = false;
         }
       }
-      // push: link into bucket `sc`, keep C = head of the lowest non-empty bucket
-      auto push = [&](int pi, uint32_t pk, uint32_t pl, int n_mm, int n_gapo, int n_gape, int pstate,
-                      int pldp) __attribute__((always_inline)) {
-        const int sc = n_mm * o.s_mm + n_gapo * o.s_gapo + n_gape * o.s_gape;
-        if (sc >= o.n_stacks) { status |= ST_BAD_SCORE; return; }
-        if (n_mm > 31 || n_gapo > 7 || n_gape > 15) { status |= ST_STACK_OVERFLOW; return; }
+      // children in the reference's push order (bwtgap.c:216-258), as bits of a mask:
+      //   bit 0 insertion (open or extend), bits 1-4 deletion by A,C,G,T, bits 5-8 the
+      //   mismatch / match children of symbols (str[i] + 1..4) & 3 (bit 8 = str[i] itself)
+      const uint32_t ne4 = (KK.x <= LL.x ? 1u : 0u) | (KK.y <= LL.y ? 2u : 0u) | (KK.z <= LL.z ? 4u : 0u) |
+                           (KK.w <= LL.w ? 8u : 0u);  // non-empty symbol children
+      const int tmp = (o.mode & MODE_LOGGAP) ? int_log2((uint32_t)(e_ge + e_go)) / 2 + 1 : e_go + e_ge;
+      uint32_t vm = 0;
+      if (allow_diff && ni >= o.indel_end_skip + tmp && len - ni >= o.indel_end_skip + tmp) {
+        if (state == STATE_M) {
+          if (e_go < o.max_gapo) vm = 1u | ne4 << 1;
+        } else if (state == STATE_I) {
+          if (e_ge < o.max_gape) vm = 1u;
+        } else if (state == STATE_D) {
+          if (e_ge < o.max_gape && (e_ge + e_go < max_diff || occ < (uint32_t)o.max_del_occ)) vm = ne4 << 1;
+        }
+      }
+      // symbol children: c_j = (csym + j) & 3 for j = 1..4 -> rotate ne4 so bit j-1 = c_j
+      const uint32_t rot = (csym + 1) & 3;
+      const uint32_t ner = ((ne4 >> rot) | (ne4 << (4 - rot))) & 15u;
+      if (allow_diff && allow_M) vm |= ner << 5;
+      else if (csym < 4) vm |= ner & 8u ? 1u << 8 : 0u;  // the match child only
+      // slots for all pushes of this expansion; one new page at most (popcount <= 9)
+      if (vm) {
+        const uint32_t npush = (uint32_t)__builtin_popcount(vm);
+        const uint32_t reuse = n_free + (fl_head != NILH ? 1u : 0u);  // fl_known holds here
+        const uint32_t nb = npush > reuse ? npush - reuse : 0u;
+        uint32_t b_end = bump + nb;
+        if (bump <= P0 - HS && b_end > P0 - HS) b_end += HS;  // bump skips the hit area
+        if (b_end > slot_end) {
+          status |= ST_STACK_OVERFLOW;
+          vm = 0;
+        } else if (b_end > P0 && ((b_end - 1 - P0) >> LG) >= n_pages) {
+          // the expansion reaches a new page: take a free page of this workgroup's pool
+          bool got = false;
+          for (int w = 0; w < bm_words && !got; ++w) {
+            uint32_t x = bitmap[w];
+            while (x != 0xFFFFFFFFu) {
+              const uint32_t bit = (uint32_t)__builtin_ctz(~x);
+              const uint32_t old = atomicOr(&bitmap[w], 1u << bit);
+              if (!(old & (1u << bit))) {
+                ptab[((n_pages) << nbl) + ltid] = (uint16_t)(w * 32 + bit);
+                ++n_pages;
+                got = true;
+                break;
+              }
+              x = old | (1u << bit);
+            }
+          }
+          if (!got) {
+            status |= ST_STACK_OVERFLOW;
+            vm = 0;
+          }
+        }
+      }
+      // push each child: link into bucket `sc`, keep C = head of the lowest non-empty bucket
+      const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
+      const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
+      while (vm) {
+        const uint32_t j = (uint32_t)__builtin_ctz(vm);
+        vm &= vm - 1;
+        const bool is_ins = j == 0, is_del = j - 1 < 4, is_sym = j >= 5;
+        const uint32_t c = is_del ? j - 1 : (csym + j - 4) & 3;
+        const uint32_t pk = is_ins ? k : pick4(KK, c);
+        const uint32_t pl = is_ins ? l : pick4(LL, c);
+        const bool gap = !is_sym, open = gap && state == STATE_M;
+        const int is_mm = is_sym && (j != 8 || csym > 3);
+        const int n_mm = e_mm + is_mm, n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (gap && !open ? 1 : 0);
+        const int pi = is_del ? ni + 1 : ni;
+        const int pstate = is_ins ? STATE_I : is_del ? STATE_D : STATE_M;
+        const int pldp = is_sym && !is_mm ? ldp : pi;
+        const int sc = sc_base + (is_sym ? (is_mm ? o.s_mm : 0) : sc_gap);
+        if (sc >= o.n_stacks) { status |= ST_BAD_SCORE; break; }
+        if (n_mm > 31 || n_gapo > 7 || n_gape > 15) { status |= ST_STACK_OVERFLOW; break; }
         uint32_t slot;
         if (n_free) {
           --n_free;
-          slot = free_slots[n_free * NB + tid];
+          slot = free_slots[((n_free) << nbl) + ltid];
+        } else if (fl_known && fl_head != NILH) {
+          slot = fl_head;
+          fl_head = fl_next;
+          fl_known = fl_head == NILH;
         } else {
-          if (bump >= A.cap1 + A.cap2 || bump >= NILH) { status |= ST_STACK_OVERFLOW; return; }
-          if (bump >= A.cap1 && ent2 == nullptr) {
-            unsigned long long x = atomicAdd(A.pool_next, 1ull);
-            if (x >= A.pool_n) { status |= ST_STACK_OVERFLOW; return; }
-            ent2 = A.pool + x * A.cap2;
-          }
+          if (bump == P0 - HS) bump = P0;  // skip the hit area
           slot = bump++;
         }
-        const uint32_t hd = lds_heads[sc * NB + tid];
+        // an empty bucket's head is stale: the new entry ends its list
+        const uint32_t hd = bm_has(nonempty, sc) ? (uint32_t)lds_heads[((sc) << nbl) + ltid] : NILH;
         const uint4 ne = E::make(pk, pl, pi, pldp, hd, n_mm, n_gapo, n_gape, a, pstate);
         *slot_ptr(slot) = ne;
-        lds_heads[sc * NB + tid] = (H)slot;
+        lds_heads[((sc) << nbl) + ltid] = (H)slot;
+        bm_set(nonempty, sc);
         ++n_entries;
         if (!C_valid || sc <= C_b) {
           C = ne;
@@ -423,49 +655,18 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           C_b = sc;
           C_valid = true;
         }
-      };
-      const int tmp = (o.mode & MODE_LOGGAP) ? int_log2((uint32_t)(e_ge + e_go)) / 2 + 1 : e_go + e_ge;
-      if (allow_diff && ni >= o.indel_end_skip + tmp && len - ni >= o.indel_end_skip + tmp) {
-        if (state == STATE_M) {
-          if (e_go < o.max_gapo) {
-            push(ni, k, l, e_mm, e_go + 1, e_ge, STATE_I, ni);
-            for (int j = 0; j != 4; ++j) {
-              const uint32_t kk = l2of(ix, j) + pick4(ck4, j) + 1, ll = l2of(ix, j) + pick4(cl4, j);
-              if (kk <= ll) push(ni + 1, kk, ll, e_mm, e_go + 1, e_ge, STATE_D, ni + 1);
-            }
-          }
-        } else if (state == STATE_I) {
-          if (e_ge < o.max_gape) push(ni, k, l, e_mm, e_go, e_ge + 1, STATE_I, ni);
-        } else if (state == STATE_D) {
-          if (e_ge < o.max_gape && (e_ge + e_go < max_diff || occ < (uint32_t)o.max_del_occ)) {
-            for (int j = 0; j != 4; ++j) {
-              const uint32_t kk = l2of(ix, j) + pick4(ck4, j) + 1, ll = l2of(ix, j) + pick4(cl4, j);
-              if (kk <= ll) push(ni + 1, kk, ll, e_mm, e_go, e_ge + 1, STATE_D, ni + 1);
-            }
-          }
-        }
       }
-      if (allow_diff && allow_M) {
-        for (int j = 1; j <= 4; ++j) {
-          const uint32_t c = (csym + j) & 3;
-          const int is_mm = (j != 4 || csym > 3);
-          const uint32_t kk = l2of(ix, c) + pick4(ck4, c) + 1, ll = l2of(ix, c) + pick4(cl4, c);
-          if (kk <= ll) push(ni, kk, ll, e_mm + is_mm, e_go, e_ge, STATE_M, is_mm ? ni : ldp);
-        }
-      } else if (csym < 4) {
-        const uint32_t c = csym;
-        const uint32_t kk = l2of(ix, c) + pick4(ck4, c) + 1, ll = l2of(ix, c) + pick4(cl4, c);
-        if (kk <= ll) push(ni, kk, ll, e_mm, e_go, e_ge, STATE_M, ldp);
-      }
-      if (status) {  // overflow / bad score: give the read to the general kernels
-        A.n_aln[r] = 0;
-        A.status[r] = status;
-        st = 0;
+      if (pl_) pf5 += pnow() - t0_;
+      if (status) {  // overflow / bad score: the retry pass re-runs the read
+        end_stat = status;
+        st = 3;
       }
       continue;
     }
   hit : {
     // ---- hit (bwtgap.c:165-197)
+    const bool pl_ = pleader();
+    const uint64_t t0_ = pnow();
     const int score = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
     bool do_add = true;
     if (n_aln == 0) {
@@ -474,18 +675,17 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       if (o.mode & MODE_GAPE) best_diff += e_ge;
       if (!(o.mode & MODE_NONSTOP)) max_diff = (best_diff + 1 > opt_max_diff) ? opt_max_diff : best_diff + 1;
     }
-    uint4 *out = A.aln + (uint64_t)r * A.aln_cap;
     if (score == best_score) {
       best_cnt = (int)((uint32_t)best_cnt + (l - k + 1));
     } else if (best_cnt > o.max_top2) {
-      A.n_aln[r] = n_aln;
-      A.status[r] = 0;
-      st = 0;
+      if (pl_) pf6 += pnow() - t0_;
+      end_stat = 0;
+      st = 3;
       continue;
     }
     if (e_go) {
       for (int j = 0; j < n_aln; ++j) {
-        const uint4 h = out[j];
+        const uint4 h = ent1[P0 - 1 - j];
         if (h.y == k && h.z == l) { do_add = false; break; }
       }
     }
@@ -499,34 +699,41 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         if (w.x > x) { w.x -= x; width[q] = w; }
         else if (w.x == x) { ++jj; width[q] = make_uint2(mx - jj, 1u); }
       }
-      if (n_aln >= (int)A.aln_cap) {
-        A.n_aln[r] = 0;
-        A.status[r] = ST_ALN_OVERFLOW;
-        st = 0;
+      if ((uint32_t)n_aln >= HS) {
+        if (pl_) pf6 += pnow() - t0_;
+        end_stat = ST_ALN_OVERFLOW;  // hit area full
+        st = 3;
         continue;
       }
-      out[n_aln++] = make_uint4((uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24, k, l,
-                                (uint32_t)score);
+      ent1[P0 - 1 - n_aln] = make_uint4((uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
+                                        k, l, (uint32_t)score);
+      ++n_aln;
     }
+    if (pl_) pf6 += pnow() - t0_;
     continue;
   }
   }
-}
-
-size_t gapped_lds_bytes(int n_stacks, int block, bool wide) {
-  return (size_t)(n_stacks + FREE_DEPTH) * block * (wide ? 4 : 2);
+  if (PROF && A.prof) {
+    const uint64_t v[8] = {pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7};
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (v[q]) atomicAdd(A.prof + q, (unsigned long long)v[q]);
+  }
 }
 
 hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int blocks, int block, bool wide,
                          hipStream_t st) {
   if (g.n <= 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(d_counter, 0, 2 * sizeof(unsigned long long), st);
+  hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
-  const size_t lds = gapped_lds_bytes(g.o.n_stacks, block, wide);
+  const size_t lds =
+      gapped_lds_bytes(g.o.n_stacks, block, wide, g.max_pages, g.pages_per_block, g.lanes_per_wave, g.free_depth);
   if (wide)
-    hipLaunchKernelGGL(k_gapped<true>, dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<true, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+  else if (g.prof)
+    hipLaunchKernelGGL((k_gapped<false, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   else
-    hipLaunchKernelGGL(k_gapped<false>, dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   return hipGetLastError();
 }
 

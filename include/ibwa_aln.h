@@ -118,10 +118,18 @@ typedef struct {
 	int kmer_k;            /* K of the K-mer interval table the exact path used (0: none) */
 	int64_t n_stack_overflow;  /* first-pass reads whose stack did not fit (re-run) */
 	int64_t n_aln_overflow;    /* first-pass reads whose hits did not fit (re-run) */
+	int64_t n_heavy;           /* first-pass reads over the iteration budget (re-run) */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 
-/* Named engine options: "exact_path" (0/1, default 1), "exact_blocks", "lanes_per_chunk". */
+/* Named engine options:
+ *   "exact_path" (0/1, default 1)  exact-match kernel when max_diff == 0
+ *   "kmer_k" (-1 auto, 0 off, 1..16) K-mer interval table length
+ *   "exact_blocks", "lanes_per_chunk"
+ *   "gapped_v2" (0/1, default 1)   persistent gapped-search kernel (else the general kernels)
+ *   "gap_cap1", "gap_pages_per_block", "gap_hit_slots", "gap_blocks_per_cu", "gap_reads_per_chunk"
+ *                                  its per-lane static slots, 128 KiB pages per workgroup pool,
+ *                                  first-pass hit slots, residency and batch slice size */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
 /* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */

@@ -1,0 +1,106 @@
+/*
+ * ibwa_bwa_compat.h -- the drop-in boundary in the reference's own types.
+ *
+ * A reference build links libibwa_amd.so in place of bwtaln.c's
+ * bwa_cal_sa_reg_gap.  The structs below are layout mirrors of
+ * the reference's bwt_t (bwt.h:41-53) and bwa_seq_t (bwtaln.h:62-93) on the
+ * x86-64 SysV ABI -- same member types, order and bit-fields -- so the
+ * reference's pointers can be passed straight through; tests/test_compat.py
+ * checks every offset against the reference headers where they exist.
+ * gap_opt_t is ibwa_gap_opt_t (ibwa_aln.h), bwt_aln1_t is ibwa_aln1_t.
+ *
+ * Failure behaviour: the reference function returns void and crashes on
+ * allocation failure; this one prints the HIP/engine error to stderr and
+ * abort()s.  It never computes on the CPU.
+ */
+#ifndef IBWA_BWA_COMPAT_H
+#define IBWA_BWA_COMPAT_H
+#include <stdint.h>
+
+#include "ibwa_aln.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* bwt_t (bwt.h:41-53) */
+typedef struct {
+	uint32_t primary;       /* row of the $ suffix */
+	uint32_t L2[5];         /* cumulative symbol counts, L2[4] = seq_len */
+	uint32_t seq_len;
+	uint32_t bwt_size;      /* words at .bwt */
+	uint32_t *bwt;          /* interleaved [4 counts][8 BWT words] per 128 rows */
+	uint32_t cnt_table[256];
+	int sa_intv;
+	uint32_t n_sa;
+	uint32_t *sa;
+} ibwa_ref_bwt_t;
+
+/* bwt_multi1_t (bwtaln.h:51-60) -- only its size matters here */
+typedef struct {
+	uint64_t pos, remapped_pos;
+	uint32_t dbidx, remapped_dbidx;
+	int32_t remapped_seqid;
+	int remap_identical;
+	uint32_t n_cigar:15, gap:8, mm:8, strand:1;
+	uint32_t *cigar;
+} ibwa_ref_multi1_t;
+
+/* bwa_seq_t (bwtaln.h:62-93) */
+typedef struct {
+	char *name;
+	uint8_t *seq, *rseq, *qual;       /* seq: the read reversed (bwaseqio.c:191) */
+	uint32_t len:20, strand:1, type:2, dummy:1, extra_flag:8;
+	uint32_t n_mm:8, n_gapo:8, n_gape:8, mapQ:8;
+	int score;
+	int clip_len;
+	int n_aln;                        /* out */
+	ibwa_aln1_t *aln;                 /* out, malloc'd (freed by bwa_free_read_seq) */
+	int n_multi;
+	ibwa_ref_multi1_t *multi;
+	uint32_t sa;
+	uint64_t pos;
+	uint64_t remapped_pos;
+	uint32_t dbidx, remapped_dbidx;
+	int32_t remapped_seqid;
+	int remap_identical;
+	uint64_t c1:28, c2:28, seQ:8;
+	int n_cigar;
+	uint32_t *cigar;
+	int tid;
+	char bc[16];
+	uint32_t full_len:20, nm:12;
+	char *md;
+} ibwa_ref_seq_t;
+
+#define IBWA_TYPE_NO_MATCH 0 /* BWA_TYPE_NO_MATCH, bwtaln.h:9 */
+
+/*
+ * Bring the index of a running `aln` onto the GPUs (called by
+ * bwa_aln_core after bwt_restore_bwt, bwtaln.c:189).  n_gpus <= 0: every
+ * visible device.  The first device receives the arrays over PCIe, the rest
+ * by device-to-device copies.  Returns 0, or an IBWA_E* code.
+ */
+int ibwa_gpu_init(ibwa_ref_bwt_t *const bwt[2], int n_gpus);
+/* Release the engines (before bwt_destroy, bwtaln.c:239). */
+void ibwa_gpu_destroy(void);
+
+/*
+ * bwa_cal_sa_reg_gap (bwtaln.h:148, bwtaln.c:80-140), same signature and
+ * effects: for every read, aln/n_aln computed exactly as the reference
+ * does; sa = 0, type = NO_MATCH, c1 = c2 = 0; name/seq/rseq/qual freed and
+ * set to NULL.  `tid` is ignored (one call per batch, from the n_threads <= 1
+ * branch); the batch is split in contiguous slices over the GPUs with the
+ * batch-level options of bwtaln.c:89-93.  Without ibwa_gpu_init the first
+ * call initialises one GPU from `bwt`.  (Inside a reference build bwtaln.h
+ * already declares it with the reference's layout-identical types.)
+ */
+#ifndef BWTALN_H
+void bwa_cal_sa_reg_gap(int tid, ibwa_ref_bwt_t *const bwt[2], int n_seqs, ibwa_ref_seq_t *seqs,
+                        const ibwa_gap_opt_t *opt);
+#endif
+
+#ifdef __cplusplus
+}
+#endif
+#endif

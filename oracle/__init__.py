@@ -229,7 +229,7 @@ def encode_reads(recs, mode, trim_qual):
 
 
 STATS_DTYPE = np.dtype([("pushes", "<u4"), ("pops", "<u4"), ("peak_entries", "<u4"), ("peak_bucket", "<u4"),
-                        ("n_aln", "<u4"), ("touches", "<u4")])
+                        ("n_aln", "<u4"), ("touches", "<u4"), ("peak_real", "<u4")])
 
 
 def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False, stats=None):

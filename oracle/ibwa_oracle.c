@@ -274,13 +274,18 @@ static void cal_width(const or_bwt_t *b, int len, const uint8_t *str, width_t *w
 typedef struct {
 	uint32_t k, l;
 	int i, a, state, n_mm, n_gapo, n_gape, last_diff_pos, score;
+	int phantom; /* instrumentation: can never be expanded (see gs_push) */
 } entry_t;
 
 typedef struct { int n, m; entry_t *e; } bucket_t;
-typedef struct { int n_stacks, best, n_entries; bucket_t *b; uint32_t pushes, pops, peak, peak_bucket; } gstack_t;
+typedef struct {
+	int n_stacks, best, n_entries; bucket_t *b; uint32_t pushes, pops, peak, peak_bucket;
+	/* instrumentation: entries that can still be expanded when pushed */
+	int md_now, score_cap, gape; uint32_t n_real, peak_real;
+} gstack_t;
 
 /* per-read search statistics (test/bench instrumentation only) */
-typedef struct { uint32_t pushes, pops, peak_entries, peak_bucket, n_aln, touches; } or_stats_t;
+typedef struct { uint32_t pushes, pops, peak_entries, peak_bucket, n_aln, touches, peak_real; } or_stats_t;
 static or_stats_t *g_stats_next; /* consumed by the next or_cal_sa_reg_gap call */
 void or_set_stats(or_stats_t *buf) { g_stats_next = buf; }
 
@@ -313,6 +318,7 @@ static void gs_reset(gstack_t *s)
 	s->best = s->n_stacks;
 	s->n_entries = 0;
 	s->pushes = s->pops = s->peak = s->peak_bucket = 0;
+	s->n_real = s->peak_real = 0;
 }
 
 /* bwtgap.c:45-64.  last_diff_pos: a non-diff push keeps the value already in
@@ -332,6 +338,10 @@ static void gs_push(gstack_t *s, int a, int i, uint32_t k, uint32_t l, int n_mm,
 	p->n_mm = n_mm & 0xff; p->n_gapo = n_gapo & 0xff; p->n_gape = n_gape & 0xff;
 	p->last_diff_pos = ldp;
 	p->score = score & 0x7ff; /* info = score<<21 keeps 11 bits */
+	/* phantom: more diffs than the (non-increasing) max_diff allows, or a score the
+	 * search stops at once a hit has fixed best_score -- such entries are only counted */
+	p->phantom = (n_mm + n_gapo + (s->gape ? n_gape : 0) > s->md_now) || score > s->score_cap;
+	if (!p->phantom && ++s->n_real > s->peak_real) s->peak_real = s->n_real;
 	++q->n;
 	++s->n_entries;
 	if (s->best > score) s->best = score;
@@ -345,6 +355,7 @@ static void gs_pop(gstack_t *s, entry_t *e)
 	bucket_t *q = s->b + s->best;
 	++s->pops;
 	*e = q->e[q->n - 1];
+	if (!e->phantom) --s->n_real;
 	--q->n;
 	--s->n_entries;
 	if (q->n == 0 && s->n_entries) {
@@ -389,6 +400,9 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 	if (nN > max_diff) return;
 
 	gs_reset(stack);
+	stack->md_now = max_diff;
+	stack->score_cap = 0x7fffffff;
+	stack->gape = (opt->mode & OR_MODE_GAPE) != 0;
 	gs_push(stack, 0, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
 	gs_push(stack, 1, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
 
@@ -430,8 +444,11 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 				best_score = score;
 				best_diff = e.n_mm + e.n_gapo;
 				if (opt->mode & OR_MODE_GAPE) best_diff += e.n_gape;
-				if (!(opt->mode & OR_MODE_NONSTOP))
+				if (!(opt->mode & OR_MODE_NONSTOP)) {
 					max_diff = (best_diff + 1 > opt->max_diff) ? opt->max_diff : best_diff + 1;
+					stack->md_now = max_diff;
+					stack->score_cap = best_score + opt->s_mm;
+				}
 			}
 			if (score == best_score) best_cnt = (int)((uint32_t)best_cnt + (l - k + 1));
 			else if (best_cnt > opt->max_top2) break;
@@ -614,6 +631,7 @@ static void *worker(void *data)
 				or_stats_t *st = B->stats + r;
 				st->pushes = stack->pushes; st->pops = stack->pops; st->peak_entries = stack->peak;
 				st->peak_bucket = stack->peak_bucket; st->n_aln = out.n; st->touches = t;
+				st->peak_real = stack->peak_real;
 			}
 			if (out.n) {
 				B->per_read[r] = (or_aln1_t*)malloc(out.n * sizeof(or_aln1_t));

@@ -1,0 +1,160 @@
+"""The drop-in boundary in the reference's own types (include/ibwa_bwa_compat.h).
+
+* layout: every member offset and the sizes of the mirrored bwt_t / bwa_seq_t /
+  gap_opt_t / bwt_aln1_t equal the reference's (compile-time checks against the
+  reference headers; runs only where /root/reference exists -- this container);
+* drop-in parity (GPU): bwa_cal_sa_reg_gap called exactly as bwa_aln_core calls
+  it -- reference-layout bwt_t from the .bwt/.rbwt files, a bwa_seq_t array
+  with malloc'd seq/rseq/qual/name -- reproduces the golden .sai bytes and
+  performs the reference's side effects (seq/rseq/qual/name freed and NULL,
+  sa = 0, type = NO_MATCH, c1 = c2 = 0).
+"""
+import ctypes as c
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from ibwa_amd import _native
+from ibwa_amd import engine as E
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+
+
+class RefBwt(c.Structure):  # bwt_t (bwt.h:41-53)
+    _fields_ = [("primary", c.c_uint32), ("L2", c.c_uint32 * 5), ("seq_len", c.c_uint32),
+                ("bwt_size", c.c_uint32), ("bwt", c.POINTER(c.c_uint32)), ("cnt_table", c.c_uint32 * 256),
+                ("sa_intv", c.c_int), ("n_sa", c.c_uint32), ("sa", c.POINTER(c.c_uint32))]
+
+
+class RefSeq(c.Structure):  # bwa_seq_t (bwtaln.h:62-93)
+    _fields_ = [("name", c.c_void_p), ("seq", c.c_void_p), ("rseq", c.c_void_p), ("qual", c.c_void_p),
+                ("len", c.c_uint32, 20), ("strand", c.c_uint32, 1), ("type", c.c_uint32, 2),
+                ("dummy", c.c_uint32, 1), ("extra_flag", c.c_uint32, 8),
+                ("n_mm", c.c_uint32, 8), ("n_gapo", c.c_uint32, 8), ("n_gape", c.c_uint32, 8),
+                ("mapQ", c.c_uint32, 8), ("score", c.c_int), ("clip_len", c.c_int), ("n_aln", c.c_int),
+                ("aln", c.c_void_p), ("n_multi", c.c_int), ("multi", c.c_void_p), ("sa", c.c_uint32),
+                ("pos", c.c_uint64), ("remapped_pos", c.c_uint64), ("dbidx", c.c_uint32),
+                ("remapped_dbidx", c.c_uint32), ("remapped_seqid", c.c_int32), ("remap_identical", c.c_int),
+                ("c1", c.c_uint64, 28), ("c2", c.c_uint64, 28), ("seQ", c.c_uint64, 8), ("n_cigar", c.c_int),
+                ("cigar", c.c_void_p), ("tid", c.c_int), ("bc", c.c_char * 16),
+                ("full_len", c.c_uint32, 20), ("nm", c.c_uint32, 12), ("md", c.c_void_p)]
+
+
+LAYOUT_C = r"""
+#include <stddef.h>
+#include "bwtaln.h"
+#include "ibwa_bwa_compat.h"
+#define SAME(R, M, F) _Static_assert(offsetof(R, F) == offsetof(M, F), #R "." #F); \
+                      _Static_assert(sizeof(((R *)0)->F) == sizeof(((M *)0)->F), #R "." #F " size");
+#define SIZE(R, M) _Static_assert(sizeof(R) == sizeof(M), #R " size");
+SIZE(bwt_t, ibwa_ref_bwt_t)
+SAME(bwt_t, ibwa_ref_bwt_t, primary) SAME(bwt_t, ibwa_ref_bwt_t, L2) SAME(bwt_t, ibwa_ref_bwt_t, seq_len)
+SAME(bwt_t, ibwa_ref_bwt_t, bwt_size) SAME(bwt_t, ibwa_ref_bwt_t, bwt) SAME(bwt_t, ibwa_ref_bwt_t, cnt_table)
+SAME(bwt_t, ibwa_ref_bwt_t, sa_intv) SAME(bwt_t, ibwa_ref_bwt_t, n_sa) SAME(bwt_t, ibwa_ref_bwt_t, sa)
+SIZE(bwa_seq_t, ibwa_ref_seq_t)
+SAME(bwa_seq_t, ibwa_ref_seq_t, name) SAME(bwa_seq_t, ibwa_ref_seq_t, seq) SAME(bwa_seq_t, ibwa_ref_seq_t, rseq)
+SAME(bwa_seq_t, ibwa_ref_seq_t, qual) SAME(bwa_seq_t, ibwa_ref_seq_t, score) SAME(bwa_seq_t, ibwa_ref_seq_t, clip_len)
+SAME(bwa_seq_t, ibwa_ref_seq_t, n_aln) SAME(bwa_seq_t, ibwa_ref_seq_t, aln) SAME(bwa_seq_t, ibwa_ref_seq_t, n_multi)
+SAME(bwa_seq_t, ibwa_ref_seq_t, multi) SAME(bwa_seq_t, ibwa_ref_seq_t, sa) SAME(bwa_seq_t, ibwa_ref_seq_t, pos)
+SAME(bwa_seq_t, ibwa_ref_seq_t, remapped_pos) SAME(bwa_seq_t, ibwa_ref_seq_t, dbidx)
+SAME(bwa_seq_t, ibwa_ref_seq_t, remapped_dbidx) SAME(bwa_seq_t, ibwa_ref_seq_t, remapped_seqid)
+SAME(bwa_seq_t, ibwa_ref_seq_t, remap_identical) SAME(bwa_seq_t, ibwa_ref_seq_t, n_cigar)
+SAME(bwa_seq_t, ibwa_ref_seq_t, cigar) SAME(bwa_seq_t, ibwa_ref_seq_t, tid) SAME(bwa_seq_t, ibwa_ref_seq_t, bc)
+SAME(bwa_seq_t, ibwa_ref_seq_t, md)
+SIZE(bwt_multi1_t, ibwa_ref_multi1_t)
+SIZE(gap_opt_t, ibwa_gap_opt_t)
+SAME(gap_opt_t, ibwa_gap_opt_t, s_mm) SAME(gap_opt_t, ibwa_gap_opt_t, mode) SAME(gap_opt_t, ibwa_gap_opt_t, fnr)
+SAME(gap_opt_t, ibwa_gap_opt_t, max_diff) SAME(gap_opt_t, ibwa_gap_opt_t, seed_len)
+SAME(gap_opt_t, ibwa_gap_opt_t, max_top2) SAME(gap_opt_t, ibwa_gap_opt_t, trim_qual)
+SIZE(bwt_aln1_t, ibwa_aln1_t)
+SAME(bwt_aln1_t, ibwa_aln1_t, k) SAME(bwt_aln1_t, ibwa_aln1_t, l) SAME(bwt_aln1_t, ibwa_aln1_t, score)
+int main(void) { return 0; }
+"""
+
+
+@pytest.mark.skipif(not os.path.isdir(REF) or not shutil.which("gcc"), reason="reference headers absent")
+def test_layout_matches_reference_headers(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(LAYOUT_C)
+    r = subprocess.run(["gcc", "-std=gnu11", "-fsyntax-only", f"-I{REF}", f"-I{os.path.join(ROOT, 'include')}",
+                        str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_python_mirror_sizes():
+    # the ctypes mirrors used below agree with the C header's (x86-64 SysV) sizes
+    assert c.sizeof(RefBwt) == 4 * 8 + 8 + 1024 + 8 + 8
+    assert c.sizeof(RefSeq) % 8 == 0 and RefSeq.bc.offset + 16 <= c.sizeof(RefSeq)
+
+
+def _load_ref_bwt(path, keep):
+    raw = np.fromfile(path, dtype=np.uint32)
+    words = np.ascontiguousarray(raw[5:])
+    keep.append(words)
+    b = RefBwt()
+    b.primary = int(raw[0])
+    for j in range(4):
+        b.L2[j + 1] = int(raw[1 + j])
+    b.seq_len = b.L2[4]
+    b.bwt_size = words.size
+    b.bwt = words.ctypes.data_as(c.POINTER(c.c_uint32))
+    return b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["r100.default", "mixed.default", "mixed.n0", "r150.default", "mixed.c"])
+def test_dropin_matches_golden_sai(golden_dir, sai_manifest, key):
+    L = c.CDLL(_native.LIB_PATH)
+    libc = c.CDLL(None)
+    libc.malloc.restype = c.c_void_p
+    libc.malloc.argtypes = [c.c_size_t]
+    libc.free.argtypes = [c.c_void_p]
+    keep = []
+    b0 = _load_ref_bwt(os.path.join(golden_dir, "g1m.bwt"), keep)
+    b1 = _load_ref_bwt(os.path.join(golden_dir, "g1m.rbwt"), keep)
+    bw = (c.POINTER(RefBwt) * 2)(c.pointer(b0), c.pointer(b1))
+    L.ibwa_gpu_init.argtypes = [c.c_void_p, c.c_int]
+    L.bwa_cal_sa_reg_gap.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.POINTER(E.GapOpt)]
+    L.bwa_cal_sa_reg_gap.restype = None
+    assert L.ibwa_gpu_init(bw, 1) == 0
+    try:
+        m = sai_manifest[key]
+        opt, _ = oracle.parse_aln_args(m["argv"])
+        recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+        seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+        n = lens.size
+        arr = (RefSeq * n)()
+        for i in range(n):
+            s = seqs[int(offs[i]):int(offs[i]) + int(lens[i])]
+            p = libc.malloc(max(1, s.size))
+            c.memmove(p, s.ctypes.data, s.size)
+            arr[i].seq = p
+            arr[i].rseq = libc.malloc(max(1, s.size))  # content unused by the engine; freed by it
+            arr[i].qual = libc.malloc(8)
+            arr[i].name = libc.malloc(8)
+            arr[i].len = int(lens[i])
+            arr[i].tid = -1
+            arr[i].sa = 7
+            arr[i].type = 3
+        eo = E.GapOpt()
+        for f, _ in E.GapOpt._fields_:
+            setattr(eo, f, getattr(opt, f))
+        L.bwa_cal_sa_reg_gap(0, bw, n, arr, c.byref(eo))
+        n_aln = np.array([arr[i].n_aln for i in range(n)], dtype=np.int32)
+        parts = [c.string_at(arr[i].aln, 16 * arr[i].n_aln) for i in range(n)]
+        alns = np.frombuffer(b"".join(parts), dtype=oracle.ALN_DTYPE)
+        assert all(arr[i].seq is None and arr[i].rseq is None and arr[i].qual is None and arr[i].name is None
+                   for i in range(n))
+        assert all(arr[i].sa == 0 and arr[i].type == 0 and arr[i].c1 == 0 and arr[i].c2 == 0 for i in range(n))
+        got = oracle.sai_bytes(opt, n_aln, alns)
+        exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+        assert oracle.sai_body_equal(got, exp), key
+        for i in range(n):
+            libc.free(c.c_void_p(arr[i].aln))
+    finally:
+        L.ibwa_gpu_destroy()

@@ -62,8 +62,8 @@ def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap
         gpu_engine.set_tuning(stack_cap=stack_cap, aln_cap=aln_cap)
         gpu_engine.set_option("gapped_v2", v2)
         gpu_engine.set_option("gap_cap1", stack_cap)
-        gpu_engine.set_option("gap_pool_n", 4)
-        gpu_engine.set_option("gap_aln_cap", aln_cap)
+        gpu_engine.set_option("gap_pages_per_block", 1)
+        gpu_engine.set_option("gap_hit_slots", aln_cap)
         for key in ["r150.default", "mixed.N", "r100.default"]:
             m = sai_manifest[key]
             opt, _ = oracle.parse_aln_args(m["argv"])
@@ -75,7 +75,7 @@ def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap
             assert oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp), key
     finally:
         gpu_engine.set_tuning(stack_cap=4096, aln_cap=8)
-        for k, v in [("gapped_v2", 1), ("gap_cap1", 8192), ("gap_pool_n", 8192), ("gap_aln_cap", 64)]:
+        for k, v in [("gapped_v2", 1), ("gap_cap1", 8192), ("gap_pages_per_block", 384), ("gap_hit_slots", 256)]:
             gpu_engine.set_option(k, v)
 
 

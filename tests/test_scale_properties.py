@@ -79,15 +79,15 @@ def test_exact_reads_round_trip(mid_genome):
 @pytest.mark.parametrize("argv,ln,sub,n,tune", [
     ([], 100, 0.01, 30_000, {}), (["-n", "0"], 100, 0.01, 100_000, {}),
     ([], 150, 0.02, 8_000, {}), (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {}),
-    # small primary stack regions: many reads spill into the extension pool, some overflow it
-    ([], 100, 0.02, 20_000, {"gap_cap1": 256, "gap_pool_n": 64}),
+    # small static regions: many reads take pages from their workgroup pool, some exhaust it
+    ([], 100, 0.02, 20_000, {"gap_cap1": 256, "gap_pages_per_block": 2}),
     (["-n", "0"], 100, 0.01, 20_000, {"exact_path": 0}),
     ([], 100, 0.01, 4_000, {"gapped_v2": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
     o, e = eopt(argv)
-    defaults = {"gap_cap1": 8192, "gap_pool_n": 8192, "exact_path": 1, "gapped_v2": 1}
+    defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--read-len", type=int, default=100)
     ap.add_argument("--aln", default="")
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--save", default="", help="write the per-read stats (npy) here")
     a = ap.parse_args()
     den = 1_000_000
     ascii_, codes, lens, _ = bench.make_genome(int(round(a.scale * den)), den, 37, a.threads)
@@ -39,12 +40,15 @@ def main():
     opt, _ = oracle.parse_aln_args(a.aln.split())
     st = np.zeros(a.reads, dtype=oracle.STATS_DTYPE)
     n_aln, _, _ = oracle.cal_sa_reg_gap(b0, b1, seq, off, lns, opt, n_threads=a.threads, stats=st)
-    for f in ["pushes", "pops", "peak_entries", "peak_bucket", "n_aln", "touches"]:
+    if a.save:
+        np.save(a.save, st)
+    for f in ["pushes", "pops", "peak_entries", "peak_real", "peak_bucket", "n_aln", "touches"]:
         v = st[f].astype(np.float64)
         print(f"{f:13s} mean {v.mean():9.1f}  p50 {np.percentile(v, 50):8.0f}  p99 {np.percentile(v, 99):8.0f}  "
               f"p99.9 {np.percentile(v, 99.9):8.0f}  max {v.max():8.0f}")
     for cap in [4096, 16384, 65535]:
-        print(f"pushes > {cap}: {(st['pushes'] > cap).sum()}   peak_entries > {cap}: {(st['peak_entries'] > cap).sum()}")
+        print(f"pushes > {cap}: {(st['pushes'] > cap).sum()}   peak_entries > {cap}: {(st['peak_entries'] > cap).sum()}"
+              f"   peak_real > {cap}: {(st['peak_real'] > cap).sum()}")
     for cap in [8, 16, 32, 64]:
         print(f"n_aln > {cap}: {(n_aln > cap).sum()}")
 
