@@ -71,6 +71,37 @@ def make_reads(ascii_, lens, seed, n, ln, sub, indel, threads):
     return seq, off, lns
 
 
+def shard_seed(rank):
+    """Reads seed of a rank: every rank aligns its own, disjoint synthetic reads (weak scaling)."""
+    return 2 + 1000 * rank
+
+
+def reduce_max(x, dist, device):
+    """Max of a per-rank float over all ranks (the timed region ends on the slowest rank)."""
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
+    same workload (profiles/<round>_<tag>_pmc.json, written by tools/profile_round.sh: separate
+    --pmc passes, EA read/write requests by size).  None if no such profile exists."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and d.get("bench_line", {}).get("config", {}).get("workload") == workload:
+            return k["read_bytes_per_dispatch"] + k["write_bytes_per_dispatch"], os.path.basename(f), k.get("avg_ms")
+    return None
+
+
 def cpu_baseline(eng, opt_args, seq, off, lns, budget_s, threads):
     """Time the CPU path on a bounded sample of the same reads (rank 0, N=1 only).
 
@@ -130,12 +161,7 @@ def main():
         dist = dist_
 
     def barrier_max(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return reduce_max(x, dist, f"cuda:{local}")
 
     import oracle
     from ibwa_amd import engine as E
@@ -145,7 +171,7 @@ def main():
     ascii_, codes, lens, n_amb = make_genome(int(round(args.scale * den)), den, 37, threads)
     log(f"genome {codes.size/1e9:.3f} Gbp ({n_amb} N->random), {time.perf_counter()-tg:.1f} s")
     tr = time.perf_counter()
-    seq, off, lns = make_reads(ascii_, lens, 2 + 1000 * rank, args.reads, args.read_len, 0.01, 0.05, threads)
+    seq, off, lns = make_reads(ascii_, lens, shard_seed(rank), args.reads, args.read_len, 0.01, 0.05, threads)
     del ascii_
     log(f"{args.reads} reads x {args.read_len} bp, {time.perf_counter()-tr:.1f} s")
 
@@ -249,8 +275,13 @@ def main():
                 kname = "k_width+k_gapped" if path == 2 else "k_width+k_search"
                 k_ms = (ms_w + ms_s) / launches
             ach = path_touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9
+            pmc = pmc_traffic(kname, result["config"]["workload"])
             result["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": kname,
+                                  "frac": ach / HBM_PEAK_GBS, "traffic": pmc[0] if pmc else None, "kernel": kname,
+                                  "traffic_source": pmc[1] if pmc else None,
+                                  "traffic_GBps": pmc[0] / (k_ms * 1e-3) / 1e9 if pmc else None,
+                                  "profiled_kernel_ms": pmc[2] if pmc else None,
+                                  "algorithmic_bytes_per_launch": path_touches * 64.0 * args.reads,
                                   "kernel_ms_per_launch": k_ms,
                                   "touches_per_read": path_touches, "bytes_per_touch": 64,
                                   "reference_touches_per_read": touches,
@@ -259,7 +290,7 @@ def main():
         result["extra"] = {"index_build_s": build_s, "n_retry": int(n_retry), "parity_sample_ok": check_ok,
                            "n_stack_overflow": int(stl.n_stack_overflow), "n_aln_overflow": int(stl.n_aln_overflow),
                            "path": {0: "width+search", 1: "exact", 2: "width+gapped"}.get(path, str(path)),
-                           "k_width_ms": ms_w / launches, "k_search_ms": ms_s / launches,
+                           "k_width_or_pack_ms": ms_w / launches, "k_search_ms": ms_s / launches,
                            "retry_ms": ms_r / launches}
         print(json.dumps(result), flush=True)
         for k in [int(x) for x in args.sweep_k.split(",") if x.strip()]:

@@ -114,7 +114,7 @@ hipError_t launch_width(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_search(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1, const uint2 *kt0,
                         const uint2 *kt1, int K, uint4 *rec, uint32_t stride, unsigned long long *d_counter,
-                        int blocks, hipStream_t st);
+                        int blocks, hipEvent_t ev_mid, hipStream_t st);
 uint64_t occ64_blocks(uint32_t seq_len);
 hipError_t build_occ64(const IndexView &ix, uint4 *out, hipStream_t st);
 uint32_t exact_record_stride(int max_len);

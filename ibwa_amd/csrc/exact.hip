@@ -49,17 +49,30 @@ __global__ void __launch_bounds__(256) k_pack_reads(const uint8_t *__restrict__ 
   const bool use_tab = K > 0 && L >= K;
   const int p0 = use_tab ? L - 1 - K : L - 1;
   uint32_t nN = 0, xa = 0, xb = 0, w = 0, first = 0;
-  for (int j = 0; j < L; ++j) {
-    const uint32_t c = s[j];
-    nN += c > 3;
-    const uint32_t c2 = c & 3;
-    xa = (xa << 2) | (comp ? c2 ^ 3u : c2);
-    xb = (xb << 2) | c2;
-    w |= c2 << (2 * (j & 15));
-    if ((j & 15) == 15 || j == L - 1) {
-      W[j >> 4] = w;
-      if (p0 >= 0 && (p0 >> 4) == (j >> 4)) first = w;
-      w = 0;
+  // 16 B loads from the aligned-down start (the staging buffer has 16 B of tail padding):
+  // neighbouring lanes read neighbouring reads, so each line is fetched about once
+  const uint4 *q0 = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15);
+  const int mis = (int)(reinterpret_cast<uintptr_t>(s) & 15);
+  const int nq = (mis + L + 15) >> 4;
+  for (int q = 0; q < nq; ++q) {
+    const uint4 v = q0[q];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const uint32_t word = b < 4 ? v.x : b < 8 ? v.y : b < 12 ? v.z : v.w;
+      const uint32_t c = (word >> (8 * (b & 3))) & 0xffu;
+      const int j = q * 16 + b - mis;
+      if (j >= 0 && j < L) {
+        nN += c > 3;
+        const uint32_t c2 = c & 3;
+        xa = (xa << 2) | (comp ? c2 ^ 3u : c2);
+        xb = (xb << 2) | c2;
+        w |= c2 << (2 * (j & 15));
+        if ((j & 15) == 15 || j == L - 1) {
+          W[j >> 4] = w;
+          if (p0 >= 0 && (p0 >> 4) == (j >> 4)) first = w;
+          w = 0;
+        }
+      }
     }
   }
   const uint32_t kmask = K >= 16 ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
@@ -211,7 +224,7 @@ uint32_t exact_record_stride(int max_len) {  // in uint4 units
 
 hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1, const uint2 *kt0,
                         const uint2 *kt1, int K, uint4 *rec, uint32_t stride, unsigned long long *d_counter,
-                        int blocks, hipStream_t st) {
+                        int blocks, hipEvent_t ev_mid, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   const int comp = (a.o.mode & MODE_COMPREAD) ? 1 : 0;
   hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a.seq, a.off, a.len, a.n,
@@ -220,6 +233,7 @@ hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
+  if (ev_mid && (e = hipEventRecord(ev_mid, st)) != hipSuccess) return e;  // pack | search boundary
   ExactArgs x;
   x.ix[0] = a.ix[0];
   x.ix[1] = a.ix[1];

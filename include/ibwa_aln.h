@@ -107,8 +107,8 @@ int ibwa_batch_run(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt, int batch_max_len
 int ibwa_batch_fetch(ibwa_ctx_t *ctx, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total);
 
 typedef struct {
-	double ms_width;       /* width kernel, HIP events on the engine stream */
-	double ms_search;      /* search kernel (first pass) */
+	double ms_width;       /* width kernel (exact path: its read-packing pre-pass), HIP events */
+	double ms_search;      /* search kernel (first pass; exact path: k_exact alone) */
 	double ms_retry;       /* large-capacity retry pass (0 if none) */
 	double ms_total;       /* ibwa_batch_run wall, device-synchronised */
 	int64_t n_retry;       /* reads re-run in the large-capacity pass */
