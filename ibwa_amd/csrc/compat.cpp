@@ -150,4 +150,87 @@ void bwa_cal_sa_reg_gap(int tid, ibwa_ref_bwt_t *const bwt[2], int n_seqs, ibwa_
   }
 }
 
+/*
+ * bwa_sw_core (bwasw.c:29-112) for a batch of mate rescues: the host checks and
+ * post-processing of the reference around one batched aln_local_core launch.
+ */
+int ibwa_sw_core_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *seq, const uint64_t *off, const uint32_t *len,
+                       const uint8_t *ref, const uint64_t *ref_off, const uint32_t *ref_len, const int32_t *reglen,
+                       int64_t *beg, int64_t l_pac, int32_t *n_cigar, uint32_t *cnt, uint32_t **cigar) {
+  *cigar = nullptr;
+  std::vector<int64_t> idx;  // pairs that pass the pre-checks (bwasw.c:40-43)
+  for (int64_t p = 0; p < n; ++p) {
+    n_cigar[p] = 0;
+    cnt[p] = 0;
+    const int L = (int)len[p];
+    if (reglen[p] < 20 || l_pac - beg[p] < L) continue;
+    int x = 0;
+    for (int k = 0; k < L; ++k) x += seq[off[p] + k] >= 4;
+    if (L == 0 || (float)x / L >= 0.25f || L - x < 20) continue;
+    idx.push_back(p);
+  }
+  const int64_t m = (int64_t)idx.size();
+  std::vector<uint64_t> o1(m), o2(m);
+  std::vector<uint32_t> l1(m), l2(m);
+  for (int64_t q = 0; q < m; ++q) {
+    o1[q] = ref_off[idx[q]]; l1[q] = ref_len[idx[q]];
+    o2[q] = off[idx[q]]; l2[q] = len[idx[q]];
+  }
+  std::vector<int32_t> score(m), plen(m), ends(4 * m), ncig(m);
+  uint32_t *c32 = nullptr;
+  int64_t tot = 0;
+  if (int rc = ibwa_sw_batch(ctx, m, ref, o1.data(), l1.data(), seq, o2.data(), l2.data(), score.data(), plen.data(),
+                             ends.data(), ncig.data(), &c32, &tot))
+    return rc;
+  std::vector<uint32_t> out;
+  std::vector<std::vector<uint32_t>> per(n);
+  int64_t q32 = 0;
+  for (int64_t q = 0; q < m; ++q) {
+    const int64_t p = idx[q];
+    const uint32_t *cg = c32 + q32;
+    q32 += ncig[q];
+    if (score[q] < 0 || ncig[q] == 0) continue;  // ret < 0 (bwasw.c:52-55), or no path
+    // aln_path2cigar32 -> bwa_cigar_t op << 29 | len (bwtaln.c:332-342)
+    std::vector<uint32_t> c;
+    uint32_t x = 0, y = 0;
+    for (int k = 0; k < ncig[q]; ++k) {
+      const uint32_t op = cg[k] & 0xf, ln = cg[k] >> 4;
+      c.push_back(op << 29 | ln);
+      if (op == 0) { x += ln; y += ln; } else if (op == 2) x += ln; else y += ln;
+    }
+    if (x < 20 || y < 20) continue;  // bwasw.c:59-69
+    const int si = ends[4 * q], sj = ends[4 * q + 1], ej = ends[4 * q + 3];
+    const int L = (int)len[p];
+    beg[p] += (si ? si : 1) - 1;
+    const int start = (sj ? sj : 1) - 1;
+    if (start) c.insert(c.begin(), 3u << 29 | (uint32_t)start);  // soft clips (bwasw.c:71-87)
+    if (ej < L) c.push_back(3u << 29 | (uint32_t)(L - ej));
+    // mismatches and gaps (bwasw.c:89-108)
+    int n_mm = 0, n_gapo = 0, n_gape = 0;
+    uint32_t rx = si ? si - 1 : 0, ry = sj ? sj - 1 : 0;
+    const uint8_t *rs = ref + ref_off[p], *ss = seq + off[p];
+    for (uint32_t v : c) {
+      const uint32_t op = v >> 29, ln = v & 0x1fffffffu;
+      if (op == 0) {
+        for (uint32_t l = 0; l < ln; ++l)
+          if (rs[rx + l] < 4 && ss[ry + l] < 4 && rs[rx + l] != ss[ry + l]) ++n_mm;
+        rx += ln; ry += ln;
+      } else if (op == 2) {
+        rx += ln; ++n_gapo; n_gape += (int)ln - 1;
+      } else if (op == 1) {
+        ry += ln; ++n_gapo; n_gape += (int)ln - 1;
+      }
+    }
+    cnt[p] = (uint32_t)n_mm << 16 | (uint32_t)n_gapo << 8 | (uint32_t)n_gape;
+    n_cigar[p] = (int32_t)c.size();
+    per[p].swap(c);
+  }
+  ibwa_free(c32);
+  for (int64_t p = 0; p < n; ++p) out.insert(out.end(), per[p].begin(), per[p].end());
+  *cigar = (uint32_t *)malloc(std::max<size_t>(out.size(), 1) * 4);
+  if (!*cigar) return IBWA_EINVAL;
+  if (!out.empty()) memcpy(*cigar, out.data(), out.size() * 4);
+  return 0;
+}
+
 }  // extern "C"

@@ -920,6 +920,99 @@ int ibwa_aln_batch(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int64_t n, const ui
   return ibwa_batch_fetch(c, n_aln, aln, n_total);
 }
 
+int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
+                  const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int32_t *score,
+                  int32_t *path_len, int32_t *ends, int32_t *n_cigar, uint32_t **cigar, int64_t *n_cigar_total) {
+  if (n < 0) return fail(IBWA_EINVAL, "negative pair count");
+  *cigar = nullptr;
+  if (n_cigar_total) *n_cigar_total = 0;
+  if (n == 0) {
+    *cigar = (uint32_t *)malloc(4);
+    return 0;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  int max1 = 0, max2 = 0;
+  uint64_t end1 = 0, end2 = 0;
+  for (int64_t p = 0; p < n; ++p) {
+    if (std::min(len1[p], len2[p]) * 11ull > 32000)
+      return fail(IBWA_EINVAL, "pair %lld: min(len1, len2) * 11 > 32000", (long long)p);
+    max1 = std::max<int>(max1, (int)len1[p]);
+    max2 = std::max<int>(max2, (int)len2[p]);
+    end1 = std::max<uint64_t>(end1, off1[p] + len1[p]);
+    end2 = std::max<uint64_t>(end2, off2[p] + len2[p]);
+  }
+  const int cap = std::max(1, max1 + max2);
+  DBuf s1, s2, o1, o2, l1, l2, sc, pl, nc, en, cg, scr, tbb;
+  auto release = [&]() {
+    for (DBuf *b : {&s1, &s2, &o1, &o2, &l1, &l2, &sc, &pl, &nc, &en, &cg, &scr, &tbb}) b->release();
+  };
+  const uint64_t wpl = sw_words_per_lane(max1), tpl = sw_tb_per_lane(max1, max2);
+  const uint64_t per_wave = (wpl * 4 + tpl) * 64;
+  // a persistent grid within ~8 GiB of DP scratch
+  const int64_t waves = std::max<int64_t>(1, std::min<int64_t>((n + 63) / 64, (int64_t)((8ull << 30) / per_wave)));
+  const int blocks = (int)((waves + 3) / 4);
+  int rc = 0;
+  if ((rc = s1.ensure(end1 + 16)) || (rc = s2.ensure(end2 + 16)) || (rc = o1.ensure(n * 8)) || (rc = o2.ensure(n * 8)) ||
+      (rc = l1.ensure(n * 4)) || (rc = l2.ensure(n * 4)) || (rc = sc.ensure(n * 4)) || (rc = pl.ensure(n * 4)) ||
+      (rc = nc.ensure(n * 4)) || (rc = en.ensure(n * 16)) || (rc = cg.ensure((uint64_t)n * cap * 4)) ||
+      (rc = scr.ensure((uint64_t)blocks * 4 * wpl * 4 * 64)) || (rc = tbb.ensure((uint64_t)blocks * 4 * tpl * 64)) ||
+      (rc = c->d_counter.ensure(64))) {
+    release();
+    return rc;
+  }
+  auto chk = [&](hipError_t e, const char *what) {
+    if (e != hipSuccess && !rc) rc = fail(IBWA_EHIP, "%s: %s", what, hipGetErrorString(e));
+  };
+  chk(hipMemcpyAsync(s1.p, ref, end1, hipMemcpyHostToDevice, c->stream), "H2D ref");
+  chk(hipMemcpyAsync(s2.p, qry, end2, hipMemcpyHostToDevice, c->stream), "H2D qry");
+  chk(hipMemcpyAsync(o1.p, off1, n * 8, hipMemcpyHostToDevice, c->stream), "H2D off1");
+  chk(hipMemcpyAsync(o2.p, off2, n * 8, hipMemcpyHostToDevice, c->stream), "H2D off2");
+  chk(hipMemcpyAsync(l1.p, len1, n * 4, hipMemcpyHostToDevice, c->stream), "H2D len1");
+  chk(hipMemcpyAsync(l2.p, len2, n * 4, hipMemcpyHostToDevice, c->stream), "H2D len2");
+  SwArgs A = {};
+  A.seq1 = s1.as<uint8_t>(); A.seq2 = s2.as<uint8_t>();
+  A.off1 = o1.as<uint64_t>(); A.off2 = o2.as<uint64_t>();
+  A.len1 = l1.as<uint32_t>(); A.len2 = l2.as<uint32_t>();
+  A.n = n;
+  A.max_len1 = max1;
+  A.scratch = scr.as<uint32_t>(); A.words_per_lane = wpl;
+  A.tb = tbb.as<uint8_t>(); A.tb_per_lane = tpl;
+  A.score = sc.as<int32_t>(); A.path_len = pl.as<int32_t>(); A.n_cigar = nc.as<int32_t>();
+  A.ends = en.as<int4>();
+  A.cigar = cg.as<uint32_t>(); A.cigar_cap = cap;
+  if (!rc) {
+    chk(hipEventRecord(c->ev[0], c->stream), "event");
+    chk(launch_sw(A, c->d_counter.as<unsigned long long>(), blocks, c->stream), "k_sw");
+    chk(hipEventRecord(c->ev[1], c->stream), "event");
+  }
+  std::vector<uint32_t> hc;
+  if (!rc) {
+    hc.resize((uint64_t)n * cap);
+    chk(hipMemcpyAsync(score, sc.p, n * 4, hipMemcpyDeviceToHost, c->stream), "D2H score");
+    chk(hipMemcpyAsync(path_len, pl.p, n * 4, hipMemcpyDeviceToHost, c->stream), "D2H path_len");
+    chk(hipMemcpyAsync(n_cigar, nc.p, n * 4, hipMemcpyDeviceToHost, c->stream), "D2H n_cigar");
+    chk(hipMemcpyAsync(ends, en.p, n * 16, hipMemcpyDeviceToHost, c->stream), "D2H ends");
+    chk(hipMemcpyAsync(hc.data(), cg.p, (uint64_t)n * cap * 4, hipMemcpyDeviceToHost, c->stream), "D2H cigar");
+    chk(hipStreamSynchronize(c->stream), "sync");
+    float ms = 0;
+    if (!rc && hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->stats.ms_sw = ms;
+  }
+  release();
+  if (rc) return rc;
+  int64_t tot = 0;
+  for (int64_t p = 0; p < n; ++p) tot += n_cigar[p];
+  uint32_t *o = (uint32_t *)malloc(std::max<int64_t>(tot, 1) * 4);
+  if (!o) return fail(IBWA_EINVAL, "out of host memory");
+  int64_t q = 0;
+  for (int64_t p = 0; p < n; ++p) {
+    memcpy(o + q, hc.data() + (uint64_t)p * cap, (size_t)n_cigar[p] * 4);
+    q += n_cigar[p];
+  }
+  *cigar = o;
+  if (n_cigar_total) *n_cigar_total = tot;
+  return 0;
+}
+
 int ibwa_occ4(ibwa_ctx_t *c, int strand, int64_t n, const uint32_t *k, uint32_t *cnt) {
   if (!c->loaded[strand]) return fail(IBWA_ENOINDEX, "index not loaded");
   HIPCHK(hipSetDevice(c->device));

@@ -29,7 +29,7 @@ class RunStats(c.Structure):
     _fields_ = [("ms_width", c.c_double), ("ms_search", c.c_double), ("ms_retry", c.c_double),
                 ("ms_total", c.c_double), ("n_retry", c.c_int64), ("n_launch_width", c.c_int64),
                 ("n_launch_search", c.c_int64), ("path", c.c_int), ("kmer_k", c.c_int),
-                ("n_stack_overflow", c.c_int64), ("n_aln_overflow", c.c_int64), ("n_heavy", c.c_int64)]
+                ("n_stack_overflow", c.c_int64), ("n_aln_overflow", c.c_int64), ("n_heavy", c.c_int64), ("ms_sw", c.c_double)]
 
 
 assert c.sizeof(GapOpt) == 64
@@ -63,6 +63,10 @@ CAPI = {
     "ibwa_ctx_bwt_info": (_i, [_vp, _i, c.POINTER(_u32), c.POINTER(_u32), c.POINTER(_u64)]),
     "ibwa_ctx_export_bwt": (_i, [_vp, _i, _vp, _u64]),
     "ibwa_ctx_export_sa": (_i, [_vp, _i, _vp, _u64]),
+    "ibwa_sw_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, c.POINTER(c.c_void_p),
+                           c.POINTER(_i64)]),
+    "ibwa_sw_core_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
+                                c.POINTER(c.c_void_p)]),
 }
 
 
@@ -198,6 +202,74 @@ class Engine:
         n = self.bwt_info(strand)[1][3]
         out = np.zeros((n + intv) // intv, dtype=np.uint32)
         _chk(lib().ibwa_ctx_export_sa(self.h, strand, out.ctypes.data, out.size))
+        return out
+
+    def sw(self, refs, reads):
+        """Batched aln_local_core (stdaln.c:529) over code arrays.  Returns a list of
+        (score, path_len, start (i, j) | None, end (i, j) | None, cigar str | None)."""
+        n = len(refs)
+        o1 = np.zeros(n, np.uint64)
+        o2 = np.zeros(n, np.uint64)
+        l1 = np.array([len(x) for x in refs], np.uint32)
+        l2 = np.array([len(x) for x in reads], np.uint32)
+        if n:
+            o1[1:] = np.cumsum(l1[:-1])
+            o2[1:] = np.cumsum(l2[:-1])
+        s1 = np.concatenate([np.asarray(x, np.uint8) for x in refs] + [np.zeros(1, np.uint8)])
+        s2 = np.concatenate([np.asarray(x, np.uint8) for x in reads] + [np.zeros(1, np.uint8)])
+        score = np.zeros(n, np.int32)
+        plen = np.zeros(n, np.int32)
+        ends = np.zeros((n, 4), np.int32)
+        ncig = np.zeros(n, np.int32)
+        ptr = c.c_void_p()
+        tot = c.c_int64()
+        _chk(lib().ibwa_sw_batch(self.h, n, s1.ctypes.data, o1.ctypes.data, l1.ctypes.data, s2.ctypes.data,
+                                 o2.ctypes.data, l2.ctypes.data, score.ctypes.data, plen.ctypes.data,
+                                 ends.ctypes.data, ncig.ctypes.data, c.byref(ptr), c.byref(tot)))
+        cig = np.frombuffer(c.string_at(ptr.value, 4 * max(tot.value, 0)), dtype=np.uint32).copy()
+        lib().ibwa_free(ptr)
+        out, q = [], 0
+        for p in range(n):
+            if score[p] >= 0 and plen[p] > 0:
+                cs = "".join(f"{x >> 4}{'MIDS'[x & 0xf]}" for x in cig[q:q + ncig[p]])
+                out.append((int(score[p]), int(plen[p]), (int(ends[p, 0]), int(ends[p, 1])),
+                            (int(ends[p, 2]), int(ends[p, 3])), cs))
+            else:
+                out.append((int(score[p]), int(plen[p]), None, None, None))
+            q += ncig[p]
+        return out
+
+    def sw_core(self, reads, windows, reglen, beg, l_pac):
+        """bwa_sw_core (bwasw.c:29-112) per mate rescue, batched.  Returns a list of
+        None (rejected) or (beg, [bwa_cigar_t ...], cnt)."""
+        n = len(reads)
+        off = np.zeros(n, np.uint64)
+        roff = np.zeros(n, np.uint64)
+        ln = np.array([len(x) for x in reads], np.uint32)
+        rl = np.array([len(x) for x in windows], np.uint32)
+        if n:
+            off[1:] = np.cumsum(ln[:-1])
+            roff[1:] = np.cumsum(rl[:-1])
+        s = np.concatenate([np.asarray(x, np.uint8) for x in reads] + [np.zeros(1, np.uint8)])
+        r = np.concatenate([np.asarray(x, np.uint8) for x in windows] + [np.zeros(1, np.uint8)])
+        rg = np.ascontiguousarray(reglen, np.int32)
+        bg = np.ascontiguousarray(beg, np.int64).copy()
+        nc = np.zeros(n, np.int32)
+        cnt = np.zeros(n, np.uint32)
+        ptr = c.c_void_p()
+        _chk(lib().ibwa_sw_core_batch(self.h, n, s.ctypes.data, off.ctypes.data, ln.ctypes.data, r.ctypes.data,
+                                      roff.ctypes.data, rl.ctypes.data, rg.ctypes.data, bg.ctypes.data, int(l_pac),
+                                      nc.ctypes.data, cnt.ctypes.data, c.byref(ptr)))
+        tot = int(nc.sum())
+        cig = np.frombuffer(c.string_at(ptr.value, 4 * tot), dtype=np.uint32).copy() if tot else np.zeros(0, np.uint32)
+        lib().ibwa_free(ptr)
+        out, q = [], 0
+        for p in range(n):
+            if nc[p]:
+                out.append((int(bg[p]), [int(x) for x in cig[q:q + nc[p]]], int(cnt[p])))
+            else:
+                out.append(None)
+            q += nc[p]
         return out
 
     def occ4(self, strand, ks):

@@ -119,6 +119,7 @@ typedef struct {
 	int64_t n_stack_overflow;  /* first-pass reads whose stack did not fit (re-run) */
 	int64_t n_aln_overflow;    /* first-pass reads whose hits did not fit (re-run) */
 	int64_t n_heavy;           /* first-pass reads over the iteration budget (re-run) */
+	double ms_sw;              /* last ibwa_sw_batch kernel time */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 
@@ -152,6 +153,22 @@ int ibwa_ctx_export_bwt(const ibwa_ctx_t *ctx, int strand, uint32_t *words, uint
 /* Export the sampled SA kept by ibwa_ctx_build_index: out[(n+intv)/intv] with out[0] = (u32)-1
  * (bwt.c:56-66); entries 1.. are what bwt_dump_sa writes. */
 int ibwa_ctx_export_sa(const ibwa_ctx_t *ctx, int strand, uint32_t *out, uint64_t cap);
+
+/*
+ * Batched Smith-Waterman with path: aln_local_core (stdaln.c:529-760) with
+ * aln_param_bwa and _thres = 1, as bwa_sw_core (bwasw.c:51) calls it for each
+ * mate rescue, plus aln_path2cigar32 (stdaln.c:1010-1040).  Pair p aligns
+ * seq1 = ref[off1[p] .. +len1[p]) (the reference window) against seq2 =
+ * qry[off2[p] .. +len2[p]) (the read), codes 0..4.  Per pair: score (-1 if a
+ * length is 0), path_len, ends[4p..4p+3] = start i, start j, end i, end j
+ * (1-based, path[path_len-1] and path[0]), n_cigar; *cigar = malloc'd
+ * concatenation of all CIGARs (len << 4 | op, op 0 M, 1 I, 2 D; ibwa_free).
+ * Requires min(len1, len2) * 11 <= 32000 (the reference's score rebasing is
+ * then unreachable); IBWA_EINVAL otherwise.
+ */
+int ibwa_sw_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
+                  const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int32_t *score,
+                  int32_t *path_len, int32_t *ends, int32_t *n_cigar, uint32_t **cigar, int64_t *n_cigar_total);
 
 /* Device Occ KAT: bwt_occ4 (bwt.c:157) for n positions k[] on strand s -> cnt[4*n] */
 int ibwa_occ4(ibwa_ctx_t *ctx, int strand, int64_t n, const uint32_t *k, uint32_t *cnt);

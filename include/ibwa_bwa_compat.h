@@ -100,6 +100,21 @@ void bwa_cal_sa_reg_gap(int tid, ibwa_ref_bwt_t *const bwt[2], int n_seqs, ibwa_
                         const ibwa_gap_opt_t *opt);
 #endif
 
+/*
+ * bwa_sw_core (bwasw.c:29-112) for n mate rescues at once -- the per-rescue
+ * body that bwa_paired_sw_thread (bwasw.c:145-268) calls, with the alignment
+ * itself batched on the GPU (ibwa_sw_batch).  Pair p: read codes
+ * seq[off[p] .. +len[p]); the reference window already extracted by
+ * dbset_extract_sequence (bwasw.c:46): ref[ref_off[p] .. +ref_len[p]), its
+ * requested length reglen[p] and start beg[p] (in/out, as *beg), l_pac the
+ * packed reference length.  Out: n_cigar[p] (0 = rejected, the reference's
+ * NULL), cnt[p] = n_mm << 16 | n_gapo << 8 | n_gape, *cigar = malloc'd
+ * concatenation of the bwa_cigar_t arrays (op << 29 | len, soft clips op 3).
+ */
+int ibwa_sw_core_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *seq, const uint64_t *off, const uint32_t *len,
+                       const uint8_t *ref, const uint64_t *ref_off, const uint32_t *ref_len, const int32_t *reglen,
+                       int64_t *beg, int64_t l_pac, int32_t *n_cigar, uint32_t *cnt, uint32_t **cigar);
+
 #ifdef __cplusplus
 }
 #endif

@@ -80,10 +80,11 @@ def lib():
         L.or_set_stats.argtypes = [c.c_void_p]
         L.or_exact_touches.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p, c.c_void_p,
                                        c.c_int, c.c_int, c.c_void_p]
-        if hasattr(L, "or_aln_local_core"):
-            L.or_aln_local_core.restype = c.c_int
-            L.or_aln_local_core.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
-                                            c.POINTER(c.c_int), c.c_int, c.c_void_p]
+        L.or_aln_local_core.restype = c.c_int
+        L.or_aln_local_core.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
+                                        c.POINTER(c.c_int), c.c_int, c.c_void_p]
+        L.or_path2cigar32.restype = c.c_int
+        L.or_path2cigar32.argtypes = [c.c_void_p, c.c_int, c.c_void_p]
         _lib = L
     return _lib
 
@@ -282,3 +283,92 @@ def sai_bytes(opt, n_aln, alns, batch=0x40000):
 def sai_body_equal(a, b):
     """Compare .sai files, masking header bytes 52..55 (gap_opt_t.n_threads)."""
     return a[:52] == b[:52] and a[56:64] == b[56:64] and a[64:] == b[64:]
+
+
+class PathT(ctypes.Structure):
+    """path_t (stdaln.h:97-101)."""
+    _fields_ = [("i", ctypes.c_int), ("j", ctypes.c_int), ("ctype", ctypes.c_ubyte)]
+
+
+def sw_local(ref_codes, read_codes):
+    """aln_local_core(ref, read, aln_param_bwa, thres 1) restated (stdaln.c:529) + path2cigar32.
+    Returns (score, path_len, (start_i, start_j), (end_i, end_j), cigar string) -- the fields of
+    tests/golden/sw_vectors.tsv; start/end/cigar are None without a path."""
+    L = lib()
+    a = np.ascontiguousarray(ref_codes, dtype=np.uint8)
+    b = np.ascontiguousarray(read_codes, dtype=np.uint8)
+    path = (PathT * (a.size + b.size + 2))()
+    pl = ctypes.c_int(0)
+    sc = L.or_aln_local_core(a.ctypes.data, a.size, b.ctypes.data, b.size, path, ctypes.byref(pl), 1, None)
+    if sc < 0 or pl.value == 0:
+        return sc, pl.value, None, None, None
+    cig = (ctypes.c_uint32 * (pl.value + 1))()
+    n = L.or_path2cigar32(path, pl.value, cig)
+    cs = "".join(f"{cig[k] >> 4}{'MIDS'[cig[k] & 0xf]}" for k in range(n))
+    return sc, pl.value, (path[pl.value - 1].i, path[pl.value - 1].j), (path[0].i, path[0].j), cs
+
+
+def read_sw_vectors(path):
+    """tests/golden/sw_vectors.tsv -> list of (ref, read, score, path_len, start, end, cigar)."""
+    out = []
+    for line in open(path):
+        if line.startswith("#"):
+            continue
+        f = line.rstrip("\n").split("\t")
+        start = tuple(map(int, f[4].split(","))) if f[4] else None
+        end = tuple(map(int, f[5].split(","))) if f[5] else None
+        out.append((f[0], f[1], int(f[2]), int(f[3]), start, end, f[6] or None))
+    return out
+
+
+def nt4(s):
+    """nst_nt4_table (bntseq.c:39-56) over a str."""
+    return _NT4[np.frombuffer(s.encode(), dtype=np.uint8)] if s else np.zeros(0, np.uint8)
+
+
+def sw_core(read, window, reglen, beg, l_pac):
+    """bwa_sw_core (bwasw.c:29-112) restated over sw_local: None when rejected, else
+    (beg, [bwa_cigar_t op << 29 | len ...], cnt = n_mm << 16 | n_gapo << 8 | n_gape)."""
+    read = np.asarray(read, np.uint8)
+    window = np.asarray(window, np.uint8)
+    L = read.size
+    if reglen < 20 or l_pac - beg < L:
+        return None
+    x = int((read >= 4).sum())
+    if L == 0 or np.float32(x) / np.float32(L) >= np.float32(0.25) or L - x < 20:
+        return None
+    score, pl, start, end, cig = sw_local(window, read)
+    if score < 0 or not cig:
+        return None
+    import re
+    ops = [(int(n), "MIDS".index(t)) for n, t in re.findall(r"(\d+)([MIDS])", cig)]
+    xx = sum(n for n, t in ops if t in (0, 2))
+    yy = sum(n for n, t in ops if t in (0, 1))
+    if xx < 20 or yy < 20:
+        return None
+    c = [t << 29 | n for n, t in ops]
+    beg += (start[0] or 1) - 1
+    st = (start[1] or 1) - 1
+    if st:
+        c.insert(0, 3 << 29 | st)
+    if end[1] < L:
+        c.append(3 << 29 | (L - end[1]))
+    n_mm = n_gapo = n_gape = 0
+    rx = start[0] - 1 if start[0] else 0
+    ry = start[1] - 1 if start[1] else 0
+    for v in c:
+        t, n = v >> 29, v & 0x1FFFFFFF
+        if t == 0:
+            a, b = window[rx:rx + n], read[ry:ry + n]
+            n_mm += int(((a < 4) & (b < 4) & (a != b)).sum())
+            rx += n
+            ry += n
+        elif t == 2:
+            rx += n
+            n_gapo += 1
+            n_gape += n - 1
+        elif t == 1:
+            ry += n
+            n_gapo += 1
+            n_gape += n - 1
+    return beg, c, n_mm << 16 | n_gapo << 8 | n_gape

@@ -683,3 +683,249 @@ int64_t or_cal_sa_reg_gap(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_
 	pthread_mutex_destroy(&B.lock);
 	return tot;
 }
+
+/* ======================================================================
+ * Smith-Waterman refinement, restating
+ * stdaln.c with aln_param_bwa = {gap_open 26, gap_ext 9, gap_end 5,
+ * aln_sm_maq, row 5, band 50} (stdaln.c:206-212, :227).  The 32000-score
+ * rebasing of the local passes (stdaln.c:581-598, :655-668) is omitted: it is
+ * unreachable while min(len1, len2) * 11 <= 32000, which or_aln_local_core
+ * requires (returns -2 otherwise).
+ * ====================================================================== */
+#define SW_Q 26
+#define SW_R 9
+#define SW_GAP_END 5
+#define SW_BAND 50
+#define SW_MAXSC 11
+#define SW_NEG_INF (-1073741823)
+#define SW_M 0
+#define SW_I 1
+#define SW_D 2
+static const int sw_mat[25] = { /* aln_sm_maq (stdaln.c:206-212) */
+	 11, -19, -19, -19, -13,
+	-19,  11, -19, -19, -13,
+	-19, -19,  11, -19, -13,
+	-19, -19, -19,  11, -13,
+	-13, -13, -13, -13, -13 };
+
+typedef struct { int M, I, D; } sw_cell_t;
+
+/* set_M / set_I / set_D (stdaln.c:271-319): pick the predecessor state, ties as there */
+static inline int sw_from_diag(const sw_cell_t *p, int sc, unsigned char *t)
+{
+	if (p->M >= p->I) {
+		if (p->M >= p->D) { *t = SW_M; return p->M + sc; }
+		*t = SW_D; return p->D + sc;
+	}
+	if (p->I > p->D) { *t = SW_I; return p->I + sc; }
+	*t = SW_D; return p->D + sc;
+}
+/* gap state `g` (I or D value of p) opened from p->M or extended; ext = gap_ext or gap_end */
+static inline int sw_gap(int pM, int pg, int ext, unsigned char *t)
+{
+	if (pM - SW_Q > pg) { *t = SW_M; return pM - SW_Q - ext; }
+	*t = 1; return pg - ext; /* caller maps 1 to its own state */
+}
+
+/* aln_global_core (stdaln.c:345-525): banded global DP, M/I/D, full traceback.
+ * seq1 is the i axis (FROM_D steps i), seq2 the j axis (FROM_I steps j). */
+int or_aln_global_core(const uint8_t *seq1, int len1, const uint8_t *seq2, int len2,
+                       int band_width, int gap_end, or_path_t *path, int *path_len)
+{
+	int b1, b2, i, j, end, tmp_end, n;
+	sw_cell_t *curr, *last, *tswap;
+	unsigned char *tM, *tI, *tD; /* traceback per (j, i), full matrix */
+	const int W = len1 + 1;
+	const int endI = gap_end >= 0 ? gap_end : SW_R; /* set_end_I/D fall back to set_I/D */
+	int best, ctype, type;
+	if (len1 == 0 || len2 == 0) { *path_len = 0; return 0; }
+	if (len1 > len2) { b1 = len1 - len2 + band_width; b2 = band_width; }
+	else { b1 = band_width; b2 = len2 - len1 + band_width; }
+	if (b1 > len1) b1 = len1;
+	if (b2 > len2) b2 = len2;
+	tM = (unsigned char*)calloc((size_t)(len2 + 1) * W, 1);
+	tI = (unsigned char*)calloc((size_t)(len2 + 1) * W, 1);
+	tD = (unsigned char*)calloc((size_t)(len2 + 1) * W, 1);
+	curr = (sw_cell_t*)malloc(sizeof(sw_cell_t) * W);
+	last = (sw_cell_t*)malloc(sizeof(sw_cell_t) * W);
+#define CM(i_, p_, sc_) curr[i_].M = sw_from_diag(p_, sc_, &tM[(size_t)j * W + (i_)])
+#define CI(i_, p_, e_) do { unsigned char t_; curr[i_].I = sw_gap((p_)->M, (p_)->I, e_, &t_); tI[(size_t)j * W + (i_)] = t_ == SW_M ? SW_M : SW_I; } while (0)
+#define CD(i_, p_, e_) do { unsigned char t_; curr[i_].D = sw_gap((p_)->M, (p_)->D, e_, &t_); tD[(size_t)j * W + (i_)] = t_ == SW_M ? SW_M : SW_D; } while (0)
+#define INF(c_) ((c_).M = (c_).I = (c_).D = SW_NEG_INF)
+#define SC(i_) sw_mat[seq2[j - 1] * 5 + seq1[(i_) - 1]]
+	/* row 0 */
+	j = 0;
+	INF(curr[0]); curr[0].M = 0;
+	for (i = 1; i < b1; ++i) { INF(curr[i]); CD(i, &curr[i - 1], endI); }
+	tswap = curr; curr = last; last = tswap;
+	/* part 1: rows whose band starts at column 0 */
+	tmp_end = b2 < len2 ? b2 : len2 - 1;
+	for (j = 1; j <= tmp_end; ++j) {
+		INF(curr[0]); CI(0, &last[0], endI);
+		end = (j + b1 <= len1 + 1) ? j + b1 - 1 : len1;
+		for (i = 1; i != end; ++i) { CM(i, &last[i - 1], SC(i)); CI(i, &last[i], SW_R); CD(i, &curr[i - 1], SW_R); }
+		CM(i, &last[i - 1], SC(i)); CD(i, &curr[i - 1], SW_R);
+		if (j + b1 - 1 > len1) CI(i, &last[i], endI); else curr[i].I = SW_NEG_INF;
+		tswap = curr; curr = last; last = tswap;
+	}
+	if (j == len2 && b2 != len2 - 1) { /* last row of part 1: end-gap deletions */
+		INF(curr[0]); CI(0, &last[0], endI);
+		end = (j + b1 <= len1 + 1) ? j + b1 - 1 : len1;
+		for (i = 1; i != end; ++i) { CM(i, &last[i - 1], SC(i)); CI(i, &last[i], SW_R); CD(i, &curr[i - 1], endI); }
+		CM(i, &last[i - 1], SC(i)); CD(i, &curr[i - 1], endI);
+		if (j + b1 - 1 > len1) CI(i, &last[i], endI); else curr[i].I = SW_NEG_INF;
+		tswap = curr; curr = last; last = tswap;
+		++j;
+	}
+	/* part 2: bands strictly inside */
+	for (; j <= len2 - b2 + 1; ++j) {
+		INF(curr[j - b2]);
+		end = j + b1 - 1;
+		for (i = j - b2 + 1; i != end; ++i) { CM(i, &last[i - 1], SC(i)); CI(i, &last[i], SW_R); CD(i, &curr[i - 1], SW_R); }
+		CM(i, &last[i - 1], SC(i)); CD(i, &curr[i - 1], SW_R);
+		curr[i].I = SW_NEG_INF;
+		tswap = curr; curr = last; last = tswap;
+	}
+	/* part 3: bands reaching the last column */
+	for (; j < len2; ++j) {
+		INF(curr[j - b2]);
+		for (i = j - b2 + 1; i < len1; ++i) { CM(i, &last[i - 1], SC(i)); CI(i, &last[i], SW_R); CD(i, &curr[i - 1], SW_R); }
+		CM(i, &last[len1 - 1], SC(i)); CI(i, &last[i], endI); CD(i, &curr[i - 1], SW_R);
+		tswap = curr; curr = last; last = tswap;
+	}
+	if (j == len2) { /* last row */
+		INF(curr[j - b2]);
+		for (i = j - b2 + 1; i < len1; ++i) { CM(i, &last[i - 1], SC(i)); CI(i, &last[i], SW_R); CD(i, &curr[i - 1], endI); }
+		CM(i, &last[len1 - 1], SC(i)); CI(i, &last[i], endI); CD(i, &curr[i - 1], endI);
+		tswap = curr; curr = last; last = tswap;
+	}
+#undef CM
+#undef CI
+#undef CD
+#undef INF
+#undef SC
+	/* traceback from (len1, len2) (stdaln.c:487-514) */
+	i = len1; j = len2;
+	best = last[len1].M; type = tM[(size_t)j * W + i]; ctype = SW_M;
+	if (last[len1].I > best) { best = last[len1].I; type = tI[(size_t)j * W + i]; ctype = SW_I; }
+	if (last[len1].D > best) { best = last[len1].D; type = tD[(size_t)j * W + i]; ctype = SW_D; }
+	n = 0;
+	path[n].ctype = (unsigned char)ctype; path[n].i = i; path[n].j = j; ++n;
+	do {
+		if (ctype == SW_M) { --i; --j; } else if (ctype == SW_I) --j; else --i;
+		ctype = type;
+		type = ctype == SW_M ? tM[(size_t)j * W + i] : ctype == SW_I ? tI[(size_t)j * W + i] : tD[(size_t)j * W + i];
+		path[n].ctype = (unsigned char)ctype; path[n].i = i; path[n].j = j; ++n;
+	} while (i || j);
+	*path_len = n - 1;
+	free(tM); free(tI); free(tD); free(curr); free(last);
+	return best;
+}
+
+/* aln_local_core (stdaln.c:529-760) with _thres > 0 and no sub-optimal score:
+ * forward local pass (packed h<<16|e per seq1 column), banded reverse pass for
+ * the start, then the path by aln_global_core with band doubling from 50. */
+int or_aln_local_core(const uint8_t *seq1, int len1, const uint8_t *seq2, int len2,
+                      or_path_t *path, int *path_len, int thres, int *subo)
+{
+	const int q = SW_Q, r = SW_R, qr = SW_Q + SW_R, qr_shift = (qr + 1) << 16;
+	int32_t *eh;
+	int i, j, h, e, f, last_h, score_f = 0, score_r, score_g, end_i = 0, end_j = 0, start_i, start_j, start, end;
+	(void)subo;
+	if (len1 == 0 || len2 == 0) return -1;
+	if ((len1 < len2 ? len1 : len2) * SW_MAXSC > 32000) return -2; /* rebasing not restated */
+	if (thres < 0) thres = -thres;
+	eh = (int32_t*)calloc(len1 + 2, sizeof(int32_t));
+	/* forward pass: row j over seq2, column i over seq1; eh[i-1] = H[j-1][i-1] << 16 | E[j-1][i] */
+	for (j = 1; j <= len2; ++j) {
+		const int *row = sw_mat + seq2[j - 1] * 5;
+		last_h = f = 0;
+		for (i = 1; i <= len1; ++i) {
+			h = (eh[i - 1] >> 16) + row[seq1[i - 1]];
+			if (h < 0) h = 0;
+			if (last_h > 0) { /* F: gap along seq1, only after a positive H */
+				f = (f > last_h - q) ? f - r : last_h - qr;
+				if (h < f) h = f;
+			}
+			if (eh[i] >= qr_shift) { /* E: gap along seq2, only under an H above q+r */
+				const int above = eh[i] >> 16, e_old = eh[i - 1] & 0xffff;
+				e = (e_old > above - q) ? e_old - r : above - qr;
+				if (h < e) h = e;
+				eh[i - 1] = (int32_t)((uint32_t)last_h << 16 | (uint32_t)e);
+			} else eh[i - 1] = (int32_t)((uint32_t)last_h << 16);
+			last_h = h;
+			if (score_f < h) { score_f = h; end_i = i; end_j = j; } /* first maximum in row-major order */
+		}
+		eh[len1] = (int32_t)((uint32_t)last_h << 16);
+	}
+	if (score_f < thres) { *path_len = 0; free(eh); return score_f; }
+	/* reverse pass from (end_i, end_j) towards the start, in an adaptive band */
+	for (i = end_i; i >= 0; --i) eh[i] = 0;
+	if (end_i == 0 || end_j == 0) { free(eh); return score_f; }
+	score_r = sw_mat[seq1[end_i - 1] * 5 + seq2[end_j - 1]];
+	start_i = end_i; start_j = end_j;
+	eh[end_i] = (int32_t)((uint32_t)(qr + score_r) << 16);
+	start = end_i - 1;
+	end = end_i - 3;
+	if (end <= 0) end = 0;
+	for (j = end_j - 1; j != 0; --j) {
+		const int *row = sw_mat + seq2[j - 1] * 5;
+		last_h = f = 0;
+		for (i = start; i != end; --i) { /* eh[i+1] = H[j+1][i+1] << 16 | E, eh[i] = H above */
+			h = (eh[i + 1] >> 16) + row[seq1[i - 1]];
+			if (h < 0) h = 0;
+			if (last_h > 0) {
+				f = (f > last_h - q) ? f - r : last_h - qr;
+				if (h < f) h = f;
+			}
+			{
+				const int above = eh[i] >> 16, e_old = eh[i + 1] & 0xffff;
+				e = (e_old > above - q) ? e_old - r : above - qr;
+				if (e < 0) e = 0;
+				if (h < e) h = e;
+			}
+			eh[i + 1] = (int32_t)((uint32_t)last_h << 16 | (uint32_t)e);
+			last_h = h;
+			if (score_r < h) {
+				score_r = h; start_i = i; start_j = j;
+				if (score_r - qr == score_f) { j = 1; break; } /* the start is found */
+			}
+		}
+		eh[i + 1] = (int32_t)((uint32_t)last_h << 16);
+		if ((eh[start] >> 16) <= qr) --start;
+		if (start <= 0) start = 0;
+		end = start_i - (start_j - j) - (score_r + (start_j - j) * SW_MAXSC) / r - 1;
+		if (end <= 0) end = 0;
+	}
+	score_r -= qr;
+	/* path: banded global alignment of [start_i, end_i] x [start_j, end_j], band doubling */
+	{
+		const int span = ((end_i - start_i > end_j - start_j) ? end_i - start_i : end_j - start_j) + 1;
+		int bw;
+		score_g = 0;
+		for (bw = SW_BAND;; bw <<= 1) {
+			score_g = or_aln_global_core(seq1 + start_i - 1, end_i - start_i + 1, seq2 + start_j - 1,
+			                             end_j - start_j + 1, bw, -1, path, path_len);
+			if (score_g == score_r || score_f == score_g) break;
+			if (bw > span) break;
+		}
+		if (score_r > score_g && score_f > score_g) score_f = -1; /* the reference's "potential bug" branch */
+		else score_f = score_g;
+		for (i = 0; i < *path_len; ++i) { path[i].i += start_i - 1; path[i].j += start_j - 1; }
+	}
+	free(eh);
+	return score_f;
+}
+
+/* aln_path2cigar32 (stdaln.c:1010-1040): run-length ops from the start of the path */
+int or_path2cigar32(const or_path_t *path, int path_len, uint32_t *cigar)
+{
+	int i, n;
+	if (path_len == 0) return 0;
+	cigar[0] = 1u << 4 | path[path_len - 1].ctype;
+	for (i = path_len - 2, n = 0; i >= 0; --i) {
+		if (path[i].ctype == (cigar[n] & 0xf)) cigar[n] += 1u << 4;
+		else cigar[++n] = 1u << 4 | path[i].ctype;
+	}
+	return n + 1;
+}

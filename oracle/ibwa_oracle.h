@@ -89,6 +89,7 @@ int or_aln_local_core(const uint8_t *seq1, int len1, const uint8_t *seq2, int le
                       or_path_t *path, int *path_len, int thres, int *subo);
 int or_aln_global_core(const uint8_t *seq1, int len1, const uint8_t *seq2, int len2,
                        int band_width, int gap_end, or_path_t *path, int *path_len);
+int or_path2cigar32(const or_path_t *path, int path_len, uint32_t *cigar);
 
 #ifdef __cplusplus
 }

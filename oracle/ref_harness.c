@@ -12,6 +12,7 @@
  *   ibwa_ref aln [opts] <prefix> <in.fq>   -> bwa_aln     (bwtaln.c:243)
  *   ibwa_ref occ4 <prefix.bwt> k...        -> bwt_occ4    (bwt.c:157)  (KAT)
  *   ibwa_ref sw <ref_seq> <read_seq>       -> aln_local_core (stdaln.c:529)
+ *   ibwa_ref swf <pairs.tsv>               -> aln_local_core over a file of pairs
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -67,6 +68,42 @@ static int cmd_sw(int argc, char *argv[])
 	return 0;
 }
 
+/* swf <pairs.tsv> : one "ref<TAB>read" (ACGTN strings) per line; prints one line of
+ * score, path_len, start i,j, end i,j, CIGAR per input line (empty fields when no path) */
+static int cmd_swf(int argc, char *argv[])
+{
+	static char line[1 << 16];
+	FILE *fp;
+	AlnParam ap = aln_param_bwa;
+	if (argc < 2 || !(fp = fopen(argv[1], "r"))) return 1;
+	while (fgets(line, sizeof line, fp)) {
+		char *t = strchr(line, '\t'), *r2;
+		int l1, l2, i, path_len = 0, score, n_cigar = 0;
+		unsigned char *s1, *s2;
+		path_t *path;
+		if (!t) continue;
+		*t = 0; r2 = t + 1;
+		r2[strcspn(r2, "\r\n")] = 0;
+		l1 = strlen(line); l2 = strlen(r2);
+		s1 = (unsigned char*)malloc(l1 + 1); s2 = (unsigned char*)malloc(l2 + 1);
+		for (i = 0; i < l1; ++i) s1[i] = nst_nt4_table[(int)line[i]];
+		for (i = 0; i < l2; ++i) s2[i] = nst_nt4_table[(int)r2[i]];
+		path = (path_t*)calloc(l1 + l2 + 2, sizeof(path_t));
+		score = aln_local_core(s1, l1, s2, l2, &ap, path, &path_len, 1, 0);
+		printf("%d\t%d", score, path_len);
+		if (score >= 0 && path_len > 0) {
+			uint32_t *cigar = aln_path2cigar32(path, path_len, &n_cigar);
+			printf("\t%d,%d\t%d,%d\t", path[path_len-1].i, path[path_len-1].j, path[0].i, path[0].j);
+			for (i = 0; i < n_cigar; ++i) printf("%u%c", cigar[i]>>4, "MIDS"[cigar[i]&0xf]);
+			free(cigar);
+		} else printf("\t\t\t");
+		printf("\n");
+		free(path); free(s1); free(s2);
+	}
+	fclose(fp);
+	return 0;
+}
+
 int main(int argc, char *argv[])
 {
 	if (argc < 2) {
@@ -77,6 +114,7 @@ int main(int argc, char *argv[])
 	if (strcmp(argv[1], "aln") == 0) return bwa_aln(argc - 1, argv + 1);
 	if (strcmp(argv[1], "occ4") == 0) return cmd_occ4(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sw") == 0) return cmd_sw(argc - 1, argv + 1);
+	if (strcmp(argv[1], "swf") == 0) return cmd_swf(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }

@@ -49,3 +49,15 @@ def test_touch_counts_positive(golden_dir, sai_manifest, oracle_index):
     _, _, t = oracle.cal_sa_reg_gap(b0, b1, seqs, offs, lens, opt, touches=True)
     # -n 0 on 100 bp: 2 full + 2 seed widths (264 steps) plus exact tails
     assert 250 < t.mean() < 500
+
+
+def test_sw_restatement_matches_reference_vectors(golden_dir):
+    """aln_local_core restated (oracle) == the reference's outputs on 2 520 pairs."""
+    vecs = oracle.read_sw_vectors(os.path.join(golden_dir, "sw_vectors.tsv"))
+    assert len(vecs) > 2000
+    bad = []
+    for k, (ref, rd, score, pl, start, end, cig) in enumerate(vecs):
+        got = oracle.sw_local(oracle.nt4(ref), oracle.nt4(rd))
+        if got != (score, pl, start, end, cig):
+            bad.append((k, got, (score, pl, start, end, cig)))
+    assert not bad, bad[:5]
