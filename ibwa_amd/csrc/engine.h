@@ -110,7 +110,7 @@ struct SwArgs {
   const uint64_t *off1, *off2;
   const uint32_t *len1, *len2;
   int64_t n;
-  int max_len1;                   // sizes the per-lane scratch
+  int max_len1, max_len2;         // size the per-lane scratch
   uint32_t *scratch;              // sw_words_per_lane(max_len1) u32 per lane, lane-minor per wave
   uint64_t words_per_lane;
   uint8_t *tb;                    // sw_tb_per_lane bytes per lane, lane-minor per wave
@@ -119,9 +119,10 @@ struct SwArgs {
   int4 *ends;                     // start_i, start_j, end_i, end_j (1-based, stdaln path_t)
   uint32_t *cigar;                // cigar_cap per pair, aln_path2cigar32 encoding (len << 4 | op)
   int cigar_cap;
+  int stop_after;                 // diagnostics: 1 after the forward pass, 2 after the reverse pass
 };
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st);
-uint64_t sw_words_per_lane(int max_len1);
+uint64_t sw_words_per_lane(int max_len1, int max_len2);
 uint64_t sw_tb_per_lane(int max_len1, int max_len2);
 
 hipError_t build_kmer_table(const IndexView &ix, int K, uint2 *table, uint2 *tmp, hipStream_t st);

@@ -112,6 +112,7 @@ struct ibwa_ctx {
   bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
   bool verbose = getenv("IBWA_VERBOSE") != nullptr;
   bool prof_phases = getenv("IBWA_PROF_PHASES") != nullptr;  // diagnostics kernel variant
+  int sw_stop_after = getenv("IBWA_SW_STOP") ? atoi(getenv("IBWA_SW_STOP")) : 0;  // diagnostics
   DBuf d_prof;
   unsigned long long stream_len = 0;
   std::vector<uint64_t> h_aoff;
@@ -946,10 +947,11 @@ int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *
   auto release = [&]() {
     for (DBuf *b : {&s1, &s2, &o1, &o2, &l1, &l2, &sc, &pl, &nc, &en, &cg, &scr, &tbb}) b->release();
   };
-  const uint64_t wpl = sw_words_per_lane(max1), tpl = sw_tb_per_lane(max1, max2);
+  const uint64_t wpl = sw_words_per_lane(max1, max2), tpl = sw_tb_per_lane(max1, max2);
   const uint64_t per_wave = (wpl * 4 + tpl) * 64;
-  // a persistent grid within ~8 GiB of DP scratch
-  const int64_t waves = std::max<int64_t>(1, std::min<int64_t>((n + 63) / 64, (int64_t)((8ull << 30) / per_wave)));
+  // a persistent grid within ~32 GiB of DP scratch (5 waves per SIMD at most: 94 VGPRs)
+  const int64_t waves = std::max<int64_t>(
+      1, std::min<int64_t>({(n + 63) / 64, (int64_t)((32ull << 30) / per_wave), (int64_t)c->n_cus * 20}));
   const int blocks = (int)((waves + 3) / 4);
   int rc = 0;
   if ((rc = s1.ensure(end1 + 16)) || (rc = s2.ensure(end2 + 16)) || (rc = o1.ensure(n * 8)) || (rc = o2.ensure(n * 8)) ||
@@ -975,11 +977,13 @@ int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *
   A.len1 = l1.as<uint32_t>(); A.len2 = l2.as<uint32_t>();
   A.n = n;
   A.max_len1 = max1;
+  A.max_len2 = max2;
   A.scratch = scr.as<uint32_t>(); A.words_per_lane = wpl;
   A.tb = tbb.as<uint8_t>(); A.tb_per_lane = tpl;
   A.score = sc.as<int32_t>(); A.path_len = pl.as<int32_t>(); A.n_cigar = nc.as<int32_t>();
   A.ends = en.as<int4>();
   A.cigar = cg.as<uint32_t>(); A.cigar_cap = cap;
+  A.stop_after = c->sw_stop_after;
   if (!rc) {
     chk(hipEventRecord(c->ev[0], c->stream), "event");
     chk(launch_sw(A, c->d_counter.as<unsigned long long>(), blocks, c->stream), "k_sw");

@@ -23,6 +23,8 @@ namespace ibwa {
 namespace {
 
 constexpr int Q = 26, R = 9, QR = Q + R, BAND = 50, MAXSC = 11;
+constexpr int STRIP = 32;  // forward-pass columns held in registers
+constexpr int RCHUNK = 8;  // reverse-pass cells whose loads are issued together
 constexpr int NEG_INF = -1073741823;  // MINOR_INF (stdaln.h:84)
 constexpr int FM = 0, FI = 1, FD = 2;  // FROM_M / FROM_I / FROM_D
 
@@ -171,8 +173,9 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
   L.tb = A.tb + wave * A.tb_per_lane * 64;
   L.lane = lane;
   // scratch elements (u32): eh[0..l1+1], ref4[(l1+7)/8], then M/I/D rows for the global fill
-  const uint32_t eEH = 0, eREF = A.max_len1 + 2, eM = eREF + (A.max_len1 + 7) / 8;
+  const uint32_t eEH = 0, eREF = A.max_len1 + 2, eM = eREF + (A.max_len1 + 31) / 32 * 4;
   const uint32_t eI = eM + 2 * (A.max_len1 + 1), eD = eI + 2 * (A.max_len1 + 1);
+  const uint32_t eBH = eD + 2 * (A.max_len1 + 1), eBF = eBH + A.max_len2 + 1;  // strip boundaries per row
   int64_t cur = 0, cend = 0;
   for (;;) {
     // one pair per lane, claimed per wave
@@ -193,47 +196,69 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
     uint32_t *cig = A.cigar + (uint64_t)p * A.cigar_cap;
     int score = -1, path_len = 0, n_cig = 0, s_i = 0, s_j = 0, e_i = 0, e_j = 0;
     if (n1 > 0 && n2 > 0) {
-      // ---- forward pass (stdaln.c:579-631): row j over seq2, columns i over seq1
-      for (int w = 0; w < (n1 + 7) / 8; ++w) {
+      // ---- forward pass (stdaln.c:579-631): row j over seq2, columns i over seq1.
+      // Strip-mined: STRIP columns at a time for all rows, the strip's H / E of the row
+      // above in registers; between strips only (H[j][i0-1], F) per row goes through
+      // scratch.  The reference's first maximum in row-major order is kept by comparing
+      // (score, j, i) lexicographically.
+      for (int w = 0; w < (n1 + 31) / 32 * 4; ++w) {
         uint32_t x = 0;
         for (int k = 0; k < 8 && w * 8 + k < n1; ++k) x |= (uint32_t)a[w * 8 + k] << (4 * k);
         L.u(eREF + w) = x;
       }
-      for (int i = 0; i <= n1 + 1; ++i) L.u(eEH + i) = 0;
       int score_f = 0, end_i = 0, end_j = 0;
-      for (int j = 1; j <= n2; ++j) {
-        const uint32_t cb = b[j - 1];
-        int last_h = 0, f = 0;
-        int diag = (int)L.u(eEH);  // eh[i-1]: H[j-1][i-1] << 16 | E[j-1][i]
-        uint32_t word = 0;
-        for (int i = 1; i <= n1; ++i) {
-          if (((i - 1) & 7) == 0) word = L.u(eREF + ((i - 1) >> 3));
-          const uint32_t ca = (word >> (4 * ((i - 1) & 7))) & 15u;
-          const int up = (int)L.u(eEH + i);  // eh[i]: H[j-1][i] << 16 | ...
-          int h = (diag >> 16) + sm(cb, ca);
-          if (h < 0) h = 0;
-          if (last_h > 0) {
-            f = (f > last_h - Q) ? f - R : last_h - QR;
-            if (h < f) h = f;
+      for (int i0 = 1; i0 <= n1; i0 += STRIP) {
+        const int wcols = n1 - i0 + 1 < STRIP ? n1 - i0 + 1 : STRIP;
+        int Hc[STRIP], Ec[STRIP];  // H[j-1][i], E[j-1][i] of the strip's columns
+        uint32_t rc[STRIP / 8];    // the strip's reference codes, 4 bits each
+#pragma unroll
+        for (int k = 0; k < STRIP; ++k) Hc[k] = Ec[k] = 0;
+#pragma unroll
+        for (int k = 0; k < STRIP / 8; ++k) rc[k] = L.u(eREF + (uint32_t)(i0 - 1) / 8 + k);
+        int diag_next = 0;  // H[j-1][i0-1]
+        for (int j = 1; j <= n2; ++j) {
+          const uint32_t cb = b[j - 1];
+          int last_h = 0, f = 0;  // H[j][i0-1] and the row's F state, from the previous strip
+          if (i0 > 1) {
+            last_h = (int)L.u(eBH + j);
+            f = (int)L.u(eBF + j);
           }
-          int packed;
-          if (up >= (QR + 1) << 16) {
-            const int above = up >> 16, e_old = diag & 0xffff;
-            const int e = (e_old > above - Q) ? e_old - R : above - QR;
-            if (h < e) h = e;
-            packed = (int)((uint32_t)last_h << 16 | (uint32_t)e);
-          } else {
-            packed = (int)((uint32_t)last_h << 16);
+          int diag = diag_next;
+          diag_next = last_h;
+#pragma unroll
+          for (int k = 0; k < STRIP; ++k) {
+            if (k < wcols) {
+              const uint32_t ca = (rc[k >> 3] >> (4 * (k & 7))) & 15u;
+              const int above = Hc[k], e_old = Ec[k];
+              int h = diag + sm(cb, ca);
+              if (h < 0) h = 0;
+              if (last_h > 0) {
+                f = (f > last_h - Q) ? f - R : last_h - QR;
+                if (h < f) h = f;
+              }
+              int e = 0;
+              if (above >= QR + 1) {
+                e = (e_old > above - Q) ? e_old - R : above - QR;
+                if (h < e) h = e;
+              }
+              Ec[k] = e;
+              Hc[k] = h;
+              diag = above;
+              last_h = h;
+              const int i = i0 + k;
+              if (h > score_f || (h == score_f && h > 0 && (j < end_j || (j == end_j && i < end_i)))) {
+                score_f = h; end_i = i; end_j = j;
+              }
+            }
           }
-          L.u(eEH + i - 1) = (uint32_t)packed;
-          last_h = h;
-          if (score_f < h) { score_f = h; end_i = i; end_j = j; }
-          diag = up;
+          if (i0 + STRIP <= n1) {  // boundary for the next strip
+            L.u(eBH + j) = (uint32_t)last_h;
+            L.u(eBF + j) = (uint32_t)f;
+          }
         }
-        L.u(eEH + n1) = (uint32_t)last_h << 16;
       }
       score = score_f;
-      if (score_f >= 1 && end_i > 0 && end_j > 0) {
+      if (score_f >= 1 && end_i > 0 && end_j > 0 && A.stop_after != 1) {
         // ---- reverse pass (stdaln.c:639-696) in the adaptive band
         for (int i = 0; i <= end_i; ++i) L.u(eEH + i) = 0;
         int score_r = sm(a[end_i - 1], b[end_j - 1]);
@@ -244,25 +269,48 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
         for (int j = end_j - 1; j != 0; --j) {
           const uint32_t cb = b[j - 1];
           int last_h = 0, f = 0, i = start;
-          for (; i != end && i > 0; --i) {  // i > 0: memory guard, never binding (start > end)
-            const int nxt = (int)L.u(eEH + i + 1);
-            int h = (nxt >> 16) + sm(cb, a[i - 1]);
-            if (h < 0) h = 0;
-            if (last_h > 0) {
-              f = (f > last_h - Q) ? f - R : last_h - QR;
-              if (h < f) h = f;
+          bool found = false;
+          int nxt = (int)L.u(eEH + i + 1);  // eh[i+1] of the row below (old value)
+          // cells start, start-1, ..., end+1 (start > end always), RCHUNK at a time: the
+          // chunk's old eh values and codes are loaded together before its cells are updated
+          // (a cell writes eh[i+1] only, so all loaded values are still the row below's)
+          while (i != end && i > 0 && !found) {  // i > 0: memory guard, never binding
+            int ab[RCHUNK];
+            uint32_t cd[RCHUNK];
+#pragma unroll
+            for (int k = 0; k < RCHUNK; ++k) {
+              const int ik = i - k;
+              const bool ok = ik > end && ik > 0;
+              ab[k] = ok ? (int)L.u(eEH + ik) : 0;
+              cd[k] = ok ? a[ik - 1] : 0u;
             }
-            const int above = (int)L.u(eEH + i) >> 16, e_old = nxt & 0xffff;
-            int e = (e_old > above - Q) ? e_old - R : above - QR;
-            if (e < 0) e = 0;
-            if (h < e) h = e;
-            L.u(eEH + i + 1) = (uint32_t)last_h << 16 | (uint32_t)e;
-            last_h = h;
-            if (score_r < h) {
-              score_r = h; start_i = i; start_j = j;
-              if (score_r - QR == score_f) { j = 1; break; }
+#pragma unroll
+            for (int k = 0; k < RCHUNK; ++k) {
+              if (i != end && i > 0 && !found) {
+                int h = (nxt >> 16) + sm(cb, cd[k]);
+                if (h < 0) h = 0;
+                if (last_h > 0) {
+                  f = (f > last_h - Q) ? f - R : last_h - QR;
+                  if (h < f) h = f;
+                }
+                const int above = ab[k] >> 16, e_old = nxt & 0xffff;
+                int e = (e_old > above - Q) ? e_old - R : above - QR;
+                if (e < 0) e = 0;
+                if (h < e) h = e;
+                L.u(eEH + i + 1) = (uint32_t)last_h << 16 | (uint32_t)e;
+                last_h = h;
+                if (score_r < h) {
+                  score_r = h; start_i = i; start_j = j;
+                  if (score_r - QR == score_f) found = true;  // the start: stop here (j = 1; break)
+                }
+                if (!found) {
+                  nxt = ab[k];
+                  --i;
+                }
+              }
             }
           }
+          if (found) j = 1;
           L.u(eEH + i + 1) = (uint32_t)last_h << 16;
           if (((int)L.u(eEH + start) >> 16) <= QR) --start;
           if (start <= 0) start = 0;
@@ -270,6 +318,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
           if (end <= 0) end = 0;
         }
         score_r -= QR;
+        if (A.stop_after == 2) goto done;
         // ---- path by banded global alignment, band doubling from 50 (stdaln.c:723-745)
         const int span = ((end_i - start_i > end_j - start_j) ? end_i - start_i : end_j - start_j) + 1;
         const int n1s = end_i - start_i + 1, n2s = end_j - start_j + 1;
@@ -291,6 +340,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
         e_i = n1s + start_i - 1; e_j = n2s + start_j - 1;
       }
     }
+  done:
     A.score[p] = score;
     A.path_len[p] = path_len;
     A.n_cigar[p] = n_cig;
@@ -306,8 +356,9 @@ hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks,
   return hipGetLastError();
 }
 
-uint64_t sw_words_per_lane(int max_len1) {
-  return (uint64_t)(max_len1 + 2) + (uint64_t)(max_len1 + 7) / 8 + 6ull * (uint64_t)(max_len1 + 1);
+uint64_t sw_words_per_lane(int max_len1, int max_len2) {
+  return (uint64_t)(max_len1 + 2) + (uint64_t)(max_len1 + 31) / 32 * 4 + 6ull * (uint64_t)(max_len1 + 1) +
+         2ull * (uint64_t)(max_len2 + 1);
 }
 
 uint64_t sw_tb_per_lane(int max_len1, int max_len2) {
