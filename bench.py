@@ -257,7 +257,7 @@ def main():
         if touches:
             # touches of the path actually run: the exact-match kernel skips bwt_cal_width,
             # so its algorithmic bytes are priced from its own exact-search touches
-            if path == 1:
+            if path in (1, 3):
                 n_t = min(len(lns), 200_000)
                 p0, L20, w0 = eng.export_bwt(0)
                 p1, L21, w1 = eng.export_bwt(1)
@@ -265,7 +265,7 @@ def main():
                 b1 = oracle.Bwt(primary=p1, L2=L21, words=w1)
                 kk = eng.stats().kmer_k
                 path_touches = float(oracle.exact_touches(b0, b1, seq[:n_t * args.read_len], off[:n_t], lns[:n_t],
-                                                          ropt.mode, kk).mean())
+                                                          ropt.mode, kk, jump=path == 3).mean())
                 result["extra_kmer_k"] = kk
                 kname, k_ms = "k_exact", ms_s / launches
             else:
@@ -289,7 +289,7 @@ def main():
         stl = eng.stats()
         result["extra"] = {"index_build_s": build_s, "n_retry": int(n_retry), "parity_sample_ok": check_ok,
                            "n_stack_overflow": int(stl.n_stack_overflow), "n_aln_overflow": int(stl.n_aln_overflow),
-                           "path": {0: "width+search", 1: "exact", 2: "width+gapped"}.get(path, str(path)),
+                           "path": {0: "width+search", 1: "exact", 2: "width+gapped", 3: "exact+jump"}.get(path, str(path)),
                            "k_width_or_pack_ms": ms_w / launches, "k_search_ms": ms_s / launches,
                            "retry_ms": ms_r / launches}
         print(json.dumps(result), flush=True)

@@ -102,6 +102,9 @@ struct ExactArgs {
   const uint2 *kt0, *kt1;  // K-mer interval tables of .bwt / .rbwt (kmer.hip), or null
   int K;                   // K-mer length (0: no table)
   const uint4 *o64[2];     // bit-plane Occ layouts (occ64.hip)
+  // unique-interval jump (optional): full SA / ISA and the 2-bit text of each strand's index
+  const uint32_t *sa[2], *isa[2], *txt[2];
+  int jump;
 };
 
 // Batched local alignment with path (sw.hip).
@@ -135,13 +138,15 @@ hipError_t launch_width(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_search(const AlnArgs &a, int block, hipStream_t st);
 hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1, const uint2 *kt0,
                         const uint2 *kt1, int K, uint4 *rec, uint32_t stride, unsigned long long *d_counter,
-                        int blocks, hipEvent_t ev_mid, hipStream_t st);
+                        int blocks, hipEvent_t ev_mid, const uint32_t *const jump[6], hipStream_t st);
 uint64_t occ64_blocks(uint32_t seq_len);
 hipError_t build_occ64(const IndexView &ix, uint4 *out, hipStream_t st);
 uint32_t exact_record_stride(int max_len);
 hipError_t launch_occ4(const IndexView &ix, int64_t n, const uint32_t *k, uint32_t *cnt, hipStream_t st);
 hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_t *primary, uint32_t totals[4],
-                        uint32_t *sa_sample, uint32_t sa_intv, int *rounds, hipStream_t st);
+                        uint32_t *sa_sample, uint32_t sa_intv, int *rounds, uint32_t *sa_full, uint32_t *isa_full,
+                        hipStream_t st);
+hipError_t pack_text2(const uint8_t *T, uint64_t n, uint32_t *out, uint64_t out_words, hipStream_t st);
 hipError_t reverse_text(uint8_t *T, uint64_t n, hipStream_t st);
 
 }  // namespace ibwa

@@ -90,6 +90,10 @@ struct ibwa_ctx {
   uint32_t aln_cap_used = 0;
   // sampled suffix arrays kept by ibwa_ctx_build_index
   DBuf sa_s[2];
+  // full SA / ISA and 2-bit texts of an index built here: the exact path's unique-interval jump
+  DBuf sa_full[2], isa_full[2], txt2[2];
+  bool jump_ready = false;
+  int exact_jump = 1;
   uint32_t sa_intv = 0;
   int build_rounds[2] = {0, 0};
   // tuning
@@ -245,7 +249,8 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
-                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof})
+                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
+                  &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1]})
     b->release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(c->stream);
@@ -265,6 +270,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_hit_slots" && value >= 1 && value <= 4096) c->gap_hit_slots = (uint32_t)value;
   else if (k == "gap_reads_per_chunk" && value > 0) c->gap_reads_per_chunk = value;
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
+  else if (k == "exact_jump") c->exact_jump = value != 0;
   else return fail(IBWA_EINVAL, "unknown option %s", k.c_str());
   return 0;
 }
@@ -305,6 +311,7 @@ int ibwa_ctx_load_bwt(ibwa_ctx_t *c, int strand, uint32_t primary, const uint32_
   for (int j = 0; j < 4; ++j) ix.L2[j + 1] = L2[j];
   c->loaded[strand] = true;
   c->kmer_valid = false;
+  c->jump_ready = false;  // SA / ISA / text belong to an index built here
   return 0;
 }
 
@@ -341,6 +348,7 @@ int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
     dst->loaded[s] = true;
     dst->kmer_valid = false;
   }
+  dst->jump_ready = false;
   return 0;
 }
 
@@ -351,11 +359,30 @@ int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa
   DBuf T;
   if (int rc = T.ensure(n)) return rc;
   HIPCHK(hipMemcpyAsync(T.p, codes, n, hipMemcpyHostToDevice, c->stream));
+  // keep SA / ISA / text for the exact path's jump when HBM allows (2 x 8.25 B per base)
+  c->jump_ready = false;
+  bool keep_full = c->exact_jump != 0;
+  if (keep_full) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || (double)free_b < 0.6 * total_b) keep_full = false;
+    if ((double)n * 16.5 > 0.3 * (double)total_b) keep_full = false;
+  }
+  if (!keep_full)
+    for (int s = 0; s < 2; ++s) { c->sa_full[s].release(); c->isa_full[s].release(); c->txt2[s].release(); }
   for (int s = 0; s < 2; ++s) {
     c->loaded[s] = false;
     if (s == 1) HIPCHK(reverse_text(T.as<uint8_t>(), n, c->stream));  // .rpac (bwtmisc.c:160-185)
     const uint64_t n_blocks = (n + 127) / 128 + 1;
     if (int rc = c->idx[s].ensure(n_blocks * 64)) { T.release(); return rc; }
+    uint32_t *sa_full = nullptr, *isa_full = nullptr;
+    if (keep_full) {
+      if (int rc = c->sa_full[s].ensure((n + 1) * 4)) { T.release(); return rc; }
+      if (int rc = c->isa_full[s].ensure((n + 1) * 4)) { T.release(); return rc; }
+      if (int rc = c->txt2[s].ensure((n / 16 + 4) * 4)) { T.release(); return rc; }
+      HIPCHK(pack_text2(T.as<uint8_t>(), n, c->txt2[s].as<uint32_t>(), n / 16 + 4, c->stream));
+      sa_full = c->sa_full[s].as<uint32_t>();
+      isa_full = c->isa_full[s].as<uint32_t>();
+    }
     uint32_t *sa_out = nullptr;
     if (sa_intv > 0) {
       if (int rc = c->sa_s[s].ensure(((n + sa_intv) / sa_intv) * 4)) { T.release(); return rc; }
@@ -363,7 +390,7 @@ int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa
     }
     uint32_t primary = 0, tot[4] = {0, 0, 0, 0};
     hipError_t e = build_strand(T.as<uint8_t>(), n, c->idx[s].as<uint4>(), &primary, tot, sa_out, (uint32_t)sa_intv,
-                                &c->build_rounds[s], c->stream);
+                                &c->build_rounds[s], sa_full, isa_full, c->stream);
     if (e != hipSuccess) {
       T.release();
       return fail(IBWA_EHIP, "suffix sort (strand %d): %s", s, hipGetErrorString(e));
@@ -382,6 +409,7 @@ int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa
   }
   c->kmer_valid = false;
   c->sa_intv = (uint32_t)sa_intv;
+  c->jump_ready = keep_full;
   T.release();
   return 0;
 }
@@ -543,9 +571,15 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     const uint32_t stride = exact_record_stride(max_len);
     if (int rc = c->d_rec.ensure(std::max<int64_t>(n, 1) * (uint64_t)stride * 16)) return rc;
+    const uint32_t *jump[6] = {c->sa_full[0].as<uint32_t>(), c->sa_full[1].as<uint32_t>(),
+                               c->isa_full[0].as<uint32_t>(), c->isa_full[1].as<uint32_t>(),
+                               c->txt2[0].as<uint32_t>(), c->txt2[1].as<uint32_t>()};
+    const bool use_jump = c->jump_ready && c->exact_jump;
+    c->stats.path = use_jump ? 3 : 1;
     HIPCHK(launch_exact(A, c->o64[0].as<uint4>(), c->o64[1].as<uint4>(), c->kt[0].as<uint2>(),
                         c->kt[1].as<uint2>(), c->kmer_K, c->d_rec.as<uint4>(), stride,
-                        c->d_counter.as<unsigned long long>(), c->exact_blocks, c->ev[2], c->stream));
+                        c->d_counter.as<unsigned long long>(), c->exact_blocks, c->ev[2], use_jump ? jump : nullptr,
+                        c->stream));
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[1]));
     float ms_pack = 0, ms = 0;

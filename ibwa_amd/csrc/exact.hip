@@ -106,6 +106,19 @@ __device__ __forceinline__ void extend64(const IndexView &ix, uint32_t &k, uint3
 
 __device__ __forceinline__ bool share_block(uint32_t k, uint32_t l) { return k != 0 && ((k - 1) >> 6) == (l >> 6); }
 
+// Do the next min(32, left) read symbols (2-bit words rw0|rw1, positions t..t+31; complemented
+// for strand 1 under COMPREAD) equal the text at positions tpos.. (words tw0..tw2 from tpos >> 4)?
+__device__ __forceinline__ bool jump_cmp(uint32_t tw0, uint32_t tw1, uint32_t tw2, uint32_t rw0, uint32_t rw1,
+                                         uint32_t tpos, int left, bool complement) {
+  const uint32_t sh = 2 * (tpos & 15);
+  const uint64_t lo = (uint64_t)tw1 << 32 | tw0;
+  const uint64_t x = sh ? (lo >> sh) | ((uint64_t)tw2 << (64 - sh)) : lo;
+  uint64_t rd = (uint64_t)rw1 << 32 | rw0;
+  if (complement) rd = ~rd;
+  const uint64_t mask = left >= 32 ? ~0ull : ((1ull << (2 * left)) - 1ull);
+  return ((x ^ rd) & mask) == 0;
+}
+
 __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restrict__ rec, uint32_t stride,
                                                unsigned long long *counter) {
   const int lane = threadIdx.x & 63;
@@ -121,6 +134,10 @@ __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restr
   int len = 0, p = 0;         // p: next position (both strands advance together)
   uint32_t ka = 0, la = 0, kb = 0, lb = 0, ia = 0, ib = 0, bw = 0;
   bool ra = false, rb = false, fa = false, fb = false, lk = false;
+  // unique-interval jump per strand: 1 = SA[k] wanted, 2 = comparing the read's remaining
+  // m symbols with the text before q = SA[k], 32 per iteration (t: compared so far)
+  int ja = 0, jb = 0, ma = 0, mb = 0, tca = 0, tcb = 0;
+  uint32_t qa = 0, qb = 0, isa_a = 0, isa_b = 0;
   for (;;) {
     // ---- claim reads for idle lanes (no memory traffic unless the chunk runs out)
     unsigned long long need = __ballot(st == 0);
@@ -149,7 +166,7 @@ __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restr
     const bool hdr = st == 1;
     const bool run = st == 2;
     const bool look_a = run && lk && ra, look_b = run && lk && rb;
-    const bool step_a = run && !lk && ra, step_b = run && !lk && rb;
+    const bool step_a = run && !lk && ra && p >= 0, step_b = run && !lk && rb && p >= 0;
     const uint32_t c = (bw >> (2 * (p & 15))) & 3;  // symbol of seq at p (valid when running and !lk)
     const uint32_t ca = comp ? c ^ 3u : c, cb = c;
     uint4 h = make_uint4(0, 0, 0, 0);
@@ -164,8 +181,28 @@ __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restr
     uint4 vbk = load64(A.o64[1], kb - 1, cb, step_b && kb != 0 && !shb);
     // next symbol word: crossing into a new 16-symbol word on the next step
     uint32_t nbw = 0;
+    const uint32_t *recw = reinterpret_cast<const uint32_t *>(rec + (uint64_t)r * stride + 1);
     const bool need_word = run && !lk && (ra || rb) && (p & 15) == 0 && p > 0;
-    if (need_word) nbw = reinterpret_cast<const uint32_t *>(rec + (uint64_t)r * stride + 1)[(p - 1) >> 4];
+    if (need_word) nbw = recw[(p - 1) >> 4];
+    // jump loads: SA[k]; or 3 text words + 2 read words (+ ISA[q - m] on the first compare)
+    uint32_t sa_ld_a = 0, sa_ld_b = 0, isa_ld_a = 0, isa_ld_b = 0;
+    uint32_t twa0 = 0, twa1 = 0, twa2 = 0, rwa0 = 0, rwa1 = 0, twb0 = 0, twb1 = 0, twb2 = 0, rwb0 = 0, rwb1 = 0;
+    if (run && ja == 1) sa_ld_a = A.sa[0][ka];
+    if (run && jb == 1) sa_ld_b = A.sa[1][kb];
+    if (run && ja == 2) {
+      const uint32_t w = (qa - (uint32_t)ma + (uint32_t)tca) >> 4;
+      twa0 = A.txt[0][w]; twa1 = A.txt[0][w + 1]; twa2 = A.txt[0][w + 2];
+      rwa0 = recw[tca >> 4];
+      if (((tca >> 4) + 1) * 16 < ma) rwa1 = recw[(tca >> 4) + 1];
+      if (tca == 0) isa_ld_a = A.isa[0][qa - (uint32_t)ma];
+    }
+    if (run && jb == 2) {
+      const uint32_t w = (qb - (uint32_t)mb + (uint32_t)tcb) >> 4;
+      twb0 = A.txt[1][w]; twb1 = A.txt[1][w + 1]; twb2 = A.txt[1][w + 2];
+      rwb0 = recw[tcb >> 4];
+      if (((tcb >> 4) + 1) * 16 < mb) rwb1 = recw[(tcb >> 4) + 1];
+      if (tcb == 0) isa_ld_b = A.isa[1][qb - (uint32_t)mb];
+    }
 
     // ---- consume
     if (hdr) {
@@ -183,6 +220,33 @@ __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restr
       lk = ra && K > 0 && len >= K;
       st = 2;
     } else if (run) {
+      // jumps in flight
+      if (ja == 1) {
+        qa = sa_ld_a;
+        if (qa < (uint32_t)ma) { fa = true; ja = 0; } else { ja = 2; tca = 0; }
+      } else if (ja == 2) {
+        if (tca == 0) isa_a = isa_ld_a;
+        if (jump_cmp(twa0, twa1, twa2, rwa0, rwa1, qa - (uint32_t)ma + (uint32_t)tca, ma - tca, comp)) {
+          tca += 32;
+          if (tca >= ma) { ka = la = isa_a; ja = 0; }
+        } else {
+          fa = true;
+          ja = 0;
+        }
+      }
+      if (jb == 1) {
+        qb = sa_ld_b;
+        if (qb < (uint32_t)mb) { fb = true; jb = 0; } else { jb = 2; tcb = 0; }
+      } else if (jb == 2) {
+        if (tcb == 0) isa_b = isa_ld_b;
+        if (jump_cmp(twb0, twb1, twb2, rwb0, rwb1, qb - (uint32_t)mb + (uint32_t)tcb, mb - tcb, false)) {
+          tcb += 32;
+          if (tcb >= mb) { kb = lb = isa_b; jb = 0; }
+        } else {
+          fb = true;
+          jb = 0;
+        }
+      }
       if (lk) {
         if (look_a) { ka = ta.x; la = ta.y; if (ka > la) { ra = false; fa = true; } }
         if (look_b) { kb = tb.x; lb = tb.y; if (kb > lb) { rb = false; fb = true; } }
@@ -200,10 +264,16 @@ __global__ void __launch_bounds__(256) k_exact(ExactArgs A, const uint4 *__restr
           if (kb > lb) { rb = false; fb = true; }
         }
         if (need_word) bw = nbw;
-        --p;
+        if (step_a || step_b) --p;
+      }
+      // a chain whose interval became one row jumps over its remaining p + 1 symbols:
+      // stepping from row k succeeds exactly while the text before SA[k] spells them
+      if (A.jump && !lk && p >= 0) {
+        if (ra && ka == la) { ra = false; ja = 1; ma = p + 1; }
+        if (rb && kb == lb) { rb = false; jb = 1; mb = p + 1; }
       }
     }
-    if (st == 2 && (p < 0 || (!ra && !rb))) {
+    if (st == 2 && ja == 0 && jb == 0 && (p < 0 || (!ra && !rb))) {
       // both chains finished: a chain that did not fail consumed every symbol
       uint4 *out = A.aln + (uint64_t)r * A.aln_cap;
       int nh = 0;
@@ -224,7 +294,7 @@ uint32_t exact_record_stride(int max_len) {  // in uint4 units
 
 hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1, const uint2 *kt0,
                         const uint2 *kt1, int K, uint4 *rec, uint32_t stride, unsigned long long *d_counter,
-                        int blocks, hipEvent_t ev_mid, hipStream_t st) {
+                        int blocks, hipEvent_t ev_mid, const uint32_t *const jump[6], hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   const int comp = (a.o.mode & MODE_COMPREAD) ? 1 : 0;
   hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a.seq, a.off, a.len, a.n,
@@ -251,6 +321,12 @@ hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1
   x.K = K;
   x.o64[0] = o64_0;
   x.o64[1] = o64_1;
+  x.jump = jump != nullptr;
+  for (int s = 0; s < 2; ++s) {
+    x.sa[s] = jump ? jump[s] : nullptr;
+    x.isa[s] = jump ? jump[2 + s] : nullptr;
+    x.txt[s] = jump ? jump[4 + s] : nullptr;
+  }
   hipLaunchKernelGGL(k_exact, dim3(blocks), dim3(256), 0, st, x, rec, stride, d_counter);
   return hipGetLastError();
 }

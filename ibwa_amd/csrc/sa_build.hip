@@ -150,6 +150,25 @@ __global__ void k_reverse(uint8_t *T, uint64_t n) {
   }
 }
 
+// inverse suffix array: isa[sa[r]] = r
+__global__ void k_isa(const uint32_t *__restrict__ sa, uint64_t N, uint32_t *__restrict__ isa) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (uint64_t)gridDim.x * blockDim.x)
+    isa[sa[r]] = (uint32_t)r;
+}
+
+// text codes -> 2 bits per base, base t at bits 2 (t & 15) of word t >> 4 (tail words zero)
+__global__ void k_pack_text2(const uint8_t *__restrict__ T, uint64_t n, uint64_t n_words, uint32_t *__restrict__ out) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t x = 0;
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t t = w * 16 + k;
+      if (t < n) x |= (uint32_t)(T[t] & 3) << (2 * k);
+    }
+    out[w] = x;
+  }
+}
+
 __global__ void k_sample_sa(const uint32_t *__restrict__ sa, uint64_t n_sa, uint32_t intv, uint32_t *__restrict__ out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_sa; i += (uint64_t)gridDim.x * blockDim.x)
     out[i] = sa[i * intv];
@@ -295,7 +314,8 @@ static hipError_t suffix_sort(const uint8_t *T, uint64_t n, SaScratch &S, hipStr
 // Build one strand's index from the device text T (codes 0..3, length n).
 // out_blocks: ceil(n/128)+1 blocks of 64 B.  totals: symbol counts.
 hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_t *primary, uint32_t totals[4],
-                        uint32_t *sa_sample, uint32_t sa_intv, int *rounds, hipStream_t st) {
+                        uint32_t *sa_sample, uint32_t sa_intv, int *rounds, uint32_t *sa_full, uint32_t *isa_full,
+                        hipStream_t st) {
   const uint64_t N = n + 1;
   SaScratch S;
   HC(hipMalloc(&S.sa, N * 4));
@@ -320,6 +340,11 @@ hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_
     hipLaunchKernelGGL(k_find_primary, grid_for(N), dim3(256), 0, st, S.sa, N, d_primary);
     e = hipMemcpyAsync(primary, d_primary, 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+  if (e == hipSuccess && sa_full) e = hipMemcpyAsync(sa_full, S.sa, N * 4, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && isa_full) {
+    hipLaunchKernelGGL(k_isa, grid_for(N), dim3(256), 0, st, S.sa, N, isa_full);
+    e = hipGetLastError();
   }
   if (e == hipSuccess && sa_sample) {
     uint64_t n_sa = (n + sa_intv) / sa_intv;  // bwt.c:56
@@ -350,6 +375,11 @@ hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_
   (void)hipFree(S.sa); (void)hipFree(S.rank); (void)hipFree(S.v1);
   (void)hipFree(S.k0); (void)hipFree(S.k1); (void)hipFree(S.tmp);
   return e;
+}
+
+hipError_t pack_text2(const uint8_t *T, uint64_t n, uint32_t *out, uint64_t out_words, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_text2, grid_for(out_words), dim3(256), 0, st, T, n, out_words, out);
+  return hipGetLastError();
 }
 
 hipError_t reverse_text(uint8_t *T, uint64_t n, hipStream_t st) {

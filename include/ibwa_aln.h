@@ -114,7 +114,8 @@ typedef struct {
 	int64_t n_retry;       /* reads re-run in the large-capacity pass */
 	int64_t n_launch_width, n_launch_search;
 	int path;              /* 0: width + general search; 1: exact-match path (max_diff == 0);
-	                          2: width + persistent gapped search */
+	                          2: width + persistent gapped search; 3: exact path with the
+	                          unique-interval jump (index built by ibwa_ctx_build_index) */
 	int kmer_k;            /* K of the K-mer interval table the exact path used (0: none) */
 	int64_t n_stack_overflow;  /* first-pass reads whose stack did not fit (re-run) */
 	int64_t n_aln_overflow;    /* first-pass reads whose hits did not fit (re-run) */
@@ -125,6 +126,8 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 
 /* Named engine options:
  *   "exact_path" (0/1, default 1)  exact-match kernel when max_diff == 0
+ *   "exact_jump" (0/1, default 1)  keep full SA / ISA / text at ibwa_ctx_build_index and let
+ *                                  the exact path jump over a unique interval's remaining symbols
  *   "kmer_k" (-1 auto, 0 off, 1..16) K-mer interval table length
  *   "exact_blocks", "lanes_per_chunk"
  *   "gapped_v2" (0/1, default 1)   persistent gapped-search kernel (else the general kernels)

@@ -79,7 +79,7 @@ def lib():
         L.or_free.argtypes = [c.c_void_p]
         L.or_set_stats.argtypes = [c.c_void_p]
         L.or_exact_touches.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p, c.c_void_p,
-                                       c.c_int, c.c_int, c.c_void_p]
+                                       c.c_int, c.c_int, c.c_int, c.c_void_p]
         L.or_aln_local_core.restype = c.c_int
         L.or_aln_local_core.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
                                         c.POINTER(c.c_int), c.c_int, c.c_void_p]
@@ -256,15 +256,16 @@ def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False
     return n_aln, alns, tch
 
 
-def exact_touches(bwt0, bwt1, seqs, offs, lens, mode, K=0):
+def exact_touches(bwt0, bwt1, seqs, offs, lens, mode, K=0, jump=False):
     """Per-read touches of the exact-match path (max_diff == 0) the GPU runs; with a
-    K-mer table the first K steps of a chain count as one (table) touch."""
+    K-mer table the first K steps of a chain count as one (table) touch; with `jump`
+    the rest of a chain whose interval is one row costs SA + text (+ ISA on a match)."""
     seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     out = np.zeros(lens.size, dtype=np.uint32)
     lib().or_exact_touches(bwt0.h, bwt1.h, lens.size, seqs.ctypes.data, offs.ctypes.data, lens.ctypes.data,
-                           int(mode), int(K), out.ctypes.data)
+                           int(mode), int(K), int(bool(jump)), out.ctypes.data)
     return out
 
 

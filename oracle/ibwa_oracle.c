@@ -529,20 +529,41 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
  * GPU takes for max_diff == 0: strand 1 = bwt_match_exact_alt(bwt0, rseq),
  * strand 0 = bwt_match_exact_alt(bwt1, seq), none for reads with an N.  Used
  * to price the GPU path's own algorithmic bytes (it skips bwt_cal_width). */
-/* one exact chain priced with a K-mer table: the first K steps are one lookup */
-static void exact_chain_touches(const or_bwt_t *b, int L, const uint8_t *str, int K, uint32_t *t)
+/* The unique-interval jump: once k == l with m symbols left the
+ * GPU reads SA[k], compares the m symbols against the packed text and, if they
+ * all match, reads ISA at the final position -- one 64 B touch each (the m <= 256
+ * symbols of text span one 64 B line), instead of m Occ steps. */
+static void jump_touches(const or_bwt_t *b, int m, const uint8_t *str, uint32_t k, uint32_t l, uint32_t *t)
 {
-	uint32_t k = 0, l = b->seq_len, dummy = 0;
+	uint32_t dummy = 0;
+	*t += 2 + (uint32_t)((2 * m - 1) / 512);
+	if (match_exact_alt(b, m, str, &k, &l, &dummy)) ++*t;
+}
+
+/* one exact chain priced with a K-mer table: the first K steps are one lookup;
+ * with `jump`, the steps after the interval narrows to one row are priced as a jump */
+static void exact_chain_touches(const or_bwt_t *b, int L, const uint8_t *str, int K, int jump, uint32_t *t)
+{
+	uint32_t k = 0, l = b->seq_len, dummy = 0, ok, ol;
+	int i;
 	if (K > 0 && L >= K) {
 		++*t;
 		if (!match_exact_alt(b, K, str + L - K, &k, &l, &dummy)) return;
 		L -= K;
 	}
-	match_exact_alt(b, L, str, &k, &l, t);
+	for (i = L - 1; i >= 0; --i) {
+		int c = str[i];
+		if (jump && k == l) { jump_touches(b, i + 1, str, k, l, t); return; }
+		if (c > 3) return;
+		twoocc_t(b, k - 1, l, c, &ok, &ol, t);
+		k = b->L2[c] + ok + 1;
+		l = b->L2[c] + ol;
+		if (k > l) return;
+	}
 }
 
 void or_exact_touches(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_seqs, const uint8_t *seq,
-                      const uint64_t *off, const uint32_t *len, int mode, int K, uint32_t *touches)
+                      const uint64_t *off, const uint32_t *len, int mode, int K, int jump, uint32_t *touches)
 {
 	int64_t r;
 	uint8_t *rseq = 0;
@@ -557,8 +578,8 @@ void or_exact_touches(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_seqs
 			rseq[j] = (mode & OR_MODE_COMPREAD) && s[j] < 4 ? 3 - s[j] : s[j];
 		}
 		if (nN == 0) {
-			exact_chain_touches(bwt0, L, rseq, K, &t);
-			exact_chain_touches(bwt1, L, s, K, &t);
+			exact_chain_touches(bwt0, L, rseq, K, jump, &t);
+			exact_chain_touches(bwt1, L, s, K, jump, &t);
 		}
 		(void)k; (void)l;
 		touches[r] = t;

@@ -81,7 +81,7 @@ int64_t or_cal_sa_reg_gap(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_
                           int32_t *n_aln, or_aln1_t **alns_out, uint32_t *touches_out);
 void or_free(void *p);
 void or_exact_touches(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_seqs, const uint8_t *seq,
-                      const uint64_t *off, const uint32_t *len, int mode, int K, uint32_t *touches);
+                      const uint64_t *off, const uint32_t *len, int mode, int K, int jump, uint32_t *touches);
 
 /* stdaln.c:529 restated: local SW + banded global path fill (aln_param_bwa) */
 typedef struct { int i, j; unsigned char ctype; } or_path_t;

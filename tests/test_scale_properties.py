@@ -59,6 +59,14 @@ def eopt(argv):
     return o, e
 
 
+def test_device_built_index_uses_the_jump(mid_genome):
+    ascii_, lens, eng, _, _ = mid_genome
+    seq, off, lns, _, _ = reads(ascii_, lens, 3, 1000, 100, 0.0, 0.0)
+    _, e = eopt(["-n", "0"])
+    eng.aln(seq, off, lns, e)
+    assert eng.stats().path == 3
+
+
 def test_exact_reads_round_trip(mid_genome):
     ascii_, lens, eng, _, _ = mid_genome
     seq, off, lns, strand, raw = reads(ascii_, lens, 11, 200_000, 100, 0.0, 0.0)
@@ -82,12 +90,14 @@ def test_exact_reads_round_trip(mid_genome):
     # small static regions: many reads take pages from their workgroup pool, some exhaust it
     ([], 100, 0.02, 20_000, {"gap_cap1": 256, "gap_pages_per_block": 2}),
     (["-n", "0"], 100, 0.01, 20_000, {"exact_path": 0}),
+    (["-n", "0"], 100, 0.01, 100_000, {"exact_jump": 0}),
+    (["-n", "0"], 150, 0.0, 50_000, {}), (["-n", "0"], 36, 0.0, 50_000, {}),
     ([], 100, 0.01, 4_000, {"gapped_v2": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
     o, e = eopt(argv)
-    defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1}
+    defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
