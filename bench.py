@@ -198,7 +198,8 @@ def main():
         st_ = eng.stats()
         log(f"{tag}: total {st_.ms_total:.1f} ms (width {st_.ms_width:.1f}, search {st_.ms_search:.1f}, "
             f"retry {st_.ms_retry:.1f} ms for {st_.n_retry} reads: {st_.n_stack_overflow} stack, "
-            f"{st_.n_aln_overflow} hit overflows)")
+            f"{st_.n_aln_overflow} hit overflows, {st_.n_heavy} heavy; coop pass {st_.ms_coop:.1f} ms "
+            f"resolved {st_.n_coop})")
 
     for w in range(args.warmup):
         eng.run(opt)

@@ -1,0 +1,729 @@
+// coop.hip -- bwt_match_gap (bwtgap.c:104-264) for the heavy reads: one read per
+// wavefront, its search spread over the 64 lanes, results bit-identical to the
+// sequential search.
+//
+// Why the search parallelises exactly.  The reference pops the top of the
+// lowest non-empty score bucket (bucketed LIFO, bwtgap.c:45-79).  Every child
+// of an entry scores at least its parent (penalties are positive; the engine
+// rejects others) and only the match child (pushed last, bwtgap.c:244-258)
+// scores the same, so:
+//   * the search visits score levels in increasing order, and nothing is ever
+//     pushed into the level being processed except match children;
+//   * a match child is popped right after its parent's expansion.
+// So a level is a fixed list of entries (the bucket at the time the level
+// starts, popped from the top), and each entry starts a "match chain": the
+// entry, its match child, that one's match child, ..., ending in a prune
+// (bwtgap.c:147,155), an expansion without a match child, a hit at i == 0
+// (:159) or an exact tail (bwt_match_exact_alt, :160-163).  Between two hits
+// the only state a chain reads is fixed (max_diff, best_score, the width arrays
+// gap_shadow rewrites, :81-91), so the chains of a level are independent: the
+// lanes run them concurrently, each writing its children, in the reference's
+// push order, to a private staging ring.  A reorder buffer of chain records
+// (LDS) commits finished chains strictly in pop order: their children are
+// appended to the target buckets by a wave prefix sum, which reproduces the
+// reference's bucket contents and order exactly.  A chain that ends in a hit
+// is a barrier: chains after it were run with stale state, so they are
+// discarded (their staging rolled back) and re-run once the hit (top-2 rule,
+// dedup, gap_shadow, max_diff) has been applied.
+//
+// Reasons a read is handed on (status bits 8-15, diagnostics): 1 read too long /
+// too many buckets / staging too small, 2 max_entries could be reached, 3 page pool
+// empty, 4 a bucket past COOP_MAXP pages, 5 runaway guard.
+//
+// The max_entries check before each pop (:139) is tracked per chain: if a
+// committed prefix could reach it, the read goes to the sequential kernel
+// (gapped.hip, wide), as does anything that outgrows this kernel's storage.
+//
+// Storage per wave: LDS holds the read's two strands, its width arrays (so
+// gap_shadow and the pruning tests are LDS work), bucket sizes, the page
+// directories of the level and its three target buckets, and the chain
+// records.  Buckets live in 128 KiB pages of a global pool (per-wave free
+// stack, global bump pointer); staging rings are per lane.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "engine.h"
+#include "occ.h"
+
+namespace ibwa {
+
+namespace {
+
+constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_NONSTOP = 0x10;
+constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
+constexpr int RREC = 256;            // chain records in flight (ring)
+constexpr int MAXP = COOP_MAXP;      // pages per bucket
+constexpr int NSTK = COOP_NSTK;      // buckets
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// lane states
+constexpr int L_IDLE = 0, L_FETCH = 1, L_EXP = 2, L_TAIL = 3;
+
+struct Blk {
+  uint4 v0, v1, v2, v3;
+};
+
+__device__ __forceinline__ void load_blk(const uint4 *o, uint32_t row, bool run, Blk &b) {
+  if (run) {
+    const uint4 *p = o + (size_t)(row >> 6) * 4;
+    b.v0 = p[0];
+    b.v1 = p[1];
+    b.v2 = p[2];
+    b.v3 = p[3];
+  }
+}
+
+__device__ __forceinline__ uint32_t occ_of(const uint4 &v, uint32_t row) {
+  const uint32_t o = row & 63;
+  const uint32_t mlo = o >= 31 ? 0xFFFFFFFFu : ((2u << o) - 1u);
+  const uint32_t mhi = o < 32 ? 0u : (o == 63 ? 0xFFFFFFFFu : ((2u << (o - 32)) - 1u));
+  return v.x + (uint32_t)__builtin_popcount(v.z & mlo) + (uint32_t)__builtin_popcount(v.w & mhi);
+}
+
+__device__ __forceinline__ uint32_t pick4(uint4 v, uint32_t c) {
+  const uint32_t lo = (c & 1) ? v.y : v.x, hi = (c & 1) ? v.w : v.z;
+  return (c & 2) ? hi : lo;
+}
+
+__device__ __forceinline__ int int_log2(uint32_t v) { return v ? 31 - __builtin_clz(v) : 0; }
+
+// wave-wide exclusive prefix sum and total (64 lanes)
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, int lane, uint32_t &total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  total = __shfl(x, 63);
+  return x - v;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t y = __shfl_xor(v, d);
+    v = y < v ? y : v;
+  }
+  return v;
+}
+
+// entry (uint4): {k, l, i | ldp << 10 | rank << 20, n_mm | n_gapo << 8 | n_gape << 16 | a << 24 | state << 25
+//                  | cat << 27}
+// i, ldp <= COOP_MAXLEN < 1024.  rank / cat: a staged child's target bucket (0..2 = mismatch, gap
+// extension, gap open, merged when penalties coincide) and its index among the chain's children of
+// that bucket -- so a commit can place every child independently.
+__device__ __forceinline__ uint4 mk_ent(uint32_t k, uint32_t l, int i, int ldp, int n_mm, int n_gapo, int n_gape,
+                                        int a, int state, uint32_t cat = 0, uint32_t rank = 0) {
+  return make_uint4(k, l, (uint32_t)i | (uint32_t)ldp << 10 | rank << 20,
+                    (uint32_t)n_mm | (uint32_t)n_gapo << 8 | (uint32_t)n_gape << 16 | (uint32_t)a << 24 |
+                        (uint32_t)state << 25 | cat << 27);
+}
+
+struct Shm {
+  uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | lane << 16 | hit << 24, done}
+  uint4 recB[RREC];   // hit: {k, l, n_mm | n_gapo << 8 | n_gape << 16 | a << 24, ldp}
+  uint32_t dirc[4][MAXP];  // page ids of the level's bucket and of its (up to) three target buckets
+  uint32_t nb[NSTK];       // entries per bucket
+  uint32_t np[NSTK];       // pages per bucket
+  uint2 W[2][COOP_MAXLEN + 1];   // width arrays {w, bid} of strands 0 / 1 (bwt_width_t)
+  uint2 SW[2][COOP_MAXLEN + 1];  // seed width arrays
+  uint8_t str[2][COOP_MAXLEN];   // strand 0 = bwa_seq_t.seq, strand 1 = complement (COMPREAD)
+  uint32_t head[64];             // per-lane staging ring: first uncommitted slot
+  uint32_t rb[64];               // per-lane staging rollback point (discarded chains)
+};
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *counter) {
+  __shared__ Shm S;
+  const int lane = threadIdx.x;
+  const uint64_t wave = blockIdx.x;
+  const AlnOpt o = A.o;
+  const bool comp = o.mode & MODE_COMPREAD;
+  const bool gape = o.mode & MODE_GAPE;
+  const IndexView ixv0 = A.ix[0], ixv1 = A.ix[1];
+  uint4 *const stg_base = A.stg + ((wave * 64) << A.stg_log2);
+  uint4 *const stg = stg_base + ((uint64_t)lane << A.stg_log2);
+  const uint32_t SMASK = (1u << A.stg_log2) - 1u;
+  const uint32_t STG = 1u << A.stg_log2;
+  uint32_t *const dir = A.dir + wave * (uint64_t)NSTK * MAXP;
+  uint32_t *const freel = A.freel + wave * (uint64_t)A.freecap;
+  uint4 *const hitv = A.hits + wave * (uint64_t)A.hcap;
+  uint32_t n_free = 0;  // pages on this wave's free stack (kept across reads)
+
+  // take a page: this wave's free stack, else the global pool (NONE when exhausted)
+  auto alloc_page = [&]() __attribute__((always_inline)) -> uint32_t {
+    uint32_t p = NONE;
+    if (n_free) {
+      --n_free;
+      p = freel[n_free];
+    } else {
+      uint32_t q = 0;
+      if (lane == 0) q = atomicAdd(A.pool_next, 1u);
+      q = __shfl(q, 0);
+      p = q < A.pool_pages ? q : NONE;
+    }
+    return p;
+  };
+  // give back the pages of bucket b (dirc slot ds holds its directory)
+  auto free_pages = [&](uint32_t npg, const uint32_t *d) __attribute__((always_inline)) {
+    const uint32_t room = A.freecap - n_free;
+    const uint32_t nf = npg < room ? npg : room;  // beyond the stack's room pages are dropped
+    for (uint32_t j = lane; j < nf; j += 64) freel[n_free + j] = d[j];
+    n_free += nf;
+  };
+
+  for (;;) {
+    // ------------------------------------------------ claim a read
+    int64_t r = 0;
+    if (lane == 0) r = (int64_t)atomicAdd(counter, 1ull);
+    r = __shfl(r, 0);
+    if (r >= A.n) break;
+    const int64_t rr = A.ids ? A.ids[r] : r;
+    const int64_t ro = A.out_by_id ? rr : r;
+    const int len = (int)A.len[rr];
+    const uint8_t *sq = A.seq + A.off[rr];
+    const int opt_max_diff = o.fnr_pos ? (int)A.maxdiff_tab[len] : o.max_diff;
+    uint32_t status = 0;
+    int n_aln = 0;
+    uint32_t n_iter = 0;
+    if (len > COOP_MAXLEN || o.n_stacks > NSTK || (1u << A.stg_log2) < 9u * (uint32_t)(len + 1) + 16u) {
+      status = ST_STACK_OVERFLOW | 1u << 8;  // not for this kernel: the sequential kernel takes it
+    } else if ((int)A.nN[r] > opt_max_diff) {
+      // bwtgap.c:116-122: no hit
+    } else {
+      // ---------------------------------------------- per-read setup
+      const bool seeded = len > o.seed_len;
+      const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
+      for (int j = lane; j < len; j += 64) {
+        const uint32_t c = sq[j];
+        S.str[0][j] = (uint8_t)c;
+        S.str[1][j] = (uint8_t)(comp && c < 4 ? 3u - c : c);
+      }
+      for (int j = lane; j <= len; j += 64) {
+        S.W[0][j] = wb[j];
+        S.W[1][j] = wb[A.wlen1 + j];
+      }
+      if (seeded)
+        for (int j = lane; j <= o.seed_len; j += 64) {
+          S.SW[0][j] = wb[2 * A.wlen1 + j];
+          S.SW[1][j] = wb[2 * A.wlen1 + o.seed_len + 1 + j];
+        }
+      for (int b = lane; b < NSTK; b += 64) {
+        S.nb[b] = 0;
+        S.np[b] = 0;
+      }
+      S.head[lane] = 0;
+      S.rb[lane] = NONE;
+      for (int j = lane; j < RREC; j += 64) S.recA[j].w = 0;
+      __syncthreads();
+      // roots (bwtgap.c:126-127): strand 0 then strand 1, both in bucket 0
+      {
+        const uint32_t p = alloc_page();
+        if (p == NONE) {
+          status = ST_STACK_OVERFLOW | 3u << 8;
+        } else {
+          if (lane == 0) {
+            dir[0] = p;
+            S.np[0] = 1;
+            S.nb[0] = 2;
+            uint4 *pg = A.pool + ((uint64_t)p << COOP_PG_LOG2);
+            pg[0] = mk_ent(0u, ixv0.seq_len, len, 0, 0, 0, 0, 0, STATE_M);
+            pg[1] = mk_ent(0u, ixv0.seq_len, len, 0, 0, 0, 0, 1, STATE_M);
+          }
+          __syncthreads();
+        }
+      }
+      int best_score = (opt_max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape;
+      int max_diff = opt_max_diff, best_cnt = 0;
+      uint32_t n_live = 2;  // entries on the stack (bwtgap.c n_entries)
+      uint32_t stg_w = 0;   // this lane's staging write counter
+      int s = 0;            // level (score bucket)
+      bool done = status != 0;
+      // ---------------------------------------------- levels
+      while (!done) {
+        while (s < o.n_stacks && S.nb[s] == 0) ++s;
+        if (s >= o.n_stacks) break;                                              // stack empty
+        if (n_live > (uint32_t)o.max_entries) { status = ST_STACK_OVERFLOW | 2u << 8; break; }  // :139, exactly there
+        if (!(o.mode & MODE_NONSTOP) && s > best_score + o.s_mm) break;         // :143
+        const uint32_t N = S.nb[s];
+        // targets: mismatch, gap extension, gap open (deduplicated when penalties coincide)
+        const int t0 = s + o.s_mm;
+        const int t1 = s + o.s_gape;
+        const int t2 = s + o.s_gapo;
+        const int q1 = t1 == t0 ? 0 : 1;
+        const int q2 = t2 == t0 ? 0 : (t2 == t1 ? q1 : 2);
+        auto tg = [&](int q) __attribute__((always_inline)) { return q == 0 ? t0 : q == 1 ? t1 : t2; };
+        // directories into LDS
+        for (uint32_t j = lane; j < S.np[s]; j += 64) S.dirc[0][j] = dir[s * MAXP + j];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (tg(q) < o.n_stacks)
+            for (uint32_t j = lane; j < S.np[tg(q)]; j += 64) S.dirc[1 + q][j] = dir[tg(q) * MAXP + j];
+        __syncthreads();
+        uint32_t next_c = 0, cp = 0, barrier = NONE;
+        // lane chain state
+        int lst = L_IDLE;
+        uint32_t c = 0, cstart = 0, cnt0 = 0, cnt1 = 0, cnt2 = 0;
+        uint32_t k = 0, l = 0;
+        int i = 0, ldp = 0, e_mm = 0, e_go = 0, e_ge = 0, a = 0, state = 0;
+        int xj = 0;
+        uint32_t xk = 0, xl = 0;
+        uint32_t ent_page = 0, ent_off = 0;
+        uint32_t hit_c = NONE;  // chain this lane ended with a hit in the last iteration
+        // end the lane's chain: its record (hit or not) goes to the reorder buffer
+        auto end_chain = [&](bool hit, uint32_t hk, uint32_t hl) __attribute__((always_inline)) {
+          const uint32_t slot = c & (RREC - 1);
+          S.recB[slot] = make_uint4(hk, hl,
+                                    (uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
+                                    (uint32_t)ldp);
+          S.recA[slot] = make_uint4(cstart, cnt0 | cnt1 << 16, cnt2 | (uint32_t)lane << 16 | (hit ? 1u << 24 : 0u), 1u);
+          if (hit) hit_c = c;
+          lst = L_IDLE;
+        };
+        // the pops of bwtgap.c:139-163 for the node in registers: prune, hit, tail or expand
+        auto pop_node = [&]() __attribute__((always_inline)) {
+          int m = max_diff - (e_mm + e_go);
+          if (gape) m -= e_ge;
+          if (m < 0) { end_chain(false, 0, 0); return; }                                  // :147
+          if (i > 0 && m < (int)S.W[a][i - 1].y) { end_chain(false, 0, 0); return; }      // :155
+          if (i == 0) { end_chain(true, k, l); return; }                                   // :159
+          if (m == 0 && (state == STATE_M || gape || e_ge == o.max_gape)) {              // :160
+            xj = i - 1;
+            xk = k;
+            xl = l;
+            if (S.str[a][xj] > 3) { end_chain(false, 0, 0); return; }
+            lst = L_TAIL;
+            return;
+          }
+          lst = L_EXP;
+        };
+
+        for (;;) {
+          if (++n_iter > A.max_iters) {  // runaway guard: hand the read to the sequential kernel
+            status = ST_STACK_OVERFLOW | 5u << 8;
+            done = true;
+            break;
+          }
+          // ============================================ uniform control
+          // (a) hits of chains that ended last iteration: the earliest becomes the barrier, and
+          //     every chain after it (running or finished) is discarded
+          {
+            uint32_t newb = NONE;
+            if (__ballot(hit_c != NONE)) newb = wave_min(hit_c);
+            hit_c = NONE;
+            if (newb < barrier) {
+              if (lst != L_IDLE && c > newb) {
+                S.rb[lane] = S.rb[lane] < cstart ? S.rb[lane] : cstart;
+                lst = L_IDLE;
+              }
+              __syncthreads();
+              for (uint32_t base = newb + 1; base < next_c; base += 64) {
+                const uint32_t cc = base + lane;
+                if (cc < next_c) {
+                  const uint32_t slot = cc & (RREC - 1);
+                  const uint4 ra = S.recA[slot];
+                  if (ra.w) {
+                    atomicMin(&S.rb[(ra.z >> 16) & 63], ra.x);
+                    S.recA[slot].w = 0;
+                  }
+                }
+              }
+              __syncthreads();
+              if (S.rb[lane] != NONE) {
+                stg_w = S.rb[lane];
+                S.rb[lane] = NONE;
+              }
+              barrier = newb;
+              next_c = newb + 1;
+            }
+          }
+          // finished chains from cp on, in pop order
+          uint32_t ndone = 0;
+          for (uint32_t base = cp; base < next_c; base += 64) {
+            const uint32_t cc = base + lane;
+            const bool dn = cc < next_c && S.recA[cc & (RREC - 1)].w != 0u;
+            const unsigned long long dm = __ballot(dn);
+            const uint32_t run = dm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~dm);
+            ndone += run;
+            if (run < 64) break;
+          }
+          // (b) commit the finished prefix (in pop order): at least 32 chains, or all there is
+          const unsigned long long active = __ballot(lst != L_IDLE);
+          uint32_t lim = ndone;
+          if (barrier != NONE && lim > barrier + 1 - cp) lim = barrier + 1 - cp;
+          const bool at_barrier = barrier != NONE && cp + lim == barrier + 1;
+          if (lim && (lim >= 32 || active == 0ull || at_barrier)) {
+            __threadfence_block();  // staging stores of earlier iterations are visible
+            for (uint32_t base = 0; base < lim && !done; base += 64) {
+              const uint32_t cc = cp + base + lane;
+              const bool v = base + lane < lim;
+              const uint4 ra = v ? S.recA[cc & (RREC - 1)] : make_uint4(0, 0, 0, 0);
+              const uint32_t n0 = ra.y & 0xffffu, n1 = ra.y >> 16, n2 = ra.z & 0xffffu;
+              const uint32_t tot = n0 + n1 + n2;
+              // n_entries before each pop of this chain <= n_c + tot (bwtgap.c:139)
+              uint32_t dsum = 0;
+              const uint32_t pre = wave_excl(v ? tot : 0u, lane, dsum);
+              const uint32_t nc = n_live + pre - (uint32_t)lane;  // each earlier chain popped one entry
+              if (__ballot(v && nc + tot > (uint32_t)o.max_entries)) {
+                status = ST_STACK_OVERFLOW | 2u << 8;
+                done = true;
+                break;
+              }
+              const uint32_t nv = (lim - base) < 64 ? (lim - base) : 64;
+              n_live = n_live + dsum - nv;
+              uint32_t T0 = 0, T1 = 0, T2 = 0;
+              const uint32_t o0 = wave_excl(n0, lane, T0);
+              const uint32_t o1 = wave_excl(n1, lane, T1);
+              const uint32_t o2 = wave_excl(n2, lane, T2);
+              auto Tq = [&](int q) __attribute__((always_inline)) { return q == 0 ? T0 : q == 1 ? T1 : T2; };
+              // pages for the targets
+              bool bad = false;
+              uint32_t why = 0;
+              for (int q = 0; q < 3; ++q) {
+                if (!Tq(q)) continue;
+                const int tb = tg(q);
+                if (tb >= o.n_stacks) { bad = true; continue; }
+                const uint32_t need = (S.nb[tb] + Tq(q) + COOP_PG - 1) >> COOP_PG_LOG2;
+                if (need > MAXP) { bad = true; why = 4; continue; }
+                for (uint32_t pq = S.np[tb]; pq < need; ++pq) {
+                  const uint32_t p = alloc_page();
+                  if (p == NONE) { bad = true; why = 3; break; }
+                  if (lane == 0) {
+                    S.dirc[1 + q][pq] = p;
+                    dir[tb * MAXP + pq] = p;
+                  }
+                  S.np[tb] = pq + 1;  // same value from every lane
+                }
+              }
+              if (bad) {
+                // a score past the last bucket is an option error; the rest is storage
+                status = (T0 && t0 >= o.n_stacks) || (T1 && t1 >= o.n_stacks) || (T2 && t2 >= o.n_stacks)
+                             ? ST_BAD_SCORE : ST_STACK_OVERFLOW | why << 8;
+                done = true;
+                break;
+              }
+              __syncthreads();
+              // copy: the batch's children, flattened, 64 per round trip and four round trips'
+              // loads in flight; child g belongs to chain j with pre_j <= g < pre_j + tot_j
+              // (binary search over the lanes' prefixes) and goes to its category's bucket at
+              // (bucket size) + (chain's offset in the batch) + (its rank in the chain)
+              {
+                const uint32_t my_rl = (ra.z >> 16) & 63, my_st = ra.x;
+                const uint32_t nb0 = S.nb[t0], nb1 = t1 < o.n_stacks ? S.nb[t1] : 0u,
+                               nb2 = t2 < o.n_stacks ? S.nb[t2] : 0u;
+                for (uint32_t g0 = 0; g0 < dsum; g0 += 256) {
+                  uint4 e[4];
+                  uint32_t f0[4], f1[4], f2[4];
+#pragma unroll
+                  for (int u = 0; u < 4; ++u) {
+                    const uint32_t g = g0 + 64u * u + (uint32_t)lane;
+                    int j = 0;
+#pragma unroll
+                    for (int step = 32; step >= 1; step >>= 1) {
+                      const uint32_t pm = __shfl(pre, j + step);
+                      if (pm <= g) j += step;
+                    }
+                    const uint32_t x = g - __shfl(pre, j);
+                    const uint32_t rl = __shfl(my_rl, j), st0 = __shfl(my_st, j);
+                    f0[u] = nb0 + __shfl(o0, j);
+                    f1[u] = nb1 + __shfl(o1, j);
+                    f2[u] = nb2 + __shfl(o2, j);
+                    e[u] = make_uint4(0, 0, 0, 0);
+                    if (g < dsum) e[u] = stg_base[((uint64_t)rl << A.stg_log2) + ((st0 + x) & SMASK)];
+                  }
+#pragma unroll
+                  for (int u = 0; u < 4; ++u) {
+                    if (g0 + 64u * u + (uint32_t)lane < dsum) {
+                      const uint32_t q = (e[u].w >> 27) & 3u, rk = e[u].z >> 20;
+                      const uint32_t pos = (q == 0 ? f0[u] : q == 1 ? f1[u] : f2[u]) + rk;
+                      const uint32_t pg = S.dirc[1 + q][pos >> COOP_PG_LOG2];
+                      A.pool[((uint64_t)pg << COOP_PG_LOG2) + (pos & (COOP_PG - 1))] = e[u];
+                    }
+                  }
+                }
+                if (v && tot) atomicMax(&S.head[my_rl], my_st + tot);
+              }
+              if (v) S.recA[cc & (RREC - 1)].w = 0;
+              __syncthreads();
+              if (lane == 0) {
+                S.nb[t0] += T0;
+                if (q1 == 1) S.nb[t1] += T1;
+                if (q2 == 2) S.nb[t2] += T2;
+              }
+              __syncthreads();
+            }
+            if (done) break;
+            cp += lim;
+            if (at_barrier) {
+              // ---- the hit of chain `barrier` (bwtgap.c:165-197)
+              const uint4 hb = S.recB[barrier & (RREC - 1)];
+              const uint32_t hk = hb.x, hl = hb.y;
+              const int h_mm = (int)(hb.z & 0xff), h_go = (int)((hb.z >> 8) & 0xff), h_ge = (int)((hb.z >> 16) & 0xff);
+              const int h_a = (int)((hb.z >> 24) & 1), h_ldp = (int)hb.w;
+              const int score = h_mm * o.s_mm + h_go * o.s_gapo + h_ge * o.s_gape;
+              barrier = NONE;
+              if (n_aln == 0) {
+                best_score = score;
+                int best_diff = h_mm + h_go;
+                if (gape) best_diff += h_ge;
+                if (!(o.mode & MODE_NONSTOP)) max_diff = (best_diff + 1 > opt_max_diff) ? opt_max_diff : best_diff + 1;
+              }
+              if (score == best_score) {
+                best_cnt = (int)((uint32_t)best_cnt + (hl - hk + 1));
+              } else if (best_cnt > o.max_top2) {
+                done = true;  // :185
+                break;
+              }
+              bool add = true;
+              if (h_go) {
+                bool dup = false;
+                for (int j = lane; j < n_aln; j += 64) {
+                  const uint4 h = hitv[j];
+                  dup |= h.y == hk && h.z == hl;
+                }
+                add = __ballot(dup) == 0ull;
+              }
+              if (add) {
+                // gap_shadow (bwtgap.c:81-91) on strand h_a's widths, 64 positions at a time
+                const uint32_t x = hl - hk + 1, mx = ixv0.seq_len;
+                uint32_t jrun = 0;
+                for (int base = 0; base < h_ldp; base += 64) {
+                  const int q = base + lane;
+                  uint2 w = q < h_ldp ? S.W[h_a][q] : make_uint2(0, 0);
+                  const bool eq = q < h_ldp && w.x == x;
+                  const unsigned long long em = __ballot(eq);
+                  if (q < h_ldp) {
+                    if (w.x > x) {
+                      w.x -= x;
+                      S.W[h_a][q] = w;
+                    } else if (eq) {
+                      const uint32_t jj = jrun + (uint32_t)__popcll(em & ((1ull << lane) - 1ull)) + 1u;
+                      S.W[h_a][q] = make_uint2(mx - jj, 1u);
+                    }
+                  }
+                  jrun += (uint32_t)__popcll(em);
+                }
+                if ((uint32_t)n_aln >= A.hcap) {
+                  status = ST_ALN_OVERFLOW;
+                  done = true;
+                  break;
+                }
+                if (lane == 0)
+                  hitv[n_aln] = make_uint4((uint32_t)h_mm | (uint32_t)h_go << 8 | (uint32_t)h_ge << 16 |
+                                               (uint32_t)h_a << 24, hk, hl, (uint32_t)score);
+                ++n_aln;
+                __threadfence_block();
+                __syncthreads();
+              }
+            }
+          }
+          // (c) level finished
+          if (cp == N && __ballot(lst != L_IDLE) == 0ull) break;
+          // (d) claims: idle lanes take the next chains in pop order
+          {
+            const uint32_t ch_max = 9u * (uint32_t)(len + 1) + 16u;
+            const bool want = lst == L_IDLE && barrier == NONE && STG - (stg_w - S.head[lane]) >= ch_max;
+            const unsigned long long wm = __ballot(want);
+            const uint32_t cap_c = cp + RREC < N ? cp + RREC : N;
+            const uint32_t avail = cap_c > next_c ? cap_c - next_c : 0u;
+            const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
+            if (want && rank < avail) {
+              c = next_c + rank;
+              cstart = stg_w;
+              cnt0 = cnt1 = cnt2 = 0;
+              const uint32_t idx = N - 1u - c;  // LIFO: chain 0 is the top of the bucket
+              ent_page = S.dirc[0][idx >> COOP_PG_LOG2];
+              ent_off = idx & (COOP_PG - 1);
+              lst = L_FETCH;
+            }
+            const uint32_t nw = (uint32_t)__popcll(wm);
+            next_c += nw < avail ? nw : avail;
+          }
+          // ============================================ loads of this iteration (one round trip)
+          const IndexView ix = a ? ixv0 : ixv1;  // strand a searches bwt[1-a]
+          const uint4 *ob = a ? A.o64[0] : A.o64[1];
+          uint4 ent = make_uint4(0, 0, 0, 0);
+          if (lst == L_FETCH) ent = A.pool[((uint64_t)ent_page << COOP_PG_LOG2) + ent_off];
+          const bool exp = lst == L_EXP;
+          const bool tail = lst == L_TAIL;
+          const uint32_t qk = tail ? xk : k, ql = tail ? xl : l;
+          const bool qkneg = qk == 0;
+          const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
+          Blk bk, bl;
+          load_blk(ob, ql, exp, bl);
+          load_blk(ob, qk - 1, exp && !qkneg && !qshare, bk);
+          const uint32_t tsym = tail ? S.str[a][xj] : 0u;
+          uint4 tvl = make_uint4(0, 0, 0, 0), tvk = make_uint4(0, 0, 0, 0);
+          if (tail) tvl = ob[(size_t)(ql >> 6) * 4 + tsym];
+          if (tail && !qkneg && !qshare) tvk = ob[(size_t)((qk - 1) >> 6) * 4 + tsym];
+
+          // ============================================ consume
+          if (lst == L_FETCH) {
+            k = ent.x;
+            l = ent.y;
+            i = (int)(ent.z & 0x3ff);
+            ldp = (int)((ent.z >> 10) & 0x3ff);
+            e_mm = (int)(ent.w & 0xff);
+            e_go = (int)((ent.w >> 8) & 0xff);
+            e_ge = (int)((ent.w >> 16) & 0xff);
+            a = (int)((ent.w >> 24) & 1);
+            state = (int)((ent.w >> 25) & 3);
+            pop_node();
+          } else if (tail) {
+            // one step of bwt_match_exact_alt (bwt.c:240-247)
+            if (qshare) tvk = tvl;
+            const uint32_t ok = qkneg ? 0u : occ_of(tvk, qk - 1), ol = occ_of(tvl, ql);
+            const uint32_t base = l2of(ix, tsym);
+            xk = base + ok + 1;
+            xl = base + ol;
+            if (xk > xl) {
+              end_chain(false, 0, 0);
+            } else if (--xj < 0) {
+              end_chain(true, xk, xl);
+            } else if (S.str[a][xj] > 3) {
+              end_chain(false, 0, 0);
+            }
+          } else if (exp) {
+            // ---- expansion (bwtgap.c:200-258); the match child continues the chain
+            if (qshare) bk = bl;
+            uint4 KK, LL;
+            {
+              const uint4 cl4 = make_uint4(occ_of(bl.v0, ql), occ_of(bl.v1, ql), occ_of(bl.v2, ql), occ_of(bl.v3, ql));
+              const uint4 ck4 = qkneg ? make_uint4(0, 0, 0, 0)
+                                      : make_uint4(occ_of(bk.v0, qk - 1), occ_of(bk.v1, qk - 1), occ_of(bk.v2, qk - 1),
+                                                   occ_of(bk.v3, qk - 1));
+              KK = make_uint4(ix.L2[0] + ck4.x + 1, ix.L2[1] + ck4.y + 1, ix.L2[2] + ck4.z + 1, ix.L2[3] + ck4.w + 1);
+              LL = make_uint4(ix.L2[0] + cl4.x, ix.L2[1] + cl4.y, ix.L2[2] + cl4.z, ix.L2[3] + cl4.w);
+            }
+            int m = max_diff - (e_mm + e_go);
+            if (gape) m -= e_ge;
+            int m_seed = 0;
+            if (seeded) {
+              m_seed = o.max_seed_diff - (e_mm + e_go);
+              if (gape) m_seed -= e_ge;
+            }
+            const int ni = i - 1;
+            const uint32_t csym = S.str[a][ni];
+            const uint32_t occ = l - k + 1;
+            bool allow_diff = true, allow_M = true;
+            if (ni > 0) {
+              const uint2 w_im2 = S.W[a][ni - 1], w_im1 = S.W[a][ni];
+              if ((int)w_im2.y > m - 1) allow_diff = false;
+              else if ((int)w_im2.y == m - 1 && (int)w_im1.y == m - 1 && w_im2.x == w_im1.x) allow_M = false;
+              const int ii = ni - (len - o.seed_len);
+              if (seeded && ii > 0) {
+                const uint2 sw_lo = S.SW[a][ii - 1], sw_hi = S.SW[a][ii];
+                if ((int)sw_lo.y > m_seed - 1) allow_diff = false;
+                else if ((int)sw_lo.y == m_seed - 1 && (int)sw_hi.y == m_seed - 1 && sw_lo.x == sw_hi.x) allow_M = false;
+              }
+            }
+            const uint32_t ne4 = (KK.x <= LL.x ? 1u : 0u) | (KK.y <= LL.y ? 2u : 0u) | (KK.z <= LL.z ? 4u : 0u) |
+                                 (KK.w <= LL.w ? 8u : 0u);
+            const int tmp = (o.mode & MODE_LOGGAP) ? int_log2((uint32_t)(e_ge + e_go)) / 2 + 1 : e_go + e_ge;
+            uint32_t vm = 0;
+            if (allow_diff && ni >= o.indel_end_skip + tmp && len - ni >= o.indel_end_skip + tmp) {
+              if (state == STATE_M) {
+                if (e_go < o.max_gapo) vm = 1u | ne4 << 1;
+              } else if (state == STATE_I) {
+                if (e_ge < o.max_gape) vm = 1u;
+              } else if (state == STATE_D) {
+                if (e_ge < o.max_gape && (e_ge + e_go < max_diff || occ < (uint32_t)o.max_del_occ)) vm = ne4 << 1;
+              }
+            }
+            const uint32_t rot = (csym + 1) & 3;
+            const uint32_t ner = ((ne4 >> rot) | (ne4 << (4 - rot))) & 15u;
+            if (allow_diff && allow_M) vm |= ner << 5;
+            else if (csym < 4) vm |= ner & 8u ? 1u << 8 : 0u;
+            // bit 8 with csym < 4 is the match child: it continues the chain instead of being staged
+            const bool match = (vm >> 8) & 1u && csym < 4;
+            if (match) vm &= ~(1u << 8);
+            const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
+            const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
+            while (vm) {
+              const uint32_t j = (uint32_t)__builtin_ctz(vm);
+              vm &= vm - 1;
+              const bool is_ins = j == 0, is_del = j - 1 < 4, is_sym = j >= 5;
+              const uint32_t cc = is_del ? j - 1 : (csym + j - 4) & 3;
+              const uint32_t pk = is_ins ? k : pick4(KK, cc);
+              const uint32_t pl = is_ins ? l : pick4(LL, cc);
+              const bool open = !is_sym && state == STATE_M;
+              const int n_mm = e_mm + (is_sym ? 1 : 0);  // staged symbol children are mismatches
+              const int n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (!is_sym && !open ? 1 : 0);
+              const int pi = is_del ? ni + 1 : ni;
+              const int pstate = is_ins ? STATE_I : is_del ? STATE_D : STATE_M;
+              const int sc = sc_base + (is_sym ? o.s_mm : sc_gap);
+              const int q = sc == t0 ? 0 : sc == t1 ? q1 : q2;
+              const uint32_t rk = q == 0 ? cnt0++ : q == 1 ? cnt1++ : cnt2++;
+              stg[(stg_w++) & SMASK] = mk_ent(pk, pl, pi, pi, n_mm, n_gapo, n_gape, a, pstate, (uint32_t)q, rk);
+            }
+            if (match) {
+              k = pick4(KK, csym);
+              l = pick4(LL, csym);
+              i = ni;
+              state = STATE_M;
+              pop_node();
+            } else {
+              end_chain(false, 0, 0);
+            }
+          }
+        }
+        if (done) break;
+        // level s is consumed: its pages go back
+        free_pages(S.np[s], S.dirc[0]);
+        __syncthreads();
+        if (lane == 0) {
+          S.nb[s] = 0;
+          S.np[s] = 0;
+        }
+        __syncthreads();
+        ++s;
+      }
+      // every bucket's pages go back (termination leaves entries behind)
+      for (int b = 0; b < o.n_stacks; ++b) {
+        const uint32_t npg = S.np[b];
+        if (npg) {
+          const uint32_t room = A.freecap - n_free;
+          const uint32_t nf = npg < room ? npg : room;
+          for (uint32_t j = lane; j < nf; j += 64) freel[n_free + j] = dir[b * MAXP + j];
+          n_free += nf;
+        }
+      }
+      __syncthreads();
+    }
+    // ------------------------------------------------ hits of the read to the stream
+    int na = status ? 0 : n_aln;
+    if (na) {
+      unsigned long long pos = 0;
+      if (lane == 0) pos = atomicAdd(A.aln_next, (unsigned long long)na);
+      pos = __shfl(pos, 0);
+      if (pos + (unsigned long long)na > A.aln_total) {
+        status |= ST_ALN_OVERFLOW;
+        na = 0;
+      } else {
+        __threadfence_block();
+        for (int j = lane; j < na; j += 64) A.aln[pos + j] = hitv[j];
+        if (lane == 0) A.aln_off[ro] = pos;
+      }
+    }
+    if (lane == 0) {
+      A.n_aln[ro] = na;
+      A.status[ro] = status;
+      if (A.iters) A.iters[ro] = n_iter;
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {
+  if (g.n <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(g.pool_next, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_coop, dim3(blocks), dim3(64), 0, st, g, d_counter);
+  return hipGetLastError();
+}
+
+}  // namespace ibwa

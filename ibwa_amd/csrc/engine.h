@@ -87,6 +87,48 @@ size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int p
 hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int blocks, int block, bool wide,
                          hipStream_t st);
 
+// Wave-cooperative gapped search for heavy reads (coop.hip): one read per wavefront,
+// its match chains run across the lanes and committed in the reference's pop order.
+constexpr int COOP_MAXLEN = 256;       // longest read the kernel takes (LDS strands / widths)
+constexpr int COOP_PG_LOG2 = 13;       // bucket pages of 8192 entries (128 KiB): 256 pages hold 2M entries
+constexpr uint32_t COOP_PG = 1u << COOP_PG_LOG2;
+constexpr int COOP_NSTK = 128, COOP_MAXP = 256;
+struct CoopArgs {
+  IndexView ix[2];
+  const uint4 *o64[2];
+  const uint8_t *seq;
+  const uint64_t *off;
+  const uint32_t *len;
+  const int64_t *ids;        // read r of this launch -> input read (nullptr: identity)
+  int64_t n;
+  int out_by_id;
+  const int16_t *maxdiff_tab;
+  const uint2 *wbuf;         // widths of read r at wbuf + r * wstride (k_width)
+  uint64_t wstride;
+  uint32_t wlen1;
+  const uint16_t *nN;
+  uint4 *stg;                // per-lane staging rings, 2^stg_log2 entries each, 64 lanes per wave
+  uint32_t stg_log2;
+  uint32_t *dir;             // per-wave page directories [COOP_NSTK][COOP_MAXP]
+  uint32_t *freel;           // per-wave free page stacks [freecap]
+  uint32_t freecap;
+  uint4 *pool;               // bucket pages (COOP_PG entries each)
+  uint32_t pool_pages;
+  uint32_t *pool_next;       // global bump pointer into the pool (zeroed per launch)
+  uint4 *hits;               // per-wave hit lists [hcap]
+  uint32_t hcap;
+  uint32_t max_iters;        // runaway guard (loop iterations per read)
+  uint4 *aln;                // hit stream
+  unsigned long long aln_total;
+  unsigned long long *aln_next;
+  uint64_t *aln_off;
+  int32_t *n_aln;
+  uint32_t *status;
+  uint32_t *iters;
+  AlnOpt o;
+};
+hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);
+
 // Kernel arguments of the exact-match path: only what it reads (fewer SGPRs).
 struct ExactArgs {
   IndexView ix[2];

@@ -111,8 +111,13 @@ struct ibwa_ctx {
   int gap_pages_per_block = 384;      // 128 KiB pages per 256-lane workgroup pool
   uint32_t gap_hit_slots = 256;      // hits a read may hold in the first pass
   int64_t gap_reads_per_chunk = 1 << 22;
-  uint32_t gap_iter_budget = 0;      // first-pass iterations per read before handing it to the retry pass
+  uint32_t gap_iter_budget = 4000;   // first-pass iterations per read before handing it to the coop pass
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
+  // wave-cooperative heavy-read pass (coop.hip)
+  int gap_coop = 1;
+  int coop_waves_per_cu = 7;         // 22.5 KiB of LDS and 173 VGPRs per wave
+  int coop_pool_gb = 16;             // bucket page pool
+  DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next;
   bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
   bool verbose = getenv("IBWA_VERBOSE") != nullptr;
   bool prof_phases = getenv("IBWA_PROF_PHASES") != nullptr;  // diagnostics kernel variant
@@ -271,6 +276,9 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_reads_per_chunk" && value > 0) c->gap_reads_per_chunk = value;
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
+  else if (k == "gap_coop") c->gap_coop = value != 0;
+  else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
+  else if (k == "coop_pool_gb" && value > 0 && value <= 256) c->coop_pool_gb = (int)value;
   else return fail(IBWA_EINVAL, "unknown option %s", k.c_str());
   return 0;
 }
@@ -364,7 +372,9 @@ int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa
   bool keep_full = c->exact_jump != 0;
   if (keep_full) {
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || (double)free_b < 0.6 * total_b) keep_full = false;
+    // the kept arrays (16.5 B per base) plus the builder's sort temporaries (~45 B per base)
+    // and headroom must fit in what is free now
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || (double)free_b < (double)n * 61.5 + 4e9) keep_full = false;
     if ((double)n * 16.5 > 0.3 * (double)total_b) keep_full = false;
   }
   if (!keep_full)
@@ -761,6 +771,127 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   std::vector<int64_t> where(todo.size());
   for (size_t j = 0; j < todo.size(); ++j) where[j] = (int64_t)j;
   float ms_r = 0;
+  // heavy and overflowing reads: the wave-cooperative kernel first (exact; whatever it cannot
+  // hold is flagged and continues below)
+  if (v2 && c->gap_coop && !todo.empty() && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK) {
+    const int64_t lanes = (int64_t)todo.size();
+    uint32_t stg_log2 = 10;
+    while ((1u << stg_log2) < 2u * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
+    const int blocks = c->n_cus * c->coop_waves_per_cu;
+    const uint32_t freecap = 4096, hcap = 4096;
+    const uint32_t pool_pages = (uint32_t)(((uint64_t)c->coop_pool_gb << 30) / (COOP_PG * 16ull));
+    const uint64_t r_total = (uint64_t)lanes * 64 + (1u << 20);
+    if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
+    if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
+    if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
+    if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
+    if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
+    if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
+    if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
+    if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
+    if (int rc = c->c_next.ensure(64)) return rc;
+    if (int rc = c->r_aln.ensure(r_total * 16)) return rc;
+    if (int rc = c->r_aoff.ensure(lanes * 8)) return rc;
+    if (int rc = c->r_naln.ensure(lanes * 4)) return rc;
+    if (int rc = c->r_status.ensure(lanes * 4)) return rc;
+    if (int rc = c->d_counter.ensure(64)) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_ids.p, todo.data(), lanes * 8, hipMemcpyHostToDevice, c->stream));
+    AlnArgs B = A;
+    B.ids = c->d_ids.as<int64_t>();
+    B.n = lanes;
+    B.wbuf = c->d_wbuf.as<uint2>();
+    B.nN = c->d_nN.as<uint16_t>();
+    CoopArgs K = {};
+    K.ix[0] = c->ix[0];
+    K.ix[1] = c->ix[1];
+    K.o64[0] = c->o64[0].as<uint4>();
+    K.o64[1] = c->o64[1].as<uint4>();
+    K.seq = A.seq;
+    K.off = A.off;
+    K.len = A.len;
+    K.ids = B.ids;
+    K.n = lanes;
+    K.out_by_id = 0;
+    K.maxdiff_tab = A.maxdiff_tab;
+    K.wbuf = B.wbuf;
+    K.wstride = A.wstride;
+    K.wlen1 = A.wlen1;
+    K.nN = B.nN;
+    K.stg = c->c_stg.as<uint4>();
+    K.stg_log2 = stg_log2;
+    K.dir = c->c_dir.as<uint32_t>();
+    K.freel = c->c_free.as<uint32_t>();
+    K.freecap = freecap;
+    K.pool = c->c_pool.as<uint4>();
+    K.pool_pages = pool_pages;
+    K.pool_next = c->c_next.as<uint32_t>();
+    K.hits = c->c_hits.as<uint4>();
+    K.hcap = hcap;
+    K.max_iters = 1u << 24;  // runaway guard; a read past it goes to the sequential kernel
+    K.aln = c->r_aln.as<uint4>();
+    K.aln_total = r_total;
+    K.aln_next = c->d_counter.as<unsigned long long>() + 2;
+    K.aln_off = c->r_aoff.as<uint64_t>();
+    K.n_aln = c->r_naln.as<int32_t>();
+    K.status = c->r_status.as<uint32_t>();
+    if (c->verbose) {
+      if (int rc = c->d_iters.ensure(lanes * 4)) return rc;
+      K.iters = c->d_iters.as<uint32_t>();
+    }
+    K.o = o;
+    HIPCHK(hipMemsetAsync(K.aln_next, 0, 8, c->stream));
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(launch_width(B, c->block, c->stream));
+    HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
+    HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[4]));
+    float a = 0;
+    HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
+    ms_r += a;
+    std::vector<int32_t> rn(lanes);
+    std::vector<uint32_t> rs(lanes);
+    std::vector<uint64_t> ro(lanes);
+    unsigned long long used = 0;
+    HIPCHK(hipMemcpyAsync(rn.data(), c->r_naln.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(ro.data(), c->r_aoff.p, lanes * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&used, K.aln_next, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<uint4> ra(std::min<unsigned long long>(used, r_total));
+    if (!ra.empty()) HIPCHK(hipMemcpy(ra.data(), c->r_aln.p, ra.size() * 16, hipMemcpyDeviceToHost));
+    std::vector<int64_t> next, next_where;
+    for (int64_t j = 0; j < lanes; ++j) {
+      if (rs[j] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "score outside the stack range");
+      if (rs[j]) {
+        next.push_back(todo[j]);
+        next_where.push_back(where[j]);
+        continue;
+      }
+      const uint64_t first = rn[j] ? ro[j] : 0;
+      found[where[j]].assign(ra.begin() + first, ra.begin() + first + rn[j]);
+    }
+    if (c->verbose) {
+      uint32_t mx = 0;
+      if (K.iters) {
+        std::vector<uint32_t> it(lanes);
+        HIPCHK(hipMemcpy(it.data(), K.iters, lanes * 4, hipMemcpyDeviceToHost));
+        mx = *std::max_element(it.begin(), it.end());
+      }
+      uint32_t pages = 0;
+      HIPCHK(hipMemcpy(&pages, K.pool_next, 4, hipMemcpyDeviceToHost));
+      int why[8] = {0};
+      for (int64_t j = 0; j < lanes; ++j)
+        if (rs[j]) ++why[(rs[j] >> 8) & 7];
+      fprintf(stderr, "[ibwa_amd] coop hand-on reasons: len %d, max_entries %d, pool %d, bucket pages %d, guard %d\n",
+              why[1], why[2], why[3], why[4], why[5]);
+      fprintf(stderr, "[ibwa_amd] coop pass: %lld reads, %zu handed on, max %u wave iterations, %u pages, %.1f ms\n",
+              (long long)lanes, next.size(), mx, pages, a);
+    }
+    c->stats.n_coop = lanes - (int64_t)next.size();
+    c->stats.ms_coop = a;
+    todo.swap(next);
+    where.swap(next_where);
+  }
   // first two retry rounds: the persistent gapped kernel with 24-bit slot links and one
   // large static region per read (4 MiB, then 64 MiB; reads < 4096 bp); then the general kernels
   int wide_rounds = v2 && max_len < 4096 ? 2 : 0;

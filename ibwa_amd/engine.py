@@ -29,7 +29,8 @@ class RunStats(c.Structure):
     _fields_ = [("ms_width", c.c_double), ("ms_search", c.c_double), ("ms_retry", c.c_double),
                 ("ms_total", c.c_double), ("n_retry", c.c_int64), ("n_launch_width", c.c_int64),
                 ("n_launch_search", c.c_int64), ("path", c.c_int), ("kmer_k", c.c_int),
-                ("n_stack_overflow", c.c_int64), ("n_aln_overflow", c.c_int64), ("n_heavy", c.c_int64), ("ms_sw", c.c_double)]
+                ("n_stack_overflow", c.c_int64), ("n_aln_overflow", c.c_int64), ("n_heavy", c.c_int64), ("ms_sw", c.c_double),
+                ("n_coop", c.c_int64), ("ms_coop", c.c_double)]
 
 
 assert c.sizeof(GapOpt) == 64

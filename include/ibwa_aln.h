@@ -121,6 +121,8 @@ typedef struct {
 	int64_t n_aln_overflow;    /* first-pass reads whose hits did not fit (re-run) */
 	int64_t n_heavy;           /* first-pass reads over the iteration budget (re-run) */
 	double ms_sw;              /* last ibwa_sw_batch kernel time */
+	int64_t n_coop;            /* heavy reads the wave-cooperative pass resolved */
+	double ms_coop;            /* its time (width + search), part of ms_retry */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 

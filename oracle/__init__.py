@@ -230,7 +230,10 @@ def encode_reads(recs, mode, trim_qual):
 
 
 STATS_DTYPE = np.dtype([("pushes", "<u4"), ("pops", "<u4"), ("peak_entries", "<u4"), ("peak_bucket", "<u4"),
-                        ("n_aln", "<u4"), ("touches", "<u4"), ("peak_real", "<u4")])
+                        ("n_aln", "<u4"), ("touches", "<u4"), ("peak_real", "<u4"), ("tails", "<u4"),
+                        ("tail_steps", "<u4"), ("pruned_m", "<u4"), ("pruned_w", "<u4"), ("expansions", "<u4"),
+                        ("hits", "<u4"), ("distinct_exp", "<u4"), ("chains", "<u4"), ("rounds", "<u4"),
+                        ("rounds_g4", "<u4"), ("rounds_g16", "<u4"), ("rounds_lvl", "<u4")])
 
 
 def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False, stats=None):

@@ -199,13 +199,15 @@ void or_2occ4(const or_bwt_t *b, uint32_t k, uint32_t l, uint32_t ck[4], uint32_
 }
 
 /* bwt.c:235-250: continue an exact backward search over str[0..len-1] */
-static int match_exact_alt(const or_bwt_t *b, int len, const uint8_t *str, uint32_t *k0, uint32_t *l0, uint32_t *t)
+static int match_exact_alt_n(const or_bwt_t *b, int len, const uint8_t *str, uint32_t *k0, uint32_t *l0, uint32_t *t,
+                             uint32_t *steps)
 {
 	int i;
 	uint32_t k = *k0, l = *l0, ok, ol;
 	for (i = len - 1; i >= 0; --i) {
 		int c = str[i];
 		if (c > 3) return 0;
+		if (steps) ++*steps;
 		twoocc_t(b, k - 1, l, c, &ok, &ol, t);
 		k = b->L2[c] + ok + 1;
 		l = b->L2[c] + ol;
@@ -213,6 +215,11 @@ static int match_exact_alt(const or_bwt_t *b, int len, const uint8_t *str, uint3
 	}
 	*k0 = k; *l0 = l;
 	return (int)(l - k + 1);
+}
+
+static int match_exact_alt(const or_bwt_t *b, int len, const uint8_t *str, uint32_t *k0, uint32_t *l0, uint32_t *t)
+{
+	return match_exact_alt_n(b, len, str, k0, l0, t, 0);
 }
 
 /* ---------------- options (bwtaln.c:21-51) ---------------- */
@@ -275,17 +282,30 @@ typedef struct {
 	uint32_t k, l;
 	int i, a, state, n_mm, n_gapo, n_gape, last_diff_pos, score;
 	int phantom; /* instrumentation: can never be expanded (see gs_push) */
+	int mc;      /* instrumentation: a match child (popped right after its parent's expansion) */
 } entry_t;
 
 typedef struct { int n, m; entry_t *e; } bucket_t;
+#define OR_CHAIN_W 64
 typedef struct {
 	int n_stacks, best, n_entries; bucket_t *b; uint32_t pushes, pops, peak, peak_bucket;
 	/* instrumentation: entries that can still be expanded when pushed */
 	int md_now, score_cap, gape; uint32_t n_real, peak_real;
+	/* search-shape counters (tools/dfs_stats.py) */
+	uint32_t tails, tail_steps, pruned_m, pruned_w, expansions, hits;
+	/* match chains (a popped non-match-child entry and its run of match children + tail):
+	 * rounds = sum over windows of W consecutive chains of one level of the longest chain */
+	uint32_t chains, rounds, next_mc, ch_len, win_n, win_max, win_level;
+	uint32_t *chl, chl_n, chl_m; /* chain (length << 11 | level) in pop order, when stats are on */
+	uint64_t *hset; uint32_t hcap, hn; /* distinct (a,i,k,l) expansions, when stats are on */
 } gstack_t;
 
 /* per-read search statistics (test/bench instrumentation only) */
-typedef struct { uint32_t pushes, pops, peak_entries, peak_bucket, n_aln, touches, peak_real; } or_stats_t;
+typedef struct {
+	uint32_t pushes, pops, peak_entries, peak_bucket, n_aln, touches, peak_real;
+	uint32_t tails, tail_steps, pruned_m, pruned_w, expansions, hits, distinct_exp, chains, rounds;
+	uint32_t rounds_g4, rounds_g16, rounds_lvl;
+} or_stats_t;
 static or_stats_t *g_stats_next; /* consumed by the next or_cal_sa_reg_gap call */
 void or_set_stats(or_stats_t *buf) { g_stats_next = buf; }
 
@@ -308,7 +328,7 @@ static void gs_free(gstack_t *s)
 {
 	int i;
 	for (i = 0; i < s->n_stacks; ++i) free(s->b[i].e);
-	free(s->b); free(s);
+	free(s->hset); free(s->chl); free(s->b); free(s);
 }
 
 static void gs_reset(gstack_t *s)
@@ -319,6 +339,35 @@ static void gs_reset(gstack_t *s)
 	s->n_entries = 0;
 	s->pushes = s->pops = s->peak = s->peak_bucket = 0;
 	s->n_real = s->peak_real = 0;
+	s->tails = s->tail_steps = s->pruned_m = s->pruned_w = s->expansions = s->hits = 0;
+	s->chains = s->rounds = s->next_mc = s->ch_len = s->win_n = s->win_max = 0;
+	s->win_level = ~0u;
+	s->chl_n = 0;
+	if (s->hset) memset(s->hset, 0, (size_t)s->hcap * 8);
+	s->hn = 0;
+}
+
+/* distinct-expansion set (instrumentation): open addressing on a 64-bit mix of (a,i,k,l) */
+static void gs_note_exp(gstack_t *s, int a, int i, uint32_t k, uint32_t l)
+{
+	uint64_t h = ((uint64_t)k << 32 | l) * 0x9E3779B97F4A7C15ull ^ ((uint64_t)(i << 1 | a) + 1) * 0xC2B2AE3D27D4EB4Full;
+	uint32_t j;
+	if (!s->hset) return;
+	if (!h) h = 1;
+	if (2 * (s->hn + 1) > s->hcap) {
+		uint64_t *o = s->hset; uint32_t oc = s->hcap, q;
+		s->hcap = oc ? oc * 2 : 1024;
+		s->hset = (uint64_t*)calloc(s->hcap, 8);
+		s->hn = 0;
+		for (q = 0; q < oc; ++q) if (o[q]) {
+			for (j = (uint32_t)(o[q] >> 20) & (s->hcap - 1); s->hset[j]; j = (j + 1) & (s->hcap - 1));
+			s->hset[j] = o[q]; ++s->hn;
+		}
+		free(o);
+	}
+	for (j = (uint32_t)(h >> 20) & (s->hcap - 1); s->hset[j]; j = (j + 1) & (s->hcap - 1))
+		if (s->hset[j] == h) return;
+	s->hset[j] = h; ++s->hn;
 }
 
 /* bwtgap.c:45-64.  last_diff_pos: a non-diff push keeps the value already in
@@ -337,6 +386,7 @@ static void gs_push(gstack_t *s, int a, int i, uint32_t k, uint32_t l, int n_mm,
 	p->k = k; p->l = l; p->i = i & 0xffff; p->a = a; p->state = state;
 	p->n_mm = n_mm & 0xff; p->n_gapo = n_gapo & 0xff; p->n_gape = n_gape & 0xff;
 	p->last_diff_pos = ldp;
+	p->mc = s->next_mc; s->next_mc = 0;
 	p->score = score & 0x7ff; /* info = score<<21 keeps 11 bits */
 	/* phantom: more diffs than the (non-increasing) max_diff allows, or a score the
 	 * search stops at once a hit has fixed best_score -- such entries are only counted */
@@ -356,6 +406,21 @@ static void gs_pop(gstack_t *s, entry_t *e)
 	++s->pops;
 	*e = q->e[q->n - 1];
 	if (!e->phantom) --s->n_real;
+	if (!e->mc && s->hset) { /* a chain starts: record the previous one */
+		if (s->chains) {
+			if (s->chl_n == s->chl_m) { s->chl_m = s->chl_m ? s->chl_m * 2 : 4096; s->chl = (uint32_t*)realloc(s->chl, s->chl_m * 4); }
+			s->chl[s->chl_n++] = s->ch_len << 11 | s->win_level;
+		}
+	}
+	if (!e->mc) { /* a chain starts: close the previous one into its window */
+		if (s->ch_len > s->win_max) s->win_max = s->ch_len;
+		if (s->win_n && (s->win_n == OR_CHAIN_W || (uint32_t)e->score != s->win_level)) {
+			s->rounds += s->win_max; s->win_n = 0; s->win_max = 0;
+		}
+		if (s->ch_len == 0 && s->win_n == 0) s->win_max = 0;
+		++s->win_n; s->win_level = e->score; ++s->chains; s->ch_len = 0;
+	}
+	++s->ch_len;
 	--q->n;
 	--s->n_entries;
 	if (q->n == 0 && s->n_entries) {
@@ -423,22 +488,28 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 
 		m = max_diff - (e.n_mm + e.n_gapo);
 		if (opt->mode & OR_MODE_GAPE) m -= e.n_gape;
-		if (m < 0) continue;
+		if (m < 0) { ++stack->pruned_m; continue; }
 		bwt = bwts[1 - a]; str = seq[a]; width = w[a];
 		if (seed_w) {
 			sw = seed_w[a];
 			m_seed = opt->max_seed_diff - (e.n_mm + e.n_gapo);
 			if (opt->mode & OR_MODE_GAPE) m_seed -= e.n_gape;
 		}
-		if (i > 0 && m < width[i - 1].bid) continue;
+		if (i > 0 && m < width[i - 1].bid) { ++stack->pruned_w; continue; }
 
 		hit = 0;
 		if (i == 0) hit = 1;
 		else if (m == 0 && (e.state == ST_M || (opt->mode & OR_MODE_GAPE) || e.n_gape == opt->max_gape)) {
-			if (match_exact_alt(bwt, i, str, &k, &l, t)) hit = 1;
-			else continue;
+			++stack->tails;
+			{
+				uint32_t ts0 = stack->tail_steps;
+				hit = match_exact_alt_n(bwt, i, str, &k, &l, t, &stack->tail_steps) != 0;
+				stack->ch_len += stack->tail_steps - ts0;
+			}
+			if (!hit) continue;
 		}
 		if (hit) {
+			++stack->hits;
 			int score = SCORE(e.n_mm, e.n_gapo, e.n_gape, opt), do_add = 1;
 			if (out->n == 0) {
 				best_score = score;
@@ -472,6 +543,8 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 		}
 
 		--i;
+		++stack->expansions;
+		gs_note_exp(stack, a, i, k, l);
 		twoocc4_t(bwt, k - 1, l, ck, cl, t);
 		occ = l - k + 1;
 		allow_diff = allow_M = 1;
@@ -513,12 +586,14 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 				int c = (str[i] + j) & 3;
 				int is_mm = (j != 4 || str[i] > 3);
 				uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
+				stack->next_mc = !is_mm;
 				if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm + is_mm, e.n_gapo, e.n_gape, ST_M,
 				                      is_mm ? i : e.last_diff_pos, opt);
 			}
 		} else if (str[i] < 4) {
 			int c = str[i] & 3;
 			uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
+			stack->next_mc = 1;
 			if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm, e.n_gapo, e.n_gape, ST_M, e.last_diff_pos, opt);
 		}
 	}
@@ -612,6 +687,7 @@ static void *worker(void *data)
 	const or_gap_opt_t *opt = B->opt;
 	or_gap_opt_t local = B->base;
 	gstack_t *stack = gs_init(local.max_diff, local.max_gapo, local.max_gape, &local);
+	if (B->stats) { stack->hcap = 1024; stack->hset = (uint64_t*)calloc(1024, 8); }
 	width_t *w[2], *sw[2];
 	uint8_t *rseq = (uint8_t*)malloc(B->max_len + 1);
 	alnv_t out = {0, 0, 0};
@@ -653,6 +729,37 @@ static void *worker(void *data)
 				st->pushes = stack->pushes; st->pops = stack->pops; st->peak_entries = stack->peak;
 				st->peak_bucket = stack->peak_bucket; st->n_aln = out.n; st->touches = t;
 				st->peak_real = stack->peak_real;
+				st->tails = stack->tails; st->tail_steps = stack->tail_steps; st->pruned_m = stack->pruned_m;
+				st->pruned_w = stack->pruned_w; st->expansions = stack->expansions; st->hits = stack->hits;
+				st->distinct_exp = stack->hn;
+				if (stack->ch_len > stack->win_max) stack->win_max = stack->ch_len;
+				st->chains = stack->chains; st->rounds = stack->rounds + stack->win_max;
+				if (stack->chains) {
+					int gi;
+					if (stack->chl_n == stack->chl_m) { stack->chl_m = stack->chl_m ? stack->chl_m * 2 : 4096; stack->chl = (uint32_t*)realloc(stack->chl, stack->chl_m * 4); }
+					stack->chl[stack->chl_n++] = stack->ch_len << 11 | stack->win_level;
+					/* lanes take contiguous groups of g chains, 64 lanes per window, windows within a level */
+					for (gi = 0; gi < 3; ++gi) {
+						uint32_t g = gi == 0 ? 4 : gi == 1 ? 16 : 0, q = 0, tot = 0;
+						while (q < stack->chl_n) {
+							uint32_t lev = stack->chl[q] & 2047, e2 = q, mx = 0, lane, gg;
+							while (e2 < stack->chl_n && (stack->chl[e2] & 2047) == lev) ++e2; /* level [q, e2) */
+							while (q < e2) {
+								uint32_t rem = e2 - q;
+								gg = g ? g : (rem + 63) / 64; /* g = 0: adaptive, all of the level in one window */
+								if (g && rem < 64 * g) gg = (rem + 63) / 64;
+								mx = 0;
+								for (lane = 0; lane < 64 && q < e2; ++lane) {
+									uint32_t sum = 0, j;
+									for (j = 0; j < gg && q < e2; ++j, ++q) sum += stack->chl[q] >> 11;
+									if (sum > mx) mx = sum;
+								}
+								tot += mx;
+							}
+						}
+						if (gi == 0) st->rounds_g4 = tot; else if (gi == 1) st->rounds_g16 = tot; else st->rounds_lvl = tot;
+					}
+				}
 			}
 			if (out.n) {
 				B->per_read[r] = (or_aln1_t*)malloc(out.n * sizeof(or_aln1_t));

@@ -54,6 +54,33 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path, gappe
     assert not bad, bad
 
 
+@pytest.mark.parametrize("coop", [1, 0])
+def test_sai_goldens_heavy_pass(golden_dir, sai_manifest, gpu_engine, coop):
+    """An iteration budget of 1 hands every gapped read to the heavy-read pass: the
+    wave-cooperative kernel (coop.hip), or with coop=0 the sequential wide kernel."""
+    bad = []
+    try:
+        gpu_engine.set_option("gap_iter_budget", 1)
+        gpu_engine.set_option("gap_coop", coop)
+        for key, m in sorted(sai_manifest.items()):
+            if m["argv"] == ["-n", "0"]:
+                continue
+            opt, _ = oracle.parse_aln_args(m["argv"])
+            recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+            seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+            n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+            exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+            if not oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp):
+                bad.append(key)
+            st = gpu_engine.stats()
+            if st.path == 2 and (st.n_heavy == 0 or (coop and st.n_coop == 0)):
+                bad.append(key + f":heavy {st.n_heavy} coop {st.n_coop}")
+    finally:
+        gpu_engine.set_option("gap_iter_budget", 4000)
+        gpu_engine.set_option("gap_coop", 1)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("stack_cap,aln_cap,v2", [(16, 1, 0), (64, 2, 0), (16, 1, 1), (64, 2, 1)])
 def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap, aln_cap, v2):
     """Tiny per-lane capacities force most reads through the large-capacity retry pass

@@ -92,12 +92,18 @@ def test_exact_reads_round_trip(mid_genome):
     (["-n", "0"], 100, 0.01, 20_000, {"exact_path": 0}),
     (["-n", "0"], 100, 0.01, 100_000, {"exact_jump": 0}),
     (["-n", "0"], 150, 0.0, 50_000, {}), (["-n", "0"], 36, 0.0, 50_000, {}),
-    ([], 100, 0.01, 4_000, {"gapped_v2": 0})])
+    ([], 100, 0.01, 4_000, {"gapped_v2": 0}),
+    # every read past one first-pass iteration goes to the wave-cooperative kernel (coop.hip) ...
+    ([], 100, 0.01, 30_000, {"gap_iter_budget": 1}), ([], 150, 0.02, 8_000, {"gap_iter_budget": 1}),
+    (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_iter_budget": 1}),
+    # ... or, with it off, to the sequential wide kernel
+    ([], 100, 0.01, 8_000, {"gap_iter_budget": 1, "gap_coop": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
     o, e = eopt(argv)
-    defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1}
+    defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
+                "gap_iter_budget": 4000, "gap_coop": 1}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
