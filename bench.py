@@ -96,9 +96,11 @@ def pmc_traffic(kernel, workload):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        k = d.get("kernels", {}).get(kernel)
-        if k and d.get("bench_line", {}).get("config", {}).get("workload") == workload:
-            return k["read_bytes_per_dispatch"] + k["write_bytes_per_dispatch"], os.path.basename(f), k.get("avg_ms")
+        ks = [d.get("kernels", {}).get(n) for n in kernel.split("+")]
+        if all(ks) and d.get("bench_line", {}).get("config", {}).get("workload") == workload:
+            # a '+'-joined name prices kernels that run back to back on one batch (per-launch sums)
+            return (sum(k["read_bytes_per_dispatch"] + k["write_bytes_per_dispatch"] for k in ks),
+                    os.path.basename(f), sum(k.get("avg_ms") or 0.0 for k in ks))
     return None
 
 
@@ -229,12 +231,13 @@ def main():
     value = total_reads / dt
     ms_step = dt * 1e3 / args.steps
 
+    cfg_name = "configs[1]" if ropt.max_diff == 0 and ropt.fnr <= 0 else "configs[2]"
     result = {
-        "metric": "reads/s `ibwa aln` GRCh37-sized 100bp (-n 0), achieved HBM GB/s vs peak",
+        "metric": "reads/s `ibwa aln` GRCh37-sized 100bp, achieved HBM GB/s vs peak",
         "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic",
-        "config": {"workload": f"configs[1]: GRCh37-sized synthetic genome ({lens and sum(lens)/1e9:.2f} Gbp, "
+        "config": {"workload": f"{cfg_name}: GRCh37-sized synthetic genome ({lens and sum(lens)/1e9:.2f} Gbp, "
                                f"index built on device), {args.reads} x {args.read_len} bp SE reads per GPU, "
                                f"aln {args.aln}",
                    "reads_per_gpu": args.reads, "read_len": args.read_len, "aln_options": args.aln,

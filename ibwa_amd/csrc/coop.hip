@@ -27,12 +27,20 @@
 // dedup, gap_shadow, max_diff) has been applied.
 //
 // Reasons a read is handed on (status bits 8-15, diagnostics): 1 read too long /
-// too many buckets / staging too small, 2 max_entries could be reached, 3 page pool
-// empty, 4 a bucket past COOP_MAXP pages, 5 runaway guard.
+// too many buckets / staging too small, 3 page pool empty, 4 a bucket past
+// COOP_MAXP pages, 5 runaway guard.  Such reads go to the sequential kernel
+// (gapped.hip, wide).
 //
-// The max_entries check before each pop (:139) is tracked per chain: if a
-// committed prefix could reach it, the read goes to the sequential kernel
-// (gapped.hip, wide), as does anything that outgrows this kernel's storage.
+// The max_entries check before each pop (bwtgap.c:138) is exact.  Inside a
+// chain the stack size before pop t is (size before the chain's first pop) +
+// (children the chain staged before pop t): each consumed match child was
+// pushed and popped.  Staged counts only grow, so the largest of these is the
+// count at the chain's last pop, which the chain record carries.  The commit
+// knows the size before each chain's first pop (prefix sum over the chains
+// before it), so it finds the first chain whose last pop would see more than
+// max_entries: the reference breaks before that pop, so neither that chain
+// (whose only possible hit is its last pop) nor anything after it counts, and
+// the read ends with the hits committed so far.
 //
 // Storage per wave: LDS holds the read's two strands, its width arrays (so
 // gap_shadow and the pruning tests are LDS work), bucket sizes, the page
@@ -121,7 +129,8 @@ __device__ __forceinline__ uint4 mk_ent(uint32_t k, uint32_t l, int i, int ldp, 
 }
 
 struct Shm {
-  uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | lane << 16 | hit << 24, done}
+  uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | lane << 16 | hit << 24,
+                      //  done (1) | children staged before the chain's last pop << 1}
   uint4 recB[RREC];   // hit: {k, l, n_mm | n_gapo << 8 | n_gape << 16 | a << 24, ldp}
   uint32_t dirc[4][MAXP];  // page ids of the level's bucket and of its (up to) three target buckets
   uint32_t nb[NSTK];       // entries per bucket
@@ -245,7 +254,7 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
       while (!done) {
         while (s < o.n_stacks && S.nb[s] == 0) ++s;
         if (s >= o.n_stacks) break;                                              // stack empty
-        if (n_live > (uint32_t)o.max_entries) { status = ST_STACK_OVERFLOW | 2u << 8; break; }  // :139, exactly there
+        if (n_live > (uint32_t)o.max_entries) break;                            // :138, before the level's first pop
         if (!(o.mode & MODE_NONSTOP) && s > best_score + o.s_mm) break;         // :143
         const uint32_t N = S.nb[s];
         // targets: mismatch, gap extension, gap open (deduplicated when penalties coincide)
@@ -266,6 +275,7 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
         // lane chain state
         int lst = L_IDLE;
         uint32_t c = 0, cstart = 0, cnt0 = 0, cnt1 = 0, cnt2 = 0;
+        uint32_t mpre = 0;  // children staged before the chain's latest pop
         uint32_t k = 0, l = 0;
         int i = 0, ldp = 0, e_mm = 0, e_go = 0, e_ge = 0, a = 0, state = 0;
         int xj = 0;
@@ -278,12 +288,14 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
           S.recB[slot] = make_uint4(hk, hl,
                                     (uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
                                     (uint32_t)ldp);
-          S.recA[slot] = make_uint4(cstart, cnt0 | cnt1 << 16, cnt2 | (uint32_t)lane << 16 | (hit ? 1u << 24 : 0u), 1u);
+          S.recA[slot] = make_uint4(cstart, cnt0 | cnt1 << 16, cnt2 | (uint32_t)lane << 16 | (hit ? 1u << 24 : 0u),
+                                    1u | mpre << 1);
           if (hit) hit_c = c;
           lst = L_IDLE;
         };
         // the pops of bwtgap.c:139-163 for the node in registers: prune, hit, tail or expand
         auto pop_node = [&]() __attribute__((always_inline)) {
+          mpre = cnt0 + cnt1 + cnt2;
           int m = max_diff - (e_mm + e_go);
           if (gape) m -= e_ge;
           if (m < 0) { end_chain(false, 0, 0); return; }                                  // :147
@@ -362,13 +374,13 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
               const uint4 ra = v ? S.recA[cc & (RREC - 1)] : make_uint4(0, 0, 0, 0);
               const uint32_t n0 = ra.y & 0xffffu, n1 = ra.y >> 16, n2 = ra.z & 0xffffu;
               const uint32_t tot = n0 + n1 + n2;
-              // n_entries before each pop of this chain <= n_c + tot (bwtgap.c:139)
+              // stack size before this chain's first pop; its largest before any of its pops is
+              // nc + (children staged before its last pop) (bwtgap.c:138)
               uint32_t dsum = 0;
               const uint32_t pre = wave_excl(v ? tot : 0u, lane, dsum);
               const uint32_t nc = n_live + pre - (uint32_t)lane;  // each earlier chain popped one entry
-              if (__ballot(v && nc + tot > (uint32_t)o.max_entries)) {
-                status = ST_STACK_OVERFLOW | 2u << 8;
-                done = true;
+              if (__ballot(v && nc + (ra.w >> 1) > (uint32_t)o.max_entries)) {
+                done = true;  // the search breaks inside the first such chain: the hits so far stand
                 break;
               }
               const uint32_t nv = (lim - base) < 64 ? (lim - base) : 64;

@@ -170,6 +170,21 @@ hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks,
 uint64_t sw_words_per_lane(int max_len1, int max_len2);
 uint64_t sw_tb_per_lane(int max_len1, int max_len2);
 
+// SA row -> coordinate (sa2pos.hip): bwt_sa (bwt.c:69-79) inside bwtdb_sa2seq (dbset.c:240-246).
+struct SaArgs {
+  IndexView ix[2];           // ix[0] = .bwt (strand-1 hits), ix[1] = .rbwt (strand-0 hits)
+  const uint32_t *sa[2];     // sampled SA (walk) or full SA (gather) of each index
+  uint32_t intv[2];          // sampling interval of each sampled SA
+  const uint8_t *strand;     // bwt_aln1_t.a of each hit
+  const uint32_t *k, *len;   // SA row and read length of each hit
+  int64_t n;
+  uint64_t offset;           // bwtdb_t.offset
+  uint64_t *pos;             // out
+  uint32_t *steps;           // optional out: LF steps of each walk
+};
+hipError_t launch_sa2pos(const SaArgs &a, bool full, hipStream_t st);
+hipError_t expand_sa(const IndexView &ix, const uint32_t *sa_s, uint32_t intv, uint32_t *full, hipStream_t st);
+
 hipError_t build_kmer_table(const IndexView &ix, int K, uint2 *table, uint2 *tmp, hipStream_t st);
 
 hipError_t relayout_reference_bwt(const uint32_t *d_ref, uint64_t n_words, uint64_t n_blocks, uint4 *d_out,

@@ -95,6 +95,10 @@ struct ibwa_ctx {
   bool jump_ready = false;
   int exact_jump = 1;
   uint32_t sa_intv = 0;
+  bool sa_loaded[2] = {false, false};  // sa_s[s] holds a sampled SA of the resident index
+  bool sa_expanded = false;            // sa_full[0/1] derived from the sampled SA (ibwa_ctx_expand_sa)
+  int sa_walk = 0;                     // option: always walk the sampled SA (parity / low-memory)
+  DBuf h2p_in, h2p_out;                // staging of ibwa_sa2pos
   int build_rounds[2] = {0, 0};
   // tuning
   uint32_t stack_cap = 4096, aln_cap = 8;
@@ -252,7 +256,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (DBuf *b : {&c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
+  for (DBuf *b : {&c->h2p_in, &c->h2p_out, &c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
                   &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
                   &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1]})
@@ -276,6 +280,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_reads_per_chunk" && value > 0) c->gap_reads_per_chunk = value;
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
+  else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
   else if (k == "coop_pool_gb" && value > 0 && value <= 256) c->coop_pool_gb = (int)value;
@@ -320,6 +325,8 @@ int ibwa_ctx_load_bwt(ibwa_ctx_t *c, int strand, uint32_t primary, const uint32_
   c->loaded[strand] = true;
   c->kmer_valid = false;
   c->jump_ready = false;  // SA / ISA / text belong to an index built here
+  c->sa_loaded[strand] = false;
+  c->sa_expanded = false;
   return 0;
 }
 
@@ -355,8 +362,10 @@ int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
     dst->ix[s].blk = dst->idx[s].as<uint4>();
     dst->loaded[s] = true;
     dst->kmer_valid = false;
+    dst->sa_loaded[s] = false;
   }
   dst->jump_ready = false;
+  dst->sa_expanded = false;
   return 0;
 }
 
@@ -419,6 +428,8 @@ int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa
   }
   c->kmer_valid = false;
   c->sa_intv = (uint32_t)sa_intv;
+  c->sa_loaded[0] = c->sa_loaded[1] = sa_intv > 0;
+  c->sa_expanded = false;
   c->jump_ready = keep_full;
   T.release();
   return 0;
@@ -465,6 +476,101 @@ int ibwa_ctx_export_sa(const ibwa_ctx_t *c, int strand, uint32_t *out, uint64_t 
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemcpy(out, c->sa_s[strand].p, n_sa * 4, hipMemcpyDeviceToHost));
   out[0] = 0xFFFFFFFFu;  // bwt.c:66
+  return 0;
+}
+
+int ibwa_ctx_load_sa(ibwa_ctx_t *c, int strand, uint32_t sa_intv, const uint32_t *sa, uint64_t n_sa) {
+  if (strand < 0 || strand > 1 || !c->loaded[strand]) return fail(IBWA_ENOINDEX, "index not loaded");
+  if (sa_intv == 0) return fail(IBWA_EINVAL, "sa_intv == 0");
+  const uint64_t n = c->ix[strand].seq_len;
+  if (n_sa != (n + sa_intv) / sa_intv)
+    return fail(IBWA_EINVAL, "n_sa %llu != (seq_len + intv) / intv", (unsigned long long)n_sa);
+  if (c->sa_loaded[1 - strand] && c->sa_intv != sa_intv)
+    return fail(IBWA_EINVAL, "sa_intv %u differs from the other strand's %u", sa_intv, c->sa_intv);
+  HIPCHK(hipSetDevice(c->device));
+  if (int rc = c->sa_s[strand].ensure(n_sa * 4)) return rc;
+  HIPCHK(hipMemcpy(c->sa_s[strand].p, sa, n_sa * 4, hipMemcpyHostToDevice));
+  c->sa_intv = sa_intv;
+  c->sa_loaded[strand] = true;
+  c->sa_expanded = false;
+  if (c->jump_ready) c->sa_full[strand].release(), c->isa_full[strand].release(), c->jump_ready = false;
+  return 0;
+}
+
+int ibwa_ctx_load_sa_file(ibwa_ctx_t *c, int strand, const char *path) {  // bwt_restore_sa, bwtio.c:29-49
+  if (strand < 0 || strand > 1 || !c->loaded[strand]) return fail(IBWA_ENOINDEX, "index not loaded");
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return fail(IBWA_EIO, "cannot open %s", path);
+  uint32_t hdr[7];
+  if (fread(hdr, 4, 7, fp) != 7) { fclose(fp); return fail(IBWA_EIO, "%s: short header", path); }
+  const IndexView &ix = c->ix[strand];
+  if (hdr[0] != ix.primary) { fclose(fp); return fail(IBWA_EINVAL, "SA-BWT inconsistency: primary is not the same."); }
+  if (hdr[6] != ix.seq_len) { fclose(fp); return fail(IBWA_EINVAL, "SA-BWT inconsistency: seq_len is not the same."); }
+  if (hdr[5] == 0) { fclose(fp); return fail(IBWA_EINVAL, "%s: sa_intv 0", path); }
+  const uint64_t n_sa = ((uint64_t)ix.seq_len + hdr[5]) / hdr[5];
+  std::vector<uint32_t> sa(n_sa);
+  sa[0] = 0xFFFFFFFFu;  // bwtio.c:45
+  const bool ok = fread(sa.data() + 1, 4, n_sa - 1, fp) == n_sa - 1;
+  fclose(fp);
+  if (!ok) return fail(IBWA_EIO, "%s: short read", path);
+  return ibwa_ctx_load_sa(c, strand, hdr[5], sa.data(), n_sa);
+}
+
+int ibwa_ctx_expand_sa(ibwa_ctx_t *c) {
+  if (!c->sa_loaded[0] || !c->sa_loaded[1]) return fail(IBWA_ENOINDEX, "sampled SA of both strands needed");
+  if (c->jump_ready || c->sa_expanded) return 0;  // full SA already resident
+  HIPCHK(hipSetDevice(c->device));
+  for (int s = 0; s < 2; ++s) {
+    if (int rc = c->sa_full[s].ensure(((uint64_t)c->ix[s].seq_len + 1) * 4)) return rc;
+    HIPCHK(expand_sa(c->ix[s], c->sa_s[s].as<uint32_t>(), c->sa_intv, c->sa_full[s].as<uint32_t>(), c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->sa_expanded = true;
+  return 0;
+}
+
+int ibwa_sa2pos(ibwa_ctx_t *c, int64_t n, const uint8_t *strand, const uint32_t *k, const uint32_t *len,
+                uint64_t offset, uint64_t *pos) {
+  if (n < 0) return fail(IBWA_EINVAL, "n < 0");
+  if (!c->loaded[0] || !c->loaded[1]) return fail(IBWA_ENOINDEX, "index not loaded");
+  const bool full = (c->jump_ready || c->sa_expanded) && !c->sa_walk;
+  if (!full && (!c->sa_loaded[0] || !c->sa_loaded[1])) return fail(IBWA_ENOINDEX, "no suffix array loaded");
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t sl = c->ix[strand[i] ? 0 : 1].seq_len;
+    if (k[i] > sl) return fail(IBWA_EINVAL, "hit %lld: row %u > seq_len %u", (long long)i, k[i], sl);
+  }
+  c->stats.ms_sa2pos = 0;
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  // one staging buffer: strand bytes, rows, lengths in; positions + walk lengths out
+  const uint64_t o_k = (n + 15) / 16 * 16, o_len = o_k + n * 4, in_bytes = o_len + n * 4;
+  if (int rc = c->h2p_in.ensure(in_bytes)) return rc;
+  if (int rc = c->h2p_out.ensure(n * 12)) return rc;
+  uint8_t *din = c->h2p_in.as<uint8_t>();
+  HIPCHK(hipMemcpyAsync(din, strand, n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(din + o_k, k, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(din + o_len, len, n * 4, hipMemcpyHostToDevice, c->stream));
+  SaArgs a = {};
+  for (int s = 0; s < 2; ++s) {
+    a.ix[s] = c->ix[s];
+    a.sa[s] = full ? c->sa_full[s].as<uint32_t>() : c->sa_s[s].as<uint32_t>();
+    a.intv[s] = full ? 1 : c->sa_intv;
+  }
+  a.strand = din;
+  a.k = reinterpret_cast<const uint32_t *>(din + o_k);
+  a.len = reinterpret_cast<const uint32_t *>(din + o_len);
+  a.n = n;
+  a.offset = offset;
+  a.pos = c->h2p_out.as<uint64_t>();
+  a.steps = reinterpret_cast<uint32_t *>(c->h2p_out.as<uint8_t>() + n * 8);
+  HIPCHK(hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(launch_sa2pos(a, full, c->stream));
+  HIPCHK(hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(hipMemcpyAsync(pos, a.pos, n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->stats.ms_sa2pos = ms;
+  c->stats.sa2pos_full = full;
   return 0;
 }
 

@@ -30,7 +30,8 @@ class RunStats(c.Structure):
                 ("ms_total", c.c_double), ("n_retry", c.c_int64), ("n_launch_width", c.c_int64),
                 ("n_launch_search", c.c_int64), ("path", c.c_int), ("kmer_k", c.c_int),
                 ("n_stack_overflow", c.c_int64), ("n_aln_overflow", c.c_int64), ("n_heavy", c.c_int64), ("ms_sw", c.c_double),
-                ("n_coop", c.c_int64), ("ms_coop", c.c_double)]
+                ("n_coop", c.c_int64), ("ms_coop", c.c_double), ("ms_sa2pos", c.c_double),
+                ("sa2pos_full", c.c_int)]
 
 
 assert c.sizeof(GapOpt) == 64
@@ -60,6 +61,10 @@ CAPI = {
     "ibwa_ctx_set_tuning": (_i, [_vp, _i, _i, _i]),
     "ibwa_ctx_set_option": (_i, [_vp, c.c_char_p, c.c_long]),
     "ibwa_occ4": (_i, [_vp, _i, _i64, _vp, _vp]),
+    "ibwa_ctx_load_sa": (_i, [_vp, _i, _u32, _vp, _u64]),
+    "ibwa_ctx_load_sa_file": (_i, [_vp, _i, c.c_char_p]),
+    "ibwa_ctx_expand_sa": (_i, [_vp]),
+    "ibwa_sa2pos": (_i, [_vp, _i64, _vp, _vp, _vp, _u64, _vp]),
     "ibwa_ctx_build_index": (_i, [_vp, _vp, _u64, _i]),
     "ibwa_ctx_bwt_info": (_i, [_vp, _i, c.POINTER(_u32), c.POINTER(_u32), c.POINTER(_u64)]),
     "ibwa_ctx_export_bwt": (_i, [_vp, _i, _vp, _u64]),
@@ -204,6 +209,28 @@ class Engine:
         out = np.zeros((n + intv) // intv, dtype=np.uint32)
         _chk(lib().ibwa_ctx_export_sa(self.h, strand, out.ctypes.data, out.size))
         return out
+
+    def load_sa_files(self, prefix):
+        """bwt_restore_sa (bwtio.c:29) of prefix.sa / prefix.rsa onto the device."""
+        _chk(lib().ibwa_ctx_load_sa_file(self.h, 0, (prefix + ".sa").encode()))
+        _chk(lib().ibwa_ctx_load_sa_file(self.h, 1, (prefix + ".rsa").encode()))
+
+    def load_sa(self, strand, sa, intv):
+        sa = np.ascontiguousarray(sa, dtype=np.uint32)
+        _chk(lib().ibwa_ctx_load_sa(self.h, strand, int(intv), sa.ctypes.data, sa.size))
+
+    def expand_sa(self):
+        _chk(lib().ibwa_ctx_expand_sa(self.h))
+
+    def sa2pos(self, strand, k, lens, offset=0):
+        """bwtdb_sa2seq (dbset.c:240-246) for arrays of hits -> uint64 positions."""
+        strand = np.ascontiguousarray(strand, dtype=np.uint8)
+        k = np.ascontiguousarray(k, dtype=np.uint32)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        pos = np.zeros(k.size, dtype=np.uint64)
+        _chk(lib().ibwa_sa2pos(self.h, k.size, strand.ctypes.data, k.ctypes.data, lens.ctypes.data, int(offset),
+                               pos.ctypes.data))
+        return pos
 
     def sw(self, refs, reads):
         """Batched aln_local_core (stdaln.c:529) over code arrays.  Returns a list of

@@ -123,6 +123,8 @@ typedef struct {
 	double ms_sw;              /* last ibwa_sw_batch kernel time */
 	int64_t n_coop;            /* heavy reads the wave-cooperative pass resolved */
 	double ms_coop;            /* its time (width + search), part of ms_retry */
+	double ms_sa2pos;          /* last ibwa_sa2pos kernel time */
+	int sa2pos_full;           /* 1: it gathered from a full SA, 0: it walked the sampled SA */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 
@@ -174,6 +176,33 @@ int ibwa_ctx_export_sa(const ibwa_ctx_t *ctx, int strand, uint32_t *out, uint64_
 int ibwa_sw_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
                   const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int32_t *score,
                   int32_t *path_len, int32_t *ends, int32_t *n_cigar, uint32_t **cigar, int64_t *n_cigar_total);
+
+/*
+ * SA -> coordinate.
+ *
+ * ibwa_ctx_load_sa: make a sampled suffix array device-resident, as
+ * bwt_restore_sa (bwtio.c:29-49) loads it into bwt_t: sa[0..n_sa) with
+ * sa[0] = (u32)-1, n_sa = (seq_len + sa_intv) / sa_intv; strand 0 = prefix.sa,
+ * 1 = prefix.rsa.  ibwa_ctx_load_sa_file reads the .sa/.rsa file itself and
+ * applies bwt_restore_sa's primary / seq_len consistency checks (IBWA_EINVAL).
+ * An index built by ibwa_ctx_build_index(sa_intv > 0) already has both.
+ *
+ * ibwa_ctx_expand_sa: derive the full SA of both strands on the device from
+ * the sampled ones (one LF walk per sampled row, seq_len steps in all;
+ * 2 x 4 B per base of HBM) so that ibwa_sa2pos is one gather per hit.
+ *
+ * ibwa_sa2pos: bwtdb_sa2seq (dbset.c:240-246) over n hits, i.e. bwt_sa
+ * (bwt.c:69-79) on bwt[0] for strand 1 and seq_len - (bwt_sa(bwt[1], k) + len)
+ * (u32 arithmetic) for strand 0, plus `offset` (bwtdb_t.offset; 0 for a single
+ * database).  Replaces the per-hit calls of bwa_cal_pac_pos (bwase.c:133,
+ * :146, :157), bwa_cal_pac_pos_pe (bwape.c:347, :400) and saiset.c:136, :147.
+ * Uses the full SA when resident (option "sa_walk" = 1 forces the walk).
+ */
+int ibwa_ctx_load_sa(ibwa_ctx_t *ctx, int strand, uint32_t sa_intv, const uint32_t *sa, uint64_t n_sa);
+int ibwa_ctx_load_sa_file(ibwa_ctx_t *ctx, int strand, const char *path);
+int ibwa_ctx_expand_sa(ibwa_ctx_t *ctx);
+int ibwa_sa2pos(ibwa_ctx_t *ctx, int64_t n, const uint8_t *strand, const uint32_t *k, const uint32_t *len,
+                uint64_t offset, uint64_t *pos);
 
 /* Device Occ KAT: bwt_occ4 (bwt.c:157) for n positions k[] on strand s -> cnt[4*n] */
 int ibwa_occ4(ibwa_ctx_t *ctx, int strand, int64_t n, const uint32_t *k, uint32_t *cnt);

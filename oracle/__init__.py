@@ -85,6 +85,13 @@ def lib():
                                         c.POINTER(c.c_int), c.c_int, c.c_void_p]
         L.or_path2cigar32.restype = c.c_int
         L.or_path2cigar32.argtypes = [c.c_void_p, c.c_int, c.c_void_p]
+        L.or_bwt_info.argtypes = [c.c_void_p, c.POINTER(c.c_uint32), c.POINTER(c.c_uint32)]
+        L.or_sa_load.restype = c.c_void_p
+        L.or_sa_load.argtypes = [c.c_char_p, c.c_void_p, c.POINTER(c.c_uint32), c.POINTER(c.c_uint64)]
+        L.or_bwt_sa.restype = c.c_uint32
+        L.or_bwt_sa.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p]
+        L.or_sa2seq_batch.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_int64,
+                                      c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p]
         _lib = L
     return _lib
 
@@ -104,6 +111,37 @@ class Bwt:
             arr = (ctypes.c_uint32 * 4)(*[int(x) for x in L2])
             self.h = L.or_bwt_wrap(int(primary), arr, self._keep.ctypes.data, self._keep.size)
 
+    def info(self):
+        p, n = ctypes.c_uint32(), ctypes.c_uint32()
+        lib().or_bwt_info(self.h, ctypes.byref(p), ctypes.byref(n))
+        return p.value, n.value
+
+    def primary(self):
+        return self.info()[0]
+
+    def seq_len(self):
+        return self.info()[1]
+
+    def load_sa(self, path):
+        """bwt_restore_sa (bwtio.c:29-49): keeps sa[0..n_sa) (sa[0] = -1) and sa_intv on this index."""
+        intv, n = ctypes.c_uint32(), ctypes.c_uint64()
+        p = lib().or_sa_load(path.encode(), self.h, ctypes.byref(intv), ctypes.byref(n))
+        if not p:
+            raise IOError(path)
+        self.sa = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(n.value,)).copy()
+        lib().or_free(p)
+        self.sa_intv = intv.value
+        return self
+
+    def set_sa(self, sa, intv):
+        self.sa = np.ascontiguousarray(sa, dtype=np.uint32)
+        self.sa_intv = int(intv)
+        return self
+
+    def bwt_sa(self, k):
+        """bwt_sa (bwt.c:69-79)"""
+        return lib().or_bwt_sa(self.h, self.sa.ctypes.data, self.sa_intv, k & 0xFFFFFFFF, None)
+
     def occ4(self, k):
         out = (ctypes.c_uint32 * 4)()
         lib().or_occ4(self.h, k & 0xFFFFFFFF, out)
@@ -114,6 +152,28 @@ class Bwt:
             lib().or_bwt_free(self.h)
         except Exception:
             pass
+
+
+def sa2seq(bwt0, bwt1, strand, k, lens, steps=False):
+    """bwtdb_sa2seq (dbset.c:240-246, db offset 0) over arrays; both indexes need load_sa/set_sa.
+    steps=True also returns the LF-walk length of each row (bwt_sa's loop, bwt.c:72-75)."""
+    strand = np.ascontiguousarray(strand, dtype=np.uint8)
+    k = np.ascontiguousarray(k, dtype=np.uint32)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    assert bwt0.sa_intv == bwt1.sa_intv
+    pos = np.empty(k.size, dtype=np.uint64)
+    st = np.zeros(k.size, dtype=np.uint32) if steps else None
+    lib().or_sa2seq_batch(bwt0.h, bwt0.sa.ctypes.data, bwt1.h, bwt1.sa.ctypes.data, bwt0.sa_intv, k.size,
+                          strand.ctypes.data, k.ctypes.data, lens.ctypes.data, pos.ctypes.data,
+                          st.ctypes.data if steps else None)
+    return (pos, st) if steps else pos
+
+
+def read_sa2pos_vectors(path):
+    """tests/golden/sa2pos_vectors.tsv -> (strand, k, len, bwt_sa, pos) arrays"""
+    a = np.loadtxt(path, dtype=np.uint64, comments="#", ndmin=2)
+    return (a[:, 0].astype(np.uint8), a[:, 1].astype(np.uint32), a[:, 2].astype(np.uint32),
+            a[:, 3].astype(np.uint32), a[:, 4])
 
 
 def default_opt():

@@ -1057,3 +1057,72 @@ int or_path2cigar32(const or_path_t *path, int path_len, uint32_t *cigar)
 	}
 	return n + 1;
 }
+
+/* ---------------- SA -> coordinate (bwt.c:69-79, bwtio.c:29-49, dbset.c:240-246) ---------------- */
+
+void or_bwt_info(const or_bwt_t *b, uint32_t *primary, uint32_t *seq_len)
+{
+	*primary = b->primary;
+	*seq_len = b->seq_len;
+}
+
+/* bwt_restore_sa (bwtio.c:29-49): header primary, L2[1..4], sa_intv, seq_len, then sa[1..n_sa-1];
+ * returns sa[0..n_sa) with sa[0] = (u32)-1, or NULL on a mismatch with the index */
+uint32_t *or_sa_load(const char *fn, const or_bwt_t *b, uint32_t *intv, uint64_t *n_sa)
+{
+	FILE *fp = fopen(fn, "rb");
+	uint32_t hdr[7], *sa;
+	uint64_t n;
+	if (!fp) return 0;
+	if (fread(hdr, 4, 7, fp) != 7 || hdr[0] != b->primary || hdr[6] != b->seq_len || hdr[5] == 0) {
+		fclose(fp); return 0;
+	}
+	n = ((uint64_t)b->seq_len + hdr[5]) / hdr[5];
+	sa = (uint32_t*)calloc(n, 4);
+	sa[0] = (uint32_t)-1;
+	if (fread(sa + 1, 4, n - 1, fp) != n - 1) { fclose(fp); free(sa); return 0; }
+	fclose(fp);
+	*intv = hdr[5];
+	*n_sa = n;
+	return sa;
+}
+
+/* symbol of BWT row r's stored base (bwt_B0, bwt.h:61) */
+static inline uint32_t b0(const or_bwt_t *b, uint32_t p)
+{
+	return b->bwt[p / OCC_INTERVAL * 12 + 4 + p % OCC_INTERVAL / 16] >> ((~p & 0xf) << 1) & 3;
+}
+
+/* bwt_invPsi (bwt.h:66-70) */
+static inline uint32_t inv_psi(const or_bwt_t *b, uint32_t k)
+{
+	uint32_t c;
+	if (k == b->primary) return 0;
+	c = k < b->primary ? b0(b, k) : b0(b, k - 1);
+	return b->L2[c] + or_occ(b, k, c);
+}
+
+/* bwt_sa (bwt.c:69-79): LF-walk to a sampled row; *steps (optional) += walk length */
+uint32_t or_bwt_sa(const or_bwt_t *b, const uint32_t *sa, uint32_t intv, uint32_t k, uint32_t *steps)
+{
+	uint32_t s = 0;
+	while (k % intv != 0) {
+		++s;
+		k = inv_psi(b, k);
+	}
+	if (steps) *steps += s;
+	return s + sa[k / intv];
+}
+
+/* bwtdb_sa2seq (dbset.c:240-246) with db->offset = 0, over a batch:
+ * strand 1 -> bwt_sa(bwt[0], k); strand 0 -> bwt[1]->seq_len - (bwt_sa(bwt[1], k) + len) (u32) */
+void or_sa2seq_batch(const or_bwt_t *b0_, const uint32_t *sa0, const or_bwt_t *b1, const uint32_t *sa1,
+                     uint32_t intv, int64_t n, const uint8_t *strand, const uint32_t *k, const uint32_t *len,
+                     uint64_t *pos, uint32_t *steps)
+{
+	int64_t i;
+	for (i = 0; i < n; ++i) {
+		if (strand[i]) pos[i] = or_bwt_sa(b0_, sa0, intv, k[i], steps ? steps + i : 0);
+		else pos[i] = (uint32_t)(b1->seq_len - (uint32_t)(or_bwt_sa(b1, sa1, intv, k[i], steps ? steps + i : 0) + len[i]));
+	}
+}

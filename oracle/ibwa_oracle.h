@@ -7,6 +7,7 @@
  *   bwtaln.c   gap_init_opt, bwa_cal_maxdiff, bwt_cal_width, bwa_cal_sa_reg_gap
  *   bwtgap.c   gap stack, gap_shadow, bwt_match_gap
  *   stdaln.c   aln_global_core, aln_local_core (row a11/a12 of SURVEY §8a)
+ *   bwt.c      bwt_sa, bwtio.c bwt_restore_sa, dbset.c bwtdb_sa2seq
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline use this
  * library, and only as the checker or the CPU baseline -- never as a product
@@ -90,6 +91,14 @@ int or_aln_local_core(const uint8_t *seq1, int len1, const uint8_t *seq2, int le
 int or_aln_global_core(const uint8_t *seq1, int len1, const uint8_t *seq2, int len2,
                        int band_width, int gap_end, or_path_t *path, int *path_len);
 int or_path2cigar32(const or_path_t *path, int path_len, uint32_t *cigar);
+
+/* SA -> coordinate: bwt_restore_sa (bwtio.c:29), bwt_sa (bwt.c:69), bwtdb_sa2seq (dbset.c:240) */
+void or_bwt_info(const or_bwt_t *b, uint32_t *primary, uint32_t *seq_len);
+uint32_t *or_sa_load(const char *fn, const or_bwt_t *b, uint32_t *intv, uint64_t *n_sa);
+uint32_t or_bwt_sa(const or_bwt_t *b, const uint32_t *sa, uint32_t intv, uint32_t k, uint32_t *steps);
+void or_sa2seq_batch(const or_bwt_t *b0, const uint32_t *sa0, const or_bwt_t *b1, const uint32_t *sa1,
+                     uint32_t intv, int64_t n, const uint8_t *strand, const uint32_t *k, const uint32_t *len,
+                     uint64_t *pos, uint32_t *steps);
 
 #ifdef __cplusplus
 }

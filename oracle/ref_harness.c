@@ -13,6 +13,7 @@
  *   ibwa_ref occ4 <prefix.bwt> k...        -> bwt_occ4    (bwt.c:157)  (KAT)
  *   ibwa_ref sw <ref_seq> <read_seq>       -> aln_local_core (stdaln.c:529)
  *   ibwa_ref swf <pairs.tsv>               -> aln_local_core over a file of pairs
+ *   ibwa_ref sa <prefix> <rows.tsv>        -> bwt_sa (bwt.c:69) over bwt_restore_sa (bwtio.c:29)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -104,6 +105,33 @@ static int cmd_swf(int argc, char *argv[])
 	return 0;
 }
 
+/* sa <prefix> <rows.tsv> : one "strand<TAB>k<TAB>len" per line; prints the line plus the
+ * bwt_sa value of row k on the strand's index and the position bwtdb_sa2seq computes from it
+ * (dbset.c:240-246 with db->offset = 0: strand 1 -> bwt_sa(bwt[0], k); strand 0 ->
+ * bwt[1]->seq_len - (bwt_sa(bwt[1], k) + len), in bwtint_t arithmetic).  dbset.c itself is not
+ * compiled here (it pulls in the remap / cache layers); its three lines are restated. */
+static int cmd_sa(int argc, char *argv[])
+{
+	char fn[4096];
+	bwt_t *bwt[2];
+	FILE *fp;
+	unsigned strand, k, len;
+	if (argc < 3) return 1;
+	snprintf(fn, sizeof fn, "%s.bwt", argv[1]); bwt[0] = bwt_restore_bwt(fn);
+	snprintf(fn, sizeof fn, "%s.sa", argv[1]); bwt_restore_sa(fn, bwt[0]);
+	snprintf(fn, sizeof fn, "%s.rbwt", argv[1]); bwt[1] = bwt_restore_bwt(fn);
+	snprintf(fn, sizeof fn, "%s.rsa", argv[1]); bwt_restore_sa(fn, bwt[1]);
+	if (!(fp = fopen(argv[2], "r"))) return 1;
+	while (fscanf(fp, "%u %u %u", &strand, &k, &len) == 3) {
+		bwtint_t sa = bwt_sa(bwt[strand ? 0 : 1], k);
+		uint64_t pos = strand ? (uint64_t)sa : (uint64_t)(bwtint_t)(bwt[1]->seq_len - (bwtint_t)(sa + len));
+		printf("%u\t%u\t%u\t%u\t%llu\n", strand, k, len, sa, (unsigned long long)pos);
+	}
+	fclose(fp);
+	bwt_destroy(bwt[0]); bwt_destroy(bwt[1]);
+	return 0;
+}
+
 int main(int argc, char *argv[])
 {
 	if (argc < 2) {
@@ -115,6 +143,7 @@ int main(int argc, char *argv[])
 	if (strcmp(argv[1], "occ4") == 0) return cmd_occ4(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sw") == 0) return cmd_sw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "swf") == 0) return cmd_swf(argc - 1, argv + 1);
+	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }

@@ -61,3 +61,16 @@ def test_sw_restatement_matches_reference_vectors(golden_dir):
         if got != (score, pl, start, end, cig):
             bad.append((k, got, (score, pl, start, end, cig)))
     assert not bad, bad[:5]
+
+
+def test_sa2pos_restatement_matches_reference_vectors(golden_dir):
+    """bwt_sa (bwt.c:69) + bwtdb_sa2seq (dbset.c:240) restated == the reference on 10 755 rows."""
+    g = os.path.join(golden_dir, "g1m")
+    b0 = oracle.Bwt(g + ".bwt").load_sa(g + ".sa")
+    b1 = oracle.Bwt(g + ".rbwt").load_sa(g + ".rsa")
+    s, k, ln, sa, pos = oracle.read_sa2pos_vectors(os.path.join(golden_dir, "sa2pos_vectors.tsv"))
+    assert len(k) > 10000 and b0.sa_intv == 32
+    got, steps = oracle.sa2seq(b0, b1, s, k, ln, steps=True)
+    assert (got == pos).all()
+    assert all((b0 if s[i] else b1).bwt_sa(int(k[i])) == sa[i] for i in range(0, len(k), 7))
+    assert steps.max() > 64  # walks well past one sampling interval are covered

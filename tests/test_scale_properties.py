@@ -96,6 +96,9 @@ def test_exact_reads_round_trip(mid_genome):
     # every read past one first-pass iteration goes to the wave-cooperative kernel (coop.hip) ...
     ([], 100, 0.01, 30_000, {"gap_iter_budget": 1}), ([], 150, 0.02, 8_000, {"gap_iter_budget": 1}),
     (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_iter_budget": 1}),
+    # ... including reads cut off by max_entries (bwtgap.c:138), which it resolves itself ...
+    (["-m", "300"], 100, 0.02, 8_000, {"gap_iter_budget": 1}),
+    (["-m", "2000"], 150, 0.02, 4_000, {"gap_iter_budget": 1}),
     # ... or, with it off, to the sequential wide kernel
     ([], 100, 0.01, 8_000, {"gap_iter_budget": 1, "gap_coop": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
@@ -108,9 +111,12 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
         for k, v in tune.items():
             eng.set_option(k, v)
         n_aln, alns = eng.aln(seq, off, lns, e)
+        st = eng.stats()
     finally:
         for k in tune:
             eng.set_option(k, defaults[k])
+    if "-m" in argv:
+        assert st.n_heavy > 0 and st.n_coop == st.n_heavy  # nothing handed on to the sequential kernel
     rn, ra, _ = oracle.cal_sa_reg_gap(b0, b1, seq, off, lns, o, n_threads=8)
     assert (n_aln == rn).all()
     assert alns.tobytes() == ra.tobytes()
