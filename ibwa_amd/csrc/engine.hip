@@ -631,6 +631,8 @@ static int run_pass(ibwa_ctx *c, AlnArgs A, int64_t base, int64_t lanes, const i
 
 int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) {
   auto t0 = std::chrono::steady_clock::now();
+  // host-phase timestamps (IBWA_VERBOSE)
+  auto since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   if (!c->loaded[0] || !c->loaded[1]) return fail(IBWA_ENOINDEX, "load both .bwt and .rbwt first");
   if (c->ix[0].seq_len != c->ix[1].seq_len) return fail(IBWA_EINVAL, ".bwt and .rbwt lengths differ");
   if (int rc = check_opt(opt)) return rc;
@@ -847,6 +849,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   c->stats.ms_search = ms_s;
   c->aln_cap_used = A.aln_cap;
 
+  if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: first pass done\n", since());
   // results + overflow detection
   c->h_naln.resize(n);
   c->h_status.resize(n);
@@ -869,6 +872,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->stats.n_aln_overflow += (c->h_status[i] & ST_ALN_OVERFLOW) != 0;
     c->stats.n_heavy += (c->h_status[i] & ST_HEAVY) != 0;
   }
+  if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: status scanned, %zu to retry\n", since(), c->retry_ids.size());
   // retry pass: larger stacks / hit arrays for the few reads that overflowed
   std::vector<int64_t> todo = c->retry_ids;
   uint64_t cap = std::max<uint64_t>((uint64_t)c->stack_cap * 16, 65536);
@@ -951,6 +955,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[4]));
+    if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop kernel done\n", since());
     float a = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
     ms_r += a;
@@ -993,6 +998,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       fprintf(stderr, "[ibwa_amd] coop pass: %lld reads, %zu handed on, max %u wave iterations, %u pages, %.1f ms\n",
               (long long)lanes, next.size(), mx, pages, a);
     }
+    if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop results on host\n", since());
     c->stats.n_coop = lanes - (int64_t)next.size();
     c->stats.ms_coop = a;
     todo.swap(next);

@@ -14,6 +14,7 @@
  *   ibwa_ref sw <ref_seq> <read_seq>       -> aln_local_core (stdaln.c:529)
  *   ibwa_ref swf <pairs.tsv>               -> aln_local_core over a file of pairs
  *   ibwa_ref sa <prefix> <rows.tsv>        -> bwt_sa (bwt.c:69) over bwt_restore_sa (bwtio.c:29)
+ *   ibwa_ref samse|sampe ...               -> bwa_sai2sam_se / bwa_sai2sam_pe (bwase.c:710, bwape.c)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -24,6 +25,16 @@
 #include "stdaln.h"
 
 int bwa_index(int argc, char *argv[]);
+int bwa_sai2sam_se(int argc, char *argv[]);
+int bwa_sai2sam_pe(int argc, char *argv[]);
+
+/* This harness takes the place of the reference's main.cpp (which needs the cmake-generated
+ * version.h): besides main() that file defines only the @PG printer samse/sampe call
+ * (main.cpp:31-34).  Here it names the harness instead of a version string. */
+void bwa_print_sam_PG(void)
+{
+	printf("@PG\tID:bwa\tPN:bwa\tVN:ibwa_ref-harness\n");
+}
 int bwa_aln(int argc, char *argv[]);
 extern unsigned char nst_nt4_table[256];
 
@@ -144,6 +155,8 @@ int main(int argc, char *argv[])
 	if (strcmp(argv[1], "sw") == 0) return cmd_sw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "swf") == 0) return cmd_swf(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
+	if (strcmp(argv[1], "samse") == 0) return bwa_sai2sam_se(argc - 1, argv + 1);
+	if (strcmp(argv[1], "sampe") == 0) return bwa_sai2sam_pe(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }
