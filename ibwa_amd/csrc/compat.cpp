@@ -5,6 +5,7 @@
 // contiguous slices, one per GPU (each keeping the batch-level max length,
 // bwtaln.c:89-93), and every slice runs on its own engine from a host thread.
 #include <hip/hip_runtime_api.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -230,6 +231,176 @@ int ibwa_sw_core_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *seq, const uin
   *cigar = (uint32_t *)malloc(std::max<size_t>(out.size(), 1) * 4);
   if (!*cigar) return IBWA_EINVAL;
   if (!out.empty()) memcpy(*cigar, out.data(), out.size() * 4);
+  return 0;
+}
+
+namespace {
+// seq_reverse (bwaseqio.c:55-72) into a copy
+void rev_copy(const uint8_t *src, int len, bool comp, uint8_t *dst) {
+  for (int i = 0; i < len; ++i) {
+    const uint8_t c = src[len - 1 - i];
+    dst[i] = comp && c < 4 ? 3 - c : c;
+  }
+}
+}  // namespace
+
+int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                   const ibwa_ref_isize_info_t *ii, const uint8_t *pac, uint64_t l_pac, uint64_t n_tot[2],
+                   uint64_t n_mapped[2]) {
+  n_tot[0] = n_tot[1] = n_mapped[0] = n_mapped[1] = 0;
+  if (!popt->is_sw || ii->avg < 0.0) return 0;  // bwasw.c:279
+  const bool std_pe = popt->type == IBWA_PET_STD;
+  // ---- pass 1: eligible pairs, candidate windows (bwasw.c:157-219)
+  struct Cand {
+    int pair, k;
+  };
+  std::vector<Cand> cand;
+  std::vector<uint8_t> qbuf, rbuf;
+  std::vector<uint64_t> qoff, roff;
+  std::vector<uint32_t> qlen, rlen;
+  std::vector<int32_t> reglen;
+  std::vector<int64_t> beg;
+  std::vector<int8_t> single(std::max(n_seqs, 0), -1);
+  for (int i = 0; i < n_seqs; ++i) {
+    ibwa_ref_seq_t *p[2] = {seqs[0] + i, seqs[1] + i};
+    if (!((p[0]->mapQ >= 17 || p[1]->mapQ >= 17) && (p[0]->extra_flag & IBWA_SAM_FPP) == 0)) continue;
+    single[i] = (p[0]->type == IBWA_TYPE_NO_MATCH || p[1]->type == IBWA_TYPE_NO_MATCH) ? 1 : 0;
+    ++n_tot[single[i]];
+    if (popt->type != IBWA_PET_STD && popt->type != IBWA_PET_SOLID) continue;
+    for (int k = 0; k < 2; ++k) {
+      const ibwa_ref_seq_t *ref = p[1 - k], *mate = p[k];
+      if (ref->type == IBWA_TYPE_NO_MATCH) continue;
+      const int L = (int)mate->len;
+      int64_t b, e;
+      // set_right_coordinate / set_left_coordinate (bwasw.c:114-143), in the reference's double arithmetic
+      auto right = [&]() {
+        b = (int64_t)((int64_t)ref->remapped_pos + ii->avg - 3 * ii->std - mate->len * 1.5);
+        e = (int64_t)(b + 6 * ii->std + 2 * mate->len);
+        if (b < (int64_t)ref->remapped_pos + (int64_t)ref->len) b = ref->remapped_pos + ref->len;
+        if (e > (int64_t)l_pac) e = (int64_t)l_pac;
+      };
+      auto left = [&]() {
+        b = (int64_t)((int64_t)ref->remapped_pos + ref->len - ii->avg - 3 * ii->std - mate->len * 0.5);
+        e = (int64_t)(b + 6 * ii->std + 2 * mate->len);
+        if (b < 0) b = 0;
+        if (e > (int64_t)ref->remapped_pos) e = (int64_t)ref->remapped_pos;
+      };
+      // the read as bwa_sw_core sees it: a copy (the reference reverses p[k]->seq in place and back)
+      const size_t q0 = qbuf.size();
+      qbuf.resize(q0 + L);
+      uint8_t *q = qbuf.data() + q0;
+      if (std_pe) {
+        if (ref->strand == 0) { right(); memcpy(q, mate->rseq, L); }
+        else { left(); rev_copy(mate->seq, L, false, q); }
+      } else {
+        if (ref->strand == 0) { if (k == 0) left(); else right(); rev_copy(mate->rseq, L, false, q); }
+        else { if (k == 0) right(); else left(); memcpy(q, mate->seq, L); }
+      }
+      const int rl = (int)(e - b);
+      // dbset_extract_sequence (dbset.c:306-325), only for windows bwa_sw_core would extract (bwasw.c:40)
+      const size_t r0 = rbuf.size();
+      uint32_t got = 0;
+      if (rl >= 20 && b >= 0 && (uint64_t)b < l_pac) {
+        got = (uint32_t)std::min<uint64_t>((uint64_t)rl, l_pac - (uint64_t)b);
+        rbuf.resize(r0 + got);
+        for (uint32_t j = 0; j < got; ++j) {
+          const uint64_t x = (uint64_t)b + j;
+          rbuf[r0 + j] = (pac[x >> 2] >> ((~x & 3) << 1)) & 3;  // bns_pac (bntseq.h)
+        }
+      }
+      cand.push_back({i, k});
+      qoff.push_back(q0); qlen.push_back((uint32_t)L);
+      roff.push_back(r0); rlen.push_back(got);
+      reglen.push_back(rl);
+      beg.push_back(b);
+    }
+  }
+  // ---- pass 2: every bwa_sw_core of the batch in one launch
+  const int64_t m = (int64_t)cand.size();
+  std::vector<int32_t> ncig(m);
+  std::vector<uint32_t> cnt(m);
+  uint32_t *cig = nullptr;
+  qbuf.push_back(0);
+  rbuf.push_back(0);
+  if (m) {
+    if (int rc = ibwa_sw_core_batch(ctx, m, qbuf.data(), qoff.data(), qlen.data(), rbuf.data(), roff.data(), rlen.data(),
+                                    reglen.data(), beg.data(), (int64_t)l_pac, ncig.data(), cnt.data(), &cig))
+      return rc;
+  }
+  // ---- pass 3: acceptance and fix-up in pair order (bwasw.c:220-265)
+  std::vector<uint64_t> cfirst(m);
+  for (int64_t j = 0, acc = 0; j < m; ++j) { cfirst[j] = acc; acc += ncig[j]; }
+  const double prior_term = -4.343 * log(ii->ap_prior / l_pac);
+  const int new_term = (int)(-4.343 * log(.5 * erfc(M_SQRT1_2 * 1.5) + .499));
+  int64_t j = 0;
+  for (int i = 0; i < n_seqs; ++i) {
+    if (single[i] < 0) continue;
+    ibwa_ref_seq_t *p[2] = {seqs[0] + i, seqs[1] + i};
+    const uint32_t *cg[2] = {nullptr, nullptr};
+    int nc[2] = {0, 0}, mq_adjust[2] = {255, 255};
+    int64_t bg[2] = {0, 0};
+    uint32_t ct[2] = {0, 0};
+    for (; j < m && cand[j].pair == i; ++j) {
+      const int k = cand[j].k;
+      bg[k] = beg[j];
+      if (!ncig[j]) continue;
+      cg[k] = cig + cfirst[j];
+      nc[k] = ncig[j];
+      ct[k] = cnt[j];
+      if (p[k]->type != IBWA_TYPE_NO_MATCH) {  // re-evaluate (bwasw.c:222-236)
+        int clip = 0;
+        if ((cg[k][0] >> 29) == 3) clip += cg[k][0] & 0x1fffffff;
+        if ((cg[k][nc[k] - 1] >> 29) == 3) clip += cg[k][nc[k] - 1] & 0x1fffffff;
+        int s_old = (int)((p[k]->n_mm * 9 + p[k]->n_gapo * 13 + p[k]->n_gape * 2) / 3. * 8. + .499);
+        int s_new = (int)(((ct[k] >> 16) * 9 + (ct[k] >> 8 & 0xff) * 13 + (ct[k] & 0xff) * 2 + clip * 3) / 3. * 8. + .499);
+        s_old += prior_term;
+        s_new += new_term;
+        if (s_old < s_new) {
+          mq_adjust[k] = s_new - s_old;
+          cg[k] = nullptr;
+          nc[k] = 0;
+        } else {
+          mq_adjust[k] = s_old - s_new;
+        }
+      }
+    }
+    int k = -1, mapQ = 0;
+    if (cg[0] && cg[1]) {
+      k = p[0]->mapQ < p[1]->mapQ ? 0 : 1;
+      mapQ = abs((int)p[1]->mapQ - (int)p[0]->mapQ);
+    } else if (cg[0]) {
+      k = 0, mapQ = p[1]->mapQ;
+    } else if (cg[1]) {
+      k = 1, mapQ = p[0]->mapQ;
+    }
+    if (k < 0 || p[k]->pos == (uint64_t)bg[k]) continue;
+    ++n_mapped[single[i]];
+    ibwa_ref_seq_t *fx = p[k], *rf = p[1 - k];
+    int tmp = (int)rf->mapQ - fx->mapQ / 2 - 8;
+    if (tmp <= 0) tmp = 1;
+    if (mapQ > tmp) mapQ = tmp;
+    fx->mapQ = rf->mapQ = mapQ;
+    fx->seQ = rf->seQ = rf->seQ < (uint64_t)mapQ ? rf->seQ : (uint64_t)mapQ;
+    if ((int)fx->mapQ > mq_adjust[k]) fx->mapQ = mq_adjust[k];
+    if ((int)fx->seQ > mq_adjust[k]) fx->seQ = mq_adjust[k];
+    free(fx->cigar);
+    fx->cigar = (uint32_t *)malloc(sizeof(uint32_t) * nc[k]);
+    if (!fx->cigar) { ibwa_free(cig); return IBWA_EHIP; }
+    memcpy(fx->cigar, cg[k], sizeof(uint32_t) * nc[k]);
+    fx->n_cigar = nc[k];
+    // __set_fixed (bwasw.c:167-178)
+    fx->type = IBWA_TYPE_MATESW;
+    fx->pos = fx->remapped_pos = (uint64_t)bg[k];
+    fx->dbidx = fx->remapped_dbidx = 0;
+    fx->seQ = rf->seQ;
+    fx->strand = std_pe ? 1 - rf->strand : rf->strand;
+    fx->n_mm = ct[k] >> 16;
+    fx->n_gapo = ct[k] >> 8 & 0xff;
+    fx->n_gape = ct[k] & 0xff;
+    fx->extra_flag |= IBWA_SAM_FPP;
+    rf->extra_flag |= IBWA_SAM_FPP;
+  }
+  ibwa_free(cig);
   return 0;
 }
 

@@ -115,7 +115,7 @@ struct ibwa_ctx {
   int gap_pages_per_block = 384;      // 128 KiB pages per 256-lane workgroup pool
   uint32_t gap_hit_slots = 256;      // hits a read may hold in the first pass
   int64_t gap_reads_per_chunk = 1 << 22;
-  uint32_t gap_iter_budget = 4000;   // first-pass iterations per read before handing it to the coop pass
+  uint32_t gap_iter_budget = 8000;   // first-pass iterations per read before handing it to the coop pass (swept 1000-8000 at 50M reads: 8000 best)
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
   int gap_coop = 1;

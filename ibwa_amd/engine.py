@@ -34,6 +34,33 @@ class RunStats(c.Structure):
                 ("sa2pos_full", c.c_int)]
 
 
+class RefSeq(c.Structure):
+    """bwa_seq_t (bwtaln.h:62-93) == ibwa_ref_seq_t (ibwa_bwa_compat.h)"""
+    _fields_ = [("name", c.c_void_p), ("seq", c.c_void_p), ("rseq", c.c_void_p), ("qual", c.c_void_p),
+                ("len", c.c_uint32, 20), ("strand", c.c_uint32, 1), ("type", c.c_uint32, 2),
+                ("dummy", c.c_uint32, 1), ("extra_flag", c.c_uint32, 8),
+                ("n_mm", c.c_uint32, 8), ("n_gapo", c.c_uint32, 8), ("n_gape", c.c_uint32, 8),
+                ("mapQ", c.c_uint32, 8), ("score", c.c_int), ("clip_len", c.c_int), ("n_aln", c.c_int),
+                ("aln", c.c_void_p), ("n_multi", c.c_int), ("multi", c.c_void_p), ("sa", c.c_uint32),
+                ("pos", c.c_uint64), ("remapped_pos", c.c_uint64), ("dbidx", c.c_uint32),
+                ("remapped_dbidx", c.c_uint32), ("remapped_seqid", c.c_int32), ("remap_identical", c.c_int),
+                ("c1", c.c_uint64, 28), ("c2", c.c_uint64, 28), ("seQ", c.c_uint64, 8), ("n_cigar", c.c_int),
+                ("cigar", c.c_void_p), ("tid", c.c_int), ("bc", c.c_char * 16),
+                ("full_len", c.c_uint32, 20), ("nm", c.c_uint32, 12), ("md", c.c_void_p)]
+
+
+class PeOpt(c.Structure):
+    """pe_opt_t (bwtaln.h:120-128) == ibwa_ref_pe_opt_t"""
+    _fields_ = [(n, c.c_int) for n in ("max_isize", "force_isize", "max_occ", "n_multi", "N_multi", "n_threads",
+                                       "type", "is_sw", "is_preload", "remapping")] + [("ap_prior", c.c_double)]
+
+
+class IsizeInfo(c.Structure):
+    """isize_info_t (bwapair.h:8-11) == ibwa_ref_isize_info_t"""
+    _fields_ = [("avg", c.c_double), ("std", c.c_double), ("ap_prior", c.c_double), ("low", c.c_uint32),
+                ("high", c.c_uint32), ("high_bayesian", c.c_uint32)]
+
+
 assert c.sizeof(GapOpt) == 64
 ALN_DTYPE = np.dtype([("info", "<u4"), ("k", "<u4"), ("l", "<u4"), ("score", "<i4")])  # bwt_aln1_t
 
@@ -71,6 +98,8 @@ CAPI = {
     "ibwa_ctx_export_sa": (_i, [_vp, _i, _vp, _u64]),
     "ibwa_sw_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, c.POINTER(c.c_void_p),
                            c.POINTER(_i64)]),
+    "ibwa_paired_sw": (_i, [_vp, _i, c.POINTER(c.POINTER(RefSeq)), c.POINTER(PeOpt), c.POINTER(IsizeInfo), _vp,
+                            _u64, c.POINTER(_u64), c.POINTER(_u64)]),
     "ibwa_sw_core_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
                                 c.POINTER(c.c_void_p)]),
 }
@@ -231,6 +260,17 @@ class Engine:
         _chk(lib().ibwa_sa2pos(self.h, k.size, strand.ctypes.data, k.ctypes.data, lens.ctypes.data, int(offset),
                                pos.ctypes.data))
         return pos
+
+    def paired_sw(self, seqs0, seqs1, pe_opt, ii, pac, l_pac):
+        """bwa_paired_sw (bwasw.c:270) over two RefSeq arrays (mutated in place);
+        pac = the packed .pac bytes.  Returns [mated singletons, singletons, fixed, discordant]."""
+        arr = (c.POINTER(RefSeq) * 2)(c.cast(seqs0, c.POINTER(RefSeq)), c.cast(seqs1, c.POINTER(RefSeq)))
+        pac = np.ascontiguousarray(pac, dtype=np.uint8)
+        tot = (c.c_uint64 * 2)()
+        mapped = (c.c_uint64 * 2)()
+        _chk(lib().ibwa_paired_sw(self.h, len(seqs0), arr, c.byref(pe_opt), c.byref(ii), pac.ctypes.data, int(l_pac),
+                                  tot, mapped))
+        return [mapped[1], tot[1], mapped[0], tot[0]]
 
     def sw(self, refs, reads):
         """Batched aln_local_core (stdaln.c:529) over code arrays.  Returns a list of

@@ -73,7 +73,28 @@ typedef struct {
 	char *md;
 } ibwa_ref_seq_t;
 
-#define IBWA_TYPE_NO_MATCH 0 /* BWA_TYPE_NO_MATCH, bwtaln.h:9 */
+#define IBWA_TYPE_NO_MATCH 0 /* BWA_TYPE_NO_MATCH, bwtaln.h:7 */
+#define IBWA_TYPE_MATESW 3   /* BWA_TYPE_MATESW, bwtaln.h:10 */
+#define IBWA_SAM_FPP 2       /* SAM_FPP, bwtaln.h:13 */
+#define IBWA_PET_STD 1       /* BWA_PET_STD, bwtaln.h:117 */
+#define IBWA_PET_SOLID 2     /* BWA_PET_SOLID, bwtaln.h:118 */
+
+/* pe_opt_t (bwtaln.h:120-128) */
+typedef struct {
+	int max_isize, force_isize;
+	int max_occ;
+	int n_multi, N_multi;
+	int n_threads;
+	int type, is_sw, is_preload;
+	int remapping;
+	double ap_prior;
+} ibwa_ref_pe_opt_t;
+
+/* isize_info_t (bwapair.h:8-11) */
+typedef struct {
+	double avg, std, ap_prior;
+	uint32_t low, high, high_bayesian;
+} ibwa_ref_isize_info_t;
 
 /*
  * Bring the index of a running `aln` onto the GPUs (called by
@@ -114,6 +135,22 @@ void bwa_cal_sa_reg_gap(int tid, ibwa_ref_bwt_t *const bwt[2], int n_seqs, ibwa_
 int ibwa_sw_core_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *seq, const uint64_t *off, const uint32_t *len,
                        const uint8_t *ref, const uint64_t *ref_off, const uint32_t *ref_len, const int32_t *reglen,
                        int64_t *beg, int64_t l_pac, int32_t *n_cigar, uint32_t *cnt, uint32_t **cigar);
+
+/*
+ * bwa_paired_sw (bwasw.c:270-304) -- the mate rescue of `sampe` -- for one reference
+ * database (db offset 0): `pac` is the packed reference as seq_t.data holds it after
+ * dbset_load_pac (bns_pac order, 4 bases per byte, MSB first) and l_pac its length.
+ * Same effects on seqs[0][i] / seqs[1][i] as the reference (bwa_paired_sw_thread,
+ * bwasw.c:145-268): the candidate selection and window placement run on the host, every
+ * bwa_sw_core of the batch (<= 2 per pair) is one batched GPU launch (ibwa_sw_core_batch),
+ * then the acceptance test and the mapQ / CIGAR / __set_fixed updates are applied in pair
+ * order.  A replaced CIGAR is free()d and the new one malloc()ed, as the reference does.
+ * Counters: n_tot / n_mapped as the reference's stderr summary ([1] singletons,
+ * [0] discordant pairs).  Returns 0, or a negative IBWA_E* code (nothing is modified then).
+ */
+int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                   const ibwa_ref_isize_info_t *ii, const uint8_t *pac, uint64_t l_pac, uint64_t n_tot[2],
+                   uint64_t n_mapped[2]);
 
 #ifdef __cplusplus
 }

@@ -436,3 +436,174 @@ def sw_core(read, window, reglen, beg, l_pac):
             n_gapo += 1
             n_gape += n - 1
     return beg, c, n_mm << 16 | n_gapo << 8 | n_gape
+
+
+# ---------------------------------------------------------------- bwa_paired_sw
+
+PSW_IN = ("read", "strand", "type", "mapQ", "seQ", "extra_flag", "n_mm", "n_gapo", "n_gape", "pos")
+PSW_OUT = ("type", "strand", "pos", "remapped_pos", "dbidx", "remapped_dbidx", "mapQ", "seQ", "n_mm", "n_gapo",
+           "n_gape", "extra_flag", "n_cigar", "cigar")
+
+
+def read_psw(golden_dir, name):
+    """tests/golden/psw_<name>.{in,out}.tsv -> (pairs, expected): lists of [end0, end1] dicts."""
+    def parse(line, keys):
+        out = []
+        for half in line.rstrip("\n").split("\t"):
+            f = half.split()
+            d = {}
+            for k, v in zip(keys, f):
+                d[k] = v if k in ("read", "cigar") else int(v)
+            out.append(d)
+        return out
+    pin = [parse(l, PSW_IN) for l in open(os.path.join(golden_dir, f"psw_{name}.in.tsv")) if l.strip()]
+    pout = [parse(l, PSW_OUT) for l in open(os.path.join(golden_dir, f"psw_{name}.out.tsv")) if l.strip()]
+    return pin, pout
+
+
+def read_pac(prefix):
+    """The packed reference (bntseq.c bns_dump / bns_pac, 4 bases per byte MSB first) unpacked
+    to one code per base, and l_pac from the .ann header (bntseq.c:100)."""
+    with open(prefix + ".ann") as f:
+        l_pac = int(f.readline().split()[0])
+    raw = np.fromfile(prefix + ".pac", dtype=np.uint8)
+    codes = np.stack([(raw >> 6) & 3, (raw >> 4) & 3, (raw >> 2) & 3, raw & 3], axis=1).reshape(-1)
+    return codes[:l_pac].copy(), l_pac
+
+
+def _seq_rev(x, comp):
+    """seq_reverse (bwaseqio.c:55-72)"""
+    y = x[::-1].copy()
+    if comp:
+        m = y < 4
+        y[m] = 3 - y[m]
+    return y
+
+
+def paired_sw(pairs, pe_type, avg, std, ap_prior, pac, l_pac):
+    """bwa_paired_sw / bwa_paired_sw_thread (bwasw.c:145-304) restated over the ends of
+    read_psw (db offset 0, one database): mutates the end dicts like the reference mutates
+    bwa_seq_t (type, pos, strand, mapQ, seQ, n_mm/gapo/gape, extra_flag, cigar) and returns
+    the counters [mated singletons, singletons, fixed, discordant] of its stderr summary."""
+    import math
+    SAM_FPP, NO_MATCH, MATESW, STD, SOLID = 2, 0, 3, 1, 2
+    n_tot, n_mapped = [0, 0], [0, 0]
+    for p in pairs:
+        for e in p:
+            e.setdefault("remapped_pos", e["pos"])
+            e.setdefault("dbidx", 0)
+            e.setdefault("remapped_dbidx", 0)
+            e.setdefault("cigar_list", [])
+            c = nt4(e["read"])
+            e["_seq"] = _seq_rev(c, False)   # bwa_seq_t.seq (bwaseqio.c:191)
+            e["_rseq"] = _seq_rev(c, True)   # bwa_seq_t.rseq (bwaseqio.c:192)
+        if not ((p[0]["mapQ"] >= 17 or p[1]["mapQ"] >= 17) and (p[0]["extra_flag"] & SAM_FPP) == 0):
+            continue
+        mq_adjust = [255, 255]
+        single = 1 if (p[0]["type"] == NO_MATCH or p[1]["type"] == NO_MATCH) else 0
+        n_tot[single] += 1
+        cig, beg, cnt = [None, None], [0, 0], [0, 0]
+        if pe_type not in (STD, SOLID):
+            continue
+        for k in (0, 1):
+            ref, mate = p[1 - k], p[k]
+            if ref["type"] == NO_MATCH:
+                continue
+            L = len(mate["read"])
+
+            def right():  # set_right_coordinate (bwasw.c:114-129), double arithmetic then truncation
+                b = int(ref["remapped_pos"] + avg - 3 * std - L * 1.5)
+                e = int(b + 6 * std + 2 * L)
+                if b < ref["remapped_pos"] + len(ref["read"]):
+                    b = ref["remapped_pos"] + len(ref["read"])
+                if e > l_pac:
+                    e = l_pac
+                return b, e
+
+            def left():  # set_left_coordinate (bwasw.c:131-143)
+                b = int(ref["remapped_pos"] + len(ref["read"]) - avg - 3 * std - L * 0.5)
+                e = int(b + 6 * std + 2 * L)
+                if b < 0:
+                    b = 0
+                if e > ref["remapped_pos"]:
+                    e = ref["remapped_pos"]
+                return b, e
+            if pe_type == STD:
+                if ref["strand"] == 0:
+                    b, e = right()
+                    seq = mate["_rseq"]
+                else:
+                    b, e = left()
+                    seq = _seq_rev(mate["_seq"], False)
+            else:
+                if ref["strand"] == 0:
+                    b, e = left() if k == 0 else right()
+                    seq = _seq_rev(mate["_rseq"], False)
+                else:
+                    b, e = right() if k == 0 else left()
+                    seq = mate["_seq"]
+            beg[k] = b
+            reglen = int(np.int32(e - b))
+            win = pac[b:b + reglen] if 0 <= b < l_pac and reglen > 0 else np.zeros(0, np.uint8)
+            r = sw_core(seq, win, reglen, b, l_pac)
+            if r is not None:
+                beg[k], cig[k], cnt[k] = r
+            if cig[k] is not None and mate["type"] != NO_MATCH:  # bwasw.c:222-236
+                clip = 0
+                if cig[k][0] >> 29 == 3:
+                    clip += cig[k][0] & 0x1FFFFFFF
+                if cig[k][-1] >> 29 == 3:
+                    clip += cig[k][-1] & 0x1FFFFFFF
+                s_old = int((mate["n_mm"] * 9 + mate["n_gapo"] * 13 + mate["n_gape"] * 2) / 3. * 8. + .499)
+                s_new = int(((cnt[k] >> 16) * 9 + (cnt[k] >> 8 & 0xff) * 13 + (cnt[k] & 0xff) * 2 + clip * 3)
+                            / 3. * 8. + .499)
+                s_old = int(s_old + -4.343 * math.log(ap_prior / l_pac))
+                s_new += int(-4.343 * math.log(.5 * math.erfc(math.sqrt(0.5) * 1.5) + .499))
+                if s_old < s_new:
+                    mq_adjust[k] = s_new - s_old
+                    cig[k] = None
+                else:
+                    mq_adjust[k] = s_old - s_new
+        k, mapQ = -1, 0
+        if cig[0] is not None and cig[1] is not None:
+            k = 0 if p[0]["mapQ"] < p[1]["mapQ"] else 1
+            mapQ = abs(p[1]["mapQ"] - p[0]["mapQ"])
+        elif cig[0] is not None:
+            k, mapQ = 0, p[1]["mapQ"]
+        elif cig[1] is not None:
+            k, mapQ = 1, p[0]["mapQ"]
+        if k >= 0 and p[k]["pos"] != beg[k]:
+            n_mapped[single] += 1
+            fx, rf = p[k], p[1 - k]
+            tmp = rf["mapQ"] - fx["mapQ"] // 2 - 8
+            if tmp <= 0:
+                tmp = 1
+            if mapQ > tmp:
+                mapQ = tmp
+            fx["mapQ"] = rf["mapQ"] = mapQ & 0xff
+            sq = rf["seQ"] if rf["seQ"] < mapQ else mapQ
+            fx["seQ"] = rf["seQ"] = sq & 0xff
+            if fx["mapQ"] > mq_adjust[k]:
+                fx["mapQ"] = mq_adjust[k] & 0xff
+            if fx["seQ"] > mq_adjust[k]:
+                fx["seQ"] = mq_adjust[k] & 0xff
+            fx["cigar_list"] = cig[k]
+            # __set_fixed (bwasw.c:167-178)
+            fx["type"] = MATESW
+            fx["pos"] = fx["remapped_pos"] = beg[k]
+            fx["dbidx"] = fx["remapped_dbidx"] = 0
+            fx["seQ"] = rf["seQ"]
+            fx["strand"] = 1 - rf["strand"] if pe_type == STD else rf["strand"]
+            fx["n_mm"], fx["n_gapo"], fx["n_gape"] = (cnt[k] >> 16) & 0xff, cnt[k] >> 8 & 0xff, cnt[k] & 0xff
+            fx["extra_flag"] |= SAM_FPP
+            rf["extra_flag"] |= SAM_FPP
+    return [n_mapped[1], n_tot[1], n_mapped[0], n_tot[0]]
+
+
+def psw_row(e):
+    """an end in the field order of psw_<set>.out.tsv"""
+    cg = e.get("cigar_list") or []
+    cs = "".join(f"{v & 0x1FFFFFFF}{'MIDS'[v >> 29]}" for v in cg) or "*"
+    return (e["type"], e["strand"], e["pos"], e.get("remapped_pos", e["pos"]), e.get("dbidx", 0),
+            e.get("remapped_dbidx", 0), e["mapQ"], e["seQ"], e["n_mm"], e["n_gapo"], e["n_gape"], e["extra_flag"],
+            len(cg), cs)

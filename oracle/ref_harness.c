@@ -15,6 +15,8 @@
  *   ibwa_ref swf <pairs.tsv>               -> aln_local_core over a file of pairs
  *   ibwa_ref sa <prefix> <rows.tsv>        -> bwt_sa (bwt.c:69) over bwt_restore_sa (bwtio.c:29)
  *   ibwa_ref samse|sampe ...               -> bwa_sai2sam_se / bwa_sai2sam_pe (bwase.c:710, bwape.c)
+ *   ibwa_ref psw <prefix> <pairs.tsv> <type> <avg> <std> <ap_prior>
+ *                                          -> bwa_paired_sw (bwasw.c:270) on pairs read from a file
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +25,8 @@
 #include "bwt.h"
 #include "bwtaln.h"
 #include "stdaln.h"
+#include "dbset.h"
+#include "bwasw.h"
 
 int bwa_index(int argc, char *argv[]);
 int bwa_sai2sam_se(int argc, char *argv[]);
@@ -143,6 +147,87 @@ static int cmd_sa(int argc, char *argv[])
 	return 0;
 }
 
+/* psw: bwa_paired_sw (bwasw.c:270-304) over mate pairs described one per line as
+ *   <end 0 fields> <TAB> <end 1 fields>, each end = read(ACGTN) strand type mapQ seQ extra_flag
+ *   n_mm n_gapo n_gape pos   (space separated)
+ * The bwa_seq_t are set up as bwa_read_seq does (bwaseqio.c:180-192: seq = the read reversed,
+ * rseq = its reverse complement); remapped_pos = pos.  Prints per end the fields bwa_paired_sw
+ * may change and the CIGAR, then the four counters of its stderr summary. */
+pe_opt_t *bwa_init_pe_opt(void); /* bwape.c:72, not declared in a header */
+static void psw_end(bwa_seq_t *p, char *f)
+{
+	char rd[4096];
+	unsigned strand, type, mapQ, seQ, xf, mm, go, ge;
+	unsigned long long pos;
+	int i, l;
+	sscanf(f, "%4095s %u %u %u %u %u %u %u %u %llu", rd, &strand, &type, &mapQ, &seQ, &xf, &mm, &go, &ge, &pos);
+	l = strlen(rd);
+	memset(p, 0, sizeof(*p));
+	p->len = p->full_len = p->clip_len = l;
+	p->seq = (ubyte_t*)calloc(l, 1);
+	p->rseq = (ubyte_t*)calloc(l, 1);
+	for (i = 0; i < l; ++i) p->seq[i] = nst_nt4_table[(int)rd[i]];
+	memcpy(p->rseq, p->seq, l);
+	seq_reverse(l, p->seq, 0);
+	seq_reverse(l, p->rseq, 1);
+	p->strand = strand; p->type = type; p->mapQ = mapQ; p->seQ = seQ; p->extra_flag = xf;
+	p->n_mm = mm; p->n_gapo = go; p->n_gape = ge;
+	p->pos = p->remapped_pos = pos;
+}
+
+static int cmd_psw(int argc, char *argv[])
+{
+	static char line[1 << 14];
+	const char *prefix[1];
+	dbset_t *dbs;
+	pe_opt_t *popt;
+	isize_info_t ii;
+	bwa_seq_t *seqs[2];
+	int n = 0, m = 1024, i, k, j;
+	FILE *fp;
+	if (argc < 7) return 1;
+	prefix[0] = argv[1];
+	dbs = dbset_restore(1, prefix, BWA_MODE_GAPE | BWA_MODE_COMPREAD, 0, 0);
+	popt = bwa_init_pe_opt();
+	popt->type = atoi(argv[3]);
+	popt->n_threads = 1;
+	memset(&ii, 0, sizeof ii);
+	ii.avg = atof(argv[4]); ii.std = atof(argv[5]); ii.ap_prior = atof(argv[6]);
+	seqs[0] = (bwa_seq_t*)calloc(m, sizeof(bwa_seq_t));
+	seqs[1] = (bwa_seq_t*)calloc(m, sizeof(bwa_seq_t));
+	if (!(fp = fopen(argv[2], "r"))) return 1;
+	while (fgets(line, sizeof line, fp)) {
+		char *t = strchr(line, '\t');
+		if (!t) continue;
+		*t = 0;
+		if (n == m) {
+			m <<= 1;
+			seqs[0] = (bwa_seq_t*)realloc(seqs[0], m * sizeof(bwa_seq_t));
+			seqs[1] = (bwa_seq_t*)realloc(seqs[1], m * sizeof(bwa_seq_t));
+		}
+		psw_end(seqs[0] + n, line);
+		psw_end(seqs[1] + n, t + 1);
+		++n;
+	}
+	fclose(fp);
+	bwa_paired_sw(dbs, n, seqs, popt, &ii);
+	for (i = 0; i < n; ++i) {
+		for (k = 0; k < 2; ++k) {
+			bwa_seq_t *p = seqs[k] + i;
+			printf("%s%u %u %llu %llu %u %u %u %u %u %u %u %u %d ", k ? "\t" : "", p->type, p->strand,
+			       (unsigned long long)p->pos, (unsigned long long)p->remapped_pos, p->dbidx, p->remapped_dbidx,
+			       p->mapQ, (unsigned)p->seQ, p->n_mm, p->n_gapo, p->n_gape, p->extra_flag, p->n_cigar);
+			if (!p->n_cigar) printf("*");
+			for (j = 0; j < p->n_cigar; ++j) printf("%u%c", __cigar_len(p->cigar[j]), "MIDS"[__cigar_op(p->cigar[j])]);
+			free(p->seq); free(p->rseq); free(p->cigar);
+		}
+		printf("\n");
+	}
+	free(seqs[0]); free(seqs[1]); free(popt);
+	dbset_destroy(dbs);
+	return 0;
+}
+
 int main(int argc, char *argv[])
 {
 	if (argc < 2) {
@@ -155,6 +240,7 @@ int main(int argc, char *argv[])
 	if (strcmp(argv[1], "sw") == 0) return cmd_sw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "swf") == 0) return cmd_swf(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
+	if (strcmp(argv[1], "psw") == 0) return cmd_psw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "samse") == 0) return bwa_sai2sam_se(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sampe") == 0) return bwa_sai2sam_pe(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);

@@ -31,23 +31,13 @@ class RefBwt(c.Structure):  # bwt_t (bwt.h:41-53)
                 ("sa_intv", c.c_int), ("n_sa", c.c_uint32), ("sa", c.POINTER(c.c_uint32))]
 
 
-class RefSeq(c.Structure):  # bwa_seq_t (bwtaln.h:62-93)
-    _fields_ = [("name", c.c_void_p), ("seq", c.c_void_p), ("rseq", c.c_void_p), ("qual", c.c_void_p),
-                ("len", c.c_uint32, 20), ("strand", c.c_uint32, 1), ("type", c.c_uint32, 2),
-                ("dummy", c.c_uint32, 1), ("extra_flag", c.c_uint32, 8),
-                ("n_mm", c.c_uint32, 8), ("n_gapo", c.c_uint32, 8), ("n_gape", c.c_uint32, 8),
-                ("mapQ", c.c_uint32, 8), ("score", c.c_int), ("clip_len", c.c_int), ("n_aln", c.c_int),
-                ("aln", c.c_void_p), ("n_multi", c.c_int), ("multi", c.c_void_p), ("sa", c.c_uint32),
-                ("pos", c.c_uint64), ("remapped_pos", c.c_uint64), ("dbidx", c.c_uint32),
-                ("remapped_dbidx", c.c_uint32), ("remapped_seqid", c.c_int32), ("remap_identical", c.c_int),
-                ("c1", c.c_uint64, 28), ("c2", c.c_uint64, 28), ("seQ", c.c_uint64, 8), ("n_cigar", c.c_int),
-                ("cigar", c.c_void_p), ("tid", c.c_int), ("bc", c.c_char * 16),
-                ("full_len", c.c_uint32, 20), ("nm", c.c_uint32, 12), ("md", c.c_void_p)]
+RefSeq = E.RefSeq  # bwa_seq_t (bwtaln.h:62-93)
 
 
 LAYOUT_C = r"""
 #include <stddef.h>
 #include "bwtaln.h"
+#include "bwapair.h"
 #include "ibwa_bwa_compat.h"
 #define SAME(R, M, F) _Static_assert(offsetof(R, F) == offsetof(M, F), #R "." #F); \
                       _Static_assert(sizeof(((R *)0)->F) == sizeof(((M *)0)->F), #R "." #F " size");
@@ -73,6 +63,14 @@ SAME(gap_opt_t, ibwa_gap_opt_t, max_diff) SAME(gap_opt_t, ibwa_gap_opt_t, seed_l
 SAME(gap_opt_t, ibwa_gap_opt_t, max_top2) SAME(gap_opt_t, ibwa_gap_opt_t, trim_qual)
 SIZE(bwt_aln1_t, ibwa_aln1_t)
 SAME(bwt_aln1_t, ibwa_aln1_t, k) SAME(bwt_aln1_t, ibwa_aln1_t, l) SAME(bwt_aln1_t, ibwa_aln1_t, score)
+SIZE(pe_opt_t, ibwa_ref_pe_opt_t)
+SAME(pe_opt_t, ibwa_ref_pe_opt_t, max_isize) SAME(pe_opt_t, ibwa_ref_pe_opt_t, n_threads)
+SAME(pe_opt_t, ibwa_ref_pe_opt_t, type) SAME(pe_opt_t, ibwa_ref_pe_opt_t, is_sw)
+SAME(pe_opt_t, ibwa_ref_pe_opt_t, remapping) SAME(pe_opt_t, ibwa_ref_pe_opt_t, ap_prior)
+SIZE(isize_info_t, ibwa_ref_isize_info_t)
+SAME(isize_info_t, ibwa_ref_isize_info_t, avg) SAME(isize_info_t, ibwa_ref_isize_info_t, std)
+SAME(isize_info_t, ibwa_ref_isize_info_t, ap_prior) SAME(isize_info_t, ibwa_ref_isize_info_t, low)
+SAME(isize_info_t, ibwa_ref_isize_info_t, high) SAME(isize_info_t, ibwa_ref_isize_info_t, high_bayesian)
 int main(void) { return 0; }
 """
 

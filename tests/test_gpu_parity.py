@@ -79,7 +79,7 @@ def test_sai_goldens_heavy_pass(golden_dir, sai_manifest, gpu_engine, coop):
             if coop and "-m" in m["argv"] and max(lens) <= 256 and st.n_coop != st.n_heavy:
                 bad.append(key + f":coop resolved {st.n_coop} of {st.n_heavy}")
     finally:
-        gpu_engine.set_option("gap_iter_budget", 4000)
+        gpu_engine.set_option("gap_iter_budget", 8000)
         gpu_engine.set_option("gap_coop", 1)
     assert not bad, bad
 

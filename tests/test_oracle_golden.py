@@ -74,3 +74,17 @@ def test_sa2pos_restatement_matches_reference_vectors(golden_dir):
     assert (got == pos).all()
     assert all((b0 if s[i] else b1).bwt_sa(int(k[i])) == sa[i] for i in range(0, len(k), 7))
     assert steps.max() > 64  # walks well past one sampling interval are covered
+
+
+@pytest.mark.parametrize("name", ["std100", "std150", "solid50"])
+def test_paired_sw_restatement_matches_reference(golden_dir, name):
+    """bwa_paired_sw (bwasw.c:145-304) restated == the reference's own outputs (tools/make_psw_golden.py)."""
+    import json
+    m = json.load(open(os.path.join(golden_dir, "psw_manifest.json")))[name]
+    pac, l_pac = oracle.read_pac(os.path.join(golden_dir, "g1m"))
+    pin, pout = oracle.read_psw(golden_dir, name)
+    cnt = oracle.paired_sw(pin, m["type"], m["avg"], m["std"], m["ap_prior"], pac, l_pac)
+    assert cnt == [m["mated_singletons"], m["singletons"], m["fixed"], m["discordant"]]
+    bad = [(i, k) for i, (p, q) in enumerate(zip(pin, pout)) for k in (0, 1)
+           if oracle.psw_row(p[k]) != tuple(q[k][f] for f in oracle.PSW_OUT)]
+    assert not bad, bad[:5]

@@ -106,7 +106,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
     o, e = eopt(argv)
     defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
-                "gap_iter_budget": 4000, "gap_coop": 1}
+                "gap_iter_budget": 8000, "gap_coop": 1}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
