@@ -133,6 +133,34 @@ def cpu_baseline(eng, opt_args, seq, off, lns, budget_s, threads):
                       f"{threads} pthreads, oracle/ibwa_oracle.c)"}, tch, n_s, (n_aln, alns)
 
 
+def sa2pos_leg(eng, lns):
+    """SA -> coordinate (bwtdb_sa2seq, dbset.c:240) of each read's first hit after the timed aln
+    steps, as samse/sampe would ask for it: kernel time (HIP events) with the full SA resident
+    (one gather per hit) and with the sampled SA (bwt_sa's LF walk, bwt.c:69), plus a check
+    that both agree.  Not part of `value`."""
+    n_aln, alns = eng.fetch()
+    has = n_aln > 0
+    first = np.concatenate([[0], np.cumsum(n_aln)[:-1]])[has]
+    a = ((alns["info"][first] >> 24) & 1).astype(np.uint8)
+    k = alns["k"][first]
+    ln = lns[has]
+    out = {"hits": int(k.size)}
+    res = []
+    for walk in (0, 1):
+        eng.set_option("sa_walk", walk)
+        eng.sa2pos(a, k, ln)  # warm
+        pos = eng.sa2pos(a, k, ln)
+        st = eng.stats()
+        tag = "walk" if walk else "full"
+        out[f"{tag}_ms"] = st.ms_sa2pos
+        out[f"{tag}_Mpos_per_s"] = k.size / (st.ms_sa2pos * 1e-3) / 1e6 if st.ms_sa2pos > 0 else None
+        out[f"{tag}_used_full_sa"] = int(st.sa2pos_full)
+        res.append(pos)
+    eng.set_option("sa_walk", 0)
+    out["walk_equals_full"] = bool((res[0] == res[1]).all())
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,6 +176,7 @@ def main():
     ap.add_argument("--kmer-k", type=int, default=-1, help="K-mer table length for the exact path (-1 auto, 0 off)")
     ap.add_argument("--exact-path", type=int, default=1, help="use the exact-match kernel when max_diff == 0")
     ap.add_argument("--sweep-k", default="", help="comma list of K values to time after the main run")
+    ap.add_argument("--sa2pos", type=int, default=1, help="also time SA->coordinate of every read's first hit")
     ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
     args = ap.parse_args()
 
@@ -179,7 +208,7 @@ def main():
 
     eng = E.Engine(local)
     tb = time.perf_counter()
-    eng.build_index(codes)
+    eng.build_index(codes, sa_intv=32)  # the sampled SA too (bwa index's .sa/.rsa), for the sa2pos leg
     build_s = time.perf_counter() - tb
     del codes
     log(f"index built on device in {build_s:.1f} s")
@@ -296,6 +325,8 @@ def main():
                            "path": {0: "width+search", 1: "exact", 2: "width+gapped", 3: "exact+jump"}.get(path, str(path)),
                            "k_width_or_pack_ms": ms_w / launches, "k_search_ms": ms_s / launches,
                            "retry_ms": ms_r / launches}
+        if args.sa2pos:
+            result["extra"]["sa2pos"] = sa2pos_leg(eng, lns)
         print(json.dumps(result), flush=True)
         for k in [int(x) for x in args.sweep_k.split(",") if x.strip()]:
             eng.set_option("kmer_k", k)
