@@ -26,8 +26,8 @@
 // discarded (their staging rolled back) and re-run once the hit (top-2 rule,
 // dedup, gap_shadow, max_diff) has been applied.
 //
-// Reasons a read is handed on (status bits 8-15, diagnostics): 1 read too long /
-// too many buckets / staging too small, 3 page pool empty, 4 a bucket past
+// Reasons a read is handed on (status bits 8-15, diagnostics): 1 read too long / seed
+// too long / too many buckets / staging too small, 3 page pool empty, 4 a bucket past
 // COOP_MAXP pages, 5 runaway guard.  Such reads go to the sequential kernel
 // (gapped.hip, wide).
 //
@@ -136,7 +136,7 @@ struct Shm {
   uint32_t nb[NSTK];       // entries per bucket
   uint32_t np[NSTK];       // pages per bucket
   uint2 W[2][COOP_MAXLEN + 1];   // width arrays {w, bid} of strands 0 / 1 (bwt_width_t)
-  uint2 SW[2][COOP_MAXLEN + 1];  // seed width arrays
+  uint2 SW[2][COOP_SEEDMAX + 1];  // seed width arrays
   uint8_t str[2][COOP_MAXLEN];   // strand 0 = bwa_seq_t.seq, strand 1 = complement (COMPREAD)
   uint32_t head[64];             // per-lane staging ring: first uncommitted slot
   uint32_t rb[64];               // per-lane staging rollback point (discarded chains)
@@ -197,7 +197,8 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
     uint32_t status = 0;
     int n_aln = 0;
     uint32_t n_iter = 0;
-    if (len > COOP_MAXLEN || o.n_stacks > NSTK || (1u << A.stg_log2) < 9u * (uint32_t)(len + 1) + 16u) {
+    if (len > COOP_MAXLEN || o.n_stacks > NSTK || (1u << A.stg_log2) < 9u * (uint32_t)(len + 1) + 16u ||
+        (len > o.seed_len && o.seed_len > COOP_SEEDMAX)) {
       status = ST_STACK_OVERFLOW | 1u << 8;  // not for this kernel: the sequential kernel takes it
     } else if ((int)A.nN[r] > opt_max_diff) {
       // bwtgap.c:116-122: no hit

@@ -90,6 +90,7 @@ hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int bl
 // Wave-cooperative gapped search for heavy reads (coop.hip): one read per wavefront,
 // its match chains run across the lanes and committed in the reference's pop order.
 constexpr int COOP_MAXLEN = 256;       // longest read the kernel takes (LDS strands / widths)
+constexpr int COOP_SEEDMAX = 64;       // longest seed (-l) of a seeded read it takes (LDS seed widths)
 constexpr int COOP_PG_LOG2 = 13;       // bucket pages of 8192 entries (128 KiB): 256 pages hold 2M entries
 constexpr uint32_t COOP_PG = 1u << COOP_PG_LOG2;
 constexpr int COOP_NSTK = 128, COOP_MAXP = 256;

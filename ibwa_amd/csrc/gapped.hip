@@ -53,6 +53,9 @@ constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
 // per-lane LDS stack of popped slots awaiting reuse (the retry pass's heavy reads get more)
 constexpr int NARROW_FREE_DEPTH = 8;
 constexpr int MAX_BUCKETS = 128;  // non-empty-bucket bitmask: four 32-bit registers
+// first pass: a read of <= 16 * RDW bases without N is kept 2-bit packed in LDS, so the read
+// symbol of an iteration is an LDS access instead of one more HBM line request
+constexpr int RDW = 8;
 
 // Non-empty score buckets as a 128-bit mask in four named registers (no array: scratch).
 struct BMask {
@@ -148,7 +151,8 @@ template <bool WIDE> struct Ent {
 }  // namespace
 
 // LDS layout (per workgroup of NB lanes, lane-minor so a wave's accesses are consecutive):
-//   heads[n_stacks][LN] (H), free[free_depth][LN] (H), ptab[max_pages][LN] (u16), bitmap[ceil(NPB/32)] (u32)
+//   heads[n_stacks][LN] (H), free[free_depth][LN] (H), ptab[max_pages][LN] (u16), bitmap[ceil(NPB/32)] (u32),
+//   narrow only: reads[RDW][LN] (u32, 16 bases each)
 // with LN = the block's lanes that run reads (block / 64 * lanes_per_wave)
 size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int pages_per_block, int lanes_per_wave,
                         int free_depth) {
@@ -156,7 +160,7 @@ size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int p
   const int fd = wide ? free_depth : NARROW_FREE_DEPTH;
   size_t b = (size_t)(n_stacks + fd) * ln * (wide ? 4 : 2) + (size_t)max_pages * ln * 2;
   b = (b + 3) & ~(size_t)3;
-  return b + (size_t)((pages_per_block + 31) / 32) * 4;
+  return b + (size_t)((pages_per_block + 31) / 32) * 4 + (wide ? 0 : (size_t)RDW * ln * 4);
 }
 
 // PROF: per-wave cycle accounting of the loop's phases into A.prof[] (diagnostics build of
@@ -184,6 +188,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   uint32_t *const bitmap =
       reinterpret_cast<uint32_t *>(ptab + ((A.max_pages * LNB + 1) & ~1));  // 4-byte aligned, still LDS
   const int bm_words = (A.pages_per_block + 31) / 32;
+  uint32_t *const rdl = bitmap + bm_words;  // narrow: the lane's read, rdl[(w << nbl) + ltid]
   for (int w = tid; w < bm_words; w += NB) {
     const int lo = w * 32, hi = lo + 32 < A.pages_per_block ? lo + 32 : A.pages_per_block;
     bitmap[w] = hi - lo >= 32 ? 0u : ~((1u << (hi - lo)) - 1u);  // bits past the pool stay taken
@@ -216,6 +221,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   bool fl_known = true;
   bool seeded = false;
   const uint8_t *s = nullptr;
+  bool fastrd = false;  // the read's symbols are in LDS (rdl)
   const uint2 *W0 = nullptr, *W1 = nullptr, *SW0 = nullptr, *SW1 = nullptr;
   BMask nonempty = {0u, 0u, 0u, 0u};
   uint4 C = make_uint4(0, 0, 0, 0);
@@ -308,10 +314,34 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         W1 = wb + A.wlen1;
         SW0 = wb + 2 * A.wlen1;
         SW1 = SW0 + (o.seed_len + 1);
-        if ((int)A.nN[r] > max_diff) {  // bwtgap.c:116-122
+        const int nN = (int)A.nN[r];
+        if (nN > max_diff) {  // bwtgap.c:116-122
           A.n_aln[ro] = 0;
           A.status[ro] = 0;
         } else {
+          fastrd = !WIDE && nN == 0 && len <= 16 * RDW;
+          if (fastrd) {
+            // 16 B loads from the aligned-down start (the staging buffer has 16 B of tail padding)
+            const uint4 *q0 = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15);
+            const int mis = (int)(reinterpret_cast<uintptr_t>(s) & 15);
+            const int nq = (mis + len + 15) >> 4;
+            uint32_t w = 0;
+            for (int q = 0; q < nq; ++q) {
+              const uint4 v = q0[q];
+#pragma unroll
+              for (int b = 0; b < 16; ++b) {
+                const uint32_t word = b < 4 ? v.x : b < 8 ? v.y : b < 12 ? v.z : v.w;
+                const int jj = q * 16 + b - mis;
+                if (jj >= 0 && jj < len) {
+                  w |= ((word >> (8 * (b & 3))) & 3u) << (2 * (jj & 15));
+                  if ((jj & 15) == 15 || jj == len - 1) {
+                    rdl[((jj >> 4) << nbl) + ltid] = w;
+                    w = 0;
+                  }
+                }
+              }
+            }
+          }
           // roots (bwtgap.c:126-127): strand 0 then strand 1, both score 0 -> C = strand 1
           ent1[0] = E::make(0u, ixv0.seq_len, len, 0, NILH, 0, 0, 0, 0, STATE_M);
           C = E::make(0u, ixv0.seq_len, len, 0, 0u, 0, 0, 0, 1, STATE_M);
@@ -443,8 +473,10 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     }
     // read symbol str[i-1] (search) or str[xj] (exact); strand 1 = complement under COMPREAD
     uint32_t sym = 0;
-    if (srch && i > 0) sym = s[i - 1];
-    if (st == 2 && xj >= 0) sym = s[xj];
+    {
+      const int sp = (srch && i > 0) ? i - 1 : (st == 2 && xj >= 0) ? xj : -1;
+      if (sp >= 0) sym = fastrd ? (rdl[((sp >> 4) << nbl) + ltid] >> (2 * (sp & 15))) & 3u : s[sp];
+    }
     // next candidate
     uint4 Cn = make_uint4(0, 0, 0, 0);
     if (do_pop && C_load) Cn = *slot_ptr(load_slot);
