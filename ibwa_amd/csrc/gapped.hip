@@ -723,13 +723,22 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     }
     if (do_add) {
       // gap_shadow (bwtgap.c:81-91) on this strand's width array
+      // (8 positions per round trip: a load-modify-store per position would cost one HBM
+      // round trip each, and a wave waits for its longest lane)
       uint2 *width = const_cast<uint2 *>(a ? W1 : W0);
       const uint32_t x = l - k + 1, mx = ix.seq_len;
       uint32_t jj = 0;
-      for (int q = 0; q < ldp; ++q) {
-        uint2 w = width[q];
-        if (w.x > x) { w.x -= x; width[q] = w; }
-        else if (w.x == x) { ++jj; width[q] = make_uint2(mx - jj, 1u); }
+      for (int q0 = 0; q0 < ldp; q0 += 8) {
+        uint2 wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wv[u] = q0 + u < ldp ? width[q0 + u] : make_uint2(0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (q0 + u >= ldp) break;
+          const uint2 w = wv[u];
+          if (w.x > x) width[q0 + u] = make_uint2(w.x - x, w.y);
+          else if (w.x == x) { ++jj; width[q0 + u] = make_uint2(mx - jj, 1u); }
+        }
       }
       if ((uint32_t)n_aln >= HS) {
         if (pl_) pf6 += pnow() - t0_;
