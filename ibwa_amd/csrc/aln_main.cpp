@@ -17,8 +17,10 @@
 #include <zlib.h>
 
 #include <chrono>
+#include <algorithm>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "ibwa_aln.h"
@@ -92,6 +94,80 @@ struct SeqReader {
   }
 };
 
+// BAM input: bam_header_read / bam_read1 (bamlite.c:34-116) over gzread (a BGZF file is a
+// series of gzip members), and the record selection and decoding of bwa_read_bam
+// (bwaseqio.c:89-143): `which` bit 1 = read 1, 2 = read 2, 4 = neither (bwtaln.c:159-171);
+// 4-bit bases -> A/C/G/T/N, reverse-strand records reverse-complemented back, qualities
+// +33 capped at 126.  The record is handed on as FASTQ-like strings.
+struct BamReader {
+  gzFile fp = nullptr;
+  int which = 7;
+  std::string name, seq, qual;
+  std::vector<uint8_t> data;
+  bool readn(void *p, int n) { return gzread(fp, p, (unsigned)n) == n; }
+  bool open(const char *fn, int w) {
+    which = w;
+    fp = strcmp(fn, "-") ? gzopen(fn, "r") : gzdopen(fileno(stdin), "r");
+    if (!fp) return false;
+    gzbuffer(fp, 1 << 20);
+    char magic[4];
+    if (!readn(magic, 4) || memcmp(magic, "BAM\1", 4) != 0) {
+      fprintf(stderr, "[bam_header_read] invalid BAM binary header (this is not a BAM file).\n");
+      return false;
+    }
+    int32_t l_text = 0, n_ref = 0;
+    if (!readn(&l_text, 4)) return false;
+    std::vector<char> text(l_text > 0 ? l_text : 0);
+    if (l_text > 0 && !readn(text.data(), l_text)) return false;
+    if (!readn(&n_ref, 4)) return false;
+    for (int32_t i = 0; i < n_ref; ++i) {
+      int32_t l_name = 0;
+      uint32_t l_ref = 0;
+      if (!readn(&l_name, 4) || l_name < 0) return false;
+      std::vector<char> nm(l_name);
+      if ((l_name && !readn(nm.data(), l_name)) || !readn(&l_ref, 4)) return false;
+    }
+    return true;
+  }
+  ~BamReader() {
+    if (fp) gzclose(fp);
+  }
+  // seq length of the next selected record, -1 at EOF, -2 on a truncated record
+  int read() {
+    static const char nt16[] = "NACNGNNNTNNNNNNN";  // bam_nt16_nt4_table (bwaseqio.c:11) as bases
+    for (;;) {
+      int32_t block_len = 0;
+      const int got = gzread(fp, &block_len, 4);
+      if (got == 0) return -1;
+      if (got != 4 || block_len < 32) return -2;
+      uint32_t x[8];
+      if (!readn(x, 32)) return -2;
+      const int l_qname = x[2] & 0xff, flag = x[3] >> 16, n_cigar = x[3] & 0xffff, l_qseq = (int)x[4];
+      data.resize(block_len - 32);
+      if (!data.empty() && !readn(data.data(), (int)data.size())) return -2;
+      int go = 0;
+      if ((which & 1) && (flag & 0x40)) go = 1;
+      if ((which & 2) && (flag & 0x80)) go = 1;
+      if ((which & 4) && !(flag & 0x40) && !(flag & 0x80)) go = 1;
+      if (!go) continue;
+      const uint8_t *sq = data.data() + l_qname + 4 * n_cigar, *q = sq + (l_qseq + 1) / 2;
+      name.assign((const char *)data.data());
+      seq.resize(l_qseq);
+      qual.resize(l_qseq);
+      for (int i = 0; i < l_qseq; ++i) {
+        seq[i] = nt16[(sq[i >> 1] >> ((~i & 1) << 2)) & 0xf];
+        qual[i] = (char)(q[i] + 33 < 126 ? q[i] + 33 : 126);
+      }
+      if (flag & 0x10) {  // seq_reverse(len, seq, 1) / seq_reverse(len, qual, 0)
+        std::reverse(seq.begin(), seq.end());
+        std::reverse(qual.begin(), qual.end());
+        for (auto &ch : seq) ch = ch == 'A' ? 'T' : ch == 'C' ? 'G' : ch == 'G' ? 'C' : ch == 'T' ? 'A' : ch;
+      }
+      return l_qseq;
+    }
+  }
+};
+
 struct Batch {
   std::vector<uint8_t> seq;
   std::vector<uint64_t> off;
@@ -100,12 +176,14 @@ struct Batch {
   int64_t n() const { return (int64_t)len.size(); }
 };
 
-// bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input
-bool read_batch(SeqReader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
+// bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input, bwa_read_bam (:89-143) for BAM
+template <class Reader>
+bool read_batch(Reader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
   b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0;
-  const bool is_64 = mode & IBWA_MODE_IL13;
-  const int l_bc = (unsigned)mode >> 24;
-  if (l_bc > 15) {
+  const bool bam = std::is_same<Reader, BamReader>::value;
+  const bool is_64 = !bam && (mode & IBWA_MODE_IL13);
+  const int l_bc = bam ? 0 : (int)((unsigned)mode >> 24);  // no barcode for BAM (bwaseqio.c:156)
+  if (((unsigned)mode >> 24) > 15) {
     fprintf(stderr, "[bwa_read_seq] the maximum barcode length is 15.\n");
     return false;
   }
@@ -114,7 +192,7 @@ bool read_batch(SeqReader &rd, int mode, int trim_qual, Batch &b, long *n_trimme
     std::string &s = rd.seq, &q = rd.qual;
     if (is_64 && !q.empty())
       for (auto &ch : q) ch = (char)(ch - 31);
-    if ((int)s.size() <= l_bc) continue;
+    if (!bam && (int)s.size() <= l_bc) continue;  // bwaseqio.c:162 (not on the BAM path)
     if (l_bc) {
       s.erase(0, l_bc);
       if (!q.empty()) q.erase(0, l_bc);
@@ -171,6 +249,9 @@ int die(const char *what) {
 
 }  // namespace
 
+template <class Reader>
+int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out, int n_gpus);
+
 int main(int argc, char *argv[]) {
   if (argc < 2 || strcmp(argv[1], "aln") != 0) {
     fprintf(stderr, "Usage: ibwa-amd aln [options] <prefix> <in.fq>\n");
@@ -224,10 +305,6 @@ int main(int argc, char *argv[]) {
     usage(&opt);
     return 1;
   }
-  if (opt.mode & IBWA_MODE_BAM) {
-    fprintf(stderr, "[ibwa-amd aln] BAM input (-b) is not supported yet; convert to FASTQ\n");
-    return 1;
-  }
   if (opt.fnr > 0.0f) {  // bwtaln.c:317-324
     for (int i = 17, k = 0; i <= 250; ++i) {
       int l = ibwa_cal_maxdiff(i, 0.02, opt.fnr);
@@ -236,11 +313,29 @@ int main(int argc, char *argv[]) {
     }
   }
   const std::string prefix = argv[optind];
+  if (opt.mode & IBWA_MODE_BAM) {  // bwa_open_reads (bwtaln.c:159-171)
+    int which = 0;
+    if (opt.mode & IBWA_MODE_BAM_SE) which |= 4;
+    if (opt.mode & IBWA_MODE_BAM_READ1) which |= 1;
+    if (opt.mode & IBWA_MODE_BAM_READ2) which |= 2;
+    if (which == 0) which = 7;
+    BamReader rd;
+    if (!rd.open(argv[optind + 1], which)) {
+      fprintf(stderr, "[ibwa-amd aln] cannot open %s as BAM\n", argv[optind + 1]);
+      return 1;
+    }
+    return run_aln(rd, opt, prefix, fn_out, n_gpus);
+  }
   SeqReader rd;
   if (!rd.open(argv[optind + 1])) {
     fprintf(stderr, "[ibwa-amd aln] cannot open %s\n", argv[optind + 1]);
     return 1;
   }
+  return run_aln(rd, opt, prefix, fn_out, n_gpus);
+}
+
+template <class Reader>
+int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out, int n_gpus) {
   FILE *out = fn_out ? fopen(fn_out, "wb") : stdout;
   if (!out) {
     fprintf(stderr, "[ibwa-amd aln] cannot write %s\n", fn_out);

@@ -1,0 +1,47 @@
+"""The `ibwa-amd aln` CLI (aln_main.cpp) against the reference's `aln` output: FASTQ input over
+a cross-section of the option matrix, and BAM input (-b, -0/-1/-2, bwa_read_bam
+bwaseqio.c:89-143) on tests/golden/reads.bam (tools/make_bam_golden.py).  Byte-identical .sai,
+n_threads header field masked (bwtaln.c:192)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "ibwa_amd", "bin", "ibwa-amd")
+FASTQ_KEYS = ["r100.default", "mixed.default", "r36.n0", "mixed.n3o2e3", "mixed.q15", "mixed.B4", "illumina.I",
+              "mixed.c", "r100.t4", "mixed.N"]
+
+
+def run_cli(argv, golden_dir, reads, tmp_path):
+    out = tmp_path / "out.sai"
+    r = subprocess.run([CLI, "aln"] + argv + ["-f", str(out), os.path.join(golden_dir, "g1m"),
+                                              os.path.join(golden_dir, reads)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return out.read_bytes()
+
+
+@pytest.mark.parametrize("key", FASTQ_KEYS)
+def test_cli_fastq(golden_dir, sai_manifest, key, tmp_path):
+    m = sai_manifest[key]
+    got = run_cli(m["argv"], golden_dir, m["reads"], tmp_path)
+    assert oracle.sai_body_equal(got, open(os.path.join(golden_dir, key + ".sai"), "rb").read())
+
+
+@pytest.mark.parametrize("key", ["all", "se", "r1", "r2", "r12", "q15", "n0"])
+def test_cli_bam(golden_dir, key, tmp_path):
+    m = json.load(open(os.path.join(golden_dir, "bam_manifest.json")))[key]
+    got = run_cli(m["argv"], golden_dir, "reads.bam", tmp_path)
+    assert oracle.sai_body_equal(got, open(os.path.join(golden_dir, m["sai"]), "rb").read())
+
+
+def test_cli_rejects_non_bam(golden_dir, tmp_path):
+    r = subprocess.run([CLI, "aln", "-b", os.path.join(golden_dir, "g1m"), os.path.join(golden_dir, "reads_r36.fq")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "BAM" in r.stderr
