@@ -776,8 +776,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         G.iters = c->d_iters.as<uint32_t>() + b0;
       }
       if (c->prof_phases) {
-        if (int rc = c->d_prof.ensure(64)) return rc;
-        HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 64, c->stream));
+        if (int rc = c->d_prof.ensure(128)) return rc;
+        HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 128, c->stream));
         G.prof = c->d_prof.as<unsigned long long>();
       }
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
@@ -805,13 +805,16 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                 it[(size_t)(cnt * 0.99)], it[(size_t)(cnt * 0.9999)], mx, b, sum / (b * 1e-3));
       }
       if (c->prof_phases) {
-        unsigned long long pf[8];
-        HIPCHK(hipMemcpy(pf, c->d_prof.p, 64, hipMemcpyDeviceToHost));
-        const char *nm[8] = {"claim", "pop", "wait", "rest", " exact", " expand", " hit", " end"};
+        unsigned long long pf[11];
+        HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
+        const char *nm[4] = {"claim", "pop", "wait", "rest"};
         double tot = (double)(pf[0] + pf[1] + pf[2] + pf[3]);
         fprintf(stderr, "[ibwa_amd] k_gapped phases (wave cycles, %d waves):", blocks * block / 64);
-        for (int q = 0; q < 8; ++q) fprintf(stderr, " %s %.1f%%", nm[q], tot > 0 ? 100.0 * pf[q] / tot : 0.0);
-        fprintf(stderr, "\n");
+        for (int q = 0; q < 4; ++q) fprintf(stderr, " %s %.1f%%", nm[q], tot > 0 ? 100.0 * pf[q] / tot : 0.0);
+        const double wi = pf[9] ? (double)pf[9] : 1.0;
+        fprintf(stderr, "; per wave-iteration: exact %.3f push trips %.3f hits %.3f ends %.3f expansions %.3f "
+                "claims %.3f (%llu wave-iterations)\n", pf[4] / wi, pf[5] / wi, pf[6] / wi, pf[7] / wi, pf[8] / wi,
+                pf[10] / wi, pf[9]);
       }
     }
   }
@@ -987,6 +990,12 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         std::vector<uint32_t> it(lanes);
         HIPCHK(hipMemcpy(it.data(), K.iters, lanes * 4, hipMemcpyDeviceToHost));
         mx = *std::max_element(it.begin(), it.end());
+        double sum = 0;
+        for (uint32_t v : it) sum += v;
+        std::sort(it.begin(), it.end());
+        fprintf(stderr, "[ibwa_amd] coop wave-iterations: sum %.3g (%.0f per wave of %d), p50 %u p99 %u p99.9 %u max %u\n",
+                sum, sum / blocks, blocks, it[it.size() / 2], it[(size_t)(it.size() * 0.99)],
+                it[(size_t)(it.size() * 0.999)], mx);
       }
       uint32_t pages = 0;
       HIPCHK(hipMemcpy(&pages, K.pool_next, 4, hipMemcpyDeviceToHost));

@@ -164,8 +164,9 @@ size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int p
 }
 
 // PROF: per-wave cycle accounting of the loop's phases into A.prof[] (diagnostics build of
-// the same kernel): 0 claim, 1 pop, 2 wait for the loads, 3 rest, 4 exact step, 5 expansion,
-// 6 hit, 7 end of read.  Phases 4-7 are parts of 3, timed by the first active lane.
+// the same kernel): 0 claim, 1 pop, 2 wait for the loads, 3 rest; then wave-level event
+// counts (the wave executes a block once for all its lanes in it): 4 exact steps, 5 push-loop
+// trips, 6 hit blocks, 7 read ends, 8 expansions, 9 wave iterations, 10 read claims.
 template <bool WIDE, bool PROF>
 __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *counter) {
   using E = Ent<WIDE>;
@@ -241,6 +242,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   };
   // the read is done: hits to the output stream, pages back to the pool
   uint64_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0, pf7 = 0, t_rest = 0;
+  uint64_t pf8 = 0, pf9 = 0, pf10 = 0;
   auto pnow = []() __attribute__((always_inline)) -> uint64_t {
     uint64_t t = 0;
     if (PROF) __asm__ volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -251,7 +253,6 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   };
   auto end_read = [&](uint32_t stat) __attribute__((always_inline)) {
     const bool pl_ = pleader();
-    const uint64_t t0_ = pnow();
     int na = stat ? 0 : n_aln;
     if (na) {
       const unsigned long long pos = atomicAdd(A.aln_next, (unsigned long long)na);
@@ -272,7 +273,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     }
     n_pages = 0;
     st = 0;
-    if (pl_) pf7 += pnow() - t0_;
+    if (pl_) ++pf7;
   };
 
   for (;;) {
@@ -297,6 +298,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       const int rank = __popcll(need & lt_mask);
       const int64_t avail = cend - cur;
       if (st == 0 && rank < avail) {
+        if (pleader()) ++pf10;
         r = cur + rank;
         const int64_t rr = A.ids ? A.ids[r] : r;
         ro = A.out_by_id ? rr : r;
@@ -372,6 +374,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     pf0 += t_pop - t_top;
 
     ++n_iter;
+    if (PROF && lane == 0) ++pf9;
     // ------------------------------------------------ decide this iteration's work
     // search lanes pop C; exact lanes advance one symbol
     bool do_pop = false, finish = false;
@@ -521,7 +524,6 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     if (st == 2) {
       // one step of bwt_match_exact_alt (bwt.c:240-247)
       const bool pl_ = pleader();
-      const uint64_t t0_ = pnow();
       bool fail = false;
       if (xj >= 0) {
         if (csym > 3) {
@@ -533,7 +535,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           --xj;
         }
       }
-      if (pl_) pf4 += pnow() - t0_;
+      if (pl_) ++pf4;
       if (fail) {
         st = 1;  // no hit (bwtgap.c:162): back to popping
       } else if (xj < 0) {
@@ -576,7 +578,6 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     {
       // ---- expansion (bwtgap.c:200-258)
       const bool pl_ = pleader();
-      const uint64_t t0_ = pnow();
       const int ni = i - 1;
       const uint32_t occ = l - k + 1;
       bool allow_diff = true, allow_M = true;
@@ -647,6 +648,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
       const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
       while (vm) {
+        if (pleader()) ++pf5;
         const uint32_t j = (uint32_t)__builtin_ctz(vm);
         vm &= vm - 1;
         const bool is_ins = j == 0, is_del = j - 1 < 4, is_sym = j >= 5;
@@ -688,7 +690,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           C_valid = true;
         }
       }
-      if (pl_) pf5 += pnow() - t0_;
+      if (pl_) ++pf8;
       if (status) {  // overflow / bad score: the retry pass re-runs the read
         end_stat = status;
         st = 3;
@@ -698,7 +700,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   hit : {
     // ---- hit (bwtgap.c:165-197)
     const bool pl_ = pleader();
-    const uint64_t t0_ = pnow();
+    if (pl_) ++pf6;
     const int score = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
     bool do_add = true;
     if (n_aln == 0) {
@@ -710,7 +712,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     if (score == best_score) {
       best_cnt = (int)((uint32_t)best_cnt + (l - k + 1));
     } else if (best_cnt > o.max_top2) {
-      if (pl_) pf6 += pnow() - t0_;
+      
       end_stat = 0;
       st = 3;
       continue;
@@ -741,7 +743,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         }
       }
       if ((uint32_t)n_aln >= HS) {
-        if (pl_) pf6 += pnow() - t0_;
+        
         end_stat = ST_ALN_OVERFLOW;  // hit area full
         st = 3;
         continue;
@@ -750,14 +752,14 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
                                         k, l, (uint32_t)score);
       ++n_aln;
     }
-    if (pl_) pf6 += pnow() - t0_;
+    
     continue;
   }
   }
   if (PROF && A.prof) {
-    const uint64_t v[8] = {pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7};
+    const uint64_t v[11] = {pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7, pf8, pf9, pf10};
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
+    for (int q = 0; q < 11; ++q)
       if (v[q]) atomicAdd(A.prof + q, (unsigned long long)v[q]);
   }
 }
