@@ -166,6 +166,8 @@ struct SwArgs {
   uint32_t *cigar;                // cigar_cap per pair, aln_path2cigar32 encoding (len << 4 | op)
   int cigar_cap;
   int stop_after;                 // diagnostics: 1 after the forward pass, 2 after the reverse pass
+  int global_band;                // > 0: aln_global_core alone with this band (and gap_end), no local passes
+  int gap_end;
 };
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st);
 uint64_t sw_words_per_lane(int max_len1, int max_len2);

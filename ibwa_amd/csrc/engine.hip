@@ -1207,9 +1207,14 @@ int ibwa_aln_batch(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int64_t n, const ui
   return ibwa_batch_fetch(c, n_aln, aln, n_total);
 }
 
-int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
-                  const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int32_t *score,
-                  int32_t *path_len, int32_t *ends, int32_t *n_cigar, uint32_t **cigar, int64_t *n_cigar_total) {
+}  // extern "C"
+
+namespace {
+// k_sw launch over host arrays: the local core (global_band == 0) or aln_global_core alone
+int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
+             const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int global_band, int gap_end,
+             int32_t *score, int32_t *path_len, int32_t *ends, int32_t *n_cigar, uint32_t **cigar,
+             int64_t *n_cigar_total) {
   if (n < 0) return fail(IBWA_EINVAL, "negative pair count");
   *cigar = nullptr;
   if (n_cigar_total) *n_cigar_total = 0;
@@ -1221,8 +1226,10 @@ int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *
   int max1 = 0, max2 = 0;
   uint64_t end1 = 0, end2 = 0;
   for (int64_t p = 0; p < n; ++p) {
-    if (std::min(len1[p], len2[p]) * 11ull > 32000)
+    if (!global_band && std::min(len1[p], len2[p]) * 11ull > 32000)
       return fail(IBWA_EINVAL, "pair %lld: min(len1, len2) * 11 > 32000", (long long)p);
+    if (global_band && (uint64_t)len1[p] * len2[p] > (64ull << 20))
+      return fail(IBWA_EINVAL, "pair %lld: %u x %u cells is past the traceback bound", (long long)p, len1[p], len2[p]);
     max1 = std::max<int>(max1, (int)len1[p]);
     max2 = std::max<int>(max2, (int)len2[p]);
     end1 = std::max<uint64_t>(end1, off1[p] + len1[p]);
@@ -1270,6 +1277,8 @@ int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *
   A.ends = en.as<int4>();
   A.cigar = cg.as<uint32_t>(); A.cigar_cap = cap;
   A.stop_after = c->sw_stop_after;
+  A.global_band = global_band;
+  A.gap_end = gap_end;
   if (!rc) {
     chk(hipEventRecord(c->ev[0], c->stream), "event");
     chk(launch_sw(A, c->d_counter.as<unsigned long long>(), blocks, c->stream), "k_sw");
@@ -1301,6 +1310,24 @@ int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *
   *cigar = o;
   if (n_cigar_total) *n_cigar_total = tot;
   return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int ibwa_sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
+                  const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int32_t *score,
+                  int32_t *path_len, int32_t *ends, int32_t *n_cigar, uint32_t **cigar, int64_t *n_cigar_total) {
+  return sw_batch(c, n, ref, off1, len1, qry, off2, len2, 0, -1, score, path_len, ends, n_cigar, cigar, n_cigar_total);
+}
+
+int ibwa_global_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
+                      const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int band, int gap_end,
+                      int32_t *score, int32_t *path_len, int32_t *n_cigar, uint32_t **cigar, int64_t *n_cigar_total) {
+  if (band <= 0) return fail(IBWA_EINVAL, "band must be > 0");
+  std::vector<int32_t> ends(4 * std::max<int64_t>(n, 1));
+  return sw_batch(c, n, ref, off1, len1, qry, off2, len2, band, gap_end, score, path_len, ends.data(), n_cigar, cigar,
+                  n_cigar_total);
 }
 
 int ibwa_occ4(ibwa_ctx_t *c, int strand, int64_t n, const uint32_t *k, uint32_t *cnt) {

@@ -41,15 +41,20 @@ struct Lane {
   __device__ __forceinline__ uint8_t &t(uint32_t e) const { return tb[(uint64_t)e * 64 + lane]; }
 };
 
-// banded global alignment (aln_global_core with gap_end < 0, so its set_end_* rules are set_*):
+// banded global alignment (aln_global_core, stdaln.c:345-525).  gap_end < 0 (the local core's
+// path fill): the set_end_* rules are set_*; gap_end >= 0 (bwa_refine_gapped's aln_param_bwa,
+// stdaln.c:227): the extension penalty becomes gap_end in the set_end_I / set_end_D cells --
+// row 0's deletions, cell 0's insertions, the last cell's insertion of a row clipped at len1,
+// and every deletion of the last row (stdaln.c:392-470).
 // seq1 = a[0..n1) along i (FROM_D steps i), seq2 = b[0..n2) along j (FROM_I steps j).
 // Rows are written generically: row j covers lo(j)..hi(j) with lo = 0 while j <= b2 (cell 0 takes
 // an I from above) and j - b2 after (a -inf boundary cell); the last cell takes an I from above only
 // when the band was clipped at len1 (j + b1 - 1 > len1) -- the union of the reference's part 1-3 rows.
 // Returns the score; the path is traced into the CIGAR (reversed) and start/end coordinates.
 __device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD, uint32_t eT, uint32_t t_w,
-                           const uint8_t *a, int n1, const uint8_t *b, int n2, int band, uint32_t *cig, int cap,
-                           int &n_cig, int &path_len, int &si, int &sj) {
+                           const uint8_t *a, int n1, const uint8_t *b, int n2, int band, int gap_end, uint32_t *cig,
+                           int cap, int &n_cig, int &path_len, int &si, int &sj) {
+  const int RE = gap_end >= 0 ? gap_end : R;  // extension penalty of the set_end_* cells
   int b1, b2;
   if (n1 > n2) { b1 = n1 - n2 + band; b2 = band; } else { b1 = band; b2 = n2 - n1 + band; }
   if (b1 > n1) b1 = n1;
@@ -68,7 +73,7 @@ __device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD,
     for (int i = 1; i < b1; ++i) {
       int d;
       uint8_t tt;
-      if (pm - Q > pd) { d = pm - Q - R; tt = FM; } else { d = pd - R; tt = FD; }
+      if (pm - Q > pd) { d = pm - Q - RE; tt = FM; } else { d = pd - RE; tt = FD; }
       M(0, i) = (uint32_t)NEG_INF;
       I(0, i) = (uint32_t)NEG_INF;
       D(0, i) = (uint32_t)d;
@@ -87,7 +92,7 @@ __device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD,
       const int um = (int)M(prv, 0), ui = (int)I(prv, 0);
       uint8_t tt;
       int iv;
-      if (um - Q > ui) { iv = um - Q - R; tt = FM; } else { iv = ui - R; tt = FI; }
+      if (um - Q > ui) { iv = um - Q - RE; tt = FM; } else { iv = ui - RE; tt = FI; }
       M(cur, 0) = (uint32_t)NEG_INF;
       I(cur, 0) = (uint32_t)iv;
       D(cur, 0) = (uint32_t)NEG_INF;
@@ -111,15 +116,17 @@ __device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD,
       }
       // above cell (j-1, i)
       const int um = (int)M(prv, i), ui = (int)I(prv, i), ud = (int)D(prv, i);
-      // set_I from above; the last cell only when the band was clipped at len1
+      // set_I from above; the last cell only when the band was clipped at len1 (set_end_I)
       if (i < hi || j + b1 - 1 > n1) {
-        if (um - Q > ui) { iv = um - Q - R; ti = FM; } else { iv = ui - R; ti = FI; }
+        const int ri = i < hi ? R : RE;
+        if (um - Q > ui) { iv = um - Q - ri; ti = FM; } else { iv = ui - ri; ti = FI; }
       } else {
         iv = NEG_INF;
         ti = FM;
       }
-      // set_D from the left
-      if (lm - Q > ld) { dv = lm - Q - R; td = FM; } else { dv = ld - R; td = FD; }
+      // set_D from the left (set_end_D on the last row)
+      const int rd = j == n2 ? RE : R;
+      if (lm - Q > ld) { dv = lm - Q - rd; td = FM; } else { dv = ld - rd; td = FD; }
       M(cur, i) = (uint32_t)m;
       I(cur, i) = (uint32_t)iv;
       D(cur, i) = (uint32_t)dv;
@@ -195,7 +202,21 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
     const uint8_t *b = A.seq2 + A.off2[p];
     uint32_t *cig = A.cigar + (uint64_t)p * A.cigar_cap;
     int score = -1, path_len = 0, n_cig = 0, s_i = 0, s_j = 0, e_i = 0, e_j = 0;
-    if (n1 > 0 && n2 > 0) {
+    if (A.global_band > 0) {
+      // aln_global_core alone (bwa_refine_gapped, bwase.c:198): whole sequences, one band
+      score = 0;
+      if (n1 > 0 && n2 > 0) {
+        int si = 0, sj = 0;
+        score = global_fill(L, eM, eI, eD, 0, (uint32_t)A.max_len1 + 1, a, n1, b, n2, A.global_band, A.gap_end, cig,
+                            A.cigar_cap, n_cig, path_len, si, sj);
+        for (int k = 0; k < n_cig / 2; ++k) {
+          const uint32_t t = cig[k];
+          cig[k] = cig[n_cig - 1 - k];
+          cig[n_cig - 1 - k] = t;
+        }
+        s_i = si; s_j = sj; e_i = n1; e_j = n2;
+      }
+    } else if (n1 > 0 && n2 > 0) {
       // ---- forward pass (stdaln.c:579-631): row j over seq2, columns i over seq1.
       // Strip-mined: STRIP columns at a time for all rows, the strip's H / E of the row
       // above in registers; between strips only (H[j][i0-1], F) per row goes through
@@ -325,7 +346,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
         int score_g = 0, si = 0, sj = 0;
         for (int bw = BAND;; bw <<= 1) {
           score_g = global_fill(L, eM, eI, eD, 0, (uint32_t)A.max_len1 + 1, a + start_i - 1, n1s, b + start_j - 1, n2s,
-                                bw, cig, A.cigar_cap, n_cig, path_len, si, sj);
+                                bw, -1, cig, A.cigar_cap, n_cig, path_len, si, sj);
           if (score_g == score_r || score_f == score_g) break;
           if (bw > span) break;
         }

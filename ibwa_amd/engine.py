@@ -98,6 +98,8 @@ CAPI = {
     "ibwa_ctx_export_sa": (_i, [_vp, _i, _vp, _u64]),
     "ibwa_sw_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, c.POINTER(c.c_void_p),
                            c.POINTER(_i64)]),
+    "ibwa_global_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, c.POINTER(c.c_void_p),
+                               c.POINTER(_i64)]),
     "ibwa_paired_sw": (_i, [_vp, _i, c.POINTER(c.POINTER(RefSeq)), c.POINTER(PeOpt), c.POINTER(IsizeInfo), _vp,
                             _u64, c.POINTER(_u64), c.POINTER(_u64)]),
     "ibwa_sw_core_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
@@ -271,6 +273,36 @@ class Engine:
         _chk(lib().ibwa_paired_sw(self.h, len(seqs0), arr, c.byref(pe_opt), c.byref(ii), pac.ctypes.data, int(l_pac),
                                   tot, mapped))
         return [mapped[1], tot[1], mapped[0], tot[0]]
+
+    def global_align(self, refs, reads, band=50, gap_end=5):
+        """Batched aln_global_core (stdaln.c:345) with aln_param_bwa scores -> list of
+        (score, path_len, cigar str) per pair."""
+        n = len(refs)
+        o1 = np.zeros(n, np.uint64)
+        o2 = np.zeros(n, np.uint64)
+        l1 = np.array([len(x) for x in refs], np.uint32)
+        l2 = np.array([len(x) for x in reads], np.uint32)
+        if n:
+            o1[1:] = np.cumsum(l1[:-1])
+            o2[1:] = np.cumsum(l2[:-1])
+        s1 = np.concatenate([np.asarray(x, np.uint8) for x in refs] + [np.zeros(1, np.uint8)])
+        s2 = np.concatenate([np.asarray(x, np.uint8) for x in reads] + [np.zeros(1, np.uint8)])
+        score = np.zeros(n, np.int32)
+        plen = np.zeros(n, np.int32)
+        ncig = np.zeros(n, np.int32)
+        ptr = c.c_void_p()
+        tot = c.c_int64()
+        _chk(lib().ibwa_global_batch(self.h, n, s1.ctypes.data, o1.ctypes.data, l1.ctypes.data, s2.ctypes.data,
+                                     o2.ctypes.data, l2.ctypes.data, band, gap_end, score.ctypes.data,
+                                     plen.ctypes.data, ncig.ctypes.data, c.byref(ptr), c.byref(tot)))
+        cig = np.frombuffer(c.string_at(ptr.value, 4 * max(tot.value, 0)), dtype=np.uint32).copy()
+        lib().ibwa_free(ptr)
+        out, q = [], 0
+        for p in range(n):
+            out.append((int(score[p]), int(plen[p]),
+                        "".join(f"{x >> 4}{'MIDS'[x & 0xf]}" for x in cig[q:q + ncig[p]])))
+            q += ncig[p]
+        return out
 
     def sw(self, refs, reads):
         """Batched aln_local_core (stdaln.c:529) over code arrays.  Returns a list of

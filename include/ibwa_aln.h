@@ -204,6 +204,18 @@ int ibwa_ctx_expand_sa(ibwa_ctx_t *ctx);
 int ibwa_sa2pos(ibwa_ctx_t *ctx, int64_t n, const uint8_t *strand, const uint32_t *k, const uint32_t *len,
                 uint64_t offset, uint64_t *pos);
 
+/*
+ * Batched banded global alignment: aln_global_core (stdaln.c:345-525) with aln_param_bwa's
+ * scores (gap open 26, extend 9, aln_sm_maq) and the given band_width / gap_end, as
+ * refine_gapped_core (bwase.c:167-199) calls it with band 50, gap_end 5 for each gapped read.
+ * Pair p aligns seq1 = ref[off1[p] .. +len1[p]) against seq2 = qry[off2[p] .. +len2[p]).
+ * Per pair: score (0 and path_len 0 if a length is 0), path_len, n_cigar; *cigar = malloc'd
+ * concatenation of the CIGARs in aln_path2cigar32 encoding (len << 4 | op: 0 M, 1 I, 2 D).
+ */
+int ibwa_global_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *ref, const uint64_t *off1, const uint32_t *len1,
+                      const uint8_t *qry, const uint64_t *off2, const uint32_t *len2, int band, int gap_end,
+                      int32_t *score, int32_t *path_len, int32_t *n_cigar, uint32_t **cigar, int64_t *n_cigar_total);
+
 /* Device Occ KAT: bwt_occ4 (bwt.c:157) for n positions k[] on strand s -> cnt[4*n] */
 int ibwa_occ4(ibwa_ctx_t *ctx, int strand, int64_t n, const uint32_t *k, uint32_t *cnt);
 

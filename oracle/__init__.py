@@ -607,3 +607,35 @@ def psw_row(e):
     return (e["type"], e["strand"], e["pos"], e.get("remapped_pos", e["pos"]), e.get("dbidx", 0),
             e.get("remapped_dbidx", 0), e["mapQ"], e["seQ"], e["n_mm"], e["n_gapo"], e["n_gape"], e["extra_flag"],
             len(cg), cs)
+
+
+def global_core(ref_codes, read_codes, band=50, gap_end=5):
+    """aln_global_core (stdaln.c:345-525) restated, aln_param_bwa scores, + path -> CIGAR.
+    Returns (score, path_len, cigar str) -- the fields of tests/golden/gsw_vectors.tsv."""
+    L = lib()
+    if not hasattr(L.or_aln_global_core, "_typed"):
+        L.or_aln_global_core.restype = ctypes.c_int
+        L.or_aln_global_core.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.or_aln_global_core._typed = True
+    a = np.ascontiguousarray(ref_codes, dtype=np.uint8)
+    b = np.ascontiguousarray(read_codes, dtype=np.uint8)
+    path = (PathT * (a.size + b.size + 2))()
+    pl = ctypes.c_int(0)
+    sc = L.or_aln_global_core(a.ctypes.data, a.size, b.ctypes.data, b.size, band, gap_end, path, ctypes.byref(pl))
+    if pl.value <= 0:
+        return sc, pl.value, ""
+    cig = (ctypes.c_uint32 * (pl.value + 1))()
+    n = L.or_path2cigar32(path, pl.value, cig)
+    return sc, pl.value, "".join(f"{cig[k] >> 4}{'MIDS'[cig[k] & 0xf]}" for k in range(n))
+
+
+def read_gsw_vectors(path):
+    """tests/golden/gsw_vectors.tsv -> list of (ref, read, score, path_len, cigar)"""
+    out = []
+    for line in open(path):
+        if line.startswith("#"):
+            continue
+        f = line.rstrip("\n").split("\t")
+        out.append((f[0], f[1], int(f[2]), int(f[3]), f[4] if len(f) > 4 else ""))
+    return out

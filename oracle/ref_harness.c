@@ -15,6 +15,8 @@
  *   ibwa_ref swf <pairs.tsv>               -> aln_local_core over a file of pairs
  *   ibwa_ref sa <prefix> <rows.tsv>        -> bwt_sa (bwt.c:69) over bwt_restore_sa (bwtio.c:29)
  *   ibwa_ref samse|sampe ...               -> bwa_sai2sam_se / bwa_sai2sam_pe (bwase.c:710, bwape.c)
+ *   ibwa_ref gswf <pairs.tsv>              -> aln_global_core (stdaln.c:345) + bwa_aln_path2cigar
+ *                                             with aln_param_bwa, as refine_gapped_core calls it
  *   ibwa_ref psw <prefix> <pairs.tsv> <type> <avg> <std> <ap_prior>
  *                                          -> bwa_paired_sw (bwasw.c:270) on pairs read from a file
  */
@@ -147,6 +149,42 @@ static int cmd_sa(int argc, char *argv[])
 	return 0;
 }
 
+/* gswf <pairs.tsv> : one "ref<TAB>read" per line; prints score, path_len and the CIGAR of
+ * aln_global_core(ref, read, &aln_param_bwa) as refine_gapped_core (bwase.c:196-198) runs it */
+static int cmd_gswf(int argc, char *argv[])
+{
+	static char line[1 << 16];
+	FILE *fp;
+	AlnParam ap = aln_param_bwa;
+	if (argc < 2 || !(fp = fopen(argv[1], "r"))) return 1;
+	while (fgets(line, sizeof line, fp)) {
+		char *t = strchr(line, '\t'), *r2;
+		int l1, l2, i, path_len = 0, score, n_cigar = 0;
+		unsigned char *s1, *s2;
+		path_t *path;
+		bwa_cigar_t *cigar;
+		if (!t) continue;
+		*t = 0; r2 = t + 1;
+		r2[strcspn(r2, "\r\n")] = 0;
+		l1 = strlen(line); l2 = strlen(r2);
+		s1 = (unsigned char*)malloc(l1 + 1); s2 = (unsigned char*)malloc(l2 + 1);
+		for (i = 0; i < l1; ++i) s1[i] = nst_nt4_table[(int)line[i]];
+		for (i = 0; i < l2; ++i) s2[i] = nst_nt4_table[(int)r2[i]];
+		path = (path_t*)calloc(l1 + l2 + 2, sizeof(path_t));
+		score = aln_global_core(s1, l1, s2, l2, &ap, path, &path_len);
+		printf("%d\t%d\t", score, path_len);
+		if (path_len > 0) {
+			cigar = bwa_aln_path2cigar(path, path_len, &n_cigar);
+			for (i = 0; i < n_cigar; ++i) printf("%u%c", __cigar_len(cigar[i]), "MIDS"[__cigar_op(cigar[i])]);
+			free(cigar);
+		}
+		printf("\n");
+		free(path); free(s1); free(s2);
+	}
+	fclose(fp);
+	return 0;
+}
+
 /* psw: bwa_paired_sw (bwasw.c:270-304) over mate pairs described one per line as
  *   <end 0 fields> <TAB> <end 1 fields>, each end = read(ACGTN) strand type mapQ seQ extra_flag
  *   n_mm n_gapo n_gape pos   (space separated)
@@ -240,6 +278,7 @@ int main(int argc, char *argv[])
 	if (strcmp(argv[1], "sw") == 0) return cmd_sw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "swf") == 0) return cmd_swf(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
+	if (strcmp(argv[1], "gswf") == 0) return cmd_gswf(argc - 1, argv + 1);
 	if (strcmp(argv[1], "psw") == 0) return cmd_psw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "samse") == 0) return bwa_sai2sam_se(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sampe") == 0) return bwa_sai2sam_pe(argc - 1, argv + 1);

@@ -88,3 +88,13 @@ def test_paired_sw_restatement_matches_reference(golden_dir, name):
     bad = [(i, k) for i, (p, q) in enumerate(zip(pin, pout)) for k in (0, 1)
            if oracle.psw_row(p[k]) != tuple(q[k][f] for f in oracle.PSW_OUT)]
     assert not bad, bad[:5]
+
+
+def test_global_core_restatement_matches_reference_vectors(golden_dir):
+    """aln_global_core with aln_param_bwa (band 50, gap_end 5; refine_gapped_core) restated ==
+    the reference on 3 006 pairs (tools/make_gsw_golden.py)."""
+    vecs = oracle.read_gsw_vectors(os.path.join(golden_dir, "gsw_vectors.tsv"))
+    assert len(vecs) > 3000
+    bad = [k for k, (a, b, sc, pl, cg) in enumerate(vecs)
+           if oracle.global_core(oracle.nt4(a), oracle.nt4(b)) != (sc, pl, cg)]
+    assert not bad, bad[:5]

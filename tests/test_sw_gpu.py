@@ -91,3 +91,25 @@ def test_sw_core_batch_vs_oracle(gpu_engine):
     bad = [(k, a, b) for k, (a, b) in enumerate(zip(got, exp)) if a != b]
     assert not bad, bad[:5]
     assert sum(e is not None for e in exp) > 500
+
+
+def test_global_golden_vectors(golden_dir, gpu_engine):
+    """Batched aln_global_core (bwa_refine_gapped's band 50, gap_end 5) == the reference."""
+    vecs = oracle.read_gsw_vectors(os.path.join(golden_dir, "gsw_vectors.tsv"))
+    got = gpu_engine.global_align([oracle.nt4(v[0]) for v in vecs], [oracle.nt4(v[1]) for v in vecs], 50, 5)
+    bad = [(k, g, v[2:]) for k, (g, v) in enumerate(zip(got, vecs)) if g != tuple(v[2:])]
+    assert not bad, bad[:3]
+
+
+def test_global_gap_end_negative_vs_oracle(gpu_engine):
+    """gap_end < 0 (the local core's path fill) and other bands on random shapes vs the restatement."""
+    rng = np.random.default_rng(3)
+    refs, reads = [], []
+    for _ in range(400):
+        n1, n2 = int(rng.integers(1, 160)), int(rng.integers(1, 160))
+        refs.append(rng.integers(0, 5, n1).astype(np.uint8))
+        reads.append(rng.integers(0, 5, n2).astype(np.uint8))
+    for band, ge in ((50, -1), (5, 5), (20, -1)):
+        got = gpu_engine.global_align(refs, reads, band, ge)
+        exp = [oracle.global_core(a, b, band, ge) for a, b in zip(refs, reads)]
+        assert got == exp, (band, ge, [k for k in range(len(got)) if got[k] != exp[k]][:5])
