@@ -24,8 +24,12 @@
 #include <vector>
 
 #include "ibwa_aln.h"
+#include "readers.h"
 
 namespace {
+
+using ibwa_cli::BamReader;
+using ibwa_cli::SeqReader;
 
 const int kBatch = 0x40000;  // bwtaln.c:193
 const int kMinRdLen = 35;    // BWA_MIN_RDLEN, bwtaln.h:23
@@ -40,133 +44,6 @@ void init_nt4() {  // nst_nt4_table (bntseq.c:39-56)
   nt4[(int)'T'] = nt4[(int)'t'] = 3;
   nt4[(int)'-'] = 5;
 }
-
-// Buffered gz reader with the record semantics of kseq_read (kseq.h:156-195).
-struct SeqReader {
-  gzFile fp = nullptr;
-  std::vector<char> buf = std::vector<char>(1 << 20);
-  int begin = 0, end = 0;
-  bool eof = false;
-  int last_char = 0;
-  std::string name, seq, qual;
-
-  bool open(const char *fn) {
-    fp = strcmp(fn, "-") ? gzopen(fn, "r") : gzdopen(fileno(stdin), "r");
-    if (fp) gzbuffer(fp, 1 << 20);
-    return fp != nullptr;
-  }
-  ~SeqReader() {
-    if (fp) gzclose(fp);
-  }
-  int getc_() {
-    if (begin >= end) {
-      if (eof) return -1;
-      end = gzread(fp, buf.data(), (unsigned)buf.size());
-      begin = 0;
-      if (end <= 0) { eof = true; end = 0; return -1; }
-    }
-    return (unsigned char)buf[begin++];
-  }
-  // returns seq length, -1 at EOF, -2 on a truncated quality string
-  int read() {
-    int c;
-    if (last_char == 0) {
-      while ((c = getc_()) != -1 && c != '>' && c != '@') {}
-      if (c == -1) return -1;
-      last_char = c;
-    }
-    name.clear(); seq.clear(); qual.clear();
-    bool got = false;
-    while ((c = getc_()) != -1 && !isspace(c)) { name.push_back((char)c); got = true; }
-    if (c == -1 && !got) return -1;
-    if (c != '\n') while ((c = getc_()) != -1 && c != '\n') {}  // comment
-    while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@')
-      if (isgraph(c)) seq.push_back((char)c);
-    if (c == '>' || c == '@') last_char = c;
-    if (c != '+') return (int)seq.size();
-    while ((c = getc_()) != -1 && c != '\n') {}
-    if (c == -1) return -2;
-    while ((c = getc_()) != -1 && qual.size() < seq.size())
-      if (c >= 33 && c <= 127) qual.push_back((char)c);
-    last_char = 0;
-    if (seq.size() != qual.size()) return -2;
-    return (int)seq.size();
-  }
-};
-
-// BAM input: bam_header_read / bam_read1 (bamlite.c:34-116) over gzread (a BGZF file is a
-// series of gzip members), and the record selection and decoding of bwa_read_bam
-// (bwaseqio.c:89-143): `which` bit 1 = read 1, 2 = read 2, 4 = neither (bwtaln.c:159-171);
-// 4-bit bases -> A/C/G/T/N, reverse-strand records reverse-complemented back, qualities
-// +33 capped at 126.  The record is handed on as FASTQ-like strings.
-struct BamReader {
-  gzFile fp = nullptr;
-  int which = 7;
-  std::string name, seq, qual;
-  std::vector<uint8_t> data;
-  bool readn(void *p, int n) { return gzread(fp, p, (unsigned)n) == n; }
-  bool open(const char *fn, int w) {
-    which = w;
-    fp = strcmp(fn, "-") ? gzopen(fn, "r") : gzdopen(fileno(stdin), "r");
-    if (!fp) return false;
-    gzbuffer(fp, 1 << 20);
-    char magic[4];
-    if (!readn(magic, 4) || memcmp(magic, "BAM\1", 4) != 0) {
-      fprintf(stderr, "[bam_header_read] invalid BAM binary header (this is not a BAM file).\n");
-      return false;
-    }
-    int32_t l_text = 0, n_ref = 0;
-    if (!readn(&l_text, 4)) return false;
-    std::vector<char> text(l_text > 0 ? l_text : 0);
-    if (l_text > 0 && !readn(text.data(), l_text)) return false;
-    if (!readn(&n_ref, 4)) return false;
-    for (int32_t i = 0; i < n_ref; ++i) {
-      int32_t l_name = 0;
-      uint32_t l_ref = 0;
-      if (!readn(&l_name, 4) || l_name < 0) return false;
-      std::vector<char> nm(l_name);
-      if ((l_name && !readn(nm.data(), l_name)) || !readn(&l_ref, 4)) return false;
-    }
-    return true;
-  }
-  ~BamReader() {
-    if (fp) gzclose(fp);
-  }
-  // seq length of the next selected record, -1 at EOF, -2 on a truncated record
-  int read() {
-    static const char nt16[] = "NACNGNNNTNNNNNNN";  // bam_nt16_nt4_table (bwaseqio.c:11) as bases
-    for (;;) {
-      int32_t block_len = 0;
-      const int got = gzread(fp, &block_len, 4);
-      if (got == 0) return -1;
-      if (got != 4 || block_len < 32) return -2;
-      uint32_t x[8];
-      if (!readn(x, 32)) return -2;
-      const int l_qname = x[2] & 0xff, flag = x[3] >> 16, n_cigar = x[3] & 0xffff, l_qseq = (int)x[4];
-      data.resize(block_len - 32);
-      if (!data.empty() && !readn(data.data(), (int)data.size())) return -2;
-      int go = 0;
-      if ((which & 1) && (flag & 0x40)) go = 1;
-      if ((which & 2) && (flag & 0x80)) go = 1;
-      if ((which & 4) && !(flag & 0x40) && !(flag & 0x80)) go = 1;
-      if (!go) continue;
-      const uint8_t *sq = data.data() + l_qname + 4 * n_cigar, *q = sq + (l_qseq + 1) / 2;
-      name.assign((const char *)data.data());
-      seq.resize(l_qseq);
-      qual.resize(l_qseq);
-      for (int i = 0; i < l_qseq; ++i) {
-        seq[i] = nt16[(sq[i >> 1] >> ((~i & 1) << 2)) & 0xf];
-        qual[i] = (char)(q[i] + 33 < 126 ? q[i] + 33 : 126);
-      }
-      if (flag & 0x10) {  // seq_reverse(len, seq, 1) / seq_reverse(len, qual, 0)
-        std::reverse(seq.begin(), seq.end());
-        std::reverse(qual.begin(), qual.end());
-        for (auto &ch : seq) ch = ch == 'A' ? 'T' : ch == 'C' ? 'G' : ch == 'G' ? 'C' : ch == 'T' ? 'A' : ch;
-      }
-      return l_qseq;
-    }
-  }
-};
 
 struct Batch {
   std::vector<uint8_t> seq;
@@ -252,9 +129,13 @@ int die(const char *what) {
 template <class Reader>
 int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out, int n_gpus);
 
+int samse_main(int argc, char *argv[]);  // samse_main.cpp
+
 int main(int argc, char *argv[]) {
+  if (argc >= 2 && strcmp(argv[1], "samse") == 0) return samse_main(argc - 1, argv + 1);
   if (argc < 2 || strcmp(argv[1], "aln") != 0) {
-    fprintf(stderr, "Usage: ibwa-amd aln [options] <prefix> <in.fq>\n");
+    fprintf(stderr, "Usage: ibwa-amd aln [options] <prefix> <in.fq>\n"
+                    "       ibwa-amd samse [-n max_occ] [-f out.sam] [-r RG] <prefix> <in.sai> <in.fq>\n");
     return 1;
   }
   --argc; ++argv;
