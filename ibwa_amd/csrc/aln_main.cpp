@@ -130,12 +130,15 @@ template <class Reader>
 int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out, int n_gpus);
 
 int samse_main(int argc, char *argv[]);  // samse_main.cpp
+int sampe_main(int argc, char *argv[]);  // sampe_main.cpp
 
 int main(int argc, char *argv[]) {
   if (argc >= 2 && strcmp(argv[1], "samse") == 0) return samse_main(argc - 1, argv + 1);
+  if (argc >= 2 && strcmp(argv[1], "sampe") == 0) return sampe_main(argc - 1, argv + 1);
   if (argc < 2 || strcmp(argv[1], "aln") != 0) {
     fprintf(stderr, "Usage: ibwa-amd aln [options] <prefix> <in.fq>\n"
-                    "       ibwa-amd samse [-n max_occ] [-f out.sam] [-r RG] <prefix> <in.sai> <in.fq>\n");
+                    "       ibwa-amd samse [-n max_occ] [-f out.sam] [-r RG] <prefix> <in.sai> <in.fq>\n"
+                    "       ibwa-amd sampe [options] <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq>\n");
     return 1;
   }
   --argc; ++argv;

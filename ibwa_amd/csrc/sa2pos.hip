@@ -4,7 +4,8 @@
 // call it once per reported hit.
 //
 //   strand 1: pos = offset + bwt_sa(bwt[0], k)
-//   strand 0: pos = offset + (u32)(bwt[1].seq_len - (u32)(bwt_sa(bwt[1], k) + len))
+//   strand 0: pos = offset + bwt[1].seq_len - (u32)(bwt_sa(bwt[1], k) + len)   (u64: wraps past 2^64
+//             when the hit hangs off the end, as the reference's uint64_t expression does)
 //
 // bwt_sa walks the LF mapping bwt_invPsi (bwt.h:66-70) until the row is a
 // multiple of the SA sampling interval and adds the walk length to the sampled
@@ -45,8 +46,8 @@ __device__ __forceinline__ uint32_t inv_psi(const IndexView &ix, uint32_t k) {
 }
 
 __device__ __forceinline__ uint64_t to_pos(const SaArgs &a, uint32_t strand, uint32_t sa, uint32_t len) {
-  // dbset.c:241-245, bwtint_t (u32) arithmetic then + offset (u64)
-  return a.offset + (strand ? (uint64_t)sa : (uint64_t)(uint32_t)(a.ix[1].seq_len - (uint32_t)(sa + len)));
+  // dbset.c:241-245: (u64 offset + u32 seq_len) - u32 (sa + len), evaluated in u64
+  return strand ? a.offset + sa : a.offset + a.ix[1].seq_len - (uint32_t)(sa + len);
 }
 
 __global__ void __launch_bounds__(256) k_sa2pos_full(SaArgs a) {

@@ -1,0 +1,877 @@
+// sampe_main.cpp -- `ibwa-amd sampe [options] <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq>`: the
+// reference's sampe (bwa_sai2sam_pe_core, bwape.c:436-540) for one reference database, with its
+// compute steps on the GPU:
+//   * SA -> coordinate (bwtdb_sa2seq, dbset.c:240-246) of every primary hit and of every row of
+//     every SA interval both ends have (compute_seq_coords_and_counts, filter_alignments.cpp:53-140):
+//     one ibwa_sa2pos launch per batch for each of the two passes;
+//   * the mate rescue (bwa_paired_sw, bwasw.c:270-304): ibwa_paired_sw, one local-SW launch;
+//   * bwa_refine_gapped's banded global alignments (bwase.c:333-416): one launch for both ends.
+// The host runs the reference's logic in its order and with its quirks: select_sai_ibwa's hit
+// choice (bwape.c:281-358) on the POSIX drand48 stream seeded from .ann, infer_isize (bwape.c:91-198,
+// including the std accumulator that starts at -1), the per-pair position array sorted by klib's
+// introsort (not stable, so its exact algorithm is restated), find_optimal_pair (bwapair.c:166-279)
+// with its look-ahead one element past the array, select_sai_multi (saiset.c:124-163), and the
+// (k,l)-keyed position cache of bwtcache.c for intervals of >= 1000 rows, whose key ignores the
+// strand and the read length.
+//
+// Remapping (-R): without .remap files every hit remaps to itself (bwaremap's status 1), which is
+// what this build supports; a prefix with a .remap file, or more than one database, is rejected.
+// Without -R the reference's select_sai_ibwa never sees a successful remap status and leaves every
+// read unmapped ("Failed to select primary alignment"); that is reproduced.
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ibwa_bwa_compat.h"
+#include "sam_common.h"
+
+using namespace ibwa_sam;
+
+namespace {
+
+constexpr uint32_t kMinHashWidth = 1000;  // MIN_HASH_WIDTH (bwape.c:46, filter_alignments.cpp:10)
+
+struct PeOpt {  // pe_opt_t defaults (bwa_init_pe_opt, bwape.c:68-84)
+  int max_isize = 500, force_isize = 0, max_occ = 100000, n_multi = 3, N_multi = 10, type = IBWA_PET_STD;
+  int is_sw = 1, is_preload = 0, remapping = 0, n_threads = 1;
+  double ap_prior = 1e-5;
+};
+
+struct Isize {  // isize_info_t (bwapair.h:8-11)
+  double avg = -1.0, std = -1.0, ap_prior = 0.0;
+  uint32_t low = 0, high = 0, high_bayesian = 0;
+};
+
+int die(const char *what) {
+  fprintf(stderr, "[ibwa-amd sampe] %s: %s\n", what, ibwa_last_error());
+  return 1;
+}
+
+// ---------------------------------------------------------------- klib ks_introsort (ksort.h:142-219)
+// Restated because the order of equal keys (not stable) decides which position find_optimal_pair
+// sees first.
+template <class T, class Lt>
+void ks_insertsort(T *s, T *t, Lt lt) {
+  for (T *i = s + 1; i < t; ++i)
+    for (T *j = i; j > s && lt(*j, *(j - 1)); --j) std::swap(*j, *(j - 1));
+}
+template <class T, class Lt>
+void ks_combsort(size_t n, T *a, Lt lt) {
+  const double shrink = 1.2473309501039786540366528676643;
+  bool do_swap;
+  size_t gap = n;
+  do {
+    if (gap > 2) {
+      gap = (size_t)(gap / shrink);
+      if (gap == 9 || gap == 10) gap = 11;
+    }
+    do_swap = false;
+    for (T *i = a; i < a + n - gap; ++i) {
+      T *j = i + gap;
+      if (lt(*j, *i)) {
+        std::swap(*i, *j);
+        do_swap = true;
+      }
+    }
+  } while (do_swap || gap > 2);
+  if (gap != 1) ks_insertsort(a, a + n, lt);
+}
+template <class T, class Lt>
+void ks_introsort(size_t n, T *a, Lt lt) {
+  struct Frame {
+    T *left, *right;
+    int depth;
+  };
+  if (n < 1) return;
+  if (n == 2) {
+    if (lt(a[1], a[0])) std::swap(a[0], a[1]);
+    return;
+  }
+  int d;
+  for (d = 2; 1ul << d < n; ++d) {}
+  std::vector<Frame> stack;
+  T *s = a, *t = a + (n - 1);
+  d <<= 1;
+  for (;;) {
+    if (s < t) {
+      if (--d == 0) {
+        ks_combsort((size_t)(t - s + 1), s, lt);
+        t = s;
+        continue;
+      }
+      T *i = s, *j = t, *k = i + ((j - i) >> 1) + 1;
+      if (lt(*k, *i)) {
+        if (lt(*k, *j)) k = j;
+      } else {
+        k = lt(*j, *i) ? i : j;
+      }
+      const T rp = *k;
+      if (k != t) std::swap(*k, *t);
+      for (;;) {
+        do ++i; while (lt(*i, rp));
+        do --j; while (i <= j && lt(rp, *j));
+        if (j <= i) break;
+        std::swap(*i, *j);
+      }
+      std::swap(*i, *t);
+      if (i - s > t - i) {
+        if (i - s > 16) stack.push_back({s, i - 1, d});
+        s = t - i > 16 ? i + 1 : t;
+      } else {
+        if (t - i > 16) stack.push_back({i + 1, t, d});
+        t = i - s > 16 ? i - 1 : s;
+      }
+    } else {
+      if (stack.empty()) {
+        ks_insertsort(a, a + n, lt);
+        return;
+      }
+      s = stack.back().left;
+      t = stack.back().right;
+      d = stack.back().depth;
+      stack.pop_back();
+    }
+  }
+}
+
+// ---------------------------------------------------------------- pairing (bwapair.c)
+struct Position {  // position_t (bwapair.h:13-24): single database, hits remap to themselves
+  uint64_t pos = 0, remapped_pos = 0;
+  uint32_t idx_and_end = 0;
+};
+inline bool position_lt(const Position &a, const Position &b) {  // bwapair.c:22-28
+  if (a.remapped_pos == b.remapped_pos) return a.pos < b.pos;
+  return a.remapped_pos < b.remapped_pos;
+}
+
+// kvec-style position array reused for every pair of a batch (bwape.c:244, filter_alignments.cpp:62):
+// find_optimal_pair's look-ahead (bwapair.c:204) reads the slot past the last position, which
+// holds whatever an earlier pair left there.
+struct PosArr {
+  std::vector<Position> a;  // capacity slots; a.size() == kvec m
+  size_t n = 0;
+  void clear() { n = 0; }
+  void push(const Position &p) {
+    if (n == a.size()) a.resize(a.empty() ? 2 : a.size() << 1);  // kv_push growth
+    a[n++] = p;
+  }
+  const Position &at(size_t i) const {
+    static const Position zero;
+    return i < a.size() ? a[i] : zero;
+  }
+};
+
+inline uint64_t hash_64(uint64_t key) {  // bwapair.c:31-41
+  key += ~(key << 32);
+  key ^= (key >> 22);
+  key += ~(key << 13);
+  key ^= (key >> 8);
+  key += (key << 3);
+  key ^= (key >> 15);
+  key += ~(key << 27);
+  key ^= (key >> 31);
+  return key;
+}
+
+struct PairCtx {
+  Read *p[2];
+  const std::vector<ibwa_aln1_t> *aln[2];
+  const PeOpt *opt;
+  const Isize *ii;
+  int s_mm;
+  const ibwa_aln1_t &al(const Position &x) const { return (*aln[x.idx_and_end & 1])[x.idx_and_end >> 1]; }
+};
+
+struct Pint {  // pairing_internals_t (bwapair.c:8-17)
+  int o_n = 0, subo_n = 0, cnt_chg = 0, max_len = 0;
+  Position last_pos[2][2];
+  Position o_pos[2];
+  uint64_t subo_score = ~0ull, o_score = ~0ull;
+};
+
+// pairing_aux (bwapair.c:92-140)
+void pairing_aux(const PairCtx &c, Pint &pi, const Position &u, const Position &v, int n_optimal) {
+  const uint32_t l = (uint32_t)(v.remapped_pos + (uint64_t)c.p[v.idx_and_end & 1]->len - u.remapped_pos);
+  if (u.remapped_pos != ~0ull && v.remapped_pos > u.remapped_pos && l >= (uint32_t)pi.max_len &&
+      ((c.ii->high && l <= c.ii->high_bayesian) || (c.ii->high == 0 && l <= (uint32_t)c.opt->max_isize))) {
+    uint64_t s = (uint64_t)(int64_t)(c.al(v).score + c.al(u).score);
+    s *= 10;
+    if (c.ii->high) s += (int)(-4.343 * log(.5 * erfc(M_SQRT1_2 * fabs(l - c.ii->avg) / c.ii->std)) + .499);
+    s = s << 32 | (uint32_t)hash_64(u.remapped_pos << 32 | v.remapped_pos);
+    if (s >> 32 == pi.o_score >> 32) {
+      pi.o_n += n_optimal;
+    } else if (s >> 32 < pi.o_score >> 32) {
+      pi.subo_n += pi.o_n;
+      pi.o_n = n_optimal;
+    } else {
+      ++pi.subo_n;
+    }
+    if (s < pi.o_score) {
+      pi.subo_score = pi.o_score;
+      pi.o_score = s;
+      pi.o_pos[u.idx_and_end & 1] = u;
+      pi.o_pos[v.idx_and_end & 1] = v;
+    } else if (s < pi.subo_score) {
+      pi.subo_score = s;
+    }
+  }
+}
+
+// pairing_aux2 (bwapair.c:142-158)
+void pairing_aux2(const PairCtx &c, Pint &pi, Read &r, const Position &pos) {
+  const ibwa_aln1_t &a = c.al(pos);
+  r.extra_flag |= SAM_FPP;
+  if (r.pos != pos.pos || r.strand != (int)a.a) {
+    r.n_mm = a.n_mm; r.n_gapo = a.n_gapo; r.n_gape = a.n_gape; r.strand = a.a;
+    r.score = a.score;
+    r.pos = pos.pos;
+    r.remapped_pos = pos.remapped_pos;
+    if (r.mapQ > 0) ++pi.cnt_chg;
+  }
+}
+
+// find_optimal_pair (bwapair.c:166-279), BWA_PET_STD
+int find_optimal_pair(const PairCtx &c, PosArr &arr) {
+  Read **p = (Read **)c.p;
+  Pint pi;
+  pi.max_len = std::max(p[0]->full_len, p[1]->full_len);
+  ks_introsort(arr.n, arr.a.data(), position_lt);
+  for (int j = 0; j < 2; ++j)
+    for (int t = 0; t < 2; ++t) pi.last_pos[j][t].pos = pi.last_pos[j][t].remapped_pos = ~0ull;
+  // mappings_overlap (bwapair.c:43-62)
+  auto overlap = [](const Position &a, const Position &b) {
+    if (a.pos == ~0ull || b.pos == ~0ull) return false;
+    return a.remapped_pos == b.remapped_pos && (a.idx_and_end & 1) == (b.idx_and_end & 1);
+  };
+  size_t i = 0;
+  while (i < arr.n) {
+    Position pos = arr.a[i];
+    const int strand = c.al(arr.a[i]).a;
+    const int n_optimal = 1;
+    if (i < arr.n - 1) {
+      size_t k = i;
+      while (overlap(pos, arr.at(k + 1))) ++k;
+      if (k > i) {  // select_mapping (bwapair.c:64-90): the first of the lowest score
+        size_t best = i;
+        for (size_t t = i + 1; t <= k; ++t)
+          if (c.al(arr.at(t)).score < c.al(arr.at(best)).score) best = t;
+        pos = arr.at(best);
+        i = k;
+      }
+    }
+    const int e = pos.idx_and_end & 1;
+    if (strand == 1) {
+      pairing_aux(c, pi, pi.last_pos[1 - e][1], pos, n_optimal);
+      pairing_aux(c, pi, pi.last_pos[1 - e][0], pos, n_optimal);
+    } else {
+      pi.last_pos[e][0] = pi.last_pos[e][1];
+      pi.last_pos[e][1] = pos;
+    }
+    ++i;
+  }
+  if (pi.o_score != ~0ull) {
+    int mapQ_p = 0;  // the maximum mapping quality when one end is moved
+    if (pi.o_n == 1) {
+      if (pi.subo_score == ~0ull) {
+        mapQ_p = 29;
+      } else if ((pi.subo_score >> 32) - (pi.o_score >> 32) > (uint64_t)(int64_t)(c.s_mm * 10)) {
+        mapQ_p = 23;
+      } else {
+        const int n = pi.subo_n > 255 ? 255 : pi.subo_n;
+        mapQ_p = (int)(((pi.subo_score >> 32) - (pi.o_score >> 32)) / 2 - (uint64_t)(int64_t)g_log_n[n]);
+        if (mapQ_p < 0) mapQ_p = 0;
+      }
+    }
+    const int rr0 = c.al(pi.o_pos[0]).a, rr1 = c.al(pi.o_pos[1]).a;
+    const bool keep0 = p[0]->remapped_pos == pi.o_pos[0].remapped_pos && p[0]->strand == rr0;
+    const bool keep1 = p[1]->remapped_pos == pi.o_pos[1].remapped_pos && p[1]->strand == rr1;
+    if (keep0 && keep1) {
+      if (p[0]->mapQ > 0 && p[1]->mapQ > 0) {
+        int mapQ = p[0]->mapQ + p[1]->mapQ;
+        if (mapQ > 60) mapQ = 60;
+        p[0]->mapQ = p[1]->mapQ = mapQ;
+      } else {
+        if (p[0]->mapQ == 0) p[0]->mapQ = (mapQ_p + 7 < p[1]->mapQ) ? mapQ_p + 7 : p[1]->mapQ;
+        if (p[1]->mapQ == 0) p[1]->mapQ = (mapQ_p + 7 < p[0]->mapQ) ? mapQ_p + 7 : p[0]->mapQ;
+      }
+    } else if (keep0) {
+      p[1]->seQ = 0;
+      p[1]->mapQ = p[0]->mapQ;
+      if (p[1]->mapQ > mapQ_p) p[1]->mapQ = mapQ_p;
+    } else if (keep1) {
+      p[0]->seQ = 0;
+      p[0]->mapQ = p[1]->mapQ;
+      if (p[0]->mapQ > mapQ_p) p[0]->mapQ = mapQ_p;
+    } else {
+      p[0]->seQ = p[1]->seQ = 0;
+      mapQ_p -= 20;
+      if (mapQ_p < 0) mapQ_p = 0;
+      p[0]->mapQ = p[1]->mapQ = mapQ_p;
+    }
+    p[0]->mapQ &= 0xff;
+    p[1]->mapQ &= 0xff;
+    pairing_aux2(c, pi, *p[0], pi.o_pos[0]);
+    pairing_aux2(c, pi, *p[1], pi.o_pos[1]);
+  }
+  return pi.cnt_chg;
+}
+
+// ---------------------------------------------------------------- insert size (infer_isize, bwape.c:91-198)
+int infer_isize(const std::vector<Read> &s0, const std::vector<Read> &s1, Isize &ii, double ap_prior, int64_t L) {
+  const int n_seqs = (int)s0.size();
+  ii = Isize();
+  ii.avg = ii.std = -1.0;
+  std::vector<uint64_t> isizes;
+  int max_len = 1;
+  int n_rej = 0;
+  for (int i = 0; i < n_seqs; ++i) {
+    const Read *p[2] = {&s0[i], &s1[i]};
+    const uint64_t x = p[0]->pos < p[1]->pos ? p[1]->pos + p[1]->len - p[0]->pos : p[0]->pos + p[0]->len - p[1]->pos;
+    if (p[0]->mapQ >= 20 && p[1]->mapQ >= 20 && x < 100000) isizes.push_back(x);
+    else ++n_rej;
+    max_len = std::max(max_len, std::max(p[0]->len, p[1]->len));
+  }
+  fprintf(stderr, "[infer_isize]  total rejected pairs: %d\n", n_rej);
+  const int tot = (int)isizes.size();
+  if (tot < 20) {
+    fprintf(stderr, "[infer_isize] fail to infer insert size: too few good pairs\n");
+    return -1;
+  }
+  std::sort(isizes.begin(), isizes.end());
+  const int p25 = (int)isizes[(int)(tot * 0.25 + 0.5)];
+  const int p50 = (int)isizes[(int)(tot * 0.50 + 0.5)];
+  const int p75 = (int)isizes[(int)(tot * 0.75 + 0.5)];
+  const int tmp = (int)(p25 - 2.0 * (p75 - p25) + .499);  // OUTLIER_BOUND
+  ii.low = (uint32_t)(tmp > max_len ? tmp : max_len);
+  ii.high = (uint32_t)(int)(p75 + 2.0 * (p75 - p25) + .499);
+  uint64_t x = 0;
+  int n = 0;
+  for (int i = 0; i < tot; ++i)
+    if (isizes[i] >= ii.low && isizes[i] <= ii.high) ++n, x += isizes[i];
+  ii.avg = (double)x / n;
+  for (int i = 0; i < tot; ++i)
+    if (isizes[i] >= ii.low && isizes[i] <= ii.high) ii.std += (isizes[i] - ii.avg) * (isizes[i] - ii.avg);
+  ii.std = sqrt(ii.std / n);
+  double y;
+  for (y = 1.0; y < 10.0; y += 0.01)
+    if (.5 * erfc(y / M_SQRT2) < ap_prior / L * (y * ii.std + ii.avg)) break;
+  ii.high_bayesian = (uint32_t)(y * ii.std + ii.avg + .499);
+  uint64_t n_ap = 0;
+  for (int i = 0; i < tot; ++i)
+    if (isizes[i] > ii.high_bayesian) ++n_ap;
+  ii.ap_prior = .01 * (n_ap + .01) / tot;
+  if (ii.ap_prior < ap_prior) ii.ap_prior = ap_prior;
+  fprintf(stderr, "[infer_isize] (25, 50, 75) percentile: (%d, %d, %d)\n", p25, p50, p75);
+  if (std::isnan(ii.std) || p75 > 100000) {
+    ii.low = ii.high = ii.high_bayesian = 0;
+    ii.avg = ii.std = -1.0;
+    fprintf(stderr, "[infer_isize] fail to infer insert size: weird pairing\n");
+    return -1;
+  }
+  for (y = 1.0; y < 10.0; y += 0.01)
+    if (.5 * erfc(y / M_SQRT2) < ap_prior / L * (y * ii.std + ii.avg)) break;
+  ii.high_bayesian = (uint32_t)(y * ii.std + ii.avg + .499);
+  fprintf(stderr, "[infer_isize] inferred external isize from %d pairs: %.3lf +/- %.3lf\n", n, ii.avg, ii.std);
+  fprintf(stderr, "[infer_isize] inferred maximum insert size: %u (%.2lf sigma)\n", ii.high_bayesian, y);
+  return 0;
+}
+
+// ---------------------------------------------------------------- read sources (bwa_open_reads, bwtaln.c:159-171)
+struct Source {
+  std::unique_ptr<ibwa_cli::SeqReader> fq;
+  std::unique_ptr<ibwa_cli::BamReader> bam;
+  int mode = 0, trim_qual = 0;
+  bool open(const char *fn, const ibwa_gap_opt_t &opt) {
+    mode = opt.mode;
+    trim_qual = opt.trim_qual;
+    if (mode & IBWA_MODE_BAM) {
+      int which = 0;
+      if (mode & IBWA_MODE_BAM_SE) which |= 4;
+      if (mode & IBWA_MODE_BAM_READ1) which |= 1;
+      if (mode & IBWA_MODE_BAM_READ2) which |= 2;
+      if (which == 0) which = 7;
+      bam.reset(new ibwa_cli::BamReader);
+      return bam->open(fn, which);
+    }
+    fq.reset(new ibwa_cli::SeqReader);
+    return fq->open(fn);
+  }
+  bool next(Read &r) { return bam ? next_read(*bam, mode, trim_qual, r) : next_read(*fq, mode, trim_qual, r); }
+};
+
+// ---------------------------------------------------------------- the batch loop (bwa_sai2sam_pe_core)
+struct Sampe {
+  ibwa_ctx_t *ctx = nullptr;
+  Bns b;
+  PeOpt popt;
+  ibwa_gap_opt_t gopt[2];
+  FILE *fp_sai[2] = {nullptr, nullptr};
+  Drand48 rnd;
+  Isize last_ii;
+  // bwtcache (bwtcache.c:27-45): positions of an interval of >= 1000 rows, keyed by (k, l) only
+  std::unordered_map<uint64_t, std::vector<uint64_t>> cache;
+  const char *rg_id = nullptr;
+
+  int max_diff_of(const Read &r) const {
+    return gopt[1].fnr > 0.0 ? ibwa_cal_maxdiff(r.len, 0.02, gopt[1].fnr) : gopt[1].max_diff;
+  }
+
+  // alngrp_create (saiset.c:42-74) for one read and one database
+  bool read_alns(int j, std::vector<ibwa_aln1_t> &v) {
+    uint32_t count = 0;
+    v.clear();
+    if (fread(&count, 4, 1, fp_sai[j]) != 1) return true;  // past the end: nothing (count stays 0)
+    v.resize(count);
+    if (count && fread(v.data(), sizeof(ibwa_aln1_t), count, fp_sai[j]) != count) {
+      fprintf(stderr, "[ibwa-amd sampe] truncated .sai\n");
+      return false;
+    }
+    return true;
+  }
+
+  static void unmap(Read &s) {  // UNMAP_READ (bwape.c:48-56)
+    s.type = TYPE_NO_MATCH;
+    s.pos = s.remapped_pos = s.sa = s.c1 = s.c2 = 0;
+    s.cigar.clear();
+    s.has_cigar = false;
+  }
+
+  // select_sai_ibwa (bwape.c:281-358) up to the coordinate: the RNG decisions and the SA row
+  // (main alignment index and the row inside it); returns false when the read is unmapped.
+  bool select_sai(const std::vector<ibwa_aln1_t> &ag, Read &s) {
+    if (ag.empty()) {
+      unmap(s);
+      return false;
+    }
+    int main_idx = 0, i, cnt;
+    double rng_cache = 0.0;
+    const int best = ag[0].score;
+    for (i = cnt = 0; i < (int)ag.size(); ++i) {
+      const ibwa_aln1_t &p = ag[i];
+      const int naln = (int)(p.l - p.k + 1);
+      if (p.score > best) break;
+      if (rnd.next() * (double)(uint32_t)(p.l - p.k + 1 + (uint32_t)cnt) > (double)cnt) {
+        main_idx = i;
+        rng_cache = rnd.next();
+      }
+      cnt += naln;
+    }
+    s.c1 = (uint32_t)cnt & 0xfffffffu;
+    for (int t = i; t < (int)ag.size(); ++t) cnt += (int)(ag[t].l - ag[t].k + 1);
+    s.c2 = ((uint32_t)cnt - s.c1) & 0xfffffffu;
+    if (s.c1 != 0) s.type = s.c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
+    const ibwa_aln1_t &p = ag[main_idx];
+    const uint32_t num = p.l - p.k + 1;
+    const uint32_t start = (uint32_t)(rng_cache * num);
+    s.n_mm = p.n_mm; s.n_gapo = p.n_gapo; s.n_gape = p.n_gape; s.strand = p.a;
+    s.score = p.score;
+    if (!popt.remapping) {  // remap() never reports success: every row, then UNMAP_READ
+      s.sa = p.k + (start == 0 ? num - 1 : start - 1);
+      unmap(s);
+      fprintf(stderr, "Failed to select primary alignment for %s\n", s.name.c_str());
+      return false;
+    }
+    s.sa = p.k + start;
+    return true;
+  }
+
+  int run(Source src[2], FILE *out) {
+    Out o{out, {}};
+    long tot = 0;
+    for (;;) {
+      std::vector<Read> seqs[2];
+      for (int j = 0; j < 2; ++j) {
+        Read r;
+        while ((int)seqs[j].size() < 0x40000 && src[j].next(r)) seqs[j].push_back(std::move(r));
+      }
+      if (seqs[0].empty()) break;
+      if (seqs[1].size() != seqs[0].size()) {
+        fprintf(stderr, "[ibwa-amd sampe] the two read files hold different numbers of reads\n");
+        return 1;
+      }
+      const int n = (int)seqs[0].size();
+      tot += n;
+      if (int rc = batch(seqs, n, o)) return rc;
+      fprintf(stderr, "[bwa_sai2sam_pe_core] %ld sequences have been processed.\n", tot);
+    }
+    o.flush();
+    return 0;
+  }
+
+  int batch(std::vector<Read> seqs[2], int n, Out &o) {
+    std::vector<std::vector<ibwa_aln1_t>> alns[2];
+    alns[0].resize(n);
+    alns[1].resize(n);
+    // ---- SE (bwa_cal_pac_pos_pe, bwape.c:366-385): hit choice in pair order, then one SA->pos launch
+    std::vector<uint8_t> hs;
+    std::vector<uint32_t> hk, hl;
+    std::vector<Read *> hr;
+    for (int i = 0; i < n; ++i) {
+      for (int j = 0; j < 2; ++j) {
+        Read &p = seqs[j][i];
+        p.multi.clear();
+        p.extra_flag |= SAM_FPD | (j == 0 ? SAM_FR1 : SAM_FR2);
+        if (!read_alns(j, alns[j][i])) return 1;
+        if (select_sai(alns[j][i], p)) {
+          hs.push_back((uint8_t)p.strand); hk.push_back(p.sa); hl.push_back((uint32_t)p.len);
+          hr.push_back(&p);
+        }
+      }
+    }
+    std::vector<uint64_t> pos(hk.size());
+    if (!hk.empty() && ibwa_sa2pos(ctx, (int64_t)hk.size(), hs.data(), hk.data(), hl.data(), 0, pos.data()))
+      return die("sa2pos");
+    for (size_t t = 0; t < hr.size(); ++t) {
+      Read &p = *hr[t];
+      p.pos = p.remapped_pos = pos[t];  // remap(): no .remap file, the hit maps to itself
+      p.seQ = p.mapQ = approx_mapQ(p, max_diff_of(p)) & 0xff;
+    }
+    // ---- insert size
+    Isize ii;
+    infer_isize(seqs[0], seqs[1], ii, popt.ap_prior, b.l_pac);
+    if (ii.avg < 0.0 && last_ii.avg > 0.0) ii = last_ii;
+    if (popt.force_isize) {
+      fprintf(stderr, "[bwa_cal_pac_pos_pe] discard insert size estimate as user's request.\n");
+      ii.low = ii.high = 0;
+      ii.avg = ii.std = -1.0;
+    }
+    // ---- every row of every interval (compute_seq_coords_and_counts): one SA->pos launch
+    // rows of intervals narrower than kMinHashWidth are computed per (read, alignment); wider ones
+    // come from the cache, filled on first use with that caller's strand and read length.
+    std::vector<int64_t> row0[2];  // per (pair, end): first alignment slot in aslot
+    std::vector<int64_t> aslot;    // per alignment: first row in rows (-1: cached)
+    hs.clear(); hk.clear(); hl.clear();
+    std::vector<std::pair<uint64_t, int64_t>> fill;  // new cache keys -> first row
+    if (popt.remapping) {
+      for (int j = 0; j < 2; ++j) row0[j].assign(n + 1, 0);
+      for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < 2; ++j) {
+          row0[j][i] = (int64_t)aslot.size();
+          for (const ibwa_aln1_t &a : alns[j][i]) {
+            const uint32_t w = a.l - a.k + 1;
+            if (w >= kMinHashWidth) {
+              const uint64_t key = (uint64_t)a.k << 32 | a.l;
+              if (!cache.count(key)) {
+                fill.push_back({key, (int64_t)hk.size()});
+                cache[key];  // reserve: later uses in this batch share it
+                for (uint32_t r = 0; r < w; ++r) { hs.push_back((uint8_t)a.a); hk.push_back(a.k + r); hl.push_back((uint32_t)seqs[j][i].len); }
+              }
+              aslot.push_back(-1);
+            } else {
+              aslot.push_back((int64_t)hk.size());
+              for (uint32_t r = 0; r < w; ++r) { hs.push_back((uint8_t)a.a); hk.push_back(a.k + r); hl.push_back((uint32_t)seqs[j][i].len); }
+            }
+          }
+        }
+      }
+    }
+    pos.assign(hk.size(), 0);
+    if (!hk.empty() && ibwa_sa2pos(ctx, (int64_t)hk.size(), hs.data(), hk.data(), hl.data(), 0, pos.data()))
+      return die("sa2pos");
+    for (auto &f : fill) {
+      const uint32_t k = (uint32_t)(f.first >> 32), l = (uint32_t)f.first;
+      cache[f.first].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
+    }
+    // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:226-279), pair by pair
+    PosArr arr;
+    int cnt_chg = 0;
+    const uint64_t l_pac = (uint64_t)b.l_pac;
+    for (int i = 0; i < n; ++i) {
+      Read *p[2] = {&seqs[0][i], &seqs[1][i]};
+      arr.clear();
+      if (popt.remapping) {
+        for (int j = 0; j < 2; ++j) {
+          std::map<uint64_t, const ibwa_aln1_t *> pos2score;
+          int min_score = INT32_MAX;
+          const std::vector<ibwa_aln1_t> &ag = alns[j][i];
+          for (size_t k = 0; k < ag.size(); ++k) {
+            const ibwa_aln1_t &a = ag[k];
+            min_score = std::min(min_score, a.score);
+            const uint32_t w = a.l - a.k + 1;
+            const int64_t slot = aslot[row0[j][i] + (int64_t)k];
+            const uint64_t *pp = slot < 0 ? cache[(uint64_t)a.k << 32 | a.l].data() : pos.data() + slot;
+            for (uint32_t r = 0; r < w; ++r) {
+              const uint64_t x = pp[r];
+              if (x >= l_pac) continue;
+              Position ap;
+              ap.pos = ap.remapped_pos = x;
+              ap.idx_and_end = (uint32_t)k << 1 | (uint32_t)j;
+              arr.push(ap);
+              auto ins = pos2score.insert({x, &a});
+              if (!ins.second && a.score < ins.first->second->score) ins.first->second = &a;
+            }
+          }
+          size_t c[2] = {0, 0};
+          for (auto &kv : pos2score) ++c[kv.second->score == min_score ? 0 : 1];
+          p[j]->c1 = (uint32_t)c[0] & 0xfffffffu;
+          p[j]->c2 = (uint32_t)c[1] & 0xfffffffu;
+          if (p[j]->c1 != 0) p[j]->type = p[j]->c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
+        }
+      }
+      for (int j = 0; j < 2; ++j)
+        if (p[j]->c1 || p[j]->c2) p[j]->seQ = p[j]->mapQ = approx_mapQ(*p[j], max_diff_of(*p[j])) & 0xff;
+      const bool m0 = p[0]->type == TYPE_UNIQUE || p[0]->type == TYPE_REPEAT;
+      const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
+      if (m0 && m1) {
+        PairCtx c{{p[0], p[1]}, {&alns[0][i], &alns[1][i]}, &popt, &ii, gopt[1].s_mm};
+        cnt_chg += find_optimal_pair(c, arr);
+      }
+      if (popt.N_multi || popt.n_multi) {
+        for (int j = 0; j < 2; ++j) {
+          if (p[j]->type == TYPE_NO_MATCH) continue;
+          int max_multi = popt.n_multi;
+          if (!(p[j]->extra_flag & SAM_FPP) && p[1 - j]->type != TYPE_NO_MATCH)
+            max_multi = (int)(p[j]->c1 + p[j]->c2) - 1 > popt.N_multi ? popt.n_multi : popt.N_multi;
+          if (int rc = select_sai_multi(alns[j][i], *p[j], max_multi, row0[j].empty() ? -1 : row0[j][i], aslot, pos))
+            return rc;
+        }
+      }
+    }
+    fprintf(stderr, "[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);
+    // ---- mate rescue (bwa_paired_sw): the drop-in over the reference's bwa_seq_t layout
+    if (int rc = paired_sw(seqs, n, ii)) return rc;
+    // ---- refine gapped alignments of both ends, MD/NM, trimmed reads; then remap()
+    std::vector<Read *> rp;
+    for (int j = 0; j < 2; ++j)
+      for (Read &r : seqs[j]) rp.push_back(&r);
+    if (int rc = refine_gapped(ctx, b, rp)) return rc == 1 ? 1 : die("global alignment");
+    for (int j = 0; j < 2; ++j) {
+      for (Read &r : seqs[j]) {
+        if (popt.remapping) {
+          r.remapped_pos = r.pos;
+        } else {
+          fprintf(stderr, "Failed to remap read %s after refining gaps.\n", r.name.c_str());
+          unmap(r);
+        }
+      }
+    }
+    // ---- print
+    for (int i = 0; i < n; ++i) {
+      Read *p[2] = {&seqs[0][i], &seqs[1][i]};
+      if (p[0]->bc[0] || p[1]->bc[0]) {
+        strncat(p[0]->bc, p[1]->bc, sizeof p[0]->bc - strlen(p[0]->bc) - 1);
+        memcpy(p[1]->bc, p[0]->bc, sizeof p[1]->bc);
+      }
+      p[0]->remapped_pos = p[0]->pos;  // -R swaps pos and remapped_pos, which are equal here
+      p[1]->remapped_pos = p[1]->pos;
+      print_sam1(o, b, *p[0], p[1], gopt[1].mode, gopt[1].max_top2, rg_id);
+      print_sam1(o, b, *p[1], p[0], gopt[1].mode, gopt[1].max_top2, rg_id);
+      if (o.b.size() > (1u << 20)) o.flush();
+    }
+    o.flush();
+    last_ii = ii;
+    return 0;
+  }
+
+  // select_sai_multi (saiset.c:124-163): every hit when there are at most n_multi + 1 of them
+  int select_sai_multi(const std::vector<ibwa_aln1_t> &ag, Read &s, int n_multi, int64_t slot0,
+                       const std::vector<int64_t> &aslot, const std::vector<uint64_t> &pos) {
+    int n_occ = 0;
+    for (const ibwa_aln1_t &q : ag) n_occ += (int)(q.l - q.k + 1);
+    s.multi.clear();
+    if (n_occ > n_multi + 1) return 0;
+    std::vector<Multi> all;
+    for (size_t k = 0; k < ag.size(); ++k) {
+      const ibwa_aln1_t &q = ag[k];
+      const uint32_t w = q.l - q.k + 1;
+      std::vector<uint64_t> own;
+      const uint64_t *pp = nullptr;
+      const int64_t slot = slot0 >= 0 ? aslot[slot0 + (int64_t)k] : -1;
+      if (slot >= 0) {
+        pp = pos.data() + slot;
+      } else {  // not on hand (no -R pass, or a cached interval): bwtdb_sa2seq for this read
+        std::vector<uint8_t> st(w, (uint8_t)q.a);
+        std::vector<uint32_t> kk(w), ll(w, (uint32_t)s.len);
+        for (uint32_t r = 0; r < w; ++r) kk[r] = q.k + r;
+        own.resize(w);
+        if (ibwa_sa2pos(ctx, (int64_t)w, st.data(), kk.data(), ll.data(), 0, own.data())) return die("sa2pos");
+        pp = own.data();
+      }
+      for (uint32_t r = 0; r < w; ++r) {
+        Multi m;
+        m.pos = pp[r];
+        m.gap = (q.n_gapo + q.n_gape) & 0xff;
+        m.mm = q.n_mm;
+        m.strand = q.a;
+        all.push_back(m);
+      }
+    }
+    for (const Multi &m : all)
+      if (m.pos != s.pos) s.multi.push_back(m);
+    if ((int)s.multi.size() > n_multi) s.multi.resize(std::max(n_multi, 0));
+    return 0;
+  }
+
+  // bwa_paired_sw through the C-ABI drop-in (compat.cpp), on bwa_seq_t mirrors of the batch
+  int paired_sw(std::vector<Read> seqs[2], int n, const Isize &ii) {
+    if (!popt.is_sw || ii.avg < 0.0) return 0;
+    std::vector<ibwa_ref_seq_t> ref[2];
+    std::vector<std::vector<uint8_t>> rev[2];
+    for (int j = 0; j < 2; ++j) {
+      ref[j].assign(n, ibwa_ref_seq_t());
+      rev[j].resize(n);
+      for (int i = 0; i < n; ++i) {
+        Read &r = seqs[j][i];
+        ibwa_ref_seq_t &t = ref[j][i];
+        memset(&t, 0, sizeof t);
+        rev[j][i].assign(r.seq.rbegin() + (r.full_len - r.len), r.seq.rend());  // bwa_seq_t.seq: the read reversed
+        t.seq = rev[j][i].data();
+        t.rseq = r.rseq.data();
+        t.len = (uint32_t)r.len;
+        t.full_len = (uint32_t)r.full_len;
+        t.strand = (uint32_t)r.strand;
+        t.type = (uint32_t)r.type;
+        t.extra_flag = (uint32_t)r.extra_flag;
+        t.n_mm = (uint32_t)r.n_mm; t.n_gapo = (uint32_t)r.n_gapo; t.n_gape = (uint32_t)r.n_gape;
+        t.mapQ = (uint32_t)r.mapQ;
+        t.seQ = (uint64_t)r.seQ;
+        t.pos = r.pos;
+        t.remapped_pos = r.remapped_pos;
+        t.c1 = r.c1; t.c2 = r.c2;
+      }
+    }
+    ibwa_ref_pe_opt_t po;
+    memset(&po, 0, sizeof po);
+    po.max_isize = popt.max_isize; po.force_isize = popt.force_isize; po.max_occ = popt.max_occ;
+    po.n_multi = popt.n_multi; po.N_multi = popt.N_multi; po.n_threads = 1;
+    po.type = popt.type; po.is_sw = popt.is_sw; po.is_preload = popt.is_preload; po.remapping = popt.remapping;
+    po.ap_prior = popt.ap_prior;
+    ibwa_ref_isize_info_t ri{ii.avg, ii.std, ii.ap_prior, ii.low, ii.high, ii.high_bayesian};
+    ibwa_ref_seq_t *sp[2] = {ref[0].data(), ref[1].data()};
+    uint64_t n_tot[2], n_mapped[2];
+    if (ibwa_paired_sw(ctx, n, sp, &po, &ri, b.pac.data(), (uint64_t)b.l_pac, n_tot, n_mapped)) return die("paired SW");
+    fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 singletons are mated.\n", (unsigned long long)n_mapped[1],
+            (unsigned long long)n_tot[1]);
+    fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 discordant pairs are fixed.\n", (unsigned long long)n_mapped[0],
+            (unsigned long long)n_tot[0]);
+    for (int j = 0; j < 2; ++j) {
+      for (int i = 0; i < n; ++i) {
+        Read &r = seqs[j][i];
+        ibwa_ref_seq_t &t = ref[j][i];
+        r.type = t.type;
+        r.strand = t.strand;
+        r.extra_flag = t.extra_flag;
+        r.n_mm = t.n_mm; r.n_gapo = t.n_gapo; r.n_gape = t.n_gape;
+        r.mapQ = t.mapQ;
+        r.seQ = (int)t.seQ;
+        r.pos = t.pos;
+        r.remapped_pos = t.remapped_pos;
+        if (t.cigar) {
+          r.cigar.assign(t.cigar, t.cigar + t.n_cigar);
+          r.has_cigar = true;
+          free(t.cigar);
+        }
+      }
+    }
+    return 0;
+  }
+};
+
+}  // namespace
+
+int sampe_main(int argc, char *argv[]) {
+  init_tables();
+  Sampe S;
+  int c;
+  const char *fn_out = nullptr;
+  std::string rg_line, rg_id;
+  optind = 1;
+  while ((c = getopt(argc, argv, "a:o:sPn:N:c:f:ARr:t:")) >= 0) {  // bwa_sai2sam_pe (bwape.c:583-610)
+    switch (c) {
+      case 'r':
+        if (!set_rg(optarg, rg_line, rg_id)) {
+          fprintf(stderr, "[bwa_sai2sam_pe] malformated @RG line\n");
+          return 1;
+        }
+        break;
+      case 'a': S.popt.max_isize = atoi(optarg); break;
+      case 'o': S.popt.max_occ = atoi(optarg); break;
+      case 's': S.popt.is_sw = 0; break;
+      case 'P': S.popt.is_preload = 1; break;
+      case 'n': S.popt.n_multi = atoi(optarg); break;
+      case 'N': S.popt.N_multi = atoi(optarg); break;
+      case 't': S.popt.n_threads = atoi(optarg); break;
+      case 'c': S.popt.ap_prior = atof(optarg); break;
+      case 'f': fn_out = optarg; break;
+      case 'A': S.popt.force_isize = 1; break;
+      case 'R': S.popt.remapping = 1; break;
+      default: return 1;
+    }
+  }
+  if (optind + 5 > argc) {
+    fprintf(stderr, "Usage: ibwa-amd sampe [-a INT] [-o INT] [-n INT] [-N INT] [-c FLOAT] [-f out.sam] [-r RG] [-sAR]\n"
+                    "                      <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq>\n");
+    return 1;
+  }
+  if (argc - optind > 5) {
+    fprintf(stderr, "[ibwa-amd sampe] several databases (<prefix2> <sai> <sai> ...) are not supported\n");
+    return 1;
+  }
+  const std::string prefix = argv[optind];
+  if (S.popt.remapping) {
+    if (FILE *fr = fopen((prefix + ".remap").c_str(), "r")) {
+      fclose(fr);
+      fprintf(stderr, "[ibwa-amd sampe] %s.remap: compound sequence remapping tables are not supported\n", prefix.c_str());
+      return 1;
+    }
+  }
+  for (int j = 0; j < 2; ++j) {  // saiset_create (saiset.c:14-33)
+    S.fp_sai[j] = fopen(argv[optind + 1 + j], "rb");
+    if (!S.fp_sai[j] || fread(&S.gopt[j], sizeof S.gopt[j], 1, S.fp_sai[j]) != 1) {
+      fprintf(stderr, "[ibwa-amd sampe] cannot read the .sai header of %s\n", argv[optind + 1 + j]);
+      return 1;
+    }
+    if (!(S.gopt[j].mode & IBWA_MODE_COMPREAD)) {
+      fprintf(stderr, "[ibwa-amd sampe] color-space alignments (aln -c) need the .nt index: not supported\n");
+      return 1;
+    }
+  }
+  Source src[2];
+  for (int j = 0; j < 2; ++j) {
+    if (!src[j].open(argv[optind + 3 + j], S.gopt[j])) {
+      fprintf(stderr, "[ibwa-amd sampe] cannot open %s\n", argv[optind + 3 + j]);
+      return 1;
+    }
+  }
+  if (!bns_restore(prefix, S.b)) {
+    fprintf(stderr, "[ibwa-amd sampe] cannot read %s.ann / .amb / .pac\n", prefix.c_str());
+    return 1;
+  }
+  if (ibwa_ctx_create(0, &S.ctx)) return die("ibwa_ctx_create");
+  if (ibwa_ctx_load_bwt_file(S.ctx, 0, (prefix + ".bwt").c_str()) ||
+      ibwa_ctx_load_bwt_file(S.ctx, 1, (prefix + ".rbwt").c_str()))
+    return die("load .bwt / .rbwt");
+  if (ibwa_ctx_load_sa_file(S.ctx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(S.ctx, 1, (prefix + ".rsa").c_str()))
+    return die("load .sa / .rsa");
+  if (ibwa_ctx_expand_sa(S.ctx)) return die("expand SA");
+  S.rnd.seed((long)S.b.seed);  // srand48(bns->seed), bwape.c:461
+  S.rg_id = rg_id.empty() ? nullptr : rg_id.c_str();
+  FILE *out = fn_out ? fopen(fn_out, "w") : stdout;
+  if (!out) {
+    fprintf(stderr, "[ibwa-amd sampe] cannot write %s\n", fn_out);
+    return 1;
+  }
+  // @SQ lines, then @RG, then @PG (dbset_print_sam_SQ, bwa_print_sam_PG)
+  std::string head;
+  for (const Ann &a : S.b.anns) head += "@SQ\tSN:" + a.name + "\tLN:" + std::to_string(a.len) + "\n";
+  if (!rg_line.empty()) head += rg_line + "\n";
+  head += "@PG\tID:bwa\tPN:bwa\tVN:ibwa-amd\n";
+  fwrite(head.data(), 1, head.size(), out);
+  Source *sp = src;
+  const int rc = S.run(sp, out);
+  for (int j = 0; j < 2; ++j) fclose(S.fp_sai[j]);
+  if (out != stdout) fclose(out);
+  ibwa_ctx_destroy(S.ctx);
+  return rc;
+}

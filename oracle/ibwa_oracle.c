@@ -1115,7 +1115,7 @@ uint32_t or_bwt_sa(const or_bwt_t *b, const uint32_t *sa, uint32_t intv, uint32_
 }
 
 /* bwtdb_sa2seq (dbset.c:240-246) with db->offset = 0, over a batch:
- * strand 1 -> bwt_sa(bwt[0], k); strand 0 -> bwt[1]->seq_len - (bwt_sa(bwt[1], k) + len) (u32) */
+ * strand 1 -> bwt_sa(bwt[0], k); strand 0 -> bwt[1]->seq_len - (u32)(bwt_sa(bwt[1], k) + len) in u64 (dbset.c:244) */
 void or_sa2seq_batch(const or_bwt_t *b0_, const uint32_t *sa0, const or_bwt_t *b1, const uint32_t *sa1,
                      uint32_t intv, int64_t n, const uint8_t *strand, const uint32_t *k, const uint32_t *len,
                      uint64_t *pos, uint32_t *steps)
@@ -1123,6 +1123,6 @@ void or_sa2seq_batch(const or_bwt_t *b0_, const uint32_t *sa0, const or_bwt_t *b
 	int64_t i;
 	for (i = 0; i < n; ++i) {
 		if (strand[i]) pos[i] = or_bwt_sa(b0_, sa0, intv, k[i], steps ? steps + i : 0);
-		else pos[i] = (uint32_t)(b1->seq_len - (uint32_t)(or_bwt_sa(b1, sa1, intv, k[i], steps ? steps + i : 0) + len[i]));
+		else pos[i] = (uint64_t)b1->seq_len - (uint32_t)(or_bwt_sa(b1, sa1, intv, k[i], steps ? steps + i : 0) + len[i]);
 	}
 }

@@ -141,7 +141,8 @@ static int cmd_sa(int argc, char *argv[])
 	if (!(fp = fopen(argv[2], "r"))) return 1;
 	while (fscanf(fp, "%u %u %u", &strand, &k, &len) == 3) {
 		bwtint_t sa = bwt_sa(bwt[strand ? 0 : 1], k);
-		uint64_t pos = strand ? (uint64_t)sa : (uint64_t)(bwtint_t)(bwt[1]->seq_len - (bwtint_t)(sa + len));
+		/* bwtdb_sa2seq (dbset.c:244): u64 offset + u32 seq_len - u32 (sa + len), i.e. u64 arithmetic */
+		uint64_t pos = strand ? (uint64_t)sa : (uint64_t)0 + bwt[1]->seq_len - (bwtint_t)(sa + len);
 		printf("%u\t%u\t%u\t%u\t%llu\n", strand, k, len, sa, (unsigned long long)pos);
 	}
 	fclose(fp);

@@ -65,6 +65,18 @@ def main():
                 rows.append((strand, k, ln))
         for _ in range(3000):
             rows.append((strand, rng.randrange(0, seq_len + 1), rng.choice((17, 36, 100, 150, 250))))
+    # rows whose reverse-index suffix is shorter than the read: seq_len - (sa + len) wraps in u64
+    with tempfile.NamedTemporaryFile("w", suffix=".tsv", delete=False) as f:
+        for k in range(seq_len + 1):
+            f.write("0\t%d\t1\n" % k)
+        tmp = f.name
+    out = subprocess.run([REF, "sa", os.path.join(GOLD, "g1m"), tmp], check=True, capture_output=True, text=True).stdout
+    os.unlink(tmp)
+    for ln in out.splitlines():
+        _, k, _, sa, _ = (int(x) for x in ln.split("\t"))
+        if seq_len - 250 < sa < seq_len:
+            for L in (17, 36, 100, 150, 250):
+                rows.append((0, k, L))
     with tempfile.NamedTemporaryFile("w", suffix=".tsv", delete=False) as f:
         for r in rows:
             f.write("%d\t%d\t%d\n" % r)

@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/pe_*: paired reads, their .sai and the reference's sampe SAM (build container only).
+
+TEST INFRASTRUCTURE.  Mate pairs are drawn from the golden g1m genome (tests/synth_util.py) with
+a mix of the situations sampe's code paths branch on: proper pairs, pairs with one end made
+unalignable by `aln` but rescuable by bwa_paired_sw (dense mismatches), random (unmappable) ends,
+discordant pairs (far apart / same strand / different contigs), pairs inside repeat families,
+reads with N, fragments at contig ends and reads with low base qualities (for `aln -q`).
+The reference's own `aln` and `sampe` (bwa_sai2sam_pe_core, bwape.c:436-540, compiled into
+oracle/_ref/ibwa_ref by oracle/Makefile) are run on them; the FASTQ, .sai and gzip'd SAM are
+committed with sampe_manifest.json.  The @PG line names the program that wrote the file and is
+not compared.
+"""
+import gzip
+import json
+import os
+import random
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+REF = os.path.join(ROOT, "oracle", "_ref", "ibwa_ref")
+sys.path.insert(0, ROOT)
+
+from tests.synth_util import golden_genome_ascii  # noqa: E402
+
+COMP = str.maketrans("ACGTN", "TGCAN")
+
+# read set -> (read length, insert avg, insert std, substitution rate, pairs, seed)
+SETS = {
+    "pe100": (100, 300.0, 30.0, 0.01, 1500, 11),
+    "pe150": (150, 350.0, 35.0, 0.02, 600, 12),
+    "pe70few": (70, 250.0, 20.0, 0.01, 15, 13),  # too few pairs: insert size not inferred
+}
+# sampe cases: key -> (read set, aln options, sampe options)
+CASES = {
+    "pe100.default": ("pe100", [], ["-R"]),
+    "pe100.noR": ("pe100", [], []),  # without -R the reference unmaps every read (select_sai_ibwa's remap status)
+    "pe100.s": ("pe100", [], ["-R", "-s"]),
+    "pe100.A": ("pe100", [], ["-R", "-A"]),
+    "pe100.a1000": ("pe100", [], ["-R", "-a", "1000"]),
+    "pe100.n5N20": ("pe100", [], ["-R", "-n", "5", "-N", "20"]),
+    "pe100.n0N0": ("pe100", [], ["-R", "-n", "0", "-N", "0"]),
+    "pe100.c1e-3": ("pe100", [], ["-R", "-c", "1e-3"]),
+    "pe100.rg": ("pe100", [], ["-R", "-r", "@RG\\tID:lane1\\tSM:x"]),
+    "pe100.q20": ("pe100", ["-q", "20"], ["-R"]),
+    "pe100.k0n3": ("pe100", ["-k", "0", "-n", "3"], ["-R"]),
+    "pe150.default": ("pe150", [], ["-R"]),
+    "pe150.o1000": ("pe150", [], ["-R", "-o", "1000"]),
+    "pe70few.default": ("pe70few", [], ["-R"]),
+}
+
+
+def rc(s):
+    return s.translate(COMP)[::-1]
+
+
+def mutate(rng, s, sub):
+    out = list(s)
+    for i in range(len(out)):
+        if out[i] != "N" and rng.random() < sub:
+            out[i] = rng.choice([b for b in "ACGT" if b != out[i]])
+    s = "".join(out)
+    if rng.random() < 0.05:  # one short indel
+        p = rng.randrange(10, len(s) - 10)
+        if rng.random() < 0.5:
+            s = (s[:p] + "".join(rng.choice("ACGT") for _ in range(rng.randint(1, 3))) + s[p:])[:len(out)]
+        else:
+            d = rng.randint(1, 3)
+            s = s[:p] + s[p + d:] + "".join(rng.choice("ACGT") for _ in range(d))
+    return s
+
+
+def qual(rng, L, low_tail):
+    q = [chr(33 + rng.randint(20, 40)) for _ in range(L)]
+    if low_tail:
+        for i in range(L - rng.randint(5, 30), L):
+            q[i] = chr(33 + rng.randint(2, 12))
+    return "".join(q)
+
+
+def make_pairs(genome, starts, rng, L, avg, std, sub, n):
+    G = len(genome)
+    kinds = ["pair"] * 6 + ["dense1", "dense2", "rand1", "rand2", "disc", "samestrand", "far", "withN", "edge",
+                            "lowq", "repeat"]
+    r1s, r2s = [], []
+    while len(r1s) < n:
+        kind = kinds[len(r1s) % len(kinds)]
+        ins = max(L + 10, int(rng.gauss(avg, std)))
+        if kind == "edge":
+            c = rng.randrange(len(starts) - 1)
+            f = rng.choice([starts[c] + rng.randrange(0, 40), starts[c + 1] - ins - rng.randrange(0, 40)])
+        else:
+            f = rng.randrange(0, G - ins)
+        seg = genome[f:f + ins]
+        if "N" in seg and kind != "withN":
+            continue
+        if kind == "withN" and "N" not in seg:
+            seg = seg[:ins // 3] + "N" + seg[ins // 3 + 1:]
+        a, b = mutate(rng, seg[:L], sub), mutate(rng, rc(seg[-L:]), sub)
+        if kind == "dense1":  # aln misses end 1 (9 mismatches), local SW still finds it
+            a = mutate(rng, seg[:L], 0.09)
+        elif kind == "dense2":
+            b = mutate(rng, rc(seg[-L:]), 0.09)
+        elif kind == "rand1":
+            a = "".join(rng.choice("ACGT") for _ in range(L))
+        elif kind == "rand2":
+            b = "".join(rng.choice("ACGT") for _ in range(L))
+        elif kind == "samestrand":
+            b = mutate(rng, seg[-L:], sub)
+        elif kind == "far":
+            g = rng.randrange(0, G - L)
+            if "N" in genome[g:g + L]:
+                continue
+            b = mutate(rng, rc(genome[g:g + L]), sub)
+        elif kind == "disc":
+            b = mutate(rng, rc(genome[f + ins + 2000:f + ins + 2000 + L]), sub) if f + ins + 2000 + L < G else b
+        if len(a) != L or len(b) != L:
+            continue
+        if rng.random() < 0.5:  # which end comes first in the fragment
+            a, b = b, a
+        low = kind == "lowq"
+        r1s.append((a, qual(rng, L, low)))
+        r2s.append((b, qual(rng, L, low and rng.random() < 0.5)))
+    return r1s, r2s
+
+
+def write_fq(path, name, recs, suffix):
+    with open(path, "w") as f:
+        for i, (s, q) in enumerate(recs):
+            f.write(f"@{name}{i}/{suffix}\n{s}\n+\n{q}\n")
+
+
+def main():
+    genome, names, lens = golden_genome_ascii()
+    starts = [0]
+    for ln in lens:
+        starts.append(starts[-1] + ln)
+    for key, (L, avg, std, sub, n, seed) in SETS.items():
+        rng = random.Random(seed)
+        r1, r2 = make_pairs(genome, starts, rng, L, avg, std, sub, n)
+        write_fq(os.path.join(GOLD, f"{key}_1.fq"), key + "_", r1, 1)
+        write_fq(os.path.join(GOLD, f"{key}_2.fq"), key + "_", r2, 2)
+    manifest = {}
+    prefix = os.path.join(GOLD, "g1m")
+    for key, (rs, aln_argv, sampe_argv) in CASES.items():
+        sai = []
+        for end in (1, 2):
+            tag = "default" if not aln_argv else "".join(a.strip("-") for a in aln_argv)
+            fn = f"{rs}.{tag}_{end}.sai"
+            subprocess.run([REF, "aln"] + aln_argv + ["-f", os.path.join(GOLD, fn), prefix,
+                                                      os.path.join(GOLD, f"{rs}_{end}.fq")],
+                           check=True, capture_output=True)
+            sai.append(fn)
+        out = subprocess.run([REF, "sampe"] + sampe_argv + [prefix, os.path.join(GOLD, sai[0]), os.path.join(GOLD, sai[1]),
+                                                            os.path.join(GOLD, f"{rs}_1.fq"),
+                                                            os.path.join(GOLD, f"{rs}_2.fq")],
+                             check=True, capture_output=True)
+        with open(os.path.join(GOLD, f"sampe_{key}.sam.gz"), "wb") as raw:
+            with gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:
+                f.write(out.stdout)
+        manifest[key] = {"sai": sai, "reads": [f"{rs}_1.fq", f"{rs}_2.fq"], "aln_argv": aln_argv,
+                         "argv": sampe_argv, "sam": f"sampe_{key}.sam.gz"}
+        print(key, len(out.stdout.splitlines()), "lines")
+    with open(os.path.join(GOLD, "sampe_manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
