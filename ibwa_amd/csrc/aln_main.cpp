@@ -131,14 +131,22 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
 
 int samse_main(int argc, char *argv[]);  // samse_main.cpp
 int sampe_main(int argc, char *argv[]);  // sampe_main.cpp
+int index_main(int argc, char *argv[]);  // index_main.cpp
+int fa2pac_main(int argc, char *argv[]);
+int pac_rev_main(int argc, char *argv[]);
 
 int main(int argc, char *argv[]) {
   if (argc >= 2 && strcmp(argv[1], "samse") == 0) return samse_main(argc - 1, argv + 1);
   if (argc >= 2 && strcmp(argv[1], "sampe") == 0) return sampe_main(argc - 1, argv + 1);
+  if (argc >= 2 && strcmp(argv[1], "index") == 0) return index_main(argc - 1, argv + 1);
+  if (argc >= 2 && strcmp(argv[1], "fa2pac") == 0) return fa2pac_main(argc - 1, argv + 1);
+  if (argc >= 2 && strcmp(argv[1], "pac_rev") == 0) return pac_rev_main(argc - 1, argv + 1);
   if (argc < 2 || strcmp(argv[1], "aln") != 0) {
     fprintf(stderr, "Usage: ibwa-amd aln [options] <prefix> <in.fq>\n"
                     "       ibwa-amd samse [-n max_occ] [-f out.sam] [-r RG] <prefix> <in.sai> <in.fq>\n"
-                    "       ibwa-amd sampe [options] <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq>\n");
+                    "       ibwa-amd sampe [options] <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq>\n"
+                    "       ibwa-amd index [-a bwtsw|div|is] [-p prefix] <in.fasta>\n"
+                    "       ibwa-amd fa2pac <in.fasta> [<out.prefix>] | pac_rev <in.pac> <out.pac>\n");
     return 1;
   }
   --argc; ++argv;

@@ -21,6 +21,10 @@ struct SeqReader {
   bool eof = false;
   int last_char = 0;
   std::string name, seq, qual;
+  // kseq's comment buffer (index): once allocated it keeps the last comment read, and a header
+  // without one leaves it as it was (kseq_read only resets its length)
+  bool keep_comment = false, comment_alloc = false;
+  std::string comment;
 
   bool open(const char *fn) {
     fp = strcmp(fn, "-") ? gzopen(fn, "r") : gzdopen(fileno(stdin), "r");
@@ -51,7 +55,11 @@ struct SeqReader {
     bool got = false;
     while ((c = getc_()) != -1 && !isspace(c)) { name.push_back((char)c); got = true; }
     if (c == -1 && !got) return -1;
-    if (c != '\n') while ((c = getc_()) != -1 && c != '\n') {}  // comment
+    if (c != '\n' && c != -1) {  // comment
+      if (keep_comment) { comment.clear(); comment_alloc = true; }
+      while ((c = getc_()) != -1 && c != '\n')
+        if (keep_comment) comment.push_back((char)c);
+    }
     while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@')
       if (isgraph(c)) seq.push_back((char)c);
     if (c == '>' || c == '@') last_char = c;
