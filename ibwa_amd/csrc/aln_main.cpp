@@ -25,6 +25,7 @@
 
 #include "ibwa_aln.h"
 #include "readers.h"
+#include "sam_common.h"
 
 namespace {
 
@@ -234,6 +235,7 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
     return 1;
   }
   if (n_gpus < 1) n_gpus = 1;
+  ibwa_sam::Phases ph;
   std::vector<ibwa_ctx_t *> ctx(n_gpus, nullptr);
   for (int g = 0; g < n_gpus; ++g) {
     if (ibwa_ctx_create(g, &ctx[g])) return die("ibwa_ctx_create");
@@ -245,11 +247,13 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
     }
   }
   fwrite(&opt, sizeof opt, 1, out);  // bwtaln.c:192
+  ph.mark("load index");
 
   Batch cur, nxt;
   long n_trim = 0, n_tot = 0;
   int64_t tot_seqs = 0;
   bool have = read_batch(rd, opt.mode, opt.trim_qual, cur, &n_trim, &n_tot);
+  ph.mark("read");
   while (have) {
     auto t0 = std::chrono::steady_clock::now();
     const int64_t n = cur.n();
@@ -277,6 +281,7 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
     for (auto &t : th) t.join();
     for (int g = 0; g < n_gpus; ++g)
       if (g_rc[g]) return die("aln");
+    ph.mark("align (next batch parsed meanwhile)");
     double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fprintf(stderr, "%.2f sec\n", sec);
     fprintf(stderr, "[bwa_aln_core] write to the disk... ");
@@ -289,6 +294,7 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
       }
       ibwa_free(g_aln[g]);
     }
+    ph.mark("write");
     fprintf(stderr, "0.00 sec\n");
     fprintf(stderr, "[bwa_aln_core] %lld sequences have been processed.\n", (long long)tot_seqs);
     std::swap(cur, nxt);
@@ -296,5 +302,6 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
   }
   if (out != stdout) fclose(out);
   for (auto *x : ctx) ibwa_ctx_destroy(x);
+  ph.print("ibwa-amd aln");
   return 0;
 }

@@ -11,7 +11,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <functional>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -19,6 +22,45 @@
 #include "readers.h"
 
 namespace ibwa_sam {
+
+// ---------------------------------------------------------------- host parallelism and timing
+// Host threads for the per-read steps that do not touch the RNG stream (MD/NM, SAM formatting):
+// OMP_NUM_THREADS when set (the GPU box sets it to its CPU share), else the hardware's, at most 32.
+inline int host_threads() {
+  const char *e = getenv("OMP_NUM_THREADS");
+  int n = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(n, 32));
+}
+// f(begin, end, chunk) over [0, n) in contiguous chunks, one per thread
+inline void parallel_chunks(int64_t n, const std::function<void(int64_t, int64_t, int)> &f, int nt = 0) {
+  if (nt <= 0) nt = host_threads();
+  nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 256 + 1));
+  if (nt == 1) {
+    f(0, n, 0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) th.emplace_back(f, n * t / nt, n * (t + 1) / nt, t);
+  for (auto &x : th) x.join();
+}
+// wall-clock seconds per named phase, printed to stderr at the end of a command
+struct Phases {
+  std::vector<std::pair<const char *, double>> acc;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  void mark(const char *name) {
+    const auto t = std::chrono::steady_clock::now();
+    const double dt = std::chrono::duration<double>(t - t0).count();
+    t0 = t;
+    for (auto &a : acc)
+      if (!strcmp(a.first, name)) { a.second += dt; return; }
+    acc.push_back({name, dt});
+  }
+  void print(const char *who) const {
+    fprintf(stderr, "[%s] wall s:", who);
+    for (auto &a : acc) fprintf(stderr, " %s %.2f", a.first, a.second);
+    fprintf(stderr, "\n");
+  }
+};
 
 
 constexpr int TYPE_NO_MATCH = 0, TYPE_UNIQUE = 1, TYPE_REPEAT = 2, TYPE_MATESW = 3;  // bwtaln.h:7-10
@@ -513,15 +555,17 @@ inline int refine_gapped(ibwa_ctx_t *ctx, const Bns &b, std::vector<Read *> &rea
     }
     ibwa_free(c32);
   }
-  for (Read *pp : reads) {
-    Read &p = *pp;
-    if (p.type != TYPE_NO_MATCH) {
-      p.md = cal_md1(p, p.remapped_pos, p.strand ? p.rseq.data() : p.seq.data(), b, &p.nm);
-      p.nm &= 0xfff;
-      p.has_md = true;
+  parallel_chunks((int64_t)reads.size(), [&](int64_t lo, int64_t hi, int) {
+    for (int64_t t = lo; t < hi; ++t) {
+      Read &p = *reads[t];
+      if (p.type != TYPE_NO_MATCH) {
+        p.md = cal_md1(p, p.remapped_pos, p.strand ? p.rseq.data() : p.seq.data(), b, &p.nm);
+        p.nm &= 0xfff;
+        p.has_md = true;
+      }
+      correct_trimmed(p);
     }
-  }
-  for (Read *pp : reads) correct_trimmed(*pp);
+  });
   return 0;
 }
 
@@ -658,6 +702,20 @@ inline void print_sam1(Out &o, const Bns &b, Read &p, const Read *mate, int mode
     if (p.clip_len < p.full_len) o.s("\tXC:i:").i(p.clip_len);
     o.c('\n');
   }
+}
+
+// SAM lines of items [0, n) formatted on host threads into per-chunk buffers, written in order
+inline void print_parallel(Out &o, int64_t n, const std::function<void(Out &, int64_t)> &fmt) {
+  o.flush();
+  const int nt = host_threads();
+  std::vector<std::string> bufs(nt);
+  parallel_chunks(n, [&](int64_t lo, int64_t hi, int t) {
+    Out ob{nullptr, {}};
+    for (int64_t i = lo; i < hi; ++i) fmt(ob, i);
+    bufs[t].swap(ob.b);
+  }, nt);
+  for (auto &x : bufs)
+    if (!x.empty()) fwrite(x.data(), 1, x.size(), o.fp);
 }
 
 // bwa_escape / bwa_set_rg (bwase.c:608-641)

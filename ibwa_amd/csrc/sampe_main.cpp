@@ -422,6 +422,7 @@ struct Sampe {
   // bwtcache (bwtcache.c:27-45): positions of an interval of >= 1000 rows, keyed by (k, l) only
   std::unordered_map<uint64_t, std::vector<uint64_t>> cache;
   const char *rg_id = nullptr;
+  Phases ph;
 
   int max_diff_of(const Read &r) const {
     return gopt[1].fnr > 0.0 ? ibwa_cal_maxdiff(r.len, 0.02, gopt[1].fnr) : gopt[1].max_diff;
@@ -495,6 +496,7 @@ struct Sampe {
         Read r;
         while ((int)seqs[j].size() < 0x40000 && src[j].next(r)) seqs[j].push_back(std::move(r));
       }
+      ph.mark("read");
       if (seqs[0].empty()) break;
       if (seqs[1].size() != seqs[0].size()) {
         fprintf(stderr, "[ibwa-amd sampe] the two read files hold different numbers of reads\n");
@@ -506,6 +508,7 @@ struct Sampe {
       fprintf(stderr, "[bwa_sai2sam_pe_core] %ld sequences have been processed.\n", tot);
     }
     o.flush();
+    ph.print("ibwa-amd sampe");
     return 0;
   }
 
@@ -529,6 +532,7 @@ struct Sampe {
         }
       }
     }
+    ph.mark("sai+hit choice");
     std::vector<uint64_t> pos(hk.size());
     if (!hk.empty() && ibwa_sa2pos(ctx, (int64_t)hk.size(), hs.data(), hk.data(), hl.data(), 0, pos.data()))
       return die("sa2pos");
@@ -537,6 +541,7 @@ struct Sampe {
       p.pos = p.remapped_pos = pos[t];  // remap(): no .remap file, the hit maps to itself
       p.seQ = p.mapQ = approx_mapQ(p, max_diff_of(p)) & 0xff;
     }
+    ph.mark("sa2pos");
     // ---- insert size
     Isize ii;
     infer_isize(seqs[0], seqs[1], ii, popt.ap_prior, b.l_pac);
@@ -576,6 +581,7 @@ struct Sampe {
         }
       }
     }
+    ph.mark("isize+rows");
     pos.assign(hk.size(), 0);
     if (!hk.empty() && ibwa_sa2pos(ctx, (int64_t)hk.size(), hs.data(), hk.data(), hl.data(), 0, pos.data()))
       return die("sa2pos");
@@ -583,6 +589,7 @@ struct Sampe {
       const uint32_t k = (uint32_t)(f.first >> 32), l = (uint32_t)f.first;
       cache[f.first].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
     }
+    ph.mark("sa2pos");
     // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:226-279), pair by pair
     PosArr arr;
     int cnt_chg = 0;
@@ -639,8 +646,10 @@ struct Sampe {
       }
     }
     fprintf(stderr, "[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);
+    ph.mark("pairing");
     // ---- mate rescue (bwa_paired_sw): the drop-in over the reference's bwa_seq_t layout
     if (int rc = paired_sw(seqs, n, ii)) return rc;
+    ph.mark("paired SW");
     // ---- refine gapped alignments of both ends, MD/NM, trimmed reads; then remap()
     std::vector<Read *> rp;
     for (int j = 0; j < 2; ++j)
@@ -656,8 +665,9 @@ struct Sampe {
         }
       }
     }
+    ph.mark("refine+md");
     // ---- print
-    for (int i = 0; i < n; ++i) {
+    print_parallel(o, n, [&](Out &ob, int64_t i) {
       Read *p[2] = {&seqs[0][i], &seqs[1][i]};
       if (p[0]->bc[0] || p[1]->bc[0]) {
         strncat(p[0]->bc, p[1]->bc, sizeof p[0]->bc - strlen(p[0]->bc) - 1);
@@ -665,10 +675,10 @@ struct Sampe {
       }
       p[0]->remapped_pos = p[0]->pos;  // -R swaps pos and remapped_pos, which are equal here
       p[1]->remapped_pos = p[1]->pos;
-      print_sam1(o, b, *p[0], p[1], gopt[1].mode, gopt[1].max_top2, rg_id);
-      print_sam1(o, b, *p[1], p[0], gopt[1].mode, gopt[1].max_top2, rg_id);
-      if (o.b.size() > (1u << 20)) o.flush();
-    }
+      print_sam1(ob, b, *p[0], p[1], gopt[1].mode, gopt[1].max_top2, rg_id);
+      print_sam1(ob, b, *p[1], p[0], gopt[1].mode, gopt[1].max_top2, rg_id);
+    });
+    ph.mark("print");
     o.flush();
     last_ii = ii;
     return 0;
@@ -869,6 +879,7 @@ int sampe_main(int argc, char *argv[]) {
   head += "@PG\tID:bwa\tPN:bwa\tVN:ibwa-amd\n";
   fwrite(head.data(), 1, head.size(), out);
   Source *sp = src;
+  S.ph.mark("load index");
   const int rc = S.run(sp, out);
   for (int j = 0; j < 2; ++j) fclose(S.fp_sai[j]);
   if (out != stdout) fclose(out);

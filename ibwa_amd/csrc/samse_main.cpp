@@ -34,6 +34,7 @@ int die(const char *what) {
 template <class Reader>
 int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::string &prefix, int n_occ, FILE *out,
               const std::string &rg_line, const std::string &rg_id) {
+  Phases ph;
   Bns b;
   if (!bns_restore(prefix, b)) {
     fprintf(stderr, "[ibwa-amd samse] cannot read %s.ann / .amb / .pac\n", prefix.c_str());
@@ -57,11 +58,13 @@ int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::str
   const char *rgid = rg_id.empty() ? nullptr : rg_id.c_str();
   std::vector<ibwa_aln1_t> aln;
   long tot = 0;
+  ph.mark("load index");
   for (;;) {
     std::vector<Read> seqs;
     seqs.reserve(0x40000);
     Read r;
     while ((int)seqs.size() < 0x40000 && next_read(rd, opt.mode, opt.trim_qual, r)) seqs.push_back(std::move(r));
+    ph.mark("read");
     if (seqs.empty()) break;
     tot += (long)seqs.size();
     // ---- read alignment (bwase.c:671-682)
@@ -75,6 +78,7 @@ int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::str
       }
       aln2seq(n_aln, aln.data(), p, n_occ, rnd);
     }
+    ph.mark("sai+hit choice");
     // ---- SA -> coordinate (bwa_cal_pac_pos, bwase.c:128-165): one launch for the batch
     std::vector<uint8_t> hs;
     std::vector<uint32_t> hk, hl;
@@ -98,18 +102,19 @@ int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::str
       }
       for (Multi &q : p.multi) q.pos = pos[x++];
     }
+    ph.mark("sa2pos");
     // ---- bwa_refine_gapped (bwase.c:333-416): one global-alignment launch, MD/NM, trimmed reads
     std::vector<Read *> rp;
     for (Read &p : seqs) rp.push_back(&p);
     if (int rc = refine_gapped(ctx, b, rp)) return rc == 1 ? 1 : die("global alignment");
+    ph.mark("refine+md");
     // ---- print
-    for (Read &p : seqs) {
-      print_sam1(o, b, p, nullptr, opt.mode, opt.max_top2, rgid);
-      if (o.b.size() > (1u << 20)) o.flush();
-    }
-    o.flush();
+    print_parallel(o, (int64_t)seqs.size(),
+                   [&](Out &ob, int64_t i) { print_sam1(ob, b, seqs[i], nullptr, opt.mode, opt.max_top2, rgid); });
+    ph.mark("print");
     fprintf(stderr, "[bwa_aln_core] %ld sequences have been processed.\n", tot);
   }
+  ph.print("ibwa-amd samse");
   ibwa_ctx_destroy(ctx);
   return 0;
 }

@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""End-to-end pipeline timing and parity on the GPU box: index -> aln x2 -> sampe -R, and samse.
+
+Measures the SURVEY §8f rows built around the hot path (index builder, samse/sampe host
+pipelines with their GPU steps) on a configs[4]-shaped workload -- synthetic GRCh37-scaled genome,
+2 x 150 bp pairs at 2 % substitutions, insert N(350, 35) -- through the `ibwa-amd` CLI exactly as a
+user runs it (files in, files out, wall clock per command).  The reference's own binary
+(oracle/_ref/ibwa_ref, compiled from /root/reference by oracle/Makefile; test infrastructure) is
+timed on a bounded sample of the same pairs with the same index files, and the SAM both write for
+that sample is compared line by line (except @PG).
+
+usage: tools/pipeline_bench.py [--scale 0.1] [--pairs 1000000] [--sample 20000] [--out json]
+"""
+import argparse
+import gzip  # noqa: F401  (kept for ad-hoc inspection of outputs)
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+CLI = os.path.join(ROOT, "ibwa_amd", "bin", "ibwa-amd")
+REF = os.path.join(ROOT, "oracle", "_ref", "ibwa_ref")
+COMP = np.frombuffer(b"TGCAN", dtype=np.uint8)
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def log(*a):
+    print("[pipeline]", *a, file=sys.stderr, flush=True)
+
+
+def run(argv, stdout=None, timeout=1200):
+    t = time.perf_counter()
+    r = subprocess.run(argv, stdout=stdout, stderr=subprocess.PIPE, timeout=timeout)
+    dt = time.perf_counter() - t
+    if r.returncode != 0:
+        raise RuntimeError(f"{argv[:2]} failed ({r.returncode}): {r.stderr.decode()[-1500:]}")
+    for ln in r.stderr.decode(errors="replace").splitlines():
+        if "wall s:" in ln or "[ibwa-amd aln]" in ln:
+            log(f"  {os.path.basename(argv[0])} {argv[1]}: {ln}")
+    return dt
+
+
+def write_fasta(path, ascii_, lens):
+    with open(path, "wb") as f:
+        o = 0
+        for i, ln in enumerate(lens):
+            f.write(b">chr%d\n" % (i + 1))
+            body = ascii_[o:o + ln]
+            o += ln
+            nl = (ln + 79) // 80
+            pad = np.full(nl * 80, ord("\n"), dtype=np.uint8)
+            pad[:ln] = body
+            rows = np.concatenate([pad.reshape(nl, 80), np.full((nl, 1), ord("\n"), dtype=np.uint8)], axis=1)
+            out = rows.reshape(-1)
+            # the last row's padding newlines collapse into one line break
+            last = ln - (nl - 1) * 80
+            f.write(out[:(nl - 1) * 81 + last].tobytes() + b"\n")
+
+
+def make_pairs(ascii_, n, L, sub, seed):
+    """Fragments with insert N(350, 35) (>= L), read 1 forward at the fragment start, read 2 the
+    reverse complement of its end (ends swapped for half), i.i.d. substitutions, no N."""
+    rng = np.random.default_rng(seed)
+    G = ascii_.size
+    isn = (ascii_ != ord("A")) & (ascii_ != ord("C")) & (ascii_ != ord("G")) & (ascii_ != ord("T"))
+    cn = np.concatenate([[0], np.cumsum(isn, dtype=np.int64)])
+    r1 = np.empty((n, L), dtype=np.uint8)
+    r2 = np.empty((n, L), dtype=np.uint8)
+    got = 0
+    while got < n:
+        m = (n - got) * 2
+        ins = np.maximum(L, rng.normal(350, 35, m).astype(np.int64))
+        f = rng.integers(0, G - 1000, m)
+        ok = cn[f + ins] - cn[f] == 0
+        f, ins = f[ok][:n - got], ins[ok][:n - got]
+        k = f.size
+        idx = f[:, None] + np.arange(L)[None, :]
+        a = ascii_[idx]
+        e = ascii_[(f + ins - L)[:, None] + np.arange(L)[None, :]]
+        b = COMP[np.searchsorted(np.frombuffer(b"ACGT", dtype=np.uint8), e)][:, ::-1]
+        swap = rng.random(k) < 0.5
+        a2 = np.where(swap[:, None], b, a)
+        b2 = np.where(swap[:, None], a, b)
+        for x in (a2, b2):
+            mm = rng.random(x.shape) < sub
+            code = np.searchsorted(np.frombuffer(b"ACGT", dtype=np.uint8), x)
+            x[mm] = ACGT[(code[mm] + rng.integers(1, 4, int(mm.sum()))) & 3]
+        r1[got:got + k] = a2
+        r2[got:got + k] = b2
+        got += k
+    return r1, r2
+
+
+def write_fastq(path, reads, tag, end, first=0, count=None):
+    n, L = reads.shape
+    count = n - first if count is None else count
+    qual = b"I" * L
+    with open(path, "wb") as f:
+        chunk = 100000
+        for s in range(first, first + count, chunk):
+            e = min(first + count, s + chunk)
+            f.write(b"".join(b"@%s%d/%d\n%s\n+\n%s\n" % (tag, i, end, reads[i].tobytes(), qual) for i in range(s, e)))
+
+
+def sam_body(path):
+    with open(path, "rb") as f:
+        return [ln for ln in f.read().split(b"\n") if ln and not ln.startswith(b"@PG")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=float, default=0.1)
+    ap.add_argument("--pairs", type=int, default=1_000_000)
+    ap.add_argument("--sample", type=int, default=20000)
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--sub", type=float, default=0.02)
+    ap.add_argument("--threads", type=int, default=bench.host_threads())
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    res = {"workload": f"configs[4] shape on one GPU: {a.scale:g} x GRCh37 synthetic genome, {a.pairs} pairs "
+                       f"2 x {a.read_len} bp at {a.sub:.0%} substitutions, insert N(350, 35)",
+           "host_threads": a.threads}
+    tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+    P = os.path.join(tmp, "g")
+    den = 1_000_000
+    t = time.perf_counter()
+    ascii_, _, lens, _ = bench.make_genome(int(round(a.scale * den)), den, 5, a.threads)
+    write_fasta(P + ".fa", ascii_, lens)
+    res["genome_bp"] = int(ascii_.size)
+    log(f"genome {ascii_.size / 1e6:.0f} Mb + FASTA in {time.perf_counter() - t:.1f} s")
+    res["index_s"] = run([CLI, "index", "-p", P, P + ".fa"])
+    log(f"ibwa-amd index: {res['index_s']:.2f} s")
+    t = time.perf_counter()
+    r1, r2 = make_pairs(ascii_, a.pairs, a.read_len, a.sub, 5)
+    del ascii_
+    fq = [os.path.join(tmp, f"r{e}.fq") for e in (1, 2)]
+    write_fastq(fq[0], r1, b"p", 1)
+    write_fastq(fq[1], r2, b"p", 2)
+    sfq = [os.path.join(tmp, f"s{e}.fq") for e in (1, 2)]
+    write_fastq(sfq[0], r1, b"p", 1, 0, a.sample)
+    write_fastq(sfq[1], r2, b"p", 2, 0, a.sample)
+    log(f"{a.pairs} pairs written in {time.perf_counter() - t:.1f} s")
+    # ---- ibwa-amd over all pairs
+    sai = [os.path.join(tmp, f"r{e}.sai") for e in (1, 2)]
+    res["aln_s"] = [run([CLI, "aln", "-f", sai[e], P, fq[e]]) for e in (0, 1)]
+    res["sampe_s"] = run([CLI, "sampe", "-R", "-f", os.path.join(tmp, "pe.sam"), P, sai[0], sai[1], fq[0], fq[1]])
+    res["samse_s"] = run([CLI, "samse", "-f", os.path.join(tmp, "se.sam"), P, sai[0], fq[0]])
+    tot = sum(res["aln_s"]) + res["sampe_s"]
+    res["pairs_per_s_aln_sampe"] = a.pairs / tot
+    log(f"ibwa-amd: aln {res['aln_s'][0]:.2f} + {res['aln_s'][1]:.2f} s, sampe -R {res['sampe_s']:.2f} s, "
+        f"samse {res['samse_s']:.2f} s -> {res['pairs_per_s_aln_sampe']:.0f} pairs/s (aln x2 + sampe, files in/out)")
+    # ---- the sample: ibwa-amd and the reference, SAM compared
+    ssai = [os.path.join(tmp, f"s{e}.sai") for e in (1, 2)]
+    rsai = [os.path.join(tmp, f"rs{e}.sai") for e in (1, 2)]
+    g_aln = [run([CLI, "aln", "-f", ssai[e], P, sfq[e]]) for e in (0, 1)]
+    g_pe = run([CLI, "sampe", "-R", "-f", os.path.join(tmp, "s_pe.sam"), P, ssai[0], ssai[1], sfq[0], sfq[1]])
+    g_se = run([CLI, "samse", "-f", os.path.join(tmp, "s_se.sam"), P, ssai[0], sfq[0]])
+    r_aln = [run([REF, "aln", "-t", str(a.threads), "-f", rsai[e], P, sfq[e]]) for e in (0, 1)]
+    with open(os.path.join(tmp, "r_pe.sam"), "wb") as f:
+        r_pe = run([REF, "sampe", "-R", "-t", str(a.threads), P, rsai[0], rsai[1], sfq[0], sfq[1]], stdout=f)
+    with open(os.path.join(tmp, "r_se.sam"), "wb") as f:
+        r_se = run([REF, "samse", P, rsai[0], sfq[0]], stdout=f)
+    same_sai = all(open(ssai[e], "rb").read()[64:] == open(rsai[e], "rb").read()[64:] for e in (0, 1))
+    pe_g, pe_r = sam_body(os.path.join(tmp, "s_pe.sam")), sam_body(os.path.join(tmp, "r_pe.sam"))
+    se_g, se_r = sam_body(os.path.join(tmp, "s_se.sam")), sam_body(os.path.join(tmp, "r_se.sam"))
+    res["sample"] = {
+        "pairs": a.sample,
+        "ibwa_amd_s": {"aln": g_aln, "sampe": g_pe, "samse": g_se},
+        "reference_s": {"aln": r_aln, "sampe": r_pe, "samse": r_se, "threads": a.threads,
+                        "note": "oracle/_ref/ibwa_ref (the reference compiled from its sources); aln and sampe -t"},
+        "sai_equal": bool(same_sai),
+        "sampe_sam_lines": len(pe_g), "sampe_sam_equal": pe_g == pe_r,
+        "sampe_lines_differing": int(sum(x != y for x, y in zip(pe_g, pe_r)) + abs(len(pe_g) - len(pe_r))),
+        "samse_sam_equal": se_g == se_r,
+        "reference_pairs_per_s_aln_sampe": a.sample / (sum(r_aln) + r_pe),
+    }
+    log(f"sample {a.sample} pairs: reference aln {r_aln[0]:.2f} + {r_aln[1]:.2f} s, sampe {r_pe:.2f} s, samse {r_se:.2f} s; "
+        f".sai equal {same_sai}, sampe SAM equal {pe_g == pe_r}, samse SAM equal {se_g == se_r}")
+    line = json.dumps(res)
+    print(line)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+    subprocess.run(["rm", "-rf", tmp])
+
+
+if __name__ == "__main__":
+    main()
