@@ -50,8 +50,12 @@ struct DBuf {
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 256);
+    static const bool verbose = getenv("IBWA_VERBOSE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMalloc(&p, want);
     if (e != hipSuccess) return fail(IBWA_EHIP, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (verbose && ms > 20.0) fprintf(stderr, "[ibwa_amd] hipMalloc(%.2f GB) took %.0f ms\n", want / 1e9, ms);
     cap = want;
     return 0;
   }

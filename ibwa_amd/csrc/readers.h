@@ -2,6 +2,7 @@
 // (.gz) with kseq_read's record semantics and unaligned BAM with bwa_read_bam's selection.
 #pragma once
 #include <ctype.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -35,39 +36,106 @@ struct SeqReader {
     if (fp) gzclose(fp);
   }
   int getc_() {
-    if (begin >= end) {
-      if (eof) return -1;
-      end = gzread(fp, buf.data(), (unsigned)buf.size());
-      begin = 0;
-      if (end <= 0) { eof = true; end = 0; return -1; }
-    }
+    if (!fill()) return -1;
     return (unsigned char)buf[begin++];
   }
-  // returns seq length, -1 at EOF, -2 on a truncated quality string
+  bool fill() {
+    if (begin < end) return true;
+    if (eof) return false;
+    end = gzread(fp, buf.data(), (unsigned)buf.size());
+    begin = 0;
+    if (end <= 0) { eof = true; end = 0; return false; }
+    return true;
+  }
+  // byte classes for the sequence scan: 0 skipped (not isgraph), 1 kept, 2 ends the sequence
+  static const uint8_t *seq_class() {
+    static uint8_t t[256];
+    static bool init = false;
+    if (!init) {
+      for (int c = 0; c < 256; ++c) t[c] = isgraph(c) ? 1 : 0;
+      t[(int)'>'] = t[(int)'+'] = t[(int)'@'] = 2;
+      init = true;
+    }
+    return t;
+  }
+  // returns seq length, -1 at EOF, -2 on a truncated quality string.  Byte-for-byte the loops of
+  // kseq_read, run over the buffer in bulk (runs of kept bytes are appended at once).
   int read() {
-    int c;
-    if (last_char == 0) {
-      while ((c = getc_()) != -1 && c != '>' && c != '@') {}
-      if (c == -1) return -1;
-      last_char = c;
+    int c = -1;
+    if (last_char == 0) {  // jump to the next header line
+      for (;;) {
+        if (!fill()) return -1;
+        const char *p = buf.data() + begin, *e = buf.data() + end, *q = p;
+        while (q < e && *q != '>' && *q != '@') ++q;
+        if (q < e) { last_char = (unsigned char)*q; begin = (int)(q + 1 - buf.data()); break; }
+        begin = end;
+      }
     }
     name.clear(); seq.clear(); qual.clear();
     bool got = false;
-    while ((c = getc_()) != -1 && !isspace(c)) { name.push_back((char)c); got = true; }
-    if (c == -1 && !got) return -1;
-    if (c != '\n' && c != -1) {  // comment
-      if (keep_comment) { comment.clear(); comment_alloc = true; }
-      while ((c = getc_()) != -1 && c != '\n')
-        if (keep_comment) comment.push_back((char)c);
+    for (;;) {  // name: up to the first isspace
+      if (!fill()) { c = -1; break; }
+      const char *p = buf.data() + begin, *e = buf.data() + end, *q = p;
+      while (q < e && !isspace((unsigned char)*q)) ++q;
+      if (q > p) { name.append(p, q); got = true; }
+      if (q < e) { c = (unsigned char)*q; begin = (int)(q + 1 - buf.data()); break; }
+      begin = end;
     }
-    while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@')
-      if (isgraph(c)) seq.push_back((char)c);
+    if (c == -1 && !got) return -1;
+    if (c != '\n' && c != -1) {  // comment: the rest of the line
+      if (keep_comment) { comment.clear(); comment_alloc = true; }
+      for (;;) {
+        if (!fill()) { c = -1; break; }
+        const char *p = buf.data() + begin, *e = buf.data() + end;
+        const char *q = (const char *)memchr(p, '\n', (size_t)(e - p));
+        if (keep_comment) comment.append(p, q ? q : e);
+        if (q) { c = '\n'; begin = (int)(q + 1 - buf.data()); break; }
+        begin = end;
+      }
+    }
+    const uint8_t *cls = seq_class();
+    c = -1;
+    for (;;) {  // sequence: kept bytes up to '>', '+' or '@'
+      if (!fill()) break;
+      const unsigned char *p = (const unsigned char *)buf.data() + begin, *e = (const unsigned char *)buf.data() + end;
+      bool stop = false;
+      while (p < e) {
+        const unsigned char *q = p;
+        while (q < e && cls[*q] == 1) ++q;
+        if (q > p) seq.append((const char *)p, (const char *)q);
+        if (q == e) { p = q; break; }
+        if (cls[*q] == 2) { c = *q; p = q + 1; stop = true; break; }
+        p = q + 1;
+      }
+      begin = (int)((const char *)p - buf.data());
+      if (stop) break;
+    }
     if (c == '>' || c == '@') last_char = c;
     if (c != '+') return (int)seq.size();
-    while ((c = getc_()) != -1 && c != '\n') {}
-    if (c == -1) return -2;
-    while ((c = getc_()) != -1 && qual.size() < seq.size())
-      if (c >= 33 && c <= 127) qual.push_back((char)c);
+    for (;;) {  // the rest of the '+' line
+      if (!fill()) return -2;
+      const char *p = buf.data() + begin, *e = buf.data() + end;
+      const char *q = (const char *)memchr(p, '\n', (size_t)(e - p));
+      if (q) { begin = (int)(q + 1 - buf.data()); break; }
+      begin = end;
+    }
+    // quality: bytes 33..127 until it is as long as the sequence; like kseq, the byte read when
+    // it is full is consumed too
+    for (;;) {
+      if (!fill()) break;
+      const unsigned char *p = (const unsigned char *)buf.data() + begin, *e = (const unsigned char *)buf.data() + end;
+      bool done = false;
+      while (p < e) {
+        if (qual.size() >= seq.size()) { ++p; done = true; break; }
+        const size_t need = seq.size() - qual.size();
+        const unsigned char *q = p;
+        while (q < e && (size_t)(q - p) < need && *q >= 33 && *q <= 127) ++q;
+        if (q > p) { qual.append((const char *)p, (const char *)q); p = q; continue; }
+        ++p;  // a byte outside 33..127 is consumed and dropped
+      }
+      begin = (int)((const char *)p - buf.data());
+      if (done) break;
+    }
     last_char = 0;
     if (seq.size() != qual.size()) return -2;
     return (int)seq.size();

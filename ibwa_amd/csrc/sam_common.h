@@ -43,6 +43,13 @@ inline void parallel_chunks(int64_t n, const std::function<void(int64_t, int64_t
   for (int t = 0; t < nt; ++t) th.emplace_back(f, n * t / nt, n * (t + 1) / nt, t);
   for (auto &x : th) x.join();
 }
+// a thread joined when it goes out of scope (the next batch's parser, on every return path)
+struct Background {
+  std::thread t;
+  template <class F> void start(F &&f) { t = std::thread(std::forward<F>(f)); }
+  void wait() { if (t.joinable()) t.join(); }
+  ~Background() { wait(); }
+};
 // wall-clock seconds per named phase, printed to stderr at the end of a command
 struct Phases {
   std::vector<std::pair<const char *, double>> acc;
@@ -243,7 +250,7 @@ inline bool next_read(Reader &rd, int mode, int trim_qual, Read &p) {
   for (;;) {
     const int l = rd.read();
     if (l < 0) return false;
-    std::string s = rd.seq, q = rd.qual;
+    std::string s = std::move(rd.seq), q = std::move(rd.qual);  // the reader refills them
     if (is_64 && !q.empty())
       for (auto &ch : q) ch = (char)(ch - 31);
     if (!bam && (int)s.size() <= l_bc) continue;
@@ -259,7 +266,7 @@ inline bool next_read(Reader &rd, int mode, int trim_qual, Read &p) {
     p.seq.resize(p.full_len);
     for (int i = 0; i < p.full_len; ++i) p.seq[i] = nt4[(unsigned char)s[i]];
     if (!q.empty() || bam) {
-      p.qual = q;
+      p.qual = std::move(q);
       p.has_qual = true;
       if (trim_qual >= 1) trim_read(trim_qual, p);
     }

@@ -30,6 +30,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -490,14 +491,28 @@ struct Sampe {
   int run(Source src[2], FILE *out) {
     Out o{out, {}};
     long tot = 0;
-    for (;;) {
-      std::vector<Read> seqs[2];
-      for (int j = 0; j < 2; ++j) {
+    // batches of 0x40000 pairs (bwa_read_seq twice, bwape.c:466-468): the two files are parsed
+    // concurrently, and the next batch while this one is processed
+    std::vector<Read> seqs[2], nxt[2];
+    auto read_batch = [&]() {
+      auto rd = [&](int j) {
+        nxt[j].clear();
+        nxt[j].reserve(0x40000);
         Read r;
-        while ((int)seqs[j].size() < 0x40000 && src[j].next(r)) seqs[j].push_back(std::move(r));
-      }
-      ph.mark("read");
+        while ((int)nxt[j].size() < 0x40000 && src[j].next(r)) nxt[j].push_back(std::move(r));
+      };
+      std::thread t1(rd, 1);
+      rd(0);
+      t1.join();
+    };
+    read_batch();
+    for (;;) {
+      seqs[0].swap(nxt[0]);
+      seqs[1].swap(nxt[1]);
+      ph.mark("read (wait)");
       if (seqs[0].empty()) break;
+      Background bg;
+      bg.start(read_batch);
       if (seqs[1].size() != seqs[0].size()) {
         fprintf(stderr, "[ibwa-amd sampe] the two read files hold different numbers of reads\n");
         return 1;
@@ -592,6 +607,7 @@ struct Sampe {
     ph.mark("sa2pos");
     // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:226-279), pair by pair
     PosArr arr;
+    std::vector<std::pair<uint64_t, int>> ps;
     int cnt_chg = 0;
     const uint64_t l_pac = (uint64_t)b.l_pac;
     for (int i = 0; i < n; ++i) {
@@ -599,7 +615,9 @@ struct Sampe {
       arr.clear();
       if (popt.remapping) {
         for (int j = 0; j < 2; ++j) {
-          std::map<uint64_t, const ibwa_aln1_t *> pos2score;
+          // pos2score (filter_alignments.cpp:60-139): the lowest score seen at each distinct
+          // position; c1 / c2 count the positions whose lowest score is / is not the best
+          ps.clear();
           int min_score = INT32_MAX;
           const std::vector<ibwa_aln1_t> &ag = alns[j][i];
           for (size_t k = 0; k < ag.size(); ++k) {
@@ -615,12 +633,13 @@ struct Sampe {
               ap.pos = ap.remapped_pos = x;
               ap.idx_and_end = (uint32_t)k << 1 | (uint32_t)j;
               arr.push(ap);
-              auto ins = pos2score.insert({x, &a});
-              if (!ins.second && a.score < ins.first->second->score) ins.first->second = &a;
+              ps.push_back({x, a.score});
             }
           }
+          std::sort(ps.begin(), ps.end());
           size_t c[2] = {0, 0};
-          for (auto &kv : pos2score) ++c[kv.second->score == min_score ? 0 : 1];
+          for (size_t t = 0; t < ps.size(); ++t)
+            if (t == 0 || ps[t].first != ps[t - 1].first) ++c[ps[t].second == min_score ? 0 : 1];
           p[j]->c1 = (uint32_t)c[0] & 0xfffffffu;
           p[j]->c2 = (uint32_t)c[1] & 0xfffffffu;
           if (p[j]->c1 != 0) p[j]->type = p[j]->c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
@@ -727,16 +746,20 @@ struct Sampe {
   int paired_sw(std::vector<Read> seqs[2], int n, const Isize &ii) {
     if (!popt.is_sw || ii.avg < 0.0) return 0;
     std::vector<ibwa_ref_seq_t> ref[2];
-    std::vector<std::vector<uint8_t>> rev[2];
+    std::vector<uint8_t> rev[2];
     for (int j = 0; j < 2; ++j) {
       ref[j].assign(n, ibwa_ref_seq_t());
-      rev[j].resize(n);
+      size_t tot = 0;
+      for (int i = 0; i < n; ++i) tot += (size_t)seqs[j][i].len;
+      rev[j].resize(tot + 1);
+      size_t ro = 0;
       for (int i = 0; i < n; ++i) {
         Read &r = seqs[j][i];
         ibwa_ref_seq_t &t = ref[j][i];
         memset(&t, 0, sizeof t);
-        rev[j][i].assign(r.seq.rbegin() + (r.full_len - r.len), r.seq.rend());  // bwa_seq_t.seq: the read reversed
-        t.seq = rev[j][i].data();
+        std::reverse_copy(r.seq.begin(), r.seq.begin() + r.len, rev[j].begin() + ro);  // bwa_seq_t.seq: reversed
+        t.seq = rev[j].data() + ro;
+        ro += (size_t)r.len;
         t.rseq = r.rseq.data();
         t.len = (uint32_t)r.len;
         t.full_len = (uint32_t)r.full_len;

@@ -59,13 +59,21 @@ int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::str
   std::vector<ibwa_aln1_t> aln;
   long tot = 0;
   ph.mark("load index");
-  for (;;) {
-    std::vector<Read> seqs;
-    seqs.reserve(0x40000);
+  // batches of 0x40000 reads (bwa_read_seq); the next one is parsed while this one is processed
+  auto read_batch = [&](std::vector<Read> &v) {
+    v.clear();
+    v.reserve(0x40000);
     Read r;
-    while ((int)seqs.size() < 0x40000 && next_read(rd, opt.mode, opt.trim_qual, r)) seqs.push_back(std::move(r));
-    ph.mark("read");
+    while ((int)v.size() < 0x40000 && next_read(rd, opt.mode, opt.trim_qual, r)) v.push_back(std::move(r));
+  };
+  std::vector<Read> seqs, nxt;
+  read_batch(nxt);
+  for (;;) {
+    seqs.swap(nxt);
+    ph.mark("read (wait)");
     if (seqs.empty()) break;
+    Background bg;
+    bg.start([&] { read_batch(nxt); });
     tot += (long)seqs.size();
     // ---- read alignment (bwase.c:671-682)
     for (Read &p : seqs) {

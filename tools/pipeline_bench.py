@@ -125,6 +125,7 @@ def main():
     ap.add_argument("--sub", type=float, default=0.02)
     ap.add_argument("--threads", type=int, default=bench.host_threads())
     ap.add_argument("--out", default="")
+    ap.add_argument("--diag", action="store_true", help="only run `aln` on the sample's end 2 with IBWA_VERBOSE")
     a = ap.parse_args()
     res = {"workload": f"configs[4] shape on one GPU: {a.scale:g} x GRCh37 synthetic genome, {a.pairs} pairs "
                        f"2 x {a.read_len} bp at {a.sub:.0%} substitutions, insert N(350, 35)",
@@ -149,6 +150,15 @@ def main():
     write_fastq(sfq[0], r1, b"p", 1, 0, a.sample)
     write_fastq(sfq[1], r2, b"p", 2, 0, a.sample)
     log(f"{a.pairs} pairs written in {time.perf_counter() - t:.1f} s")
+    if a.diag:
+        env = dict(os.environ, IBWA_VERBOSE="1")
+        for e in (0, 1):
+            r = subprocess.run([CLI, "aln", "-f", os.path.join(tmp, "d.sai"), P, sfq[e]], env=env,
+                               stderr=subprocess.PIPE, timeout=600)
+            log(f"end {e + 1}:\n" + "\n".join(x for x in r.stderr.decode(errors="replace").splitlines()
+                                               if " t " in x or "wall" in x or "hipMalloc" in x))
+        subprocess.run(["rm", "-rf", tmp])
+        return
     # ---- ibwa-amd over all pairs
     sai = [os.path.join(tmp, f"r{e}.sai") for e in (1, 2)]
     res["aln_s"] = [run([CLI, "aln", "-f", sai[e], P, fq[e]]) for e in (0, 1)]
