@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "engine.h"
 #include "occ.h"
 
@@ -37,25 +39,15 @@ constexpr int EXACT_CHUNK = 512;
 //   [0] = {len | hasN << 16, kmer index strand 1, kmer index strand 0, first symbol word}
 //   [1..] = 2-bit codes of bwa_seq_t.seq, 16 per dword, position p at bits 2*(p&15) of dword p>>4
 // `first symbol word` is the dword holding position len-1-K (table used) or len-1.
-__global__ void __launch_bounds__(256) k_pack_reads(const uint8_t *__restrict__ seq, const uint64_t *__restrict__ off,
-                                                    const uint32_t *__restrict__ len, int64_t n, uint4 *__restrict__ rec,
-                                                    uint32_t stride, int K, int comp) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const int L = (int)len[r];
-  const uint8_t *s = seq + off[r];
-  uint4 *R = rec + (uint64_t)r * stride;
-  uint32_t *W = reinterpret_cast<uint32_t *>(R + 1);
+// Pack one read: its bytes from `src` (16 B chunks, `mis` bytes before the read in the first chunk),
+// the record to `R` (header) and `W` (2-bit words).  Called with LDS or global pointers.
+__device__ __forceinline__ void pack_one(const uint4 *src, int mis, int L, int K, int comp, uint4 *R, uint32_t *W) {
   const bool use_tab = K > 0 && L >= K;
   const int p0 = use_tab ? L - 1 - K : L - 1;
   uint32_t nN = 0, xa = 0, xb = 0, w = 0, first = 0;
-  // 16 B loads from the aligned-down start (the staging buffer has 16 B of tail padding):
-  // neighbouring lanes read neighbouring reads, so each line is fetched about once
-  const uint4 *q0 = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15);
-  const int mis = (int)(reinterpret_cast<uintptr_t>(s) & 15);
   const int nq = (mis + L + 15) >> 4;
   for (int q = 0; q < nq; ++q) {
-    const uint4 v = q0[q];
+    const uint4 v = src[q];
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       const uint32_t word = b < 4 ? v.x : b < 8 ? v.y : b < 12 ? v.z : v.w;
@@ -77,6 +69,58 @@ __global__ void __launch_bounds__(256) k_pack_reads(const uint8_t *__restrict__ 
   }
   const uint32_t kmask = K >= 16 ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
   R[0] = make_uint4((uint32_t)L | (nN ? 1u << 16 : 0u), use_tab ? xa & kmask : 0u, use_tab ? xb & kmask : 0u, first);
+}
+
+// One wave packs 64 consecutive reads.  When their bytes form one span of at most `in_cap` bytes
+// (reads staged back to back), the wave loads the span into LDS with coalesced 16 B loads, packs
+// from LDS into an LDS copy of its 64 records, and stores those as one contiguous block -- the
+// per-lane layout (lane i at byte 100 i) would otherwise make every load and store instruction
+// touch 64 separate lines.  Other waves read and write per lane.
+__global__ void __launch_bounds__(256) k_pack_reads(const uint8_t *__restrict__ seq, const uint64_t *__restrict__ off,
+                                                    const uint32_t *__restrict__ len, int64_t n, uint4 *__restrict__ rec,
+                                                    uint32_t stride, int K, int comp, uint32_t in_cap) {
+  extern __shared__ uint4 lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  const int nw = r0 >= n ? 0 : (int)(n - r0 < 64 ? n - r0 : 64);
+  uint4 *in = lds + (size_t)wave * (in_cap / 16 + 64 * stride);
+  uint4 *out = in + in_cap / 16;
+  const int64_t r = r0 + lane;
+  const bool act = lane < nw;
+  const uint64_t o_r = act ? off[r] : 0;
+  const int L = act ? (int)len[r] : 0;
+  uint64_t start = 0, span = 0;
+  bool fits = false;
+  if (nw > 0) {
+    start = off[r0] & ~(uint64_t)15;
+    const uint64_t last = off[r0 + nw - 1] + len[r0 + nw - 1];
+    span = ((last + 15) & ~(uint64_t)15) - start;
+    const bool inside = !act || (o_r >= start && o_r + (uint64_t)L <= start + span);
+    fits = span <= in_cap && __all(inside);
+  }
+  if (fits) {
+    const uint4 *g = reinterpret_cast<const uint4 *>(seq + start);
+    for (uint32_t c = lane; c < span / 16; c += 64) in[c] = g[c];
+  }
+  __syncthreads();
+  if (act) {
+    if (fits) {
+      const uint64_t o = o_r - start;
+      pack_one(in + (o >> 4), (int)(o & 15), L, K, comp, out + (size_t)lane * stride,
+               reinterpret_cast<uint32_t *>(out + (size_t)lane * stride + 1));
+    } else {
+      // 16 B loads from the aligned-down start (the staging buffer has 16 B of tail padding)
+      const uint8_t *sp = seq + o_r;
+      const uint4 *q0 = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(sp) & ~(uintptr_t)15);
+      uint4 *R = rec + (uint64_t)r * stride;
+      pack_one(q0, (int)(reinterpret_cast<uintptr_t>(sp) & 15), L, K, comp, R, reinterpret_cast<uint32_t *>(R + 1));
+    }
+  }
+  __syncthreads();
+  if (fits) {
+    uint4 *dst = rec + (uint64_t)r0 * stride;
+    for (uint32_t c = lane; c < (uint32_t)nw * stride; c += 64) dst[c] = out[c];
+  }
 }
 
 // bit-plane rank query (occ64.hip): {C[c], 0, P_lo[c], P_hi[c]} of the 64-row block of `row`
@@ -297,8 +341,12 @@ hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1
                         int blocks, hipEvent_t ev_mid, const uint32_t *const jump[6], hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   const int comp = (a.o.mode & MODE_COMPREAD) ? 1 : 0;
-  hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a.seq, a.off, a.len, a.n,
-                     rec, stride, K, comp);
+  // LDS per wave: the span of 64 back-to-back reads of the batch's longest length, and 64 records
+  uint32_t in_cap = (uint32_t)(((uint64_t)64 * std::max<uint32_t>(a.wlen1 - 1, 1) + 32 + 15) & ~15ull);
+  if ((size_t)4 * (in_cap + 64 * stride * 16) > 64 * 1024) in_cap = 0;  // long reads: per-lane loads
+  const size_t lds = (size_t)4 * (in_cap + 64 * stride * 16);
+  hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)((a.n + 255) / 256)), dim3(256), lds, st, a.seq, a.off, a.len, a.n,
+                     rec, stride, K, comp, in_cap);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
