@@ -77,6 +77,8 @@ struct GapArgs {
   uint32_t *iters;           // optional: loop iterations per read (diagnostics)
   unsigned long long *prof;  // optional: per-phase cycle counters [8] (diagnostics kernel)
   uint32_t max_iters;        // iteration budget per read (0: none); over it -> ST_HEAVY
+  uint32_t early_iters;      // early hand-off: past this many iterations (0: off) a read whose
+  uint32_t early_entries;    //   stack holds more than early_entries entries -> ST_HEAVY
   int lanes_per_wave;        // reads a wave runs at once (64; 1 for heavy reads)
   int free_depth;            // LDS free-slot stack per read (wide kernel)
   AlnOpt o;

@@ -119,6 +119,9 @@ struct ibwa_ctx {
   int gap_pages_per_block = 384;      // 128 KiB pages per 256-lane workgroup pool
   uint32_t gap_hit_slots = 256;      // hits a read may hold in the first pass
   int64_t gap_reads_per_chunk = 1 << 22;
+  // early hand-off to the coop pass: a read past 3000 iterations whose stack holds > 1000 entries
+  // (swept at 10M reads: 2.28 -> 2.14 s per step; budget 6000-16000 with it: within noise)
+  uint32_t gap_early_iters = 3000, gap_early_entries = 1000;
   uint32_t gap_iter_budget = 8000;   // first-pass iterations per read before handing it to the coop pass (swept 1000-8000 at 50M reads: 8000 best)
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
@@ -283,6 +286,8 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_hit_slots" && value >= 1 && value <= 4096) c->gap_hit_slots = (uint32_t)value;
   else if (k == "gap_reads_per_chunk" && value > 0) c->gap_reads_per_chunk = value;
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
+  else if (k == "gap_early_iters" && value >= 0) c->gap_early_iters = (uint32_t)value;
+  else if (k == "gap_early_entries" && value >= 0) c->gap_early_entries = (uint32_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
@@ -775,6 +780,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.n_aln = c->d_naln.as<int32_t>() + b0;
       G.status = c->d_status.as<uint32_t>() + b0;
       G.max_iters = c->gap_iter_budget;
+      G.early_iters = c->gap_early_iters;
+      G.early_entries = c->gap_early_entries;
       if (c->verbose) {
         if (int rc = c->d_iters.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
         G.iters = c->d_iters.as<uint32_t>() + b0;

@@ -378,7 +378,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     // ------------------------------------------------ decide this iteration's work
     // search lanes pop C; exact lanes advance one symbol
     bool do_pop = false, finish = false;
-    if (A.max_iters && n_iter > A.max_iters && (st == 1 || st == 2)) {
+    if (((A.max_iters && n_iter > A.max_iters) ||
+         (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries)) &&
+        (st == 1 || st == 2)) {
       status |= ST_HEAVY;  // a long search: the retry pass re-runs it from the start
       st = 1;
       n_entries = 0;
