@@ -59,7 +59,7 @@ namespace {
 
 constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_NONSTOP = 0x10;
 constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
-constexpr int RREC = 256;            // chain records in flight (ring)
+constexpr int RREC = 128;            // chain records in flight (ring)
 constexpr int MAXP = COOP_MAXP;      // pages per bucket
 constexpr int NSTK = COOP_NSTK;      // buckets
 constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -134,22 +134,33 @@ struct Shm {
   uint4 recB[RREC];   // hit: {k, l, n_mm | n_gapo << 8 | n_gape << 16 | a << 24, ldp}
   uint32_t dirc[4][MAXP];  // page ids of the level's bucket and of its (up to) three target buckets
   uint32_t nb[NSTK];       // entries per bucket
-  uint32_t np[NSTK];       // pages per bucket
-  uint2 W[2][COOP_MAXLEN + 1];   // width arrays {w, bid} of strands 0 / 1 (bwt_width_t)
-  uint2 SW[2][COOP_SEEDMAX + 1];  // seed width arrays
-  uint8_t str[2][COOP_MAXLEN];   // strand 0 = bwa_seq_t.seq, strand 1 = complement (COMPREAD)
+  uint16_t np[NSTK];       // pages per bucket (<= MAXP)
+  // width arrays (bwt_width_t {w, bid}) of strands 0 / 1 and the seed widths, split so that the
+  // bids (<= COOP_MAXLEN + 1) take 16 bits: with the 128-record ring the wave's LDS fits 12 waves
+  // per CU
+  uint32_t Ww[2][COOP_MAXLEN + 1];
+  uint32_t SWw[2][COOP_SEEDMAX + 1];
+  uint16_t Wb[2][COOP_MAXLEN + 2];
+  uint16_t SWb[2][COOP_SEEDMAX + 1];
+  uint8_t str[COOP_MAXLEN];      // bwa_seq_t.seq; strand 1 reads it complemented (COMPREAD)
   uint32_t head[64];             // per-lane staging ring: first uncommitted slot
   uint32_t rb[64];               // per-lane staging rollback point (discarded chains)
 };
 
 }  // namespace
 
-__global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *counter) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_coop(CoopArgs A,
+                                                                                     unsigned long long *counter) {
   __shared__ Shm S;
   const int lane = threadIdx.x;
   const uint64_t wave = blockIdx.x;
   const AlnOpt o = A.o;
   const bool comp = o.mode & MODE_COMPREAD;
+  // read symbol x of strand a: strand 1 is the complement under COMPREAD
+  auto sym_of = [&](int a, int x) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t c = S.str[x];
+    return a && comp && c < 4 ? 3u - c : c;
+  };
   const bool gape = o.mode & MODE_GAPE;
   const IndexView ixv0 = A.ix[0], ixv1 = A.ix[1];
   uint4 *const stg_base = A.stg + ((wave * 64) << A.stg_log2);
@@ -208,17 +219,18 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
       const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
       for (int j = lane; j < len; j += 64) {
         const uint32_t c = sq[j];
-        S.str[0][j] = (uint8_t)c;
-        S.str[1][j] = (uint8_t)(comp && c < 4 ? 3u - c : c);
+        S.str[j] = (uint8_t)c;
       }
       for (int j = lane; j <= len; j += 64) {
-        S.W[0][j] = wb[j];
-        S.W[1][j] = wb[A.wlen1 + j];
+        const uint2 w0 = wb[j], w1 = wb[A.wlen1 + j];
+        S.Ww[0][j] = w0.x; S.Wb[0][j] = (uint16_t)w0.y;
+        S.Ww[1][j] = w1.x; S.Wb[1][j] = (uint16_t)w1.y;
       }
       if (seeded)
         for (int j = lane; j <= o.seed_len; j += 64) {
-          S.SW[0][j] = wb[2 * A.wlen1 + j];
-          S.SW[1][j] = wb[2 * A.wlen1 + o.seed_len + 1 + j];
+          const uint2 w0 = wb[2 * A.wlen1 + j], w1 = wb[2 * A.wlen1 + o.seed_len + 1 + j];
+          S.SWw[0][j] = w0.x; S.SWb[0][j] = (uint16_t)w0.y;
+          S.SWw[1][j] = w1.x; S.SWb[1][j] = (uint16_t)w1.y;
         }
       for (int b = lane; b < NSTK; b += 64) {
         S.nb[b] = 0;
@@ -300,13 +312,13 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
           int m = max_diff - (e_mm + e_go);
           if (gape) m -= e_ge;
           if (m < 0) { end_chain(false, 0, 0); return; }                                  // :147
-          if (i > 0 && m < (int)S.W[a][i - 1].y) { end_chain(false, 0, 0); return; }      // :155
+          if (i > 0 && m < (int)S.Wb[a][i - 1]) { end_chain(false, 0, 0); return; }      // :155
           if (i == 0) { end_chain(true, k, l); return; }                                   // :159
           if (m == 0 && (state == STATE_M || gape || e_ge == o.max_gape)) {              // :160
             xj = i - 1;
             xk = k;
             xl = l;
-            if (S.str[a][xj] > 3) { end_chain(false, 0, 0); return; }
+            if (sym_of(a, xj) > 3) { end_chain(false, 0, 0); return; }
             lst = L_TAIL;
             return;
           }
@@ -504,16 +516,17 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
                 uint32_t jrun = 0;
                 for (int base = 0; base < h_ldp; base += 64) {
                   const int q = base + lane;
-                  uint2 w = q < h_ldp ? S.W[h_a][q] : make_uint2(0, 0);
+                  uint2 w = q < h_ldp ? make_uint2(S.Ww[h_a][q], S.Wb[h_a][q]) : make_uint2(0, 0);
                   const bool eq = q < h_ldp && w.x == x;
                   const unsigned long long em = __ballot(eq);
                   if (q < h_ldp) {
                     if (w.x > x) {
                       w.x -= x;
-                      S.W[h_a][q] = w;
+                      S.Ww[h_a][q] = w.x;
                     } else if (eq) {
                       const uint32_t jj = jrun + (uint32_t)__popcll(em & ((1ull << lane) - 1ull)) + 1u;
-                      S.W[h_a][q] = make_uint2(mx - jj, 1u);
+                      S.Ww[h_a][q] = mx - jj;
+                      S.Wb[h_a][q] = 1u;
                     }
                   }
                   jrun += (uint32_t)__popcll(em);
@@ -567,7 +580,7 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
           Blk bk, bl;
           load_blk(ob, ql, exp, bl);
           load_blk(ob, qk - 1, exp && !qkneg && !qshare, bk);
-          const uint32_t tsym = tail ? S.str[a][xj] : 0u;
+          const uint32_t tsym = tail ? sym_of(a, xj) : 0u;
           uint4 tvl = make_uint4(0, 0, 0, 0), tvk = make_uint4(0, 0, 0, 0);
           if (tail) tvl = ob[(size_t)(ql >> 6) * 4 + tsym];
           if (tail && !qkneg && !qshare) tvk = ob[(size_t)((qk - 1) >> 6) * 4 + tsym];
@@ -595,7 +608,7 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
               end_chain(false, 0, 0);
             } else if (--xj < 0) {
               end_chain(true, xk, xl);
-            } else if (S.str[a][xj] > 3) {
+            } else if (sym_of(a, xj) > 3) {
               end_chain(false, 0, 0);
             }
           } else if (exp) {
@@ -618,16 +631,18 @@ __global__ void __launch_bounds__(64) k_coop(CoopArgs A, unsigned long long *cou
               if (gape) m_seed -= e_ge;
             }
             const int ni = i - 1;
-            const uint32_t csym = S.str[a][ni];
+            const uint32_t csym = sym_of(a, ni);
             const uint32_t occ = l - k + 1;
             bool allow_diff = true, allow_M = true;
             if (ni > 0) {
-              const uint2 w_im2 = S.W[a][ni - 1], w_im1 = S.W[a][ni];
+              const uint2 w_im2 = make_uint2(S.Ww[a][ni - 1], S.Wb[a][ni - 1]),
+                          w_im1 = make_uint2(S.Ww[a][ni], S.Wb[a][ni]);
               if ((int)w_im2.y > m - 1) allow_diff = false;
               else if ((int)w_im2.y == m - 1 && (int)w_im1.y == m - 1 && w_im2.x == w_im1.x) allow_M = false;
               const int ii = ni - (len - o.seed_len);
               if (seeded && ii > 0) {
-                const uint2 sw_lo = S.SW[a][ii - 1], sw_hi = S.SW[a][ii];
+                const uint2 sw_lo = make_uint2(S.SWw[a][ii - 1], S.SWb[a][ii - 1]),
+                            sw_hi = make_uint2(S.SWw[a][ii], S.SWb[a][ii]);
                 if ((int)sw_lo.y > m_seed - 1) allow_diff = false;
                 else if ((int)sw_lo.y == m_seed - 1 && (int)sw_hi.y == m_seed - 1 && sw_lo.x == sw_hi.x) allow_M = false;
               }

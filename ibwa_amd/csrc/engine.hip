@@ -126,7 +126,7 @@ struct ibwa_ctx {
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
   int gap_coop = 1;
-  int coop_waves_per_cu = 8;         // 19.3 KiB of LDS and 173 VGPRs per wave (2 waves per SIMD)
+  int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
   int coop_pool_gb = 16;             // bucket page pool
   DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next;
   bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
