@@ -235,6 +235,15 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   int xj = 0, xa = 0;
   uint4 xe = make_uint4(0, 0, 0, 0);  // the entry that went down the exact path
 
+  // The per-read argument pointers are re-read from the kernel-argument segment where they are used
+  // (read claim, read end) instead of staying live in SGPRs through the loop, where the compiler
+  // spilled them into VGPR lanes and read them back in the hot path.
+  typedef const __attribute__((address_space(4))) GapArgs KArgs;
+  auto args = [&]() __attribute__((always_inline)) -> KArgs * {
+    KArgs *p = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();  // A is the first kernel argument
+    asm volatile("" : "+s"(p));
+    return p;
+  };
   auto slot_ptr = [&](uint32_t slot) __attribute__((always_inline)) -> uint4 * {
     if (slot < P0) return ent1 + slot;
     const uint32_t q = (slot - P0) >> LG;
@@ -254,19 +263,20 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   auto end_read = [&](uint32_t stat) __attribute__((always_inline)) {
     const bool pl_ = pleader();
     int na = stat ? 0 : n_aln;
+    KArgs *ka = args();
     if (na) {
-      const unsigned long long pos = atomicAdd(A.aln_next, (unsigned long long)na);
-      if (pos + (unsigned long long)na > A.aln_total) {
+      const unsigned long long pos = atomicAdd(ka->aln_next, (unsigned long long)na);
+      if (pos + (unsigned long long)na > ka->aln_total) {
         stat |= ST_ALN_OVERFLOW;
         na = 0;
       } else {
-        for (int j = 0; j < na; ++j) A.aln[pos + j] = ent1[P0 - 1 - j];
-        A.aln_off[ro] = pos;
+        for (int j = 0; j < na; ++j) ka->aln[pos + j] = ent1[P0 - 1 - j];
+        ka->aln_off[ro] = pos;
       }
     }
-    A.n_aln[ro] = na;
-    A.status[ro] = stat;
-    if (A.iters) A.iters[ro] = n_iter;
+    ka->n_aln[ro] = na;
+    ka->status[ro] = stat;
+    if (ka->iters) ka->iters[ro] = n_iter;
     for (uint32_t q = 0; q < n_pages; ++q) {
       const uint32_t pg = ptab[((q) << nbl) + ltid];
       atomicAnd(&bitmap[pg >> 5], ~(1u << (pg & 31)));
@@ -300,26 +310,27 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       if (st == 0 && rank < avail) {
         if (pleader()) ++pf10;
         r = cur + rank;
-        const int64_t rr = A.ids ? A.ids[r] : r;
-        ro = A.out_by_id ? rr : r;
-        len = (int)A.len[rr];
-        s = A.seq + A.off[rr];
-        opt_max_diff = o.fnr_pos ? (int)A.maxdiff_tab[len] : o.max_diff;
+        KArgs *ka = args();
+        const int64_t rr = ka->ids ? ka->ids[r] : r;
+        ro = ka->out_by_id ? rr : r;
+        len = (int)ka->len[rr];
+        s = ka->seq + ka->off[rr];
+        opt_max_diff = o.fnr_pos ? (int)ka->maxdiff_tab[len] : o.max_diff;
         max_diff = opt_max_diff;
         best_score = (opt_max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape;
         best_cnt = 0;
         n_aln = 0;
         status = 0;
         seeded = len > o.seed_len;
-        const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
+        const uint2 *wb = ka->wbuf + (uint64_t)r * ka->wstride;
         W0 = wb;
-        W1 = wb + A.wlen1;
-        SW0 = wb + 2 * A.wlen1;
+        W1 = wb + ka->wlen1;
+        SW0 = wb + 2 * ka->wlen1;
         SW1 = SW0 + (o.seed_len + 1);
-        const int nN = (int)A.nN[r];
+        const int nN = (int)ka->nN[r];
         if (nN > max_diff) {  // bwtgap.c:116-122
-          A.n_aln[ro] = 0;
-          A.status[ro] = 0;
+          ka->n_aln[ro] = 0;
+          ka->status[ro] = 0;
         } else {
           fastrd = !WIDE && nN == 0 && len <= 16 * RDW;
           if (fastrd) {
