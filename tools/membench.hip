@@ -28,7 +28,11 @@ __device__ __forceinline__ uint64_t mix(uint64_t x) {
 }
 
 // CHAINS independent reads in flight per lane; each read is S bytes (S/4 dwords)
-template <int S, int CHAINS>
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+// NT: non-temporal loads (global_load ... nt), to see whether the L2 then asks the fabric for
+// less than a 128 B line per random read
+template <int S, int CHAINS, bool NT = false>
 __global__ void __launch_bounds__(256) k_rand(const uint32_t *__restrict__ t, uint64_t n_slots, int iters,
                                               uint32_t *__restrict__ out) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -50,8 +54,13 @@ __global__ void __launch_bounds__(256) k_rand(const uint32_t *__restrict__ t, ui
       } else {
 #pragma unroll
         for (int q = 0; q < S / 16; ++q) {
-          uint4 a = reinterpret_cast<const uint4 *>(p)[q];
-          x ^= a.x ^ a.y ^ a.z ^ a.w;
+          if constexpr (NT) {
+            const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p) + q);
+            x ^= a.x ^ a.y ^ a.z ^ a.w;
+          } else {
+            uint4 a = reinterpret_cast<const uint4 *>(p)[q];
+            x ^= a.x ^ a.y ^ a.z ^ a.w;
+          }
         }
       }
       v[c] = x;
@@ -65,21 +74,21 @@ __global__ void __launch_bounds__(256) k_rand(const uint32_t *__restrict__ t, ui
   if (acc == 0x12345678u) out[tid] = acc;
 }
 
-template <int S, int CHAINS>
+template <int S, int CHAINS, bool NT = false>
 void run(const uint32_t *t, uint64_t bytes, int iters, uint32_t *out, int blocks) {
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
   uint64_t n_slots = bytes / S;
-  hipLaunchKernelGGL((k_rand<S, CHAINS>), dim3(blocks), dim3(256), 0, 0, t, n_slots, 4, out);  // warm
+  hipLaunchKernelGGL((k_rand<S, CHAINS, NT>), dim3(blocks), dim3(256), 0, 0, t, n_slots, 4, out);  // warm
   CHK(hipEventRecord(a));
-  hipLaunchKernelGGL((k_rand<S, CHAINS>), dim3(blocks), dim3(256), 0, 0, t, n_slots, iters, out);
+  hipLaunchKernelGGL((k_rand<S, CHAINS, NT>), dim3(blocks), dim3(256), 0, 0, t, n_slots, iters, out);
   CHK(hipEventRecord(b));
   CHK(hipEventSynchronize(b));
   float ms;
   CHK(hipEventElapsedTime(&ms, a, b));
   double reads = (double)blocks * 256 * CHAINS * iters;
-  printf("{\"bytes\": %d, \"chains\": %d, \"blocks\": %d, \"ms\": %.3f, \"Greads_s\": %.2f, \"useful_GBs\": %.1f}\n", S,
+  printf("{\"nt\": %d, \"bytes\": %d, \"chains\": %d, \"blocks\": %d, \"ms\": %.3f, \"Greads_s\": %.2f, \"useful_GBs\": %.1f}\n", (int)NT, S,
          CHAINS, blocks, ms, reads / ms / 1e6, reads * S / ms / 1e6);
   fflush(stdout);
 }
@@ -87,6 +96,7 @@ void run(const uint32_t *t, uint64_t bytes, int iters, uint32_t *out, int blocks
 int main(int argc, char **argv) {
   double gib = argc > 1 ? atof(argv[1]) : 2.0;
   int iters = argc > 2 ? atoi(argv[2]) : 200;
+  const bool nt_only = argc > 3 && argv[3][0] == 'n';
   uint64_t bytes = (uint64_t)(gib * (1ull << 30));
   uint32_t *t, *out;
   CHK(hipMalloc(&t, bytes));
@@ -95,6 +105,15 @@ int main(int argc, char **argv) {
   CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   int blocks = cus * 8;
   CHK(hipMalloc(&out, (size_t)blocks * 256 * 4));
+  if (nt_only) {  // one kernel per run, for PMC passes
+    if (argv[3][1] == 't') run<16, 4, true>(t, bytes, iters, out, blocks);
+    else run<16, 4, false>(t, bytes, iters, out, blocks);
+    CHK(hipFree(t));
+    CHK(hipFree(out));
+    return 0;
+  }
+  run<16, 4, true>(t, bytes, iters, out, blocks);
+  run<64, 4, true>(t, bytes, iters, out, blocks);
   run<4, 2>(t, bytes, iters, out, blocks);
   run<8, 2>(t, bytes, iters, out, blocks);
   run<16, 2>(t, bytes, iters, out, blocks);
