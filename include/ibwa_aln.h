@@ -137,7 +137,11 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "gapped_v2" (0/1, default 1)   persistent gapped-search kernel (else the general kernels)
  *   "gap_cap1", "gap_pages_per_block", "gap_hit_slots", "gap_blocks_per_cu", "gap_reads_per_chunk"
  *                                  its per-lane static slots, 128 KiB pages per workgroup pool,
- *                                  first-pass hit slots, residency and batch slice size */
+ *                                  first-pass hit slots, residency and batch slice size
+ *   "gap_iter_budget" (8000)       first-pass iterations before a read goes to the cooperative pass
+ *   "gap_early_iters", "gap_early_entries" (3000, 1000)
+ *                                  earlier hand-off of a read whose stack holds that many entries
+ *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
 /* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */
