@@ -24,7 +24,7 @@ def _body(text):
 def test_sampe_matches_reference(golden_dir, key, tmp_path):
     m = MANIFEST[key]
     out = tmp_path / "out.sam"
-    r = subprocess.run([CLI, "sampe"] + m["argv"] + ["-f", str(out), os.path.join(golden_dir, "g1m"),
+    r = subprocess.run([CLI, "sampe"] + m["argv"] + ["-f", str(out), os.path.join(golden_dir, m.get("prefix", "g1m")),
                                                      *[os.path.join(golden_dir, x) for x in m["sai"]],
                                                      *[os.path.join(golden_dir, x) for x in m["reads"]]],
                        capture_output=True, text=True, timeout=120)
@@ -44,14 +44,14 @@ def test_sampe_rejects_several_databases(golden_dir):
     assert r.returncode != 0 and "databases" in r.stderr
 
 
-@pytest.mark.parametrize("key", ["pe100.default", "pe100.q20", "pe100.k0n3", "pe150.default"])
+@pytest.mark.parametrize("key", ["pe100.default", "pe100.q20", "pe100.k0n3", "pe150.default", "tandem.R"])
 def test_aln_pe_reads_match_reference_sai(golden_dir, key, tmp_path):
     """`ibwa-amd aln` on each end of the paired fixtures writes the reference's .sai bytes."""
     import oracle
     m = MANIFEST[key]
     for sai, reads in zip(m["sai"], m["reads"]):
         out = tmp_path / "out.sai"
-        r = subprocess.run([CLI, "aln"] + m["aln_argv"] + ["-f", str(out), os.path.join(golden_dir, "g1m"),
+        r = subprocess.run([CLI, "aln"] + m["aln_argv"] + ["-f", str(out), os.path.join(golden_dir, m.get("prefix", "g1m")),
                                                            os.path.join(golden_dir, reads)],
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-2000:]

@@ -132,6 +132,76 @@ def write_fq(path, name, recs, suffix):
             f.write(f"@{name}{i}/{suffix}\n{s}\n+\n{q}\n")
 
 
+def tandem_case():
+    """A 160 kb genome holding a 60 kb tandem array of a 50 bp unit (1 200 exact copies, except every
+    100th copy with one substitution) between random sequence, indexed by the reference; pairs from inside the array
+    (SA intervals of > 1 000 rows: the bwtcache path, position arrays of thousands of entries sorted
+    by the restated introsort with ties across the two ends), pairs across its edges, and
+    consecutive duplicate pairs (find_optimal_pair's look-ahead into the previous pair's array)."""
+    rng = random.Random(21)
+    unit = "".join(rng.choice("ACGT") for _ in range(50))
+    arr = []
+    for c in range(1200):
+        u = list(unit)
+        if c % 100 == 99:
+            k = rng.randrange(50)
+            u[k] = rng.choice([b for b in "ACGT" if b != u[k]])
+        arr.append("".join(u))
+    left = "".join(rng.choice("ACGT") for _ in range(50000))
+    right = "".join(rng.choice("ACGT") for _ in range(50000))
+    g = left + "".join(arr) + right
+    with open(os.path.join(GOLD, "tandem.fa"), "w") as f:
+        f.write(">tr1 tandem array\n")
+        for i in range(0, len(g), 70):
+            f.write(g[i:i + 70] + "\n")
+    subprocess.run([REF, "index", "-p", os.path.join(GOLD, "tandem"), os.path.join(GOLD, "tandem.fa")], check=True,
+                   capture_output=True)
+    L = 100
+    r1s, r2s = [], []
+    while len(r1s) < 400:
+        ins = max(L + 10, int(rng.gauss(300, 30)))
+        kind = len(r1s) % 4
+        if kind == 0 or kind == 1:  # inside the array
+            f0 = rng.randrange(50000, 50000 + 60000 - ins)
+        elif kind == 2:  # across an edge of the array
+            f0 = rng.choice([50000 - rng.randrange(0, ins), 110000 - rng.randrange(0, ins)])
+        else:  # unique flanks
+            f0 = rng.choice([rng.randrange(0, 45000), rng.randrange(112000, len(g) - ins)])
+        seg = g[f0:f0 + ins]
+        a, b = mutate(rng, seg[:L], 0.01), mutate(rng, rc(seg[-L:]), 0.01)
+        if len(a) != L or len(b) != L:
+            continue
+        if rng.random() < 0.5:
+            a, b = b, a
+        q = "I" * L
+        r1s.append((a, q))
+        r2s.append((b, q))
+        if rng.random() < 0.15:  # a duplicate pair right after it
+            r1s.append((a, q))
+            r2s.append((b, q))
+    write_fq(os.path.join(GOLD, "tandem_1.fq"), "td_", r1s, 1)
+    write_fq(os.path.join(GOLD, "tandem_2.fq"), "td_", r2s, 2)
+    prefix = os.path.join(GOLD, "tandem")
+    out = {}
+    for key, argv in (("tandem.R", ["-R"]), ("tandem.R.n2000", ["-R", "-n", "2000", "-N", "3000"])):
+        sai = []
+        for end in (1, 2):
+            fn = f"tandem_{end}.sai"
+            subprocess.run([REF, "aln", "-f", os.path.join(GOLD, fn), prefix, os.path.join(GOLD, f"tandem_{end}.fq")],
+                           check=True, capture_output=True)
+            sai.append(fn)
+        res = subprocess.run([REF, "sampe"] + argv + [prefix] + [os.path.join(GOLD, x) for x in sai] +
+                             [os.path.join(GOLD, "tandem_1.fq"), os.path.join(GOLD, "tandem_2.fq")],
+                             check=True, capture_output=True)
+        with open(os.path.join(GOLD, f"sampe_{key}.sam.gz"), "wb") as raw:
+            with gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:
+                f.write(res.stdout)
+        out[key] = {"prefix": "tandem", "sai": sai, "reads": ["tandem_1.fq", "tandem_2.fq"], "aln_argv": [],
+                    "argv": argv, "sam": f"sampe_{key}.sam.gz"}
+        print(key, len(res.stdout.splitlines()), "lines")
+    return out
+
+
 def main():
     genome, names, lens = golden_genome_ascii()
     starts = [0]
@@ -163,6 +233,7 @@ def main():
         manifest[key] = {"sai": sai, "reads": [f"{rs}_1.fq", f"{rs}_2.fq"], "aln_argv": aln_argv,
                          "argv": sampe_argv, "sam": f"sampe_{key}.sam.gz"}
         print(key, len(out.stdout.splitlines()), "lines")
+    manifest.update(tandem_case())
     with open(os.path.join(GOLD, "sampe_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
 
