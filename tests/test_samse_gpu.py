@@ -24,7 +24,7 @@ def _body(text):
 def test_samse_matches_reference(golden_dir, key, tmp_path):
     m = MANIFEST[key]
     out = tmp_path / "out.sam"
-    r = subprocess.run([CLI, "samse"] + m["argv"] + ["-f", str(out), os.path.join(golden_dir, "g1m"),
+    r = subprocess.run([CLI, "samse"] + m["argv"] + ["-f", str(out), os.path.join(golden_dir, m.get("prefix", "g1m")),
                                                      os.path.join(golden_dir, m["sai"]),
                                                      os.path.join(golden_dir, m["reads"])],
                        capture_output=True, text=True, timeout=120)

@@ -34,19 +34,23 @@ CASES = {
     "illumina.I": ("illumina.I.sai", "reads_illumina.fq", []),
     "bam.all": ("bam.all.sai", "reads.bam", []),
     "bam.q15": ("bam.q15.sai", "reads.bam", []),
+    # tandem-array genome (tools/make_sampe_golden.py): > 1000 equal hits, XA with -n 2000
+    "tandem.default": ("tandem_1.sai", "tandem_1.fq", [], "tandem"),
+    "tandem.n2000": ("tandem_1.sai", "tandem_1.fq", ["-n", "2000"], "tandem"),
 }
 
 
 def main():
     manifest = {}
-    for key, (sai, reads, argv) in CASES.items():
-        out = subprocess.run([REF, "samse"] + argv + [os.path.join(GOLD, "g1m"), os.path.join(GOLD, sai),
+    for key, (sai, reads, argv, *pre) in CASES.items():
+        prefix = pre[0] if pre else "g1m"
+        out = subprocess.run([REF, "samse"] + argv + [os.path.join(GOLD, prefix), os.path.join(GOLD, sai),
                                                       os.path.join(GOLD, reads)],
                              check=True, capture_output=True).stdout
         with open(os.path.join(GOLD, f"samse_{key}.sam.gz"), "wb") as raw:
             with gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:
                 f.write(out)
-        manifest[key] = {"sai": sai, "reads": reads, "argv": argv, "sam": f"samse_{key}.sam.gz"}
+        manifest[key] = {"prefix": prefix, "sai": sai, "reads": reads, "argv": argv, "sam": f"samse_{key}.sam.gz"}
         print(key, len(out.splitlines()), "lines")
     with open(os.path.join(GOLD, "samse_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
