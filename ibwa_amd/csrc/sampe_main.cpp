@@ -26,8 +26,6 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <functional>
-#include <map>
 #include <memory>
 #include <string>
 #include <thread>
