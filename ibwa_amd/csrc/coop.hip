@@ -59,7 +59,7 @@ namespace {
 
 constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_NONSTOP = 0x10;
 constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
-constexpr int RREC = 128;            // chain records in flight (ring)
+constexpr int RREC = COOP_RREC;      // chain records in flight (ring)
 constexpr int MAXP = COOP_MAXP;      // pages per bucket
 constexpr int NSTK = COOP_NSTK;      // buckets
 constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -131,7 +131,6 @@ __device__ __forceinline__ uint4 mk_ent(uint32_t k, uint32_t l, int i, int ldp, 
 struct Shm {
   uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | lane << 16 | hit << 24,
                       //  done (1) | children staged before the chain's last pop << 1}
-  uint4 recB[RREC];   // hit: {k, l, n_mm | n_gapo << 8 | n_gape << 16 | a << 24, ldp}
   uint32_t dirc[4][MAXP];  // page ids of the level's bucket and of its (up to) three target buckets
   uint32_t nb[NSTK];       // entries per bucket
   uint16_t np[NSTK];       // pages per bucket (<= MAXP)
@@ -298,9 +297,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         // end the lane's chain: its record (hit or not) goes to the reorder buffer
         auto end_chain = [&](bool hit, uint32_t hk, uint32_t hl) __attribute__((always_inline)) {
           const uint32_t slot = c & (RREC - 1);
-          S.recB[slot] = make_uint4(hk, hl,
-                                    (uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
-                                    (uint32_t)ldp);
+          if (hit) {  // the hit record {k, l, n_mm | n_gapo << 8 | n_gape << 16 | a << 24, ldp}: global,
+                      // agent-scope (L2) accesses, read once by the whole wave at the barrier
+            uint32_t *hr = reinterpret_cast<uint32_t *>(A.recb + wave * RREC + slot);
+            __hip_atomic_store(hr + 0, hk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(hr + 1, hl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(hr + 2, (uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(hr + 3, (uint32_t)ldp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
           S.recA[slot] = make_uint4(cstart, cnt0 | cnt1 << 16, cnt2 | (uint32_t)lane << 16 | (hit ? 1u << 24 : 0u),
                                     1u | mpre << 1);
           if (hit) hit_c = c;
@@ -483,7 +488,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             cp += lim;
             if (at_barrier) {
               // ---- the hit of chain `barrier` (bwtgap.c:165-197)
-              const uint4 hb = S.recB[barrier & (RREC - 1)];
+              uint4 hb;
+              {
+                __threadfence_block();
+                uint32_t *hr = reinterpret_cast<uint32_t *>(A.recb + wave * RREC + (barrier & (RREC - 1)));
+                hb.x = __hip_atomic_load(hr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hb.y = __hip_atomic_load(hr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hb.z = __hip_atomic_load(hr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hb.w = __hip_atomic_load(hr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
               const uint32_t hk = hb.x, hl = hb.y;
               const int h_mm = (int)(hb.z & 0xff), h_go = (int)((hb.z >> 8) & 0xff), h_ge = (int)((hb.z >> 16) & 0xff);
               const int h_a = (int)((hb.z >> 24) & 1), h_ldp = (int)hb.w;

@@ -96,6 +96,7 @@ constexpr int COOP_SEEDMAX = 64;       // longest seed (-l) of a seeded read it 
 constexpr int COOP_PG_LOG2 = 13;       // bucket pages of 8192 entries (128 KiB): 256 pages hold 2M entries
 constexpr uint32_t COOP_PG = 1u << COOP_PG_LOG2;
 constexpr int COOP_NSTK = 128, COOP_MAXP = 256;
+constexpr int COOP_RREC = 256;          // chain records in flight (ring)
 struct CoopArgs {
   IndexView ix[2];
   const uint4 *o64[2];
@@ -119,6 +120,7 @@ struct CoopArgs {
   uint32_t pool_pages;
   uint32_t *pool_next;       // global bump pointer into the pool (zeroed per launch)
   uint4 *hits;               // per-wave hit lists [hcap]
+  uint4 *recb;               // per-wave hit records of the chain ring [COOP_RREC] (read only at a hit)
   uint32_t hcap;
   uint32_t max_iters;        // runaway guard (loop iterations per read)
   uint4 *aln;                // hit stream

@@ -128,7 +128,7 @@ struct ibwa_ctx {
   int gap_coop = 1;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
   int coop_pool_gb = 16;             // bucket page pool
-  DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next;
+  DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb;
   bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
   bool verbose = getenv("IBWA_VERBOSE") != nullptr;
   bool prof_phases = getenv("IBWA_PROF_PHASES") != nullptr;  // diagnostics kernel variant
@@ -912,6 +912,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
     if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
     if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
+    if (int rc = c->c_recb.ensure((uint64_t)blocks * COOP_RREC * 16)) return rc;
     if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
     if (int rc = c->c_next.ensure(64)) return rc;
     if (int rc = c->r_aln.ensure(r_total * 16)) return rc;
@@ -950,6 +951,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     K.pool_pages = pool_pages;
     K.pool_next = c->c_next.as<uint32_t>();
     K.hits = c->c_hits.as<uint4>();
+    K.recb = c->c_recb.as<uint4>();
     K.hcap = hcap;
     K.max_iters = 1u << 24;  // runaway guard; a read past it goes to the sequential kernel
     K.aln = c->r_aln.as<uint4>();
