@@ -24,16 +24,6 @@
 
 namespace {
 
-// POSIX lrand48 (glibc: X' = 0x5DEECE66D X + 0xB mod 2^48, result X' >> 17)
-struct Lrand48 {
-  uint64_t x = 0;
-  void seed(long s) { x = ((uint64_t)(uint32_t)s << 16) | 0x330Eu; }
-  long next() {
-    x = (0x5DEECE66Dull * x + 0xBu) & ((1ull << 48) - 1);
-    return (long)(x >> 17);
-  }
-};
-
 struct Packed {
   std::vector<uint8_t> codes;  // one 2-bit code per byte (the device builder's input)
   int64_t l_pac = 0;
@@ -60,7 +50,7 @@ bool fa2pac(const char *fn_fa, const std::string &prefix, Packed &pk) {
   };
   std::vector<Ann> anns;
   std::vector<Hole> holes;
-  Lrand48 rnd;
+  ibwa_sam::Lrand48 rnd;
   const uint32_t seed = 11;  // fixed seed for the random generator
   rnd.seed(seed);
   pk.codes.clear();

@@ -199,6 +199,16 @@ struct Drand48 {
   }
 };
 
+// POSIX lrand48 on the same generator (bns_fasta2bntseq's N fill, bntseq.c:224): X' >> 17
+struct Lrand48 {
+  uint64_t x = 0;
+  void seed(long s) { x = ((uint64_t)(uint32_t)s << 16) | 0x330Eu; }
+  long next() {
+    x = (0x5DEECE66Dull * x + 0xBu) & ((1ull << 48) - 1);
+    return (long)(x >> 17);
+  }
+};
+
 // ---------------------------------------------------------------- reads (bwa_seq_t)
 struct Multi {  // bwt_multi1_t (bwtaln.h:51-60)
   uint64_t pos = 0;
