@@ -146,33 +146,49 @@ __device__ __forceinline__ uint32_t strand_base(uint32_t c, int a, bool comp) {
   return (a == 1 && comp && c < 4) ? 3u - c : c;
 }
 
-// two bwt_cal_width chains in lockstep: str on ixa -> wa, strand-1 str on ixb -> wb
+// two bwt_cal_width chains in lockstep (bwtaln.c:54-78): str on ixa -> wa, strand-1 str on
+// ixb -> wb.  The entries of 16 steps are kept in
+// registers and stored back to back (a lane's 128 B of widths leave in consecutive instructions,
+// so the L2 merges them into whole lines instead of 16 partial writes far apart).
 __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView ixb, int L, const uint8_t *s, bool comp,
-                           uint2 *wa, uint2 *wb) {
+                                           uint2 *wa, uint2 *wb) {
   uint32_t ka = 0, la = ixa.seq_len, kb = 0, lb = ixb.seq_len;
   uint32_t bida = 0, bidb = 0;
-  for (int i = 0; i < L; ++i) {
-    uint32_t ca = s[i];
-    uint32_t cb = strand_base(ca, 1, comp);
-    Fetch1 fa, fb;
-    fetch1(ixa, ka - 1, la, ca & 3, ca < 4, fa);
-    fetch1(ixb, kb - 1, lb, cb & 3, cb < 4, fb);
-    if (ca < 4) {
-      uint32_t ok, ol;
-      occ2_from1(fa, ca, ok, ol);
-      ka = l2of(ixa, ca) + ok + 1;
-      la = l2of(ixa, ca) + ol;
+  for (int base = 0; base < L; base += 16) {
+    uint2 ba[16], bb[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int i = base + t;
+      if (i < L) {
+        uint32_t ca = s[i];
+        uint32_t cb = strand_base(ca, 1, comp);
+        Fetch1 fa, fb;
+        fetch1(ixa, ka - 1, la, ca & 3, ca < 4, fa);
+        fetch1(ixb, kb - 1, lb, cb & 3, cb < 4, fb);
+        if (ca < 4) {
+          uint32_t ok, ol;
+          occ2_from1(fa, ca, ok, ol);
+          ka = l2of(ixa, ca) + ok + 1;
+          la = l2of(ixa, ca) + ol;
+        }
+        if (ka > la || ca > 3) { ka = 0; la = ixa.seq_len; ++bida; }
+        ba[t] = make_uint2(la - ka + 1, bida);
+        if (cb < 4) {
+          uint32_t ok, ol;
+          occ2_from1(fb, cb, ok, ol);
+          kb = l2of(ixb, cb) + ok + 1;
+          lb = l2of(ixb, cb) + ol;
+        }
+        if (kb > lb || cb > 3) { kb = 0; lb = ixb.seq_len; ++bidb; }
+        bb[t] = make_uint2(lb - kb + 1, bidb);
+      }
     }
-    if (ka > la || ca > 3) { ka = 0; la = ixa.seq_len; ++bida; }
-    wa[i] = make_uint2(la - ka + 1, bida);
-    if (cb < 4) {
-      uint32_t ok, ol;
-      occ2_from1(fb, cb, ok, ol);
-      kb = l2of(ixb, cb) + ok + 1;
-      lb = l2of(ixb, cb) + ol;
-    }
-    if (kb > lb || cb > 3) { kb = 0; lb = ixb.seq_len; ++bidb; }
-    wb[i] = make_uint2(lb - kb + 1, bidb);
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      if (base + t < L) wa[base + t] = ba[t];
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      if (base + t < L) wb[base + t] = bb[t];
   }
   wa[L] = make_uint2(0u, bida + 1);
   wb[L] = make_uint2(0u, bidb + 1);
