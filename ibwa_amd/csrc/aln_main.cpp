@@ -54,18 +54,19 @@ struct Batch {
   int64_t n() const { return (int64_t)len.size(); }
 };
 
-// bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input, bwa_read_bam (:89-143) for BAM
+// bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input, bwa_read_bam (:89-143) for BAM.
+// Returns 1 with a batch, 0 at the end of the input, -1 on a truncated or corrupt record.
 template <class Reader>
-bool read_batch(Reader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
+int read_batch(Reader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
   b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0;
   const bool bam = std::is_same<Reader, BamReader>::value;
   const bool is_64 = !bam && (mode & IBWA_MODE_IL13);
   const int l_bc = bam ? 0 : (int)((unsigned)mode >> 24);  // no barcode for BAM (bwaseqio.c:156)
   if (((unsigned)mode >> 24) > 15) {
     fprintf(stderr, "[bwa_read_seq] the maximum barcode length is 15.\n");
-    return false;
+    return -1;
   }
-  int l;
+  int l = 0;
   while ((int)b.len.size() < kBatch && (l = rd.read()) >= 0) {
     std::string &s = rd.seq, &q = rd.qual;
     if (is_64 && !q.empty())
@@ -92,7 +93,11 @@ bool read_batch(Reader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, 
     if (len > b.max_len) b.max_len = len;
     for (int j = len - 1; j >= 0; --j) b.seq.push_back(nt4[(unsigned char)s[j]]);  // seq := reverse(read)
   }
-  return !b.len.empty();
+  if (l == -2) {
+    fprintf(stderr, "[ibwa-amd aln] truncated or corrupt input record after %zu reads of this batch\n", b.len.size());
+    return -1;
+  }
+  return b.len.empty() ? 0 : 1;
 }
 
 void usage(const ibwa_gap_opt_t *o) {
@@ -252,9 +257,9 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
   Batch cur, nxt;
   long n_trim = 0, n_tot = 0;
   int64_t tot_seqs = 0;
-  bool have = read_batch(rd, opt.mode, opt.trim_qual, cur, &n_trim, &n_tot);
+  int have = read_batch(rd, opt.mode, opt.trim_qual, cur, &n_trim, &n_tot);
   ph.mark("read");
-  while (have) {
+  while (have > 0) {
     auto t0 = std::chrono::steady_clock::now();
     const int64_t n = cur.n();
     tot_seqs += n;
@@ -272,12 +277,17 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
         int64_t b = std::min<int64_t>(n, g * per), e = std::min<int64_t>(n, b + per);
         g_naln[g].resize(e - b);
         int64_t tot = 0;
-        g_rc[g] = ibwa_aln_batch(ctx[g], &opt, e - b, cur.seq.data(), cur.off.data() + b, cur.len.data() + b,
+        // each slice is staged from its own bytes only: offsets rebased to the slice's first read
+        // (reads are contiguous in input order); the batch-level max length still applies
+        const uint64_t base = b < e ? cur.off[b] : 0;
+        std::vector<uint64_t> off(cur.off.begin() + b, cur.off.begin() + e);
+        for (auto &x : off) x -= base;
+        g_rc[g] = ibwa_aln_batch(ctx[g], &opt, e - b, cur.seq.data() + base, off.data(), cur.len.data() + b,
                                  cur.max_len, g_naln[g].data(), &g_aln[g], &tot);
       });
     }
     // overlap: parse the next batch while the GPUs work
-    bool more = read_batch(rd, opt.mode, opt.trim_qual, nxt, &n_trim, &n_tot);
+    int more = read_batch(rd, opt.mode, opt.trim_qual, nxt, &n_trim, &n_tot);
     for (auto &t : th) t.join();
     for (int g = 0; g < n_gpus; ++g)
       if (g_rc[g]) return die("aln");
@@ -302,6 +312,7 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
   }
   if (out != stdout) fclose(out);
   for (auto *x : ctx) ibwa_ctx_destroy(x);
+  if (have < 0) return 1;
   ph.print("ibwa-amd aln");
   return 0;
 }

@@ -134,7 +134,10 @@ struct ibwa_ctx {
   bool prof_phases = getenv("IBWA_PROF_PHASES") != nullptr;  // diagnostics kernel variant
   int sw_stop_after = getenv("IBWA_SW_STOP") ? atoi(getenv("IBWA_SW_STOP")) : 0;  // diagnostics
   DBuf d_prof;
-  unsigned long long stream_len = 0;
+  unsigned long long stream_len = 0;  // hit-stream records written by the first pass (<= stream_total)
+  unsigned long long stream_total = 0;  // hit-stream slots of the last first-pass launch
+  uint32_t gap_stream_per_read = 4;     // first-pass hit-stream slots per read
+  uint64_t gap_stream_min = 1u << 20;   // ... and at least this many in total
   std::vector<uint64_t> h_aoff;
   bool naln_on_host = true;  // h_naln mirrors d_naln
   // K-mer interval tables for the exact-match path (kmer.hip)
@@ -288,6 +291,8 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
   else if (k == "gap_early_iters" && value >= 0) c->gap_early_iters = (uint32_t)value;
   else if (k == "gap_early_entries" && value >= 0) c->gap_early_entries = (uint32_t)value;
+  else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
+  else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
@@ -747,7 +752,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         1, std::min<int>(c->gap_blocks_per_cu * 256 / block, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
     const int blocks = c->n_cus * per_cu;
     const uint64_t lanes = (uint64_t)blocks * block;
-    const uint64_t aln_total = std::max<uint64_t>((uint64_t)n * 4, 1u << 20);
+    const uint64_t aln_total = std::max<uint64_t>((uint64_t)n * c->gap_stream_per_read, c->gap_stream_min);
     if (int rc = c->d_wbuf.ensure(chunk * A.wstride * 8)) return rc;
     if (int rc = c->d_nN.ensure(chunk * 2 + 2)) return rc;
     if (int rc = c->d_ent.ensure(lanes * P0 * 16)) return rc;
@@ -776,6 +781,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.pages_per_block = ppb;
       G.aln = c->d_aln.as<uint4>();
       G.aln_total = aln_total;
+      c->stream_total = aln_total;
       G.aln_off = c->d_aoff.as<uint64_t>() + b0;
       G.n_aln = c->d_naln.as<int32_t>() + b0;
       G.status = c->d_status.as<uint32_t>() + b0;
@@ -875,6 +881,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_status.data(), c->d_status.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    // a read whose hits did not fit advanced the fill counter but wrote nothing (gapped.hip:
+    // ST_ALN_OVERFLOW, re-run below): the records in the stream end at stream_total
+    if (v2) c->stream_len = std::min<unsigned long long>(c->stream_len, c->stream_total);
   }
   c->naln_on_host = true;
   c->retry_ids.clear();

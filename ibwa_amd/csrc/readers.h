@@ -180,8 +180,10 @@ struct BamReader {
   ~BamReader() {
     if (fp) gzclose(fp);
   }
-  // seq length of the next selected record, -1 at EOF, -2 on a truncated record
-  int read() {
+  int last = 0;  // what the last read() returned
+  // seq length of the next selected record, -1 at EOF, -2 on a truncated or corrupt record
+  int read() { return last = read_record(); }
+  int read_record() {
     static const char nt16[] = "NACNGNNNTNNNNNNN";  // bam_nt16_nt4_table (bwaseqio.c:11) as bases
     for (;;) {
       int32_t block_len = 0;
@@ -198,8 +200,12 @@ struct BamReader {
       if ((which & 2) && (flag & 0x80)) go = 1;
       if ((which & 4) && !(flag & 0x40) && !(flag & 0x80)) go = 1;
       if (!go) continue;
+      // the variable-length fields must lie inside the record (a corrupt or truncated BAM
+      // would otherwise be read past the block)
+      if (l_qseq < 0 || (uint64_t)l_qname + 4ull * n_cigar + ((uint64_t)l_qseq + 1) / 2 + (uint64_t)l_qseq > data.size())
+        return -2;
       const uint8_t *sq = data.data() + l_qname + 4 * n_cigar, *q = sq + (l_qseq + 1) / 2;
-      name.assign((const char *)data.data());
+      name.assign((const char *)data.data(), strnlen((const char *)data.data(), (size_t)l_qname));
       seq.resize(l_qseq);
       qual.resize(l_qseq);
       for (int i = 0; i < l_qseq; ++i) {

@@ -109,6 +109,31 @@ def test_overflow_retry_is_exact(golden_dir, sai_manifest, gpu_engine, stack_cap
             gpu_engine.set_option(k, v)
 
 
+@pytest.mark.parametrize("stream_min", [1, 64, 700])
+def test_hit_stream_overflow_is_exact(golden_dir, sai_manifest, gpu_engine, stream_min):
+    """A first-pass hit stream smaller than the batch's hits: reads past its end are flagged and
+    re-run, and the fetch copies only the records the stream holds (the fill counter
+    runs past the stream's end on overflow)."""
+    try:
+        gpu_engine.set_option("gap_stream_per_read", 0)
+        gpu_engine.set_option("gap_stream_min", stream_min)
+        for key in ["r100.default", "mixed.N", "r100.N"]:
+            if key not in sai_manifest:
+                continue
+            m = sai_manifest[key]
+            opt, _ = oracle.parse_aln_args(m["argv"])
+            recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+            seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+            n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+            st = gpu_engine.stats()
+            assert st.path == 2 and st.n_aln_overflow > 0, (key, st.path, st.n_aln_overflow)
+            exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+            assert oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp), key
+    finally:
+        gpu_engine.set_option("gap_stream_per_read", 4)
+        gpu_engine.set_option("gap_stream_min", 1 << 20)
+
+
 def test_empty_batch(gpu_engine):
     n_aln, alns = gpu_engine.aln(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
                                  E.default_opt())
