@@ -1,21 +1,29 @@
 #!/usr/bin/env python3
-"""bench.py -- `ibwa aln` reads/s on a GRCh37-sized index (BASELINE.json configs[1]).
+"""bench.py -- `ibwa aln` reads/s on a GRCh37-sized index (BASELINE.json configs[2], and configs[3]
+per GPU under torchrun).
 
-Workload (N=1): a synthetic 3.10 Gbp genome with the 24 GRCh37 contig lengths,
-45 % repeat-family copies and N runs (no GRCh37 FASTA exists
-here), indexed ON THE GPU by the repo's builder (bit-identical to `bwa index`),
-and 10M synthetic 100 bp single-end reads (1 % substitutions, 5 % with a
-1-3 bp indel) aligned with `-n 0` (exact match only).  One step = one aln
-pass over the 10M reads already resident in HBM (the batch C ABI,
-ibwa_batch_run); results stay in HBM.
+Workload (N=1): a synthetic 3.10 Gbp genome with the 24 GRCh37 contig lengths, 45 % repeat-family
+copies and N runs (no GRCh37 FASTA exists here), indexed ON THE GPU by the repo's
+builder (bit-identical to `bwa index`), and 50M synthetic 100 bp single-end reads (1 %
+substitutions, 5 % with a 1-3 bp indel) aligned with the default options (`-n 0.04 -o 1`, the
+gapped search, bwtaln.c:21-37).  One step = one bwa_cal_sa_reg_gap pass over the 50M reads
+already resident in HBM (the batch C ABI, ibwa_batch_run: widths, the persistent gapped search,
+the cooperative heavy-read pass and any retry); results stay in HBM.  Options are parsed by the
+product's own parser (ibwa_aln_parse_args).
 
-Multi-GPU (torchrun, one rank per GPU): reads shard embarrassingly -- every
-rank holds a full index replica and its own 10M-read shard (weak scaling);
-the only collectives are the timing barrier and the max-over-ranks.
+Multi-GPU (torchrun, one rank per GPU): reads shard embarrassingly -- every rank holds a full
+index replica and its own 50M-read shard (weak scaling: 8 GPUs = configs[3]'s 400M reads); the
+only collectives are the timing barrier and the max-over-ranks.
 
-Extra JSON fields: `roofline` (HIP-event kernel times x algorithmic bytes =
-64 B x Occ-interval touches, counted by the CPU restatement on a sample) and
-`cpu_baseline` (the CPU path timed on the host cores on a bounded sample).
+Extra JSON fields (rank 0, N=1):
+  roofline      -- algorithmic bytes (64 B x Occ-interval touches per read, counted by the CPU
+                   restatement on the measured reads) over the step's kernel time (HIP events);
+                   `traffic` = HBM bytes per step from the committed rocprofv3 PMC profile of
+                   this workload
+  cpu_baseline  -- the CPU restatement timed on the host cores on a bounded sample
+  extra.parity  -- GPU == CPU restatement on >= 200k reads plus reads the cooperative / wide /
+                   general passes resolved
+  extra.exact_leg -- configs[1] (10M reads, -n 0) on the same index, with its own roofline
 """
 import argparse
 import ctypes
@@ -41,6 +49,16 @@ def host_threads():
     n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     cpu = os.cpu_count() or 8
     return max(1, min(n if n > 0 else cpu, cpu, 64))
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def make_genome(scale_num, scale_den, seed, threads):
@@ -71,9 +89,9 @@ def make_reads(ascii_, lens, seed, n, ln, sub, indel, threads):
     return seq, off, lns
 
 
-def shard_seed(rank):
+def shard_seed(rank, base=3):
     """Reads seed of a rank: every rank aligns its own, disjoint synthetic reads (weak scaling)."""
-    return 2 + 1000 * rank
+    return base + 1000 * rank
 
 
 def reduce_max(x, dist, device):
@@ -86,61 +104,119 @@ def reduce_max(x, dist, device):
     return float(t.item())
 
 
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
-    same workload (profiles/<round>_<tag>_pmc.json, written by tools/profile_round.sh: separate
-    --pmc passes, EA read/write requests by size).  None if no such profile exists."""
+def pmc_traffic(kernels, workload):
+    """HBM bytes per step of the named kernels from the newest committed rocprofv3 PMC summary of
+    the same workload (profiles/<round>_<tag>_pmc.json, tools/profile_round.sh: separate --pmc
+    passes, EA read/write requests by size, MI355X_MICROARCH.md HBM section).  A profile states
+    per kernel how many aln runs of its command it took part in (`runs`); bytes per step = bytes
+    over all its dispatches / runs.
+    Returns (bytes, file, kernel ms per step) or None if no such profile exists."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        ks = [d.get("kernels", {}).get(n) for n in kernel.split("+")]
-        if all(ks) and d.get("bench_line", {}).get("config", {}).get("workload") == workload:
-            # a '+'-joined name prices kernels that run back to back on one batch (per-launch sums)
-            return (sum(k["read_bytes_per_dispatch"] + k["write_bytes_per_dispatch"] for k in ks),
-                    os.path.basename(f), sum(k.get("avg_ms") or 0.0 for k in ks))
+        if workload not in d.get("workloads", []):
+            continue
+        ks = [d.get("kernels", {}).get(n) for n in kernels]
+        if not all(ks) or not all(k.get("runs") for k in ks):
+            continue
+        return (sum((k["total_read_bytes"] + k["total_write_bytes"]) / k["runs"] for k in ks), os.path.basename(f),
+                sum(k["total_ms"] / k["runs"] for k in ks))
     return None
 
 
-def cpu_baseline(eng, opt_args, seq, off, lns, budget_s, threads):
-    """Time the CPU path on a bounded sample of the same reads (rank 0, N=1 only).
-
-    kind "reference": the reference's own bwa_cal_sa_reg_gap compiled from
-    /root/reference into oracle/_ref (test infrastructure); else "port": the
-    repo's C restatement (oracle/).  Both over `threads` host threads.
-    """
+def oracle_bwts(eng):
     import oracle
-    p0, L20, w0 = eng.export_bwt(0)
-    p1, L21, w1 = eng.export_bwt(1)
-    b0 = oracle.Bwt(primary=p0, L2=L20, words=w0)
-    b1 = oracle.Bwt(primary=p1, L2=L21, words=w1)
-    opt, _ = oracle.parse_aln_args(opt_args)
-    # calibrate on a small slice, then size the sample for ~budget_s
-    n_cal = min(len(lns), 20000)
-    t = time.perf_counter()
-    _, _, tch = oracle.cal_sa_reg_gap(b0, b1, seq[:int(off[n_cal - 1] + lns[n_cal - 1])], off[:n_cal], lns[:n_cal],
-                                      opt, n_threads=threads, touches=True)
-    dt = time.perf_counter() - t
-    n_s = int(min(len(lns), max(n_cal, n_cal * budget_s / max(dt, 1e-3))))
-    t = time.perf_counter()
-    n_aln, alns, tch = oracle.cal_sa_reg_gap(b0, b1, seq[:int(off[n_s - 1] + lns[n_s - 1])], off[:n_s], lns[:n_s],
-                                             opt, n_threads=threads, touches=True)
-    dt = time.perf_counter() - t
-    return {"value": n_s / dt, "unit": "reads/s", "cores": threads, "kind": "port",
-            "sample": f"first {n_s} of the same reads, same index and options ({dt:.1f} s wall, "
-                      f"{threads} pthreads, oracle/ibwa_oracle.c)"}, tch, n_s, (n_aln, alns)
+    bw = []
+    for s in (0, 1):
+        p, L2, w = eng.export_bwt(s)
+        bw.append(oracle.Bwt(primary=p, L2=L2, words=w))
+    return bw
 
 
-def sa2pos_leg(eng, lns):
+def to_oracle_opt(eopt):
+    import oracle
+    return oracle.GapOpt.from_buffer_copy(bytes(eopt))
+
+
+def per_read(n_aln, alns, ids):
+    """Hits of reads `ids` as bytes, from the concatenated per-read hit array."""
+    first = np.concatenate([[0], np.cumsum(n_aln, dtype=np.int64)[:-1]])
+    return [alns[first[i]:first[i] + n_aln[i]].tobytes() for i in ids]
+
+
+def cpu_and_parity(eng, eopt, seq, off, lns, n_aln, alns, budget_s, check, heavy_budget_s, threads):
+    """CPU baseline + touches + parity (rank 0, N=1).  The checker is the C restatement in oracle/
+    (test infrastructure; pinned to the reference's .sai goldens by tests/test_oracle_golden.py).
+
+    1. the first n_s reads (n_s >= `check`, sized so the CPU run takes ~budget_s): timed -> the
+       CPU baseline; per-read Occ touches -> the roofline's algorithmic bytes; hits == GPU's;
+    2. reads the first pass handed on (cooperative / wide / general passes), sampled evenly over
+       the batch, in chunks until heavy_budget_s: hits == GPU's."""
+    import oracle
+    b0, b1 = oracle_bwts(eng)
+    opt = to_oracle_opt(eopt)
+    n = len(lns)
+    n_cal = min(n, 20000)
+    t = time.perf_counter()
+    oracle.cal_sa_reg_gap(b0, b1, seq, off[:n_cal], lns[:n_cal], opt, n_threads=threads)
+    dt = time.perf_counter() - t
+    n_s = int(min(n, max(check, n_cal * budget_s / max(dt, 1e-3))))
+    t = time.perf_counter()
+    rn, ra, tch = oracle.cal_sa_reg_gap(b0, b1, seq, off[:n_s], lns[:n_s], opt, n_threads=threads, touches=True)
+    dt = time.perf_counter() - t
+    p = int(rn.sum())
+    ok_first = bool((n_aln[:n_s] == rn).all() and alns[:p].tobytes() == ra.tobytes())
+    cpu = {"value": n_s / dt, "unit": "reads/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "sample": f"first {n_s} of the same reads, same index and options ({dt:.1f} s wall, {threads} pthreads, "
+                     f"oracle/ibwa_oracle.c)"}
+    # heavy reads: resolved outside the first pass
+    ids, ps = eng.retry_info()
+    by_pass = {int(k): int((ps == k).sum()) for k in (1, 2, 3)}
+    sel = []
+    for k, cap in ((2, 2000), (3, 2000), (1, 1 << 30)):
+        cand = ids[(ps == k) & (ids >= n_s)]
+        if cand.size > cap:
+            cand = cand[np.linspace(0, cand.size - 1, cap).astype(np.int64)]
+        sel.append(cand)
+    # wide/general first (few), then coop reads spread evenly over the batch
+    coop = sel[2]
+    order = np.concatenate([sel[0], sel[1], coop[np.argsort(np.arange(coop.size) % 64, kind="stable")]])
+    checked = {1: 0, 2: 0, 3: 0}
+    bad = []
+    t0 = time.perf_counter()
+    pass_of = dict(zip(ids.tolist(), ps.tolist()))
+    chunk = 256
+    for c0 in range(0, order.size, chunk):
+        if c0 and time.perf_counter() - t0 > heavy_budget_s:
+            break
+        sub = np.sort(order[c0:c0 + chunk])
+        hn, ha, _ = oracle.cal_sa_reg_gap(b0, b1, seq, off[sub], lns[sub], opt, n_threads=threads)
+        got = per_read(n_aln, alns, sub)
+        exp = per_read(hn, ha, range(sub.size))
+        for j, i in enumerate(sub):
+            checked[pass_of[int(i)]] += 1
+            if got[j] != exp[j] or n_aln[i] != hn[j]:
+                bad.append(int(i))
+    parity = {"first_reads": n_s, "first_reads_ok": ok_first,
+              "handed_on_reads": int(ids.size), "handed_on_by_pass": {"coop": by_pass[1], "wide": by_pass[2],
+                                                                       "general": by_pass[3]},
+              "handed_on_checked": {"coop": checked[1], "wide": checked[2], "general": checked[3]},
+              "handed_on_mismatches": bad[:20], "handed_on_ok": not bad,
+              "heavy_check_s": time.perf_counter() - t0}
+    parity["ok"] = ok_first and not bad and n_s + sum(checked.values()) >= 200_000
+    return cpu, tch, parity
+
+
+def sa2pos_leg(eng, lns, n_aln, alns):
     """SA -> coordinate (bwtdb_sa2seq, dbset.c:240) of each read's first hit after the timed aln
     steps, as samse/sampe would ask for it: kernel time (HIP events) with the full SA resident
     (one gather per hit) and with the sampled SA (bwt_sa's LF walk, bwt.c:69), plus a check
     that both agree.  Not part of `value`."""
-    n_aln, alns = eng.fetch()
     has = n_aln > 0
-    first = np.concatenate([[0], np.cumsum(n_aln)[:-1]])[has]
+    first = np.concatenate([[0], np.cumsum(n_aln, dtype=np.int64)[:-1]])[has]
     a = ((alns["info"][first] >> 24) & 1).astype(np.uint8)
     k = alns["k"][first]
     ln = lns[has]
@@ -161,21 +237,75 @@ def sa2pos_leg(eng, lns):
     return out
 
 
+def exact_leg(eng, ascii_, lens, args, threads, hip, do_cpu):
+    """configs[1]: 10M x 100 bp, `-n 0`, on the same resident index (k_pack_reads + k_exact with
+    the K-mer table and the unique-interval jump).  Kernel-time roofline priced with the exact
+    path's own touches (oracle.exact_touches, jump-aware) and, for reference, the reference
+    algorithm's touches."""
+    import oracle
+    from ibwa_amd import engine as E
+    seq, off, lns = make_reads(ascii_, lens, 2, args.exact_reads, args.read_len, 0.01, 0.05, threads)
+    opt = E.parse_aln_args(["-n", "0"])
+    eng.stage(seq, off, lns)
+    eng.run(opt)
+    hip.hipDeviceSynchronize()
+    t0 = time.perf_counter()
+    ms_k = ms_p = 0.0
+    for _ in range(args.exact_steps):
+        eng.run(opt)
+        st = eng.stats()
+        ms_k += st.ms_search
+        ms_p += st.ms_width
+    hip.hipDeviceSynchronize()
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    out = {"workload": f"configs[1]: {args.exact_reads} x {args.read_len} bp, aln -n 0, same index",
+           "value": args.exact_reads * args.exact_steps / dt, "unit": "reads/s", "steps": args.exact_steps,
+           "ms_per_step": dt * 1e3 / args.exact_steps, "k_exact_ms": ms_k / args.exact_steps,
+           "k_pack_reads_ms": ms_p / args.exact_steps, "path": {1: "exact", 3: "exact+jump"}.get(st.path, st.path),
+           "kmer_k": st.kmer_k}
+    if do_cpu:
+        n_aln, alns = eng.fetch()
+        b0, b1 = oracle_bwts(eng)
+        n_t = min(lns.size, 100_000)
+        tch = oracle.exact_touches(b0, b1, seq, off[:n_t], lns[:n_t], opt.mode, st.kmer_k, jump=st.path == 3)
+        n_c = min(lns.size, 100_000)
+        t = time.perf_counter()
+        rn, ra, rt = oracle.cal_sa_reg_gap(b0, b1, seq, off[:n_c], lns[:n_c], to_oracle_opt(opt), n_threads=threads,
+                                           touches=True)
+        cdt = time.perf_counter() - t
+        p = int(rn.sum())
+        out["parity_reads"] = n_c
+        out["parity_ok"] = bool((n_aln[:n_c] == rn).all() and alns[:p].tobytes() == ra.tobytes())
+        k_ms = ms_k / args.exact_steps
+        ach = float(tch.mean()) * 64.0 * args.exact_reads / (k_ms * 1e-3) / 1e9
+        pmc = pmc_traffic(["k_exact"], out["workload"])
+        out["roofline"] = {"bound": "hbm", "kernel": "k_exact", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": ach / HBM_PEAK_GBS, "traffic": pmc[0] if pmc else None,
+                           "traffic_source": pmc[1] if pmc else None,
+                           "touches_per_read": float(tch.mean()), "reference_touches_per_read": float(rt.mean())}
+        out["cpu_baseline"] = {"value": n_c / cdt, "unit": "reads/s", "cores": threads, "kind": "port",
+                               "cpu_model": cpu_model(), "sample": f"first {n_c} reads ({cdt:.1f} s wall)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
+    ap.add_argument("--reads", type=int, default=50_000_000, help="reads per GPU")
     ap.add_argument("--read-len", type=int, default=100)
     ap.add_argument("--scale", type=float, default=1.0, help="genome size as a fraction of GRCh37")
-    ap.add_argument("--aln", default="-n 0", help="aln options (reference syntax)")
+    ap.add_argument("--aln", default="", help="aln options (reference syntax); default: gap_init_opt's")
+    ap.add_argument("--seed", type=int, default=3, help="reads seed (SURVEY §8d: configs[2] = 3)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--heavy-budget", type=float, default=20.0, help="seconds of CPU parity on handed-on reads")
+    ap.add_argument("--check", type=int, default=200_000, help="min. first reads checked bit-exact vs the CPU")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--check", type=int, default=20000, help="reads checked bit-exact vs the CPU restatement")
-    ap.add_argument("--kmer-k", type=int, default=-1, help="K-mer table length for the exact path (-1 auto, 0 off)")
-    ap.add_argument("--exact-path", type=int, default=1, help="use the exact-match kernel when max_diff == 0")
-    ap.add_argument("--sweep-k", default="", help="comma list of K values to time after the main run")
+    ap.add_argument("--exact-leg", type=int, default=1, help="also run configs[1] (-n 0) as extra.exact_leg")
+    ap.add_argument("--exact-reads", type=int, default=10_000_000)
+    ap.add_argument("--exact-steps", type=int, default=5)
     ap.add_argument("--sa2pos", type=int, default=1, help="also time SA->coordinate of every read's first hit")
     ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
     args = ap.parse_args()
@@ -191,19 +321,16 @@ def main():
         dist_.init_process_group("nccl")
         dist = dist_
 
-    def barrier_max(x):
-        return reduce_max(x, dist, f"cuda:{local}")
-
-    import oracle
     from ibwa_amd import engine as E
     threads = host_threads()
+    opt = E.parse_aln_args(args.aln.split())  # the product's own parser (bwtaln.c:249-284)
     tg = time.perf_counter()
     den = 1_000_000
     ascii_, codes, lens, n_amb = make_genome(int(round(args.scale * den)), den, 37, threads)
     log(f"genome {codes.size/1e9:.3f} Gbp ({n_amb} N->random), {time.perf_counter()-tg:.1f} s")
     tr = time.perf_counter()
-    seq, off, lns = make_reads(ascii_, lens, shard_seed(rank), args.reads, args.read_len, 0.01, 0.05, threads)
-    del ascii_
+    seq, off, lns = make_reads(ascii_, lens, shard_seed(rank, args.seed), args.reads, args.read_len, 0.01, 0.05,
+                               threads)
     log(f"{args.reads} reads x {args.read_len} bp, {time.perf_counter()-tr:.1f} s")
 
     eng = E.Engine(local)
@@ -212,17 +339,9 @@ def main():
     build_s = time.perf_counter() - tb
     del codes
     log(f"index built on device in {build_s:.1f} s")
-    opt_args = args.aln.split()
-    ropt, _ = oracle.parse_aln_args(opt_args)
-    opt = E.GapOpt()
-    for f, _ in E.GapOpt._fields_:
-        setattr(opt, f, getattr(ropt, f))
-
     for kv in args.opt:
         k_, v_ = kv.split("=")
         eng.set_option(k_, int(v_))
-    eng.set_option("kmer_k", args.kmer_k)
-    eng.set_option("exact_path", args.exact_path)
     eng.stage(seq, off, lns)
 
     def progress(tag):
@@ -236,10 +355,9 @@ def main():
         eng.run(opt)
         progress(f"warmup {w}")
     # timed region: inputs resident in HBM, results left in HBM
-    ms_w = ms_s = ms_r = 0.0
+    ms_w = ms_s = ms_r = ms_c = 0.0
     if dist is not None:
         dist.barrier()
-    import torch  # noqa: F401  (torch.cuda.synchronize semantics via hipDeviceSynchronize below)
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipDeviceSynchronize()
     t0 = time.perf_counter()
@@ -250,92 +368,76 @@ def main():
         ms_w += st.ms_width
         ms_s += st.ms_search
         ms_r += st.ms_retry
+        ms_c += st.ms_coop
     hip.hipDeviceSynchronize()
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt = barrier_max(dt)
-    n_retry = eng.stats().n_retry
+    dt = reduce_max(dt, dist, f"cuda:{local}")
     total_reads = args.reads * world * args.steps
     value = total_reads / dt
     ms_step = dt * 1e3 / args.steps
-
-    cfg_name = "configs[1]" if ropt.max_diff == 0 and ropt.fnr <= 0 else "configs[2]"
+    launches = max(1, args.steps)
+    stl = eng.stats()
+    path = stl.path
+    exact_cfg = opt.max_diff == 0 and opt.fnr <= 0
+    cfg_name = "configs[1]" if exact_cfg else "configs[2]" if world == 1 else "configs[3]"
     result = {
         "metric": "reads/s `ibwa aln` GRCh37-sized 100bp, achieved HBM GB/s vs peak",
         "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic",
-        "config": {"workload": f"{cfg_name}: GRCh37-sized synthetic genome ({lens and sum(lens)/1e9:.2f} Gbp, "
-                               f"index built on device), {args.reads} x {args.read_len} bp SE reads per GPU, "
-                               f"aln {args.aln}",
-                   "reads_per_gpu": args.reads, "read_len": args.read_len, "aln_options": args.aln,
+        "config": {"workload": f"{cfg_name}: GRCh37-sized synthetic genome ({sum(lens)/1e9:.2f} Gbp, index built on "
+                               f"device), {args.reads} x {args.read_len} bp SE reads per GPU, aln "
+                               f"{args.aln or 'defaults (-n 0.04 -o 1)'}",
+                   "reads_per_gpu": args.reads, "read_len": args.read_len, "aln_options": args.aln or "defaults",
                    "parallelism": f"replicated index, reads sharded x{world}"},
     }
     if rank == 0:
-        # correctness check + per-read touch counts on a sample (CPU restatement)
-        cpu = None
-        check_ok = None
-        if not args.no_cpu and world == 1:
-            cpu, tch, n_s, (rn, ra) = cpu_baseline(eng, opt_args, seq, off, lns, args.cpu_budget, threads)
+        extra = {"index_build_s": build_s, "n_retry": int(stl.n_retry), "n_stack_overflow": int(stl.n_stack_overflow),
+                 "n_aln_overflow": int(stl.n_aln_overflow), "n_heavy": int(stl.n_heavy), "n_coop": int(stl.n_coop),
+                 "path": {0: "width+search", 1: "exact", 2: "width+gapped", 3: "exact+jump"}.get(path, str(path)),
+                 "kernel_ms_per_step": {"k_width(first pass)": ms_w / launches, "k_gapped": ms_s / launches,
+                                        "k_coop(+its widths)": ms_c / launches,
+                                        "wide+general retry": (ms_r - ms_c) / launches},
+                 "host_cores": threads, "cpu_model": cpu_model()}
+        do_cpu = not args.no_cpu and world == 1
+        n_aln = alns = None
+        if do_cpu or args.sa2pos:
             n_aln, alns = eng.fetch()
-            p = int(rn[:n_s].sum())
-            check_ok = bool((n_aln[:n_s] == rn[:n_s]).all() and alns[:p].tobytes() == ra[:p].tobytes())
-            touches = float(tch.mean())
+        kernels = ["k_width", "k_gapped", "k_coop"] if path == 2 else ["k_pack_reads", "k_exact"]
+        k_ms = (ms_w + ms_s + ms_r) / launches
+        if do_cpu:
+            tc = time.perf_counter()
+            cpu, tch, parity = cpu_and_parity(eng, opt, seq, off, lns, n_aln, alns, args.cpu_budget, args.check,
+                                              args.heavy_budget, threads)
+            log(f"CPU baseline + parity {time.perf_counter()-tc:.1f} s: {cpu['value']:.0f} reads/s, parity {parity}")
             result["cpu_baseline"] = cpu
-        else:
-            touches = None
-        launches = max(1, args.steps)
-        path = eng.stats().path
-        if touches:
-            # touches of the path actually run: the exact-match kernel skips bwt_cal_width,
-            # so its algorithmic bytes are priced from its own exact-search touches
-            if path in (1, 3):
-                n_t = min(len(lns), 200_000)
-                p0, L20, w0 = eng.export_bwt(0)
-                p1, L21, w1 = eng.export_bwt(1)
-                b0 = oracle.Bwt(primary=p0, L2=L20, words=w0)
-                b1 = oracle.Bwt(primary=p1, L2=L21, words=w1)
-                kk = eng.stats().kmer_k
-                path_touches = float(oracle.exact_touches(b0, b1, seq[:n_t * args.read_len], off[:n_t], lns[:n_t],
-                                                          ropt.mode, kk, jump=path == 3).mean())
-                result["extra_kmer_k"] = kk
-                kname, k_ms = "k_exact", ms_s / launches
-            else:
-                # the general path runs the reference algorithm: its touches are the oracle's;
-                # the two kernels (width, search) are priced together
-                path_touches = touches
-                kname = "k_width+k_gapped" if path == 2 else "k_width+k_search"
-                k_ms = (ms_w + ms_s) / launches
-            ach = path_touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9
-            pmc = pmc_traffic(kname, result["config"]["workload"])
+            extra["parity"] = parity
+            extra["parity_sample_ok"] = parity["ok"]
+            touches = float(tch.mean())
+            # the step's kernels run the reference algorithm (widths + bwt_match_gap): its bytes are
+            # 64 B per Occ-interval touch of the restatement, over all kernel time
+            ach = touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9
+            pmc = pmc_traffic(kernels, result["config"]["workload"])
             result["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": ach / HBM_PEAK_GBS, "traffic": pmc[0] if pmc else None, "kernel": kname,
+                                  "frac": ach / HBM_PEAK_GBS, "traffic": pmc[0] if pmc else None,
+                                  "kernel": "+".join(kernels) + " (one step's launches)",
                                   "traffic_source": pmc[1] if pmc else None,
                                   "traffic_GBps": pmc[0] / (k_ms * 1e-3) / 1e9 if pmc else None,
-                                  "profiled_kernel_ms": pmc[2] if pmc else None,
-                                  "algorithmic_bytes_per_launch": path_touches * 64.0 * args.reads,
-                                  "kernel_ms_per_launch": k_ms,
-                                  "touches_per_read": path_touches, "bytes_per_touch": 64,
-                                  "reference_touches_per_read": touches,
-                                  "reference_equivalent_GBps": touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9}
-        stl = eng.stats()
-        result["extra"] = {"index_build_s": build_s, "n_retry": int(n_retry), "parity_sample_ok": check_ok,
-                           "n_stack_overflow": int(stl.n_stack_overflow), "n_aln_overflow": int(stl.n_aln_overflow),
-                           "path": {0: "width+search", 1: "exact", 2: "width+gapped", 3: "exact+jump"}.get(path, str(path)),
-                           "k_width_or_pack_ms": ms_w / launches, "k_search_ms": ms_s / launches,
-                           "retry_ms": ms_r / launches}
-        if args.sa2pos:
-            result["extra"]["sa2pos"] = sa2pos_leg(eng, lns)
+                                  "profiled_kernel_ms_per_step": pmc[2] if pmc else None,
+                                  "algorithmic_bytes_per_step": touches * 64.0 * args.reads,
+                                  "kernel_ms_per_step": k_ms, "touches_per_read": touches, "bytes_per_touch": 64,
+                                  "touches_sample": f"first {tch.size} reads, oracle/ibwa_oracle.c touch counter"}
+        if args.sa2pos and n_aln is not None:
+            extra["sa2pos"] = sa2pos_leg(eng, lns, n_aln, alns)
+        if args.exact_leg and world == 1 and not exact_cfg:
+            del seq, off, lns
+            te = time.perf_counter()
+            extra["exact_leg"] = exact_leg(eng, ascii_, lens, args, threads, hip, do_cpu)
+            log(f"exact leg {time.perf_counter()-te:.1f} s: {extra['exact_leg']}")
+        result["extra"] = extra
         print(json.dumps(result), flush=True)
-        for k in [int(x) for x in args.sweep_k.split(",") if x.strip()]:
-            eng.set_option("kmer_k", k)
-            eng.run(opt)
-            t = time.perf_counter()
-            for _ in range(args.steps):
-                eng.run(opt)
-            dt_k = (time.perf_counter() - t) / args.steps
-            log(f"sweep K={k}: {args.reads / dt_k / 1e6:.1f} M reads/s, kernel {eng.stats().ms_search:.2f} ms")
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

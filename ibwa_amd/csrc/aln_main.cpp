@@ -10,7 +10,6 @@
 // contiguous slices that keep the batch-level max length, bwtaln.c:89-93).
 // Reading the next batch overlaps the GPU work on the current one.
 #include <ctype.h>
-#include <getopt.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -158,48 +157,11 @@ int main(int argc, char *argv[]) {
   --argc; ++argv;
   init_nt4();
   ibwa_gap_opt_t opt;
-  ibwa_gap_init_opt(&opt);
-  int opte = -1, n_gpus = 1, c;
+  int n_gpus = 1;
   const char *fn_out = nullptr;
-  // bwtaln.c:249-284 (+ -G)
-  while ((c = getopt(argc, argv, "n:o:e:i:d:l:k:cLR:m:t:NM:O:E:q:f:b012IB:G:")) >= 0) {
-    switch (c) {
-      case 'n':
-        if (strstr(optarg, ".")) opt.fnr = (float)atof(optarg), opt.max_diff = -1;
-        else opt.max_diff = atoi(optarg), opt.fnr = -1.0f;
-        break;
-      case 'o': opt.max_gapo = atoi(optarg); break;
-      case 'e': opte = atoi(optarg); break;
-      case 'M': opt.s_mm = atoi(optarg); break;
-      case 'O': opt.s_gapo = atoi(optarg); break;
-      case 'E': opt.s_gape = atoi(optarg); break;
-      case 'd': opt.max_del_occ = atoi(optarg); break;
-      case 'i': opt.indel_end_skip = atoi(optarg); break;
-      case 'l': opt.seed_len = atoi(optarg); break;
-      case 'k': opt.max_seed_diff = atoi(optarg); break;
-      case 'm': opt.max_entries = atoi(optarg); break;
-      case 't': opt.n_threads = atoi(optarg); break;
-      case 'L': opt.mode |= IBWA_MODE_LOGGAP; break;
-      case 'R': opt.max_top2 = atoi(optarg); break;
-      case 'q': opt.trim_qual = atoi(optarg); break;
-      case 'c': opt.mode &= ~IBWA_MODE_COMPREAD; break;
-      case 'N': opt.mode |= IBWA_MODE_NONSTOP; opt.max_top2 = 0x7fffffff; break;
-      case 'f': fn_out = optarg; break;
-      case 'b': opt.mode |= IBWA_MODE_BAM; break;
-      case '0': opt.mode |= IBWA_MODE_BAM_SE; break;
-      case '1': opt.mode |= IBWA_MODE_BAM_READ1; break;
-      case '2': opt.mode |= IBWA_MODE_BAM_READ2; break;
-      case 'I': opt.mode |= IBWA_MODE_IL13; break;
-      case 'B': opt.mode |= atoi(optarg) << 24; break;
-      case 'G': n_gpus = atoi(optarg); break;
-      default: return 1;
-    }
-  }
-  if (opte > 0) {
-    opt.max_gape = opte;
-    opt.mode &= ~IBWA_MODE_GAPE;
-  }
-  if (optind + 2 > argc) {
+  const int first_arg = ibwa_aln_parse_args(argc, argv, &opt, &n_gpus, &fn_out);  // bwtaln.c:249-284 (+ -G)
+  if (first_arg < 0) return 1;
+  if (first_arg + 2 > argc) {
     usage(&opt);
     return 1;
   }
@@ -210,7 +172,7 @@ int main(int argc, char *argv[]) {
       k = l;
     }
   }
-  const std::string prefix = argv[optind];
+  const std::string prefix = argv[first_arg];
   if (opt.mode & IBWA_MODE_BAM) {  // bwa_open_reads (bwtaln.c:159-171)
     int which = 0;
     if (opt.mode & IBWA_MODE_BAM_SE) which |= 4;
@@ -218,15 +180,15 @@ int main(int argc, char *argv[]) {
     if (opt.mode & IBWA_MODE_BAM_READ2) which |= 2;
     if (which == 0) which = 7;
     BamReader rd;
-    if (!rd.open(argv[optind + 1], which)) {
-      fprintf(stderr, "[ibwa-amd aln] cannot open %s as BAM\n", argv[optind + 1]);
+    if (!rd.open(argv[first_arg + 1], which)) {
+      fprintf(stderr, "[ibwa-amd aln] cannot open %s as BAM\n", argv[first_arg + 1]);
       return 1;
     }
     return run_aln(rd, opt, prefix, fn_out, n_gpus);
   }
   SeqReader rd;
-  if (!rd.open(argv[optind + 1])) {
-    fprintf(stderr, "[ibwa-amd aln] cannot open %s\n", argv[optind + 1]);
+  if (!rd.open(argv[first_arg + 1])) {
+    fprintf(stderr, "[ibwa-amd aln] cannot open %s\n", argv[first_arg + 1]);
     return 1;
   }
   return run_aln(rd, opt, prefix, fn_out, n_gpus);

@@ -139,6 +139,7 @@ struct ibwa_ctx {
   uint32_t gap_stream_per_read = 4;     // first-pass hit-stream slots per read
   uint64_t gap_stream_min = 1u << 20;   // ... and at least this many in total
   std::vector<uint64_t> h_aoff;
+  std::vector<uint8_t> retry_pass;  // per retry_ids entry: 1 coop, 2 wide, 3 general kernels
   bool naln_on_host = true;  // h_naln mirrors d_naln
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
@@ -726,6 +727,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->naln_on_host = false;  // results stay in HBM; ibwa_batch_fetch copies them
     c->retry_ids.clear();
     c->retry_alns.clear();
+    c->retry_pass.clear();
     c->stats.ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return 0;
@@ -888,6 +890,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   c->naln_on_host = true;
   c->retry_ids.clear();
   c->retry_alns.clear();
+  c->retry_pass.clear();
   for (int64_t i = 0; i < n; ++i) {
     if (c->h_status[i] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "read %lld: score outside the stack range", (long long)i);
     if (c->h_status[i]) c->retry_ids.push_back(i);
@@ -901,6 +904,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   uint64_t cap = std::max<uint64_t>((uint64_t)c->stack_cap * 16, 65536);
   uint32_t acap = std::max<uint32_t>(c->aln_cap * 64, 4096);
   std::vector<std::vector<uint4>> found(todo.size());
+  std::vector<uint8_t> found_by(todo.size(), 0);
   std::vector<int64_t> where(todo.size());
   for (size_t j = 0; j < todo.size(); ++j) where[j] = (int64_t)j;
   float ms_r = 0;
@@ -1005,6 +1009,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       }
       const uint64_t first = rn[j] ? ro[j] : 0;
       found[where[j]].assign(ra.begin() + first, ra.begin() + first + rn[j]);
+      found_by[where[j]] = 1;
     }
     if (c->verbose) {
       uint32_t mx = 0;
@@ -1143,6 +1148,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         }
         const uint64_t first = wide_round ? (rn[j] ? ro[j] : 0) : (uint64_t)j * acap;
         found[slot].assign(ra.begin() + first, ra.begin() + first + rn[j]);
+        found_by[slot] = wide_round ? 2 : 3;
       }
     }
     if (c->verbose)
@@ -1164,10 +1170,21 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     where.swap(next_where);
   }
   c->retry_alns.swap(found);
+  c->retry_pass.swap(found_by);
   c->stats.ms_retry = ms_r;
   c->stats.n_retry = (int64_t)c->retry_ids.size();
   c->stats.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}
+
+int ibwa_batch_retry_info(const ibwa_ctx_t *c, int64_t *ids, uint8_t *pass, int64_t cap, int64_t *n) {
+  const int64_t m = (int64_t)c->retry_ids.size();
+  for (int64_t j = 0; j < std::min(m, cap); ++j) {
+    if (ids) ids[j] = c->retry_ids[j];
+    if (pass) pass[j] = j < (int64_t)c->retry_pass.size() ? c->retry_pass[j] : 0;
+  }
+  if (n) *n = m;
   return 0;
 }
 

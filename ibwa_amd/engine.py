@@ -86,6 +86,8 @@ CAPI = {
     "ibwa_batch_fetch": (_i, [_vp, _vp, c.POINTER(_vp), c.POINTER(_i64)]),
     "ibwa_batch_stats": (_i, [_vp, c.POINTER(RunStats)]),
     "ibwa_ctx_set_tuning": (_i, [_vp, _i, _i, _i]),
+    "ibwa_aln_parse_args": (_i, [_i, c.POINTER(c.c_char_p), c.POINTER(GapOpt), c.POINTER(_i), c.POINTER(c.c_char_p)]),
+    "ibwa_batch_retry_info": (_i, [_vp, _vp, _vp, _i64, c.POINTER(_i64)]),
     "ibwa_ctx_set_option": (_i, [_vp, c.c_char_p, c.c_long]),
     "ibwa_occ4": (_i, [_vp, _i, _i64, _vp, _vp]),
     "ibwa_ctx_load_sa": (_i, [_vp, _i, _u32, _vp, _u64]),
@@ -138,6 +140,19 @@ def _chk(rc):
 def default_opt():
     o = GapOpt()
     lib().ibwa_gap_init_opt(c.byref(o))
+    return o
+
+
+def parse_aln_args(args):
+    """The product's own `aln` option parser (ibwa_aln_parse_args: bwtaln.c:249-284) -> GapOpt."""
+    argv = [b"aln"] + [a.encode() for a in args]
+    arr = (c.c_char_p * len(argv))(*argv)
+    o = GapOpt()
+    rc = lib().ibwa_aln_parse_args(len(argv), arr, c.byref(o), None, None)
+    if rc < 0:
+        raise IbwaError(f"bad aln options {args}")
+    if rc != len(argv):
+        raise IbwaError(f"unexpected positional arguments in {args}")
     return o
 
 
@@ -204,6 +219,16 @@ class Engine:
         buf = c.string_at(ptr.value, tot.value * 16)
         lib().ibwa_free(ptr)
         return n_aln, np.frombuffer(buf, dtype=ALN_DTYPE).copy()
+
+    def retry_info(self):
+        """(read ids, pass) of the reads the last run's first pass handed on; pass 1 = coop,
+        2 = sequential wide, 3 = general kernels."""
+        n = c.c_int64()
+        _chk(lib().ibwa_batch_retry_info(self.h, None, None, 0, c.byref(n)))
+        ids = np.zeros(n.value, np.int64)
+        ps = np.zeros(n.value, np.uint8)
+        _chk(lib().ibwa_batch_retry_info(self.h, ids.ctypes.data, ps.ctypes.data, n.value, c.byref(n)))
+        return ids, ps
 
     def stats(self):
         st = RunStats()

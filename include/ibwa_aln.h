@@ -144,6 +144,21 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
+/*
+ * The `aln` command line (bwa_aln's getopt loop, bwtaln.c:249-284; same option string and
+ * semantics, plus -G INT = number of GPUs) into *opt, starting from gap_init_opt's defaults.
+ * argv[0] is the command name.  Returns the index of the first positional argument, -1 on an
+ * unknown option.  n_gpus / fn_out (-f) may be NULL.  Thread-safe (getopt is serialised).
+ */
+int ibwa_aln_parse_args(int argc, char *const *argv, ibwa_gap_opt_t *opt, int *n_gpus, const char **fn_out);
+
+/*
+ * Reads of the last ibwa_batch_run that the first pass handed on, and the pass that resolved
+ * each: 1 the wave-cooperative pass (coop.hip), 2 the sequential wide pass (gapped.hip, one
+ * read per wave), 3 the general kernels (aln.hip).  Writes min(cap, n) entries; *n = their count.
+ */
+int ibwa_batch_retry_info(const ibwa_ctx_t *ctx, int64_t *ids, uint8_t *pass, int64_t cap, int64_t *n);
+
 /* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */
 int ibwa_ctx_set_tuning(ibwa_ctx_t *ctx, int stack_cap, int aln_cap, int block);
 

@@ -39,3 +39,25 @@ def test_cpu_only_calls():
     o = engine.default_opt()
     assert (o.s_mm, o.s_gapo, o.s_gape, o.seed_len, o.max_top2) == (3, 11, 4, 32, 30)
     assert engine.lib().ibwa_cal_maxdiff(100, 0.02, 0.04) == 5
+
+
+def test_product_option_parser_matches_reference_semantics():
+    """ibwa_aln_parse_args (the product's getopt, used by the CLI and bench.py) against the
+    oracle's restatement of bwa_aln's option handling, over every golden option set."""
+    import json
+
+    import oracle
+    from ibwa_amd import engine
+    man = json.load(open(os.path.join(ROOT, "tests", "golden", "sai_manifest.json")))
+    sets = [m["argv"] for m in man.values()] + [["-n", "0.01", "-e", "0"], ["-e", "5", "-N", "-R", "7"],
+                                                ["-B", "4", "-q", "20", "-I", "-c", "-L", "-m", "1000"]]
+    for argv in sets:
+        got = engine.parse_aln_args(argv)
+        exp, _ = oracle.parse_aln_args(argv)
+        for f, _ in engine.GapOpt._fields_:
+            assert getattr(got, f) == getattr(exp, f), (argv, f)
+    # repeated calls start from the defaults again (getopt state is re-initialised)
+    assert engine.parse_aln_args([]).max_diff == -1
+    import pytest
+    with pytest.raises(engine.IbwaError):
+        engine.parse_aln_args(["-Z"])

@@ -57,6 +57,17 @@ def main():
             res["bench_line"] = json.loads(open(log).read().strip().splitlines()[-1])
         except Exception:
             pass
+    line = res.get("bench_line", {})
+    main_exact = "-n 0" in str(line.get("config", {}).get("aln_options", ""))
+    leg = line.get("extra", {}).get("exact_leg") or {}
+    res["workloads"] = [w for w in (line.get("config", {}).get("workload"), leg.get("workload")) if w]
+
+    def runs_of(k):
+        """aln runs (ibwa_batch_run calls) of the profiled command in which kernel k ran."""
+        main = line.get("steps", 0) + line.get("warmup", 0)
+        if k in ("k_exact", "k_pack_reads") and not main_exact:
+            return leg.get("steps", 0) + 1 if leg else 0
+        return main
     for k in sorted(set(dur) | set(cnt)):
         c = cnt.get(k, {})
         # each pmc pass ran the same dispatches: per-dispatch = sum / dispatches of that pass
@@ -70,6 +81,9 @@ def main():
             "per_dispatch": {n.replace("_sum", ""): g(n) for n in sorted(c)},
             "read_bytes_per_dispatch": rd, "write_bytes_per_dispatch": wr,
             "dram_read_fraction": (g("TCC_EA0_RDREQ_DRAM_sum") / g("TCC_EA0_RDREQ_sum")) if g("TCC_EA0_RDREQ_sum") else None,
+            # over all dispatches of the command (a step runs several launches of some kernels)
+            "total_ms": sum(d), "total_read_bytes": rd * n_pass, "total_write_bytes": wr * n_pass,
+            "runs": runs_of(k),
         }
     path = os.path.join(prof, f"{rnd}_{tag}_pmc.json")
     json.dump(res, open(path, "w"), indent=1)
