@@ -191,6 +191,11 @@ struct SaArgs {
 };
 hipError_t launch_sa2pos(const SaArgs &a, bool full, hipStream_t st);
 hipError_t expand_sa(const IndexView &ix, const uint32_t *sa_s, uint32_t intv, uint32_t *full, hipStream_t st);
+// sampled SA (bwt_cal_sa's values, interval intv) from the BWT alone; tmp: 4 * (n / intv + 1) + 1 words
+hipError_t derive_sampled_sa(const IndexView &ix, uint32_t intv, uint32_t *sa_s, uint32_t *tmp, hipStream_t st);
+// ISA (seq_len + 1 words) and the 2-bit text from a full SA (full[0] = -1)
+hipError_t derive_isa_text(const IndexView &ix, const uint32_t *full, uint32_t *isa, uint32_t *txt2, uint64_t txt_words,
+                           hipStream_t st);
 
 hipError_t build_kmer_table(const IndexView &ix, int K, uint2 *table, uint2 *tmp, hipStream_t st);
 

@@ -97,6 +97,8 @@ struct ibwa_ctx {
   // full SA / ISA and 2-bit texts of an index built here: the exact path's unique-interval jump
   DBuf sa_full[2], isa_full[2], txt2[2];
   bool jump_ready = false;
+  bool jump_derived = false;  // jump arrays derived from a loaded BWT (ensure_jump), not built here
+  int jump_derive = 1;        // option: derive them for a loaded index when HBM allows
   int exact_jump = 1;
   uint32_t sa_intv = 0;
   bool sa_loaded[2] = {false, false};  // sa_s[s] holds a sampled SA of the resident index
@@ -187,6 +189,54 @@ int ensure_kmer(ibwa_ctx *c) {
   c->kmer_valid = true;
   return 0;
 }
+// The exact path's unique-interval jump needs the full SA, the ISA and the 2-bit text of both
+// strands.  An index built here keeps them (ibwa_ctx_build_index); for an index loaded from .bwt
+// files (the drop-in, the CLI) they are derived on the device from the BWT alone: the sampled SA
+// by an LF walk between marked rows plus list ranking, then the full SA (k_expand_sa), the ISA
+// (a scatter) and the text (a gather through the ISA).  Skipped when HBM is short: the exact path
+// then runs without the jump (same results).
+int derive_sa_locked(ibwa_ctx *c, uint32_t intv) {
+  HIPCHK(hipSetDevice(c->device));
+  for (int s = 0; s < 2; ++s) {
+    const uint64_t n_nodes = ((uint64_t)c->ix[s].seq_len + intv) / intv;
+    DBuf tmp;
+    if (int rc = tmp.ensure((4 * n_nodes + 1) * 4)) return rc;
+    if (int rc = c->sa_s[s].ensure(n_nodes * 4)) { tmp.release(); return rc; }
+    hipError_t e = derive_sampled_sa(c->ix[s], intv, c->sa_s[s].as<uint32_t>(), tmp.as<uint32_t>(), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    tmp.release();
+    if (e != hipSuccess) return fail(IBWA_EHIP, "sampled SA from the BWT (strand %d): %s", s, hipGetErrorString(e));
+    c->sa_loaded[s] = true;
+  }
+  c->sa_intv = intv;
+  c->sa_expanded = false;
+  return 0;
+}
+
+int ensure_jump(ibwa_ctx *c) {
+  if (c->jump_ready || !c->exact_jump || !c->jump_derive) return 0;
+  const uint64_t n = c->ix[0].seq_len;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
+  // full SA + ISA + text of both strands (~16.6 B per base) and the derivation's temporaries
+  if ((double)free_b < (double)n * 18.0 + 4e9 || (double)n * 16.6 > 0.3 * (double)total_b) return 0;
+  if (!c->sa_loaded[0] || !c->sa_loaded[1])
+    if (int rc = derive_sa_locked(c, 32)) return rc;
+  if (int rc = ibwa_ctx_expand_sa(c)) return rc;
+  for (int s = 0; s < 2; ++s) {
+    const uint64_t words = n / 16 + 4;
+    if (int rc = c->isa_full[s].ensure((n + 1) * 4)) return rc;
+    if (int rc = c->txt2[s].ensure(words * 4)) return rc;
+    HIPCHK(hipMemsetAsync(c->txt2[s].p, 0, words * 4, c->stream));
+    HIPCHK(derive_isa_text(c->ix[s], c->sa_full[s].as<uint32_t>(), c->isa_full[s].as<uint32_t>(),
+                           c->txt2[s].as<uint32_t>(), words, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->jump_ready = true;
+  c->jump_derived = true;
+  return 0;
+}
+
 // Kernel arguments of the persistent gapped search shared by the first and retry passes;
 // the caller fills the per-pass scratch and output pointers.
 GapArgs gap_args(const ibwa_ctx *c, const AlnArgs &A, const AlnOpt &o, int64_t b0, int64_t cnt) {
@@ -295,6 +345,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
   else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
+  else if (k == "jump_derive") c->jump_derive = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
@@ -339,7 +390,8 @@ int ibwa_ctx_load_bwt(ibwa_ctx_t *c, int strand, uint32_t primary, const uint32_
   for (int j = 0; j < 4; ++j) ix.L2[j + 1] = L2[j];
   c->loaded[strand] = true;
   c->kmer_valid = false;
-  c->jump_ready = false;  // SA / ISA / text belong to an index built here
+  c->jump_ready = false;  // SA / ISA / text belong to an index built here (or are derived again)
+  c->jump_derived = false;
   c->sa_loaded[strand] = false;
   c->sa_expanded = false;
   return 0;
@@ -531,6 +583,12 @@ int ibwa_ctx_load_sa_file(ibwa_ctx_t *c, int strand, const char *path) {  // bwt
   return ibwa_ctx_load_sa(c, strand, hdr[5], sa.data(), n_sa);
 }
 
+int ibwa_ctx_derive_sa(ibwa_ctx_t *c, uint32_t sa_intv) {
+  if (!c->loaded[0] || !c->loaded[1]) return fail(IBWA_ENOINDEX, "load both .bwt and .rbwt first");
+  if (sa_intv == 0) return fail(IBWA_EINVAL, "sa_intv == 0");
+  return derive_sa_locked(c, sa_intv);
+}
+
 int ibwa_ctx_expand_sa(ibwa_ctx_t *c) {
   if (!c->sa_loaded[0] || !c->sa_loaded[1]) return fail(IBWA_ENOINDEX, "sampled SA of both strands needed");
   if (c->jump_ready || c->sa_expanded) return 0;  // full SA already resident
@@ -700,6 +758,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     A.n_aln = c->d_naln.as<int32_t>();
     A.status = c->d_status.as<uint32_t>();
     if (int rc = ensure_kmer(c)) return rc;
+    if (int rc = ensure_jump(c)) return rc;
     c->stats.kmer_k = c->kmer_K;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     const uint32_t stride = exact_record_stride(max_len);

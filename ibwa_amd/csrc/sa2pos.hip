@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "engine.h"
 #include "occ.h"
 
@@ -107,7 +109,132 @@ __global__ void __launch_bounds__(256) k_expand_sa(IndexView ix, const uint32_t 
   }
 }
 
+// ---- the unique-interval jump's SA / ISA / text for an index that arrives as .bwt files only
+// (bwt_restore_bwt, bwtaln.c:184-189: `aln` never loads .sa or .pac).  Everything follows from
+// the LF cycle: row 0 (suffix "$") -> seq_len - 1 -> ... -> primary (suffix 0) -> row 0.
+
+// symbol of BWT row k (k != primary): the stored position bwt_kk(k) of the $-removed BWT
+__device__ __forceinline__ uint32_t bwt_sym(const IndexView &ix, uint32_t k) {
+  const uint32_t p = k < ix.primary ? k : k - 1;
+  const uint4 *b = ix.blk + (size_t)(p >> 7) * 4;
+  const uint32_t off = p & 127, q = off >> 5;
+  uint32_t w0, w1;
+  chunk_words(b[1 + (q >> 1)], q, w0, w1);
+  const uint32_t r = off & 31;
+  return ((r < 16 ? w0 : w1) >> (2 * (15 - (r & 15)))) & 3u;
+}
+
+// 1. marked rows j * intv: walk LF from each to the next marked row -> link and distance
+__global__ void __launch_bounds__(256) k_sa_link(IndexView ix, uint32_t intv, uint64_t n_nodes,
+                                                 uint32_t *__restrict__ next, uint32_t *__restrict__ dist) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_nodes; j += stride) {
+    uint32_t k = (uint32_t)(j * intv), d = 0;
+    do {
+      k = inv_psi(ix, k);
+      ++d;
+    } while (k % intv);
+    next[j] = k / intv;
+    dist[j] = d;
+  }
+}
+
+// 2. list ranking by pointer jumping (node 0 = row 0 is the sink): after the last round
+//    rank[j] = LF steps from row j * intv to row 0 = SA[j * intv] + 1
+__global__ void __launch_bounds__(256) k_sa_jump(uint64_t n_nodes, const uint32_t *__restrict__ nx,
+                                                 const uint32_t *__restrict__ rk, uint32_t *__restrict__ nx2,
+                                                 uint32_t *__restrict__ rk2, uint32_t *__restrict__ active) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t any = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_nodes; j += stride) {
+    const uint32_t a = nx[j];
+    if (a != 0) {
+      rk2[j] = rk[j] + rk[a];
+      nx2[j] = nx[a];
+      any |= nx[a] != 0;
+    } else {
+      rk2[j] = rk[j];
+      nx2[j] = 0;
+    }
+  }
+  if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(active, 1u);
+}
+
+__global__ void __launch_bounds__(256) k_sa_sample(uint64_t n_nodes, const uint32_t *__restrict__ rk,
+                                                   uint32_t *__restrict__ sa_s) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_nodes; j += stride)
+    sa_s[j] = j == 0 ? 0xFFFFFFFFu : rk[j] - 1;  // bwtio.c:45 stores sa[0] = -1
+}
+
+// 3. ISA over text positions [0, seq_len] from the full SA (full[0] is the stored -1: row 0 is
+//    the suffix at seq_len)
+__global__ void __launch_bounds__(256) k_isa_from_sa(const uint32_t *__restrict__ full, uint64_t n_rows,
+                                                     uint32_t seq_len, uint32_t *__restrict__ isa) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_rows; r += stride)
+    isa[r == 0 ? seq_len : full[r]] = (uint32_t)r;
+}
+
+// 4. the 2-bit text (sa_build.hip's k_pack_text2 layout): T[p] is the BWT symbol of the row of
+//    suffix p + 1
+__global__ void __launch_bounds__(256) k_text_from_isa(IndexView ix, const uint32_t *__restrict__ isa,
+                                                       uint64_t n_words, uint32_t *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t n = ix.seq_len;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += stride) {
+    uint32_t x = 0;
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t t = w * 16 + k;
+      if (t < n) x |= bwt_sym(ix, isa[t + 1]) << (2 * k);
+    }
+    out[w] = x;
+  }
+}
+
 }  // namespace
+
+hipError_t derive_sampled_sa(const IndexView &ix, uint32_t intv, uint32_t *sa_s, uint32_t *tmp, hipStream_t st) {
+  const uint64_t n_nodes = ((uint64_t)ix.seq_len + intv) / intv;  // rows 0 .. seq_len
+  uint32_t *nx = tmp, *rk = tmp + n_nodes, *nx2 = tmp + 2 * n_nodes, *rk2 = tmp + 3 * n_nodes;
+  uint32_t *active = tmp + 4 * n_nodes;
+  const unsigned g = (unsigned)std::min<uint64_t>((n_nodes + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_sa_link, dim3(g), dim3(256), 0, st, ix, intv, n_nodes, nx, rk);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // sink: node 0
+  e = hipMemsetAsync(nx, 0, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(rk, 0, 4, st);
+  bool done = false;
+  for (int round = 0; e == hipSuccess && !done && round < 40; ++round) {
+    e = hipMemsetAsync(active, 0, 4, st);
+    if (e != hipSuccess) break;
+    hipLaunchKernelGGL(k_sa_jump, dim3(g), dim3(256), 0, st, n_nodes, nx, rk, nx2, rk2, active);
+    e = hipGetLastError();
+    std::swap(nx, nx2);
+    std::swap(rk, rk2);
+    uint32_t more = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&more, active, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    done = more == 0;
+  }
+  if (e != hipSuccess) return e;
+  if (!done) return hipErrorUnknown;  // more than 2^40 nodes: cannot happen for a 32-bit index
+  hipLaunchKernelGGL(k_sa_sample, dim3(g), dim3(256), 0, st, n_nodes, rk, sa_s);
+  return hipGetLastError();
+}
+
+hipError_t derive_isa_text(const IndexView &ix, const uint32_t *full, uint32_t *isa, uint32_t *txt2, uint64_t txt_words,
+                           hipStream_t st) {
+  const uint64_t n_rows = (uint64_t)ix.seq_len + 1;
+  const unsigned g = (unsigned)std::min<uint64_t>((n_rows + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_isa_from_sa, dim3(g), dim3(256), 0, st, full, n_rows, ix.seq_len, isa);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const unsigned gw = (unsigned)std::min<uint64_t>((txt_words + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_text_from_isa, dim3(gw), dim3(256), 0, st, ix, isa, txt_words, txt2);
+  return hipGetLastError();
+}
 
 hipError_t launch_sa2pos(const SaArgs &a, bool full, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;

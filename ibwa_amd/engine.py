@@ -93,6 +93,7 @@ CAPI = {
     "ibwa_ctx_load_sa": (_i, [_vp, _i, _u32, _vp, _u64]),
     "ibwa_ctx_load_sa_file": (_i, [_vp, _i, c.c_char_p]),
     "ibwa_ctx_expand_sa": (_i, [_vp]),
+    "ibwa_ctx_derive_sa": (_i, [_vp, _u32]),
     "ibwa_sa2pos": (_i, [_vp, _i64, _vp, _vp, _vp, _u64, _vp]),
     "ibwa_ctx_build_index": (_i, [_vp, _vp, _u64, _i]),
     "ibwa_ctx_bwt_info": (_i, [_vp, _i, c.POINTER(_u32), c.POINTER(_u32), c.POINTER(_u64)]),
@@ -274,6 +275,10 @@ class Engine:
     def load_sa(self, strand, sa, intv):
         sa = np.ascontiguousarray(sa, dtype=np.uint32)
         _chk(lib().ibwa_ctx_load_sa(self.h, strand, int(intv), sa.ctypes.data, sa.size))
+
+    def derive_sa(self, intv=32):
+        """Sampled SA of both strands derived on the device from the resident BWT alone."""
+        _chk(lib().ibwa_ctx_derive_sa(self.h, intv))
 
     def expand_sa(self):
         _chk(lib().ibwa_ctx_expand_sa(self.h))

@@ -132,6 +132,8 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "exact_path" (0/1, default 1)  exact-match kernel when max_diff == 0
  *   "exact_jump" (0/1, default 1)  keep full SA / ISA / text at ibwa_ctx_build_index and let
  *                                  the exact path jump over a unique interval's remaining symbols
+ *   "jump_derive" (0/1, default 1) for an index loaded from .bwt files, derive those arrays on
+ *                                  the device from the BWT at the first -n 0 batch (HBM permitting)
  *   "kmer_k" (-1 auto, 0 off, 1..16) K-mer interval table length
  *   "exact_blocks", "lanes_per_chunk"
  *   "gapped_v2" (0/1, default 1)   persistent gapped-search kernel (else the general kernels)
@@ -220,6 +222,9 @@ int ibwa_sw_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *ref, const uint64_t
 int ibwa_ctx_load_sa(ibwa_ctx_t *ctx, int strand, uint32_t sa_intv, const uint32_t *sa, uint64_t n_sa);
 int ibwa_ctx_load_sa_file(ibwa_ctx_t *ctx, int strand, const char *path);
 int ibwa_ctx_expand_sa(ibwa_ctx_t *ctx);
+/* The sampled SA of both strands (bwt_cal_sa's values at interval sa_intv, what `bwa index`
+ * writes to .sa / .rsa, bwt.c:48-67) derived on the device from the resident BWT alone. */
+int ibwa_ctx_derive_sa(ibwa_ctx_t *ctx, uint32_t sa_intv);
 int ibwa_sa2pos(ibwa_ctx_t *ctx, int64_t n, const uint8_t *strand, const uint32_t *k, const uint32_t *len,
                 uint64_t offset, uint64_t *pos);
 

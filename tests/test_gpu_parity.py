@@ -46,7 +46,8 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path, gappe
         if not oracle.sai_body_equal(got, exp):
             bad.append(key)
         if m["argv"] == ["-n", "0"]:
-            assert gpu_engine.stats().path == (1 if exact_path else 2 if gapped_v2 else 0), key
+            # a file-loaded index gets the jump arrays derived from its BWT (path 3)
+            assert gpu_engine.stats().path == (3 if exact_path else 2 if gapped_v2 else 0), key
         elif gapped_v2 and gpu_engine.stats().path != 2:
             bad.append(key + ":path")
     gpu_engine.set_option("exact_path", 1)
@@ -126,12 +127,53 @@ def test_hit_stream_overflow_is_exact(golden_dir, sai_manifest, gpu_engine, stre
             seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
             n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
             st = gpu_engine.stats()
-            assert st.path == 2 and st.n_aln_overflow > 0, (key, st.path, st.n_aln_overflow)
+            assert st.path == 2, (key, st.path)
+            if int(n_aln.sum()) > stream_min:  # more hits than the stream holds: some reads overflowed
+                assert st.n_aln_overflow > 0, (key, st.n_aln_overflow)
             exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
             assert oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp), key
     finally:
         gpu_engine.set_option("gap_stream_per_read", 4)
         gpu_engine.set_option("gap_stream_min", 1 << 20)
+
+
+def test_exact_path_without_jump(golden_dir, sai_manifest, gpu_engine):
+    """-n 0 goldens with the jump arrays not derived (path 1), then derived again (path 3)."""
+    for derive, path in [(0, 1), (1, 3)]:
+        eng = E.Engine(0)
+        try:
+            eng.load_index_files(os.path.join(golden_dir, "g1m"))
+            eng.set_option("jump_derive", derive)
+            for key, m in sorted(sai_manifest.items()):
+                if m["argv"] != ["-n", "0"]:
+                    continue
+                opt, _ = oracle.parse_aln_args(m["argv"])
+                recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+                seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+                n_aln, alns = eng.aln(seqs, offs, lens, _eopt(opt))
+                assert eng.stats().path == path, (key, derive)
+                exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+                assert oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp), (key, derive)
+        finally:
+            eng.close()
+
+
+@pytest.mark.parametrize("prefix", ["g1m", "tandem", "idx_quirks"])
+def test_sampled_sa_derived_from_bwt(golden_dir, prefix):
+    """The sampled SA derived on the device from .bwt / .rbwt alone (LF walks between marked rows
+    + list ranking) equals the reference-built .sa / .rsa byte for byte."""
+    eng = E.Engine(0)
+    try:
+        eng.load_index_files(os.path.join(golden_dir, prefix))
+        eng.derive_sa(32)
+        for s, ext in [(0, ".sa"), (1, ".rsa")]:
+            raw = np.fromfile(os.path.join(golden_dir, prefix + ext), dtype=np.uint32)
+            intv = int(raw[5])
+            assert intv == 32
+            got = eng.export_sa(s, 32)
+            assert got[0] == 0xFFFFFFFF and (got[1:] == raw[7:]).all(), (prefix, ext)
+    finally:
+        eng.close()
 
 
 def test_empty_batch(gpu_engine):
