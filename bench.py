@@ -308,17 +308,31 @@ def main():
     ap.add_argument("--exact-steps", type=int, default=5)
     ap.add_argument("--sa2pos", type=int, default=1, help="also time SA->coordinate of every read's first hit")
     ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
+    ap.add_argument("--shards", type=int, default=1,
+                    help="single process: align the reads of ranks 0..K-1 as one batch (checks the sharded path)")
+    ap.add_argument("--dump", default="", help="write this rank's hits to DUMP.rank<r>.npz after the timed steps")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    dev = local
+    red_dev = f"cuda:{local}"
     if world > 1:
         import torch
         import torch.distributed as dist_
-        torch.cuda.set_device(local)
-        dist_.init_process_group("nccl")
+        n_dev = torch.cuda.device_count()  # does not initialise the GPU
+        if world <= n_dev:
+            torch.cuda.set_device(local)
+            dist_.init_process_group("nccl")  # RCCL over xGMI: only the barrier and the max
+        else:
+            # more ranks than GPUs (a rehearsal of the sharded path on one box): ranks share
+            # devices round-robin; RCCL refuses two ranks on one device, so the two
+            # collectives go over gloo
+            dev = local % max(n_dev, 1)
+            red_dev = "cpu"
+            dist_.init_process_group("gloo")
         dist = dist_
 
     from ibwa_amd import engine as E
@@ -329,11 +343,20 @@ def main():
     ascii_, codes, lens, n_amb = make_genome(int(round(args.scale * den)), den, 37, threads)
     log(f"genome {codes.size/1e9:.3f} Gbp ({n_amb} N->random), {time.perf_counter()-tg:.1f} s")
     tr = time.perf_counter()
-    seq, off, lns = make_reads(ascii_, lens, shard_seed(rank, args.seed), args.reads, args.read_len, 0.01, 0.05,
-                               threads)
+    parts = [make_reads(ascii_, lens, shard_seed(r, args.seed), args.reads, args.read_len, 0.01, 0.05, threads)
+             for r in ([rank] if world > 1 else range(max(1, args.shards)))]
+    if len(parts) == 1:
+        seq, off, lns = parts[0]
+    else:  # reads of shards 0..K-1 back to back, as one batch
+        seq = np.concatenate([p[0] for p in parts])
+        lns = np.concatenate([p[2] for p in parts])
+        base = np.cumsum([0] + [p[0].size for p in parts[:-1]]).astype(np.uint64)
+        off = np.concatenate([p[1] + b for p, b in zip(parts, base)])
+    del parts
+    args.reads = int(lns.size)
     log(f"{args.reads} reads x {args.read_len} bp, {time.perf_counter()-tr:.1f} s")
 
-    eng = E.Engine(local)
+    eng = E.Engine(dev)
     tb = time.perf_counter()
     eng.build_index(codes, sa_intv=32)  # the sampled SA too (bwa index's .sa/.rsa), for the sa2pos leg
     build_s = time.perf_counter() - tb
@@ -373,7 +396,10 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt = reduce_max(dt, dist, f"cuda:{local}")
+    dt = reduce_max(dt, dist, red_dev)
+    if args.dump:
+        n_d, a_d = eng.fetch()
+        np.savez(f"{args.dump}.rank{rank}.npz", n_aln=n_d, alns=a_d.view(np.uint32))
     total_reads = args.reads * world * args.steps
     value = total_reads / dt
     ms_step = dt * 1e3 / args.steps

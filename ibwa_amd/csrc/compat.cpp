@@ -3,7 +3,8 @@
 // Replaces the per-thread body of bwtaln.c:80-140 and the pthread fan-out
 // around it (bwtaln.c:199-218): the batch is flattened once, split into
 // contiguous slices, one per GPU (each keeping the batch-level max length,
-// bwtaln.c:89-93), and every slice runs on its own engine from a host thread.
+// bwtaln.c:89-93), and every slice runs on its own engine from a host thread.  Several
+// slices may share a GPU (ibwa_gpu_init_ex): they run concurrently on their own streams.
 #include <hip/hip_runtime_api.h>
 #include <math.h>
 #include <stdio.h>
@@ -21,7 +22,8 @@
 namespace {
 
 std::mutex g_mu;
-std::vector<ibwa_ctx_t *> g_ctx;
+std::vector<ibwa_ctx_t *> g_ctx;  // one engine per slice: slices_per_gpu on each GPU, GPU-major
+int g_min_slice = 1024;          // fewest reads per slice (the reference's THREAD_BLOCK_SIZE, bwtaln.c:16)
 
 [[noreturn]] void die(const char *what, int rc) {
   fprintf(stderr, "[ibwa_amd] %s failed (%d): %s\n", what, rc, ibwa_last_error());
@@ -33,15 +35,17 @@ void destroy_locked() {
   g_ctx.clear();
 }
 
-int init_locked(ibwa_ref_bwt_t *const bwt[2], int n_gpus) {
+int init_locked(ibwa_ref_bwt_t *const bwt[2], int n_gpus, int slices_per_gpu, int min_slice) {
   destroy_locked();
   int n_dev = 0;
   if (hipGetDeviceCount(&n_dev) != hipSuccess || n_dev <= 0) n_dev = 0;
   if (n_gpus <= 0 || n_gpus > n_dev) n_gpus = n_dev;
   if (n_gpus <= 0) return IBWA_EHIP;
-  for (int g = 0; g < n_gpus; ++g) {
+  if (slices_per_gpu < 1) slices_per_gpu = 1;
+  g_min_slice = min_slice > 0 ? min_slice : 1024;
+  for (int g = 0; g < n_gpus * slices_per_gpu; ++g) {
     ibwa_ctx_t *c = nullptr;
-    if (int rc = ibwa_ctx_create(g, &c)) {
+    if (int rc = ibwa_ctx_create(g / slices_per_gpu, &c)) {
       destroy_locked();
       return rc;
     }
@@ -67,7 +71,12 @@ extern "C" {
 
 int ibwa_gpu_init(ibwa_ref_bwt_t *const bwt[2], int n_gpus) {
   std::lock_guard<std::mutex> lk(g_mu);
-  return init_locked(bwt, n_gpus);
+  return init_locked(bwt, n_gpus, 1, 1024);
+}
+
+int ibwa_gpu_init_ex(ibwa_ref_bwt_t *const bwt[2], int n_gpus, int slices_per_gpu, int min_reads_per_slice) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return init_locked(bwt, n_gpus, slices_per_gpu, min_reads_per_slice);
 }
 
 void ibwa_gpu_destroy(void) {
@@ -80,7 +89,7 @@ void bwa_cal_sa_reg_gap(int tid, ibwa_ref_bwt_t *const bwt[2], int n_seqs, ibwa_
   (void)tid;
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_ctx.empty())
-    if (int rc = init_locked(bwt, 1)) die("ibwa_gpu_init", rc);
+    if (int rc = init_locked(bwt, 1, 1, 1024)) die("ibwa_gpu_init", rc);
   // reads already processed by a concurrent caller (seq freed) are skipped, so the
   // reference's n_threads > 1 fan-out degenerates to one GPU pass per batch
   std::vector<int> ids;
@@ -93,7 +102,7 @@ void bwa_cal_sa_reg_gap(int tid, ibwa_ref_bwt_t *const bwt[2], int n_seqs, ibwa_
   }
   const int64_t n = (int64_t)ids.size();
   if (n == 0) return;
-  const int n_gpu = (int)std::min<int64_t>((int64_t)g_ctx.size(), (n + 1023) / 1024);
+  const int n_gpu = (int)std::min<int64_t>((int64_t)g_ctx.size(), (n + g_min_slice - 1) / g_min_slice);
   const int64_t per = (n + n_gpu - 1) / n_gpu;
   std::vector<int32_t> n_aln(n);
   std::vector<ibwa_aln1_t *> alns(n_gpu, nullptr);

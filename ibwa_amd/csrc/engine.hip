@@ -811,7 +811,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const size_t lds = lds_of(block);
     const int per_cu = std::max<int>(
         1, std::min<int>(c->gap_blocks_per_cu * 256 / block, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
-    const int blocks = c->n_cus * per_cu;
+    // persistent grid: fills the chip, but a small batch gets only the lanes it can use, so
+    // its per-lane scratch and page pools are sized by the batch, not the worst case
+    const int blocks = (int)std::min<int64_t>((int64_t)c->n_cus * per_cu, (chunk + block - 1) / block);
     const uint64_t lanes = (uint64_t)blocks * block;
     const uint64_t aln_total = std::max<uint64_t>((uint64_t)n * c->gap_stream_per_read, c->gap_stream_min);
     if (int rc = c->d_wbuf.ensure(chunk * A.wstride * 8)) return rc;
@@ -973,9 +975,14 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const int64_t lanes = (int64_t)todo.size();
     uint32_t stg_log2 = 10;
     while ((1u << stg_log2) < 2u * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
-    const int blocks = c->n_cus * c->coop_waves_per_cu;
+    // one heavy read per wave at a time: no more waves than heavy reads, and the page pool in
+    // proportion (at least 1 GiB; a read that runs out of pages goes on to the wide kernel)
+    const int full_blocks = c->n_cus * c->coop_waves_per_cu;
+    const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
     const uint32_t freecap = 4096, hcap = 4096;
-    const uint32_t pool_pages = (uint32_t)(((uint64_t)c->coop_pool_gb << 30) / (COOP_PG * 16ull));
+    const uint64_t pool_bytes = std::min<uint64_t>(
+        (uint64_t)c->coop_pool_gb << 30, std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
+    const uint32_t pool_pages = (uint32_t)(pool_bytes / (COOP_PG * 16ull));
     const uint64_t r_total = (uint64_t)lanes * 64 + (1u << 20);
     if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
     if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;

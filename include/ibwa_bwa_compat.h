@@ -103,6 +103,11 @@ typedef struct {
  * by device-to-device copies.  Returns 0, or an IBWA_E* code.
  */
 int ibwa_gpu_init(ibwa_ref_bwt_t *const bwt[2], int n_gpus);
+/* As ibwa_gpu_init, with slices_per_gpu engines on every GPU (a batch is split into
+ * n_gpus * slices_per_gpu contiguous slices, the slices of one GPU running concurrently) and a
+ * batch split only into slices of at least min_reads_per_slice reads (ibwa_gpu_init: 1 and
+ * 1024, the reference's THREAD_BLOCK_SIZE claim, bwtaln.c:16). */
+int ibwa_gpu_init_ex(ibwa_ref_bwt_t *const bwt[2], int n_gpus, int slices_per_gpu, int min_reads_per_slice);
 /* Release the engines (before bwt_destroy, bwtaln.c:239). */
 void ibwa_gpu_destroy(void);
 

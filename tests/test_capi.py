@@ -30,7 +30,7 @@ def test_library_exports_all_declared():
 
 def test_binding_covers_header():
     hdr = {n for n in declared_symbols() if n.startswith("ibwa_")}
-    compat = {"ibwa_gpu_init", "ibwa_gpu_destroy"}
+    compat = {"ibwa_gpu_init", "ibwa_gpu_init_ex", "ibwa_gpu_destroy"}
     assert hdr - compat <= set(CAPI), sorted(hdr - compat - set(CAPI))
 
 

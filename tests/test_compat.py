@@ -104,55 +104,89 @@ def _load_ref_bwt(path, keep):
     return b
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("key", ["r100.default", "mixed.default", "mixed.n0", "r150.default", "mixed.c"])
-def test_dropin_matches_golden_sai(golden_dir, sai_manifest, key):
+def _dropin_run(L, libc, bw, golden_dir, sai_manifest, key):
+    """bwa_cal_sa_reg_gap on the golden reads of `key` -> (.sai bytes, expected bytes)."""
+    m = sai_manifest[key]
+    opt, _ = oracle.parse_aln_args(m["argv"])
+    recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+    seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+    n = lens.size
+    arr = (RefSeq * n)()
+    for i in range(n):
+        s = seqs[int(offs[i]):int(offs[i]) + int(lens[i])]
+        p = libc.malloc(max(1, s.size))
+        c.memmove(p, s.ctypes.data, s.size)
+        arr[i].seq = p
+        arr[i].rseq = libc.malloc(max(1, s.size))  # content unused by the engine; freed by it
+        arr[i].qual = libc.malloc(8)
+        arr[i].name = libc.malloc(8)
+        arr[i].len = int(lens[i])
+        arr[i].tid = -1
+        arr[i].sa = 7
+        arr[i].type = 3
+    eo = E.GapOpt()
+    for f, _ in E.GapOpt._fields_:
+        setattr(eo, f, getattr(opt, f))
+    L.bwa_cal_sa_reg_gap(0, bw, n, arr, c.byref(eo))
+    n_aln = np.array([arr[i].n_aln for i in range(n)], dtype=np.int32)
+    parts = [c.string_at(arr[i].aln, 16 * arr[i].n_aln) for i in range(n)]
+    alns = np.frombuffer(b"".join(parts), dtype=oracle.ALN_DTYPE)
+    assert all(arr[i].seq is None and arr[i].rseq is None and arr[i].qual is None and arr[i].name is None
+               for i in range(n))
+    assert all(arr[i].sa == 0 and arr[i].type == 0 and arr[i].c1 == 0 and arr[i].c2 == 0 for i in range(n))
+    for i in range(n):
+        libc.free(c.c_void_p(arr[i].aln))
+    return oracle.sai_bytes(opt, n_aln, alns), open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+
+
+def _dropin_setup(golden_dir, keep):
     L = c.CDLL(_native.LIB_PATH)
     libc = c.CDLL(None)
     libc.malloc.restype = c.c_void_p
     libc.malloc.argtypes = [c.c_size_t]
     libc.free.argtypes = [c.c_void_p]
-    keep = []
     b0 = _load_ref_bwt(os.path.join(golden_dir, "g1m.bwt"), keep)
     b1 = _load_ref_bwt(os.path.join(golden_dir, "g1m.rbwt"), keep)
+    keep += [b0, b1]
     bw = (c.POINTER(RefBwt) * 2)(c.pointer(b0), c.pointer(b1))
     L.ibwa_gpu_init.argtypes = [c.c_void_p, c.c_int]
+    L.ibwa_gpu_init_ex.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int]
     L.bwa_cal_sa_reg_gap.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.POINTER(E.GapOpt)]
     L.bwa_cal_sa_reg_gap.restype = None
+    return L, libc, bw
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["r100.default", "mixed.default", "mixed.n0", "r150.default", "mixed.c"])
+def test_dropin_matches_golden_sai(golden_dir, sai_manifest, key):
+    keep = []
+    L, libc, bw = _dropin_setup(golden_dir, keep)
     assert L.ibwa_gpu_init(bw, 1) == 0
     try:
-        m = sai_manifest[key]
-        opt, _ = oracle.parse_aln_args(m["argv"])
-        recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
-        seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
-        n = lens.size
-        arr = (RefSeq * n)()
-        for i in range(n):
-            s = seqs[int(offs[i]):int(offs[i]) + int(lens[i])]
-            p = libc.malloc(max(1, s.size))
-            c.memmove(p, s.ctypes.data, s.size)
-            arr[i].seq = p
-            arr[i].rseq = libc.malloc(max(1, s.size))  # content unused by the engine; freed by it
-            arr[i].qual = libc.malloc(8)
-            arr[i].name = libc.malloc(8)
-            arr[i].len = int(lens[i])
-            arr[i].tid = -1
-            arr[i].sa = 7
-            arr[i].type = 3
-        eo = E.GapOpt()
-        for f, _ in E.GapOpt._fields_:
-            setattr(eo, f, getattr(opt, f))
-        L.bwa_cal_sa_reg_gap(0, bw, n, arr, c.byref(eo))
-        n_aln = np.array([arr[i].n_aln for i in range(n)], dtype=np.int32)
-        parts = [c.string_at(arr[i].aln, 16 * arr[i].n_aln) for i in range(n)]
-        alns = np.frombuffer(b"".join(parts), dtype=oracle.ALN_DTYPE)
-        assert all(arr[i].seq is None and arr[i].rseq is None and arr[i].qual is None and arr[i].name is None
-                   for i in range(n))
-        assert all(arr[i].sa == 0 and arr[i].type == 0 and arr[i].c1 == 0 and arr[i].c2 == 0 for i in range(n))
-        got = oracle.sai_bytes(opt, n_aln, alns)
-        exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+        got, exp = _dropin_run(L, libc, bw, golden_dir, sai_manifest, key)
         assert oracle.sai_body_equal(got, exp), key
-        for i in range(n):
-            libc.free(c.c_void_p(arr[i].aln))
+    finally:
+        L.ibwa_gpu_destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slices,min_slice", [(3, 16), (5, 32), (4, 400)])
+def test_dropin_sliced_batch(golden_dir, sai_manifest, slices, min_slice):
+    """configs[3]'s split on one GPU: the drop-in cuts a batch into `slices` contiguous slices
+    (concurrent engines on device 0).  reads_mixed (17-250 bp) gives every slice its own max
+    length, so the .sai matches the golden only if each slice keeps the batch-level max_len
+    clamps of bwtaln.c:86-93 (max_gapo, the stack size); -n 0 takes the exact path (and its
+    derived jump arrays) per slice."""
+    keep = []
+    L, libc, bw = _dropin_setup(golden_dir, keep)
+    assert L.ibwa_gpu_init_ex(bw, 1, slices, min_slice) == 0
+    try:
+        bad = []
+        for key in ["mixed.default", "mixed.n3o2e3", "mixed.N", "mixed.n0", "mixed.l1000", "mixed.q15",
+                    "r100.default", "r150.default"]:
+            got, exp = _dropin_run(L, libc, bw, golden_dir, sai_manifest, key)
+            if not oracle.sai_body_equal(got, exp):
+                bad.append(key)
+        assert not bad, bad
     finally:
         L.ibwa_gpu_destroy()
