@@ -47,4 +47,5 @@ def test_two_ranks_equal_one_batch(tmp_path, aln):
     assert b["n_aln"].size == 40000 and all(x["n_aln"].size == 20000 for x in a)
     assert (np.concatenate([x["n_aln"] for x in a]) == b["n_aln"]).all()
     assert (np.concatenate([x["alns"] for x in a]) == b["alns"]).all()
-    assert b["n_aln"].sum() > 30000  # most reads hit
+    # with 1 % substitutions most 100 bp reads have no exact hit; the gapped search places most
+    assert b["n_aln"].sum() > (10000 if aln else 30000)
