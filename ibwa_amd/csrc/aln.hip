@@ -151,9 +151,10 @@ __device__ __forceinline__ uint32_t strand_base(uint32_t c, int a, bool comp) {
 // registers and stored back to back (a lane's 128 B of widths leave in consecutive instructions,
 // so the L2 merges them into whole lines instead of 16 partial writes far apart).
 __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView ixb, int L, const uint8_t *s, bool comp,
-                                           uint2 *wa, uint2 *wb) {
+                                           uint2 *wa, uint2 *wb, uint32_t *lw = nullptr) {
   uint32_t ka = 0, la = ixa.seq_len, kb = 0, lb = ixb.seq_len;
   uint32_t bida = 0, bidb = 0;
+  uint32_t lwa = 0, lwb = 0;  // sum of log2(width) over the positions (diagnostics)
   for (int base = 0; base < L; base += 16) {
     uint2 ba[16], bb[16];
 #pragma unroll
@@ -173,6 +174,7 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
         }
         if (ka > la || ca > 3) { ka = 0; la = ixa.seq_len; ++bida; }
         ba[t] = make_uint2(la - ka + 1, bida);
+        lwa += 31 - __builtin_clz(la - ka + 1);
         if (cb < 4) {
           uint32_t ok, ol;
           occ2_from1(fb, cb, ok, ol);
@@ -181,6 +183,7 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
         }
         if (kb > lb || cb > 3) { kb = 0; lb = ixb.seq_len; ++bidb; }
         bb[t] = make_uint2(lb - kb + 1, bidb);
+        lwb += 31 - __builtin_clz(lb - kb + 1);
       }
     }
 #pragma unroll
@@ -192,6 +195,12 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
   }
   wa[L] = make_uint2(0u, bida + 1);
   wb[L] = make_uint2(0u, bidb + 1);
+  if (lw) {
+    lw[0] = lwa;
+    lw[1] = lwb;
+    lw[2] = bida;
+    lw[3] = bidb;
+  }
 }
 
 __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
@@ -209,6 +218,17 @@ __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
     uint32_t nN = 0;
     for (int j = 0; j < L; ++j) nN += s[j] > 3;
     A.nN[lane] = (uint16_t)(nN > 0xFFFFu ? 0xFFFFu : nN);
+  }
+  if (A.feat) {
+    // search-cost features: sum of log2(width) over both full-length chains, and the seed's
+    uint32_t f[4] = {0, 0, 0, 0}, g[4] = {0, 0, 0, 0};
+    width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, f);
+    if (L > A.o.seed_len) width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1, g);
+    A.feat[lane * 4 + 0] = (uint16_t)(f[0] + f[1]);
+    A.feat[lane * 4 + 1] = (uint16_t)(g[0] + g[1]);
+    A.feat[lane * 4 + 2] = (uint16_t)(f[2] < f[3] ? f[2] : f[3]);
+    A.feat[lane * 4 + 3] = (uint16_t)(g[2] < g[3] ? g[2] : g[3]);
+    return;
   }
   width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1);
   if (L > A.o.seed_len) width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1);

@@ -253,9 +253,82 @@ void rev_copy(const uint8_t *src, int len, bool comp, uint8_t *dst) {
 }
 }  // namespace
 
+namespace {
+// the packed references of a dbset, concatenated at their offsets (dbset_extract_sequence,
+// dbset.c:306-325): base x is in the last segment starting at or before x
+struct PacSeg {
+  const uint8_t *pac;
+  uint64_t offset, l_pac;
+};
+struct PacSet {
+  std::vector<PacSeg> seg;
+  uint64_t l_pac = 0;
+  uint8_t at(uint64_t x) const {
+    size_t j = seg.size() - 1;
+    while (j > 0 && seg[j].offset > x) --j;
+    const uint64_t p = x - seg[j].offset;
+    if (p >= seg[j].l_pac) return 0;  // a hole between references (the reference stops there)
+    return (seg[j].pac[p >> 2] >> ((~p & 3) << 1)) & 3;  // bns_pac (bntseq.h)
+  }
+};
+
+int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                   const ibwa_ref_isize_info_t *ii, const PacSet &ps, uint64_t n_tot[2], uint64_t n_mapped[2]);
+}  // namespace
+
 int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
                    const ibwa_ref_isize_info_t *ii, const uint8_t *pac, uint64_t l_pac, uint64_t n_tot[2],
                    uint64_t n_mapped[2]) {
+  PacSet ps;
+  ps.seg.push_back({pac, 0, l_pac});
+  ps.l_pac = l_pac;
+  return paired_sw_core(ctx, n_seqs, seqs, popt, ii, ps, n_tot, n_mapped);
+}
+
+void bwa_paired_sw(ibwa_ref_dbset_t *dbs, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                   const ibwa_ref_isize_info_t *ii) {
+  uint64_t n_tot[2] = {0, 0}, n_mapped[2] = {0, 0};
+  if (popt->is_sw && ii->avg >= 0.0) {  // bwasw.c:279
+    // dbset_load_pac (dbset.c:199-207) without touching the caller's seq_t
+    PacSet ps;
+    std::vector<std::vector<uint8_t>> own(dbs->count);
+    for (int i = 0; i < dbs->count; ++i) {
+      const ibwa_ref_seqt_t *sq = dbs->bns[i];
+      const uint64_t lp = (uint64_t)sq->bns->l_pac;
+      const uint8_t *data = sq->data;
+      if (!data) {  // seq_load_pac (dbset.c:103-108)
+        own[i].assign(lp / 4 + 1, 0);
+        rewind(sq->bns->fp_pac);
+        if (fread(own[i].data(), 1, own[i].size(), sq->bns->fp_pac) == 0 && lp) die("reading the .pac", IBWA_EIO);
+        data = own[i].data();
+      }
+      ps.seg.push_back({data, dbs->db[i]->offset, lp});
+    }
+    ps.l_pac = dbs->l_pac;
+    std::lock_guard<std::mutex> lk(g_mu);
+    ibwa_ctx_t *ctx = g_ctx.empty() ? nullptr : g_ctx[0];
+    ibwa_ctx_t *own_ctx = nullptr;
+    if (!ctx) {
+      if (int rc = ibwa_ctx_create(0, &own_ctx)) die("ibwa_ctx_create", rc);
+      ctx = own_ctx;
+    }
+    const int rc = paired_sw_core(ctx, n_seqs, seqs, popt, ii, ps, n_tot, n_mapped);
+    if (own_ctx) ibwa_ctx_destroy(own_ctx);
+    if (rc) die("bwa_paired_sw", rc);
+    // bwasw.c:296-299
+    fprintf(stderr, "[bwa_paired_sw] %lld out of %lld Q%d singletons are mated.\n", (long long)n_mapped[1],
+            (long long)n_tot[1], 17);
+    fprintf(stderr, "[bwa_paired_sw] %lld out of %lld Q%d discordant pairs are fixed.\n", (long long)n_mapped[0],
+            (long long)n_tot[0], 17);
+  }
+}
+
+}  // extern "C"
+
+namespace {
+int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                   const ibwa_ref_isize_info_t *ii, const PacSet &ps, uint64_t n_tot[2], uint64_t n_mapped[2]) {
+  const uint64_t l_pac = ps.l_pac;
   n_tot[0] = n_tot[1] = n_mapped[0] = n_mapped[1] = 0;
   if (!popt->is_sw || ii->avg < 0.0) return 0;  // bwasw.c:279
   const bool std_pe = popt->type == IBWA_PET_STD;
@@ -312,10 +385,7 @@ int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
       if (rl >= 20 && b >= 0 && (uint64_t)b < l_pac) {
         got = (uint32_t)std::min<uint64_t>((uint64_t)rl, l_pac - (uint64_t)b);
         rbuf.resize(r0 + got);
-        for (uint32_t j = 0; j < got; ++j) {
-          const uint64_t x = (uint64_t)b + j;
-          rbuf[r0 + j] = (pac[x >> 2] >> ((~x & 3) << 1)) & 3;  // bns_pac (bntseq.h)
-        }
+        for (uint32_t j = 0; j < got; ++j) rbuf[r0 + j] = ps.at((uint64_t)b + j);
       }
       cand.push_back({i, k});
       qoff.push_back(q0); qlen.push_back((uint32_t)L);
@@ -413,4 +483,4 @@ int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
   return 0;
 }
 
-}  // extern "C"
+}  // namespace

@@ -43,6 +43,7 @@ struct AlnArgs {
   uint32_t aln_cap;
   uint32_t *status;          // per lane ST_* flags
   uint16_t *nN;              // per lane N count (k_width output, may be null)
+  uint16_t *feat;            // per lane 4 search-cost features (k_width output, diagnostics, may be null)
   AlnOpt o;
 };
 

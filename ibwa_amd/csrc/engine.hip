@@ -136,6 +136,8 @@ struct ibwa_ctx {
   bool prof_phases = getenv("IBWA_PROF_PHASES") != nullptr;  // diagnostics kernel variant
   int sw_stop_after = getenv("IBWA_SW_STOP") ? atoi(getenv("IBWA_SW_STOP")) : 0;  // diagnostics
   DBuf d_prof;
+  int diag = 0;                      // option: keep per-read first-pass iterations and k_width features
+  DBuf d_feat;
   unsigned long long stream_len = 0;  // hit-stream records written by the first pass (<= stream_total)
   unsigned long long stream_total = 0;  // hit-stream slots of the last first-pass launch
   uint32_t gap_stream_per_read = 4;     // first-pass hit-stream slots per read
@@ -346,6 +348,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
   else if (k == "jump_derive") c->jump_derive = value != 0;
+  else if (k == "diag") c->diag = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
@@ -851,9 +854,13 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.max_iters = c->gap_iter_budget;
       G.early_iters = c->gap_early_iters;
       G.early_entries = c->gap_early_entries;
-      if (c->verbose) {
+      if (c->verbose || c->diag) {
         if (int rc = c->d_iters.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
         G.iters = c->d_iters.as<uint32_t>() + b0;
+      }
+      if (c->diag) {
+        if (int rc = c->d_feat.ensure(std::max<int64_t>(n, 1) * 8)) return rc;
+        B.feat = c->d_feat.as<uint16_t>() + b0 * 4;
       }
       if (c->prof_phases) {
         if (int rc = c->d_prof.ensure(128)) return rc;
@@ -1251,6 +1258,16 @@ int ibwa_batch_retry_info(const ibwa_ctx_t *c, int64_t *ids, uint8_t *pass, int6
     if (pass) pass[j] = j < (int64_t)c->retry_pass.size() ? c->retry_pass[j] : 0;
   }
   if (n) *n = m;
+  return 0;
+}
+
+int ibwa_batch_diag(const ibwa_ctx_t *c, int what, void *out, uint64_t cap_bytes) {
+  const uint64_t need = what == 0 ? (uint64_t)c->n * 4 : (uint64_t)c->n * 8;
+  if (!c->diag || (what != 0 && what != 1)) return fail(IBWA_EINVAL, "set option diag=1 before the run; what = 0 or 1");
+  if (cap_bytes < need) return fail(IBWA_EINVAL, "diag buffer too small");
+  if (c->n == 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(out, (what == 0 ? c->d_iters : c->d_feat).p, need, hipMemcpyDeviceToHost));
   return 0;
 }
 

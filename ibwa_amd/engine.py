@@ -88,6 +88,7 @@ CAPI = {
     "ibwa_ctx_set_tuning": (_i, [_vp, _i, _i, _i]),
     "ibwa_aln_parse_args": (_i, [_i, c.POINTER(c.c_char_p), c.POINTER(GapOpt), c.POINTER(_i), c.POINTER(c.c_char_p)]),
     "ibwa_batch_retry_info": (_i, [_vp, _vp, _vp, _i64, c.POINTER(_i64)]),
+    "ibwa_batch_diag": (_i, [_vp, _i, _vp, _u64]),
     "ibwa_ctx_set_option": (_i, [_vp, c.c_char_p, c.c_long]),
     "ibwa_occ4": (_i, [_vp, _i, _i64, _vp, _vp]),
     "ibwa_ctx_load_sa": (_i, [_vp, _i, _u32, _vp, _u64]),
@@ -230,6 +231,14 @@ class Engine:
         ps = np.zeros(n.value, np.uint8)
         _chk(lib().ibwa_batch_retry_info(self.h, ids.ctypes.data, ps.ctypes.data, n.value, c.byref(n)))
         return ids, ps
+
+    def diag(self):
+        """(first-pass iterations uint32[n], k_width features uint16[n, 4]) of the last run (option diag=1)."""
+        it = np.zeros(self.n, np.uint32)
+        ft = np.zeros((self.n, 4), np.uint16)
+        _chk(lib().ibwa_batch_diag(self.h, 0, it.ctypes.data, it.nbytes))
+        _chk(lib().ibwa_batch_diag(self.h, 1, ft.ctypes.data, ft.nbytes))
+        return it, ft
 
     def stats(self):
         st = RunStats()

@@ -161,6 +161,12 @@ int ibwa_aln_parse_args(int argc, char *const *argv, ibwa_gap_opt_t *opt, int *n
  */
 int ibwa_batch_retry_info(const ibwa_ctx_t *ctx, int64_t *ids, uint8_t *pass, int64_t cap, int64_t *n);
 
+/* Diagnostics of the last ibwa_batch_run with option "diag" = 1 (gapped path): what 0 = first-pass
+ * iterations per read (uint32[n]); 1 = k_width's search-cost features per read (uint16[n][4]:
+ * sum of log2 width over both full-length chains, the same over the seed chains, the smaller
+ * restart count of the two full chains, of the two seed chains). */
+int ibwa_batch_diag(const ibwa_ctx_t *ctx, int what, void *out, uint64_t cap_bytes);
+
 /* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */
 int ibwa_ctx_set_tuning(ibwa_ctx_t *ctx, int stack_cap, int aln_cap, int block);
 

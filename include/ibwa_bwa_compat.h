@@ -16,6 +16,7 @@
 #ifndef IBWA_BWA_COMPAT_H
 #define IBWA_BWA_COMPAT_H
 #include <stdint.h>
+#include <stdio.h>
 
 #include "ibwa_aln.h"
 
@@ -96,6 +97,60 @@ typedef struct {
 	uint32_t low, high, high_bayesian;
 } ibwa_ref_isize_info_t;
 
+/* bntann1_t / bntamb1_t / bntseq_t (bntseq.h:40-62) */
+typedef struct {
+	int64_t offset;
+	int32_t len;
+	int32_t n_ambs;
+	uint32_t gi;
+	char *name, *anno;
+} ibwa_ref_bntann1_t;
+typedef struct {
+	int64_t offset;
+	int32_t len;
+	char amb;
+} ibwa_ref_bntamb1_t;
+typedef struct {
+	int64_t l_pac;
+	int32_t n_seqs;
+	uint32_t seed;
+	ibwa_ref_bntann1_t *anns;
+	int32_t n_holes;
+	ibwa_ref_bntamb1_t *ambs;
+	FILE *fp_pac;                  /* the .pac, read by seq_load_pac (dbset.c:103-108) */
+} ibwa_ref_bntseq_t;
+
+/* seq_t (bwaremap.h:24-29): one reference's metadata, its packed sequence once loaded, and the
+ * compound-sequence remappings (opaque here) */
+typedef struct {
+	ibwa_ref_bntseq_t *bns;
+	uint8_t *data;                 /* l_pac / 4 + 1 bytes (dbset_load_pac), or NULL */
+	int remap;
+	void **mappings;               /* bnsremap_t ** */
+} ibwa_ref_seqt_t;
+
+/* bwtdb_t (dbset.h:12-19) */
+typedef struct {
+	const char *prefix;
+	ibwa_ref_bwt_t *bwt[2];
+	void *bwtcache;                /* bwtcache_t * */
+	uint64_t offset;               /* of this reference in the concatenated coordinates */
+	ibwa_ref_seqt_t *bns;
+	ibwa_ref_seqt_t *ntbns;
+} ibwa_ref_bwtdb_t;
+
+/* dbset_t (dbset.h:21-30): the primary reference and the alternates of `sampe`, concatenated */
+typedef struct {
+	int count;
+	int color_space;
+	int preload;
+	ibwa_ref_bwtdb_t **db;
+	ibwa_ref_seqt_t **bns;
+	ibwa_ref_seqt_t **ntbns;
+	uint64_t l_pac;                /* sum of every reference's l_pac */
+	uint64_t total_bwt_seq_len[2];
+} ibwa_ref_dbset_t;
+
 /*
  * Bring the index of a running `aln` onto the GPUs (called by
  * bwa_aln_core after bwt_restore_bwt, bwtaln.c:189).  n_gpus <= 0: every
@@ -156,6 +211,20 @@ int ibwa_sw_core_batch(ibwa_ctx_t *ctx, int64_t n, const uint8_t *seq, const uin
 int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
                    const ibwa_ref_isize_info_t *ii, const uint8_t *pac, uint64_t l_pac, uint64_t n_tot[2],
                    uint64_t n_mapped[2]);
+
+/*
+ * bwa_paired_sw (bwasw.h:12, bwasw.c:270-304) with the reference's own signature: a reference
+ * `sampe` links this in place of bwasw.o.  The references of `dbs` are concatenated at their
+ * db->offset as dbset_extract_sequence (dbset.c:306-325) reads them; each one's packed
+ * sequence is taken from seq_t.data when loaded, else read from its .pac (bntseq_t.fp_pac)
+ * as dbset_load_pac does -- neither is modified.  The SW runs on the engine of device 0 that
+ * ibwa_gpu_init made (or a new one).  Prints the reference's two stderr summary lines; a HIP
+ * failure is reported and abort()s, like the reference's allocation failures.
+ */
+#ifndef BWASW_H
+void bwa_paired_sw(ibwa_ref_dbset_t *dbs, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                   const ibwa_ref_isize_info_t *ii);
+#endif
 
 #ifdef __cplusplus
 }

@@ -38,6 +38,7 @@ LAYOUT_C = r"""
 #include <stddef.h>
 #include "bwtaln.h"
 #include "bwapair.h"
+#include "dbset.h"
 #include "ibwa_bwa_compat.h"
 #define SAME(R, M, F) _Static_assert(offsetof(R, F) == offsetof(M, F), #R "." #F); \
                       _Static_assert(sizeof(((R *)0)->F) == sizeof(((M *)0)->F), #R "." #F " size");
@@ -71,6 +72,21 @@ SIZE(isize_info_t, ibwa_ref_isize_info_t)
 SAME(isize_info_t, ibwa_ref_isize_info_t, avg) SAME(isize_info_t, ibwa_ref_isize_info_t, std)
 SAME(isize_info_t, ibwa_ref_isize_info_t, ap_prior) SAME(isize_info_t, ibwa_ref_isize_info_t, low)
 SAME(isize_info_t, ibwa_ref_isize_info_t, high) SAME(isize_info_t, ibwa_ref_isize_info_t, high_bayesian)
+SIZE(bntann1_t, ibwa_ref_bntann1_t) SAME(bntann1_t, ibwa_ref_bntann1_t, offset) SAME(bntann1_t, ibwa_ref_bntann1_t, gi)
+SAME(bntann1_t, ibwa_ref_bntann1_t, name) SAME(bntann1_t, ibwa_ref_bntann1_t, anno)
+SIZE(bntamb1_t, ibwa_ref_bntamb1_t) SAME(bntamb1_t, ibwa_ref_bntamb1_t, amb)
+SIZE(bntseq_t, ibwa_ref_bntseq_t) SAME(bntseq_t, ibwa_ref_bntseq_t, l_pac) SAME(bntseq_t, ibwa_ref_bntseq_t, n_seqs)
+SAME(bntseq_t, ibwa_ref_bntseq_t, anns) SAME(bntseq_t, ibwa_ref_bntseq_t, n_holes) SAME(bntseq_t, ibwa_ref_bntseq_t, ambs)
+SAME(bntseq_t, ibwa_ref_bntseq_t, fp_pac)
+SIZE(seq_t, ibwa_ref_seqt_t) SAME(seq_t, ibwa_ref_seqt_t, bns) SAME(seq_t, ibwa_ref_seqt_t, data)
+SAME(seq_t, ibwa_ref_seqt_t, remap) SAME(seq_t, ibwa_ref_seqt_t, mappings)
+SIZE(bwtdb_t, ibwa_ref_bwtdb_t) SAME(bwtdb_t, ibwa_ref_bwtdb_t, prefix) SAME(bwtdb_t, ibwa_ref_bwtdb_t, bwt)
+SAME(bwtdb_t, ibwa_ref_bwtdb_t, bwtcache) SAME(bwtdb_t, ibwa_ref_bwtdb_t, offset) SAME(bwtdb_t, ibwa_ref_bwtdb_t, bns)
+SAME(bwtdb_t, ibwa_ref_bwtdb_t, ntbns)
+SIZE(dbset_t, ibwa_ref_dbset_t) SAME(dbset_t, ibwa_ref_dbset_t, count) SAME(dbset_t, ibwa_ref_dbset_t, color_space)
+SAME(dbset_t, ibwa_ref_dbset_t, preload) SAME(dbset_t, ibwa_ref_dbset_t, db) SAME(dbset_t, ibwa_ref_dbset_t, bns)
+SAME(dbset_t, ibwa_ref_dbset_t, ntbns) SAME(dbset_t, ibwa_ref_dbset_t, l_pac)
+SAME(dbset_t, ibwa_ref_dbset_t, total_bwt_seq_len)
 int main(void) { return 0; }
 """
 

@@ -76,3 +76,98 @@ def test_paired_sw_off(golden_dir, gpu_engine):
                      (E.PeOpt(type=1, is_sw=1), E.IsizeInfo(avg=-1, std=30, ap_prior=1e-5))):
         assert gpu_engine.paired_sw(s0, s1, popt, ii, pac, 1000000) == [0, 0, 0, 0]
     assert [row(x) for x in s0] + [row(x) for x in s1] == before
+
+
+class BntSeq(c.Structure):  # bntseq_t (bntseq.h:54-62)
+    _fields_ = [("l_pac", c.c_int64), ("n_seqs", c.c_int32), ("seed", c.c_uint32), ("anns", c.c_void_p),
+                ("n_holes", c.c_int32), ("ambs", c.c_void_p), ("fp_pac", c.c_void_p)]
+
+
+class SeqT(c.Structure):  # seq_t (bwaremap.h:24-29)
+    _fields_ = [("bns", c.POINTER(BntSeq)), ("data", c.c_void_p), ("remap", c.c_int), ("mappings", c.c_void_p)]
+
+
+class BwtDb(c.Structure):  # bwtdb_t (dbset.h:12-19)
+    _fields_ = [("prefix", c.c_char_p), ("bwt", c.c_void_p * 2), ("bwtcache", c.c_void_p), ("offset", c.c_uint64),
+                ("bns", c.POINTER(SeqT)), ("ntbns", c.POINTER(SeqT))]
+
+
+class DbSet(c.Structure):  # dbset_t (dbset.h:21-30)
+    _fields_ = [("count", c.c_int), ("color_space", c.c_int), ("preload", c.c_int), ("db", c.POINTER(c.POINTER(BwtDb))),
+                ("bns", c.POINTER(c.POINTER(SeqT))), ("ntbns", c.POINTER(c.POINTER(SeqT))), ("l_pac", c.c_uint64),
+                ("total_bwt_seq_len", c.c_uint64 * 2)]
+
+
+def _pack(codes):
+    """bns_dump's .pac body: 4 bases per byte, MSB first; l_pac / 4 + 1 bytes."""
+    out = np.zeros(codes.size // 4 + 1, np.uint8)
+    for j in range(4):
+        sub = codes[j::4].astype(np.uint8)
+        out[:sub.size] |= sub << (6 - 2 * j)
+    return out
+
+
+@pytest.mark.parametrize("name", ["std100", "solid50"])
+@pytest.mark.parametrize("cut", [None, 400003])
+def test_dropin_bwa_paired_sw(golden_dir, tmp_path, name, cut):
+    """bwa_paired_sw with the reference's signature over a dbset_t mirror: one reference, or the
+    same genome split into two references at `cut` (concatenated at db->offset, as
+    dbset_extract_sequence reads them; the first one preloaded in seq_t.data, the second read
+    through bntseq_t.fp_pac as dbset_load_pac does).  Same fields and CIGARs as the goldens."""
+    from ibwa_amd import _native
+    L = c.CDLL(_native.LIB_PATH)
+    libc = c.CDLL(None)
+    libc.fopen.restype = c.c_void_p
+    libc.fopen.argtypes = [c.c_char_p, c.c_char_p]
+    libc.fclose.argtypes = [c.c_void_p]
+    m = json.load(open(os.path.join(golden_dir, "psw_manifest.json")))[name]
+    pin, pout = oracle.read_psw(golden_dir, name)
+    s0, k0 = build_seqs([p[0] for p in pin])
+    s1, k1 = build_seqs([p[1] for p in pin])
+    codes, l_pac = oracle.read_pac(os.path.join(golden_dir, "g1m"))
+    codes = codes[:l_pac]
+    parts = [codes] if cut is None else [codes[:cut], codes[cut:]]
+    keep, fps = [], []
+    n = len(parts)
+    dbs = DbSet(count=n, l_pac=l_pac)
+    dbp = (c.POINTER(BwtDb) * n)()
+    sqp = (c.POINTER(SeqT) * n)()
+    off = 0
+    for i, part in enumerate(parts):
+        pac = _pack(part)
+        f = tmp_path / f"r{i}.pac"
+        pac.tofile(f)
+        bns = BntSeq(l_pac=part.size, n_seqs=1)
+        sq = SeqT(bns=c.pointer(bns))
+        if i == 0 and n == 2:
+            buf = c.create_string_buffer(pac.tobytes(), pac.size)
+            keep.append(buf)
+            sq.data = c.cast(buf, c.c_void_p)
+        else:
+            fp = libc.fopen(str(f).encode(), b"rb")
+            fps.append(fp)
+            bns.fp_pac = fp
+        db = BwtDb(offset=off, bns=c.pointer(sq))
+        keep += [bns, sq, db]
+        dbp[i] = c.pointer(db)
+        sqp[i] = c.pointer(sq)
+        off += part.size
+    dbs.db = dbp
+    dbs.bns = sqp
+    popt = E.PeOpt(type=m["type"], is_sw=1, n_threads=1)
+    ii = E.IsizeInfo(avg=m["avg"], std=m["std"], ap_prior=m["ap_prior"])
+    L.bwa_paired_sw.argtypes = [c.POINTER(DbSet), c.c_int, c.c_void_p, c.POINTER(E.PeOpt), c.POINTER(E.IsizeInfo)]
+    L.bwa_paired_sw.restype = None
+    arr = (c.POINTER(E.RefSeq) * 2)(c.cast(s0, c.POINTER(E.RefSeq)), c.cast(s1, c.POINTER(E.RefSeq)))
+    L.bwa_paired_sw(c.byref(dbs), len(pin), arr, c.byref(popt), c.byref(ii))
+    for fp in fps:
+        libc.fclose(fp)
+    assert all(sqp[i].contents.data == (c.cast(keep[0], c.c_void_p).value if (i == 0 and n == 2) else None)
+               for i in range(n))  # the caller's seq_t untouched
+    bad = []
+    for i, q in enumerate(pout):
+        for k, a in ((0, s0), (1, s1)):
+            exp = tuple(q[k][f] for f in oracle.PSW_OUT)
+            if row(a[i]) != exp:
+                bad.append((i, k, row(a[i]), exp))
+    assert not bad, bad[:3]
