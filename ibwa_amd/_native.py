@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libibwa_amd.so")
+# IBWA_LIB: another build of the same library (same-box A/B measurements in tools/)
+LIB_PATH = os.environ.get("IBWA_LIB") or os.path.join(_HERE, "lib", "libibwa_amd.so")
 BIN_PATH = os.path.join(_HERE, "bin", "ibwa-amd")
 _lib = None
 

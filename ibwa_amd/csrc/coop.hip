@@ -148,6 +148,7 @@ struct Shm {
 
 }  // namespace
 
+template <bool PROF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_coop(CoopArgs A,
                                                                                      unsigned long long *counter) {
   __shared__ Shm S;
@@ -170,6 +171,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
   uint32_t *const freel = A.freel + wave * (uint64_t)A.freecap;
   uint4 *const hitv = A.hits + wave * (uint64_t)A.hcap;
   uint32_t n_free = 0;  // pages on this wave's free stack (kept across reads)
+  // diagnostics (A.prof): wave cycles per phase -- 0 hit barriers, 1 commits, 2 claims,
+  // 3 loads + consume, 4 level set-up / teardown, 5 read set-up; 6 iterations, 7 commits, 8 levels
+  const bool prof = PROF && A.prof != nullptr;
+  __shared__ unsigned long long pc[9];  // LDS: no registers taken from the hot loop
+  if (prof) {
+    if (lane < 9) pc[lane] = 0;
+    __syncthreads();
+  }
+  auto now = []() __attribute__((always_inline)) -> uint64_t { return __builtin_amdgcn_s_memtime(); };
+  uint64_t t_mark = prof ? now() : 0;
+  auto lap = [&](int ph) __attribute__((always_inline)) {
+    if (prof) {
+      const uint64_t t = now();
+      if (lane == 0) pc[ph] += t - t_mark;
+      t_mark = t;
+    }
+  };
 
   // take a page: this wave's free stack, else the global pool (NONE when exhausted)
   auto alloc_page = [&]() __attribute__((always_inline)) -> uint32_t {
@@ -262,6 +280,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       uint32_t stg_w = 0;   // this lane's staging write counter
       int s = 0;            // level (score bucket)
       bool done = status != 0;
+      lap(5);
       // ---------------------------------------------- levels
       while (!done) {
         while (s < o.n_stacks && S.nb[s] == 0) ++s;
@@ -283,6 +302,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           if (tg(q) < o.n_stacks)
             for (uint32_t j = lane; j < S.np[tg(q)]; j += 64) S.dirc[1 + q][j] = dir[tg(q) * MAXP + j];
         __syncthreads();
+        if (prof && lane == 0) ++pc[8];
+        lap(4);
         uint32_t next_c = 0, cp = 0, barrier = NONE;
         // lane chain state
         int lst = L_IDLE;
@@ -369,6 +390,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               next_c = newb + 1;
             }
           }
+          lap(0);
+          if (prof && lane == 0) ++pc[6];
           // finished chains from cp on, in pop order
           uint32_t ndone = 0;
           for (uint32_t base = cp; base < next_c; base += 64) {
@@ -385,6 +408,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           if (barrier != NONE && lim > barrier + 1 - cp) lim = barrier + 1 - cp;
           const bool at_barrier = barrier != NONE && cp + lim == barrier + 1;
           if (lim && (lim >= 32 || active == 0ull || at_barrier)) {
+            if (prof && lane == 0) ++pc[7];
             __threadfence_block();  // staging stores of earlier iterations are visible
             for (uint32_t base = 0; base < lim && !done; base += 64) {
               const uint32_t cc = cp + base + lane;
@@ -558,6 +582,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               }
             }
           }
+          lap(1);
           // (c) level finished
           if (cp == N && __ballot(lst != L_IDLE) == 0ull) break;
           // (d) claims: idle lanes take the next chains in pop order
@@ -580,6 +605,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             const uint32_t nw = (uint32_t)__popcll(wm);
             next_c += nw < avail ? nw : avail;
           }
+          lap(2);
           // ============================================ loads of this iteration (one round trip)
           const IndexView ix = a ? ixv0 : ixv1;  // strand a searches bwt[1-a]
           const uint4 *ob = a ? A.o64[0] : A.o64[1];
@@ -709,6 +735,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               end_chain(false, 0, 0);
             }
           }
+          lap(3);
         }
         if (done) break;
         // level s is consumed: its pages go back
@@ -733,6 +760,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       }
       __syncthreads();
     }
+    lap(4);
     // ------------------------------------------------ hits of the read to the stream
     int na = status ? 0 : n_aln;
     if (na) {
@@ -754,7 +782,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       if (A.iters) A.iters[ro] = n_iter;
     }
     __syncthreads();
+    lap(5);
   }
+  if (prof && lane == 0)
+    for (int q = 0; q < 9; ++q) atomicAdd(A.prof + q, (unsigned long long)pc[q]);
 }
 
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {
@@ -763,7 +794,8 @@ hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blo
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(g.pool_next, 0, sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_coop, dim3(blocks), dim3(64), 0, st, g, d_counter);
+  if (g.prof) hipLaunchKernelGGL(k_coop<true>, dim3(blocks), dim3(64), 0, st, g, d_counter);
+  else hipLaunchKernelGGL(k_coop<false>, dim3(blocks), dim3(64), 0, st, g, d_counter);
   return hipGetLastError();
 }
 

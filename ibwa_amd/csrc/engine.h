@@ -131,6 +131,7 @@ struct CoopArgs {
   int32_t *n_aln;
   uint32_t *status;
   uint32_t *iters;
+  unsigned long long *prof;  // diagnostics: per-phase wave cycles (IBWA_PROF_PHASES), may be null
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);

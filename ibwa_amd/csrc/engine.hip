@@ -1051,6 +1051,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.iters = c->d_iters.as<uint32_t>();
     }
     K.o = o;
+    if (c->prof_phases) {
+      if (int rc = c->d_prof.ensure(128)) return rc;
+      HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 128, c->stream));
+      K.prof = c->d_prof.as<unsigned long long>();
+    }
     HIPCHK(hipMemsetAsync(K.aln_next, 0, 8, c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(launch_width(B, c->block, c->stream));
@@ -1058,6 +1063,17 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[4]));
     if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop kernel done\n", since());
+    if (c->prof_phases) {
+      unsigned long long pf[9];
+      HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
+      const char *nm[6] = {"barriers", "commits", "claims", "loads+consume", "levels", "read set-up"};
+      double tot = 0;
+      for (int q = 0; q < 6; ++q) tot += (double)pf[q];
+      fprintf(stderr, "[ibwa_amd] k_coop phases (wave cycles):");
+      for (int q = 0; q < 6; ++q) fprintf(stderr, " %s %.1f%%", nm[q], tot > 0 ? 100.0 * pf[q] / tot : 0.0);
+      fprintf(stderr, "; %llu iterations (%.0f cycles each), %llu commits, %llu levels\n", pf[6],
+              pf[6] ? tot / pf[6] : 0.0, pf[7], pf[8]);
+    }
     float a = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
     ms_r += a;

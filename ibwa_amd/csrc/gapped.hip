@@ -359,6 +359,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           ent1[0] = E::make(0u, ixv0.seq_len, len, 0, NILH, 0, 0, 0, 0, STATE_M);
           C = E::make(0u, ixv0.seq_len, len, 0, 0u, 0, 0, 0, 1, STATE_M);
           ent1[1] = C;
+          // every bucket head starts empty (a pop that empties a bucket writes NIL back), so a
+          // push reads its bucket's head without consulting the non-empty mask
+          for (int b = 1; b < o.n_stacks; ++b) lds_heads[((b) << nbl) + ltid] = (H)NILH;
           lds_heads[ltid] = 1;
           nonempty.m0 = 1u;
           nonempty.m1 = nonempty.m2 = nonempty.m3 = 0u;
@@ -657,50 +660,79 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           }
         }
       }
-      // push each child: link into bucket `sc`, keep C = head of the lowest non-empty bucket
-      const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
-      const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
-      while (vm) {
-        if (pleader()) ++pf5;
-        const uint32_t j = (uint32_t)__builtin_ctz(vm);
-        vm &= vm - 1;
-        const bool is_ins = j == 0, is_del = j - 1 < 4, is_sym = j >= 5;
-        const uint32_t c = is_del ? j - 1 : (csym + j - 4) & 3;
-        const uint32_t pk = is_ins ? k : pick4(KK, c);
-        const uint32_t pl = is_ins ? l : pick4(LL, c);
-        const bool gap = !is_sym, open = gap && state == STATE_M;
-        const int is_mm = is_sym && (j != 8 || csym > 3);
-        const int n_mm = e_mm + is_mm, n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (gap && !open ? 1 : 0);
-        const int pi = is_del ? ni + 1 : ni;
-        const int pstate = is_ins ? STATE_I : is_del ? STATE_D : STATE_M;
-        const int pldp = is_sym && !is_mm ? ldp : pi;
-        const int sc = sc_base + (is_sym ? (is_mm ? o.s_mm : 0) : sc_gap);
-        if (sc >= o.n_stacks) { status |= ST_BAD_SCORE; break; }
-        if (n_mm > 31 || n_gapo > 7 || n_gape > 15) { status |= ST_STACK_OVERFLOW; break; }
-        uint32_t slot;
-        if (n_free) {
-          --n_free;
-          slot = free_slots[((n_free) << nbl) + ltid];
-        } else if (fl_known && fl_head != NILH) {
-          slot = fl_head;
-          fl_head = fl_next;
-          fl_known = fl_head == NILH;
-        } else {
-          if (bump == P0 - HS) bump = P0;  // skip the hit area
-          slot = bump++;
+      // push each child (bwtgap.c:216-258, in the reference's order): link it into its bucket and
+      // keep C = head of the lowest non-empty bucket.  The children of one expansion go to at most
+      // three buckets -- gaps (sc_base + open/extend penalty), mismatches (+ s_mm), the match child
+      // (sc_base) -- so the limits, the slot allocation and the non-empty mask are settled once per
+      // expansion and each trip of the loop is branch-free.
+      if (vm) {
+        const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
+        const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
+        const int scG = sc_base + sc_gap, scMM = sc_base + o.s_mm;
+        const bool has_match = (vm & 0x100u) && csym < 4;
+        const uint32_t vm_mm = vm & (has_match ? 0xE0u : 0x1E0u);  // mismatch children
+        const bool has_gap = (vm & 0x1Fu) != 0, has_mm = vm_mm != 0;
+        const bool open = state == STATE_M;
+        if ((has_gap && scG >= o.n_stacks) || (has_mm && scMM >= o.n_stacks) || (has_match && sc_base >= o.n_stacks)) {
+          status |= ST_BAD_SCORE;
+          vm = 0;
+        } else if ((has_mm && e_mm + 1 > 31) || (has_gap && open && e_go + 1 > 7) || (has_gap && !open && e_ge + 1 > 15)) {
+          status |= ST_STACK_OVERFLOW;
+          vm = 0;
         }
-        // an empty bucket's head is stale: the new entry ends its list
-        const uint32_t hd = bm_has(nonempty, sc) ? (uint32_t)lds_heads[((sc) << nbl) + ltid] : NILH;
-        const uint4 ne = E::make(pk, pl, pi, pldp, hd, n_mm, n_gapo, n_gape, a, pstate);
-        *slot_ptr(slot) = ne;
-        lds_heads[((sc) << nbl) + ltid] = (H)slot;
-        bm_set(nonempty, sc);
-        ++n_entries;
-        if (!C_valid || sc <= C_b) {
-          C = ne;
-          C_slot = slot;
-          C_b = sc;
+        const uint32_t npush = (uint32_t)__builtin_popcount(vm);
+        const uint32_t n_fs = npush < n_free ? npush : n_free;  // from the LDS free stack, top down
+        const bool use_fl = npush > n_fs && fl_head != NILH;    // one slot of the free list (fl_known)
+        const uint32_t fs_top = n_free, fl_slot = fl_head, b0 = bump, skip_at = P0 - HS;
+        const uint32_t fl_n = use_fl ? 1u : 0u;
+        uint32_t t = 0;
+        while (vm) {
+          if (pleader()) ++pf5;
+          const uint32_t j = (uint32_t)__builtin_ctz(vm);
+          vm &= vm - 1;
+          const bool is_ins = j == 0, is_del = j - 1 < 4, is_gap = j < 5;
+          const bool is_match = j == 8 && csym < 4;
+          const uint32_t c = is_del ? j - 1 : (csym + j - 4) & 3;
+          const uint32_t pk = is_ins ? k : pick4(KK, c);
+          const uint32_t pl = is_ins ? l : pick4(LL, c);
+          const int n_mm = e_mm + (!is_gap && !is_match ? 1 : 0);
+          const int n_gapo = e_go + (is_gap && open ? 1 : 0), n_gape = e_ge + (is_gap && !open ? 1 : 0);
+          const int pi = is_del ? ni + 1 : ni;
+          const int pstate = is_ins ? STATE_I : is_del ? STATE_D : STATE_M;
+          const int pldp = is_match ? ldp : pi;
+          const int sc = is_gap ? scG : is_match ? sc_base : scMM;
+          // slot: free stack, then the free list's head, then the bump region (skipping the hit area)
+          const uint32_t fsv = free_slots[((t < n_fs ? fs_top - 1 - t : 0u) << nbl) + ltid];
+          uint32_t bs = b0 + (t - n_fs - fl_n);
+          bs += (b0 <= skip_at && bs >= skip_at) ? HS : 0u;
+          const uint32_t slot = t < n_fs ? (uint32_t)fsv : (t == n_fs && use_fl) ? fl_slot : bs;
+          const uint32_t hd = (uint32_t)lds_heads[((sc) << nbl) + ltid];  // NIL when the bucket is empty
+          const uint4 ne = E::make(pk, pl, pi, pldp, hd, n_mm, n_gapo, n_gape, a, pstate);
+          *slot_ptr(slot) = ne;
+          lds_heads[((sc) << nbl) + ltid] = (H)slot;
+          const bool take = !C_valid || sc <= C_b;
+          // per component: a select of two uint4 aggregates is lowered to an indexed scratch access
+          C.x = take ? ne.x : C.x;
+          C.y = take ? ne.y : C.y;
+          C.z = take ? ne.z : C.z;
+          C.w = take ? ne.w : C.w;
+          C_slot = take ? slot : C_slot;
+          C_b = take ? sc : C_b;
           C_valid = true;
+          ++t;
+        }
+        if (t) {
+          n_free -= n_fs;
+          if (use_fl) {
+            fl_head = fl_next;
+            fl_known = fl_head == NILH;  // the next head's successor is loaded next iteration
+          }
+          const uint32_t nb = t - n_fs - fl_n;
+          bump = b0 + nb + ((nb && b0 <= skip_at && b0 + nb > skip_at) ? HS : 0u);
+          n_entries += (int)t;
+          if (has_match) bm_set(nonempty, sc_base);
+          if (has_mm) bm_set(nonempty, scMM);
+          if (has_gap) bm_set(nonempty, scG);
         }
       }
       if (pl_) ++pf8;
