@@ -285,6 +285,18 @@ int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
   return paired_sw_core(ctx, n_seqs, seqs, popt, ii, ps, n_tot, n_mapped);
 }
 
+int ibwa_paired_sw_dbs(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                       const ibwa_ref_isize_info_t *ii, int n_db, const uint8_t *const *pac, const uint64_t *offset,
+                       const uint64_t *l_pac, uint64_t n_tot[2], uint64_t n_mapped[2]) {
+  PacSet ps;
+  for (int i = 0; i < n_db; ++i) {
+    ps.seg.push_back({pac[i], offset[i], l_pac[i]});
+    ps.l_pac = std::max<uint64_t>(ps.l_pac, offset[i] + l_pac[i]);
+  }
+  if (ps.seg.empty()) return IBWA_EINVAL;
+  return paired_sw_core(ctx, n_seqs, seqs, popt, ii, ps, n_tot, n_mapped);
+}
+
 void bwa_paired_sw(ibwa_ref_dbset_t *dbs, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
                    const ibwa_ref_isize_info_t *ii) {
   uint64_t n_tot[2] = {0, 0}, n_mapped[2] = {0, 0};

@@ -20,6 +20,7 @@
 
 #include "ibwa_aln.h"
 #include "readers.h"
+#include "remap.h"
 
 namespace ibwa_sam {
 
@@ -189,6 +190,148 @@ inline int coor_pac2real(const Bns &b, int64_t pac_coor, int len, int32_t *seqid
   return nn;
 }
 
+// ---------------------------------------------------------------- the database set (dbset.c)
+// sampe's references concatenated at their offsets (dbset_restore, dbset.c:135-176): the primary
+// first, then the alternates; an alternate may carry a .remap table (remap.h).  samse and a
+// single-reference sampe use a set of one.
+struct RefDb {
+  Bns bns;
+  uint64_t offset = 0;
+  int remap = 0;
+  std::vector<std::unique_ptr<Mapping>> mappings;  // per sequence, when remap
+};
+struct Dbs {
+  std::vector<RefDb> db;
+  uint64_t l_pac = 0;  // sum of the references' l_pac
+  // coord2idx (dbset.c:17-39)
+  int coord2idx(int64_t pos) const {
+    const int count = (int)db.size();
+    int left = 0, right = count, mid = 0;
+    if (pos > (int64_t)l_pac) return -1;
+    while (left < right) {
+      mid = (left + right) >> 1;
+      if (pos > (int64_t)db[mid].offset) {
+        if (mid == count - 1) break;
+        if (pos < (int64_t)db[mid + 1].offset) break;
+        left = mid + 1;
+      } else if (pos < (int64_t)db[mid].offset) {
+        right = mid;
+      } else {
+        break;
+      }
+    }
+    return mid;
+  }
+};
+
+// dbset_extract_sequence (dbset.c:306-325): the references read back to back
+inline uint32_t extract(const Dbs &d, uint64_t beg, uint32_t len, uint8_t *out) {
+  uint32_t total = 0;
+  while (total < len) {
+    if (beg >= d.l_pac) break;
+    const int idx = d.coord2idx((int64_t)beg);
+    const RefDb &r = d.db[idx];
+    uint64_t pos = beg - r.offset;
+    while (pos < (uint64_t)r.bns.l_pac && total < len) out[total++] = pac_at(r.bns, pos++);
+    beg = pos + r.offset;
+  }
+  return total;
+}
+
+// dbset_coor_pac2real (dbset.c:248-255): the sequence (and reference) holding pac_coor
+inline int coor_pac2real(const Dbs &d, int64_t pac_coor, int len, int32_t *seqid, int *dbi) {
+  const int idx = d.coord2idx(pac_coor);
+  if (idx < 0) err_fatal("bns_seq_for_pos", "bug! Coordinate is longer than sequence (%lld>=%lld).", (long long)pac_coor,
+                         (long long)d.l_pac);
+  *dbi = idx;
+  return coor_pac2real(d.db[idx].bns, pac_coor - (int64_t)d.db[idx].offset, len, seqid);
+}
+
+// bns_seq_by_name (bntseq.c:269-276)
+inline int32_t seq_by_name(const Bns &b, const std::string &name) {
+  for (int32_t i = 0; i < b.n_seqs; ++i)
+    if (b.anns[i].name == name) return i;
+  return -1;
+}
+
+// bwa_remap_position_with_seqid (bwaremap.cpp:252-311): an alternate position (relative to its
+// reference) -> the target position in the primary; *status 1 on success
+inline uint64_t remap_position_with_seqid(const RefDb &r, const Bns &target, uint64_t pac_coor, int32_t seqid, int *status) {
+  *status = 0;
+  const Mapping *m = seqid >= 0 && seqid < (int32_t)r.mappings.size() ? r.mappings[seqid].get() : nullptr;
+  if (!m) err_fatal("bwa_remap_position_with_seqid", "No read mapping for sequence id %d\n", seqid);
+  const int32_t target_idx = seq_by_name(target, m->seqname);
+  if (target_idx < 0) err_fatal("bwa_remap_position_with_seqid", "Failed to locate remapping target: %s\n", m->seqname.c_str());
+  uint32_t rv = 0;
+  if (!m->exact) {
+    uint32_t offset = 0;
+    const uint32_t altpos = (uint32_t)(pac_coor - (uint64_t)r.bns.anns[seqid].offset);
+    if (!remap_cigar(m->cigar.c_str(), &offset, altpos, (uint32_t)r.bns.anns[seqid].len)) {
+      fprintf(stderr, "Failed to remap coordinates to %s (coord=%lu)", r.bns.anns[seqid].name.c_str(), (unsigned long)pac_coor);
+      return 0;
+    }
+    rv = m->start + offset;
+  } else {
+    rv = (uint32_t)(pac_coor - (uint64_t)r.bns.anns[seqid].offset);
+  }
+  if (!m->exact && (rv < m->start || rv > m->stop))
+    err_fatal("bwa_remap_position_with_seqid", "remapped position out of range (%u should be in [%u, %u])\n", rv, m->start,
+              m->stop);
+  *status = 1;
+  return rv + (uint64_t)target.anns[target_idx].offset;
+}
+
+// __remap (bwape.c:201-219, filter_alignments.cpp:15-34) for a hit at global position pos on
+// reference dbidx: its position in the primary (pos itself when the reference has no table)
+inline uint64_t remap_pos(const Dbs &d, int dbidx, uint64_t pos, uint64_t len, uint32_t gap, int32_t *seqid, int *identical,
+                          int *status) {
+  const RefDb &r = d.db[dbidx];
+  if (!r.remap) {
+    *seqid = -1;
+    *status = 1;
+    return pos;
+  }
+  const uint64_t rel = pos - r.offset;
+  *seqid = seq_for_pos(r.bns, (int64_t)rel);  // bwa_remap_position (bwaremap.cpp:244-249)
+  const uint64_t x = remap_position_with_seqid(r, d.db[0].bns, rel, *seqid, status);
+  const Mapping &m = *r.mappings[*seqid];
+  const uint64_t relpos = rel - (uint64_t)r.bns.anns[*seqid].offset;
+  *identical = is_remapped_sequence_identical(m, (uint32_t)(relpos > gap ? relpos - gap : 0), (uint32_t)(len + gap));
+  return x;
+}
+
+// dbset_extract_remapped (dbset.c:257-304): a window of an alternate sequence, continued on the
+// primary before its start and after its end
+inline uint32_t extract_remapped(const Dbs &d, int dbidx, int32_t seqid, uint64_t beg, uint32_t len, uint8_t *out) {
+  const RefDb &r = d.db[dbidx];
+  if (seqid < 0 || !r.remap) return extract(d, beg, len, out);
+  const Ann &ann = r.bns.anns[seqid];
+  const uint64_t seq_begin = r.offset + (uint64_t)ann.offset;
+  uint32_t total = 0;
+  int status = 0;
+  if (beg < seq_begin) {
+    const uint64_t remapped_begin = remap_position_with_seqid(r, d.db[0].bns, (uint64_t)ann.offset, seqid, &status);
+    const uint64_t sublen = seq_begin - beg;
+    const uint64_t offset = remapped_begin - sublen;
+    if (sublen > remapped_begin || status == 0) err_fatal("dbset_extract_remapped", "request too far ahead of remapped region");
+    total += extract(d, offset, (uint32_t)sublen, out + total);
+  }
+  if (total < len) {
+    uint32_t sublen = len - total;
+    if (sublen > (uint32_t)ann.len) sublen = (uint32_t)ann.len;
+    total += extract(d, beg, sublen, out + total);
+  }
+  if (total < len) {
+    const uint64_t remapped_end =
+        remap_position_with_seqid(r, d.db[0].bns, (uint64_t)ann.offset + ann.len - 1, seqid, &status) + 1;
+    if (status == 0) err_fatal("dbset_extract_remapped", "request too far ahead of remapped region");
+    total += extract(d, remapped_end, len - total, out + total);
+  }
+  if (total != len)
+    err_fatal("dbset_extract_remapped", "logic error: got %lu bases instead of %lu\n", (unsigned long)total, (unsigned long)len);
+  return total;
+}
+
 // POSIX drand48 / srand48 (glibc: X' = 0x5DEECE66D X + 0xB mod 2^48, the result is X' / 2^48)
 struct Drand48 {
   uint64_t x = 0x1234ABCD330Eull;
@@ -226,6 +369,7 @@ struct Read {
   int type = TYPE_NO_MATCH, strand = 0, n_mm = 0, n_gapo = 0, n_gape = 0, score = 0, extra_flag = 0;
   uint32_t sa = 0;
   uint64_t pos = 0, remapped_pos = 0;
+  int dbidx = 0, remapped_dbidx = 0, remapped_seqid = 0, remap_identical = 0;  // sampe's database set
   uint32_t c1 = 0, c2 = 0;
   int seQ = 0, mapQ = 0, nm = 0;
   std::vector<uint32_t> cigar;
@@ -355,11 +499,11 @@ inline int approx_mapQ(const Read &p, int mm) {
 }
 
 // bwa_cal_md1 (bwase.c:243-295)
-inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, const Bns &b, int *nm_out) {
+inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, const Dbs &b, int *nm_out) {
   std::string str;
   char buf[32];
   uint64_t x = pos, y = 0;
-  const uint64_t l_pac = (uint64_t)b.l_pac;
+  const uint64_t l_pac = b.l_pac;
   int u = 0, nm = 0;
   uint8_t c = 0;
   if (s.has_cigar) {
@@ -463,14 +607,16 @@ struct Refine {
   int64_t ref_start = 0;
   uint32_t l = 0;
   int ext = 0;
+  int dbidx = 0, seqid = -1;  // the hit's reference and (remapped references) its sequence
   Read *s = nullptr;
   Multi *q = nullptr;  // null: the read's own hit
 };
 
-// the window of one refinement; fills the job's reference / read slices
-inline bool refine_prepare(const Bns &b, Read &s, uint64_t pos, int ext, Refine &j, std::vector<uint8_t> &rbuf,
-                    std::vector<uint64_t> &roff, std::vector<uint32_t> &rlen) {
-  if (pos > (uint64_t)b.l_pac) {
+// the window of one refinement (dbset_extract_remapped on a remapped reference); fills the
+// job's reference / read slices
+inline bool refine_prepare(const Dbs &b, Read &s, uint64_t pos, int ext, Refine &j, std::vector<uint8_t> &rbuf,
+                           std::vector<uint64_t> &roff, std::vector<uint32_t> &rlen) {
+  if (pos > b.l_pac) {
     fprintf(stderr, "[refine_gapped_core] position=%llu > l_pac=%llu\n", (unsigned long long)pos,
             (unsigned long long)b.l_pac);
     return false;
@@ -486,7 +632,7 @@ inline bool refine_prepare(const Bns &b, Read &s, uint64_t pos, int ext, Refine 
   }
   const size_t o = rbuf.size();
   rbuf.resize(o + (size_t)ref_len);
-  j.l = extract(b, (uint64_t)ref_start, (uint32_t)ref_len, rbuf.data() + o);
+  j.l = extract_remapped(b, j.dbidx, j.seqid, (uint64_t)ref_start, (uint32_t)ref_len, rbuf.data() + o);
   rbuf.resize(o + j.l);
   j.ref_start = ref_start;
   j.ext = ext;
@@ -495,8 +641,10 @@ inline bool refine_prepare(const Bns &b, Read &s, uint64_t pos, int ext, Refine 
   return true;
 }
 
-// the CIGAR and position fix-ups after the alignment (bwase.c:200-223, no remapping)
-inline void refine_finish(const Refine &j, const uint32_t *c32, int n32, uint64_t *pos, std::vector<uint32_t> &cigar) {
+// the CIGAR and position fix-ups after the alignment (bwase.c:200-240): ends, then the CIGAR of a
+// hit on an alternate sequence translated onto the primary (translate_cigar)
+inline void refine_finish(const Dbs &b, const Refine &j, const uint32_t *c32, int n32, int len, uint64_t *pos,
+                          std::vector<uint32_t> &cigar, bool *has_cigar) {
   cigar.clear();
   for (int k = 0; k < n32; ++k) cigar.push_back(cig_make(c32[k] & 0xf, c32[k] >> 4));  // bwa_aln_path2cigar
   int64_t p = (int64_t)*pos;
@@ -516,21 +664,32 @@ inline void refine_finish(const Refine &j, const uint32_t *c32, int n32, uint64_
   if (!cigar.empty() && cig_op(cigar.back()) == FROM_I) cigar.back() = cig_make(FROM_S, cig_len(cigar.back()));
   if (!cigar.empty() && cig_op(cigar[0]) == FROM_I) cigar[0] = cig_make(FROM_S, cig_len(cigar[0]));
   *pos = (uint64_t)p;
+  *has_cigar = true;
+  const RefDb &r = b.db[j.dbidx];
+  if (r.remap && j.seqid >= 0 && j.seqid < (int)r.mappings.size() && r.mappings[j.seqid] && r.mappings[j.seqid]->has_cigar) {
+    const uint64_t start = *pos - r.offset - (uint64_t)r.bns.anns[j.seqid].offset;
+    std::vector<uint32_t> t;
+    // a failed translation leaves no CIGAR (the reference's NULL)
+    *has_cigar = translate_cigar(r.mappings[j.seqid]->cigar, (uint32_t)start, cigar.data(), (int)cigar.size(), len, t);
+    cigar.swap(t);
+  }
 }
 
 // bwa_refine_gapped (bwase.c:333-416) over a set of reads: the banded global alignment of every
 // gapped hit (refine_gapped_core, bwase.c:167-241) in one ibwa_global_batch launch, then MD/NM at
 // each read's remapped_pos as the reference has it at that point (bwase.c:401) and the
 // trimmed-read correction.  Returns 0, 1 on a bad position (message printed), -1 on a GPU error.
-inline int refine_gapped(ibwa_ctx_t *ctx, const Bns &b, std::vector<Read *> &reads) {
+inline int refine_gapped(ibwa_ctx_t *ctx, const Dbs &b, std::vector<Read *> &reads) {
   std::vector<Refine> jobs;
   std::vector<uint8_t> rbuf, qbuf;
   std::vector<uint64_t> roff, qoff;
   std::vector<uint32_t> rlen, qlen;
-  auto add_job = [&](Read &p, Multi *q, uint64_t ps, int ext, int strand) -> bool {
+  auto add_job = [&](Read &p, Multi *q, uint64_t ps, int ext, int strand, int dbidx, int seqid) -> bool {
     Refine j;
     j.s = &p;
     j.q = q;
+    j.dbidx = dbidx;
+    j.seqid = seqid;
     if (!refine_prepare(b, p, ps, ext, j, rbuf, roff, rlen)) return false;
     const std::vector<uint8_t> &sq = strand ? p.rseq : p.seq;
     qoff.push_back(qbuf.size());
@@ -541,12 +700,18 @@ inline int refine_gapped(ibwa_ctx_t *ctx, const Bns &b, std::vector<Read *> &rea
   };
   for (Read *pp : reads) {
     Read &p = *pp;
-    for (Multi &q : p.multi) {
+    // remapped sequences can also have gaps (bwase.c:341-347)
+    int remapped_gapo = 0;
+    const RefDb &r = b.db[p.dbidx];
+    if (r.remap && p.remapped_seqid >= 0 && p.remapped_seqid < (int)r.mappings.size() && r.mappings[p.remapped_seqid])
+      remapped_gapo += r.mappings[p.remapped_seqid]->n_gapo;
+    for (Multi &q : p.multi) {  // bwt_multi1_t.dbidx / remapped_seqid are 0 (select_sai_multi)
       if (q.gap == 0) continue;
-      if (!add_job(p, &q, q.pos, (q.strand ? 1 : -1) * q.gap, q.strand)) return 1;
+      if (!add_job(p, &q, q.pos, (q.strand ? 1 : -1) * q.gap, q.strand, 0, 0)) return 1;
     }
-    if (p.type == TYPE_NO_MATCH || p.type == TYPE_MATESW || p.n_gapo == 0) continue;
-    if (!add_job(p, nullptr, p.pos, (p.strand ? 1 : -1) * (p.n_gapo + p.n_gape), p.strand)) return 1;
+    if (p.type == TYPE_NO_MATCH || p.type == TYPE_MATESW || (p.n_gapo == 0 && remapped_gapo == 0)) continue;
+    if (!add_job(p, nullptr, p.pos, (p.strand ? 1 : -1) * (p.n_gapo + p.n_gape), p.strand, p.dbidx, p.remapped_seqid))
+      return 1;
   }
   if (!jobs.empty()) {
     rbuf.push_back(0);
@@ -561,13 +726,8 @@ inline int refine_gapped(ibwa_ctx_t *ctx, const Bns &b, std::vector<Read *> &rea
     int64_t q0 = 0;
     for (int64_t k = 0; k < m; ++k) {
       Refine &j = jobs[k];
-      if (j.q) {
-        refine_finish(j, c32 + q0, nc[k], &j.q->pos, j.q->cigar);
-        j.q->has_cigar = true;
-      } else {
-        refine_finish(j, c32 + q0, nc[k], &j.s->pos, j.s->cigar);
-        j.s->has_cigar = true;
-      }
+      if (j.q) refine_finish(b, j, c32 + q0, nc[k], j.s->len, &j.q->pos, j.q->cigar, &j.q->has_cigar);
+      else refine_finish(b, j, c32 + q0, nc[k], j.s->len, &j.s->pos, j.s->cigar, &j.s->has_cigar);
       q0 += nc[k];
     }
     ibwa_free(c32);
@@ -614,10 +774,10 @@ inline void print_cigar(Out &o, const std::vector<uint32_t> &cg) {
 // place for a reverse-strand read.
 inline int64_t pos_5(const Read &p) { return p.type != TYPE_NO_MATCH ? (p.strand ? pos_end(p) : (int64_t)p.pos) : -1; }
 
-inline void print_sam1(Out &o, const Bns &b, Read &p, const Read *mate, int mode, int max_top2, const char *rg_id) {
+inline void print_sam1(Out &o, const Dbs &d, Read &p, const Read *mate, int mode, int max_top2, const char *rg_id) {
   if (p.type != TYPE_NO_MATCH || (mate && mate->type != TYPE_NO_MATCH)) {
     int32_t seqid = 0;
-    int flag = p.extra_flag, am = 0, j;
+    int flag = p.extra_flag, am = 0, j, dbi = 0;
     if (p.type == TYPE_NO_MATCH) {
       p.pos = mate->pos;
       p.remapped_pos = mate->remapped_pos;
@@ -627,8 +787,12 @@ inline void print_sam1(Out &o, const Bns &b, Read &p, const Read *mate, int mode
     } else {
       j = (int)(pos_end(p) - (int64_t)p.pos);  // the reference length of the alignment
     }
-    int nn = coor_pac2real(b, (int64_t)p.pos, j, &seqid);
-    if (p.type != TYPE_NO_MATCH && (int64_t)p.pos + j - b.anns[seqid].offset > b.anns[seqid].len) flag |= SAM_FSU;
+    // dbset_coor_pac2real: the sequence, and the reference (bns, offset) it belongs to
+    int nn = coor_pac2real(d, (int64_t)p.pos, j, &seqid, &dbi);
+    const Bns *bns = &d.db[dbi].bns;
+    int64_t bnsoffset = (int64_t)d.db[dbi].offset;
+    if (p.type != TYPE_NO_MATCH && (int64_t)p.pos + j - (bns->anns[seqid].offset + bnsoffset) > bns->anns[seqid].len)
+      flag |= SAM_FSU;
     if (p.strand) flag |= SAM_FSR;
     if (mate) {
       if (mate->type != TYPE_NO_MATCH) {
@@ -637,22 +801,25 @@ inline void print_sam1(Out &o, const Bns &b, Read &p, const Read *mate, int mode
         flag |= SAM_FMU;
       }
     }
-    o.s(p.name).c('\t').i(flag).c('\t').s(b.anns[seqid].name).c('\t');
-    o.i((int)((int64_t)p.pos - b.anns[seqid].offset + 1)).c('\t').i(p.mapQ).c('\t');
+    o.s(p.name).c('\t').i(flag).c('\t').s(bns->anns[seqid].name).c('\t');
+    o.i((int)((int64_t)p.pos - (bns->anns[seqid].offset + bnsoffset) + 1)).c('\t').i(p.mapQ).c('\t');
     if (p.has_cigar) print_cigar(o, p.cigar);
     else if (p.type == TYPE_NO_MATCH) o.c('*');
     else o.i(p.len).c('M');
     if (mate && mate->type != TYPE_NO_MATCH) {
       int32_t m_seqid = 0;
+      int m_dbi = 0;
       am = mate->seQ < p.seQ ? mate->seQ : p.seQ;  // the smaller single-end mapping quality
-      coor_pac2real(b, (int64_t)mate->pos, mate->len, &m_seqid);
-      const bool same = seqid == m_seqid;
-      o.c('\t').s(same ? std::string("=") : b.anns[m_seqid].name).c('\t');
+      coor_pac2real(d, (int64_t)mate->pos, mate->len, &m_seqid, &m_dbi);
+      const int64_t m_bnsoffset = (int64_t)d.db[m_dbi].offset;
+      bns = &d.db[m_dbi].bns;  // as the reference, bns now names the mate's reference
+      const bool same = seqid == m_seqid && bnsoffset == m_bnsoffset;
+      o.c('\t').s(same ? std::string("=") : bns->anns[m_seqid].name).c('\t');
       long long isize = same ? pos_5(*mate) - pos_5(p) : 0;
       if (p.type == TYPE_NO_MATCH) isize = 0;
-      o.i((int)((int64_t)mate->pos - b.anns[m_seqid].offset + 1)).c('\t').i(isize).c('\t');
+      o.i((int)((int64_t)mate->pos - (bns->anns[m_seqid].offset + m_bnsoffset) + 1)).c('\t').i(isize).c('\t');
     } else if (mate) {
-      o.s("\t=\t").i((int)((int64_t)p.pos - b.anns[seqid].offset + 1)).s("\t0\t");
+      o.s("\t=\t").i((int)((int64_t)p.pos - (bns->anns[seqid].offset + bnsoffset) + 1)).s("\t0\t");
     } else {
       o.s("\t*\t0\t0\t");
     }
@@ -686,9 +853,12 @@ inline void print_sam1(Out &o, const Bns &b, Read &p, const Read *mate, int mode
         o.s("\tXA:Z:");
         for (const Multi &q : p.multi) {
           j = (int)(pos_end_multi(q, p.len) - (int64_t)q.pos);
-          coor_pac2real(b, (int64_t)q.pos, j, &seqid);
-          o.s(b.anns[seqid].name).c(',').c(q.strand ? '-' : '+');
-          o.i((int)((int64_t)q.pos - b.anns[seqid].offset + 1)).c(',');
+          int q_dbi = 0;
+          coor_pac2real(d, (int64_t)q.pos, j, &seqid, &q_dbi);
+          const Bns &qb = d.db[q_dbi].bns;
+          const int64_t qoff = (int64_t)d.db[q_dbi].offset;
+          o.s(qb.anns[seqid].name).c(',').c(q.strand ? '-' : '+');
+          o.i((int)((int64_t)q.pos - (qb.anns[seqid].offset + qoff) + 1)).c(',');
           if (q.has_cigar) print_cigar(o, q.cigar);
           else o.i(p.len).c('M');
           o.c(',').i(q.gap + q.mm).c(';');
@@ -697,8 +867,11 @@ inline void print_sam1(Out &o, const Bns &b, Read &p, const Read *mate, int mode
     }
     if (p.pos != p.remapped_pos) {
       int32_t rs = 0;
-      coor_pac2real(b, (int64_t)p.remapped_pos, j, &rs);
-      o.s("\tZR:Z:").s(b.anns[rs].name).c(',').i((int)((int64_t)p.remapped_pos - b.anns[rs].offset + 1));
+      int r_dbi = 0;
+      coor_pac2real(d, (int64_t)p.remapped_pos, j, &rs, &r_dbi);
+      const Bns &rb = d.db[r_dbi].bns;
+      o.s("\tZR:Z:").s(rb.anns[rs].name).c(',');
+      o.i((int)((int64_t)p.remapped_pos - (rb.anns[rs].offset + (int64_t)d.db[r_dbi].offset) + 1));
     }
     o.c('\n');
   } else {

@@ -14,8 +14,13 @@
 // (k,l)-keyed position cache of bwtcache.c for intervals of >= 1000 rows, whose key ignores the
 // strand and the read length.
 //
-// Remapping (-R): without .remap files every hit remaps to itself (bwaremap's status 1), which is
-// what this build supports; a prefix with a .remap file, or more than one database, is rejected.
+// Several references (`sampe <pri> <1.sai> <2.sai> <1.fq> <2.fq> [<alt> <a1.sai> <a2.sai> ...]`,
+// pe_inputs_parse, bwape.c:548-581) are concatenated at their offsets (dbset_restore); each has its
+// own index on the GPU for SA -> coordinate, and the hits of all references are merged per read
+// (alngrp_create, saiset.c:45-76, with klib's unstable introsort when there are several).  With -R
+// a reference that has a .remap table is a set of alternate sequences: hits on them are projected
+// onto the primary (remap.h), pairing runs on the projected positions, refinement translates the
+// CIGAR of gapped hits, and the SAM prints the projected position with ZR:Z: the original.
 // Without -R the reference's select_sai_ibwa never sees a successful remap status and leaves every
 // read unmapped ("Failed to select primary alignment"); that is reproduced.
 #include <math.h>
@@ -145,9 +150,11 @@ void ks_introsort(size_t n, T *a, Lt lt) {
 }
 
 // ---------------------------------------------------------------- pairing (bwapair.c)
-struct Position {  // position_t (bwapair.h:13-24): single database, hits remap to themselves
+struct Position {  // position_t (bwapair.h:13-25)
   uint64_t pos = 0, remapped_pos = 0;
   uint32_t idx_and_end = 0;
+  int dbidx = 0, remapped_dbidx = 0, remapped_seqid = 0, remap_identical = 0;
+  int n_gapo = 0, n_gape = 0, len = 0, score = 0;
 };
 inline bool position_lt(const Position &a, const Position &b) {  // bwapair.c:22-28
   if (a.remapped_pos == b.remapped_pos) return a.pos < b.pos;
@@ -183,13 +190,18 @@ inline uint64_t hash_64(uint64_t key) {  // bwapair.c:31-41
   return key;
 }
 
+struct Aln {  // alignment_t (saiset.h:9-14)
+  ibwa_aln1_t aln;
+  int dbidx;
+};
+
 struct PairCtx {
   Read *p[2];
-  const std::vector<ibwa_aln1_t> *aln[2];
+  const std::vector<Aln> *aln[2];
   const PeOpt *opt;
   const Isize *ii;
   int s_mm;
-  const ibwa_aln1_t &al(const Position &x) const { return (*aln[x.idx_and_end & 1])[x.idx_and_end >> 1]; }
+  const ibwa_aln1_t &al(const Position &x) const { return (*aln[x.idx_and_end & 1])[x.idx_and_end >> 1].aln; }
 };
 
 struct Pint {  // pairing_internals_t (bwapair.c:8-17)
@@ -201,7 +213,12 @@ struct Pint {  // pairing_internals_t (bwapair.c:8-17)
 
 // pairing_aux (bwapair.c:92-140)
 void pairing_aux(const PairCtx &c, Pint &pi, const Position &u, const Position &v, int n_optimal) {
-  const uint32_t l = (uint32_t)(v.remapped_pos + (uint64_t)c.p[v.idx_and_end & 1]->len - u.remapped_pos);
+  uint32_t l;
+  // both remapped onto the same alternate sequence: the insert size on it
+  if (u.remapped_pos != u.pos && v.remapped_pos != v.pos && u.dbidx == v.dbidx && u.remapped_seqid == v.remapped_seqid)
+    l = (uint32_t)(v.pos + (uint64_t)c.p[v.idx_and_end & 1]->len - u.pos);
+  else
+    l = (uint32_t)(v.remapped_pos + (uint64_t)c.p[v.idx_and_end & 1]->len - u.remapped_pos);
   if (u.remapped_pos != ~0ull && v.remapped_pos > u.remapped_pos && l >= (uint32_t)pi.max_len &&
       ((c.ii->high && l <= c.ii->high_bayesian) || (c.ii->high == 0 && l <= (uint32_t)c.opt->max_isize))) {
     uint64_t s = (uint64_t)(int64_t)(c.al(v).score + c.al(u).score);
@@ -235,9 +252,31 @@ void pairing_aux2(const PairCtx &c, Pint &pi, Read &r, const Position &pos) {
     r.n_mm = a.n_mm; r.n_gapo = a.n_gapo; r.n_gape = a.n_gape; r.strand = a.a;
     r.score = a.score;
     r.pos = pos.pos;
+    r.dbidx = pos.dbidx;
     r.remapped_pos = pos.remapped_pos;
+    r.remapped_seqid = pos.remapped_seqid;
     if (r.mapQ > 0) ++pi.cnt_chg;
   }
+}
+
+// select_mapping (bwapair.c:64-90): the first lowest-score position of a run that maps to the same
+// place, skipping a remapped position identical to a primary one already seen (the set is seeded
+// from the array's first element, as the reference does)
+const Position &select_mapping(const PairCtx &c, const PosArr &arr, size_t begin, size_t end) {
+  const Position *best = &arr.at(begin);
+  std::vector<uint64_t> seen;
+  auto has = [&](uint64_t x) { return std::find(seen.begin(), seen.end(), x) != seen.end(); };
+  if (arr.at(0).pos == arr.at(0).remapped_pos) seen.push_back(arr.at(0).pos);
+  for (size_t i = begin + 1; i <= end; ++i) {
+    const Position &p = arr.at(i);
+    if (p.pos == p.remapped_pos) {
+      if (!has(p.pos)) seen.push_back(p.pos);
+    } else if (has(p.remapped_pos) && p.remap_identical) {
+      continue;
+    }
+    if (c.al(p).score < c.al(*best).score) best = &p;
+  }
+  return *best;
 }
 
 // find_optimal_pair (bwapair.c:166-279), BWA_PET_STD
@@ -261,11 +300,8 @@ int find_optimal_pair(const PairCtx &c, PosArr &arr) {
     if (i < arr.n - 1) {
       size_t k = i;
       while (overlap(pos, arr.at(k + 1))) ++k;
-      if (k > i) {  // select_mapping (bwapair.c:64-90): the first of the lowest score
-        size_t best = i;
-        for (size_t t = i + 1; t <= k; ++t)
-          if (c.al(arr.at(t)).score < c.al(arr.at(best)).score) best = t;
-        pos = arr.at(best);
+      if (k > i) {
+        pos = select_mapping(c, arr, i, k);
         i = k;
       }
     }
@@ -411,15 +447,17 @@ struct Source {
 
 // ---------------------------------------------------------------- the batch loop (bwa_sai2sam_pe_core)
 struct Sampe {
-  ibwa_ctx_t *ctx = nullptr;
-  Bns b;
+  Dbs dbs;
+  std::vector<ibwa_ctx_t *> ctx;  // one per reference (its index, SA -> coordinate)
+  std::vector<std::vector<const char *>> sai_fn;  // per reference: end 1, end 2
   PeOpt popt;
   ibwa_gap_opt_t gopt[2];
-  FILE *fp_sai[2] = {nullptr, nullptr};
+  std::vector<FILE *> fp_sai[2];  // per end, per reference
   Drand48 rnd;
   Isize last_ii;
-  // bwtcache (bwtcache.c:27-45): positions of an interval of >= 1000 rows, keyed by (k, l) only
-  std::unordered_map<uint64_t, std::vector<uint64_t>> cache;
+  // bwtcache (bwtcache.c:27-45), one per reference: positions of an interval of >= 1000 rows,
+  // keyed by (k, l) only
+  std::vector<std::unordered_map<uint64_t, std::vector<uint64_t>>> cache;
   const char *rg_id = nullptr;
   Phases ph;
 
@@ -427,15 +465,31 @@ struct Sampe {
     return gopt[1].fnr > 0.0 ? ibwa_cal_maxdiff(r.len, 0.02, gopt[1].fnr) : gopt[1].max_diff;
   }
 
-  // alngrp_create (saiset.c:42-74) for one read and one database
-  bool read_alns(int j, std::vector<ibwa_aln1_t> &v) {
-    uint32_t count = 0;
+  // alngrp_create (saiset.c:45-76): the read's records of every reference; with several
+  // references sorted by score (klib's introsort, not stable) and cut at best + s_mm
+  bool read_alns(int j, std::vector<Aln> &v) {
     v.clear();
-    if (fread(&count, 4, 1, fp_sai[j]) != 1) return true;  // past the end: nothing (count stays 0)
-    v.resize(count);
-    if (count && fread(v.data(), sizeof(ibwa_aln1_t), count, fp_sai[j]) != count) {
-      fprintf(stderr, "[ibwa-amd sampe] truncated .sai\n");
-      return false;
+    for (size_t d = 0; d < fp_sai[j].size(); ++d) {
+      uint32_t count = 0;
+      if (fread(&count, 4, 1, fp_sai[j][d]) != 1) continue;  // past the end: nothing
+      const size_t o = v.size();
+      v.resize(o + count);
+      for (uint32_t t = 0; t < count; ++t) {
+        if (fread(&v[o + t].aln, sizeof(ibwa_aln1_t), 1, fp_sai[j][d]) != 1) {
+          fprintf(stderr, "[ibwa-amd sampe] truncated .sai\n");
+          return false;
+        }
+        v[o + t].dbidx = (int)d;
+      }
+    }
+    if (fp_sai[j].size() > 1 && !v.empty()) {
+      ks_introsort(v.size(), v.data(), [](const Aln &x, const Aln &y) { return x.aln.score < y.aln.score; });
+      const int best = v[0].aln.score;
+      for (size_t t = 0; t < v.size(); ++t)
+        if (v[t].aln.score > best + gopt[0].s_mm) {
+          v.resize(t);
+          break;
+        }
     }
     return true;
   }
@@ -447,18 +501,55 @@ struct Sampe {
     s.has_cigar = false;
   }
 
-  // select_sai_ibwa (bwape.c:281-358) up to the coordinate: the RNG decisions and the SA row
-  // (main alignment index and the row inside it); returns false when the read is unmapped.
-  bool select_sai(const std::vector<ibwa_aln1_t> &ag, Read &s) {
+  // SA rows -> positions (bwtdb_sa2seq, dbset.c:240-246), one launch per reference
+  int sa2pos(const std::vector<int> &db, const std::vector<uint8_t> &st, const std::vector<uint32_t> &k,
+             const std::vector<uint32_t> &len, std::vector<uint64_t> &pos) {
+    pos.assign(k.size(), 0);
+    for (size_t d = 0; d < ctx.size(); ++d) {
+      std::vector<size_t> idx;
+      for (size_t t = 0; t < k.size(); ++t)
+        if (db[t] == (int)d) idx.push_back(t);
+      if (idx.empty()) continue;
+      std::vector<uint8_t> s2(idx.size());
+      std::vector<uint32_t> k2(idx.size()), l2(idx.size());
+      std::vector<uint64_t> p2(idx.size());
+      for (size_t t = 0; t < idx.size(); ++t) { s2[t] = st[idx[t]]; k2[t] = k[idx[t]]; l2[t] = len[idx[t]]; }
+      if (ibwa_sa2pos(ctx[d], (int64_t)idx.size(), s2.data(), k2.data(), l2.data(), dbs.db[d].offset, p2.data()))
+        return die("sa2pos");
+      for (size_t t = 0; t < idx.size(); ++t) pos[idx[t]] = p2[t];
+    }
+    return 0;
+  }
+
+  // remap (bwape.c:223-235) of a hit at pos on reference dbidx; status untouched without -R
+  template <class T>
+  void remap(T &p, uint64_t pos, int dbidx, uint64_t len, uint32_t gap, int *status) {
+    p.dbidx = dbidx;
+    p.remapped_dbidx = 0;
+    if (popt.remapping) {
+      p.remapped_pos = remap_pos(dbs, dbidx, pos, len, gap, &p.remapped_seqid, &p.remap_identical, status);
+    } else {
+      p.remapped_pos = pos;
+      p.remapped_seqid = -1;
+    }
+  }
+
+  // select_sai_ibwa (bwape.c:299-369) up to the coordinate: the RNG decisions, the main alignment
+  // and the first SA row to try; returns false when the read is unmapped without a try.
+  struct Pick {
+    int main_idx = 0;
+    uint32_t start = 0, num = 0;
+  };
+  bool select_sai(const std::vector<Aln> &ag, Read &s, Pick &pk) {
     if (ag.empty()) {
       unmap(s);
       return false;
     }
     int main_idx = 0, i, cnt;
     double rng_cache = 0.0;
-    const int best = ag[0].score;
+    const int best = ag[0].aln.score;
     for (i = cnt = 0; i < (int)ag.size(); ++i) {
-      const ibwa_aln1_t &p = ag[i];
+      const ibwa_aln1_t &p = ag[i].aln;
       const int naln = (int)(p.l - p.k + 1);
       if (p.score > best) break;
       if (rnd.next() * (double)(uint32_t)(p.l - p.k + 1 + (uint32_t)cnt) > (double)cnt) {
@@ -468,21 +559,27 @@ struct Sampe {
       cnt += naln;
     }
     s.c1 = (uint32_t)cnt & 0xfffffffu;
-    for (int t = i; t < (int)ag.size(); ++t) cnt += (int)(ag[t].l - ag[t].k + 1);
+    for (int t = i; t < (int)ag.size(); ++t) cnt += (int)(ag[t].aln.l - ag[t].aln.k + 1);
     s.c2 = ((uint32_t)cnt - s.c1) & 0xfffffffu;
     if (s.c1 != 0) s.type = s.c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
-    const ibwa_aln1_t &p = ag[main_idx];
+    const ibwa_aln1_t &p = ag[main_idx].aln;
     const uint32_t num = p.l - p.k + 1;
     const uint32_t start = (uint32_t)(rng_cache * num);
     s.n_mm = p.n_mm; s.n_gapo = p.n_gapo; s.n_gape = p.n_gape; s.strand = p.a;
     s.score = p.score;
     if (!popt.remapping) {  // remap() never reports success: every row, then UNMAP_READ
       s.sa = p.k + (start == 0 ? num - 1 : start - 1);
+      s.dbidx = ag[main_idx].dbidx;
+      s.remapped_dbidx = 0;
+      s.remapped_seqid = -1;
       unmap(s);
       fprintf(stderr, "Failed to select primary alignment for %s\n", s.name.c_str());
       return false;
     }
     s.sa = p.k + start;
+    pk.main_idx = main_idx;
+    pk.start = start;
+    pk.num = num;
     return true;
   }
 
@@ -526,112 +623,154 @@ struct Sampe {
   }
 
   int batch(std::vector<Read> seqs[2], int n, Out &o) {
-    std::vector<std::vector<ibwa_aln1_t>> alns[2];
+    std::vector<std::vector<Aln>> alns[2];
     alns[0].resize(n);
     alns[1].resize(n);
-    // ---- SE (bwa_cal_pac_pos_pe, bwape.c:366-385): hit choice in pair order, then one SA->pos launch
+    // ---- SE (bwa_cal_pac_pos_pe, bwape.c:366-385): hit choice in pair order, one SA->pos launch
+    // per reference, then remap(); a row whose remap fails moves to the next row (rare: per row)
+    std::vector<int> hd;
     std::vector<uint8_t> hs;
     std::vector<uint32_t> hk, hl;
     std::vector<Read *> hr;
+    std::vector<Pick> hp;
+    std::vector<const std::vector<Aln> *> ha;
     for (int i = 0; i < n; ++i) {
       for (int j = 0; j < 2; ++j) {
         Read &p = seqs[j][i];
         p.multi.clear();
         p.extra_flag |= SAM_FPD | (j == 0 ? SAM_FR1 : SAM_FR2);
         if (!read_alns(j, alns[j][i])) return 1;
-        if (select_sai(alns[j][i], p)) {
+        Pick pk;
+        if (select_sai(alns[j][i], p, pk)) {
+          hd.push_back(alns[j][i][pk.main_idx].dbidx);
           hs.push_back((uint8_t)p.strand); hk.push_back(p.sa); hl.push_back((uint32_t)p.len);
           hr.push_back(&p);
+          hp.push_back(pk);
+          ha.push_back(&alns[j][i]);
         }
       }
     }
     ph.mark("sai+hit choice");
-    std::vector<uint64_t> pos(hk.size());
-    if (!hk.empty() && ibwa_sa2pos(ctx, (int64_t)hk.size(), hs.data(), hk.data(), hl.data(), 0, pos.data()))
-      return die("sa2pos");
+    std::vector<uint64_t> pos;
+    if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
     for (size_t t = 0; t < hr.size(); ++t) {
       Read &p = *hr[t];
-      p.pos = p.remapped_pos = pos[t];  // remap(): no .remap file, the hit maps to itself
+      const Aln &ma = (*ha[t])[hp[t].main_idx];
+      int status = 0;
+      p.pos = pos[t];
+      remap(p, p.pos, ma.dbidx, (uint64_t)p.len, (uint32_t)(p.n_gapo + p.n_gape), &status);
+      // the other rows of the main alignment, cyclically from the chosen one (bwape.c:336-357)
+      for (uint32_t step = 1; status != 1 && step < hp[t].num; ++step) {
+        const uint32_t aidx = (hp[t].start + step) % hp[t].num;
+        std::vector<int> d1{ma.dbidx};
+        std::vector<uint8_t> s1{(uint8_t)p.strand};
+        std::vector<uint32_t> k1{ma.aln.k + aidx}, l1{(uint32_t)p.len};
+        std::vector<uint64_t> p1;
+        if (int rc = sa2pos(d1, s1, k1, l1, p1)) return rc;
+        p.sa = ma.aln.k + aidx;
+        p.pos = p1[0];
+        remap(p, p.pos, ma.dbidx, (uint64_t)p.len, (uint32_t)(p.n_gapo + p.n_gape), &status);
+      }
+      if (status != 1) {
+        unmap(p);
+        fprintf(stderr, "Failed to select primary alignment for %s\n", p.name.c_str());
+        continue;
+      }
       p.seQ = p.mapQ = approx_mapQ(p, max_diff_of(p)) & 0xff;
     }
     ph.mark("sa2pos");
     // ---- insert size
     Isize ii;
-    infer_isize(seqs[0], seqs[1], ii, popt.ap_prior, b.l_pac);
+    infer_isize(seqs[0], seqs[1], ii, popt.ap_prior, (int64_t)dbs.l_pac);
     if (ii.avg < 0.0 && last_ii.avg > 0.0) ii = last_ii;
     if (popt.force_isize) {
       fprintf(stderr, "[bwa_cal_pac_pos_pe] discard insert size estimate as user's request.\n");
       ii.low = ii.high = 0;
       ii.avg = ii.std = -1.0;
     }
-    // ---- every row of every interval (compute_seq_coords_and_counts): one SA->pos launch
-    // rows of intervals narrower than kMinHashWidth are computed per (read, alignment); wider ones
-    // come from the cache, filled on first use with that caller's strand and read length.
+    // ---- every row of every interval (compute_seq_coords_and_counts): one SA->pos launch per
+    // reference.  Rows of intervals narrower than kMinHashWidth are computed per (read, alignment);
+    // wider ones come from the reference's cache, filled on first use with that caller's strand
+    // and read length.
     std::vector<int64_t> row0[2];  // per (pair, end): first alignment slot in aslot
     std::vector<int64_t> aslot;    // per alignment: first row in rows (-1: cached)
-    hs.clear(); hk.clear(); hl.clear();
-    std::vector<std::pair<uint64_t, int64_t>> fill;  // new cache keys -> first row
+    hd.clear(); hs.clear(); hk.clear(); hl.clear();
+    std::vector<std::pair<std::pair<int, uint64_t>, int64_t>> fill;  // new cache keys -> first row
     if (popt.remapping) {
       for (int j = 0; j < 2; ++j) row0[j].assign(n + 1, 0);
       for (int i = 0; i < n; ++i) {
         for (int j = 0; j < 2; ++j) {
           row0[j][i] = (int64_t)aslot.size();
-          for (const ibwa_aln1_t &a : alns[j][i]) {
+          for (const Aln &al : alns[j][i]) {
+            const ibwa_aln1_t &a = al.aln;
             const uint32_t w = a.l - a.k + 1;
+            auto rows = [&]() {
+              for (uint32_t r = 0; r < w; ++r) {
+                hd.push_back(al.dbidx); hs.push_back((uint8_t)a.a); hk.push_back(a.k + r);
+                hl.push_back((uint32_t)seqs[j][i].len);
+              }
+            };
             if (w >= kMinHashWidth) {
               const uint64_t key = (uint64_t)a.k << 32 | a.l;
-              if (!cache.count(key)) {
-                fill.push_back({key, (int64_t)hk.size()});
-                cache[key];  // reserve: later uses in this batch share it
-                for (uint32_t r = 0; r < w; ++r) { hs.push_back((uint8_t)a.a); hk.push_back(a.k + r); hl.push_back((uint32_t)seqs[j][i].len); }
+              if (!cache[al.dbidx].count(key)) {
+                fill.push_back({{al.dbidx, key}, (int64_t)hk.size()});
+                cache[al.dbidx][key];  // reserve: later uses in this batch share it
+                rows();
               }
               aslot.push_back(-1);
             } else {
               aslot.push_back((int64_t)hk.size());
-              for (uint32_t r = 0; r < w; ++r) { hs.push_back((uint8_t)a.a); hk.push_back(a.k + r); hl.push_back((uint32_t)seqs[j][i].len); }
+              rows();
             }
           }
         }
       }
     }
     ph.mark("isize+rows");
-    pos.assign(hk.size(), 0);
-    if (!hk.empty() && ibwa_sa2pos(ctx, (int64_t)hk.size(), hs.data(), hk.data(), hl.data(), 0, pos.data()))
-      return die("sa2pos");
+    if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
     for (auto &f : fill) {
-      const uint32_t k = (uint32_t)(f.first >> 32), l = (uint32_t)f.first;
-      cache[f.first].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
+      const uint32_t k = (uint32_t)(f.first.second >> 32), l = (uint32_t)f.first.second;
+      cache[f.first.first][f.first.second].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
     }
     ph.mark("sa2pos");
-    // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:226-279), pair by pair
+    // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:238-297), pair by pair
     PosArr arr;
     std::vector<std::pair<uint64_t, int>> ps;
     int cnt_chg = 0;
-    const uint64_t l_pac = (uint64_t)b.l_pac;
     for (int i = 0; i < n; ++i) {
       Read *p[2] = {&seqs[0][i], &seqs[1][i]};
       arr.clear();
       if (popt.remapping) {
         for (int j = 0; j < 2; ++j) {
-          // pos2score (filter_alignments.cpp:60-139): the lowest score seen at each distinct
-          // position; c1 / c2 count the positions whose lowest score is / is not the best
+          // compute_seq_coords_and_counts (filter_alignments.cpp:53-140): positions inside their
+          // reference, remapped; per distinct remapped position the lowest score seen there; c1 / c2
+          // count the positions whose lowest score is / is not the best
           ps.clear();
           int min_score = INT32_MAX;
-          const std::vector<ibwa_aln1_t> &ag = alns[j][i];
+          const std::vector<Aln> &ag = alns[j][i];
           for (size_t k = 0; k < ag.size(); ++k) {
-            const ibwa_aln1_t &a = ag[k];
+            const ibwa_aln1_t &a = ag[k].aln;
+            const int d = ag[k].dbidx;
+            const RefDb &rdb = dbs.db[d];
             min_score = std::min(min_score, a.score);
             const uint32_t w = a.l - a.k + 1;
             const int64_t slot = aslot[row0[j][i] + (int64_t)k];
-            const uint64_t *pp = slot < 0 ? cache[(uint64_t)a.k << 32 | a.l].data() : pos.data() + slot;
+            const uint64_t *pp = slot < 0 ? cache[d][(uint64_t)a.k << 32 | a.l].data() : pos.data() + slot;
             for (uint32_t r = 0; r < w; ++r) {
               const uint64_t x = pp[r];
-              if (x >= l_pac) continue;
+              if (x < rdb.offset || x >= rdb.offset + (uint64_t)rdb.bns.l_pac) continue;
               Position ap;
-              ap.pos = ap.remapped_pos = x;
+              ap.pos = x;
+              ap.len = p[j]->len;
+              ap.n_gape = a.n_gape;
+              ap.n_gapo = a.n_gapo;
+              ap.score = a.score;
+              int status = 0;
+              remap(ap, x, d, (uint64_t)ap.len, (uint32_t)(ap.n_gapo + ap.n_gape), &status);
+              if (!status) continue;
               ap.idx_and_end = (uint32_t)k << 1 | (uint32_t)j;
               arr.push(ap);
-              ps.push_back({x, a.score});
+              ps.push_back({ap.remapped_pos, a.score});
             }
           }
           std::sort(ps.begin(), ps.end());
@@ -664,36 +803,41 @@ struct Sampe {
     }
     fprintf(stderr, "[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);
     ph.mark("pairing");
-    // ---- mate rescue (bwa_paired_sw): the drop-in over the reference's bwa_seq_t layout
+    // ---- mate rescue (bwa_paired_sw) over the concatenated references
     if (int rc = paired_sw(seqs, n, ii)) return rc;
     ph.mark("paired SW");
     // ---- refine gapped alignments of both ends, MD/NM, trimmed reads; then remap()
     std::vector<Read *> rp;
     for (int j = 0; j < 2; ++j)
       for (Read &r : seqs[j]) rp.push_back(&r);
-    if (int rc = refine_gapped(ctx, b, rp)) return rc == 1 ? 1 : die("global alignment");
+    if (int rc = refine_gapped(ctx[0], dbs, rp)) return rc == 1 ? 1 : die("global alignment");
     for (int j = 0; j < 2; ++j) {
       for (Read &r : seqs[j]) {
-        if (popt.remapping) {
-          r.remapped_pos = r.pos;
-        } else {
+        int status = 0;
+        remap(r, r.pos, r.dbidx, (uint64_t)r.len, (uint32_t)(r.n_gapo + r.n_gape), &status);
+        if (status == 0) {
           fprintf(stderr, "Failed to remap read %s after refining gaps.\n", r.name.c_str());
           unmap(r);
         }
       }
     }
     ph.mark("refine+md");
-    // ---- print
+    // ---- print: with -R the remapped (primary) coordinates, the original ones as ZR
     print_parallel(o, n, [&](Out &ob, int64_t i) {
       Read *p[2] = {&seqs[0][i], &seqs[1][i]};
       if (p[0]->bc[0] || p[1]->bc[0]) {
         strncat(p[0]->bc, p[1]->bc, sizeof p[0]->bc - strlen(p[0]->bc) - 1);
         memcpy(p[1]->bc, p[0]->bc, sizeof p[1]->bc);
       }
-      p[0]->remapped_pos = p[0]->pos;  // -R swaps pos and remapped_pos, which are equal here
-      p[1]->remapped_pos = p[1]->pos;
-      print_sam1(ob, b, *p[0], p[1], gopt[1].mode, gopt[1].max_top2, rg_id);
-      print_sam1(ob, b, *p[1], p[0], gopt[1].mode, gopt[1].max_top2, rg_id);
+      if (popt.remapping) {
+        std::swap(p[0]->pos, p[0]->remapped_pos);
+        std::swap(p[1]->pos, p[1]->remapped_pos);
+      } else {
+        p[0]->remapped_pos = p[0]->pos;
+        p[1]->remapped_pos = p[1]->pos;
+      }
+      print_sam1(ob, dbs, *p[0], p[1], gopt[1].mode, gopt[1].max_top2, rg_id);
+      print_sam1(ob, dbs, *p[1], p[0], gopt[1].mode, gopt[1].max_top2, rg_id);
     });
     ph.mark("print");
     o.flush();
@@ -702,15 +846,16 @@ struct Sampe {
   }
 
   // select_sai_multi (saiset.c:124-163): every hit when there are at most n_multi + 1 of them
-  int select_sai_multi(const std::vector<ibwa_aln1_t> &ag, Read &s, int n_multi, int64_t slot0,
+  // (positions as bwtdb_sa2seq gives them: not remapped)
+  int select_sai_multi(const std::vector<Aln> &ag, Read &s, int n_multi, int64_t slot0,
                        const std::vector<int64_t> &aslot, const std::vector<uint64_t> &pos) {
     int n_occ = 0;
-    for (const ibwa_aln1_t &q : ag) n_occ += (int)(q.l - q.k + 1);
+    for (const Aln &q : ag) n_occ += (int)(q.aln.l - q.aln.k + 1);
     s.multi.clear();
     if (n_occ > n_multi + 1) return 0;
     std::vector<Multi> all;
     for (size_t k = 0; k < ag.size(); ++k) {
-      const ibwa_aln1_t &q = ag[k];
+      const ibwa_aln1_t &q = ag[k].aln;
       const uint32_t w = q.l - q.k + 1;
       std::vector<uint64_t> own;
       const uint64_t *pp = nullptr;
@@ -718,11 +863,11 @@ struct Sampe {
       if (slot >= 0) {
         pp = pos.data() + slot;
       } else {  // not on hand (no -R pass, or a cached interval): bwtdb_sa2seq for this read
+        std::vector<int> dd(w, ag[k].dbidx);
         std::vector<uint8_t> st(w, (uint8_t)q.a);
         std::vector<uint32_t> kk(w), ll(w, (uint32_t)s.len);
         for (uint32_t r = 0; r < w; ++r) kk[r] = q.k + r;
-        own.resize(w);
-        if (ibwa_sa2pos(ctx, (int64_t)w, st.data(), kk.data(), ll.data(), 0, own.data())) return die("sa2pos");
+        if (int rc = sa2pos(dd, st, kk, ll, own)) return rc;
         pp = own.data();
       }
       for (uint32_t r = 0; r < w; ++r) {
@@ -740,7 +885,7 @@ struct Sampe {
     return 0;
   }
 
-  // bwa_paired_sw through the C-ABI drop-in (compat.cpp), on bwa_seq_t mirrors of the batch
+  // bwa_paired_sw through the C-ABI (compat.cpp) on bwa_seq_t mirrors of the batch
   int paired_sw(std::vector<Read> seqs[2], int n, const Isize &ii) {
     if (!popt.is_sw || ii.avg < 0.0) return 0;
     std::vector<ibwa_ref_seq_t> ref[2];
@@ -769,6 +914,8 @@ struct Sampe {
         t.seQ = (uint64_t)r.seQ;
         t.pos = r.pos;
         t.remapped_pos = r.remapped_pos;
+        t.dbidx = (uint32_t)r.dbidx;
+        t.remapped_dbidx = (uint32_t)r.remapped_dbidx;
         t.c1 = r.c1; t.c2 = r.c2;
       }
     }
@@ -781,7 +928,16 @@ struct Sampe {
     ibwa_ref_isize_info_t ri{ii.avg, ii.std, ii.ap_prior, ii.low, ii.high, ii.high_bayesian};
     ibwa_ref_seq_t *sp[2] = {ref[0].data(), ref[1].data()};
     uint64_t n_tot[2], n_mapped[2];
-    if (ibwa_paired_sw(ctx, n, sp, &po, &ri, b.pac.data(), (uint64_t)b.l_pac, n_tot, n_mapped)) return die("paired SW");
+    std::vector<const uint8_t *> pacs;
+    std::vector<uint64_t> offs, lens;
+    for (const RefDb &r : dbs.db) {
+      pacs.push_back(r.bns.pac.data());
+      offs.push_back(r.offset);
+      lens.push_back((uint64_t)r.bns.l_pac);
+    }
+    if (ibwa_paired_sw_dbs(ctx[0], n, sp, &po, &ri, (int)pacs.size(), pacs.data(), offs.data(), lens.data(), n_tot,
+                           n_mapped))
+      return die("paired SW");
     fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 singletons are mated.\n", (unsigned long long)n_mapped[1],
             (unsigned long long)n_tot[1]);
     fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 discordant pairs are fixed.\n", (unsigned long long)n_mapped[0],
@@ -798,6 +954,8 @@ struct Sampe {
         r.seQ = (int)t.seQ;
         r.pos = t.pos;
         r.remapped_pos = t.remapped_pos;
+        r.dbidx = (int)t.dbidx;
+        r.remapped_dbidx = (int)t.remapped_dbidx;
         if (t.cigar) {
           r.cigar.assign(t.cigar, t.cigar + t.n_cigar);
           r.has_cigar = true;
@@ -842,26 +1000,31 @@ int sampe_main(int argc, char *argv[]) {
   }
   if (optind + 5 > argc) {
     fprintf(stderr, "Usage: ibwa-amd sampe [-a INT] [-o INT] [-n INT] [-N INT] [-c FLOAT] [-f out.sam] [-r RG] [-sAR]\n"
-                    "                      <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq>\n");
+                    "                      <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq> [<prefix2> <in1.sai> <in2.sai> ...]\n");
     return 1;
   }
-  if (argc - optind > 5) {
-    fprintf(stderr, "[ibwa-amd sampe] several databases (<prefix2> <sai> <sai> ...) are not supported\n");
-    return 1;
-  }
-  const std::string prefix = argv[optind];
-  if (S.popt.remapping) {
-    if (FILE *fr = fopen((prefix + ".remap").c_str(), "r")) {
-      fclose(fr);
-      fprintf(stderr, "[ibwa-amd sampe] %s.remap: compound sequence remapping tables are not supported\n", prefix.c_str());
+  // pe_inputs_parse (bwape.c:548-581)
+  std::vector<std::string> prefixes{argv[optind]};
+  std::vector<std::pair<const char *, const char *>> sais{{argv[optind + 1], argv[optind + 2]}};
+  const char *fq[2] = {argv[optind + 3], argv[optind + 4]};
+  for (int i = optind + 5; i < argc; i += 3) {
+    if (argc - i < 3) {
+      fprintf(stderr, "[pe_inputs_parse] insufficient arguments\n");
       return 1;
     }
+    prefixes.push_back(argv[i]);
+    sais.push_back({argv[i + 1], argv[i + 2]});
   }
-  for (int j = 0; j < 2; ++j) {  // saiset_create (saiset.c:14-33)
-    S.fp_sai[j] = fopen(argv[optind + 1 + j], "rb");
-    if (!S.fp_sai[j] || fread(&S.gopt[j], sizeof S.gopt[j], 1, S.fp_sai[j]) != 1) {
-      fprintf(stderr, "[ibwa-amd sampe] cannot read the .sai header of %s\n", argv[optind + 1 + j]);
-      return 1;
+  const int count = (int)prefixes.size();
+  for (int j = 0; j < 2; ++j) {  // saiset_create (saiset.c:15-33): the last reference's header holds
+    for (int d = 0; d < count; ++d) {
+      const char *fn = j == 0 ? sais[d].first : sais[d].second;
+      FILE *fp = fopen(fn, "rb");
+      if (!fp || fread(&S.gopt[j], sizeof S.gopt[j], 1, fp) != 1) {
+        fprintf(stderr, "[ibwa-amd sampe] cannot read the .sai header of %s\n", fn);
+        return 1;
+      }
+      S.fp_sai[j].push_back(fp);
     }
     if (!(S.gopt[j].mode & IBWA_MODE_COMPREAD)) {
       fprintf(stderr, "[ibwa-amd sampe] color-space alignments (aln -c) need the .nt index: not supported\n");
@@ -870,40 +1033,64 @@ int sampe_main(int argc, char *argv[]) {
   }
   Source src[2];
   for (int j = 0; j < 2; ++j) {
-    if (!src[j].open(argv[optind + 3 + j], S.gopt[j])) {
-      fprintf(stderr, "[ibwa-amd sampe] cannot open %s\n", argv[optind + 3 + j]);
+    if (!src[j].open(fq[j], S.gopt[j])) {
+      fprintf(stderr, "[ibwa-amd sampe] cannot open %s\n", fq[j]);
       return 1;
     }
   }
-  if (!bns_restore(prefix, S.b)) {
-    fprintf(stderr, "[ibwa-amd sampe] cannot read %s.ann / .amb / .pac\n", prefix.c_str());
-    return 1;
+  // dbset_restore (dbset.c:135-176): references at cumulative offsets, each with its index on the
+  // GPU, and (-R) its .remap table when it has one
+  S.dbs.db.resize(count);
+  S.cache.resize(count);
+  for (int d = 0; d < count; ++d) {
+    RefDb &r = S.dbs.db[d];
+    const std::string &prefix = prefixes[d];
+    if (!bns_restore(prefix, r.bns)) {
+      fprintf(stderr, "[ibwa-amd sampe] cannot read %s.ann / .amb / .pac\n", prefix.c_str());
+      return 1;
+    }
+    r.offset = S.dbs.l_pac;
+    S.dbs.l_pac += (uint64_t)r.bns.l_pac;
+    if (S.popt.remapping) {  // seq_restore (dbset.c:81-101)
+      r.remap = load_remappings(prefix + ".remap", r.bns.n_seqs, r.mappings);
+      if (r.remap < 0) {
+        fprintf(stderr, "Fatal error loading sequence mappings from %s\n", (prefix + ".remap").c_str());
+        return 1;
+      } else if (r.remap) {
+        fprintf(stderr, " - Remapping enabled for sequence %s\n", prefix.c_str());
+      }
+    }
+    ibwa_ctx_t *cx = nullptr;
+    if (ibwa_ctx_create(0, &cx)) return die("ibwa_ctx_create");
+    S.ctx.push_back(cx);
+    if (ibwa_ctx_load_bwt_file(cx, 0, (prefix + ".bwt").c_str()) || ibwa_ctx_load_bwt_file(cx, 1, (prefix + ".rbwt").c_str()))
+      return die("load .bwt / .rbwt");
+    if (ibwa_ctx_load_sa_file(cx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(cx, 1, (prefix + ".rsa").c_str()))
+      return die("load .sa / .rsa");
+    if (ibwa_ctx_expand_sa(cx)) return die("expand SA");
   }
-  if (ibwa_ctx_create(0, &S.ctx)) return die("ibwa_ctx_create");
-  if (ibwa_ctx_load_bwt_file(S.ctx, 0, (prefix + ".bwt").c_str()) ||
-      ibwa_ctx_load_bwt_file(S.ctx, 1, (prefix + ".rbwt").c_str()))
-    return die("load .bwt / .rbwt");
-  if (ibwa_ctx_load_sa_file(S.ctx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(S.ctx, 1, (prefix + ".rsa").c_str()))
-    return die("load .sa / .rsa");
-  if (ibwa_ctx_expand_sa(S.ctx)) return die("expand SA");
-  S.rnd.seed((long)S.b.seed);  // srand48(bns->seed), bwape.c:461
+  S.rnd.seed((long)S.dbs.db[0].bns.seed);  // srand48(dbs->db[0]->bns->bns->seed), bwape.c:471
   S.rg_id = rg_id.empty() ? nullptr : rg_id.c_str();
   FILE *out = fn_out ? fopen(fn_out, "w") : stdout;
   if (!out) {
     fprintf(stderr, "[ibwa-amd sampe] cannot write %s\n", fn_out);
     return 1;
   }
-  // @SQ lines, then @RG, then @PG (dbset_print_sam_SQ, bwa_print_sam_PG)
+  // @SQ lines of every sequence that is not remapped (dbset_print_sam_SQ, dbset.c:327-339), @RG, @PG
   std::string head;
-  for (const Ann &a : S.b.anns) head += "@SQ\tSN:" + a.name + "\tLN:" + std::to_string(a.len) + "\n";
+  for (const RefDb &r : S.dbs.db)
+    for (int32_t t = 0; t < r.bns.n_seqs; ++t)
+      if (!r.remap || t >= (int32_t)r.mappings.size() || !r.mappings[t])
+        head += "@SQ\tSN:" + r.bns.anns[t].name + "\tLN:" + std::to_string(r.bns.anns[t].len) + "\n";
   if (!rg_line.empty()) head += rg_line + "\n";
   head += "@PG\tID:bwa\tPN:bwa\tVN:ibwa-amd\n";
   fwrite(head.data(), 1, head.size(), out);
   Source *sp = src;
   S.ph.mark("load index");
   const int rc = S.run(sp, out);
-  for (int j = 0; j < 2; ++j) fclose(S.fp_sai[j]);
+  for (int j = 0; j < 2; ++j)
+    for (FILE *fp : S.fp_sai[j]) fclose(fp);
   if (out != stdout) fclose(out);
-  ibwa_ctx_destroy(S.ctx);
+  for (ibwa_ctx_t *cx : S.ctx) ibwa_ctx_destroy(cx);
   return rc;
 }

@@ -35,11 +35,14 @@ template <class Reader>
 int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::string &prefix, int n_occ, FILE *out,
               const std::string &rg_line, const std::string &rg_id) {
   Phases ph;
-  Bns b;
+  Dbs dbs;  // samse: a set of one reference (dbset_restore, dbset.c:135)
+  dbs.db.resize(1);
+  Bns &b = dbs.db[0].bns;
   if (!bns_restore(prefix, b)) {
     fprintf(stderr, "[ibwa-amd samse] cannot read %s.ann / .amb / .pac\n", prefix.c_str());
     return 1;
   }
+  dbs.l_pac = (uint64_t)b.l_pac;
   ibwa_ctx_t *ctx = nullptr;
   if (ibwa_ctx_create(0, &ctx)) return die("ibwa_ctx_create");
   if (ibwa_ctx_load_bwt_file(ctx, 0, (prefix + ".bwt").c_str()) ||
@@ -114,11 +117,11 @@ int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::str
     // ---- bwa_refine_gapped (bwase.c:333-416): one global-alignment launch, MD/NM, trimmed reads
     std::vector<Read *> rp;
     for (Read &p : seqs) rp.push_back(&p);
-    if (int rc = refine_gapped(ctx, b, rp)) return rc == 1 ? 1 : die("global alignment");
+    if (int rc = refine_gapped(ctx, dbs, rp)) return rc == 1 ? 1 : die("global alignment");
     ph.mark("refine+md");
     // ---- print
     print_parallel(o, (int64_t)seqs.size(),
-                   [&](Out &ob, int64_t i) { print_sam1(ob, b, seqs[i], nullptr, opt.mode, opt.max_top2, rgid); });
+                   [&](Out &ob, int64_t i) { print_sam1(ob, dbs, seqs[i], nullptr, opt.mode, opt.max_top2, rgid); });
     ph.mark("print");
     fprintf(stderr, "[bwa_aln_core] %ld sequences have been processed.\n", tot);
   }

@@ -106,6 +106,8 @@ CAPI = {
                                c.POINTER(_i64)]),
     "ibwa_paired_sw": (_i, [_vp, _i, c.POINTER(c.POINTER(RefSeq)), c.POINTER(PeOpt), c.POINTER(IsizeInfo), _vp,
                             _u64, c.POINTER(_u64), c.POINTER(_u64)]),
+    "ibwa_paired_sw_dbs": (_i, [_vp, _i, c.POINTER(c.POINTER(RefSeq)), c.POINTER(PeOpt), c.POINTER(IsizeInfo), _i, _vp,
+                                _vp, _vp, c.POINTER(_u64), c.POINTER(_u64)]),
     "ibwa_sw_core_batch": (_i, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
                                 c.POINTER(c.c_void_p)]),
 }

@@ -213,6 +213,14 @@ int ibwa_paired_sw(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
                    uint64_t n_mapped[2]);
 
 /*
+ * ibwa_paired_sw over several references concatenated at offset[i] (dbset_extract_sequence,
+ * dbset.c:306-325): pac[i] / l_pac[i] as seq_t.data / bntseq_t.l_pac of reference i.
+ */
+int ibwa_paired_sw_dbs(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const ibwa_ref_pe_opt_t *popt,
+                       const ibwa_ref_isize_info_t *ii, int n_db, const uint8_t *const *pac, const uint64_t *offset,
+                       const uint64_t *l_pac, uint64_t n_tot[2], uint64_t n_mapped[2]);
+
+/*
  * bwa_paired_sw (bwasw.h:12, bwasw.c:270-304) with the reference's own signature: a reference
  * `sampe` links this in place of bwasw.o.  The references of `dbs` are concatenated at their
  * db->offset as dbset_extract_sequence (dbset.c:306-325) reads them; each one's packed

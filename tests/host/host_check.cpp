@@ -30,7 +30,7 @@ template <class Reader>
 int drain(Reader &rd, int mode, int trim) {
   const int kBatch = 1000;  // small batches: many hand-overs between the parser and the printer
   Out o{stdout, {}};
-  Bns none;
+  Dbs none;  // unmapped reads only: no reference is consulted
   std::vector<Read> cur, nxt;
   bool done = false;  // the reader has ended (end of input or a bad record): do not read on
   auto fill = [&](std::vector<Read> &b) {

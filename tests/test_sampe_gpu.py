@@ -36,12 +36,41 @@ def test_sampe_matches_reference(golden_dir, key, tmp_path):
     assert not bad, f"{len(bad)} lines differ; first:\n got {bad[0][1]}\nwant {bad[0][2]}"
 
 
-def test_sampe_rejects_several_databases(golden_dir):
+REMAP = json.load(open(os.path.join(ROOT, "tests", "golden", "remap_manifest.json")))
+
+
+@pytest.mark.parametrize("key", sorted(REMAP))
+def test_sampe_several_references_and_remap(golden_dir, key, tmp_path):
+    """`sampe [-R] <pri> <1.sai> <2.sai> <1.fq> <2.fq> <alt> <a1.sai> <a2.sai>` (pe_inputs_parse,
+    bwape.c:548-581) over the primary genome and an alternate-haplotype reference with a .remap
+    table (tools/make_remap_golden.py): alngrp_create's merge of both references' records,
+    remapped primary coordinates with ZR:Z, translated CIGARs, @SQ without the mapped alternates;
+    without -R, and with -R but no .remap file.  Byte for byte except @PG."""
+    m = REMAP[key]
     g = lambda x: os.path.join(golden_dir, x)  # noqa: E731
-    r = subprocess.run([CLI, "sampe", "-R", g("g1m"), g("pe70few.default_1.sai"), g("pe70few.default_2.sai"),
-                        g("pe70few_1.fq"), g("pe70few_2.fq"), g("g1m"), g("pe70few.default_1.sai"),
-                        g("pe70few.default_2.sai")], capture_output=True, text=True, timeout=120)
-    assert r.returncode != 0 and "databases" in r.stderr
+    args = [g(m["prefixes"][0]), *map(g, m["sai"][0]), *map(g, m["reads"])]
+    for pre, sai in zip(m["prefixes"][1:], m["sai"][1:]):
+        args += [g(pre), *map(g, sai)]
+    out = tmp_path / "out.sam"
+    r = subprocess.run([CLI, "sampe"] + m["argv"] + ["-f", str(out)] + args, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = _body(gzip.open(g(m["sam"]), "rt").read())
+    got = _body(out.read_text())
+    assert len(got) == len(want)
+    bad = [(i, gl, w) for i, (gl, w) in enumerate(zip(got, want)) if gl != w]
+    assert not bad, f"{len(bad)} lines differ; first:\n got {bad[0][1]}\nwant {bad[0][2]}"
+    if "-R" in m["argv"] and m["prefixes"][1] == "remap_alt":
+        assert any("\tZR:Z:" in ln for ln in got)
+
+
+def test_sampe_incomplete_reference_group(golden_dir):
+    """A trailing reference without both .sai files is refused (pe_inputs_parse)."""
+    g = lambda x: os.path.join(golden_dir, x)  # noqa: E731
+    r = subprocess.run([CLI, "sampe", g("g1m"), g("pe70few.default_1.sai"), g("pe70few.default_2.sai"),
+                        g("pe70few_1.fq"), g("pe70few_2.fq"), g("g1m"), g("pe70few.default_1.sai")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "insufficient arguments" in r.stderr
 
 
 @pytest.mark.parametrize("key", ["pe100.default", "pe100.q20", "pe100.k0n3", "pe150.default", "tandem.R"])
