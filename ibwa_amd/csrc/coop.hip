@@ -174,9 +174,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
   // diagnostics (A.prof): wave cycles per phase -- 0 hit barriers, 1 commits, 2 claims,
   // 3 loads + consume, 4 level set-up / teardown, 5 read set-up; 6 iterations, 7 commits, 8 levels
   const bool prof = PROF && A.prof != nullptr;
-  __shared__ unsigned long long pc[9];  // LDS: no registers taken from the hot loop
+  // 9..11: lanes running a chain / fetching its entry / in an exact tail, summed over iterations
+  __shared__ unsigned long long pc[12];  // LDS: no registers taken from the hot loop
   if (prof) {
-    if (lane < 9) pc[lane] = 0;
+    if (lane < 12) pc[lane] = 0;
     __syncthreads();
   }
   auto now = []() __attribute__((always_inline)) -> uint64_t { return __builtin_amdgcn_s_memtime(); };
@@ -613,6 +614,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           if (lst == L_FETCH) ent = A.pool[((uint64_t)ent_page << COOP_PG_LOG2) + ent_off];
           const bool exp = lst == L_EXP;
           const bool tail = lst == L_TAIL;
+          if (prof) {
+            const unsigned long long b_act = __ballot(lst != L_IDLE), b_f = __ballot(lst == L_FETCH),
+                                     b_t = __ballot(tail);
+            if (lane == 0) {
+              pc[9] += __popcll(b_act);
+              pc[10] += __popcll(b_f);
+              pc[11] += __popcll(b_t);
+            }
+          }
           const uint32_t qk = tail ? xk : k, ql = tail ? xl : l;
           const bool qkneg = qk == 0;
           const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
@@ -785,7 +795,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     lap(5);
   }
   if (prof && lane == 0)
-    for (int q = 0; q < 9; ++q) atomicAdd(A.prof + q, (unsigned long long)pc[q]);
+    for (int q = 0; q < 12; ++q) atomicAdd(A.prof + q, (unsigned long long)pc[q]);
 }
 
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {

@@ -1064,15 +1064,17 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(hipEventSynchronize(c->ev[4]));
     if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop kernel done\n", since());
     if (c->prof_phases) {
-      unsigned long long pf[9];
+      unsigned long long pf[12];
       HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
       const char *nm[6] = {"barriers", "commits", "claims", "loads+consume", "levels", "read set-up"};
       double tot = 0;
       for (int q = 0; q < 6; ++q) tot += (double)pf[q];
       fprintf(stderr, "[ibwa_amd] k_coop phases (wave cycles):");
       for (int q = 0; q < 6; ++q) fprintf(stderr, " %s %.1f%%", nm[q], tot > 0 ? 100.0 * pf[q] / tot : 0.0);
-      fprintf(stderr, "; %llu iterations (%.0f cycles each), %llu commits, %llu levels\n", pf[6],
-              pf[6] ? tot / pf[6] : 0.0, pf[7], pf[8]);
+      fprintf(stderr, "; %llu iterations (%.0f cycles each), %llu commits, %llu levels; lanes per iteration: "
+              "%.1f running (%.1f fetching an entry, %.1f in an exact tail)\n", pf[6], pf[6] ? tot / pf[6] : 0.0, pf[7],
+              pf[8], pf[6] ? (double)pf[9] / pf[6] : 0.0, pf[6] ? (double)pf[10] / pf[6] : 0.0,
+              pf[6] ? (double)pf[11] / pf[6] : 0.0);
     }
     float a = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));

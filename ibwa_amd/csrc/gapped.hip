@@ -230,6 +230,14 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   int C_b = 0;
   bool C_valid = false;
   bool C_load = false;  // C's data arrives with this iteration's loads (slot C_slot)
+  // Register cache of the stack top.  A push that becomes the candidate is not stored: it stays in
+  // C ("dirty") and is written only if it is displaced twice.  The entry a push displaces from C
+  // is kept in D (with its slot): it is exactly the next candidate once the pushed entry is popped
+  // (it was the head of the pushed entry's bucket, or of the next non-empty one), so a match chain
+  // -- pop, expand, pop the match child -- needs neither the candidate load nor the child's store.
+  // Flags: bit 0 C dirty, bit 1 D valid, bit 2 D dirty.
+  uint4 D = make_uint4(0, 0, 0, 0);
+  uint32_t D_slot = 0, cfl = 0;
   // exact sub-search state
   uint32_t xk = 0, xl = 0;
   int xj = 0, xa = 0;
@@ -376,6 +384,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           C_b = 0;
           C_valid = true;
           C_load = false;
+          cfl = 0;
           st = 1;
         }
       }
@@ -459,7 +468,17 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         }
       }
       C_valid = false;
-      if (C_load) C_slot = load_slot;
+      if (C_load) {
+        C_slot = load_slot;
+        if ((cfl & 2u) && load_slot == D_slot) {  // the next candidate is the cached D: no load
+          C = D;
+          C_valid = true;
+          C_load = false;
+          cfl = (cfl >> 2) & 1u;  // C dirty = D dirty; D invalid
+        } else {
+          cfl &= ~1u;  // C arrives from memory
+        }
+      }
     }
 
     uint64_t t_issue = pnow();
@@ -708,10 +727,25 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           const uint32_t slot = t < n_fs ? (uint32_t)fsv : (t == n_fs && use_fl) ? fl_slot : bs;
           const uint32_t hd = (uint32_t)lds_heads[((sc) << nbl) + ltid];  // NIL when the bucket is empty
           const uint4 ne = E::make(pk, pl, pi, pldp, hd, n_mm, n_gapo, n_gape, a, pstate);
-          *slot_ptr(slot) = ne;
           lds_heads[((sc) << nbl) + ltid] = (H)slot;
           const bool take = !C_valid || sc <= C_b;
+          // a child that does not become the candidate is stored; one that does pushes C down to D,
+          // and the old D is stored if memory does not hold it yet
+          const bool wr = !take || (cfl & 6u) == 6u;
           // per component: a select of two uint4 aggregates is lowered to an indexed scratch access
+          uint4 wv;
+          wv.x = take ? D.x : ne.x;
+          wv.y = take ? D.y : ne.y;
+          wv.z = take ? D.z : ne.z;
+          wv.w = take ? D.w : ne.w;
+          if (wr) *slot_ptr(take ? D_slot : slot) = wv;
+          D.x = take ? C.x : D.x;
+          D.y = take ? C.y : D.y;
+          D.z = take ? C.z : D.z;
+          D.w = take ? C.w : D.w;
+          D_slot = take ? C_slot : D_slot;
+          // take: D valid = C valid, D dirty = C dirty, C dirty
+          cfl = take ? (C_valid ? 2u : 0u) | (cfl & 1u) << 2 | 1u : cfl;
           C.x = take ? ne.x : C.x;
           C.y = take ? ne.y : C.y;
           C.z = take ? ne.z : C.z;
