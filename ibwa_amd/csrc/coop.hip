@@ -315,6 +315,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         int xj = 0;
         uint32_t xk = 0, xl = 0;
         uint32_t ent_page = 0, ent_off = 0;
+        // Entry window: lane x holds the entry of chain wh (wh = x mod 64), loaded with an earlier
+        // iteration's round trip, so a chain claimed inside the window starts expanding in the
+        // iteration that claims it instead of spending one on fetching its entry.
+        uint32_t wh = (uint32_t)lane;
+        uint4 wen = make_uint4(0, 0, 0, 0);
+        bool wld = false, wreq = wh < N;
         uint32_t hit_c = NONE;  // chain this lane ended with a hit in the last iteration
         // end the lane's chain: its record (hit or not) goes to the reorder buffer
         auto end_chain = [&](bool hit, uint32_t hk, uint32_t hl) __attribute__((always_inline)) {
@@ -332,6 +338,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
                                     1u | mpre << 1);
           if (hit) hit_c = c;
           lst = L_IDLE;
+        };
+        auto take_entry = [&](const uint4 &ent) __attribute__((always_inline)) {
+          k = ent.x;
+          l = ent.y;
+          i = (int)(ent.z & 0x3ff);
+          ldp = (int)((ent.z >> 10) & 0x3ff);
+          e_mm = (int)(ent.w & 0xff);
+          e_go = (int)((ent.w >> 8) & 0xff);
+          e_ge = (int)((ent.w >> 16) & 0xff);
+          a = (int)((ent.w >> 24) & 1);
+          state = (int)((ent.w >> 25) & 3);
         };
         // the pops of bwtgap.c:139-163 for the node in registers: prune, hit, tail or expand
         auto pop_node = [&]() __attribute__((always_inline)) {
@@ -389,6 +406,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               }
               barrier = newb;
               next_c = newb + 1;
+              // the window restarts at the rolled-back claim point
+              const uint32_t nh = next_c + (((uint32_t)lane - next_c) & 63u);
+              if (nh != wh) {
+                wh = nh;
+                wld = false;
+                wreq = wh < N;
+              }
             }
           }
           lap(0);
@@ -460,19 +484,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
                 break;
               }
               __syncthreads();
-              // copy: the batch's children, flattened, 64 per round trip and four round trips'
-              // loads in flight; child g belongs to chain j with pre_j <= g < pre_j + tot_j
+              // copy: the batch's children, flattened, 64 per round trip and two round trips'
+              // loads in flight (four spill registers); child g belongs to chain j with pre_j <= g < pre_j + tot_j
               // (binary search over the lanes' prefixes) and goes to its category's bucket at
               // (bucket size) + (chain's offset in the batch) + (its rank in the chain)
               {
                 const uint32_t my_rl = (ra.z >> 16) & 63, my_st = ra.x;
                 const uint32_t nb0 = S.nb[t0], nb1 = t1 < o.n_stacks ? S.nb[t1] : 0u,
                                nb2 = t2 < o.n_stacks ? S.nb[t2] : 0u;
-                for (uint32_t g0 = 0; g0 < dsum; g0 += 256) {
-                  uint4 e[4];
-                  uint32_t f0[4], f1[4], f2[4];
+                for (uint32_t g0 = 0; g0 < dsum; g0 += 64u * 2) {
+                  uint4 e[2];
+                  uint32_t f0[2], f1[2], f2[2];
 #pragma unroll
-                  for (int u = 0; u < 4; ++u) {
+                  for (int u = 0; u < 2; ++u) {
                     const uint32_t g = g0 + 64u * u + (uint32_t)lane;
                     int j = 0;
 #pragma unroll
@@ -489,7 +513,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
                     if (g < dsum) e[u] = stg_base[((uint64_t)rl << A.stg_log2) + ((st0 + x) & SMASK)];
                   }
 #pragma unroll
-                  for (int u = 0; u < 4; ++u) {
+                  for (int u = 0; u < 2; ++u) {
                     if (g0 + 64u * u + (uint32_t)lane < dsum) {
                       const uint32_t q = (e[u].w >> 27) & 3u, rk = e[u].z >> 20;
                       const uint32_t pos = (q == 0 ? f0[u] : q == 1 ? f1[u] : f2[u]) + rk;
@@ -594,17 +618,35 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             const uint32_t cap_c = cp + RREC < N ? cp + RREC : N;
             const uint32_t avail = cap_c > next_c ? cap_c - next_c : 0u;
             const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
-            if (want && rank < avail) {
-              c = next_c + rank;
-              cstart = stg_w;
-              cnt0 = cnt1 = cnt2 = 0;
-              const uint32_t idx = N - 1u - c;  // LIFO: chain 0 is the top of the bucket
-              ent_page = S.dirc[0][idx >> COOP_PG_LOG2];
-              ent_off = idx & (COOP_PG - 1);
-              lst = L_FETCH;
+            if (wm) {
+              // every lane takes part in the shuffles; the claim reads its chain's window slot
+              const uint32_t cc = next_c + rank, src = cc & 63u;
+              const uint32_t tag = __shfl(wld ? wh : NONE, (int)src);
+              const uint4 ce = make_uint4(__shfl(wen.x, (int)src), __shfl(wen.y, (int)src), __shfl(wen.z, (int)src),
+                                          __shfl(wen.w, (int)src));
+              if (want && rank < avail) {
+                c = cc;
+                cstart = stg_w;
+                cnt0 = cnt1 = cnt2 = 0;
+                if (tag == cc) {
+                  take_entry(ce);
+                  pop_node();
+                } else {
+                  const uint32_t idx = N - 1u - c;  // LIFO: chain 0 is the top of the bucket
+                  ent_page = S.dirc[0][idx >> COOP_PG_LOG2];
+                  ent_off = idx & (COOP_PG - 1);
+                  lst = L_FETCH;
+                }
+              }
+              const uint32_t nw = (uint32_t)__popcll(wm);
+              next_c += nw < avail ? nw : avail;
+              // window slots whose chain is now claimed move on to the chain 64 further
+              while (wh < next_c) {
+                wh += 64;
+                wld = false;
+                wreq = wh < N;
+              }
             }
-            const uint32_t nw = (uint32_t)__popcll(wm);
-            next_c += nw < avail ? nw : avail;
           }
           lap(2);
           // ============================================ loads of this iteration (one round trip)
@@ -612,6 +654,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           const uint4 *ob = a ? A.o64[0] : A.o64[1];
           uint4 ent = make_uint4(0, 0, 0, 0);
           if (lst == L_FETCH) ent = A.pool[((uint64_t)ent_page << COOP_PG_LOG2) + ent_off];
+          if (wreq) {
+            const uint32_t widx = N - 1u - wh;
+            wen = A.pool[((uint64_t)S.dirc[0][widx >> COOP_PG_LOG2] << COOP_PG_LOG2) + (widx & (COOP_PG - 1))];
+            wld = true;
+            wreq = false;
+          }
           const bool exp = lst == L_EXP;
           const bool tail = lst == L_TAIL;
           if (prof) {
@@ -636,15 +684,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
 
           // ============================================ consume
           if (lst == L_FETCH) {
-            k = ent.x;
-            l = ent.y;
-            i = (int)(ent.z & 0x3ff);
-            ldp = (int)((ent.z >> 10) & 0x3ff);
-            e_mm = (int)(ent.w & 0xff);
-            e_go = (int)((ent.w >> 8) & 0xff);
-            e_ge = (int)((ent.w >> 16) & 0xff);
-            a = (int)((ent.w >> 24) & 1);
-            state = (int)((ent.w >> 25) & 3);
+            take_entry(ent);
             pop_node();
           } else if (tail) {
             // one step of bwt_match_exact_alt (bwt.c:240-247)

@@ -183,7 +183,12 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   const int ltid = (tid >> 6) * A.lanes_per_wave + (lane < A.lanes_per_wave ? lane : 0);
   const AlnOpt o = A.o;
   H *const lds_heads = reinterpret_cast<H *>(lds_raw);
-  H *const free_slots = lds_heads + o.n_stacks * LNB;  // free_slots[j * NB + tid]
+  // free stack of popped slots: narrow, 8 u16 per lane side by side (one 16 B read per expansion);
+  // wide (retry pass), lane-minor rows
+  H *const free_slots = lds_heads + o.n_stacks * LNB;
+  auto fsi = [&](uint32_t j) __attribute__((always_inline)) -> uint32_t {
+    return WIDE ? (j << nbl) + ltid : (uint32_t)ltid * NARROW_FREE_DEPTH + j;
+  };
   const uint32_t FREE_DEPTH = WIDE ? (uint32_t)A.free_depth : (uint32_t)NARROW_FREE_DEPTH;
   uint16_t *const ptab = reinterpret_cast<uint16_t *>(free_slots + FREE_DEPTH * LNB);  // ptab[((q) << nbl) + ltid]
   uint32_t *const bitmap =
@@ -445,7 +450,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       if (C_slot + 1 == bump) {
         bump = C_slot;
       } else if (n_free < FREE_DEPTH) {
-        free_slots[((n_free) << nbl) + ltid] = (H)C_slot;
+        free_slots[fsi(n_free)] = (H)C_slot;
         ++n_free;
       } else {
         reinterpret_cast<uint32_t *>(slot_ptr(C_slot))[0] = fl_head;
@@ -704,56 +709,97 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         const bool use_fl = npush > n_fs && fl_head != NILH;    // one slot of the free list (fl_known)
         const uint32_t fs_top = n_free, fl_slot = fl_head, b0 = bump, skip_at = P0 - HS;
         const uint32_t fl_n = use_fl ? 1u : 0u;
-        uint32_t t = 0;
-        while (vm) {
-          if (pleader()) ++pf5;
-          const uint32_t j = (uint32_t)__builtin_ctz(vm);
-          vm &= vm - 1;
-          const bool is_ins = j == 0, is_del = j - 1 < 4, is_gap = j < 5;
-          const bool is_match = j == 8 && csym < 4;
-          const uint32_t c = is_del ? j - 1 : (csym + j - 4) & 3;
-          const uint32_t pk = is_ins ? k : pick4(KK, c);
-          const uint32_t pl = is_ins ? l : pick4(LL, c);
-          const int n_mm = e_mm + (!is_gap && !is_match ? 1 : 0);
-          const int n_gapo = e_go + (is_gap && open ? 1 : 0), n_gape = e_ge + (is_gap && !open ? 1 : 0);
-          const int pi = is_del ? ni + 1 : ni;
-          const int pstate = is_ins ? STATE_I : is_del ? STATE_D : STATE_M;
-          const int pldp = is_match ? ldp : pi;
-          const int sc = is_gap ? scG : is_match ? sc_base : scMM;
-          // slot: free stack, then the free list's head, then the bump region (skipping the hit area)
-          const uint32_t fsv = free_slots[((t < n_fs ? fs_top - 1 - t : 0u) << nbl) + ltid];
+        // narrow: the lane's whole free stack in one LDS read
+        uint4 fsr = make_uint4(0, 0, 0, 0);
+        if (!WIDE && n_fs) fsr = *reinterpret_cast<const uint4 *>(free_slots + fsi(0));
+        // slot of the t-th push: free stack, then the free list's head, then the bump region
+        // (skipping the hit area)
+        auto slot_at = [&](uint32_t t) __attribute__((always_inline)) -> uint32_t {
+          const uint32_t fj = t < n_fs ? fs_top - 1 - t : 0u;
+          uint32_t fsv;
+          if (WIDE) {
+            fsv = (uint32_t)free_slots[fsi(fj)];
+          } else {
+            const uint32_t wlo = (fj & 2) ? fsr.y : fsr.x, whi = (fj & 2) ? fsr.w : fsr.z;
+            fsv = (((fj & 4) ? whi : wlo) >> (16 * (fj & 1))) & 0xffffu;
+          }
           uint32_t bs = b0 + (t - n_fs - fl_n);
           bs += (b0 <= skip_at && bs >= skip_at) ? HS : 0u;
-          const uint32_t slot = t < n_fs ? (uint32_t)fsv : (t == n_fs && use_fl) ? fl_slot : bs;
-          const uint32_t hd = (uint32_t)lds_heads[((sc) << nbl) + ltid];  // NIL when the bucket is empty
-          const uint4 ne = E::make(pk, pl, pi, pldp, hd, n_mm, n_gapo, n_gape, a, pstate);
-          lds_heads[((sc) << nbl) + ltid] = (H)slot;
-          const bool take = !C_valid || sc <= C_b;
-          // a child that does not become the candidate is stored; one that does pushes C down to D,
-          // and the old D is stored if memory does not hold it yet
-          const bool wr = !take || (cfl & 6u) == 6u;
-          // per component: a select of two uint4 aggregates is lowered to an indexed scratch access
-          uint4 wv;
-          wv.x = take ? D.x : ne.x;
-          wv.y = take ? D.y : ne.y;
-          wv.z = take ? D.z : ne.z;
-          wv.w = take ? D.w : ne.w;
-          if (wr) *slot_ptr(take ? D_slot : slot) = wv;
-          D.x = take ? C.x : D.x;
-          D.y = take ? C.y : D.y;
-          D.z = take ? C.z : D.z;
-          D.w = take ? C.w : D.w;
-          D_slot = take ? C_slot : D_slot;
-          // take: D valid = C valid, D dirty = C dirty, C dirty
-          cfl = take ? (C_valid ? 2u : 0u) | (cfl & 1u) << 2 | 1u : cfl;
-          C.x = take ? ne.x : C.x;
-          C.y = take ? ne.y : C.y;
-          C.z = take ? ne.z : C.z;
-          C.w = take ? ne.w : C.w;
-          C_slot = take ? slot : C_slot;
-          C_b = take ? sc : C_b;
+          return t < n_fs ? fsv : (t == n_fs && use_fl) ? fl_slot : bs;
+        };
+        // a taking group puts its last child in C (stored, clean); what C and D held is stored
+        // first if memory lacks it, and D is dropped (the next candidate after C is loaded)
+        auto group_take = [&](bool tk, uint4 last, uint32_t last_slot, int sc) __attribute__((always_inline)) {
+          if (tk && C_valid && (cfl & 1u)) *slot_ptr(C_slot) = C;
+          if (tk && (cfl & 6u) == 6u) *slot_ptr(D_slot) = D;
+          if (tk) {
+            C = last;
+            C_slot = last_slot;
+            C_b = sc;
+            C_valid = true;
+            cfl = 0;
+          }
+        };
+        uint32_t t = 0;
+        // ---- gap children (bit 0 insertion, bits 1-4 deletion by A..T): bucket scG, stored in order,
+        // each linked to the one before
+        const uint32_t vg = vm & 0x1Fu;
+        if (vg) {
+          if (pleader()) ++pf5;
+          const bool tk = !C_valid || scG <= C_b;
+          uint32_t link = (uint32_t)lds_heads[((scG) << nbl) + ltid];
+          const int n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (open ? 0 : 1);
+          uint4 last = make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            if (vg & (1u << j)) {
+              const uint32_t slot = slot_at(t++);
+              const uint32_t pk = j == 0 ? k : j == 1 ? KK.x : j == 2 ? KK.y : j == 3 ? KK.z : KK.w;
+              const uint32_t pl = j == 0 ? l : j == 1 ? LL.x : j == 2 ? LL.y : j == 3 ? LL.z : LL.w;
+              const int pi = j == 0 ? ni : ni + 1;
+              last = E::make(pk, pl, pi, pi, link, e_mm, n_gapo, n_gape, a, j == 0 ? STATE_I : STATE_D);
+              *slot_ptr(slot) = last;
+              link = slot;
+            }
+          }
+          lds_heads[((scG) << nbl) + ltid] = (H)link;
+          group_take(tk, last, link, scG);
+        }
+        // ---- mismatch children (bits 5-8 but the match child): bucket scMM
+        const uint32_t vmm = vm & vm_mm;
+        if (vmm) {
+          if (pleader()) ++pf5;
+          const bool tk = !C_valid || scMM <= C_b;
+          uint32_t link = (uint32_t)lds_heads[((scMM) << nbl) + ltid];
+          uint4 last = make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int j = 5; j < 9; ++j) {
+            if (vmm & (1u << j)) {
+              const uint32_t slot = slot_at(t++);
+              const uint32_t c = (csym + (uint32_t)j - 4u) & 3u;
+              last = E::make(pick4(KK, c), pick4(LL, c), ni, ni, link, e_mm + 1, e_go, e_ge, a, STATE_M);
+              *slot_ptr(slot) = last;
+              link = slot;
+            }
+          }
+          lds_heads[((scMM) << nbl) + ltid] = (H)link;
+          group_take(tk, last, link, scMM);
+        }
+        // ---- the match child (bucket sc_base <= C_b: always the new candidate): kept in C, not
+        // stored; C moves to D, the old D is stored if memory lacks it
+        if (has_match && vm) {
+          const uint32_t slot = slot_at(t++);
+          const uint32_t hd = (uint32_t)lds_heads[((sc_base) << nbl) + ltid];
+          const uint4 ne = E::make(pick4(KK, csym), pick4(LL, csym), ni, ldp, hd, e_mm, e_go, e_ge, a, STATE_M);
+          lds_heads[((sc_base) << nbl) + ltid] = (H)slot;
+          if ((cfl & 6u) == 6u) *slot_ptr(D_slot) = D;
+          D = C;
+          D_slot = C_slot;
+          cfl = (C_valid ? 2u : 0u) | (cfl & 1u) << 2 | 1u;
+          C = ne;
+          C_slot = slot;
+          C_b = sc_base;
           C_valid = true;
-          ++t;
         }
         if (t) {
           n_free -= n_fs;

@@ -24,7 +24,8 @@ namespace {
 
 constexpr int Q = 26, R = 9, QR = Q + R, BAND = 50, MAXSC = 11;
 constexpr int STRIP = 32;  // forward-pass columns held in registers
-constexpr int RCHUNK = 8;  // reverse-pass cells whose loads are issued together
+constexpr int RCHUNK = 16;  // reverse-pass cells whose loads are issued together
+constexpr int GCH = 8;      // global-fill cells whose loads are issued together
 constexpr int NEG_INF = -1073741823;  // MINOR_INF (stdaln.h:84)
 constexpr int FM = 0, FI = 1, FD = 2;  // FROM_M / FROM_I / FROM_D
 
@@ -104,35 +105,52 @@ __device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD,
     }
     // diagonal cell (j-1, i-1) starts at column lo
     int dm = (int)M(prv, lo), di = (int)I(prv, lo), dd = (int)D(prv, lo);
-    for (int i = lo + 1; i <= hi; ++i) {
-      const int sc = sm(cb, a[i - 1]);
-      int m, iv, dv;
-      uint8_t tm, ti, td;
-      // set_M (stdaln.c:271-287)
-      if (dm >= di) {
-        if (dm >= dd) { m = dm + sc; tm = FM; } else { m = dd + sc; tm = FD; }
-      } else {
-        if (di > dd) { m = di + sc; tm = FI; } else { m = dd + sc; tm = FD; }
+    // GCH cells at a time: the row above's values and the codes of the chunk are loaded together
+    // before its cells are computed and stored (a cell stores into row `cur` only)
+    for (int i0 = lo + 1; i0 <= hi; i0 += GCH) {
+      int um_[GCH], ui_[GCH], ud_[GCH];
+      uint32_t ca_[GCH];
+#pragma unroll
+      for (int q = 0; q < GCH; ++q) {
+        const int i = i0 + q <= hi ? i0 + q : hi;
+        um_[q] = (int)M(prv, i);
+        ui_[q] = (int)I(prv, i);
+        ud_[q] = (int)D(prv, i);
+        ca_[q] = a[i - 1];
       }
-      // above cell (j-1, i)
-      const int um = (int)M(prv, i), ui = (int)I(prv, i), ud = (int)D(prv, i);
-      // set_I from above; the last cell only when the band was clipped at len1 (set_end_I)
-      if (i < hi || j + b1 - 1 > n1) {
-        const int ri = i < hi ? R : RE;
-        if (um - Q > ui) { iv = um - Q - ri; ti = FM; } else { iv = ui - ri; ti = FI; }
-      } else {
-        iv = NEG_INF;
-        ti = FM;
+#pragma unroll
+      for (int q = 0; q < GCH; ++q) {
+        const int i = i0 + q;
+        if (i > hi) break;
+        const int sc = sm(cb, ca_[q]);
+        int m, iv, dv;
+        uint8_t tm, ti, td;
+        // set_M (stdaln.c:271-287)
+        if (dm >= di) {
+          if (dm >= dd) { m = dm + sc; tm = FM; } else { m = dd + sc; tm = FD; }
+        } else {
+          if (di > dd) { m = di + sc; tm = FI; } else { m = dd + sc; tm = FD; }
+        }
+        // above cell (j-1, i)
+        const int um = um_[q], ui = ui_[q], ud = ud_[q];
+        // set_I from above; the last cell only when the band was clipped at len1 (set_end_I)
+        if (i < hi || j + b1 - 1 > n1) {
+          const int ri = i < hi ? R : RE;
+          if (um - Q > ui) { iv = um - Q - ri; ti = FM; } else { iv = ui - ri; ti = FI; }
+        } else {
+          iv = NEG_INF;
+          ti = FM;
+        }
+        // set_D from the left (set_end_D on the last row)
+        const int rd = j == n2 ? RE : R;
+        if (lm - Q > ld) { dv = lm - Q - rd; td = FM; } else { dv = ld - rd; td = FD; }
+        M(cur, i) = (uint32_t)m;
+        I(cur, i) = (uint32_t)iv;
+        D(cur, i) = (uint32_t)dv;
+        T(j, i) = (uint8_t)(tm | ti << 2 | td << 4);
+        lm = m; li = iv; ld = dv;
+        dm = um; di = ui; dd = ud;
       }
-      // set_D from the left (set_end_D on the last row)
-      const int rd = j == n2 ? RE : R;
-      if (lm - Q > ld) { dv = lm - Q - rd; td = FM; } else { dv = ld - rd; td = FD; }
-      M(cur, i) = (uint32_t)m;
-      I(cur, i) = (uint32_t)iv;
-      D(cur, i) = (uint32_t)dv;
-      T(j, i) = (uint8_t)(tm | ti << 2 | td << 4);
-      lm = m; li = iv; ld = dv;
-      dm = um; di = ui; dd = ud;
     }
     (void)li;
   }
