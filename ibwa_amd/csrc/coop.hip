@@ -828,8 +828,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     }
     if (lane == 0) {
       A.n_aln[ro] = na;
-      A.status[ro] = status;
-      if (A.iters) A.iters[ro] = n_iter;
+      A.status[r] = status;  // per launch read: the host collects the reads to re-run from it
+      if (A.iters) A.iters[r] = n_iter;
     }
     __syncthreads();
     lap(5);

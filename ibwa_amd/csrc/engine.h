@@ -135,6 +135,10 @@ struct CoopArgs {
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);
+// ids (in input order) and statuses of the reads whose status is non-zero (select.hip); tmp == nullptr
+// only sizes the rocPRIM scratch into *tmp_bytes
+hipError_t select_handed_on(const uint32_t *status, int64_t n, int64_t *ids, uint32_t *sel_status,
+                            unsigned long long *d_count, void *tmp, size_t *tmp_bytes, hipStream_t st);
 
 // Kernel arguments of the exact-match path: only what it reads (fewer SGPRs).
 struct ExactArgs {

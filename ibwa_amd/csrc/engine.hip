@@ -89,8 +89,10 @@ struct ibwa_ctx {
   std::vector<int32_t> h_naln;
   std::vector<uint32_t> h_status;
   std::vector<uint4> h_aln;      // n * aln_cap slots
-  std::vector<int64_t> retry_ids;
-  std::vector<std::vector<uint4>> retry_alns;
+  std::vector<int64_t> retry_ids;                   // every read a later pass resolved (input order)
+  std::vector<int64_t> patch_ids;                   // ... of which the wide / general passes' (input order)
+  std::vector<std::vector<uint4>> patch_alns;       // their hits (the coop pass writes into d_aln / d_naln)
+  DBuf d_selst, d_seltmp;                           // statuses of the handed-on reads, select scratch
   uint32_t aln_cap_used = 0;
   // sampled suffix arrays kept by ibwa_ctx_build_index
   DBuf sa_s[2];
@@ -120,7 +122,7 @@ struct ibwa_ctx {
   uint32_t gap_cap1 = 8192;          // per-lane static slots (stack + hit area)
   int gap_pages_per_block = 384;      // 128 KiB pages per 256-lane workgroup pool
   uint32_t gap_hit_slots = 256;      // hits a read may hold in the first pass
-  int64_t gap_reads_per_chunk = 1 << 22;
+  int64_t gap_reads_per_chunk = 1 << 24;  // at most; a batch is cut into equal chunks (each chunk's last reads run alone)
   // early hand-off to the coop pass: a read past 3000 iterations whose stack holds > 1000 entries
   // (swept at 10M reads: 2.28 -> 2.14 s per step; budget 6000-16000 with it: within noise)
   uint32_t gap_early_iters = 3000, gap_early_entries = 1000;
@@ -788,7 +790,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->h_status.clear();
     c->naln_on_host = false;  // results stay in HBM; ibwa_batch_fetch copies them
     c->retry_ids.clear();
-    c->retry_alns.clear();
+    c->patch_ids.clear();
+    c->patch_alns.clear();
     c->retry_pass.clear();
     c->stats.ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -803,7 +806,10 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   if (v2) {
     if (int rc = ensure_kmer(c)) return rc;
     c->stats.path = 2;
-    const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), c->gap_reads_per_chunk);
+    // equal chunks of at most gap_reads_per_chunk reads: every launch ends with a tail in which
+    // only its slowest reads still run, so fewer (and balanced) launches waste less
+    const int64_t n_chunks = (std::max<int64_t>(n, 1) + c->gap_reads_per_chunk - 1) / c->gap_reads_per_chunk;
+    const int64_t chunk = (std::max<int64_t>(n, 1) + n_chunks - 1) / n_chunks;
     // LDS: bucket heads + free slots + page table per lane, the page bitmap per workgroup
     const uint32_t LG = 13, P0 = c->gap_cap1;
     const int max_pages = (int)std::min<uint32_t>(7, (65536u - P0) >> LG);
@@ -940,38 +946,49 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   c->aln_cap_used = A.aln_cap;
 
   if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: first pass done\n", since());
-  // results + overflow detection
-  c->h_naln.resize(n);
-  c->h_status.resize(n);
+  // results stay in HBM; the reads handed on (non-zero status) are selected on the device
+  c->naln_on_host = false;
+  c->h_status.clear();
   c->stream_len = 0;
-  if (n) {
-    if (v2)
-      HIPCHK(hipMemcpyAsync(&c->stream_len, c->d_counter.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost,
-                            c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_status.data(), c->d_status.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    // a read whose hits did not fit advanced the fill counter but wrote nothing (gapped.hip:
-    // ST_ALN_OVERFLOW, re-run below): the records in the stream end at stream_total
-    if (v2) c->stream_len = std::min<unsigned long long>(c->stream_len, c->stream_total);
-  }
-  c->naln_on_host = true;
   c->retry_ids.clear();
-  c->retry_alns.clear();
+  c->patch_ids.clear();
+  c->patch_alns.clear();
   c->retry_pass.clear();
-  for (int64_t i = 0; i < n; ++i) {
-    if (c->h_status[i] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "read %lld: score outside the stack range", (long long)i);
-    if (c->h_status[i]) c->retry_ids.push_back(i);
-    c->stats.n_stack_overflow += (c->h_status[i] & ST_STACK_OVERFLOW) != 0;
-    c->stats.n_aln_overflow += (c->h_status[i] & ST_ALN_OVERFLOW) != 0;
-    c->stats.n_heavy += (c->h_status[i] & ST_HEAVY) != 0;
+  std::vector<uint32_t> rstat;
+  if (n) {
+    size_t tb = 0;
+    HIPCHK(select_handed_on(c->d_status.as<uint32_t>(), n, nullptr, nullptr, nullptr, nullptr, &tb, c->stream));
+    if (int rc = c->d_seltmp.ensure(tb + 16)) return rc;
+    if (int rc = c->d_ids.ensure(n * 8)) return rc;
+    if (int rc = c->d_selst.ensure(n * 4)) return rc;
+    if (int rc = c->d_counter.ensure(64)) return rc;
+    unsigned long long *d_cnt = c->d_counter.as<unsigned long long>() + 3;
+    HIPCHK(select_handed_on(c->d_status.as<uint32_t>(), n, c->d_ids.as<int64_t>(), c->d_selst.as<uint32_t>(), d_cnt,
+                            c->d_seltmp.p, &tb, c->stream));
+    unsigned long long cnt = 0;
+    HIPCHK(hipMemcpyAsync(&cnt, d_cnt, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->retry_ids.resize(cnt);
+    rstat.resize(cnt);
+    if (cnt) {
+      HIPCHK(hipMemcpyAsync(c->retry_ids.data(), c->d_ids.p, cnt * 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(rstat.data(), c->d_selst.p, cnt * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
   }
-  if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: status scanned, %zu to retry\n", since(), c->retry_ids.size());
+  for (size_t j = 0; j < rstat.size(); ++j) {
+    const uint32_t s_ = rstat[j];
+    if (s_ & ST_BAD_SCORE) return fail(IBWA_EINVAL, "read %lld: score outside the stack range", (long long)c->retry_ids[j]);
+    c->stats.n_stack_overflow += (s_ & ST_STACK_OVERFLOW) != 0;
+    c->stats.n_aln_overflow += (s_ & ST_ALN_OVERFLOW) != 0;
+    c->stats.n_heavy += (s_ & ST_HEAVY) != 0;
+  }
+  if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: handed-on reads selected, %zu to retry\n", since(), c->retry_ids.size());
   // retry pass: larger stacks / hit arrays for the few reads that overflowed
   std::vector<int64_t> todo = c->retry_ids;
   uint64_t cap = std::max<uint64_t>((uint64_t)c->stack_cap * 16, 65536);
   uint32_t acap = std::max<uint32_t>(c->aln_cap * 64, 4096);
-  std::vector<std::vector<uint4>> found(todo.size());
+  std::vector<std::pair<int64_t, std::vector<uint4>>> patch;  // (read, hits) of the wide / general passes
   std::vector<uint8_t> found_by(todo.size(), 0);
   std::vector<int64_t> where(todo.size());
   for (size_t j = 0; j < todo.size(); ++j) where[j] = (int64_t)j;
@@ -990,7 +1007,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const uint64_t pool_bytes = std::min<uint64_t>(
         (uint64_t)c->coop_pool_gb << 30, std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
     const uint32_t pool_pages = (uint32_t)(pool_bytes / (COOP_PG * 16ull));
-    const uint64_t r_total = (uint64_t)lanes * 64 + (1u << 20);
     if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
     if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
     if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
@@ -1001,12 +1017,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (int rc = c->c_recb.ensure((uint64_t)blocks * COOP_RREC * 16)) return rc;
     if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
     if (int rc = c->c_next.ensure(64)) return rc;
-    if (int rc = c->r_aln.ensure(r_total * 16)) return rc;
-    if (int rc = c->r_aoff.ensure(lanes * 8)) return rc;
-    if (int rc = c->r_naln.ensure(lanes * 4)) return rc;
     if (int rc = c->r_status.ensure(lanes * 4)) return rc;
     if (int rc = c->d_counter.ensure(64)) return rc;
-    HIPCHK(hipMemcpyAsync(c->d_ids.p, todo.data(), lanes * 8, hipMemcpyHostToDevice, c->stream));
+    // d_ids already holds todo (select_handed_on)
     AlnArgs B = A;
     B.ids = c->d_ids.as<int64_t>();
     B.n = lanes;
@@ -1022,7 +1035,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     K.len = A.len;
     K.ids = B.ids;
     K.n = lanes;
-    K.out_by_id = 0;
+    K.out_by_id = 1;  // n_aln / aln_off of the input read; status per launch read
     K.maxdiff_tab = A.maxdiff_tab;
     K.wbuf = B.wbuf;
     K.wstride = A.wstride;
@@ -1040,11 +1053,12 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     K.recb = c->c_recb.as<uint4>();
     K.hcap = hcap;
     K.max_iters = 1u << 24;  // runaway guard; a read past it goes to the sequential kernel
-    K.aln = c->r_aln.as<uint4>();
-    K.aln_total = r_total;
-    K.aln_next = c->d_counter.as<unsigned long long>() + 2;
-    K.aln_off = c->r_aoff.as<uint64_t>();
-    K.n_aln = c->r_naln.as<int32_t>();
+    // hits go on the first pass's stream (a read out of room there is flagged and re-run below)
+    K.aln = c->d_aln.as<uint4>();
+    K.aln_total = c->stream_total;
+    K.aln_next = c->d_counter.as<unsigned long long>() + 1;
+    K.aln_off = c->d_aoff.as<uint64_t>();
+    K.n_aln = c->d_naln.as<int32_t>();
     K.status = c->r_status.as<uint32_t>();
     if (c->verbose) {
       if (int rc = c->d_iters.ensure(lanes * 4)) return rc;
@@ -1056,7 +1070,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 128, c->stream));
       K.prof = c->d_prof.as<unsigned long long>();
     }
-    HIPCHK(hipMemsetAsync(K.aln_next, 0, 8, c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(launch_width(B, c->block, c->stream));
     HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
@@ -1079,17 +1092,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     float a = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
     ms_r += a;
-    std::vector<int32_t> rn(lanes);
     std::vector<uint32_t> rs(lanes);
-    std::vector<uint64_t> ro(lanes);
-    unsigned long long used = 0;
-    HIPCHK(hipMemcpyAsync(rn.data(), c->r_naln.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(ro.data(), c->r_aoff.p, lanes * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(&used, K.aln_next, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    std::vector<uint4> ra(std::min<unsigned long long>(used, r_total));
-    if (!ra.empty()) HIPCHK(hipMemcpy(ra.data(), c->r_aln.p, ra.size() * 16, hipMemcpyDeviceToHost));
     std::vector<int64_t> next, next_where;
     for (int64_t j = 0; j < lanes; ++j) {
       if (rs[j] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "score outside the stack range");
@@ -1098,8 +1103,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         next_where.push_back(where[j]);
         continue;
       }
-      const uint64_t first = rn[j] ? ro[j] : 0;
-      found[where[j]].assign(ra.begin() + first, ra.begin() + first + rn[j]);
       found_by[where[j]] = 1;
     }
     if (c->verbose) {
@@ -1238,7 +1241,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
           continue;
         }
         const uint64_t first = wide_round ? (rn[j] ? ro[j] : 0) : (uint64_t)j * acap;
-        found[slot].assign(ra.begin() + first, ra.begin() + first + rn[j]);
+        patch.emplace_back(todo[b0 + j], std::vector<uint4>(ra.begin() + first, ra.begin() + first + rn[j]));
         found_by[slot] = wide_round ? 2 : 3;
       }
     }
@@ -1260,8 +1263,23 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     todo.swap(next);
     where.swap(next_where);
   }
-  c->retry_alns.swap(found);
+  // the reads the wide / general passes resolved, in input order, for ibwa_batch_fetch to patch in
+  std::sort(patch.begin(), patch.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+  c->patch_ids.resize(patch.size());
+  c->patch_alns.resize(patch.size());
+  for (size_t j = 0; j < patch.size(); ++j) {
+    c->patch_ids[j] = patch[j].first;
+    c->patch_alns[j].swap(patch[j].second);
+  }
   c->retry_pass.swap(found_by);
+  // hit-stream records of the first and cooperative passes; a read whose hits did not fit advanced
+  // the fill counter but wrote nothing (ST_ALN_OVERFLOW, re-run above): the records end at stream_total
+  if (v2 && n) {
+    HIPCHK(hipMemcpyAsync(&c->stream_len, c->d_counter.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->stream_len = std::min<unsigned long long>(c->stream_len, c->stream_total);
+  }
   c->stats.ms_retry = ms_r;
   c->stats.n_retry = (int64_t)c->retry_ids.size();
   c->stats.ms_total =
@@ -1309,9 +1327,10 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
     if (n_slots) HIPCHK(hipMemcpyAsync(c->h_aln.data(), c->d_aln.p, n_slots * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }
-  // patch in retried reads
+  // patch in the reads the wide / general passes resolved (the first and cooperative passes wrote
+  // theirs into d_naln / d_aln)
   std::vector<int32_t> cnt(c->h_naln.begin(), c->h_naln.end());
-  for (size_t j = 0; j < c->retry_ids.size(); ++j) cnt[c->retry_ids[j]] = (int32_t)c->retry_alns[j].size();
+  for (size_t j = 0; j < c->patch_ids.size(); ++j) cnt[c->patch_ids[j]] = (int32_t)c->patch_alns[j].size();
   int64_t tot = 0;
   for (int64_t i = 0; i < n; ++i) tot += cnt[i];
   ibwa_aln1_t *o = (ibwa_aln1_t *)malloc(std::max<int64_t>(tot, 1) * sizeof(ibwa_aln1_t));
@@ -1320,8 +1339,8 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
   int64_t p = 0;
   for (int64_t i = 0; i < n; ++i) {
     const uint4 *src;
-    if (rj < c->retry_ids.size() && c->retry_ids[rj] == i) {
-      src = c->retry_alns[rj].data();
+    if (rj < c->patch_ids.size() && c->patch_ids[rj] == i) {
+      src = c->patch_alns[rj].data();
       ++rj;
     } else {
       src = c->h_aln.data() + (c->stream_out ? (cnt[i] ? c->h_aoff[i] : 0) : i * cap);

@@ -1,0 +1,44 @@
+// select.hip -- the reads a search pass handed on, selected on the device.
+//
+// After the first gapped pass every read has a status word (0: done); the reads with a
+// non-zero status go on to the cooperative / wide / general passes (bwa_cal_sa_reg_gap's results
+// are per read, so which pass resolves a read changes nothing in its output).  Their ids, in
+// input order, and their statuses are compacted here (rocPRIM select), so the host copies a few
+// MB instead of two words per read of the batch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <rocprim/rocprim.hpp>
+
+#include "engine.h"
+
+namespace ibwa {
+
+namespace {
+
+struct NonZero {
+  __host__ __device__ bool operator()(uint32_t s) const { return s != 0u; }
+};
+
+__global__ void k_gather_status(const uint32_t *status, const int64_t *ids, const unsigned long long *count,
+                                uint32_t *out) {
+  const unsigned long long m = *count;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = status[ids[i]];
+}
+
+}  // namespace
+
+hipError_t select_handed_on(const uint32_t *status, int64_t n, int64_t *ids, uint32_t *sel_status,
+                            unsigned long long *d_count, void *tmp, size_t *tmp_bytes, hipStream_t st) {
+  auto in = rocprim::make_counting_iterator<int64_t>(0);
+  auto flags = rocprim::make_transform_iterator(status, NonZero());
+  if (!tmp) return rocprim::select(nullptr, *tmp_bytes, in, flags, ids, d_count, (size_t)n, st);
+  hipError_t e = rocprim::select(tmp, *tmp_bytes, in, flags, ids, d_count, (size_t)n, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gather_status, dim3(1024), dim3(256), 0, st, status, ids, d_count, sel_status);
+  return hipGetLastError();
+}
+
+}  // namespace ibwa
