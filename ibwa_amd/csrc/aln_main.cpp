@@ -32,6 +32,17 @@ using ibwa_cli::BamReader;
 using ibwa_cli::SeqReader;
 
 const int kBatch = 0x40000;  // bwtaln.c:193
+// A GPU run takes up to kGroup consecutive batches whose batch-level options (bwtaln.c:86-93: the
+// max_diff of the batch's longest read, which clamps max_gapo and sizes the stack) are the same,
+// so its results are those of running them one by one; a 262 k-read run alone would pay the
+// launch tails and host round trips of the passes for every batch.  IBWA_ALN_GROUP /
+// IBWA_ALN_SUBBATCH override both (tests: grouped == one batch at a time).
+int env_int(const char *k, int dflt) {
+  const char *v = getenv(k);
+  return v && atoi(v) > 0 ? atoi(v) : dflt;
+}
+const int kGroup = env_int("IBWA_ALN_GROUP", 16);
+const int kSub = env_int("IBWA_ALN_SUBBATCH", kBatch);
 const int kMinRdLen = 35;    // BWA_MIN_RDLEN, bwtaln.h:23
 
 unsigned char nt4[256];
@@ -66,7 +77,7 @@ int read_batch(Reader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, l
     return -1;
   }
   int l = 0;
-  while ((int)b.len.size() < kBatch && (l = rd.read()) >= 0) {
+  while ((int)b.len.size() < kSub && (l = rd.read()) >= 0) {
     std::string &s = rd.seq, &q = rd.qual;
     if (is_64 && !q.empty())
       for (auto &ch : q) ch = (char)(ch - 31);
@@ -87,16 +98,62 @@ int read_batch(Reader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, l
       len = max_l + 1;
       *n_trimmed += full - len;
     }
-    b.off.push_back(b.seq.size());
+    const size_t o = b.seq.size();
+    b.off.push_back(o);
     b.len.push_back((uint32_t)len);
     if (len > b.max_len) b.max_len = len;
-    for (int j = len - 1; j >= 0; --j) b.seq.push_back(nt4[(unsigned char)s[j]]);  // seq := reverse(read)
+    b.seq.resize(o + len);
+    uint8_t *d = b.seq.data() + o;
+    for (int j = 0; j < len; ++j) d[j] = nt4[(unsigned char)s[len - 1 - j]];  // seq := reverse(read)
   }
   if (l == -2) {
     fprintf(stderr, "[ibwa-amd aln] truncated or corrupt input record after %zu reads of this batch\n", b.len.size());
     return -1;
   }
   return b.len.empty() ? 0 : 1;
+}
+
+// The batch-level max_diff of a batch whose longest read has max_len (bwtaln.c:86-88).
+int batch_key(const ibwa_gap_opt_t &opt, int max_len) {
+  return opt.fnr > 0.0f ? ibwa_cal_maxdiff(max_len, 0.02, opt.fnr) : opt.max_diff;
+}
+
+// Up to kGroup batches with the same batch-level options into g; a batch whose options differ is
+// left in `carry` for the next group.  Returns the batches read (0 at the end), -1 on bad input.
+template <class Reader>
+int read_group(Reader &rd, const ibwa_gap_opt_t &opt, Batch &g, Batch &sub, Batch &carry, bool &has_carry,
+               long *n_trimmed, long *n_tot) {
+  g.seq.clear(); g.off.clear(); g.len.clear(); g.max_len = 0;
+  int nb = 0, key = 0;
+  auto append = [&](const Batch &x) {
+    const uint64_t base = g.seq.size();
+    g.seq.insert(g.seq.end(), x.seq.begin(), x.seq.end());
+    for (uint64_t o : x.off) g.off.push_back(base + o);
+    g.len.insert(g.len.end(), x.len.begin(), x.len.end());
+    g.max_len = std::max(g.max_len, x.max_len);
+  };
+  if (has_carry) {
+    std::swap(g, carry);
+    has_carry = false;
+    key = batch_key(opt, g.max_len);
+    nb = 1;
+  }
+  while (nb < kGroup) {
+    const int r = read_batch(rd, opt.mode, opt.trim_qual, sub, n_trimmed, n_tot);
+    if (r < 0) return -1;
+    if (r == 0) break;
+    const int k = batch_key(opt, sub.max_len);
+    if (nb && k != key) {
+      std::swap(carry, sub);
+      has_carry = true;
+      break;
+    }
+    key = k;
+    if (nb == 0) std::swap(g, sub);
+    else append(sub);
+    ++nb;
+  }
+  return nb;
 }
 
 void usage(const ibwa_gap_opt_t *o) {
@@ -216,10 +273,11 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
   fwrite(&opt, sizeof opt, 1, out);  // bwtaln.c:192
   ph.mark("load index");
 
-  Batch cur, nxt;
+  Batch cur, nxt, sub, carry;
+  bool has_carry = false;
   long n_trim = 0, n_tot = 0;
   int64_t tot_seqs = 0;
-  int have = read_batch(rd, opt.mode, opt.trim_qual, cur, &n_trim, &n_tot);
+  int have = read_group(rd, opt, cur, sub, carry, has_carry, &n_trim, &n_tot);
   ph.mark("read");
   while (have > 0) {
     auto t0 = std::chrono::steady_clock::now();
@@ -249,7 +307,7 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
       });
     }
     // overlap: parse the next batch while the GPUs work
-    int more = read_batch(rd, opt.mode, opt.trim_qual, nxt, &n_trim, &n_tot);
+    int more = read_group(rd, opt, nxt, sub, carry, has_carry, &n_trim, &n_tot);
     for (auto &t : th) t.join();
     for (int g = 0; g < n_gpus; ++g)
       if (g_rc[g]) return die("aln");

@@ -45,3 +45,32 @@ def test_cli_rejects_non_bam(golden_dir, tmp_path):
     r = subprocess.run([CLI, "aln", "-b", os.path.join(golden_dir, "g1m"), os.path.join(golden_dir, "reads_r36.fq")],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "BAM" in r.stderr
+
+
+def run_cli_env(argv, golden_dir, reads, tmp_path, env, name):
+    out = tmp_path / name
+    r = subprocess.run([CLI, "aln"] + argv + ["-f", str(out), os.path.join(golden_dir, "g1m"),
+                                              os.path.join(golden_dir, reads)],
+                       capture_output=True, text=True, timeout=120, env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-2000:]
+    return out.read_bytes()
+
+
+@pytest.mark.parametrize("key", ["r100.default", "r36.n0", "r150.default"])
+def test_cli_grouped_batches_fixed_length(golden_dir, sai_manifest, key, tmp_path):
+    """Batches of one read length share their batch-level options (bwtaln.c:86-93), so a GPU run
+    over several of them (aln_main.cpp read_group) gives the reference's single-batch output."""
+    m = sai_manifest[key]
+    got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path,
+                      {"IBWA_ALN_SUBBATCH": "128", "IBWA_ALN_GROUP": "5"}, "g.sai")
+    assert oracle.sai_body_equal(got, open(os.path.join(golden_dir, key + ".sai"), "rb").read())
+
+
+@pytest.mark.parametrize("argv", [[], ["-q", "15"], ["-n", "0.01"]])
+def test_cli_grouped_batches_equal_one_at_a_time(golden_dir, argv, tmp_path):
+    """Mixed read lengths: small batches whose longest reads give different batch-level max_diff
+    are split between groups; grouped runs == the same batches aligned one at a time."""
+    reads = "reads_mixed.fq"
+    one = run_cli_env(argv, golden_dir, reads, tmp_path, {"IBWA_ALN_SUBBATCH": "16", "IBWA_ALN_GROUP": "1"}, "a.sai")
+    grp = run_cli_env(argv, golden_dir, reads, tmp_path, {"IBWA_ALN_SUBBATCH": "16", "IBWA_ALN_GROUP": "4"}, "b.sai")
+    assert one[64:] == grp[64:]
