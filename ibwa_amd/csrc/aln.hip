@@ -146,15 +146,45 @@ __device__ __forceinline__ uint32_t strand_base(uint32_t c, int a, bool comp) {
   return (a == 1 && comp && c < 4) ? 3u - c : c;
 }
 
+// The compact record's byte stream (engine.h AlnArgs::cw) as width_pair produces it: byte `off` of
+// the stream goes to bits 8 * (off & 3) of word off >> 2; the accumulator carries a partial word from
+// the full-length chains into the seed chains.
+struct RecOut {
+  uint32_t *words;  // the record's width bytes (word 1 + cw_rw of the record)
+  uint32_t off, acc;
+  __device__ __forceinline__ void put(uint32_t byte) {
+    acc |= byte << (8 * (off & 3));
+    if ((off & 3) == 3) {
+      words[off >> 2] = acc;
+      acc = 0;
+    }
+    ++off;
+  }
+  __device__ __forceinline__ void flush() {
+    if (off & 3) words[off >> 2] = acc;
+    acc = 0;
+  }
+};
+
+// one position's byte: per strand the bid clamped to `clamp` and "width equals the previous
+// position's", at bit offsets 0 and nb (full: 3 + 1 bits per strand, seed: 2 + 1)
+__device__ __forceinline__ uint32_t rec_byte(uint2 a, uint2 b, uint32_t pa, uint32_t pb, bool first, uint32_t clamp,
+                                             int nb) {
+  const uint32_t ea = !first && a.x == pa, eb = !first && b.x == pb;
+  return (a.y < clamp ? a.y : clamp) | ea << (nb - 1) | ((b.y < clamp ? b.y : clamp) | eb << (nb - 1)) << nb;
+}
+
 // two bwt_cal_width chains in lockstep (bwtaln.c:54-78): str on ixa -> wa, strand-1 str on
 // ixb -> wb.  The entries of 16 steps are kept in
 // registers and stored back to back (a lane's 128 B of widths leave in consecutive instructions,
 // so the L2 merges them into whole lines instead of 16 partial writes far apart).
 __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView ixb, int L, const uint8_t *s, bool comp,
-                                           uint2 *wa, uint2 *wb, uint32_t *lw = nullptr) {
+                                           uint2 *wa, uint2 *wb, uint32_t *lw = nullptr, RecOut *rec = nullptr,
+                                           uint32_t clamp = 0, int nb = 4, uint32_t *rd = nullptr) {
   uint32_t ka = 0, la = ixa.seq_len, kb = 0, lb = ixb.seq_len;
   uint32_t bida = 0, bidb = 0;
   uint32_t lwa = 0, lwb = 0;  // sum of log2(width) over the positions (diagnostics)
+  uint32_t pa = 0, pb = 0;    // previous positions' widths (record)
   for (int base = 0; base < L; base += 16) {
     uint2 ba[16], bb[16];
 #pragma unroll
@@ -192,9 +222,22 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
 #pragma unroll
     for (int t = 0; t < 16; ++t)
       if (base + t < L) wb[base + t] = bb[t];
+    if (rec) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+        if (base + t < L) {
+          rec->put(rec_byte(ba[t], bb[t], pa, pb, base + t == 0, clamp, nb));
+          pa = ba[t].x;
+          pb = bb[t].x;
+          x |= ((uint32_t)s[base + t] & 3u) << (2 * t);
+        }
+      if (rd) rd[base >> 4] = x;
+    }
   }
   wa[L] = make_uint2(0u, bida + 1);
   wb[L] = make_uint2(0u, bidb + 1);
+  if (rec) rec->put(rec_byte(wa[L], wb[L], pa, pb, L == 0, clamp, nb));
   if (lw) {
     lw[0] = lwa;
     lw[1] = lwb;
@@ -228,6 +271,22 @@ __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
     A.feat[lane * 4 + 1] = (uint16_t)(g[0] + g[1]);
     A.feat[lane * 4 + 2] = (uint16_t)(f[2] < f[3] ? f[2] : f[3]);
     A.feat[lane * 4 + 3] = (uint16_t)(g[2] < g[3] ? g[2] : g[3]);
+    return;
+  }
+  if (A.cw) {
+    // the compact record (engine.h AlnArgs::cw), built from the chains' registers
+    uint32_t *rec = A.cw + (uint64_t)lane * A.cw_words;
+    uint32_t nN = 0;
+    for (int j = 0; j < L; ++j) nN += s[j] > 3;
+    const int md = A.o.fnr_pos ? (int)A.maxdiff_tab[L] : A.o.max_diff;
+    rec[0] = (uint32_t)L | (nN < 255u ? nN : 255u) << 16 | (uint32_t)md << 24;
+    RecOut ro{rec + 1 + A.cw_rw, 0u, 0u};
+    width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, &ro, (uint32_t)md + 1u, 4, rec + 1);
+    while (ro.off < A.wlen1) ro.put(0u);  // positions past this read's length
+    if (L > A.o.seed_len)
+      width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1, nullptr, &ro,
+                 (uint32_t)A.o.max_seed_diff + 1u, 3);
+    ro.flush();
     return;
   }
   width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1);

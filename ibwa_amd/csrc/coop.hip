@@ -182,6 +182,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
   }
   auto now = []() __attribute__((always_inline)) -> uint64_t { return __builtin_amdgcn_s_memtime(); };
   uint64_t t_mark = prof ? now() : 0;
+  if (prof && A.wave_t && lane == 0) A.wave_t[2 * wave] = t_mark;
   auto lap = [&](int ph) __attribute__((always_inline)) {
     if (prof) {
       const uint64_t t = now();
@@ -836,6 +837,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
   }
   if (prof && lane == 0)
     for (int q = 0; q < 12; ++q) atomicAdd(A.prof + q, (unsigned long long)pc[q]);
+  if (prof && A.wave_t && lane == 0) A.wave_t[2 * wave + 1] = now();
 }
 
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {

@@ -44,6 +44,13 @@ struct AlnArgs {
   uint32_t *status;          // per lane ST_* flags
   uint16_t *nN;              // per lane N count (k_width output, may be null)
   uint16_t *feat;            // per lane 4 search-cost features (k_width output, diagnostics, may be null)
+  // compact per-read record for the first gapped pass's LDS (k_width output, may be null), cw_words
+  // u32 per lane: [0] len | min(nN, 255) << 16 | max_diff << 24; [1, 1 + cw_rw) the read, 16 bases
+  // per word; then bytes: per position p <= len the bids of both strands clamped to max_diff + 1
+  // (3 bits) and "width equals the previous position's" (1 bit), nibble per strand; then per seed
+  // position the same with the bid clamped to max_seed_diff + 1 (2 bits + 1 bit per strand)
+  uint32_t *cw;
+  uint32_t cw_words, cw_rw;
   AlnOpt o;
 };
 
@@ -82,10 +89,17 @@ struct GapArgs {
   uint32_t early_entries;    //   stack holds more than early_entries entries -> ST_HEAVY
   int lanes_per_wave;        // reads a wave runs at once (64; 1 for heavy reads)
   int free_depth;            // LDS free-slot stack per read (wide kernel)
+  // LDS-resident widths (first pass, when they fit): the k_width records (AlnArgs::cw) copied into
+  // LDS at a read's claim; 16 bucket heads in a ring; the page table of a lane in global memory
+  const uint32_t *cw;        // nullptr: widths from wbuf, heads per bucket, page table in LDS
+  uint32_t cw_words, cw_rw;
+  uint16_t *ptab_g;          // [lane][GAP_MAX_PAGES]
   AlnOpt o;
 };
+constexpr int GAP_RING = 16;      // bucket heads of the LDS-width variant: live scores span <= 16
+constexpr int GAP_MAX_PAGES = 8;  // page-table entries per lane (global table)
 size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int pages_per_block, int lanes_per_wave,
-                        int free_depth);
+                        int free_depth, int cw_words = 0);
 // wide: 24-bit slot links (reads < 4096 bp), for the large-capacity retry pass
 hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int blocks, int block, bool wide,
                          hipStream_t st);
@@ -132,6 +146,7 @@ struct CoopArgs {
   uint32_t *status;
   uint32_t *iters;
   unsigned long long *prof;  // diagnostics: per-phase wave cycles (IBWA_PROF_PHASES), may be null
+  unsigned long long *wave_t;  // diagnostics: per wave {start, end} shader clock (with prof)
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);

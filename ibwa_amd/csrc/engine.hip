@@ -130,6 +130,8 @@ struct ibwa_ctx {
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
   int gap_coop = 1;
+  int gap_lw = 1;                    // first pass with its widths in LDS (gapped.hip LW) when they fit
+  DBuf d_cw, d_ptabg;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
   int coop_pool_gb = 16;             // bucket page pool
   DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb;
@@ -346,6 +348,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
   else if (k == "gap_early_iters" && value >= 0) c->gap_early_iters = (uint32_t)value;
   else if (k == "gap_early_entries" && value >= 0) c->gap_early_entries = (uint32_t)value;
+  else if (k == "gap_lw" && (value == 0 || value == 1)) c->gap_lw = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
   else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
@@ -814,7 +817,19 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const uint32_t LG = 13, P0 = c->gap_cap1;
     const int max_pages = (int)std::min<uint32_t>(7, (65536u - P0) >> LG);
     auto ppb_of = [&](int blk) { return std::max(1, c->gap_pages_per_block * blk / 256); };
-    auto lds_of = [&](int blk) { return gapped_lds_bytes(o.n_stacks, blk, false, max_pages, ppb_of(blk), 64, 0); };
+    // LDS widths (gapped.hip LW): bids clamped to max_diff + 1 in 3 bits and to max_seed_diff + 1
+    // in 2, a ring of 16 bucket heads (the largest penalty <= 15), and 3 workgroups per CU still fit
+    const int maxpen = std::max(o.s_mm, std::max(o.s_gapo, o.s_gape));
+    const uint32_t cw_rw = (uint32_t)(max_len + 15) / 16;
+    const uint32_t cw_sb = max_len > o.seed_len ? (uint32_t)o.seed_len + 1u : 0u;
+    const uint32_t cw_words = 1u + cw_rw + ((uint32_t)max_len + 1u + cw_sb + 3u) / 4u;
+    const bool lw = c->gap_lw && !c->diag && batch_md <= 6 && o.max_seed_diff >= 0 && o.max_seed_diff <= 2 && maxpen <= 15 &&
+                    max_pages <= GAP_MAX_PAGES &&
+                    gapped_lds_bytes(o.n_stacks, 256, false, max_pages, ppb_of(256), 64, 0, (int)cw_words) * 3 <=
+                        160 * 1024;
+    auto lds_of = [&](int blk) {
+      return gapped_lds_bytes(o.n_stacks, blk, false, max_pages, ppb_of(blk), 64, 0, lw ? (int)cw_words : 0);
+    };
     const int block = lds_of(256) <= 65536 ? 256 : lds_of(128) <= 65536 ? 128 : 64;
     const int ppb = ppb_of(block);
     const size_t lds = lds_of(block);
@@ -827,6 +842,10 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const uint64_t aln_total = std::max<uint64_t>((uint64_t)n * c->gap_stream_per_read, c->gap_stream_min);
     if (int rc = c->d_wbuf.ensure(chunk * A.wstride * 8)) return rc;
     if (int rc = c->d_nN.ensure(chunk * 2 + 2)) return rc;
+    if (lw) {
+      if (int rc = c->d_cw.ensure(chunk * (uint64_t)cw_words * 4)) return rc;
+      if (int rc = c->d_ptabg.ensure(lanes * GAP_MAX_PAGES * 2)) return rc;
+    }
     if (int rc = c->d_ent.ensure(lanes * P0 * 16)) return rc;
     if (int rc = c->d_pool.ensure((uint64_t)blocks * ppb * (16ull << LG))) return rc;
     if (int rc = c->d_aln.ensure(aln_total * 16)) return rc;
@@ -844,6 +863,15 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       B.wbuf = c->d_wbuf.as<uint2>();
       B.nN = c->d_nN.as<uint16_t>();
       GapArgs G = gap_args(c, A, o, b0, cnt);
+      if (lw) {
+        B.cw = c->d_cw.as<uint32_t>();
+        B.cw_words = cw_words;
+        B.cw_rw = cw_rw;
+        G.cw = B.cw;
+        G.cw_words = cw_words;
+        G.cw_rw = cw_rw;
+        G.ptab_g = c->d_ptabg.as<uint16_t>();
+      }
       G.ent = c->d_ent.as<uint4>();
       G.cap1 = P0;
       G.hit_slots = std::min<uint32_t>(c->gap_hit_slots, P0 / 2);
@@ -869,8 +897,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         B.feat = c->d_feat.as<uint16_t>() + b0 * 4;
       }
       if (c->prof_phases) {
-        if (int rc = c->d_prof.ensure(128)) return rc;
-        HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 128, c->stream));
+        if (int rc = c->d_prof.ensure(256)) return rc;
+        HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 256, c->stream));
         G.prof = c->d_prof.as<unsigned long long>();
       }
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
@@ -898,7 +926,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                 it[(size_t)(cnt * 0.99)], it[(size_t)(cnt * 0.9999)], mx, b, sum / (b * 1e-3));
       }
       if (c->prof_phases) {
-        unsigned long long pf[11];
+        unsigned long long pf[17];
         HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
         const char *nm[4] = {"claim", "pop", "wait", "rest"};
         double tot = (double)(pf[0] + pf[1] + pf[2] + pf[3]);
@@ -908,6 +936,10 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         fprintf(stderr, "; per wave-iteration: exact %.3f push trips %.3f hits %.3f ends %.3f expansions %.3f "
                 "claims %.3f (%llu wave-iterations)\n", pf[4] / wi, pf[5] / wi, pf[6] / wi, pf[7] / wi, pf[8] / wi,
                 pf[10] / wi, pf[9]);
+        const double li = pf[16] ? (double)pf[16] : 1.0;
+        fprintf(stderr, "[ibwa_amd] k_gapped loads per live lane-iteration: block %.3f second block %.3f widths %.3f "
+                "seed widths %.3f candidate %.3f (%.3g live lane-iterations)\n", pf[11] / li, pf[12] / li, pf[13] / li,
+                pf[14] / li, pf[15] / li, (double)pf[16]);
       }
     }
   }
@@ -1066,9 +1098,10 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     }
     K.o = o;
     if (c->prof_phases) {
-      if (int rc = c->d_prof.ensure(128)) return rc;
-      HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 128, c->stream));
+      if (int rc = c->d_prof.ensure(128 + (uint64_t)blocks * 16)) return rc;
+      HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 128 + (uint64_t)blocks * 16, c->stream));
       K.prof = c->d_prof.as<unsigned long long>();
+      K.wave_t = K.prof + 16;
     }
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(launch_width(B, c->block, c->stream));
@@ -1088,6 +1121,17 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
               "%.1f running (%.1f fetching an entry, %.1f in an exact tail)\n", pf[6], pf[6] ? tot / pf[6] : 0.0, pf[7],
               pf[8], pf[6] ? (double)pf[9] / pf[6] : 0.0, pf[6] ? (double)pf[10] / pf[6] : 0.0,
               pf[6] ? (double)pf[11] / pf[6] : 0.0);
+      // wave end times (shader clock) relative to the first wave start: the pass's tail
+      std::vector<unsigned long long> wt((size_t)blocks * 2);
+      HIPCHK(hipMemcpy(wt.data(), K.wave_t, wt.size() * 8, hipMemcpyDeviceToHost));
+      // each wave's own duration (the clock is per XCD; the persistent grid starts together)
+      std::vector<double> ends;
+      for (int w = 0; w < blocks; ++w) ends.push_back((double)(wt[2 * w + 1] - wt[2 * w]));
+      std::sort(ends.begin(), ends.end());
+      const double last = ends.back() > 0 ? ends.back() : 1.0;
+      fprintf(stderr, "[ibwa_amd] k_coop wave durations (fraction of the longest): p10 %.3f p50 %.3f p90 %.3f p99 %.3f\n",
+              ends[ends.size() / 10] / last, ends[ends.size() / 2] / last, ends[ends.size() * 9 / 10] / last,
+              ends[ends.size() * 99 / 100] / last);
     }
     float a = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));

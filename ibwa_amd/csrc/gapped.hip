@@ -52,6 +52,7 @@ constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_N
 constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
 // per-lane LDS stack of popped slots awaiting reuse (the retry pass's heavy reads get more)
 constexpr int NARROW_FREE_DEPTH = 8;
+constexpr int LW_FREE_DEPTH = 4;  // LDS-width variant: 8 B per lane
 constexpr int MAX_BUCKETS = 128;  // non-empty-bucket bitmask: four 32-bit registers
 // first pass: a read of <= 16 * RDW bases without N is kept 2-bit packed in LDS, so the read
 // symbol of an iteration is an LDS access instead of one more HBM line request
@@ -89,6 +90,14 @@ __device__ __forceinline__ int bm_next(const BMask &m, int from) {
   const uint32_t x3 = w > 3 ? 0u : (w == 3 ? m.m3 & lo : m.m3);
   return x0 ? __builtin_ctz(x0) : x1 ? 32 + __builtin_ctz(x1) : x2 ? 64 + __builtin_ctz(x2)
                                  : x3 ? 96 + __builtin_ctz(x3) : MAX_BUCKETS;
+}
+
+// LW: non-empty buckets of the head ring, bit (b & 15) of m0; the lowest non-empty bucket >= from
+// (every live bucket lies in [from - 1, from + 14] when this is asked)
+__device__ __forceinline__ int ring_next(uint32_t m, int from) {
+  const uint32_t r = (uint32_t)from & (GAP_RING - 1);
+  const uint32_t x = ((m >> r) | (m << (GAP_RING - r))) & ((1u << GAP_RING) - 1u);
+  return x ? from + __builtin_ctz(x) : (1 << 30);
 }
 
 // The 64-row bit-plane block (occ64.hip): v[c] = {C[c], 0, P_lo[c], P_hi[c]}.  Four named
@@ -155,8 +164,11 @@ template <bool WIDE> struct Ent {
 //   narrow only: reads[RDW][LN] (u32, 16 bases each)
 // with LN = the block's lanes that run reads (block / 64 * lanes_per_wave)
 size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int pages_per_block, int lanes_per_wave,
-                        int free_depth) {
+                        int free_depth, int cw_words) {
   const size_t ln = (size_t)block / 64 * lanes_per_wave;
+  if (cw_words > 0 && !wide)  // LDS widths: ring heads, a 4-slot free stack, bitmap, the records
+    return (size_t)(GAP_RING + LW_FREE_DEPTH) * ln * 2 + (size_t)((pages_per_block + 31) / 32) * 4 +
+           (size_t)cw_words * ln * 4;
   const int fd = wide ? free_depth : NARROW_FREE_DEPTH;
   size_t b = (size_t)(n_stacks + fd) * ln * (wide ? 4 : 2) + (size_t)max_pages * ln * 2;
   b = (b + 3) & ~(size_t)3;
@@ -167,8 +179,9 @@ size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int p
 // the same kernel): 0 claim, 1 pop, 2 wait for the loads, 3 rest; then wave-level event
 // counts (the wave executes a block once for all its lanes in it): 4 exact steps, 5 push-loop
 // trips, 6 hit blocks, 7 read ends, 8 expansions, 9 wave iterations, 10 read claims.
-template <bool WIDE, bool PROF>
+template <bool WIDE, bool PROF, bool LW>
 __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *counter) {
+  static_assert(!(WIDE && LW), "the LDS-width variant is a first-pass kernel");
   using E = Ent<WIDE>;
   using H = typename E::Head;
   constexpr uint32_t NILH = E::NIL;
@@ -183,18 +196,32 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   const int ltid = (tid >> 6) * A.lanes_per_wave + (lane < A.lanes_per_wave ? lane : 0);
   const AlnOpt o = A.o;
   H *const lds_heads = reinterpret_cast<H *>(lds_raw);
-  // free stack of popped slots: narrow, 8 u16 per lane side by side (one 16 B read per expansion);
-  // wide (retry pass), lane-minor rows
-  H *const free_slots = lds_heads + o.n_stacks * LNB;
-  auto fsi = [&](uint32_t j) __attribute__((always_inline)) -> uint32_t {
-    return WIDE ? (j << nbl) + ltid : (uint32_t)ltid * NARROW_FREE_DEPTH + j;
+  // bucket heads: one per bucket, or (LW) a ring of GAP_RING -- every live entry scores within
+  // [last popped score, last popped score + max penalty], so score & 15 names its bucket
+  auto hidx = [&](int sc) __attribute__((always_inline)) -> uint32_t {
+    return LW ? (((uint32_t)sc & (GAP_RING - 1)) << nbl) + ltid : ((uint32_t)sc << nbl) + ltid;
   };
-  const uint32_t FREE_DEPTH = WIDE ? (uint32_t)A.free_depth : (uint32_t)NARROW_FREE_DEPTH;
-  uint16_t *const ptab = reinterpret_cast<uint16_t *>(free_slots + FREE_DEPTH * LNB);  // ptab[((q) << nbl) + ltid]
+  // free stack of popped slots: narrow, 8 (LW: 4) u16 per lane side by side (one LDS read per
+  // expansion); wide (retry pass), lane-minor rows
+  constexpr uint32_t NFREE = LW ? LW_FREE_DEPTH : NARROW_FREE_DEPTH;
+  H *const free_slots = lds_heads + (LW ? GAP_RING : o.n_stacks) * LNB;
+  auto fsi = [&](uint32_t j) __attribute__((always_inline)) -> uint32_t {
+    return WIDE ? (j << nbl) + ltid : (uint32_t)ltid * NFREE + j;
+  };
+  const uint32_t FREE_DEPTH = WIDE ? (uint32_t)A.free_depth : NFREE;
+  // page table of a lane: LDS rows ptab[((q) << nbl) + ltid], or (LW) global
+  uint16_t *const ptab = reinterpret_cast<uint16_t *>(free_slots + FREE_DEPTH * LNB);
   uint32_t *const bitmap =
-      reinterpret_cast<uint32_t *>(ptab + ((A.max_pages * LNB + 1) & ~1));  // 4-byte aligned, still LDS
+      reinterpret_cast<uint32_t *>(ptab + (LW ? 0 : ((A.max_pages * LNB + 1) & ~1)));  // 4-byte aligned, still LDS
   const int bm_words = (A.pages_per_block + 31) / 32;
   uint32_t *const rdl = bitmap + bm_words;  // narrow: the lane's read, rdl[(w << nbl) + ltid]
+  // LW: the lane's k_width record (engine.h AlnArgs::cw), word w at cwl[(w << nbl) + ltid]
+  uint32_t *const cwl = bitmap + bm_words;
+  const uint32_t CWR = A.cw_rw;  // read words; the width bytes start at word 1 + CWR
+  auto cw_byte = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t w = 1u + CWR + (b >> 2);
+    return (cwl[(w << nbl) + ltid] >> (8 * (b & 3))) & 0xFFu;
+  };
   for (int w = tid; w < bm_words; w += NB) {
     const int lo = w * 32, hi = lo + 32 < A.pages_per_block ? lo + 32 : A.pages_per_block;
     bitmap[w] = hi - lo >= 32 ? 0u : ~((1u << (hi - lo)) - 1u);  // bits past the pool stay taken
@@ -215,7 +242,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   int64_t cur = 0, cend = 0;
   bool more = true;
   // ---- lane state
-  int st = 0;  // 0 idle, 1 search (C valid or empty), 2 exact sub-search, 3 ended (retire)
+  int st = 0;  // 0 idle, 1 search (C valid or empty), 2 exact sub-search, 3 ended (retire), 4 (LW) record loading
   uint32_t end_stat = 0;
   int64_t r = 0, ro = 0;  // read of this launch, its output index
   int len = 0, opt_max_diff = 0, max_diff = 0, best_score = 0, n_aln = 0;
@@ -257,14 +284,20 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     asm volatile("" : "+s"(p));
     return p;
   };
+  auto ptab_at = [&](uint32_t q) __attribute__((always_inline)) -> uint16_t & {
+    if (LW) return args()->ptab_g[gtid * GAP_MAX_PAGES + q];
+    return ptab[((q) << nbl) + ltid];
+  };
   auto slot_ptr = [&](uint32_t slot) __attribute__((always_inline)) -> uint4 * {
     if (slot < P0) return ent1 + slot;
     const uint32_t q = (slot - P0) >> LG;
-    return pool + ((uint64_t)ptab[((q) << nbl) + ltid] << LG) + ((slot - P0) & ((1u << LG) - 1u));
+    return pool + ((uint64_t)ptab_at(q) << LG) + ((slot - P0) & ((1u << LG) - 1u));
   };
   // the read is done: hits to the output stream, pages back to the pool
   uint64_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0, pf7 = 0, t_rest = 0;
   uint64_t pf8 = 0, pf9 = 0, pf10 = 0;
+  // lane counts (PROF): block loads, second-block loads, width loads, seed-width loads, candidate loads, live lanes
+  uint64_t pl11 = 0, pl12 = 0, pl13 = 0, pl14 = 0, pl15 = 0, pl16 = 0;
   auto pnow = []() __attribute__((always_inline)) -> uint64_t {
     uint64_t t = 0;
     if (PROF) __asm__ volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -291,7 +324,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     ka->status[ro] = stat;
     if (ka->iters) ka->iters[ro] = n_iter;
     for (uint32_t q = 0; q < n_pages; ++q) {
-      const uint32_t pg = ptab[((q) << nbl) + ltid];
+      const uint32_t pg = ptab_at(q);
       atomicAnd(&bitmap[pg >> 5], ~(1u << (pg & 31)));
     }
     n_pages = 0;
@@ -304,6 +337,57 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     if (PROF && t_rest) pf3 += t_top - t_rest;
     // ------------------------------------------------ retire reads that ended last iteration
     if (st == 3) end_read(end_stat);
+    // the search state of a claimed read whose length, max_diff and N count are set: the two roots
+    // (bwtgap.c:126-127: strand 0 then strand 1, both score 0 -> C = strand 1)
+    auto start_read = [&]() __attribute__((always_inline)) {
+      max_diff = opt_max_diff;
+      best_score = (opt_max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape;
+      best_cnt = 0;
+      n_aln = 0;
+      status = 0;
+      seeded = len > o.seed_len;
+      ent1[0] = E::make(0u, ixv0.seq_len, len, 0, NILH, 0, 0, 0, 0, STATE_M);
+      C = E::make(0u, ixv0.seq_len, len, 0, 0u, 0, 0, 0, 1, STATE_M);
+      ent1[1] = C;
+      // every bucket head starts empty (a pop that empties a bucket writes NIL back), so a
+      // push reads its bucket's head without consulting the non-empty mask
+      for (int b = 1; b < (LW ? GAP_RING : o.n_stacks); ++b) lds_heads[hidx(b)] = (H)NILH;
+      lds_heads[hidx(0)] = 1;
+      nonempty.m0 = 1u;
+      nonempty.m1 = nonempty.m2 = nonempty.m3 = 0u;
+      bump = 2;
+      n_free = 0;
+      fl_head = NILH;
+      fl_known = true;
+      n_pages = 0;
+      n_iter = 0;
+      n_entries = 2;
+      C_slot = 1;
+      C_b = 0;
+      C_valid = true;
+      C_load = false;
+      cfl = 0;
+      st = 1;
+    };
+    // LW: reads claimed last iteration -- their records reached LDS with that iteration's loads
+    if (LW && __ballot(st == 4)) {
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (st == 4) {
+        const uint32_t hdr = cwl[ltid];
+        len = (int)(hdr & 0xFFFFu);
+        opt_max_diff = (int)(hdr >> 24);
+        const int nN = (int)((hdr >> 16) & 0xFFu);
+        if (nN > opt_max_diff) {  // bwtgap.c:116-122
+          KArgs *ka = args();
+          ka->n_aln[ro] = 0;
+          ka->status[ro] = 0;
+          st = 0;
+        } else {
+          fastrd = nN == 0 && len <= 16 * (int)CWR;
+          start_read();
+        }
+      }
+    }
     // ------------------------------------------------ claim + init new reads
     // lanes_per_wave < 64 (retry pass): a wave runs that many heavy reads, so each
     // iteration executes only their paths
@@ -326,71 +410,56 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         KArgs *ka = args();
         const int64_t rr = ka->ids ? ka->ids[r] : r;
         ro = ka->out_by_id ? rr : r;
-        len = (int)ka->len[rr];
         s = ka->seq + ka->off[rr];
-        opt_max_diff = o.fnr_pos ? (int)ka->maxdiff_tab[len] : o.max_diff;
-        max_diff = opt_max_diff;
-        best_score = (opt_max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape;
-        best_cnt = 0;
-        n_aln = 0;
-        status = 0;
-        seeded = len > o.seed_len;
         const uint2 *wb = ka->wbuf + (uint64_t)r * ka->wstride;
         W0 = wb;
         W1 = wb + ka->wlen1;
         SW0 = wb + 2 * ka->wlen1;
         SW1 = SW0 + (o.seed_len + 1);
-        const int nN = (int)ka->nN[r];
-        if (nN > max_diff) {  // bwtgap.c:116-122
-          ka->n_aln[ro] = 0;
-          ka->status[ro] = 0;
+        if (LW) {
+          // the read's k_width record straight into its LDS rows (no registers); it is used from
+          // the next iteration on, after that iteration's loads have been waited for
+          const uint32_t *src = ka->cw + (uint64_t)r * ka->cw_words;
+          const uint32_t nw = ka->cw_words;
+          __attribute__((address_space(3))) uint32_t *dst =
+              (__attribute__((address_space(3))) uint32_t *)(cwl + (tid & ~63));
+          for (uint32_t w = 0; w < nw; ++w)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + w),
+                                             (__attribute__((address_space(3))) void *)(dst + (w << nbl)), 4, 0, 0);
+          st = 4;
         } else {
-          fastrd = !WIDE && nN == 0 && len <= 16 * RDW;
-          if (fastrd) {
-            // 16 B loads from the aligned-down start (the staging buffer has 16 B of tail padding)
-            const uint4 *q0 = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15);
-            const int mis = (int)(reinterpret_cast<uintptr_t>(s) & 15);
-            const int nq = (mis + len + 15) >> 4;
-            uint32_t w = 0;
-            for (int q = 0; q < nq; ++q) {
-              const uint4 v = q0[q];
+          len = (int)ka->len[rr];
+          opt_max_diff = o.fnr_pos ? (int)ka->maxdiff_tab[len] : o.max_diff;
+          const int nN = (int)ka->nN[r];
+          if (nN > opt_max_diff) {  // bwtgap.c:116-122
+            ka->n_aln[ro] = 0;
+            ka->status[ro] = 0;
+          } else {
+            fastrd = !WIDE && nN == 0 && len <= 16 * RDW;
+            if (fastrd) {
+              // 16 B loads from the aligned-down start (the staging buffer has 16 B of tail padding)
+              const uint4 *q0 = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15);
+              const int mis = (int)(reinterpret_cast<uintptr_t>(s) & 15);
+              const int nq = (mis + len + 15) >> 4;
+              uint32_t w = 0;
+              for (int q = 0; q < nq; ++q) {
+                const uint4 v = q0[q];
 #pragma unroll
-              for (int b = 0; b < 16; ++b) {
-                const uint32_t word = b < 4 ? v.x : b < 8 ? v.y : b < 12 ? v.z : v.w;
-                const int jj = q * 16 + b - mis;
-                if (jj >= 0 && jj < len) {
-                  w |= ((word >> (8 * (b & 3))) & 3u) << (2 * (jj & 15));
-                  if ((jj & 15) == 15 || jj == len - 1) {
-                    rdl[((jj >> 4) << nbl) + ltid] = w;
-                    w = 0;
+                for (int b = 0; b < 16; ++b) {
+                  const uint32_t word = b < 4 ? v.x : b < 8 ? v.y : b < 12 ? v.z : v.w;
+                  const int jj = q * 16 + b - mis;
+                  if (jj >= 0 && jj < len) {
+                    w |= ((word >> (8 * (b & 3))) & 3u) << (2 * (jj & 15));
+                    if ((jj & 15) == 15 || jj == len - 1) {
+                      rdl[((jj >> 4) << nbl) + ltid] = w;
+                      w = 0;
+                    }
                   }
                 }
               }
             }
+            start_read();
           }
-          // roots (bwtgap.c:126-127): strand 0 then strand 1, both score 0 -> C = strand 1
-          ent1[0] = E::make(0u, ixv0.seq_len, len, 0, NILH, 0, 0, 0, 0, STATE_M);
-          C = E::make(0u, ixv0.seq_len, len, 0, 0u, 0, 0, 0, 1, STATE_M);
-          ent1[1] = C;
-          // every bucket head starts empty (a pop that empties a bucket writes NIL back), so a
-          // push reads its bucket's head without consulting the non-empty mask
-          for (int b = 1; b < o.n_stacks; ++b) lds_heads[((b) << nbl) + ltid] = (H)NILH;
-          lds_heads[ltid] = 1;
-          nonempty.m0 = 1u;
-          nonempty.m1 = nonempty.m2 = nonempty.m3 = 0u;
-          bump = 2;
-          n_free = 0;
-          fl_head = NILH;
-          fl_known = true;
-          n_pages = 0;
-          n_iter = 0;
-          n_entries = 2;
-          C_slot = 1;
-          C_b = 0;
-          C_valid = true;
-          C_load = false;
-          cfl = 0;
-          st = 1;
         }
       }
       const int64_t cnt = __popcll(need);
@@ -445,7 +514,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     uint32_t load_slot = 0;
     if (do_pop) {
       const uint32_t prev = E::prev(e);
-      lds_heads[((C_b) << nbl) + ltid] = (H)prev;
+      lds_heads[hidx(C_b)] = (H)prev;
       --n_entries;
       if (C_slot + 1 == bump) {
         bump = C_slot;
@@ -462,10 +531,16 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         load_slot = prev;
         C_load = true;
       } else {
-        bm_clr(nonempty, C_b);
-        const int b = bm_next(nonempty, C_b + 1);
+        int b;
+        if (LW) {
+          nonempty.m0 &= ~(1u << (C_b & (GAP_RING - 1)));
+          b = ring_next(nonempty.m0, C_b + 1);
+        } else {
+          bm_clr(nonempty, C_b);
+          b = bm_next(nonempty, C_b + 1);
+        }
         if (b < o.n_stacks) {
-          load_slot = lds_heads[((b) << nbl) + ltid];
+          load_slot = lds_heads[hidx(b)];
           C_b = b;
           C_load = true;
         } else {
@@ -506,19 +581,49 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     // width bounds of strand a at positions i-2, i-1 and the seed pair
     const uint2 *Wa = a ? W1 : W0;
     const uint2 *SWa = a ? SW1 : SW0;
-    uint2 w_im1 = make_uint2(0, 0), w_im2 = make_uint2(0, 0), sw_lo = make_uint2(0, 0), sw_hi = make_uint2(0, 0);
+    // as bids (bid1 = width[i-1].bid, bid2 = width[i-2].bid), "width[i-2] == width[i-1]" (eq12), and
+    // the seed pair's (sb_lo, sb_hi, seq_hi); LW: from the LDS record (bids clamped where no test
+    // can tell them apart, engine.h AlnArgs::cw)
+    uint32_t bid1 = 0, bid2 = 0, sb_lo = 0, sb_hi = 0;
+    bool eq12 = false, seq_hi = false;
     const int ii = (i - 1) - (len - o.seed_len);
-    if (srch && i > 0) w_im1 = Wa[i - 1];
-    if (srch && i > 1) w_im2 = Wa[i - 2];
-    if (srch && i > 1 && seeded && ii > 0) {
-      sw_lo = SWa[ii - 1];
-      sw_hi = SWa[ii];
+    if (LW) {
+      if (srch && i > 0) {
+        const uint32_t n1 = cw_byte((uint32_t)(i - 1)) >> (4 * a);
+        bid1 = n1 & 7u;
+        eq12 = (n1 >> 3) & 1u;
+      }
+      if (srch && i > 1) bid2 = (cw_byte((uint32_t)(i - 2)) >> (4 * a)) & 7u;
+      if (srch && i > 1 && seeded && ii > 0) {
+        const uint32_t sbase = A.wlen1;
+        sb_lo = (cw_byte(sbase + (uint32_t)(ii - 1)) >> (3 * a)) & 3u;
+        const uint32_t nh = cw_byte(sbase + (uint32_t)ii) >> (3 * a);
+        sb_hi = nh & 3u;
+        seq_hi = (nh >> 2) & 1u;
+      }
+    } else {
+      uint2 w_im1 = make_uint2(0, 0), w_im2 = make_uint2(0, 0), sw_lo = make_uint2(0, 0), sw_hi = make_uint2(0, 0);
+      if (srch && i > 0) w_im1 = Wa[i - 1];
+      if (srch && i > 1) w_im2 = Wa[i - 2];
+      if (srch && i > 1 && seeded && ii > 0) {
+        sw_lo = SWa[ii - 1];
+        sw_hi = SWa[ii];
+      }
+      bid1 = w_im1.y;
+      bid2 = w_im2.y;
+      eq12 = w_im2.x == w_im1.x;
+      sb_lo = sw_lo.y;
+      sb_hi = sw_hi.y;
+      seq_hi = sw_lo.x == sw_hi.x;
     }
     // read symbol str[i-1] (search) or str[xj] (exact); strand 1 = complement under COMPREAD
     uint32_t sym = 0;
     {
       const int sp = (srch && i > 0) ? i - 1 : (st == 2 && xj >= 0) ? xj : -1;
-      if (sp >= 0) sym = fastrd ? (rdl[((sp >> 4) << nbl) + ltid] >> (2 * (sp & 15))) & 3u : s[sp];
+      if (sp >= 0)
+        sym = fastrd ? ((LW ? cwl[((1u + ((uint32_t)sp >> 4)) << nbl) + ltid] : rdl[((sp >> 4) << nbl) + ltid]) >>
+                        (2 * (sp & 15))) & 3u
+                     : s[sp];
     }
     // next candidate
     uint4 Cn = make_uint4(0, 0, 0, 0);
@@ -526,6 +631,19 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     // successor of the free-list head, if a push took the previous head
     uint32_t fl_ld = 0;
     if (!fl_known) fl_ld = reinterpret_cast<const uint32_t *>(slot_ptr(fl_head))[0];
+    if (PROF) {
+      const unsigned long long b11 = __ballot(qrun), b12 = __ballot(qrun && !qkneg && !qshare),
+                               b13 = __ballot(srch && i > 0), b14 = __ballot(srch && i > 1 && seeded && ii > 0),
+                               b15 = __ballot(do_pop && C_load), b16 = __ballot(st != 0);
+      if (lane == 0) {
+        pl11 += __popcll(b11);
+        pl12 += __popcll(b12);
+        pl13 += __popcll(b13);
+        pl14 += __popcll(b14);
+        pl15 += __popcll(b15);
+        pl16 += __popcll(b16);
+      }
+    }
     if (PROF) {
       __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
       t_rest = pnow();
@@ -595,7 +713,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     }
     if (!do_pop) continue;
     if (m < 0) continue;                                   // bwtgap.c:147
-    if (i > 0 && m < (int)w_im1.y) continue;              // bwtgap.c:155
+    if (i > 0 && m < (int)bid1) continue;                 // bwtgap.c:155
     if (i == 0) goto hit;                                  // bwtgap.c:159
     if (m == 0 && (state == STATE_M || (o.mode & MODE_GAPE) || e_ge == o.max_gape)) {
       // bwt_match_exact_alt over str[0..i-1] (bwtgap.c:160-163): the first step uses this
@@ -622,12 +740,12 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       const uint32_t occ = l - k + 1;
       bool allow_diff = true, allow_M = true;
       if (ni > 0) {
-        // width[ni-1] = w_im2, width[ni] = w_im1
-        if ((int)w_im2.y > m - 1) allow_diff = false;
-        else if ((int)w_im2.y == m - 1 && (int)w_im1.y == m - 1 && w_im2.x == w_im1.x) allow_M = false;
+        // width[ni-1] = position i-2, width[ni] = position i-1
+        if ((int)bid2 > m - 1) allow_diff = false;
+        else if ((int)bid2 == m - 1 && (int)bid1 == m - 1 && eq12) allow_M = false;
         if (seeded && ii > 0) {
-          if ((int)sw_lo.y > m_seed - 1) allow_diff = false;
-          else if ((int)sw_lo.y == m_seed - 1 && (int)sw_hi.y == m_seed - 1 && sw_lo.x == sw_hi.x) allow_M = false;
+          if ((int)sb_lo > m_seed - 1) allow_diff = false;
+          else if ((int)sb_lo == m_seed - 1 && (int)sb_hi == m_seed - 1 && seq_hi) allow_M = false;
         }
       }
       // children in the reference's push order (bwtgap.c:216-258), as bits of a mask:
@@ -670,7 +788,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
               const uint32_t bit = (uint32_t)__builtin_ctz(~x);
               const uint32_t old = atomicOr(&bitmap[w], 1u << bit);
               if (!(old & (1u << bit))) {
-                ptab[((n_pages) << nbl) + ltid] = (uint16_t)(w * 32 + bit);
+                ptab_at(n_pages) = (uint16_t)(w * 32 + bit);
                 ++n_pages;
                 got = true;
                 break;
@@ -711,7 +829,13 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         const uint32_t fl_n = use_fl ? 1u : 0u;
         // narrow: the lane's whole free stack in one LDS read
         uint4 fsr = make_uint4(0, 0, 0, 0);
-        if (!WIDE && n_fs) fsr = *reinterpret_cast<const uint4 *>(free_slots + fsi(0));
+        if (LW && n_fs) {
+          const uint2 f2 = *reinterpret_cast<const uint2 *>(free_slots + fsi(0));
+          fsr.x = f2.x;
+          fsr.y = f2.y;
+        } else if (!WIDE && n_fs) {
+          fsr = *reinterpret_cast<const uint4 *>(free_slots + fsi(0));
+        }
         // slot of the t-th push: free stack, then the free list's head, then the bump region
         // (skipping the hit area)
         auto slot_at = [&](uint32_t t) __attribute__((always_inline)) -> uint32_t {
@@ -747,7 +871,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         if (vg) {
           if (pleader()) ++pf5;
           const bool tk = !C_valid || scG <= C_b;
-          uint32_t link = (uint32_t)lds_heads[((scG) << nbl) + ltid];
+          uint32_t link = (uint32_t)lds_heads[hidx(scG)];
           const int n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (open ? 0 : 1);
           uint4 last = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -762,7 +886,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
               link = slot;
             }
           }
-          lds_heads[((scG) << nbl) + ltid] = (H)link;
+          lds_heads[hidx(scG)] = (H)link;
           group_take(tk, last, link, scG);
         }
         // ---- mismatch children (bits 5-8 but the match child): bucket scMM
@@ -770,7 +894,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         if (vmm) {
           if (pleader()) ++pf5;
           const bool tk = !C_valid || scMM <= C_b;
-          uint32_t link = (uint32_t)lds_heads[((scMM) << nbl) + ltid];
+          uint32_t link = (uint32_t)lds_heads[hidx(scMM)];
           uint4 last = make_uint4(0, 0, 0, 0);
 #pragma unroll
           for (int j = 5; j < 9; ++j) {
@@ -782,16 +906,16 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
               link = slot;
             }
           }
-          lds_heads[((scMM) << nbl) + ltid] = (H)link;
+          lds_heads[hidx(scMM)] = (H)link;
           group_take(tk, last, link, scMM);
         }
         // ---- the match child (bucket sc_base <= C_b: always the new candidate): kept in C, not
         // stored; C moves to D, the old D is stored if memory lacks it
         if (has_match && vm) {
           const uint32_t slot = slot_at(t++);
-          const uint32_t hd = (uint32_t)lds_heads[((sc_base) << nbl) + ltid];
+          const uint32_t hd = (uint32_t)lds_heads[hidx(sc_base)];
           const uint4 ne = E::make(pick4(KK, csym), pick4(LL, csym), ni, ldp, hd, e_mm, e_go, e_ge, a, STATE_M);
-          lds_heads[((sc_base) << nbl) + ltid] = (H)slot;
+          lds_heads[hidx(sc_base)] = (H)slot;
           if ((cfl & 6u) == 6u) *slot_ptr(D_slot) = D;
           D = C;
           D_slot = C_slot;
@@ -810,9 +934,14 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           const uint32_t nb = t - n_fs - fl_n;
           bump = b0 + nb + ((nb && b0 <= skip_at && b0 + nb > skip_at) ? HS : 0u);
           n_entries += (int)t;
-          if (has_match) bm_set(nonempty, sc_base);
-          if (has_mm) bm_set(nonempty, scMM);
-          if (has_gap) bm_set(nonempty, scG);
+          if (LW) {
+            nonempty.m0 |= (has_match ? 1u << (sc_base & (GAP_RING - 1)) : 0u) |
+                           (has_mm ? 1u << (scMM & (GAP_RING - 1)) : 0u) | (has_gap ? 1u << (scG & (GAP_RING - 1)) : 0u);
+          } else {
+            if (has_match) bm_set(nonempty, sc_base);
+            if (has_mm) bm_set(nonempty, scMM);
+            if (has_gap) bm_set(nonempty, scG);
+          }
         }
       }
       if (pl_) ++pf8;
@@ -855,6 +984,16 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       uint2 *width = const_cast<uint2 *>(a ? W1 : W0);
       const uint32_t x = l - k + 1, mx = ix.seq_len;
       uint32_t jj = 0;
+      // LW: the LDS nibbles of strand a follow -- bid (clamped) of every changed position and the
+      // "equals the previous width" bit of positions 1..ldp
+      const uint32_t cf = (uint32_t)opt_max_diff + 1u;
+      const uint32_t w_ldp = LW && ldp <= len ? width[ldp].x : 0u;
+      uint32_t prevx = 0;
+      auto set_nib = [&](int p, uint32_t nib, uint32_t keep) __attribute__((always_inline)) {
+        const uint32_t w = 1u + CWR + ((uint32_t)p >> 2), sh = 8u * ((uint32_t)p & 3u) + 4u * (uint32_t)a;
+        uint32_t &cell = cwl[(w << nbl) + ltid];
+        cell = (cell & ~(keep << sh)) | (nib << sh);
+      };
       for (int q0 = 0; q0 < ldp; q0 += 8) {
         uint2 wv[8];
 #pragma unroll
@@ -862,11 +1001,18 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           if (q0 + u >= ldp) break;
-          const uint2 w = wv[u];
-          if (w.x > x) width[q0 + u] = make_uint2(w.x - x, w.y);
-          else if (w.x == x) { ++jj; width[q0 + u] = make_uint2(mx - jj, 1u); }
+          uint2 w = wv[u];
+          if (w.x > x) { w.x -= x; width[q0 + u] = w; }
+          else if (w.x == x) { ++jj; w = make_uint2(mx - jj, 1u); width[q0 + u] = w; }
+          if (LW) {
+            const int p = q0 + u;
+            const uint32_t eq = p > 0 && prevx == w.x;
+            set_nib(p, (w.y < cf ? w.y : cf) | eq << 3, 0xFu);
+            prevx = w.x;
+          }
         }
       }
+      if (LW && ldp > 0 && ldp <= len) set_nib(ldp, (prevx == w_ldp ? 1u : 0u) << 3, 0x8u);
       if ((uint32_t)n_aln >= HS) {
         
         end_stat = ST_ALN_OVERFLOW;  // hit area full
@@ -882,9 +1028,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   }
   }
   if (PROF && A.prof) {
-    const uint64_t v[11] = {pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7, pf8, pf9, pf10};
+    const uint64_t v[17] = {pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7, pf8, pf9, pf10, pl11, pl12, pl13, pl14, pl15, pl16};
 #pragma unroll
-    for (int q = 0; q < 11; ++q)
+    for (int q = 0; q < 17; ++q)
       if (v[q]) atomicAdd(A.prof + q, (unsigned long long)v[q]);
   }
 }
@@ -894,14 +1040,19 @@ hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int bl
   if (g.n <= 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
-  const size_t lds =
-      gapped_lds_bytes(g.o.n_stacks, block, wide, g.max_pages, g.pages_per_block, g.lanes_per_wave, g.free_depth);
+  const bool lw = !wide && g.cw != nullptr;
+  const size_t lds = gapped_lds_bytes(g.o.n_stacks, block, wide, g.max_pages, g.pages_per_block, g.lanes_per_wave,
+                                      g.free_depth, lw ? (int)g.cw_words : 0);
   if (wide)
-    hipLaunchKernelGGL((k_gapped<true, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<true, false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+  else if (lw && g.prof)
+    hipLaunchKernelGGL((k_gapped<false, true, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+  else if (lw)
+    hipLaunchKernelGGL((k_gapped<false, false, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   else if (g.prof)
-    hipLaunchKernelGGL((k_gapped<false, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<false, true, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   else
-    hipLaunchKernelGGL((k_gapped<false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<false, false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   return hipGetLastError();
 }
 
