@@ -926,7 +926,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                 it[(size_t)(cnt * 0.99)], it[(size_t)(cnt * 0.9999)], mx, b, sum / (b * 1e-3));
       }
       if (c->prof_phases) {
-        unsigned long long pf[17];
+        unsigned long long pf[19];
         HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
         const char *nm[4] = {"claim", "pop", "wait", "rest"};
         double tot = (double)(pf[0] + pf[1] + pf[2] + pf[3]);
@@ -938,8 +938,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                 pf[10] / wi, pf[9]);
         const double li = pf[16] ? (double)pf[16] : 1.0;
         fprintf(stderr, "[ibwa_amd] k_gapped loads per live lane-iteration: block %.3f second block %.3f widths %.3f "
-                "seed widths %.3f candidate %.3f (%.3g live lane-iterations)\n", pf[11] / li, pf[12] / li, pf[13] / li,
-                pf[14] / li, pf[15] / li, (double)pf[16]);
+                "seed widths %.3f candidate %.3f; exact steps %.3f (unique interval %.3f) (%.3g live lane-iterations)\n",
+                pf[11] / li, pf[12] / li, pf[13] / li, pf[14] / li, pf[15] / li, pf[17] / li, pf[18] / li, (double)pf[16]);
       }
     }
   }

@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   uint64_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0, pf7 = 0, t_rest = 0;
   uint64_t pf8 = 0, pf9 = 0, pf10 = 0;
   // lane counts (PROF): block loads, second-block loads, width loads, seed-width loads, candidate loads, live lanes
-  uint64_t pl11 = 0, pl12 = 0, pl13 = 0, pl14 = 0, pl15 = 0, pl16 = 0;
+  uint64_t pl11 = 0, pl12 = 0, pl13 = 0, pl14 = 0, pl15 = 0, pl16 = 0, pl17 = 0, pl18 = 0;
   auto pnow = []() __attribute__((always_inline)) -> uint64_t {
     uint64_t t = 0;
     if (PROF) __asm__ volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -634,7 +634,8 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     if (PROF) {
       const unsigned long long b11 = __ballot(qrun), b12 = __ballot(qrun && !qkneg && !qshare),
                                b13 = __ballot(srch && i > 0), b14 = __ballot(srch && i > 1 && seeded && ii > 0),
-                               b15 = __ballot(do_pop && C_load), b16 = __ballot(st != 0);
+                               b15 = __ballot(do_pop && C_load), b16 = __ballot(st != 0), b17 = __ballot(st == 2),
+                               b18 = __ballot(st == 2 && xk == xl);
       if (lane == 0) {
         pl11 += __popcll(b11);
         pl12 += __popcll(b12);
@@ -642,6 +643,8 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         pl14 += __popcll(b14);
         pl15 += __popcll(b15);
         pl16 += __popcll(b16);
+        pl17 += __popcll(b17);
+        pl18 += __popcll(b18);
       }
     }
     if (PROF) {
@@ -1028,9 +1031,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   }
   }
   if (PROF && A.prof) {
-    const uint64_t v[17] = {pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7, pf8, pf9, pf10, pl11, pl12, pl13, pl14, pl15, pl16};
+    const uint64_t v[19] = {pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7, pf8, pf9, pf10, pl11, pl12, pl13, pl14, pl15, pl16, pl17, pl18};
 #pragma unroll
-    for (int q = 0; q < 17; ++q)
+    for (int q = 0; q < 19; ++q)
       if (v[q]) atomicAdd(A.prof + q, (unsigned long long)v[q]);
   }
 }
