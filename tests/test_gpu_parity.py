@@ -187,3 +187,24 @@ def test_rejects_zero_penalty(gpu_engine):
     o.s_gapo = 0  # the reference aborts on -O 0
     with pytest.raises(E.IbwaError):
         gpu_engine.aln(np.zeros(36, np.uint8), np.zeros(1, np.uint64), np.full(1, 36, np.uint32), o)
+
+
+@pytest.mark.parametrize("gap_lw", [1, 0])
+def test_sai_goldens_lds_widths(golden_dir, sai_manifest, gpu_engine, gap_lw):
+    """The first pass with its width bounds in LDS (gapped.hip LW: clamped bids, equality bits,
+    ring of bucket heads; used when the options and the LDS budget allow) and without them: every
+    gapped golden .sai either way (150 bp reads and the -M 1 -O 3 -E 1 penalties also exercise the
+    fallback's selection)."""
+    gpu_engine.set_option("gap_lw", gap_lw)
+    bad = []
+    for key, m in sorted(sai_manifest.items()):
+        if m["argv"] == ["-n", "0"]:
+            continue
+        opt, _ = oracle.parse_aln_args(m["argv"])
+        recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+        seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+        n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+        if not oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), open(os.path.join(golden_dir, key + ".sai"), "rb").read()):
+            bad.append(key)
+    gpu_engine.set_option("gap_lw", 1)
+    assert not bad, bad
