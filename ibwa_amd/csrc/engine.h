@@ -154,6 +154,10 @@ hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blo
 // only sizes the rocPRIM scratch into *tmp_bytes
 hipError_t select_handed_on(const uint32_t *status, int64_t n, int64_t *ids, uint32_t *sel_status,
                             unsigned long long *d_count, void *tmp, size_t *tmp_bytes, hipStream_t st);
+// the order in which the cooperative pass takes the handed-on reads: largest first-pass stack first
+// (status bits 16-31); idx[0, n) gets the permutation of the selection, ids_out the ids in that order
+hipError_t order_heavy_first(const uint32_t *sel_status, const int64_t *ids, unsigned long long n, uint32_t *keys,
+                             uint32_t *idx, int64_t *ids_out, void *tmp, size_t *tmp_bytes, hipStream_t st);
 
 // Kernel arguments of the exact-match path: only what it reads (fewer SGPRs).
 struct ExactArgs {

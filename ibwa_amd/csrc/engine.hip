@@ -93,6 +93,8 @@ struct ibwa_ctx {
   std::vector<int64_t> patch_ids;                   // ... of which the wide / general passes' (input order)
   std::vector<std::vector<uint4>> patch_alns;       // their hits (the coop pass writes into d_aln / d_naln)
   DBuf d_selst, d_seltmp;                           // statuses of the handed-on reads, select scratch
+  DBuf d_ordk, d_ordi, d_ordids, d_ordtmp;          // the coop pass's order (largest first-pass stack first)
+  int coop_order = 1;                               // option
   uint32_t aln_cap_used = 0;
   // sampled suffix arrays kept by ibwa_ctx_build_index
   DBuf sa_s[2];
@@ -349,6 +351,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_early_iters" && value >= 0) c->gap_early_iters = (uint32_t)value;
   else if (k == "gap_early_entries" && value >= 0) c->gap_early_entries = (uint32_t)value;
   else if (k == "gap_lw" && (value == 0 || value == 1)) c->gap_lw = (int)value;
+  else if (k == "coop_order" && (value == 0 || value == 1)) c->coop_order = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
   else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
@@ -1051,9 +1054,30 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (int rc = c->c_next.ensure(64)) return rc;
     if (int rc = c->r_status.ensure(lanes * 4)) return rc;
     if (int rc = c->d_counter.ensure(64)) return rc;
-    // d_ids already holds todo (select_handed_on)
+    // d_ids holds todo (select_handed_on, input order); the pass takes the reads with the largest
+    // first-pass stacks first (its longest reads then do not start near its end) -- which pass or
+    // which order resolves a read changes nothing in its results
+    const int64_t *coop_ids = c->d_ids.as<int64_t>();
+    if (c->coop_order && lanes > 1) {
+      size_t tb = 0;
+      HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &tb, c->stream));
+      if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;
+      if (int rc = c->d_ordi.ensure(lanes * 8)) return rc;
+      if (int rc = c->d_ordids.ensure(lanes * 8)) return rc;
+      if (int rc = c->d_ordtmp.ensure(tb + 16)) return rc;
+      HIPCHK(order_heavy_first(c->d_selst.as<uint32_t>(), c->d_ids.as<int64_t>(), lanes, c->d_ordk.as<uint32_t>(),
+                               c->d_ordi.as<uint32_t>(), c->d_ordids.as<int64_t>(), c->d_ordtmp.p, &tb, c->stream));
+      std::vector<uint32_t> perm(lanes);
+      HIPCHK(hipMemcpyAsync(perm.data(), c->d_ordi.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      for (int64_t j = 0; j < lanes; ++j) {
+        todo[j] = c->retry_ids[perm[j]];
+        where[j] = perm[j];
+      }
+      coop_ids = c->d_ordids.as<int64_t>();
+    }
     AlnArgs B = A;
-    B.ids = c->d_ids.as<int64_t>();
+    B.ids = coop_ids;
     B.n = lanes;
     B.wbuf = c->d_wbuf.as<uint2>();
     B.nN = c->d_nN.as<uint16_t>();

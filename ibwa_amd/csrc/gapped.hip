@@ -478,7 +478,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     if (((A.max_iters && n_iter > A.max_iters) ||
          (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries)) &&
         (st == 1 || st == 2)) {
-      status |= ST_HEAVY;  // a long search: the retry pass re-runs it from the start
+      // a long search: the retry pass re-runs it from the start; bits 16-31 keep the stack size
+      // (the cooperative pass takes the biggest first, so its longest reads do not start last)
+      status |= ST_HEAVY | (uint32_t)(n_entries < 0xFFFF ? n_entries : 0xFFFF) << 16;
       st = 1;
       n_entries = 0;
     }

@@ -28,7 +28,33 @@ __global__ void k_gather_status(const uint32_t *status, const int64_t *ids, cons
     out[i] = status[ids[i]];
 }
 
+__global__ void k_order_keys(const uint32_t *sel_status, unsigned long long n, uint32_t *keys, uint32_t *idx) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    keys[i] = 0xFFFFu - (sel_status[i] >> 16);  // ascending sort = largest stack first
+    idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ void k_gather_ids(const int64_t *ids, const uint32_t *perm, unsigned long long n, int64_t *out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = ids[perm[i]];
+}
+
 }  // namespace
+
+hipError_t order_heavy_first(const uint32_t *sel_status, const int64_t *ids, unsigned long long n, uint32_t *keys,
+                             uint32_t *idx, int64_t *ids_out, void *tmp, size_t *tmp_bytes, hipStream_t st) {
+  // keys / idx hold 2n entries each (double buffers); on return idx[0, n) is the order
+  rocprim::double_buffer<uint32_t> kb(keys, keys + n), vb(idx, idx + n);
+  if (!tmp) return rocprim::radix_sort_pairs(nullptr, *tmp_bytes, kb, vb, (size_t)n, 0, 16, st);
+  hipLaunchKernelGGL(k_order_keys, dim3(1024), dim3(256), 0, st, sel_status, n, keys, idx);
+  hipError_t e = rocprim::radix_sort_pairs(tmp, *tmp_bytes, kb, vb, (size_t)n, 0, 16, st);
+  if (e != hipSuccess) return e;
+  if (vb.current() != idx) e = hipMemcpyAsync(idx, vb.current(), n * 4, hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gather_ids, dim3(1024), dim3(256), 0, st, ids, idx, n, ids_out);
+  return hipGetLastError();
+}
 
 hipError_t select_handed_on(const uint32_t *status, int64_t n, int64_t *ids, uint32_t *sel_status,
                             unsigned long long *d_count, void *tmp, size_t *tmp_bytes, hipStream_t st) {
