@@ -34,11 +34,20 @@ __device__ __forceinline__ int sm(uint32_t x, uint32_t y) {
   return (x > 3 || y > 3) ? -13 : (x == y ? 11 : -19);
 }
 
+// Per-wave scratch.  What the lanes touch in step with each other (the forward pass's reference
+// words and strip boundaries, the global fill's M / I / D rows and traceback bytes: the lanes'
+// alignments have the same shape, so a wave's access at one element is one contiguous segment) is
+// lane-minor; the reverse pass's eh row, where each lane's adaptive band goes its own way, is
+// lane-major, so a lane's consecutive cells share cache lines instead of each touching a line of
+// its own (measured: reverse pass 89 -> 25 ms per 200 k rescues; the global fill lane-major was
+// 4x slower).
 struct Lane {
-  uint32_t *w;   // this wave's u32 scratch, element e of lane at w[e * 64 + lane]
+  uint32_t *w;   // lane-minor words: element e of lane at w[e * 64 + lane]
+  uint32_t *wv;  // this lane's lane-major words
   uint8_t *tb;   // this wave's traceback bytes, element e at tb[e * 64 + lane]
   int lane;
   __device__ __forceinline__ uint32_t &u(uint32_t e) const { return w[(uint64_t)e * 64 + lane]; }
+  __device__ __forceinline__ uint32_t &v(uint32_t e) const { return wv[e]; }
   __device__ __forceinline__ uint8_t &t(uint32_t e) const { return tb[(uint64_t)e * 64 + lane]; }
 };
 
@@ -193,14 +202,17 @@ __device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD,
 __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counter) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // lane-minor elements: ref4[(l1+31)/32*4], the strip boundaries H / F per row, two rows each of
+  // M / I / D for the global fill; lane-major: eh[0..l1+1] (sw_words_per_lane in total)
+  const uint32_t eREF = 0, eBH = eREF + (A.max_len1 + 31) / 32 * 4, eBF = eBH + A.max_len2 + 1;
+  const uint32_t eM = eBF + A.max_len2 + 1, eI = eM + 2 * (A.max_len1 + 1), eD = eI + 2 * (A.max_len1 + 1);
+  const uint32_t nminor = eD + 2 * (A.max_len1 + 1);
+  const uint32_t eEH = 0, nmajor = A.max_len1 + 2;
   Lane L;
   L.w = A.scratch + wave * A.words_per_lane * 64;
+  L.wv = L.w + (uint64_t)nminor * 64 + (uint64_t)lane * nmajor;
   L.tb = A.tb + wave * A.tb_per_lane * 64;
   L.lane = lane;
-  // scratch elements (u32): eh[0..l1+1], ref4[(l1+7)/8], then M/I/D rows for the global fill
-  const uint32_t eEH = 0, eREF = A.max_len1 + 2, eM = eREF + (A.max_len1 + 31) / 32 * 4;
-  const uint32_t eI = eM + 2 * (A.max_len1 + 1), eD = eI + 2 * (A.max_len1 + 1);
-  const uint32_t eBH = eD + 2 * (A.max_len1 + 1), eBF = eBH + A.max_len2 + 1;  // strip boundaries per row
   int64_t cur = 0, cend = 0;
   for (;;) {
     // one pair per lane, claimed per wave
@@ -299,17 +311,17 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
       score = score_f;
       if (score_f >= 1 && end_i > 0 && end_j > 0 && A.stop_after != 1) {
         // ---- reverse pass (stdaln.c:639-696) in the adaptive band
-        for (int i = 0; i <= end_i; ++i) L.u(eEH + i) = 0;
+        for (int i = 0; i <= end_i; ++i) L.v(eEH + i) = 0;
         int score_r = sm(a[end_i - 1], b[end_j - 1]);
         int start_i = end_i, start_j = end_j;
-        L.u(eEH + end_i) = (uint32_t)(QR + score_r) << 16;
+        L.v(eEH + end_i) = (uint32_t)(QR + score_r) << 16;
         int start = end_i - 1, end = end_i - 3;
         if (end <= 0) end = 0;
         for (int j = end_j - 1; j != 0; --j) {
           const uint32_t cb = b[j - 1];
           int last_h = 0, f = 0, i = start;
           bool found = false;
-          int nxt = (int)L.u(eEH + i + 1);  // eh[i+1] of the row below (old value)
+          int nxt = (int)L.v(eEH + i + 1);  // eh[i+1] of the row below (old value)
           // cells start, start-1, ..., end+1 (start > end always), RCHUNK at a time: the
           // chunk's old eh values and codes are loaded together before its cells are updated
           // (a cell writes eh[i+1] only, so all loaded values are still the row below's)
@@ -320,7 +332,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
             for (int k = 0; k < RCHUNK; ++k) {
               const int ik = i - k;
               const bool ok = ik > end && ik > 0;
-              ab[k] = ok ? (int)L.u(eEH + ik) : 0;
+              ab[k] = ok ? (int)L.v(eEH + ik) : 0;
               cd[k] = ok ? a[ik - 1] : 0u;
             }
 #pragma unroll
@@ -336,7 +348,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
                 int e = (e_old > above - Q) ? e_old - R : above - QR;
                 if (e < 0) e = 0;
                 if (h < e) h = e;
-                L.u(eEH + i + 1) = (uint32_t)last_h << 16 | (uint32_t)e;
+                L.v(eEH + i + 1) = (uint32_t)last_h << 16 | (uint32_t)e;
                 last_h = h;
                 if (score_r < h) {
                   score_r = h; start_i = i; start_j = j;
@@ -350,8 +362,8 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
             }
           }
           if (found) j = 1;
-          L.u(eEH + i + 1) = (uint32_t)last_h << 16;
-          if (((int)L.u(eEH + start) >> 16) <= QR) --start;
+          L.v(eEH + i + 1) = (uint32_t)last_h << 16;
+          if (((int)L.v(eEH + start) >> 16) <= QR) --start;
           if (start <= 0) start = 0;
           end = start_i - (start_j - j) - (score_r + (start_j - j) * MAXSC) / R - 1;
           if (end <= 0) end = 0;
