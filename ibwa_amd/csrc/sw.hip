@@ -197,6 +197,73 @@ __device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD,
   return best;
 }
 
+// One strip of the forward pass (stdaln.c:600-631): columns i0 .. i0+STRIP-1 for every row, the
+// strip's H / E of the row above in registers, (H[j][i0-1], F) per row from / to scratch.  Branch
+// free: sm() comes from a per-column profile (6-bit field 6*cb = sm(cb, column code) + 32), the
+// F / E rules are selects, and the first maximum is found per row as the largest (h << 5 | 31-k)
+// (the leftmost cell of the row's largest h), then compared with the running (score, j, i) in
+// the reference's row-major order.  PART: the last strip is narrower than STRIP (its extra
+// columns compute junk that nothing reads, and they are kept out of the maximum).
+template <bool PART>
+__device__ __forceinline__ void fwd_strip(const Lane &L, uint32_t eREF, uint32_t eBH, uint32_t eBF,
+                                          const uint8_t *b, int n1, int n2, int i0, int &score_f, int &end_i,
+                                          int &end_j) {
+  const int wcols = n1 - i0 + 1;
+  int Hc[STRIP], Ec[STRIP];  // H[j-1][i], E[j-1][i] of the strip's columns
+  uint32_t cp[STRIP];        // column profiles
+  uint32_t rc[STRIP / 8];
+#pragma unroll
+  for (int k = 0; k < STRIP / 8; ++k) rc[k] = L.u(eREF + (uint32_t)(i0 - 1) / 8 + k);
+#pragma unroll
+  for (int k = 0; k < STRIP; ++k) {
+    const uint32_t ca = (rc[k >> 3] >> (4 * (k & 7))) & 15u;
+    // fields cb = 0..3: 13 (mismatch) or 43 (match), field 4 (N): 19; an N column: 19 everywhere
+    cp[k] = ca > 3 ? 19u * 0x1041041u : 13u * 0x41041u + (19u << 24) + (30u << (6 * ca));
+    Hc[k] = Ec[k] = 0;
+  }
+  int diag_next = 0;  // H[j-1][i0-1]
+  for (int j = 1; j <= n2; ++j) {
+    uint32_t cb = b[j - 1];
+    cb = cb > 4 ? 24u : cb * 6u;
+    int last_h = 0, f = 0;  // H[j][i0-1] and the row's F state, from the previous strip
+    if (i0 > 1) {
+      last_h = (int)L.u(eBH + j);
+      f = (int)L.u(eBF + j);
+    }
+    int diag = diag_next;
+    diag_next = last_h;
+    uint32_t rk = 0;
+#pragma unroll
+    for (int k = 0; k < STRIP; ++k) {
+      const int above = Hc[k], e_old = Ec[k];
+      const int hd = diag + (int)__builtin_amdgcn_ubfe(cp[k], cb, 6) - 32;
+      const int fn = max(f - R, last_h - QR);
+      const bool lp = last_h > 0;
+      f = lp ? fn : f;
+      const int fm = lp ? fn : 0;
+      const int e = above > QR ? max(e_old - R, above - QR) : 0;
+      const int h = max(max(hd, fm), e);  // >= 0: e is
+      Ec[k] = e;
+      Hc[k] = h;
+      diag = above;
+      last_h = h;
+      uint32_t key = (uint32_t)h << 5 | (uint32_t)(31 - k);
+      if (PART && k >= wcols) key = 0;
+      rk = max(rk, key);
+    }
+    if (!PART && i0 + STRIP <= n1) {  // boundary for the next strip
+      L.u(eBH + j) = (uint32_t)last_h;
+      L.u(eBF + j) = (uint32_t)f;
+    }
+    const int rh = (int)(rk >> 5), ri = i0 + 31 - (int)(rk & 31);
+    if (rh > score_f || (rh == score_f && rh > 0 && (j < end_j || (j == end_j && ri < end_i)))) {
+      score_f = rh;
+      end_i = ri;
+      end_j = j;
+    }
+  }
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counter) {
@@ -250,8 +317,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
       // ---- forward pass (stdaln.c:579-631): row j over seq2, columns i over seq1.
       // Strip-mined: STRIP columns at a time for all rows, the strip's H / E of the row
       // above in registers; between strips only (H[j][i0-1], F) per row goes through
-      // scratch.  The reference's first maximum in row-major order is kept by comparing
-      // (score, j, i) lexicographically.
+      // scratch (fwd_strip).
       for (int w = 0; w < (n1 + 31) / 32 * 4; ++w) {
         uint32_t x = 0;
         for (int k = 0; k < 8 && w * 8 + k < n1; ++k) x |= (uint32_t)a[w * 8 + k] << (4 * k);
@@ -259,54 +325,10 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
       }
       int score_f = 0, end_i = 0, end_j = 0;
       for (int i0 = 1; i0 <= n1; i0 += STRIP) {
-        const int wcols = n1 - i0 + 1 < STRIP ? n1 - i0 + 1 : STRIP;
-        int Hc[STRIP], Ec[STRIP];  // H[j-1][i], E[j-1][i] of the strip's columns
-        uint32_t rc[STRIP / 8];    // the strip's reference codes, 4 bits each
-#pragma unroll
-        for (int k = 0; k < STRIP; ++k) Hc[k] = Ec[k] = 0;
-#pragma unroll
-        for (int k = 0; k < STRIP / 8; ++k) rc[k] = L.u(eREF + (uint32_t)(i0 - 1) / 8 + k);
-        int diag_next = 0;  // H[j-1][i0-1]
-        for (int j = 1; j <= n2; ++j) {
-          const uint32_t cb = b[j - 1];
-          int last_h = 0, f = 0;  // H[j][i0-1] and the row's F state, from the previous strip
-          if (i0 > 1) {
-            last_h = (int)L.u(eBH + j);
-            f = (int)L.u(eBF + j);
-          }
-          int diag = diag_next;
-          diag_next = last_h;
-#pragma unroll
-          for (int k = 0; k < STRIP; ++k) {
-            if (k < wcols) {
-              const uint32_t ca = (rc[k >> 3] >> (4 * (k & 7))) & 15u;
-              const int above = Hc[k], e_old = Ec[k];
-              int h = diag + sm(cb, ca);
-              if (h < 0) h = 0;
-              if (last_h > 0) {
-                f = (f > last_h - Q) ? f - R : last_h - QR;
-                if (h < f) h = f;
-              }
-              int e = 0;
-              if (above >= QR + 1) {
-                e = (e_old > above - Q) ? e_old - R : above - QR;
-                if (h < e) h = e;
-              }
-              Ec[k] = e;
-              Hc[k] = h;
-              diag = above;
-              last_h = h;
-              const int i = i0 + k;
-              if (h > score_f || (h == score_f && h > 0 && (j < end_j || (j == end_j && i < end_i)))) {
-                score_f = h; end_i = i; end_j = j;
-              }
-            }
-          }
-          if (i0 + STRIP <= n1) {  // boundary for the next strip
-            L.u(eBH + j) = (uint32_t)last_h;
-            L.u(eBF + j) = (uint32_t)f;
-          }
-        }
+        if (n1 - i0 + 1 >= STRIP)
+          fwd_strip<false>(L, eREF, eBH, eBF, b, n1, n2, i0, score_f, end_i, end_j);
+        else
+          fwd_strip<true>(L, eREF, eBH, eBF, b, n1, n2, i0, score_f, end_i, end_j);
       }
       score = score_f;
       if (score_f >= 1 && end_i > 0 && end_j > 0 && A.stop_after != 1) {
