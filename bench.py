@@ -24,6 +24,9 @@ Extra JSON fields (rank 0, N=1):
   extra.parity  -- GPU == CPU restatement on >= 200k reads plus reads the cooperative / wide /
                    general passes resolved
   extra.exact_leg -- configs[1] (10M reads, -n 0) on the same index, with its own roofline
+  extra.sw_leg  -- k_sw on 200k mate-rescue pairs (510 bp window x 150 bp read, configs[4]'s SW
+                   shape) from the same genome: alignments/s, GCUPS over the forward cells, the
+                   forward pass alone (engine option sw_stop=1) against its VALU roofline
 """
 import argparse
 import ctypes
@@ -289,6 +292,68 @@ def exact_leg(eng, ascii_, lens, args, threads, hip, do_cpu):
     return out
 
 
+SW_OPS_PER_CELL = 18  # VALU instructions per cell of k_sw's branch-free forward strip (gfx950 asm)
+VALU_PEAK_LANE_OPS = 256 * 64 * 2.4e9  # MI355X_MICROARCH.md: 256 CUs x 64 lanes/clk x 2.4 GHz
+
+
+def make_sw_pairs(codes, n, seed=5):
+    """bwa_paired_sw's rescue shape (tools/sw_bench.py): a 510 bp window around a 150 bp read
+    drawn from inside it, 2 % substitutions, 30 % of reads with a 1-5 bp indel."""
+    import random
+    rng = np.random.default_rng(seed)
+    r = random.Random(seed)
+    W, L = 510, 150
+    starts = rng.integers(0, codes.size - W, n)
+    refs, reads = [], []
+    for k in range(n):
+        w = codes[starts[k]:starts[k] + W]
+        o = r.randrange(0, W - L)
+        rd = w[o:o + L].copy()
+        m = rng.random(L) < 0.02
+        rd[m] = (rd[m] + rng.integers(1, 4, int(m.sum()))) & 3
+        if r.random() < 0.3:
+            j, d = r.randrange(10, L - 10), r.randint(1, 5)
+            rd = np.concatenate([rd[:j], rd[j + d:], rng.integers(0, 4, d).astype(np.uint8)])
+        refs.append(w)
+        reads.append(rd)
+    return refs, reads
+
+
+def sw_leg(eng, refs, reads, do_cpu, steps=3):
+    """k_sw (aln_local_core + aln_global_core + CIGAR) over the pairs; the forward pass alone with
+    sw_stop=1.  Parity: a sample bit-exact against the CPU restatement."""
+    n = len(refs)
+    cells = 510.0 * 150.0 * n
+    out = {"workload": f"{n} mate-rescue pairs, 510 bp window x 150 bp read", "pairs": n}
+    for stop, tag in ((1, "forward"), (0, "full")):
+        eng.set_option("sw_stop", stop)
+        eng.sw(refs[:1000], reads[:1000])
+        ms = 0.0
+        for _ in range(steps):
+            res = eng.sw(refs, reads)
+            ms += eng.stats().ms_sw
+        ms /= steps
+        out[f"{tag}_kernel_ms"] = ms
+        out[f"{tag}_GCUPS"] = cells / (ms * 1e-3) / 1e9
+    eng.set_option("sw_stop", 0)
+    out["value"] = n / (out["full_kernel_ms"] * 1e-3)
+    out["unit"] = "alignments/s"
+    ach = out["forward_GCUPS"] * 1e9 * SW_OPS_PER_CELL
+    out["roofline"] = {"bound": "valu", "kernel": "k_sw forward pass", "achieved": ach / 1e12,
+                       "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T lane-ops/s", "frac": ach / VALU_PEAK_LANE_OPS,
+                       "ops_per_cell": SW_OPS_PER_CELL}
+    if do_cpu:
+        import oracle
+        s = min(1000, n)
+        t = time.perf_counter()
+        exp = [oracle.sw_local(refs[k], reads[k]) for k in range(s)]
+        cdt = time.perf_counter() - t
+        out["parity_sample_ok"] = all(res[k] == exp[k] for k in range(s))
+        out["cpu_baseline"] = {"value": s / cdt, "unit": "alignments/s", "cores": 1, "kind": "port",
+                               "sample": f"first {s} pairs, oracle/ibwa_oracle.c"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,6 +372,7 @@ def main():
     ap.add_argument("--exact-reads", type=int, default=10_000_000)
     ap.add_argument("--exact-steps", type=int, default=5)
     ap.add_argument("--sa2pos", type=int, default=1, help="also time SA->coordinate of every read's first hit")
+    ap.add_argument("--sw-leg", type=int, default=200_000, help="SW mate-rescue pairs for extra.sw_leg (0: off)")
     ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
     ap.add_argument("--shards", type=int, default=1,
                     help="single process: align the reads of ranks 0..K-1 as one batch (checks the sharded path)")
@@ -360,6 +426,7 @@ def main():
     tb = time.perf_counter()
     eng.build_index(codes, sa_intv=32)  # the sampled SA too (bwa index's .sa/.rsa), for the sa2pos leg
     build_s = time.perf_counter() - tb
+    sw_pairs = make_sw_pairs(codes, args.sw_leg) if args.sw_leg and rank == 0 and world == 1 else None
     del codes
     log(f"index built on device in {build_s:.1f} s")
     for kv in args.opt:
@@ -457,6 +524,11 @@ def main():
                                   "touches_sample": f"first {tch.size} reads, oracle/ibwa_oracle.c touch counter"}
         if args.sa2pos and n_aln is not None:
             extra["sa2pos"] = sa2pos_leg(eng, lns, n_aln, alns)
+        if sw_pairs is not None:
+            ts = time.perf_counter()
+            extra["sw_leg"] = sw_leg(eng, sw_pairs[0], sw_pairs[1], do_cpu)
+            del sw_pairs
+            log(f"sw leg {time.perf_counter()-ts:.1f} s: {extra['sw_leg']}")
         if args.exact_leg and world == 1 and not exact_cfg:
             del seq, off, lns
             te = time.perf_counter()

@@ -361,6 +361,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_coop") c->gap_coop = value != 0;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
   else if (k == "coop_pool_gb" && value > 0 && value <= 256) c->coop_pool_gb = (int)value;
+  else if (k == "sw_stop" && value >= 0 && value <= 2) c->sw_stop_after = (int)value;  // SW phase timing
   else return fail(IBWA_EINVAL, "unknown option %s", k.c_str());
   return 0;
 }
