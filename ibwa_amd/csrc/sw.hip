@@ -25,7 +25,9 @@ namespace {
 constexpr int Q = 26, R = 9, QR = Q + R, BAND = 50, MAXSC = 11;
 constexpr int STRIP = 32;  // forward-pass columns held in registers
 constexpr int RCHUNK = 16;  // reverse-pass cells whose loads are issued together
-constexpr int GCH = 8;      // global-fill cells whose loads are issued together
+constexpr int GS = 16;      // global-fill columns held in registers (strip width; 32: 296 VGPRs)
+// traceback bytes per row: whole strips, so a strip's junk columns past len1 stay in their row
+__host__ __device__ inline uint32_t sw_tb_width(int max_len1) { return (uint32_t)((max_len1 + GS) / GS * GS); }
 constexpr int NEG_INF = -1073741823;  // MINOR_INF (stdaln.h:84)
 constexpr int FM = 0, FI = 1, FD = 2;  // FROM_M / FROM_I / FROM_D
 
@@ -44,11 +46,14 @@ __device__ __forceinline__ int sm(uint32_t x, uint32_t y) {
 struct Lane {
   uint32_t *w;   // lane-minor words: element e of lane at w[e * 64 + lane]
   uint32_t *wv;  // this lane's lane-major words
-  uint8_t *tb;   // this wave's traceback bytes, element e at tb[e * 64 + lane]
+  uint8_t *tb;   // this wave's traceback bytes: dword e / 4 of lane at tb[(e / 4 * 64 + lane) * 4]
   int lane;
   __device__ __forceinline__ uint32_t &u(uint32_t e) const { return w[(uint64_t)e * 64 + lane]; }
   __device__ __forceinline__ uint32_t &v(uint32_t e) const { return wv[e]; }
-  __device__ __forceinline__ uint8_t &t(uint32_t e) const { return tb[(uint64_t)e * 64 + lane]; }
+  __device__ __forceinline__ uint8_t &t(uint32_t e) const { return tb[((uint64_t)(e >> 2) * 64 + lane) * 4 + (e & 3)]; }
+  __device__ __forceinline__ uint32_t &tw(uint32_t w) const {
+    return reinterpret_cast<uint32_t *>(tb)[(uint64_t)w * 64 + lane];
+  }
 };
 
 // banded global alignment (aln_global_core, stdaln.c:345-525).  gap_end < 0 (the local core's
@@ -57,119 +62,144 @@ struct Lane {
 // row 0's deletions, cell 0's insertions, the last cell's insertion of a row clipped at len1,
 // and every deletion of the last row (stdaln.c:392-470).
 // seq1 = a[0..n1) along i (FROM_D steps i), seq2 = b[0..n2) along j (FROM_I steps j).
-// Rows are written generically: row j covers lo(j)..hi(j) with lo = 0 while j <= b2 (cell 0 takes
-// an I from above) and j - b2 after (a -inf boundary cell); the last cell takes an I from above only
-// when the band was clipped at len1 (j + b1 - 1 > len1) -- the union of the reference's part 1-3 rows.
-// Returns the score; the path is traced into the CIGAR (reversed) and start/end coordinates.
-__device__ int global_fill(const Lane &L, uint32_t eM, uint32_t eI, uint32_t eD, uint32_t eT, uint32_t t_w,
-                           const uint8_t *a, int n1, const uint8_t *b, int n2, int band, int gap_end, uint32_t *cig,
-                           int cap, int &n_cig, int &path_len, int &si, int &sj) {
+// Row j covers lo(j)..hi(j) with lo = 0 while j <= b2 (cell 0 takes an I from above) and j - b2
+// after (a -inf boundary cell); the last cell takes an I from above only when the band was
+// clipped at len1 (j + b1 - 1 > len1) -- the union of the reference's part 1-3 rows.
+//
+// Strip-mined like the forward pass: GS columns at a time for every row whose band meets them,
+// the strip's M / I / D of the row above in registers, (M, I, D) of the strip's last column per
+// row through scratch (eB) for the next strip, the traceback bytes of 4 cells in one dword.  A
+// row's cells outside its band compute junk that no in-band cell reads (an in-band cell reads
+// (j-1, i-1), (j-1, i) and (j, i-1), all inside row j-1's / row j's written range, except the
+// above of an unclipped last cell, which the I rule ignores), and the junk traceback bytes lie
+// off every path.  Returns the score; the path is traced into the CIGAR (reversed) and the
+// start / end coordinates.
+__device__ int global_fill(const Lane &L, uint32_t eB, uint32_t eT, uint32_t t_w, const uint8_t *a, int n1,
+                           const uint8_t *b, int n2, int band, int gap_end, uint32_t *cig, int cap, int &n_cig,
+                           int &path_len, int &si, int &sj) {
   const int RE = gap_end >= 0 ? gap_end : R;  // extension penalty of the set_end_* cells
   int b1, b2;
   if (n1 > n2) { b1 = n1 - n2 + band; b2 = band; } else { b1 = band; b2 = n2 - n1 + band; }
   if (b1 > n1) b1 = n1;
   if (b2 > n2) b2 = n2;
-  // two rows of {M, I, D} at eM/eI/eD + parity * (n1 + 1)
-  auto M = [&](int par, int i) -> uint32_t & { return L.u(eM + par * (n1 + 1) + i); };
-  auto I = [&](int par, int i) -> uint32_t & { return L.u(eI + par * (n1 + 1) + i); };
-  auto D = [&](int par, int i) -> uint32_t & { return L.u(eD + par * (n1 + 1) + i); };
   auto T = [&](int j, int i) -> uint8_t & { return L.t(eT + (uint32_t)j * t_w + i); };
-  // row 0
-  M(0, 0) = 0;
-  I(0, 0) = (uint32_t)NEG_INF;
-  D(0, 0) = (uint32_t)NEG_INF;
-  {
-    int pm = 0, pd = NEG_INF;
-    for (int i = 1; i < b1; ++i) {
-      int d;
-      uint8_t tt;
-      if (pm - Q > pd) { d = pm - Q - RE; tt = FM; } else { d = pd - RE; tt = FD; }
-      M(0, i) = (uint32_t)NEG_INF;
-      I(0, i) = (uint32_t)NEG_INF;
-      D(0, i) = (uint32_t)d;
-      T(0, i) = (uint8_t)(tt << 4);
-      pm = NEG_INF;
-      pd = d;
+  // row 0: M(0,0) = 0, D(0,i) = -Q - i*RE for 0 < i < b1 (FROM_M at i = 1, FROM_D after)
+  for (int i = 1; i < b1; ++i) T(0, i) = (uint8_t)((i == 1 ? FM : FD) << 4);
+  auto row0 = [&](int i, int &m, int &iv, int &d) __attribute__((always_inline)) {
+    m = i == 0 ? 0 : NEG_INF;
+    iv = NEG_INF;
+    d = i == 0 ? NEG_INF : -Q - i * RE;
+  };
+  int fm = 0, fi = 0, fd = 0;  // M / I / D of (n2, n1)
+  for (int i0 = 0; i0 <= n1; i0 += GS) {
+    int Mc[GS], Ic[GS], Dc[GS];  // the row above, columns i0 .. i0+GS-1
+    uint32_t c6[GS / 4];         // 6 * column code (N: 24), 8 bits each
+#pragma unroll
+    for (int k = 0; k < GS / 4; ++k) c6[k] = 0;
+#pragma unroll
+    for (int k = 0; k < GS; ++k) {
+      row0(i0 + k, Mc[k], Ic[k], Dc[k]);
+      const int i = i0 + k;
+      const uint32_t ca = i >= 1 ? a[(i <= n1 ? i : n1) - 1] : 0u;
+      c6[k >> 2] |= (ca > 4 ? 24u : ca * 6u) << (8 * (k & 3));
     }
-  }
-  for (int j = 1; j <= n2; ++j) {
-    const int cur = j & 1, prv = cur ^ 1;
-    const int lo = j <= b2 ? 0 : j - b2;
-    const int hi = j + b1 - 1 < n1 ? j + b1 - 1 : n1;
-    const uint32_t cb = b[j - 1];
-    int lm, li, ld;  // left cell (j, i-1)
-    if (j <= b2) {
-      const int um = (int)M(prv, 0), ui = (int)I(prv, 0);
-      uint8_t tt;
-      int iv;
-      if (um - Q > ui) { iv = um - Q - RE; tt = FM; } else { iv = ui - RE; tt = FI; }
-      M(cur, 0) = (uint32_t)NEG_INF;
-      I(cur, 0) = (uint32_t)iv;
-      D(cur, 0) = (uint32_t)NEG_INF;
-      T(j, 0) = (uint8_t)(tt << 2);
-      lm = NEG_INF; li = iv; ld = NEG_INF;
+    const bool more = i0 + GS <= n1;  // a strip follows: keep the last column per row
+    const int jlo = i0 - b1 + 1 > 1 ? i0 - b1 + 1 : 1;
+    const int jhi = i0 + GS - 1 + b2 < n2 ? i0 + GS - 1 + b2 : n2;
+    int dgm, dgi, dgd;  // (j-1, i0-1)
+    if (i0 == 0) {
+      dgm = dgi = dgd = NEG_INF;
+    } else if (jlo == 1) {
+      row0(i0 - 1, dgm, dgi, dgd);
     } else {
-      M(cur, lo) = I(cur, lo) = D(cur, lo) = (uint32_t)NEG_INF;
-      lm = li = ld = NEG_INF;
+      dgm = (int)L.u(eB + 3 * (jlo - 1));
+      dgi = (int)L.u(eB + 3 * (jlo - 1) + 1);
+      dgd = (int)L.u(eB + 3 * (jlo - 1) + 2);
     }
-    // diagonal cell (j-1, i-1) starts at column lo
-    int dm = (int)M(prv, lo), di = (int)I(prv, lo), dd = (int)D(prv, lo);
-    // GCH cells at a time: the row above's values and the codes of the chunk are loaded together
-    // before its cells are computed and stored (a cell stores into row `cur` only)
-    for (int i0 = lo + 1; i0 <= hi; i0 += GCH) {
-      int um_[GCH], ui_[GCH], ud_[GCH];
-      uint32_t ca_[GCH];
-#pragma unroll
-      for (int q = 0; q < GCH; ++q) {
-        const int i = i0 + q <= hi ? i0 + q : hi;
-        um_[q] = (int)M(prv, i);
-        ui_[q] = (int)I(prv, i);
-        ud_[q] = (int)D(prv, i);
-        ca_[q] = a[i - 1];
+    for (int j = jlo; j <= jhi; ++j) {
+      const int lo = j <= b2 ? 0 : j - b2;
+      const int hi = j + b1 - 1 < n1 ? j + b1 - 1 : n1;
+      const bool clipped = j + b1 - 1 > n1;
+      const int rd = j == n2 ? RE : R;
+      const uint32_t cb = b[j - 1];
+      // the row's score profile: 6-bit field 6*ca = sm(cb, ca) + 32
+      const uint32_t rp = cb > 3 ? 19u * 0x1041041u : 13u * 0x41041u + (19u << 24) + (30u << (6 * cb));
+      int lm = NEG_INF, li = NEG_INF, ld = NEG_INF;  // (j, i0-1)
+      if (i0 > 0) {
+        lm = (int)L.u(eB + 3 * j);
+        li = (int)L.u(eB + 3 * j + 1);
+        ld = (int)L.u(eB + 3 * j + 2);
       }
+      int dm = dgm, di = dgi, dd = dgd;
+      dgm = lm; dgi = li; dgd = ld;
+      uint32_t tw = 0;
 #pragma unroll
-      for (int q = 0; q < GCH; ++q) {
-        const int i = i0 + q;
-        if (i > hi) break;
-        const int sc = sm(cb, ca_[q]);
+      for (int k = 0; k < GS; ++k) {
+        const int i = i0 + k;
+        const int um = Mc[k], ui = Ic[k], ud = Dc[k];
         int m, iv, dv;
-        uint8_t tm, ti, td;
-        // set_M (stdaln.c:271-287)
-        if (dm >= di) {
-          if (dm >= dd) { m = dm + sc; tm = FM; } else { m = dd + sc; tm = FD; }
+        uint32_t tt;
+        if (k == 0 && i0 == 0) {
+          // cell 0: an I from above (set_end_I) while j <= b2; outside the band after
+          const int x = um - Q;
+          const bool c = x > ui;
+          iv = (c ? x : ui) - RE;
+          m = dv = NEG_INF;
+          tt = (c ? (uint32_t)FM : (uint32_t)FI) << 2;
+          if (lo > 0) iv = NEG_INF;
         } else {
-          if (di > dd) { m = di + sc; tm = FI; } else { m = dd + sc; tm = FD; }
+          // set_M (stdaln.c:271-287) from the diagonal
+          const int sc = (int)__builtin_amdgcn_ubfe(rp, (c6[k >> 2] >> (8 * (k & 3))) & 255u, 6) - 32;
+          const bool c1 = dm >= di;
+          const int b1v = c1 ? dm : di;
+          const bool keep = b1v > dd || (c1 && b1v == dd);
+          m = (keep ? b1v : dd) + sc;
+          const uint32_t tm = keep ? (c1 ? (uint32_t)FM : (uint32_t)FI) : (uint32_t)FD;
+          // set_I from above; the last cell only when the band was clipped at len1 (set_end_I)
+          const bool inner = i < hi;
+          const int x = um - Q;
+          const bool ci = x > ui;
+          iv = (ci ? x : ui) - (inner ? R : RE);
+          uint32_t ti = ci ? (uint32_t)FM : (uint32_t)FI;
+          if (!(inner || clipped)) {
+            iv = NEG_INF;
+            ti = FM;
+          }
+          // set_D from the left (set_end_D on the last row)
+          const int y = lm - Q;
+          const bool cd = y > ld;
+          dv = (cd ? y : ld) - rd;
+          const uint32_t td = cd ? (uint32_t)FM : (uint32_t)FD;
+          tt = tm | ti << 2 | td << 4;
+          if (i == lo) m = iv = dv = NEG_INF;  // the -inf boundary cell of a row past b2
         }
-        // above cell (j-1, i)
-        const int um = um_[q], ui = ui_[q], ud = ud_[q];
-        // set_I from above; the last cell only when the band was clipped at len1 (set_end_I)
-        if (i < hi || j + b1 - 1 > n1) {
-          const int ri = i < hi ? R : RE;
-          if (um - Q > ui) { iv = um - Q - ri; ti = FM; } else { iv = ui - ri; ti = FI; }
-        } else {
-          iv = NEG_INF;
-          ti = FM;
+        tw |= tt << (8 * (k & 3));
+        if ((k & 3) == 3) {
+          L.tw((eT + (uint32_t)j * t_w + (uint32_t)(i - 3)) >> 2) = tw;
+          tw = 0;
         }
-        // set_D from the left (set_end_D on the last row)
-        const int rd = j == n2 ? RE : R;
-        if (lm - Q > ld) { dv = lm - Q - rd; td = FM; } else { dv = ld - rd; td = FD; }
-        M(cur, i) = (uint32_t)m;
-        I(cur, i) = (uint32_t)iv;
-        D(cur, i) = (uint32_t)dv;
-        T(j, i) = (uint8_t)(tm | ti << 2 | td << 4);
+        Mc[k] = m; Ic[k] = iv; Dc[k] = dv;
         lm = m; li = iv; ld = dv;
         dm = um; di = ui; dd = ud;
       }
+      if (more) {
+        L.u(eB + 3 * j) = (uint32_t)lm;
+        L.u(eB + 3 * j + 1) = (uint32_t)li;
+        L.u(eB + 3 * j + 2) = (uint32_t)ld;
+      }
     }
-    (void)li;
+    if (!more) {  // the strip of column n1; its last row was n2
+#pragma unroll
+      for (int k = 0; k < GS; ++k)
+        if (i0 + k == n1) { fm = Mc[k]; fi = Ic[k]; fd = Dc[k]; }
+    }
   }
   // traceback from (n1, n2) (stdaln.c:487-514); ops emitted end -> start, run-length encoded
-  const int par = n2 & 1;
-  int best = (int)M(par, n1), ctype = FM;
+  int best = fm, ctype = FM;
   uint8_t cell = T(n2, n1);
   int type = cell & 3;
-  if ((int)I(par, n1) > best) { best = (int)I(par, n1); type = (cell >> 2) & 3; ctype = FI; }
-  if ((int)D(par, n1) > best) { best = (int)D(par, n1); type = (cell >> 4) & 3; ctype = FD; }
+  if (fi > best) { best = fi; type = (cell >> 2) & 3; ctype = FI; }
+  if (fd > best) { best = fd; type = (cell >> 4) & 3; ctype = FD; }
   int i = n1, j = n2, n = 0;
   n_cig = 0;
   auto emit = [&](int op) {
@@ -269,11 +299,12 @@ __device__ __forceinline__ void fwd_strip(const Lane &L, uint32_t eREF, uint32_t
 __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counter) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  // lane-minor elements: ref4[(l1+31)/32*4], the strip boundaries H / F per row, two rows each of
-  // M / I / D for the global fill; lane-major: eh[0..l1+1] (sw_words_per_lane in total)
+  // lane-minor elements: ref4[(l1+31)/32*4], the forward pass's strip boundaries H / F per row, the
+  // global fill's (M, I, D) per row; lane-major: eh[0..l1+1] (sw_words_per_lane in total)
   const uint32_t eREF = 0, eBH = eREF + (A.max_len1 + 31) / 32 * 4, eBF = eBH + A.max_len2 + 1;
-  const uint32_t eM = eBF + A.max_len2 + 1, eI = eM + 2 * (A.max_len1 + 1), eD = eI + 2 * (A.max_len1 + 1);
-  const uint32_t nminor = eD + 2 * (A.max_len1 + 1);
+  const uint32_t eB = eBF + A.max_len2 + 1;  // the global fill's (M, I, D) per row at a strip's end
+  const uint32_t nminor = eB + 3 * (A.max_len2 + 1);
+  const uint32_t t_w = sw_tb_width(A.max_len1);
   const uint32_t eEH = 0, nmajor = A.max_len1 + 2;
   Lane L;
   L.w = A.scratch + wave * A.words_per_lane * 64;
@@ -304,7 +335,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
       score = 0;
       if (n1 > 0 && n2 > 0) {
         int si = 0, sj = 0;
-        score = global_fill(L, eM, eI, eD, 0, (uint32_t)A.max_len1 + 1, a, n1, b, n2, A.global_band, A.gap_end, cig,
+        score = global_fill(L, eB, 0, t_w, a, n1, b, n2, A.global_band, A.gap_end, cig,
                             A.cigar_cap, n_cig, path_len, si, sj);
         for (int k = 0; k < n_cig / 2; ++k) {
           const uint32_t t = cig[k];
@@ -397,7 +428,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
         const int n1s = end_i - start_i + 1, n2s = end_j - start_j + 1;
         int score_g = 0, si = 0, sj = 0;
         for (int bw = BAND;; bw <<= 1) {
-          score_g = global_fill(L, eM, eI, eD, 0, (uint32_t)A.max_len1 + 1, a + start_i - 1, n1s, b + start_j - 1, n2s,
+          score_g = global_fill(L, eB, 0, t_w, a + start_i - 1, n1s, b + start_j - 1, n2s,
                                 bw, -1, cig, A.cigar_cap, n_cig, path_len, si, sj);
           if (score_g == score_r || score_f == score_g) break;
           if (bw > span) break;
@@ -430,12 +461,11 @@ hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks,
 }
 
 uint64_t sw_words_per_lane(int max_len1, int max_len2) {
-  return (uint64_t)(max_len1 + 2) + (uint64_t)(max_len1 + 31) / 32 * 4 + 6ull * (uint64_t)(max_len1 + 1) +
-         2ull * (uint64_t)(max_len2 + 1);
+  return (uint64_t)(max_len1 + 2) + (uint64_t)(max_len1 + 31) / 32 * 4 + 5ull * (uint64_t)(max_len2 + 1);
 }
 
 uint64_t sw_tb_per_lane(int max_len1, int max_len2) {
-  return (uint64_t)(max_len1 + 1) * (uint64_t)(max_len2 + 1);
+  return (uint64_t)sw_tb_width(max_len1) * (uint64_t)(max_len2 + 1);
 }
 
 }  // namespace ibwa
