@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
   const uint32_t eB = eBF + A.max_len2 + 1;  // the global fill's (M, I, D) per row at a strip's end
   const uint32_t nminor = eB + 3 * (A.max_len2 + 1);
   const uint32_t t_w = sw_tb_width(A.max_len1);
-  const uint32_t eEH = 0, nmajor = A.max_len1 + 2;
+  const uint32_t eEH = 0, eSPARE = A.max_len1 + 1, nmajor = A.max_len1 + 2;
   Lane L;
   L.w = A.scratch + wave * A.words_per_lane * 64;
   L.wv = L.w + (uint64_t)nminor * 64 + (uint64_t)lane * nmajor;
@@ -372,47 +372,56 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
         if (end <= 0) end = 0;
         for (int j = end_j - 1; j != 0; --j) {
           const uint32_t cb = b[j - 1];
+          // the row's score profile: 6-bit field 6*ca = sm(cb, ca) + 32
+          const uint32_t rp = cb > 3 ? 19u * 0x1041041u : 13u * 0x41041u + (19u << 24) + (30u << (6 * cb));
           int last_h = 0, f = 0, i = start;
           bool found = false;
           int nxt = (int)L.v(eEH + i + 1);  // eh[i+1] of the row below (old value)
-          // cells start, start-1, ..., end+1 (start > end always), RCHUNK at a time: the
+          // cells start, start-1, ..., end+1 (start > end >= 0 always), RCHUNK at a time: the
           // chunk's old eh values and codes are loaded together before its cells are updated
-          // (a cell writes eh[i+1] only, so all loaded values are still the row below's)
-          while (i != end && i > 0 && !found) {  // i > 0: memory guard, never binding
+          // (a cell writes eh[i+1] only, so all loaded values are still the row below's).  Branch
+          // free: a cell past the row's end (or after the start was found) computes junk, changes
+          // no state and stores to the spare word eh[l1 + 1], which nothing reads.
+          while (i > end && !found) {
             int ab[RCHUNK];
             uint32_t cd[RCHUNK];
 #pragma unroll
             for (int k = 0; k < RCHUNK; ++k) {
               const int ik = i - k;
-              const bool ok = ik > end && ik > 0;
-              ab[k] = ok ? (int)L.v(eEH + ik) : 0;
-              cd[k] = ok ? a[ik - 1] : 0u;
+              const bool ok = ik > end;
+              ab[k] = (int)L.v(ok ? eEH + ik : eSPARE);
+              cd[k] = a[ok ? ik - 1 : 0];
             }
+            int ii = i;
 #pragma unroll
             for (int k = 0; k < RCHUNK; ++k) {
-              if (i != end && i > 0 && !found) {
-                int h = (nxt >> 16) + sm(cb, cd[k]);
-                if (h < 0) h = 0;
-                if (last_h > 0) {
-                  f = (f > last_h - Q) ? f - R : last_h - QR;
-                  if (h < f) h = f;
-                }
-                const int above = ab[k] >> 16, e_old = nxt & 0xffff;
-                int e = (e_old > above - Q) ? e_old - R : above - QR;
-                if (e < 0) e = 0;
-                if (h < e) h = e;
-                L.v(eEH + i + 1) = (uint32_t)last_h << 16 | (uint32_t)e;
+              const bool act = i - k > end && !found;
+              const uint32_t ca = cd[k] > 4 ? 24u : cd[k] * 6u;
+              const int hd = (nxt >> 16) + (int)__builtin_amdgcn_ubfe(rp, ca, 6) - 32;
+              const int fn = max(f - R, last_h - QR);
+              const bool lp = last_h > 0;
+              const int fc = lp ? fn : f, fm = lp ? fn : 0;
+              const int above = ab[k] >> 16, e_old = nxt & 0xffff;
+              const int e = max(max(e_old - R, above - QR), 0);
+              const int h = max(max(hd, fm), e);  // >= 0: e is
+              L.v(act ? eEH + (uint32_t)(i - k + 1) : eSPARE) = (uint32_t)last_h << 16 | (uint32_t)e;
+              const bool upd = act && score_r < h;
+              if (act) {
+                f = fc;
                 last_h = h;
-                if (score_r < h) {
-                  score_r = h; start_i = i; start_j = j;
-                  if (score_r - QR == score_f) found = true;  // the start: stop here (j = 1; break)
-                }
-                if (!found) {
-                  nxt = ab[k];
-                  --i;
-                }
+              }
+              if (upd) {
+                score_r = h;
+                start_i = i - k;
+                start_j = j;
+              }
+              found = found || (upd && h - QR == score_f);  // the start: stop here (j = 1; break)
+              if (act && !found) {
+                nxt = ab[k];
+                ii = i - k - 1;
               }
             }
+            i = ii;
           }
           if (found) j = 1;
           L.v(eEH + i + 1) = (uint32_t)last_h << 16;
