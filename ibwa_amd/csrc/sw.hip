@@ -28,6 +28,8 @@ constexpr int RCHUNK = 16;  // reverse-pass cells whose loads are issued togethe
 constexpr int GS = 16;      // global-fill columns held in registers (strip width; 32: 296 VGPRs)
 // traceback bytes per row: whole strips, so a strip's junk columns past len1 stay in their row
 __host__ __device__ inline uint32_t sw_tb_width(int max_len1) { return (uint32_t)((max_len1 + GS) / GS * GS); }
+// the reverse pass's eh row per lane: eh[0 .. l1+1] in whole 64 B blocks (its 16-word block accesses)
+__host__ __device__ inline uint32_t sw_eh_words(int max_len1) { return (uint32_t)((max_len1 + 2 + 15) / 16 * 16); }
 constexpr int NEG_INF = -1073741823;  // MINOR_INF (stdaln.h:84)
 constexpr int FM = 0, FI = 1, FD = 2;  // FROM_M / FROM_I / FROM_D
 
@@ -50,6 +52,7 @@ struct Lane {
   int lane;
   __device__ __forceinline__ uint32_t &u(uint32_t e) const { return w[(uint64_t)e * 64 + lane]; }
   __device__ __forceinline__ uint32_t &v(uint32_t e) const { return wv[e]; }
+  __device__ __forceinline__ uint4 &v4(uint32_t e4) const { return reinterpret_cast<uint4 *>(wv)[e4]; }
   __device__ __forceinline__ uint8_t &t(uint32_t e) const { return tb[((uint64_t)(e >> 2) * 64 + lane) * 4 + (e & 3)]; }
   __device__ __forceinline__ uint32_t &tw(uint32_t w) const {
     return reinterpret_cast<uint32_t *>(tb)[(uint64_t)w * 64 + lane];
@@ -305,7 +308,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
   const uint32_t eB = eBF + A.max_len2 + 1;  // the global fill's (M, I, D) per row at a strip's end
   const uint32_t nminor = eB + 3 * (A.max_len2 + 1);
   const uint32_t t_w = sw_tb_width(A.max_len1);
-  const uint32_t eEH = 0, eSPARE = A.max_len1 + 1, nmajor = A.max_len1 + 2;
+  const uint32_t eEH = 0, nmajor = sw_eh_words(A.max_len1);
   Lane L;
   L.w = A.scratch + wave * A.words_per_lane * 64;
   L.wv = L.w + (uint64_t)nminor * 64 + (uint64_t)lane * nmajor;
@@ -377,34 +380,47 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
           int last_h = 0, f = 0, i = start;
           bool found = false;
           int nxt = (int)L.v(eEH + i + 1);  // eh[i+1] of the row below (old value)
-          // cells start, start-1, ..., end+1 (start > end >= 0 always), RCHUNK at a time: the
-          // chunk's old eh values and codes are loaded together before its cells are updated
-          // (a cell writes eh[i+1] only, so all loaded values are still the row below's).  Branch
-          // free: a cell past the row's end (or after the start was found) computes junk, changes
-          // no state and stores to the spare word eh[l1 + 1], which nothing reads.
+          // cells start, start-1, ..., end+1 (start > end >= 0 always) by aligned 16-word blocks of
+          // the eh row: block q = eh[16q .. 16q+15] is loaded (4 x 16 B) before its cells are
+          // updated (a cell writes eh[i+1] only, and cells go down, so every loaded value is still
+          // the row below's) and stored back whole: cells outside [end+1, i], or after the start
+          // was found, keep their word; cell 16q+15 writes the next block's first word.  The
+          // block's reference codes are three packed words of the forward pass's eREF.
           while (i > end && !found) {
-            int ab[RCHUNK];
-            uint32_t cd[RCHUNK];
+            const int q = i >> 4;
+            int blk[16];
 #pragma unroll
-            for (int k = 0; k < RCHUNK; ++k) {
-              const int ik = i - k;
-              const bool ok = ik > end;
-              ab[k] = (int)L.v(ok ? eEH + ik : eSPARE);
-              cd[k] = a[ok ? ik - 1 : 0];
+            for (int x = 0; x < 4; ++x) {
+              const uint4 v = L.v4((uint32_t)q * 4 + x);
+              blk[4 * x] = (int)v.x; blk[4 * x + 1] = (int)v.y; blk[4 * x + 2] = (int)v.z; blk[4 * x + 3] = (int)v.w;
             }
+            const uint32_t r0 = q > 0 ? L.u(eREF + 2 * q - 1) : 0u, r1 = L.u(eREF + 2 * q), r2 = L.u(eREF + 2 * q + 1);
+            uint32_t out[16];
+            out[0] = (uint32_t)blk[0];
+            uint32_t top = 0;
+            bool top_act = false;
             int ii = i;
 #pragma unroll
-            for (int k = 0; k < RCHUNK; ++k) {
-              const bool act = i - k > end && !found;
-              const uint32_t ca = cd[k] > 4 ? 24u : cd[k] * 6u;
-              const int hd = (nxt >> 16) + (int)__builtin_amdgcn_ubfe(rp, ca, 6) - 32;
+            for (int m = 15; m >= 0; --m) {
+              const int ik = 16 * q + m;
+              const bool act = ik <= i && ik > end && !found;
+              const int nx = m == 15 ? nxt : blk[m + 1];
+              const uint32_t code = m == 0 ? r0 >> 28 : m <= 8 ? (r1 >> (4 * (m - 1))) & 15u : (r2 >> (4 * (m - 9))) & 15u;
+              const uint32_t ca = (code < 4u ? code : 4u) * 6u;
+              const int hd = (nx >> 16) + (int)__builtin_amdgcn_ubfe(rp, ca, 6) - 32;
               const int fn = max(f - R, last_h - QR);
               const bool lp = last_h > 0;
               const int fc = lp ? fn : f, fm = lp ? fn : 0;
-              const int above = ab[k] >> 16, e_old = nxt & 0xffff;
+              const int above = blk[m] >> 16, e_old = nx & 0xffff;
               const int e = max(max(e_old - R, above - QR), 0);
               const int h = max(max(hd, fm), e);  // >= 0: e is
-              L.v(act ? eEH + (uint32_t)(i - k + 1) : eSPARE) = (uint32_t)last_h << 16 | (uint32_t)e;
+              const uint32_t val = (uint32_t)last_h << 16 | (uint32_t)e;
+              if (m < 15) {
+                out[m + 1] = act ? val : (uint32_t)blk[m + 1];
+              } else {
+                top = val;
+                top_act = act;
+              }
               const bool upd = act && score_r < h;
               if (act) {
                 f = fc;
@@ -412,15 +428,17 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
               }
               if (upd) {
                 score_r = h;
-                start_i = i - k;
+                start_i = ik;
                 start_j = j;
               }
               found = found || (upd && h - QR == score_f);  // the start: stop here (j = 1; break)
-              if (act && !found) {
-                nxt = ab[k];
-                ii = i - k - 1;
-              }
+              if (act && !found) ii = ik - 1;
             }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+              L.v4((uint32_t)q * 4 + x) = make_uint4(out[4 * x], out[4 * x + 1], out[4 * x + 2], out[4 * x + 3]);
+            if (top_act) L.v(eEH + (uint32_t)(16 * q + 16)) = top;
+            nxt = blk[0];
             i = ii;
           }
           if (found) j = 1;
@@ -470,7 +488,7 @@ hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks,
 }
 
 uint64_t sw_words_per_lane(int max_len1, int max_len2) {
-  return (uint64_t)(max_len1 + 2) + (uint64_t)(max_len1 + 31) / 32 * 4 + 5ull * (uint64_t)(max_len2 + 1);
+  return (uint64_t)sw_eh_words(max_len1) + (uint64_t)(max_len1 + 31) / 32 * 4 + 5ull * (uint64_t)(max_len2 + 1);
 }
 
 uint64_t sw_tb_per_lane(int max_len1, int max_len2) {
