@@ -4,15 +4,15 @@
 // followed by aln_global_core (stdaln.c:345-525, gap_end = -1) for the path and
 // aln_path2cigar32 (stdaln.c:1010-1040) for the CIGAR.
 //
-// One alignment per lane, persistent grid with per-wave claiming.  The DP
-// vectors (packed h<<16|e of the local passes, the M/I/D rows of the global
-// fill) and the traceback bytes live in per-lane HBM/L2 scratch interleaved
-// lane-minor inside each wave, so a wave's accesses at the same column are
-// one contiguous 256 B (or 64 B) segment; the reference window is re-packed 8
-// codes per word so the forward pass loads one word per 8 cells.  The local
-// passes are integer VALU work (roofline: VALU, cells/s); the 32000-point
-// rebasing of the reference (stdaln.c:581-598) is unreachable because the
-// host rejects min(len1, len2) * 11 > 32000.
+// One alignment per lane, persistent grid with per-wave claiming.  The forward
+// pass and the global fill are strip-mined (a strip's columns of the row above in
+// registers, one boundary per row through scratch); the reverse pass walks its
+// lane-major eh row by aligned 16-word blocks; all three are branch free per cell.
+// Scratch that the lanes touch in step (strip boundaries, packed reference codes,
+// traceback bytes) is interleaved lane-minor inside each wave, so a wave's access
+// is one contiguous segment.  The passes are integer VALU work (roofline: VALU,
+// cells/s); the 32000-point rebasing of the reference (stdaln.c:581-598) is
+// unreachable because the host rejects min(len1, len2) * 11 > 32000.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -24,7 +24,6 @@ namespace {
 
 constexpr int Q = 26, R = 9, QR = Q + R, BAND = 50, MAXSC = 11;
 constexpr int STRIP = 32;  // forward-pass columns held in registers
-constexpr int RCHUNK = 16;  // reverse-pass cells whose loads are issued together
 constexpr int GS = 16;      // global-fill columns held in registers (strip width; 32: 296 VGPRs)
 // traceback bytes per row: whole strips, so a strip's junk columns past len1 stay in their row
 __host__ __device__ inline uint32_t sw_tb_width(int max_len1) { return (uint32_t)((max_len1 + GS) / GS * GS); }
