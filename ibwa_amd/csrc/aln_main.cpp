@@ -16,6 +16,7 @@
 #include <zlib.h>
 
 #include <chrono>
+#include <functional>
 #include <algorithm>
 #include <string>
 #include <thread>
@@ -29,6 +30,7 @@
 namespace {
 
 using ibwa_cli::BamReader;
+using ibwa_cli::FastqBulk;
 using ibwa_cli::SeqReader;
 
 const int kBatch = 0x40000;  // bwtaln.c:193
@@ -64,49 +66,116 @@ struct Batch {
   int64_t n() const { return (int64_t)len.size(); }
 };
 
-// bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input, bwa_read_bam (:89-143) for BAM.
-// Returns 1 with a batch, 0 at the end of the input, -1 on a truncated or corrupt record.
-template <class Reader>
-int read_batch(Reader &rd, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
-  b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0;
-  const bool bam = std::is_same<Reader, BamReader>::value;
-  const bool is_64 = !bam && (mode & IBWA_MODE_IL13);
-  const int l_bc = bam ? 0 : (int)((unsigned)mode >> 24);  // no barcode for BAM (bwaseqio.c:156)
-  if (((unsigned)mode >> 24) > 15) {
-    fprintf(stderr, "[bwa_read_seq] the maximum barcode length is 15.\n");
-    return -1;
-  }
-  int l = 0;
-  while ((int)b.len.size() < kSub && (l = rd.read()) >= 0) {
-    std::string &s = rd.seq, &q = rd.qual;
-    if (is_64 && !q.empty())
-      for (auto &ch : q) ch = (char)(ch - 31);
-    if (!bam && (int)s.size() <= l_bc) continue;  // bwaseqio.c:162 (not on the BAM path)
-    if (l_bc) {
-      s.erase(0, l_bc);
-      if (!q.empty()) q.erase(0, l_bc);
-    }
-    int len = (int)s.size(), full = len;
+// bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input, bwa_read_bam (:89-143) for BAM: one
+// read's barcode strip, -I, -q trimming and reverse into 2-bit codes.  Returns the stored length,
+// -1 for a read the reference skips (not longer than the barcode; not on the BAM path).
+struct ReadForm {
+  bool bam, is_64;
+  int l_bc, trim_qual;
+  // s / q: the record's sequence and quality (q may be null), l bytes each
+  int len_of(const char *s, const char *q, int l, long *n_trimmed, long *n_tot) const {
+    (void)s;
+    if (!bam && l <= l_bc) return -1;  // bwaseqio.c:162
+    const char *qq = q ? q + l_bc : nullptr;
+    int len = l - l_bc;
+    const int full = len;
     *n_tot += full;
-    if (!q.empty() && trim_qual >= 1) {  // bwa_trim_read (bwaseqio.c:74-87)
+    if (qq && trim_qual >= 1) {  // bwa_trim_read (bwaseqio.c:74-87)
       int sc = 0, mx = 0, max_l = len - 1;
       for (int p = len - 1; p >= kMinRdLen - 1; --p) {
-        sc += trim_qual - ((unsigned char)q[p] - 33);
+        const unsigned char c = is_64 ? (unsigned char)(char)(qq[p] - 31) : (unsigned char)qq[p];
+        sc += trim_qual - (c - 33);
         if (sc < 0) break;
         if (sc > mx) { mx = sc; max_l = p; }
       }
       len = max_l + 1;
       *n_trimmed += full - len;
     }
+    return len;
+  }
+  void put(const char *s, int len, uint8_t *d) const {
+    const char *ss = s + l_bc;
+    for (int j = 0; j < len; ++j) d[j] = nt4[(unsigned char)ss[len - 1 - j]];  // seq := reverse(read)
+  }
+};
+
+template <class Reader>
+int read_serial(Reader &rd, const ReadForm &f, Batch &b, long *n_trimmed, long *n_tot) {
+  int l = 0;
+  while ((int)b.len.size() < kSub && (l = rd.read()) >= 0) {
+    std::string &s = rd.seq, &q = rd.qual;
+    const int len = f.len_of(s.data(), q.empty() ? nullptr : q.data(), (int)s.size(), n_trimmed, n_tot);
+    if (len < 0) continue;
     const size_t o = b.seq.size();
     b.off.push_back(o);
     b.len.push_back((uint32_t)len);
     if (len > b.max_len) b.max_len = len;
     b.seq.resize(o + len);
-    uint8_t *d = b.seq.data() + o;
-    for (int j = 0; j < len; ++j) d[j] = nt4[(unsigned char)s[len - 1 - j]];  // seq := reverse(read)
+    f.put(s.data(), len, b.seq.data() + o);
   }
-  if (l == -2) {
+  return l == -2 ? -1 : 0;
+}
+
+// the records [i0, i1) of the bulk parser into b, in parallel (lengths, then bytes)
+void take_bulk(const FastqBulk &fb, size_t i0, size_t i1, const ReadForm &f, Batch &b, long *n_trimmed,
+               long *n_tot) {
+  const int64_t n = (int64_t)(i1 - i0);
+  std::vector<int> ln(n);
+  const int nt = std::max(1, std::min<int>(ibwa_sam::host_threads(), (int)(n / 4096) + 1));
+  std::vector<long> tr(nt, 0), to(nt, 0);
+  const char *base = fb.blk.data();
+  ibwa_sam::parallel_chunks(n, [&](int64_t lo, int64_t hi, int t) {
+    for (int64_t k = lo; k < hi; ++k) {
+      const FastqBulk::Rec &r = fb.recs[i0 + k];
+      ln[k] = f.len_of(base + r.s, base + r.q, (int)r.len, &tr[t], &to[t]);
+    }
+  }, nt);
+  for (int t = 0; t < nt; ++t) { *n_trimmed += tr[t]; *n_tot += to[t]; }
+  std::vector<uint64_t> off(n);
+  uint64_t o = b.seq.size();
+  for (int64_t k = 0; k < n; ++k) {
+    off[k] = o;
+    if (ln[k] >= 0) {
+      o += (uint64_t)ln[k];
+      b.off.push_back(off[k]);
+      b.len.push_back((uint32_t)ln[k]);
+      if (ln[k] > b.max_len) b.max_len = ln[k];
+    }
+  }
+  b.seq.resize(o);
+  ibwa_sam::parallel_chunks(n, [&](int64_t lo, int64_t hi, int) {
+    for (int64_t k = lo; k < hi; ++k)
+      if (ln[k] >= 0) f.put(base + fb.recs[i0 + k].s, ln[k], b.seq.data() + off[k]);
+  }, nt);
+}
+
+// Returns 1 with a batch, 0 at the end of the input, -1 on a truncated or corrupt record.
+template <class Reader>
+int read_batch(Reader &rd, FastqBulk *fb, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
+  b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0;
+  const bool bam = std::is_same<Reader, BamReader>::value;
+  const ReadForm f{bam, !bam && (mode & IBWA_MODE_IL13) != 0, bam ? 0 : (int)((unsigned)mode >> 24), trim_qual};
+  if (((unsigned)mode >> 24) > 15) {
+    fprintf(stderr, "[bwa_read_seq] the maximum barcode length is 15.\n");
+    return -1;
+  }
+  auto par = [](int nt, const std::function<void(int)> &g) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(g, t);
+    g(0);
+    for (auto &x : th) x.join();
+  };
+  // the bulk parser's records first (whole strict FASTQ records), then the serial reader
+  while (fb && (int)b.len.size() < kSub && fb->more(ibwa_sam::host_threads(), par)) {
+    // records the reference skips (barcode) are taken too: the batch is filled up to kSub kept reads
+    size_t i1 = fb->qi;
+    while ((int)b.len.size() < kSub && fb->qi < fb->recs.size()) {
+      i1 = std::min(fb->recs.size(), fb->qi + (size_t)(kSub - (int)b.len.size()));
+      take_bulk(*fb, fb->qi, i1, f, b, n_trimmed, n_tot);
+      fb->qi = i1;
+    }
+  }
+  if ((int)b.len.size() < kSub && read_serial(rd, f, b, n_trimmed, n_tot) < 0) {
     fprintf(stderr, "[ibwa-amd aln] truncated or corrupt input record after %zu reads of this batch\n", b.len.size());
     return -1;
   }
@@ -121,8 +190,8 @@ int batch_key(const ibwa_gap_opt_t &opt, int max_len) {
 // Up to kGroup batches with the same batch-level options into g; a batch whose options differ is
 // left in `carry` for the next group.  Returns the batches read (0 at the end), -1 on bad input.
 template <class Reader>
-int read_group(Reader &rd, const ibwa_gap_opt_t &opt, Batch &g, Batch &sub, Batch &carry, bool &has_carry,
-               long *n_trimmed, long *n_tot) {
+int read_group(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, Batch &g, Batch &sub, Batch &carry,
+               bool &has_carry, long *n_trimmed, long *n_tot) {
   g.seq.clear(); g.off.clear(); g.len.clear(); g.max_len = 0;
   int nb = 0, key = 0;
   auto append = [&](const Batch &x) {
@@ -139,7 +208,7 @@ int read_group(Reader &rd, const ibwa_gap_opt_t &opt, Batch &g, Batch &sub, Batc
     nb = 1;
   }
   while (nb < kGroup) {
-    const int r = read_batch(rd, opt.mode, opt.trim_qual, sub, n_trimmed, n_tot);
+    const int r = read_batch(rd, fb, opt.mode, opt.trim_qual, sub, n_trimmed, n_tot);
     if (r < 0) return -1;
     if (r == 0) break;
     const int k = batch_key(opt, sub.max_len);
@@ -189,7 +258,8 @@ int die(const char *what) {
 }  // namespace
 
 template <class Reader>
-int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out, int n_gpus);
+int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out,
+            int n_gpus);
 
 int samse_main(int argc, char *argv[]);  // samse_main.cpp
 int sampe_main(int argc, char *argv[]);  // sampe_main.cpp
@@ -241,18 +311,21 @@ int main(int argc, char *argv[]) {
       fprintf(stderr, "[ibwa-amd aln] cannot open %s as BAM\n", argv[first_arg + 1]);
       return 1;
     }
-    return run_aln(rd, opt, prefix, fn_out, n_gpus);
+    return run_aln(rd, nullptr, opt, prefix, fn_out, n_gpus);
   }
   SeqReader rd;
   if (!rd.open(argv[first_arg + 1])) {
     fprintf(stderr, "[ibwa-amd aln] cannot open %s\n", argv[first_arg + 1]);
     return 1;
   }
-  return run_aln(rd, opt, prefix, fn_out, n_gpus);
+  // IBWA_ALN_SERIAL_READ=1: the serial reader only (tests compare the two)
+  FastqBulk fb(rd);
+  return run_aln(rd, env_int("IBWA_ALN_SERIAL_READ", 0) ? nullptr : &fb, opt, prefix, fn_out, n_gpus);
 }
 
 template <class Reader>
-int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out, int n_gpus) {
+int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out,
+            int n_gpus) {
   FILE *out = fn_out ? fopen(fn_out, "wb") : stdout;
   if (!out) {
     fprintf(stderr, "[ibwa-amd aln] cannot write %s\n", fn_out);
@@ -277,7 +350,7 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
   bool has_carry = false;
   long n_trim = 0, n_tot = 0;
   int64_t tot_seqs = 0;
-  int have = read_group(rd, opt, cur, sub, carry, has_carry, &n_trim, &n_tot);
+  int have = read_group(rd, fb, opt, cur, sub, carry, has_carry, &n_trim, &n_tot);
   ph.mark("read");
   while (have > 0) {
     auto t0 = std::chrono::steady_clock::now();
@@ -307,7 +380,7 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
       });
     }
     // overlap: parse the next batch while the GPUs work
-    int more = read_group(rd, opt, nxt, sub, carry, has_carry, &n_trim, &n_tot);
+    int more = read_group(rd, fb, opt, nxt, sub, carry, has_carry, &n_trim, &n_tot);
     for (auto &t : th) t.join();
     for (int g = 0; g < n_gpus; ++g)
       if (g_rc[g]) return die("aln");
@@ -315,12 +388,22 @@ int run_aln(Reader &rd, const ibwa_gap_opt_t &opt, const std::string &prefix, co
     double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fprintf(stderr, "%.2f sec\n", sec);
     fprintf(stderr, "[bwa_aln_core] write to the disk... ");
-    for (int g = 0; g < n_gpus; ++g) {  // bwtaln.c:227-231, input order
+    for (int g = 0; g < n_gpus; ++g) {  // bwtaln.c:227-231, input order; one write per slice
       const ibwa_aln1_t *p = g_aln[g];
+      size_t bytes = 0;
+      for (int32_t k : g_naln[g]) bytes += 4 + (size_t)k * sizeof(ibwa_aln1_t);
+      std::vector<char> buf(bytes);
+      char *w = buf.data();
       for (int32_t k : g_naln[g]) {
-        fwrite(&k, 4, 1, out);
-        if (k) fwrite(p, sizeof(ibwa_aln1_t), k, out);
+        memcpy(w, &k, 4);
+        w += 4;
+        if (k) memcpy(w, p, (size_t)k * sizeof(ibwa_aln1_t));
+        w += (size_t)k * sizeof(ibwa_aln1_t);
         p += k;
+      }
+      if (bytes && fwrite(buf.data(), 1, bytes, out) != bytes) {
+        fprintf(stderr, "[ibwa-amd aln] write failed\n");
+        return 1;
       }
       ibwa_free(g_aln[g]);
     }

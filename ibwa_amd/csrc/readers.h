@@ -9,6 +9,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -39,8 +40,19 @@ struct SeqReader {
     if (!fill()) return -1;
     return (unsigned char)buf[begin++];
   }
+  // bytes handed back by FastqBulk when it stops (read before the rest of the stream)
+  std::vector<char> pending;
+  size_t pend_pos = 0;
   bool fill() {
     if (begin < end) return true;
+    if (pend_pos < pending.size()) {
+      const size_t n = std::min(buf.size(), pending.size() - pend_pos);
+      memcpy(buf.data(), pending.data() + pend_pos, n);
+      pend_pos += n;
+      begin = 0;
+      end = (int)n;
+      return true;
+    }
     if (eof) return false;
     end = gzread(fp, buf.data(), (unsigned)buf.size());
     begin = 0;
@@ -139,6 +151,168 @@ struct SeqReader {
     last_char = 0;
     if (seq.size() != qual.size()) return -2;
     return (int)seq.size();
+  }
+};
+
+// Strict 4-line FASTQ in bulk (aln's input in the common case).  Whole records -- "@header\n", a
+// line of sequence bytes (isgraph, none of '>', '+', '@'), a line starting with '+', a line of
+// quality bytes 33..127 exactly as long as the sequence -- are split and checked by several
+// threads over a large block.  On such a record kseq_read (SeqReader::read) returns exactly that
+// sequence and quality and stops right after the quality line's newline.  At the first record
+// of any other shape (FASTA, multi-line, CRLF, a short or long quality line, a truncated tail)
+// the rest of the input goes to the serial reader, whose state there -- after a record's last
+// byte, looking for the next '@' or '>' -- is the one kseq_read would be in.
+struct FastqBulk {
+  struct Rec {
+    uint64_t s, q;  // offsets of the sequence and quality lines in blk
+    uint32_t len;
+  };
+  SeqReader &rd;
+  struct Buf {  // raw bytes, not zero-filled, kept across blocks (no page faults after the first)
+    std::unique_ptr<char[]> p;
+    size_t cap = 0;
+    char *data() const { return p.get(); }
+    const char &operator[](size_t i) const { return p[i]; }
+  } blk;
+  size_t pos = 0, end = 0;  // unparsed bytes [pos, end)
+  bool eof = false;         // the stream is drained into blk
+  bool on = true;           // false from the first record the bulk parser does not take
+  bool handed = false;      // the rest went to the serial reader
+  std::vector<Rec> recs;    // parsed, not yet taken
+  size_t qi = 0;
+  size_t chunk = (size_t)32 << 20;
+  explicit FastqBulk(SeqReader &r) : rd(r) {}
+
+  // bytes of the record at p (> 0), 0 when the data ends inside it, -1 when it is not strict
+  static int64_t rec_at(const char *p, const char *e, bool at_eof, const char *base, Rec &r) {
+    const uint8_t *cls = SeqReader::seq_class();
+    if (p >= e) return 0;
+    if (*p != '@') return -1;
+    const char *h = (const char *)memchr(p, '\n', (size_t)(e - p));
+    if (!h) return at_eof ? -1 : 0;
+    const char *sq = h + 1;
+    const char *se = (const char *)memchr(sq, '\n', (size_t)(e - sq));
+    if (!se) return at_eof ? -1 : 0;
+    const int64_t L = se - sq;
+    if (L < 1 || L > (1 << 24)) return -1;
+    for (const char *x = sq; x < se; ++x)
+      if (cls[(uint8_t)*x] != 1) return -1;
+    const char *pl = se + 1;
+    if (pl >= e) return at_eof ? -1 : 0;
+    if (*pl != '+') return -1;
+    const char *pe = (const char *)memchr(pl, '\n', (size_t)(e - pl));
+    if (!pe) return at_eof ? -1 : 0;
+    const char *u = pe + 1;
+    if (e - u < L + 1) return at_eof ? -1 : 0;
+    for (int64_t k = 0; k < L; ++k) {
+      const uint8_t c = (uint8_t)u[k];
+      if (c < 33 || c > 127) return -1;
+    }
+    if (u[L] != '\n') return -1;
+    r.s = (uint64_t)(sq - base);
+    r.q = (uint64_t)(u - base);
+    r.len = (uint32_t)L;
+    return u + L + 1 - p;
+  }
+  // all taken: keep the unparsed tail, read the next block of the stream behind it
+  void refill() {
+    recs.clear();
+    qi = 0;
+    const size_t tail = end - pos;
+    if (blk.cap < tail + chunk) {
+      std::unique_ptr<char[]> q(new char[tail + chunk]);
+      if (tail) memcpy(q.get(), blk.data() + pos, tail);
+      blk.p.swap(q);
+      blk.cap = tail + chunk;
+    } else if (pos) {
+      memmove(blk.data(), blk.data() + pos, tail);
+    }
+    pos = 0;
+    end = tail;
+    if (eof) return;
+    while (end < blk.cap) {
+      const size_t want = std::min<size_t>(blk.cap - end, (size_t)1 << 26);
+      const int got = gzread(rd.fp, blk.data() + end, (unsigned)want);
+      if (got <= 0) { eof = true; break; }
+      end += (size_t)got;
+    }
+  }
+  // the records of [pos, end), nt threads from record starts spread over the block
+  template <class Par>
+  void parse(int nt, Par par) {
+    const char *base = blk.data(), *p0 = base + pos, *e = base + end;
+    const size_t n = end - pos;
+    if (!n) return;
+    nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, n >> 20));
+    std::vector<const char *> st(nt + 1, e);
+    st[0] = p0;
+    for (int t = 1; t < nt; ++t) {  // the first strict record at a line start after the split point
+      const char *x = p0 + n * t / nt;
+      st[t] = e;
+      while (x < e) {
+        const char *nl = (const char *)memchr(x, '\n', (size_t)(e - x));
+        if (!nl) break;
+        x = nl + 1;
+        Rec r;
+        if (x < e && *x == '@' && rec_at(x, e, eof, base, r) > 0) { st[t] = x; break; }
+      }
+      if (st[t] < st[t - 1]) st[t] = st[t - 1];
+    }
+    std::vector<std::vector<Rec>> out(nt);
+    std::vector<const char *> stop(nt);
+    std::vector<int> code(nt, 1);  // 1: reached the next start, 0: data ends, -1: not strict
+    par(nt, [&](int t) {
+      const char *p = st[t];
+      while (p < st[t + 1]) {
+        Rec r;
+        const int64_t k = rec_at(p, e, eof, base, r);
+        if (k <= 0) { code[t] = (int)k; break; }
+        out[t].push_back(r);
+        p += k;
+      }
+      stop[t] = p;
+    });
+    const char *P = p0;
+    for (int t = 0; t < nt; ++t) {
+      if (st[t] != P) break;  // the previous segment did not end on this start: parse on from P next time
+      recs.insert(recs.end(), out[t].begin(), out[t].end());
+      P = stop[t];
+      if (code[t] < 0) { on = false; break; }
+      if (code[t] == 0 || P != st[t + 1]) break;
+    }
+    pos = (size_t)(P - base);
+  }
+  // the serial reader continues at pos
+  void handoff() {
+    on = false;
+    handed = true;
+    rd.pending.assign(blk.data() + pos, blk.data() + end);
+    rd.pend_pos = 0;
+    rd.begin = rd.end = 0;
+    rd.last_char = 0;
+    rd.eof = false;  // pending first, then the stream (at its end if eof)
+    blk.p.reset();
+    blk.cap = 0;
+    pos = end = 0;
+  }
+  // records available to take (parses the next block when all are taken); false: bulk is over
+  template <class Par>
+  bool more(int nt, Par par) {
+    if (qi < recs.size()) return true;
+    if (!on) {
+      if (!handed) handoff();
+      return false;
+    }
+    for (int tries = 0; tries < 4 && on; ++tries) {
+      refill();
+      parse(nt, par);
+      if (!recs.empty()) return true;
+      if (eof && pos == end) return false;  // the input is exhausted in bulk
+      if (on && !eof) { chunk *= 2; continue; }  // a record longer than the block
+      break;
+    }
+    handoff();
+    return false;
   }
 };
 
