@@ -46,6 +46,7 @@ int env_int(const char *k, int dflt) {
 const int kGroup = env_int("IBWA_ALN_GROUP", 16);
 const int kSub = env_int("IBWA_ALN_SUBBATCH", kBatch);
 const int kMinRdLen = 35;    // BWA_MIN_RDLEN, bwtaln.h:23
+const bool kTimes = env_int("IBWA_ALN_TIMES", 0) != 0;
 
 unsigned char nt4[256];
 
@@ -346,12 +347,19 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   fwrite(&opt, sizeof opt, 1, out);  // bwtaln.c:192
   ph.mark("load index");
 
+  // the index's device structures for these options are built while the first reads are parsed
+  std::vector<int> prep_rc(n_gpus, 0);
+  std::vector<std::thread> prep;
+  for (int g = 0; g < n_gpus; ++g) prep.emplace_back([&, g]() { prep_rc[g] = ibwa_ctx_prepare(ctx[g], &opt); });
   Batch cur, nxt, sub, carry;
   bool has_carry = false;
   long n_trim = 0, n_tot = 0;
   int64_t tot_seqs = 0;
   int have = read_group(rd, fb, opt, cur, sub, carry, has_carry, &n_trim, &n_tot);
-  ph.mark("read");
+  for (auto &t : prep) t.join();
+  for (int g = 0; g < n_gpus; ++g)
+    if (prep_rc[g]) return die("prepare the index");
+  ph.mark("read (index prepared meanwhile)");
   while (have > 0) {
     auto t0 = std::chrono::steady_clock::now();
     const int64_t n = cur.n();
@@ -375,8 +383,22 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         const uint64_t base = b < e ? cur.off[b] : 0;
         std::vector<uint64_t> off(cur.off.begin() + b, cur.off.begin() + e);
         for (auto &x : off) x -= base;
-        g_rc[g] = ibwa_aln_batch(ctx[g], &opt, e - b, cur.seq.data() + base, off.data(), cur.len.data() + b,
-                                 cur.max_len, g_naln[g].data(), &g_aln[g], &tot);
+        // ibwa_aln_batch, in its three steps (IBWA_ALN_TIMES=1: their wall times per slice)
+        auto c0 = std::chrono::steady_clock::now();
+        int rc = ibwa_batch_stage(ctx[g], e - b, cur.seq.data() + base, off.data(), cur.len.data() + b);
+        auto c1 = std::chrono::steady_clock::now();
+        if (!rc) rc = ibwa_batch_run(ctx[g], &opt, cur.max_len);
+        auto c2 = std::chrono::steady_clock::now();
+        if (!rc) rc = ibwa_batch_fetch(ctx[g], g_naln[g].data(), &g_aln[g], &tot);
+        auto c3 = std::chrono::steady_clock::now();
+        g_rc[g] = rc;
+        if (kTimes) {
+          auto ms = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+            return std::chrono::duration<double, std::milli>(y - x).count();
+          };
+          fprintf(stderr, "[ibwa-amd aln] slice %d: %lld reads, stage %.1f run %.1f fetch %.1f ms\n", g,
+                  (long long)(e - b), ms(c0, c1), ms(c1, c2), ms(c2, c3));
+        }
       });
     }
     // overlap: parse the next batch while the GPUs work

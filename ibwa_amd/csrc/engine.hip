@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -1400,26 +1401,46 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
   // theirs into d_naln / d_aln)
   std::vector<int32_t> cnt(c->h_naln.begin(), c->h_naln.end());
   for (size_t j = 0; j < c->patch_ids.size(); ++j) cnt[c->patch_ids[j]] = (int32_t)c->patch_alns[j].size();
-  int64_t tot = 0;
-  for (int64_t i = 0; i < n; ++i) tot += cnt[i];
+  std::vector<int64_t> at(n + 1, 0);  // output offset of read i
+  for (int64_t i = 0; i < n; ++i) at[i + 1] = at[i] + cnt[i];
+  const int64_t tot = at[n];
   ibwa_aln1_t *o = (ibwa_aln1_t *)malloc(std::max<int64_t>(tot, 1) * sizeof(ibwa_aln1_t));
   if (!o) return fail(IBWA_EINVAL, "out of host memory");
-  size_t rj = 0;
-  int64_t p = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const uint4 *src;
-    if (rj < c->patch_ids.size() && c->patch_ids[rj] == i) {
-      src = c->patch_alns[rj].data();
-      ++rj;
-    } else {
-      src = c->h_aln.data() + (c->stream_out ? (cnt[i] ? c->h_aoff[i] : 0) : i * cap);
+  // the records in input order, gathered by several host threads (patch_ids ascending)
+  auto gather = [&](int64_t lo, int64_t hi) {
+    size_t rj = std::lower_bound(c->patch_ids.begin(), c->patch_ids.end(), lo) - c->patch_ids.begin();
+    for (int64_t i = lo; i < hi; ++i) {
+      const uint4 *src;
+      if (rj < c->patch_ids.size() && c->patch_ids[rj] == i) {
+        src = c->patch_alns[rj].data();
+        ++rj;
+      } else {
+        src = c->h_aln.data() + (c->stream_out ? (cnt[i] ? c->h_aoff[i] : 0) : i * cap);
+      }
+      memcpy(o + at[i], src, (size_t)cnt[i] * 16);
+      if (n_aln) n_aln[i] = cnt[i];
     }
-    memcpy(o + p, src, (size_t)cnt[i] * 16);
-    p += cnt[i];
-    if (n_aln) n_aln[i] = cnt[i];
+  };
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, n / 65536));
+  if (nt == 1) {
+    gather(0, n);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(gather, n * t / nt, n * (t + 1) / nt);
+    for (auto &x : th) x.join();
   }
   *aln = o;
   if (n_total) *n_total = tot;
+  return 0;
+}
+
+int ibwa_ctx_prepare(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt) {
+  if (!c) return fail(IBWA_EINVAL, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  if (int rc = ensure_kmer(c)) return rc;
+  // the condition of ibwa_batch_run's exact path
+  if (opt && c->exact_path && !(opt->fnr > 0.0f) && opt->max_diff == 0 && opt->max_entries >= 2)
+    if (int rc = ensure_jump(c)) return rc;
   return 0;
 }
 

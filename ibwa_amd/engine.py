@@ -94,6 +94,7 @@ CAPI = {
     "ibwa_ctx_load_sa": (_i, [_vp, _i, _u32, _vp, _u64]),
     "ibwa_ctx_load_sa_file": (_i, [_vp, _i, c.c_char_p]),
     "ibwa_ctx_expand_sa": (_i, [_vp]),
+    "ibwa_ctx_prepare": (_i, [_vp, c.POINTER(GapOpt)]),
     "ibwa_ctx_derive_sa": (_i, [_vp, _u32]),
     "ibwa_sa2pos": (_i, [_vp, _i64, _vp, _vp, _vp, _u64, _vp]),
     "ibwa_ctx_build_index": (_i, [_vp, _vp, _u64, _i]),
@@ -293,6 +294,10 @@ class Engine:
 
     def expand_sa(self):
         _chk(lib().ibwa_ctx_expand_sa(self.h))
+
+    def prepare(self, opt):
+        """The per-index device structures the first run with `opt` needs (ibwa_ctx_prepare)."""
+        _chk(lib().ibwa_ctx_prepare(self.h, c.byref(opt)))
 
     def sa2pos(self, strand, k, lens, offset=0):
         """bwtdb_sa2seq (dbset.c:240-246) for arrays of hits -> uint64 positions."""

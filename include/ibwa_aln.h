@@ -106,6 +106,16 @@ int ibwa_batch_stage(ibwa_ctx_t *ctx, int64_t n_seqs, const uint8_t *seq, const 
 int ibwa_batch_run(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt, int batch_max_len);
 int ibwa_batch_fetch(ibwa_ctx_t *ctx, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total);
 
+/*
+ * ibwa_ctx_prepare: the per-index device structures the first ibwa_batch_run with
+ * these options would otherwise build on the way (bit-plane Occ layouts and
+ * K-mer tables; for max_diff = 0 the exact path's full SA / ISA / 2-bit text,
+ * derived from a loaded BWT).  Optional: a caller (the CLI) runs it right
+ * after loading the index, while it parses its first reads.  No reference
+ * counterpart (bwt_restore_bwt, bwtaln.c:184-189, is the load it follows).
+ */
+int ibwa_ctx_prepare(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt);
+
 typedef struct {
 	double ms_width;       /* width kernel (exact path: its read-packing pre-pass), HIP events */
 	double ms_search;      /* search kernel (first pass; exact path: k_exact alone) */

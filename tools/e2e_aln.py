@@ -80,13 +80,16 @@ def write_fastq(path, reads, first=0, count=None):
 
 def run(argv, timeout=1800):
     t = time.perf_counter()
-    r = subprocess.run(argv, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout)
+    r = subprocess.run(argv, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout,
+                       env=dict(os.environ, IBWA_ALN_TIMES="1"))
     dt = time.perf_counter() - t
     err = r.stderr.decode(errors="replace")
     if r.returncode != 0:
         raise RuntimeError(f"{argv[:2]} failed ({r.returncode}): {err[-1500:]}")
     phases = {}
     for ln in err.splitlines():
+        if "slice" in ln or " sec" in ln:
+            log("  cli:", ln.strip())
         if "wall s:" in ln:
             for name, v in re.findall(r"([a-z][a-z .()]*?) (\d+\.\d+)", ln.split("wall s:", 1)[1]):
                 phases[name.strip()] = float(v)
