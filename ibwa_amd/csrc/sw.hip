@@ -254,13 +254,23 @@ __device__ __forceinline__ void fwd_strip(const Lane &L, uint32_t eREF, uint32_t
     Hc[k] = Ec[k] = 0;
   }
   int diag_next = 0;  // H[j-1][i0-1]
+  // the next row's read code and strip boundary are loaded one row ahead (row j+1's boundary
+  // words are written by the previous strip; this strip writes row j's at the end of row j)
+  uint32_t cb_n = b[0];
+  int bh_n = 0, bf_n = 0;
+  if (i0 > 1) {
+    bh_n = (int)L.u(eBH + 1);
+    bf_n = (int)L.u(eBF + 1);
+  }
   for (int j = 1; j <= n2; ++j) {
-    uint32_t cb = b[j - 1];
-    cb = cb > 4 ? 24u : cb * 6u;
-    int last_h = 0, f = 0;  // H[j][i0-1] and the row's F state, from the previous strip
-    if (i0 > 1) {
-      last_h = (int)L.u(eBH + j);
-      f = (int)L.u(eBF + j);
+    const uint32_t cb = cb_n > 4 ? 24u : cb_n * 6u;
+    int last_h = bh_n, f = bf_n;  // H[j][i0-1] and the row's F state, from the previous strip
+    if (j < n2) {
+      cb_n = b[j];
+      if (i0 > 1) {
+        bh_n = (int)L.u(eBH + j + 1);
+        bf_n = (int)L.u(eBF + j + 1);
+      }
     }
     int diag = diag_next;
     diag_next = last_h;
