@@ -74,3 +74,24 @@ def test_cli_grouped_batches_equal_one_at_a_time(golden_dir, argv, tmp_path):
     one = run_cli_env(argv, golden_dir, reads, tmp_path, {"IBWA_ALN_SUBBATCH": "16", "IBWA_ALN_GROUP": "1"}, "a.sai")
     grp = run_cli_env(argv, golden_dir, reads, tmp_path, {"IBWA_ALN_SUBBATCH": "16", "IBWA_ALN_GROUP": "4"}, "b.sai")
     assert one[64:] == grp[64:]
+
+
+@pytest.mark.parametrize("argv", [[], ["-q", "15"], ["-B", "4"], ["-I"]])
+def test_cli_bulk_parse_equals_serial(golden_dir, argv, tmp_path):
+    """The threaded FASTQ path (readers.h FastqBulk) and its hand-off to the serial reader: a file
+    whose strict 4-line records are followed by CRLF and multi-line records gives the .sai of
+    the serial reader alone (IBWA_ALN_SERIAL_READ=1), with the switch falling inside a batch."""
+    src = open(os.path.join(golden_dir, "reads_mixed.fq"), "rb").read().split(b"\n")
+    recs = [src[i:i + 4] for i in range(0, len(src) - 3, 4)]
+    head, mid, tail = recs[:len(recs) // 2], recs[len(recs) // 2:len(recs) // 2 + 40], recs[len(recs) // 2 + 40:]
+    text = b"".join(b"\n".join(r) + b"\n" for r in head)
+    text += b"".join(b"\r\n".join(r) + b"\r\n" for r in mid)  # CRLF: serial from here
+    for r in tail:  # sequence wrapped over two lines
+        s = r[1]
+        text += r[0] + b"\n" + s[:len(s) // 2] + b"\n" + s[len(s) // 2:] + b"\n" + r[2] + b"\n" + r[3] + b"\n"
+    fq = tmp_path / "mixed_irregular.fq"
+    fq.write_bytes(text)
+    env = {"IBWA_ALN_SUBBATCH": "96", "IBWA_ALN_GROUP": "3"}
+    bulk = run_cli_env(argv, golden_dir, str(fq), tmp_path, env, "bulk.sai")
+    ser = run_cli_env(argv, golden_dir, str(fq), tmp_path, dict(env, IBWA_ALN_SERIAL_READ="1"), "ser.sai")
+    assert len(bulk) > 64 and bulk[64:] == ser[64:]
