@@ -453,6 +453,7 @@ struct Sampe {
   PeOpt popt;
   ibwa_gap_opt_t gopt[2];
   std::vector<FILE *> fp_sai[2];  // per end, per reference
+  std::vector<ibwa_aln1_t> sai_tmp;
   Drand48 rnd;
   Isize last_ii;
   // bwtcache (bwtcache.c:27-45), one per reference: positions of an interval of >= 1000 rows,
@@ -474,11 +475,13 @@ struct Sampe {
       if (fread(&count, 4, 1, fp_sai[j][d]) != 1) continue;  // past the end: nothing
       const size_t o = v.size();
       v.resize(o + count);
+      sai_tmp.resize(count);  // the read's records in one read
+      if (count && fread(sai_tmp.data(), sizeof(ibwa_aln1_t), count, fp_sai[j][d]) != count) {
+        fprintf(stderr, "[ibwa-amd sampe] truncated .sai\n");
+        return false;
+      }
       for (uint32_t t = 0; t < count; ++t) {
-        if (fread(&v[o + t].aln, sizeof(ibwa_aln1_t), 1, fp_sai[j][d]) != 1) {
-          fprintf(stderr, "[ibwa-amd sampe] truncated .sai\n");
-          return false;
-        }
+        v[o + t].aln = sai_tmp[t];
         v[o + t].dbidx = (int)d;
       }
     }
@@ -1020,6 +1023,7 @@ int sampe_main(int argc, char *argv[]) {
     for (int d = 0; d < count; ++d) {
       const char *fn = j == 0 ? sais[d].first : sais[d].second;
       FILE *fp = fopen(fn, "rb");
+      if (fp) setvbuf(fp, nullptr, _IOFBF, 1 << 22);
       if (!fp || fread(&S.gopt[j], sizeof S.gopt[j], 1, fp) != 1) {
         fprintf(stderr, "[ibwa-amd sampe] cannot read the .sai header of %s\n", fn);
         return 1;
