@@ -174,15 +174,78 @@ __device__ __forceinline__ uint32_t rec_byte(uint2 a, uint2 b, uint32_t pa, uint
   return (a.y < clamp ? a.y : clamp) | ea << (nb - 1) | ((b.y < clamp ? b.y : clamp) | eb << (nb - 1)) << nb;
 }
 
+// One bwt_cal_width step (bwtaln.c:54-78) of a chain, with one-row intervals stepped from the
+// text: row k with k == l has the suffix at q = SA[k], BWT[k] = text[q-1], and stepping with c
+// stays on one row (suffix at q-1) exactly when q > 0 and text[q-1] == c; otherwise the interval
+// is empty and the reference resets it.  Mode 0: Occ steps; 1: the interval became one row at
+// the last step -- this step is an Occ step that also loads SA[k]; 2: text steps (suffix at t),
+// one 2-bit text word loaded per 16 steps.  Every mode issues its loads in the same round trip
+// as the other chain's and the other lanes' (the chains stay in lockstep).
+struct WChain {
+  uint32_t k, l, bid;
+  uint32_t mode, t, wi, w;  // text mode: suffix position, cached text word index and word
+};
+
+struct WLoad {
+  Fetch1 f;
+  uint32_t q, w;
+  bool tl;
+};
+
+// the step's loads (issued for both chains before either is consumed: one round trip)
+__device__ __forceinline__ void wchain_load(const IndexView &ix, const uint32_t *sa, const uint32_t *tx,
+                                            const WChain &h, uint32_t c, WLoad &x) {
+  fetch1(ix, h.k - 1, h.l, c & 3, c < 4 && h.mode != 2, x.f);
+  x.q = 0;
+  if (h.mode == 1) x.q = sa[h.k];
+  const uint32_t twi = (h.t - 1u) >> 4;
+  x.tl = h.mode == 2 && h.t > 0 && twi != h.wi;
+  x.w = h.w;
+  if (x.tl) x.w = tx[twi];
+}
+
+__device__ __forceinline__ void wchain_step(const IndexView &ix, bool jump, WChain &h, uint32_t c, const WLoad &x) {
+  if (h.mode == 2) {
+    if (x.tl) { h.w = x.w; h.wi = (h.t - 1u) >> 4; }
+    if (h.t > 0 && c < 4 && ((x.w >> (2 * ((h.t - 1u) & 15))) & 3u) == c) {
+      --h.t;  // still one row: k == l stays, width 1
+    } else {
+      h.k = 0; h.l = ix.seq_len; ++h.bid; h.mode = 0;
+    }
+    return;
+  }
+  bool reset = c > 3;
+  if (c < 4) {
+    uint32_t ok, ol;
+    occ2_from1(x.f, c, ok, ol);
+    h.k = l2of(ix, c) + ok + 1;
+    h.l = l2of(ix, c) + ol;
+    reset = h.k > h.l;
+  }
+  if (reset) { h.k = 0; h.l = ix.seq_len; ++h.bid; }
+  if (h.mode == 1) {
+    // the step from the one row with its suffix at q succeeded (suffix at q - 1) or emptied it
+    h.mode = reset ? 0u : 2u;
+    h.t = x.q - 1u;
+    h.wi = 0xFFFFFFFFu;
+  } else if (jump && !reset && h.k == h.l) {
+    h.mode = 1;
+  }
+}
+
 // two bwt_cal_width chains in lockstep (bwtaln.c:54-78): str on ixa -> wa, strand-1 str on
 // ixb -> wb.  The entries of 16 steps are kept in
 // registers and stored back to back (a lane's 128 B of widths leave in consecutive instructions,
 // so the L2 merges them into whole lines instead of 16 partial writes far apart).
+// With sa0/sa1 and tx0/tx1 (the exact path's full SA and 2-bit text per strand) one-row
+// intervals step from the text (wchain_step).
 __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView ixb, int L, const uint8_t *s, bool comp,
                                            uint2 *wa, uint2 *wb, uint32_t *lw = nullptr, RecOut *rec = nullptr,
-                                           uint32_t clamp = 0, int nb = 4, uint32_t *rd = nullptr) {
-  uint32_t ka = 0, la = ixa.seq_len, kb = 0, lb = ixb.seq_len;
-  uint32_t bida = 0, bidb = 0;
+                                           uint32_t clamp = 0, int nb = 4, uint32_t *rd = nullptr,
+                                           const uint32_t *sa0 = nullptr, const uint32_t *sa1 = nullptr,
+                                           const uint32_t *tx0 = nullptr, const uint32_t *tx1 = nullptr) {
+  WChain A{0u, ixa.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u};
+  WChain B{0u, ixb.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u};
   uint32_t lwa = 0, lwb = 0;  // sum of log2(width) over the positions (diagnostics)
   uint32_t pa = 0, pb = 0;    // previous positions' widths (record)
   for (int base = 0; base < L; base += 16) {
@@ -193,27 +256,15 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
       if (i < L) {
         uint32_t ca = s[i];
         uint32_t cb = strand_base(ca, 1, comp);
-        Fetch1 fa, fb;
-        fetch1(ixa, ka - 1, la, ca & 3, ca < 4, fa);
-        fetch1(ixb, kb - 1, lb, cb & 3, cb < 4, fb);
-        if (ca < 4) {
-          uint32_t ok, ol;
-          occ2_from1(fa, ca, ok, ol);
-          ka = l2of(ixa, ca) + ok + 1;
-          la = l2of(ixa, ca) + ol;
-        }
-        if (ka > la || ca > 3) { ka = 0; la = ixa.seq_len; ++bida; }
-        ba[t] = make_uint2(la - ka + 1, bida);
-        lwa += 31 - __builtin_clz(la - ka + 1);
-        if (cb < 4) {
-          uint32_t ok, ol;
-          occ2_from1(fb, cb, ok, ol);
-          kb = l2of(ixb, cb) + ok + 1;
-          lb = l2of(ixb, cb) + ol;
-        }
-        if (kb > lb || cb > 3) { kb = 0; lb = ixb.seq_len; ++bidb; }
-        bb[t] = make_uint2(lb - kb + 1, bidb);
-        lwb += 31 - __builtin_clz(lb - kb + 1);
+        WLoad xa, xb;
+        wchain_load(ixa, sa0, tx0, A, ca, xa);
+        wchain_load(ixb, sa1, tx1, B, cb, xb);
+        wchain_step(ixa, sa0 != nullptr, A, ca, xa);
+        wchain_step(ixb, sa1 != nullptr, B, cb, xb);
+        ba[t] = make_uint2(A.l - A.k + 1, A.bid);
+        lwa += 31 - __builtin_clz(A.l - A.k + 1);
+        bb[t] = make_uint2(B.l - B.k + 1, B.bid);
+        lwb += 31 - __builtin_clz(B.l - B.k + 1);
       }
     }
 #pragma unroll
@@ -235,14 +286,14 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
       if (rd) rd[base >> 4] = x;
     }
   }
-  wa[L] = make_uint2(0u, bida + 1);
-  wb[L] = make_uint2(0u, bidb + 1);
+  wa[L] = make_uint2(0u, A.bid + 1);
+  wb[L] = make_uint2(0u, B.bid + 1);
   if (rec) rec->put(rec_byte(wa[L], wb[L], pa, pb, L == 0, clamp, nb));
   if (lw) {
     lw[0] = lwa;
     lw[1] = lwb;
-    lw[2] = bida;
-    lw[3] = bidb;
+    lw[2] = A.bid;
+    lw[3] = B.bid;
   }
 }
 
@@ -253,6 +304,7 @@ __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
   const int L = (int)A.len[r];
   const uint8_t *s = A.seq + A.off[r];
   const bool comp = A.o.mode & MODE_COMPREAD;
+  const uint32_t *sa0 = A.jsa[0], *sa1 = A.jsa[1], *tx0 = A.jtxt[0], *tx1 = A.jtxt[1];
   uint2 *w0 = A.wbuf + (uint64_t)lane * A.wstride;
   uint2 *w1 = w0 + A.wlen1;
   uint2 *sw0 = w1 + A.wlen1;
@@ -281,16 +333,18 @@ __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
     const int md = A.o.fnr_pos ? (int)A.maxdiff_tab[L] : A.o.max_diff;
     rec[0] = (uint32_t)L | (nN < 255u ? nN : 255u) << 16 | (uint32_t)md << 24;
     RecOut ro{rec + 1 + A.cw_rw, 0u, 0u};
-    width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, &ro, (uint32_t)md + 1u, 4, rec + 1);
+    width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, &ro, (uint32_t)md + 1u, 4, rec + 1, sa0, sa1, tx0, tx1);
     while (ro.off < A.wlen1) ro.put(0u);  // positions past this read's length
     if (L > A.o.seed_len)
       width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1, nullptr, &ro,
-                 (uint32_t)A.o.max_seed_diff + 1u, 3);
+                 (uint32_t)A.o.max_seed_diff + 1u, 3, nullptr, sa0, sa1, tx0, tx1);
     ro.flush();
     return;
   }
-  width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1);
-  if (L > A.o.seed_len) width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1);
+  width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, nullptr, 0, 4, nullptr, sa0, sa1, tx0, tx1);
+  if (L > A.o.seed_len)
+    width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1, nullptr, nullptr, 0, 4,
+               nullptr, sa0, sa1, tx0, tx1);
 }
 
 __device__ __forceinline__ int int_log2(uint32_t v) {  // bwtgap.c:93-102

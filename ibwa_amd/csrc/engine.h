@@ -51,6 +51,10 @@ struct AlnArgs {
   // position the same with the bid clamped to max_seed_diff + 1 (2 bits + 1 bit per strand)
   uint32_t *cw;
   uint32_t cw_words, cw_rw;
+  // k_width's one-row steps from the text (full SA and 2-bit text per strand, as the exact
+  // path's jump); nullptr: every step reads the Occ blocks
+  const uint32_t *jsa[2];
+  const uint32_t *jtxt[2];
   AlnOpt o;
 };
 

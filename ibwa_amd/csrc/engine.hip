@@ -105,6 +105,7 @@ struct ibwa_ctx {
   bool jump_derived = false;  // jump arrays derived from a loaded BWT (ensure_jump), not built here
   int jump_derive = 1;        // option: derive them for a loaded index when HBM allows
   int exact_jump = 1;
+  int width_jump = 1;         // option: k_width steps one-row intervals from the text (2: derive SA / text for it)
   uint32_t sa_intv = 0;
   bool sa_loaded[2] = {false, false};  // sa_s[s] holds a sampled SA of the resident index
   bool sa_expanded = false;            // sa_full[0/1] derived from the sampled SA (ibwa_ctx_expand_sa)
@@ -357,6 +358,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
   else if (k == "jump_derive") c->jump_derive = value != 0;
+  else if (k == "width_jump" && value >= 0 && value <= 2) c->width_jump = (int)value;
   else if (k == "diag") c->diag = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
@@ -756,6 +758,15 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   A.wlen1 = (uint32_t)max_len + 1;
   A.wstride = 2ull * A.wlen1 + 2ull * ((uint64_t)std::max(opt->seed_len, 0) + 1);
   A.o = o;
+  // k_width's one-row steps from the text (1: when SA / text are resident, 2: derive them)
+  if (c->width_jump == 2 && !(c->exact_path && !o.fnr_pos && opt->max_diff == 0))
+    if (int rc = ensure_jump(c)) return rc;
+  if (c->width_jump && c->jump_ready) {
+    for (int s = 0; s < 2; ++s) {
+      A.jsa[s] = c->sa_full[s].as<uint32_t>();
+      A.jtxt[s] = c->txt2[s].as<uint32_t>();
+    }
+  }
 
   const bool exact_path = c->exact_path && !o.fnr_pos && opt->max_diff == 0 && opt->max_entries >= 2;
   c->stats.path = exact_path ? 1 : 0;

@@ -55,6 +55,31 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path, gappe
     assert not bad, bad
 
 
+@pytest.mark.parametrize("width_jump", [0, 2])
+def test_sai_goldens_width_jump(golden_dir, sai_manifest, gpu_engine, width_jump):
+    """k_width with (2: SA / text derived from the loaded BWT) and without (0) one-row steps from
+    the text: every gapped golden, in the first pass and (budget 1) through the heavy-read pass."""
+    bad = []
+    try:
+        gpu_engine.set_option("width_jump", width_jump)
+        for budget in (8000, 1):
+            gpu_engine.set_option("gap_iter_budget", budget)
+            for key, m in sorted(sai_manifest.items()):
+                if m["argv"] == ["-n", "0"]:
+                    continue
+                opt, _ = oracle.parse_aln_args(m["argv"])
+                recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+                seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+                n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+                exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+                if not oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), exp):
+                    bad.append(f"{key}:budget {budget}")
+    finally:
+        gpu_engine.set_option("width_jump", 1)
+        gpu_engine.set_option("gap_iter_budget", 8000)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("coop", [1, 0])
 def test_sai_goldens_heavy_pass(golden_dir, sai_manifest, gpu_engine, coop):
     """An iteration budget of 1 hands every gapped read to the heavy-read pass: the
