@@ -144,6 +144,9 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *                                  the exact path jump over a unique interval's remaining symbols
  *   "jump_derive" (0/1, default 1) for an index loaded from .bwt files, derive those arrays on
  *                                  the device from the BWT at the first -n 0 batch (HBM permitting)
+ *   "width_jump" (0/1/2, default 1) k_width steps one-row intervals from the 2-bit text
+ *                                  (1: when those arrays are resident; 2: derive them for a
+ *                                  gapped batch too; 0: Occ steps only) -- same widths
  *   "kmer_k" (-1 auto, 0 off, 1..16) K-mer interval table length
  *   "exact_blocks", "lanes_per_chunk"
  *   "gapped_v2" (0/1, default 1)   persistent gapped-search kernel (else the general kernels)
