@@ -493,7 +493,9 @@ def main():
                  "kernel_ms_per_step": {"k_width(first pass)": ms_w / launches, "k_gapped": ms_s / launches,
                                         "k_coop(+its widths)": ms_c / launches,
                                         "wide+general retry": (ms_r - ms_c) / launches},
-                 "host_cores": threads, "cpu_model": cpu_model()}
+                 "host_cores": threads, "cpu_model": cpu_model(),
+                 # digest of the sources libibwa_amd.so was built from (checked against this tree on load)
+                 "build_id": E.lib().ibwa_build_id().decode()}
         do_cpu = not args.no_cpu and world == 1
         n_aln = alns = None
         if do_cpu or args.sa2pos:

@@ -24,13 +24,48 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise NativeLibraryMissing(
                 f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
-        _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-        _declare(_lib)
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _declare(L)
+        if not os.environ.get("IBWA_LIB"):
+            check_build_id(L)
+        _lib = L
     return _lib
+
+
+def source_digest():
+    """The digest the Makefile bakes into ibwa_build_id(), from the sources in this tree
+    (None when the sources are not next to the library)."""
+    import glob
+    import hashlib
+    csrc = os.path.join(_HERE, "csrc")
+    inc = os.path.join(os.path.dirname(_HERE), "include")
+    if not os.path.isdir(csrc):
+        return None
+    files = sorted((f for pat in ("*.cpp", "*.h", "*.hip") for f in glob.glob(os.path.join(csrc, pat))),
+                   key=lambda f: os.path.basename(f).encode())
+    files += sorted(glob.glob(os.path.join(inc, "*.h")), key=lambda f: os.path.basename(f).encode())
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def check_build_id(L):
+    """Refuse a library built from other sources than the ones in this tree (a stale prebuilt
+    .so shipped to a GPU box)."""
+    want = source_digest()
+    got = L.ibwa_build_id().decode()
+    if want is not None and got != want:
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} was built from other sources (build id {got}, sources {want}); rebuild with "
+            "`python -c 'import __graft_entry__ as g; g.build()'`")
 
 
 def _declare(L):
     c = ctypes
+    L.ibwa_build_id.restype = c.c_char_p
+    L.ibwa_build_id.argtypes = []
     u64p = c.POINTER(c.c_uint64)
     L.ibwa_synth_grch37_lengths.restype = c.c_uint64
     L.ibwa_synth_grch37_lengths.argtypes = [c.c_uint64, c.c_uint64, u64p]

@@ -90,6 +90,7 @@ CAPI = {
     "ibwa_batch_retry_info": (_i, [_vp, _vp, _vp, _i64, c.POINTER(_i64)]),
     "ibwa_batch_diag": (_i, [_vp, _i, _vp, _u64]),
     "ibwa_ctx_set_option": (_i, [_vp, c.c_char_p, c.c_long]),
+    "ibwa_build_id": (c.c_char_p, []),
     "ibwa_occ4": (_i, [_vp, _i, _i64, _vp, _vp]),
     "ibwa_ctx_load_sa": (_i, [_vp, _i, _u32, _vp, _u64]),
     "ibwa_ctx_load_sa_file": (_i, [_vp, _i, c.c_char_p]),

@@ -159,6 +159,11 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
+/* The sources this library was built from: the first 16 hex digits of the SHA-256 of every
+ * ibwa_amd/csrc/{*.cpp,*.h,*.hip} followed by every include/*.h, each list in byte order of
+ * the file names (no reference counterpart; the Python loader refuses a stale build). */
+const char *ibwa_build_id(void);
+
 /*
  * The `aln` command line (bwa_aln's getopt loop, bwtaln.c:249-284; same option string and
  * semantics, plus -G INT = number of GPUs) into *opt, starting from gap_init_opt's defaults.

@@ -34,6 +34,12 @@ def test_binding_covers_header():
     assert hdr - compat <= set(CAPI), sorted(hdr - compat - set(CAPI))
 
 
+def test_build_id_matches_sources():
+    """The library reports the digest of the sources it was built from, and it is this tree's."""
+    L = _native.lib()
+    assert L.ibwa_build_id().decode() == _native.source_digest()
+
+
 def test_cpu_only_calls():
     from ibwa_amd import engine
     o = engine.default_opt()
