@@ -100,9 +100,14 @@ struct ReadForm {
   }
 };
 
+// A truncated last record (kseq_read's -2, kseq.h:186/:191, which only happens at the end of the
+// file; bam_read1's -2/-3 on BAM) ends the input like EOF does: bwa_read_seq's / bwa_read_bam's
+// loops (bwaseqio.c:159, :99) stop there and keep every read before it, and bwa_aln_core's next
+// read finds nothing.  The record itself is dropped, with a warning (stderr only).
 template <class Reader>
-int read_serial(Reader &rd, const ReadForm &f, Batch &b, long *n_trimmed, long *n_tot) {
+int read_serial(Reader &rd, const ReadForm &f, Batch &b, long *n_trimmed, long *n_tot, bool *eof) {
   int l = 0;
+  if (*eof) return 0;
   while ((int)b.len.size() < kSub && (l = rd.read()) >= 0) {
     std::string &s = rd.seq, &q = rd.qual;
     const int len = f.len_of(s.data(), q.empty() ? nullptr : q.data(), (int)s.size(), n_trimmed, n_tot);
@@ -114,7 +119,9 @@ int read_serial(Reader &rd, const ReadForm &f, Batch &b, long *n_trimmed, long *
     b.seq.resize(o + len);
     f.put(s.data(), len, b.seq.data() + o);
   }
-  return l == -2 ? -1 : 0;
+  if (l < -1) fprintf(stderr, "[ibwa-amd aln] warning: truncated last input record ignored\n");
+  if (l < 0) *eof = true;
+  return 0;
 }
 
 // the records [i0, i1) of the bulk parser into b, in parallel (lengths, then bytes)
@@ -150,9 +157,10 @@ void take_bulk(const FastqBulk &fb, size_t i0, size_t i1, const ReadForm &f, Bat
   }, nt);
 }
 
-// Returns 1 with a batch, 0 at the end of the input, -1 on a truncated or corrupt record.
+// Returns 1 with a batch, 0 at the end of the input, -1 on bad options.
 template <class Reader>
-int read_batch(Reader &rd, FastqBulk *fb, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot) {
+int read_batch(Reader &rd, FastqBulk *fb, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot,
+               bool *eof) {
   b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0;
   const bool bam = std::is_same<Reader, BamReader>::value;
   const ReadForm f{bam, !bam && (mode & IBWA_MODE_IL13) != 0, bam ? 0 : (int)((unsigned)mode >> 24), trim_qual};
@@ -176,10 +184,7 @@ int read_batch(Reader &rd, FastqBulk *fb, int mode, int trim_qual, Batch &b, lon
       fb->qi = i1;
     }
   }
-  if ((int)b.len.size() < kSub && read_serial(rd, f, b, n_trimmed, n_tot) < 0) {
-    fprintf(stderr, "[ibwa-amd aln] truncated or corrupt input record after %zu reads of this batch\n", b.len.size());
-    return -1;
-  }
+  if ((int)b.len.size() < kSub) read_serial(rd, f, b, n_trimmed, n_tot, eof);
   return b.len.empty() ? 0 : 1;
 }
 
@@ -192,7 +197,7 @@ int batch_key(const ibwa_gap_opt_t &opt, int max_len) {
 // left in `carry` for the next group.  Returns the batches read (0 at the end), -1 on bad input.
 template <class Reader>
 int read_group(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, Batch &g, Batch &sub, Batch &carry,
-               bool &has_carry, long *n_trimmed, long *n_tot) {
+               bool &has_carry, long *n_trimmed, long *n_tot, bool *eof) {
   g.seq.clear(); g.off.clear(); g.len.clear(); g.max_len = 0;
   int nb = 0, key = 0;
   auto append = [&](const Batch &x) {
@@ -209,7 +214,7 @@ int read_group(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, Batch &g, B
     nb = 1;
   }
   while (nb < kGroup) {
-    const int r = read_batch(rd, fb, opt.mode, opt.trim_qual, sub, n_trimmed, n_tot);
+    const int r = read_batch(rd, fb, opt.mode, opt.trim_qual, sub, n_trimmed, n_tot, eof);
     if (r < 0) return -1;
     if (r == 0) break;
     const int k = batch_key(opt, sub.max_len);
@@ -355,7 +360,8 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   bool has_carry = false;
   long n_trim = 0, n_tot = 0;
   int64_t tot_seqs = 0;
-  int have = read_group(rd, fb, opt, cur, sub, carry, has_carry, &n_trim, &n_tot);
+  bool eof = false;
+  int have = read_group(rd, fb, opt, cur, sub, carry, has_carry, &n_trim, &n_tot, &eof);
   for (auto &t : prep) t.join();
   for (int g = 0; g < n_gpus; ++g)
     if (prep_rc[g]) return die("prepare the index");
@@ -402,7 +408,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       });
     }
     // overlap: parse the next batch while the GPUs work
-    int more = read_group(rd, fb, opt, nxt, sub, carry, has_carry, &n_trim, &n_tot);
+    int more = read_group(rd, fb, opt, nxt, sub, carry, has_carry, &n_trim, &n_tot, &eof);
     for (auto &t : th) t.join();
     for (int g = 0; g < n_gpus; ++g)
       if (g_rc[g]) return die("aln");

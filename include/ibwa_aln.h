@@ -135,6 +135,8 @@ typedef struct {
 	double ms_coop;            /* its time (width + search), part of ms_retry */
 	double ms_sa2pos;          /* last ibwa_sa2pos kernel time */
 	int sa2pos_full;           /* 1: it gathered from a full SA, 0: it walked the sampled SA */
+	double ms_coop_width;      /* of ms_coop: the heavy reads' widths (k_width) */
+	double ms_coop_roots;      /* of ms_coop: their level 0 (k_coop_roots); the rest is k_coop */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 
@@ -159,8 +161,8 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
-/* The sources this library was built from: the first 16 hex digits of the SHA-256 of every
- * ibwa_amd/csrc/{*.cpp,*.h,*.hip} followed by every include/*.h, each list in byte order of
+/* The sources this library was built from: the first 16 hex digits of the SHA-256 of the
+ * ibwa_amd/csrc/ sources (cpp, h, hip) followed by the include/ headers, each list in byte order of
  * the file names (no reference counterpart; the Python loader refuses a stale build). */
 const char *ibwa_build_id(void);
 

@@ -78,6 +78,7 @@ def lib():
                                         c.POINTER(c.c_void_p), c.c_void_p]
         L.or_free.argtypes = [c.c_void_p]
         L.or_set_stats.argtypes = [c.c_void_p]
+        L.or_set_width_touches.argtypes = [c.c_void_p]
         L.or_exact_touches.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p, c.c_void_p,
                                        c.c_int, c.c_int, c.c_int, c.c_void_p]
         L.or_aln_local_core.restype = c.c_int
@@ -296,11 +297,16 @@ STATS_DTYPE = np.dtype([("pushes", "<u4"), ("pops", "<u4"), ("peak_entries", "<u
                         ("rounds_g4", "<u4"), ("rounds_g16", "<u4"), ("rounds_lvl", "<u4")])
 
 
-def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False, stats=None):
+def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False, stats=None, width_touches=None):
     """Run the restated bwa_cal_sa_reg_gap.  Returns (n_aln int32[n], alns ALN_DTYPE[...], touches).
-    `stats`: optional STATS_DTYPE[n] array filled with per-read search statistics."""
+    `stats`: optional STATS_DTYPE[n] array filled with per-read search statistics.
+    `width_touches`: optional uint32[n] array filled with the touches of each read's bwt_cal_width
+    calls (bwtaln.c:123-130) alone; touches - width_touches are bwt_match_gap's."""
     L = lib()
     n = len(lens)
+    if width_touches is not None:
+        assert width_touches.dtype == np.uint32 and width_touches.size >= n and width_touches.flags.c_contiguous
+        L.or_set_width_touches(ctypes.c_void_p(width_touches.ctypes.data))
     if stats is not None:
         assert stats.dtype == STATS_DTYPE and stats.size >= n and stats.flags.c_contiguous
         L.or_set_stats(ctypes.c_void_p(stats.ctypes.data))

@@ -308,6 +308,10 @@ typedef struct {
 } or_stats_t;
 static or_stats_t *g_stats_next; /* consumed by the next or_cal_sa_reg_gap call */
 void or_set_stats(or_stats_t *buf) { g_stats_next = buf; }
+/* per-read touches of the four bwt_cal_width calls alone (bwtaln.c:123-130; the rest of a read's
+ * touches are bwt_match_gap's), consumed by the next or_cal_sa_reg_gap call */
+static uint32_t *g_wtouch_next;
+void or_set_width_touches(uint32_t *buf) { g_wtouch_next = buf; }
 
 #define SCORE(m, o, e, p) ((m) * (p)->s_mm + (o) * (p)->s_gapo + (e) * (p)->s_gape)
 #define ST_M 0
@@ -675,7 +679,7 @@ typedef struct {
 	int max_len;
 	int32_t *n_aln;
 	or_aln1_t **per_read;
-	uint32_t *touches;
+	uint32_t *touches, *wtouches;
 	or_stats_t *stats;
 	int64_t next;  /* dynamic claim of THREAD_BLOCK reads (bwtaln.c:100-113) */
 	pthread_mutex_t lock;
@@ -721,6 +725,7 @@ static void *worker(void *data)
 				cal_width(B->bwt[0], opt->seed_len, seq[0] + (L - opt->seed_len), sw[0], &t);
 				cal_width(B->bwt[1], opt->seed_len, seq[1] + (L - opt->seed_len), sw[1], &t);
 			}
+			if (B->wtouches) B->wtouches[r] = t;
 			stack->pushes = stack->pops = stack->peak = stack->peak_bucket = 0;
 			match_gap(B->bwt, L, seq, w, L <= opt->seed_len ? 0 : sw, &local, &out, stack, &t);
 			B->n_aln[r] = out.n;
@@ -789,6 +794,8 @@ int64_t or_cal_sa_reg_gap(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_
 	B.n_aln = n_aln; B.touches = touches_out;
 	B.stats = g_stats_next;
 	g_stats_next = 0;
+	B.wtouches = g_wtouch_next;
+	g_wtouch_next = 0;
 	B.per_read = (or_aln1_t**)calloc(n_seqs > 0 ? n_seqs : 1, sizeof(or_aln1_t*));
 	pthread_mutex_init(&B.lock, 0);
 	for (i = 0; i < n_seqs; ++i) if ((int)len[i] > B.max_len) B.max_len = (int)len[i];

@@ -95,3 +95,16 @@ def test_cli_bulk_parse_equals_serial(golden_dir, argv, tmp_path):
     bulk = run_cli_env(argv, golden_dir, str(fq), tmp_path, env, "bulk.sai")
     ser = run_cli_env(argv, golden_dir, str(fq), tmp_path, dict(env, IBWA_ALN_SERIAL_READ="1"), "ser.sai")
     assert len(bulk) > 64 and bulk[64:] == ser[64:]
+
+
+@pytest.mark.parametrize("key", ["trunc_q.default", "trunc_q.n3o2e3", "trunc_p.default", "trunc_p.n3o2e3"])
+def test_cli_truncated_last_record(golden_dir, key, tmp_path):
+    """A FASTQ that ends inside its last record (kseq_read's -2, kseq.h:186/:191): the reference's
+    read loop stops there keeping every earlier read (bwaseqio.c:159) and aln exits 0; so does the
+    CLI, with the bulk parser and with the serial reader (tools/make_trunc_golden.py)."""
+    m = json.load(open(os.path.join(golden_dir, "trunc_manifest.json")))[key]
+    gold = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+    got = run_cli(m["argv"], golden_dir, m["reads"], tmp_path)
+    assert oracle.sai_body_equal(got, gold)
+    got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path, {"IBWA_ALN_SERIAL_READ": "1"}, "s.sai")
+    assert oracle.sai_body_equal(got, gold)
