@@ -76,7 +76,9 @@ def make_genome(scale_num, scale_den, seed, threads):
     return ascii_, codes, [int(x) for x in lens], int(n_amb)
 
 
-def make_reads(ascii_, lens, seed, n, ln, sub, indel, threads):
+def make_reads(ascii_, lens, seed, n, ln, sub, indel, threads, keep_raw=0):
+    """Synthetic reads, encoded as bwa_read_seq stores them (seq, offsets, lengths); with keep_raw,
+    also the first keep_raw reads as sequenced (ASCII, one row per read)."""
     from ibwa_amd import _native
     L = _native.lib()
     c_lens = (ctypes.c_uint64 * len(lens))(*lens)
@@ -89,6 +91,8 @@ def make_reads(ascii_, lens, seed, n, ln, sub, indel, threads):
     off = np.empty(n, dtype=np.uint64)
     lns = np.empty(n, dtype=np.uint32)
     L.ibwa_encode_reads_fixed(raw.ctypes.data, n, ln, seq.ctypes.data, off.ctypes.data, lns.ctypes.data, threads)
+    if keep_raw:
+        return seq, off, lns, raw[:min(n, keep_raw) * ln].reshape(-1, ln).copy()
     return seq, off, lns
 
 
@@ -167,8 +171,10 @@ def cpu_and_parity(eng, eopt, seq, off, lns, n_aln, alns, budget_s, check, heavy
     oracle.cal_sa_reg_gap(b0, b1, seq, off[:n_cal], lns[:n_cal], opt, n_threads=threads)
     dt = time.perf_counter() - t
     n_s = int(min(n, max(check, n_cal * budget_s / max(dt, 1e-3))))
+    wtch = np.zeros(n_s, dtype=np.uint32)
     t = time.perf_counter()
-    rn, ra, tch = oracle.cal_sa_reg_gap(b0, b1, seq, off[:n_s], lns[:n_s], opt, n_threads=threads, touches=True)
+    rn, ra, tch = oracle.cal_sa_reg_gap(b0, b1, seq, off[:n_s], lns[:n_s], opt, n_threads=threads, touches=True,
+                                        width_touches=wtch)
     dt = time.perf_counter() - t
     p = int(rn.sum())
     ok_first = bool((n_aln[:n_s] == rn).all() and alns[:p].tobytes() == ra.tobytes())
@@ -210,7 +216,89 @@ def cpu_and_parity(eng, eopt, seq, off, lns, n_aln, alns, budget_s, check, heavy
               "handed_on_mismatches": bad[:20], "handed_on_ok": not bad,
               "heavy_check_s": time.perf_counter() - t0}
     parity["ok"] = ok_first and not bad and n_s + sum(checked.values()) >= 200_000
-    return cpu, tch, parity
+    # which of the sampled first reads the cooperative pass resolved (for the per-kernel roofline)
+    coop_first = np.zeros(n_s, dtype=bool)
+    cid = ids[(ps == 1) & (ids < n_s)]
+    coop_first[cid] = True
+    return cpu, (tch, wtch, coop_first), parity
+
+
+REF = os.path.join(ROOT, "oracle", "_ref", "ibwa_ref")
+
+
+def write_fastq(path, raw):
+    """Fixed-width FASTQ records '@r%010d', bases, '+', 'I' qualities (raw: one ASCII read per row)."""
+    n, L = raw.shape
+    rec = 12 + 1 + L + 3 + L + 1
+    buf = np.empty((n, rec), dtype=np.uint8)
+    buf[:, :12] = np.frombuffer("".join(f"@r{i:010d}" for i in range(n)).encode(), dtype=np.uint8).reshape(n, 12)
+    buf[:, 12] = ord("\n")
+    buf[:, 13:13 + L] = raw
+    buf[:, 13 + L:16 + L] = np.frombuffer(b"\n+\n", dtype=np.uint8)
+    buf[:, 16 + L:16 + 2 * L] = ord("I")
+    buf[:, 16 + 2 * L] = ord("\n")
+    buf.tofile(path)
+
+
+def sai_records(path, n):
+    """Per-read hit records (bytes) of the first n reads of a .sai (64 B header, n_aln + 16 B each)."""
+    d = np.fromfile(path, dtype=np.uint8)
+    p, out = 64, []
+    for _ in range(n):
+        k = int(d[p:p + 4].view(np.int32)[0])
+        out.append(d[p + 4:p + 4 + 16 * k].tobytes())
+        p += 4 + 16 * k
+    return out
+
+
+def ref_baseline(eng, raw, aln_argv, threads, n_aln, alns, budget_s):
+    """The reference itself as the CPU baseline: oracle/_ref/ibwa_ref (compiled from the reference's own
+    sources by oracle/Makefile; test infrastructure, never part of the product) runs `aln -t <threads>`
+    (bwa_aln_core, bwtaln.c:173-241) on the first reads of the same workload, written as FASTQ, with
+    the device-built index written as .bwt / .rbwt (bwt_dump_bwt, bwtio.c:7-15) -- files under
+    oracle/_ref/bench/.  Its wall time less that of a 1 000-read run (index load, start-up) gives its
+    alignment rate; its .sai records must equal the GPU's hits for those reads."""
+    import subprocess
+    if not os.path.exists(REF):
+        return None
+    d = os.path.join(ROOT, "oracle", "_ref", "bench")
+    os.makedirs(d, exist_ok=True)
+    pre = os.path.join(d, "g")
+    try:
+        for s_, ext in ((0, ".bwt"), (1, ".rbwt")):
+            p, L2, w = eng.export_bwt(s_)
+            with open(pre + ext, "wb") as f:
+                np.array([p] + list(L2), dtype=np.uint32).tofile(f)
+                w.astype(np.uint32, copy=False).tofile(f)
+
+        def run(n):
+            fq = os.path.join(d, f"s{n}.fq")
+            write_fastq(fq, raw[:n])
+            sai = os.path.join(d, f"s{n}.sai")
+            t = time.perf_counter()
+            r = subprocess.run([REF, "aln", "-t", str(threads), *aln_argv, "-f", sai, pre, fq], stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, timeout=600)
+            dt = time.perf_counter() - t
+            if r.returncode != 0:
+                raise RuntimeError(r.stderr.decode(errors="replace")[-500:])
+            return dt, sai
+
+        t_small, _ = run(1000)
+        # size the sample from a 20 000-read run to about budget_s of alignment
+        t20, _ = run(20000)
+        rate = 19000 / max(t20 - t_small, 1e-3)
+        n = int(min(raw.shape[0], max(20000, rate * budget_s)))
+        t_n, sai = run(n)
+        got = per_read(n_aln, alns, range(n))
+        same = sai_records(sai, n) == got
+        return {"value": (n - 1000) / max(t_n - t_small, 1e-3), "unit": "reads/s", "cores": threads,
+                "kind": "reference", "cpu_model": cpu_model(),
+                "sample": f"first {n} of the same reads as FASTQ, same index (device-built, written as .bwt/.rbwt) "
+                          f"and options: `oracle/_ref/ibwa_ref aln -t {threads}` (the reference compiled from its "
+                          f"sources) {t_n:.1f} s wall, less {t_small:.1f} s for 1 000 reads (index load, start-up)",
+                "sai_equals_gpu": bool(same)}
+    finally:
+        subprocess.run(["rm", "-rf", d])
 
 
 def sa2pos_leg(eng, lns, n_aln, alns):
@@ -366,6 +454,8 @@ def main():
     ap.add_argument("--seed", type=int, default=3, help="reads seed (SURVEY §8d: configs[2] = 3)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--heavy-budget", type=float, default=20.0, help="seconds of CPU parity on handed-on reads")
+    ap.add_argument("--ref-budget", type=float, default=15.0,
+                    help="seconds of the reference binary's aln (oracle/_ref/ibwa_ref) for cpu_baseline (0: off)")
     ap.add_argument("--check", type=int, default=200_000, help="min. first reads checked bit-exact vs the CPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exact-leg", type=int, default=1, help="also run configs[1] (-n 0) as extra.exact_leg")
@@ -409,8 +499,14 @@ def main():
     ascii_, codes, lens, n_amb = make_genome(int(round(args.scale * den)), den, 37, threads)
     log(f"genome {codes.size/1e9:.3f} Gbp ({n_amb} N->random), {time.perf_counter()-tg:.1f} s")
     tr = time.perf_counter()
-    parts = [make_reads(ascii_, lens, shard_seed(r, args.seed), args.reads, args.read_len, 0.01, 0.05, threads)
-             for r in ([rank] if world > 1 else range(max(1, args.shards)))]
+    keep = 1_000_000 if world == 1 and rank == 0 and not args.no_cpu and args.ref_budget > 0 else 0
+    parts = [make_reads(ascii_, lens, shard_seed(r, args.seed), args.reads, args.read_len, 0.01, 0.05, threads,
+                        keep_raw=keep if j == 0 else 0)
+             for j, r in enumerate([rank] if world > 1 else range(max(1, args.shards)))]
+    raw_sample = None
+    if keep:
+        raw_sample = parts[0][3]
+        parts[0] = parts[0][:3]
     if len(parts) == 1:
         seq, off, lns = parts[0]
     else:  # reads of shards 0..K-1 back to back, as one batch
@@ -445,7 +541,7 @@ def main():
         eng.run(opt)
         progress(f"warmup {w}")
     # timed region: inputs resident in HBM, results left in HBM
-    ms_w = ms_s = ms_r = ms_c = 0.0
+    ms_w = ms_s = ms_r = ms_c = ms_cw = ms_cr = 0.0
     if dist is not None:
         dist.barrier()
     hip = ctypes.CDLL("libamdhip64.so")
@@ -459,6 +555,8 @@ def main():
         ms_s += st.ms_search
         ms_r += st.ms_retry
         ms_c += st.ms_coop
+        ms_cw += st.ms_coop_width
+        ms_cr += st.ms_coop_roots
     hip.hipDeviceSynchronize()
     if dist is not None:
         dist.barrier()
@@ -491,7 +589,9 @@ def main():
                  "n_aln_overflow": int(stl.n_aln_overflow), "n_heavy": int(stl.n_heavy), "n_coop": int(stl.n_coop),
                  "path": {0: "width+search", 1: "exact", 2: "width+gapped", 3: "exact+jump"}.get(path, str(path)),
                  "kernel_ms_per_step": {"k_width(first pass)": ms_w / launches, "k_gapped": ms_s / launches,
-                                        "k_coop(+its widths)": ms_c / launches,
+                                        "k_width(heavy reads)": ms_cw / launches,
+                                        "k_coop_roots": ms_cr / launches,
+                                        "k_coop": (ms_c - ms_cw - ms_cr) / launches,
                                         "wide+general retry": (ms_r - ms_c) / launches},
                  "host_cores": threads, "cpu_model": cpu_model(),
                  # digest of the sources libibwa_amd.so was built from (checked against this tree on load)
@@ -504,38 +604,84 @@ def main():
         k_ms = (ms_w + ms_s + ms_r) / launches
         if do_cpu:
             tc = time.perf_counter()
-            cpu, tch, parity = cpu_and_parity(eng, opt, seq, off, lns, n_aln, alns, args.cpu_budget, args.check,
-                                              args.heavy_budget, threads)
+            cpu, (tch, wtch, coop_first), parity = cpu_and_parity(eng, opt, seq, off, lns, n_aln, alns, args.cpu_budget,
+                                                                  args.check, args.heavy_budget, threads)
             log(f"CPU baseline + parity {time.perf_counter()-tc:.1f} s: {cpu['value']:.0f} reads/s, parity {parity}")
             result["cpu_baseline"] = cpu
             extra["parity"] = parity
             extra["parity_sample_ok"] = parity["ok"]
+            if raw_sample is not None:
+                tr_ = time.perf_counter()
+                try:
+                    ref = ref_baseline(eng, raw_sample, args.aln.split(), threads, n_aln, alns, args.ref_budget)
+                    if ref is not None:
+                        extra["cpu_port"] = cpu
+                        result["cpu_baseline"] = ref
+                        extra["parity"]["reference_sample_ok"] = ref["sai_equals_gpu"]
+                except Exception as e:  # the headline line is printed regardless
+                    extra["cpu_reference_error"] = repr(e)[:500]
+                log(f"reference CPU baseline {time.perf_counter()-tr_:.1f} s: {result['cpu_baseline']}")
+            del raw_sample
             touches = float(tch.mean())
-            # the step's kernels run the reference algorithm (widths + bwt_match_gap): its bytes are
-            # 64 B per Occ-interval touch of the restatement, over all kernel time
+            # algorithmic bytes: 64 B per Occ-interval touch of the reference algorithm, counted by
+            # the CPU restatement on the sampled first reads and split per kernel -- bwt_cal_width's touches
+            # (k_width), bwt_match_gap's of the reads the first pass resolves (k_gapped) and of the heavy reads
+            # (k_coop with its level-0 prologue k_coop_roots; it re-runs them from the start, so the first
+            # pass's partial work on them and their second k_width are not algorithmic bytes)
+            ns_ = tch.size
+            scale = args.reads / ns_
+            mg = tch.astype(np.float64) - wtch
+            per_k = {"k_width": (float(wtch.sum()) * scale, ms_w / launches, ["k_width"]),
+                     "k_gapped": (float(mg[~coop_first].sum()) * scale, ms_s / launches, ["k_gapped"]),
+                     "k_coop": (float(mg[coop_first].sum()) * scale, (ms_c - ms_cw) / launches,
+                                ["k_coop", "k_coop_roots"])}
+            pk = {}
+            for name, (tt, ms, kn) in per_k.items():
+                ab = tt * 64.0
+                ach = ab / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+                pmc = pmc_traffic(kn, result["config"]["workload"])
+                pk[name] = {"algorithmic_bytes_per_step": ab, "kernel_ms_per_step": ms, "achieved": ach,
+                            "frac": ach / HBM_PEAK_GBS, "touches_per_read": tt / args.reads,
+                            "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
+                            "traffic_over_algorithmic": pmc[0] / ab if pmc and ab > 0 else None}
             ach = touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9
             pmc = pmc_traffic(kernels, result["config"]["workload"])
-            result["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": ach / HBM_PEAK_GBS, "traffic": pmc[0] if pmc else None,
-                                  "kernel": "+".join(kernels) + " (one step's launches)",
-                                  "traffic_source": pmc[1] if pmc else None,
-                                  "traffic_GBps": pmc[0] / (k_ms * 1e-3) / 1e9 if pmc else None,
-                                  "profiled_kernel_ms_per_step": pmc[2] if pmc else None,
-                                  "algorithmic_bytes_per_step": touches * 64.0 * args.reads,
-                                  "kernel_ms_per_step": k_ms, "touches_per_read": touches, "bytes_per_touch": 64,
-                                  "touches_sample": f"first {tch.size} reads, oracle/ibwa_oracle.c touch counter"}
+            if path != 2:  # the exact path: one kernel does the search
+                pk = {"k_exact": {"algorithmic_bytes_per_step": touches * 64.0 * args.reads, "kernel_ms_per_step": k_ms,
+                                  "achieved": ach, "frac": ach / HBM_PEAK_GBS, "touches_per_read": touches,
+                                  "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None}}
+            dom = max(pk, key=lambda x: pk[x]["kernel_ms_per_step"])
+            d_ = pk[dom]
+            result["roofline"] = {"bound": "hbm", "kernel": dom + (" (+ k_coop_roots)" if dom == "k_coop" else ""),
+                                  "achieved": d_["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d_["frac"],
+                                  "traffic": d_["traffic"], "traffic_source": d_["traffic_source"],
+                                  "algorithmic_bytes_per_step": d_["algorithmic_bytes_per_step"],
+                                  "kernel_ms_per_step": d_["kernel_ms_per_step"], "bytes_per_touch": 64,
+                                  "per_kernel": pk,
+                                  "step": {"kernels": "+".join(kernels) + " (one step's launches)", "achieved": ach,
+                                           "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": touches * 64.0 * args.reads,
+                                           "kernel_ms": k_ms, "touches_per_read": touches,
+                                           "traffic": pmc[0] if pmc else None,
+                                           "traffic_source": pmc[1] if pmc else None},
+                                  "touches_sample": f"first {ns_} reads ({int(coop_first.sum())} of them resolved by the "
+                                                    f"cooperative pass), oracle/ibwa_oracle.c touch counter"}
+        # the extra legs cannot cost the headline line: a failure is recorded as extra.<leg>.error
+        def leg(name, fn):
+            t_ = time.perf_counter()
+            try:
+                extra[name] = fn()
+            except Exception as e:
+                extra[name] = {"error": repr(e)[:500]}
+            log(f"{name} {time.perf_counter()-t_:.1f} s: {extra[name]}")
+
         if args.sa2pos and n_aln is not None:
-            extra["sa2pos"] = sa2pos_leg(eng, lns, n_aln, alns)
+            leg("sa2pos", lambda: sa2pos_leg(eng, lns, n_aln, alns))
         if sw_pairs is not None:
-            ts = time.perf_counter()
-            extra["sw_leg"] = sw_leg(eng, sw_pairs[0], sw_pairs[1], do_cpu)
+            leg("sw_leg", lambda: sw_leg(eng, sw_pairs[0], sw_pairs[1], do_cpu))
             del sw_pairs
-            log(f"sw leg {time.perf_counter()-ts:.1f} s: {extra['sw_leg']}")
         if args.exact_leg and world == 1 and not exact_cfg:
             del seq, off, lns
-            te = time.perf_counter()
-            extra["exact_leg"] = exact_leg(eng, ascii_, lens, args, threads, hip, do_cpu)
-            log(f"exact leg {time.perf_counter()-te:.1f} s: {extra['exact_leg']}")
+            leg("exact_leg", lambda: exact_leg(eng, ascii_, lens, args, threads, hip, do_cpu))
         result["extra"] = extra
         print(json.dumps(result), flush=True)
     eng.close()

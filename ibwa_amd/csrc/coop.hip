@@ -66,6 +66,8 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 
 // lane states
 constexpr int L_IDLE = 0, L_FETCH = 1, L_EXP = 2, L_TAIL = 3;
+// prologue chain records: the root chain ended in a hit / did not run (read not for this kernel)
+constexpr uint32_t PRO_HIT = 1, PRO_SKIP = 2;
 
 struct Blk {
   uint4 v0, v1, v2, v3;
@@ -128,8 +130,108 @@ __device__ __forceinline__ uint4 mk_ent(uint32_t k, uint32_t l, int i, int ldp, 
                         (uint32_t)state << 25 | cat << 27);
 }
 
+// A node of a match chain (a popped entry, or the match child that continues the chain).
+struct Node {
+  uint32_t k, l;
+  int i, ldp, e_mm, e_go, e_ge, a, state;
+};
+
+// The widths an expansion at read position ni reads (bwtgap.c:205-214): width[ni-1], width[ni] and
+// the seed widths at ii-1, ii (ii = ni - (len - seed_len)); {w, bid}.
+struct ExpW {
+  uint2 im2, im1, slo, shi;
+};
+
+// bwtgap.c:200-258 for node nd with the Occ blocks of rows k-1 (bk) and l (bl) loaded (k_coop_roots;
+// k_coop runs the same steps inline): stages the children other than the match child, in the
+// reference's push order, each tagged with its target bucket category and its rank among the
+// chain's children of that category; returns whether the match child exists (it continues the
+// chain: its interval in mk, ml).  csym: the read symbol at i-1; w: the widths it tests.
+__device__ __forceinline__ bool expand_node(const AlnOpt &o, uint4 L2, const Blk &bl, Blk bk, bool qkneg,
+                                            bool qshare, const Node &nd, int max_diff, bool seeded, int len,
+                                            uint32_t csym, const ExpW &w, int t0, int t1, int q1, int q2, uint4 *stg,
+                                            uint32_t &stg_w, uint32_t smask, uint32_t &cnt0, uint32_t &cnt1,
+                                            uint32_t &cnt2, uint32_t &mk, uint32_t &ml) {
+  const bool gape = o.mode & MODE_GAPE;
+  const uint32_t qk = nd.k, ql = nd.l;
+  if (qshare) bk = bl;
+  uint4 KK, LL;
+  {
+    const uint4 cl4 = make_uint4(occ_of(bl.v0, ql), occ_of(bl.v1, ql), occ_of(bl.v2, ql), occ_of(bl.v3, ql));
+    const uint4 ck4 = qkneg ? make_uint4(0, 0, 0, 0)
+                            : make_uint4(occ_of(bk.v0, qk - 1), occ_of(bk.v1, qk - 1), occ_of(bk.v2, qk - 1),
+                                         occ_of(bk.v3, qk - 1));
+    KK = make_uint4(L2.x + ck4.x + 1, L2.y + ck4.y + 1, L2.z + ck4.z + 1, L2.w + ck4.w + 1);
+    LL = make_uint4(L2.x + cl4.x, L2.y + cl4.y, L2.z + cl4.z, L2.w + cl4.w);
+  }
+  const int e_mm = nd.e_mm, e_go = nd.e_go, e_ge = nd.e_ge, state = nd.state;
+  int m = max_diff - (e_mm + e_go);
+  if (gape) m -= e_ge;
+  int m_seed = 0;
+  if (seeded) {
+    m_seed = o.max_seed_diff - (e_mm + e_go);
+    if (gape) m_seed -= e_ge;
+  }
+  const int ni = nd.i - 1;
+  const uint32_t occ = nd.l - nd.k + 1;
+  bool allow_diff = true, allow_M = true;
+  if (ni > 0) {
+    const int ii = ni - (len - o.seed_len);
+    if ((int)w.im2.y > m - 1) allow_diff = false;
+    else if ((int)w.im2.y == m - 1 && (int)w.im1.y == m - 1 && w.im2.x == w.im1.x) allow_M = false;
+    if (seeded && ii > 0) {
+      if ((int)w.slo.y > m_seed - 1) allow_diff = false;
+      else if ((int)w.slo.y == m_seed - 1 && (int)w.shi.y == m_seed - 1 && w.slo.x == w.shi.x) allow_M = false;
+    }
+  }
+  const uint32_t ne4 = (KK.x <= LL.x ? 1u : 0u) | (KK.y <= LL.y ? 2u : 0u) | (KK.z <= LL.z ? 4u : 0u) |
+                       (KK.w <= LL.w ? 8u : 0u);
+  const int tmp = (o.mode & MODE_LOGGAP) ? int_log2((uint32_t)(e_ge + e_go)) / 2 + 1 : e_go + e_ge;
+  uint32_t vm = 0;
+  if (allow_diff && ni >= o.indel_end_skip + tmp && len - ni >= o.indel_end_skip + tmp) {
+    if (state == STATE_M) {
+      if (e_go < o.max_gapo) vm = 1u | ne4 << 1;
+    } else if (state == STATE_I) {
+      if (e_ge < o.max_gape) vm = 1u;
+    } else if (state == STATE_D) {
+      if (e_ge < o.max_gape && (e_ge + e_go < max_diff || occ < (uint32_t)o.max_del_occ)) vm = ne4 << 1;
+    }
+  }
+  const uint32_t rot = (csym + 1) & 3;
+  const uint32_t ner = ((ne4 >> rot) | (ne4 << (4 - rot))) & 15u;
+  if (allow_diff && allow_M) vm |= ner << 5;
+  else if (csym < 4) vm |= ner & 8u ? 1u << 8 : 0u;
+  // bit 8 with csym < 4 is the match child: it continues the chain instead of being staged
+  const bool match = (vm >> 8) & 1u && csym < 4;
+  if (match) vm &= ~(1u << 8);
+  const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
+  const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
+  while (vm) {
+    const uint32_t j = (uint32_t)__builtin_ctz(vm);
+    vm &= vm - 1;
+    const bool is_ins = j == 0, is_del = j - 1 < 4, is_sym = j >= 5;
+    const uint32_t cc = is_del ? j - 1 : (csym + j - 4) & 3;
+    const uint32_t pk = is_ins ? nd.k : pick4(KK, cc);
+    const uint32_t pl = is_ins ? nd.l : pick4(LL, cc);
+    const bool open = !is_sym && state == STATE_M;
+    const int n_mm = e_mm + (is_sym ? 1 : 0);  // staged symbol children are mismatches
+    const int n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (!is_sym && !open ? 1 : 0);
+    const int pi = is_del ? ni + 1 : ni;
+    const int pstate = is_ins ? STATE_I : is_del ? STATE_D : STATE_M;
+    const int sc = sc_base + (is_sym ? o.s_mm : sc_gap);
+    const int q = sc == t0 ? 0 : sc == t1 ? q1 : q2;
+    const uint32_t rk = q == 0 ? cnt0++ : q == 1 ? cnt1++ : cnt2++;
+    stg[(stg_w++) & smask] = mk_ent(pk, pl, pi, pi, n_mm, n_gapo, n_gape, nd.a, pstate, (uint32_t)q, rk);
+  }
+  if (match) {
+    mk = pick4(KK, csym);
+    ml = pick4(LL, csym);
+  }
+  return match;
+}
+
 struct Shm {
-  uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | lane << 16 | hit << 24,
+  uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | ring << 16 | hit << 24,
                       //  done (1) | children staged before the chain's last pop << 1}
   uint32_t dirc[4][MAXP];  // page ids of the level's bucket and of its (up to) three target buckets
   uint32_t nb[NSTK];       // entries per bucket
@@ -175,9 +277,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
   // 3 loads + consume, 4 level set-up / teardown, 5 read set-up; 6 iterations, 7 commits, 8 levels
   const bool prof = PROF && A.prof != nullptr;
   // 9..11: lanes running a chain / fetching its entry / in an exact tail, summed over iterations
-  __shared__ unsigned long long pc[12];  // LDS: no registers taken from the hot loop
+  // 12..15: idle lanes per iteration waiting on a hit barrier / with the level's chains all claimed /
+  // held by the chain ring / short of staging room; 16 chains per level (sum of N); 17 chains
+  // discarded at barriers; 18 barriers; 19 children committed
+  // 20..24 iterations in levels of N <= 2, <= 16, <= 64, <= 256, > 256 chains; 25..29 running lanes
+  // summed over those iterations; 30/31 lane-steps expanding / in an exact tail at a one-row
+  // interval; 32..35 chains of < 4, < 16, < 64, >= 64 steps, 36..39 their steps
+  __shared__ unsigned long long pc[40];  // LDS: no registers taken from the hot loop
   if (prof) {
-    if (lane < 12) pc[lane] = 0;
+    if (lane < 40) pc[lane] = 0;
     __syncthreads();
   }
   auto now = []() __attribute__((always_inline)) -> uint64_t { return __builtin_amdgcn_s_memtime(); };
@@ -235,6 +343,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     } else {
       // ---------------------------------------------- per-read setup
       const bool seeded = len > o.seed_len;
+      // level 0 done by k_coop_roots: the records of its two chains (A.proot[2 r], [2 r + 1])
+      bool pro = A.proot && A.proot[2 * r].w == 0u && A.proot[2 * r + 1].w == 0u;
       const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
       for (int j = lane; j < len; j += 64) {
         const uint32_t c = sq[j];
@@ -258,6 +368,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       S.head[lane] = 0;
       S.rb[lane] = NONE;
       for (int j = lane; j < RREC; j += 64) S.recA[j].w = 0;
+      if (pro && lane < 2) {
+        // the finished chains 0 and 1 of level 0: staging start = their offset in A.pstore (ring 64)
+        const uint4 q = A.proot[2 * r + lane];
+        S.recA[lane] = make_uint4(q.x, q.y, (q.z & 0xffffu) | 64u << 16, 1u | (q.z >> 16) << 1);
+      }
       __syncthreads();
       // roots (bwtgap.c:126-127): strand 0 then strand 1, both in bucket 0
       {
@@ -304,7 +419,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           if (tg(q) < o.n_stacks)
             for (uint32_t j = lane; j < S.np[tg(q)]; j += 64) S.dirc[1 + q][j] = dir[tg(q) * MAXP + j];
         __syncthreads();
-        if (prof && lane == 0) ++pc[8];
+        const int nbk = N <= 2 ? 0 : N <= 16 ? 1 : N <= 64 ? 2 : N <= 256 ? 3 : 4;
+        if (prof && lane == 0) {
+          ++pc[8];
+          pc[16] += N;
+        }
         lap(4);
         uint32_t next_c = 0, cp = 0, barrier = NONE;
         // lane chain state
@@ -322,10 +441,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         uint32_t wh = (uint32_t)lane;
         uint4 wen = make_uint4(0, 0, 0, 0);
         bool wld = false, wreq = wh < N;
+        if (pro) {
+          // level 0 ran in the prologue: its two chains are finished (records in place) and commit below
+          pro = false;
+          next_c = 2;
+          wreq = false;
+        }
         uint32_t hit_c = NONE;  // chain this lane ended with a hit in the last iteration
+        uint32_t csteps = 0;    // (prof) steps of the lane's chain
         // end the lane's chain: its record (hit or not) goes to the reorder buffer
         auto end_chain = [&](bool hit, uint32_t hk, uint32_t hl) __attribute__((always_inline)) {
           const uint32_t slot = c & (RREC - 1);
+          if (prof) {
+            const int b = csteps < 4 ? 0 : csteps < 16 ? 1 : csteps < 64 ? 2 : 3;
+            atomicAdd(&pc[32 + b], 1ull);
+            atomicAdd(&pc[36 + b], (unsigned long long)csteps);
+            csteps = 0;
+          }
           if (hit) {  // the hit record {k, l, n_mm | n_gapo << 8 | n_gape << 16 | a << 24, ldp}: global,
                       // agent-scope (L2) accesses, read once by the whole wave at the barrier
             uint32_t *hr = reinterpret_cast<uint32_t *>(A.recb + wave * RREC + slot);
@@ -384,6 +516,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             if (__ballot(hit_c != NONE)) newb = wave_min(hit_c);
             hit_c = NONE;
             if (newb < barrier) {
+              if (prof) {
+                const unsigned long long dr = __ballot(lst != L_IDLE && c > newb);
+                if (lane == 0) {
+                  pc[17] += __popcll(dr);
+                  ++pc[18];
+                }
+              }
               if (lst != L_IDLE && c > newb) {
                 S.rb[lane] = S.rb[lane] < cstart ? S.rb[lane] : cstart;
                 lst = L_IDLE;
@@ -395,7 +534,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
                   const uint32_t slot = cc & (RREC - 1);
                   const uint4 ra = S.recA[slot];
                   if (ra.w) {
-                    atomicMin(&S.rb[(ra.z >> 16) & 63], ra.x);
+                    const uint32_t rl = (ra.z >> 16) & 127;
+                    if (rl < 64) atomicMin(&S.rb[rl], ra.x);  // (a prologue chain is never rolled back)
                     S.recA[slot].w = 0;
                   }
                 }
@@ -417,7 +557,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             }
           }
           lap(0);
-          if (prof && lane == 0) ++pc[6];
+          if (prof && lane == 0) {
+            ++pc[6];
+            ++pc[20 + nbk];
+          }
           // finished chains from cp on, in pop order
           uint32_t ndone = 0;
           for (uint32_t base = cp; base < next_c; base += 64) {
@@ -453,6 +596,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               }
               const uint32_t nv = (lim - base) < 64 ? (lim - base) : 64;
               n_live = n_live + dsum - nv;
+              if (prof && lane == 0) pc[19] += dsum;
               uint32_t T0 = 0, T1 = 0, T2 = 0;
               const uint32_t o0 = wave_excl(n0, lane, T0);
               const uint32_t o1 = wave_excl(n1, lane, T1);
@@ -490,7 +634,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               // (binary search over the lanes' prefixes) and goes to its category's bucket at
               // (bucket size) + (chain's offset in the batch) + (its rank in the chain)
               {
-                const uint32_t my_rl = (ra.z >> 16) & 63, my_st = ra.x;
+                const uint32_t my_rl = (ra.z >> 16) & 127, my_st = ra.x;
                 const uint32_t nb0 = S.nb[t0], nb1 = t1 < o.n_stacks ? S.nb[t1] : 0u,
                                nb2 = t2 < o.n_stacks ? S.nb[t2] : 0u;
                 for (uint32_t g0 = 0; g0 < dsum; g0 += 64u * 2) {
@@ -511,7 +655,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
                     f1[u] = nb1 + __shfl(o1, j);
                     f2[u] = nb2 + __shfl(o2, j);
                     e[u] = make_uint4(0, 0, 0, 0);
-                    if (g < dsum) e[u] = stg_base[((uint64_t)rl << A.stg_log2) + ((st0 + x) & SMASK)];
+                    if (g < dsum)
+                      e[u] = rl < 64 ? stg_base[((uint64_t)rl << A.stg_log2) + ((st0 + x) & SMASK)] : A.pstore[st0 + x];
                   }
 #pragma unroll
                   for (int u = 0; u < 2; ++u) {
@@ -523,7 +668,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
                     }
                   }
                 }
-                if (v && tot) atomicMax(&S.head[my_rl], my_st + tot);
+                if (v && tot && my_rl < 64) atomicMax(&S.head[my_rl], my_st + tot);
               }
               if (v) S.recA[cc & (RREC - 1)].w = 0;
               __syncthreads();
@@ -619,6 +764,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             const uint32_t cap_c = cp + RREC < N ? cp + RREC : N;
             const uint32_t avail = cap_c > next_c ? cap_c - next_c : 0u;
             const uint32_t rank = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
+            if (prof) {
+              const bool idle = lst == L_IDLE;
+              const unsigned long long i_b = __ballot(idle && barrier != NONE),
+                                       i_n = __ballot(idle && barrier == NONE && next_c >= N),
+                                       i_r = __ballot(idle && barrier == NONE && next_c < N && next_c >= cap_c),
+                                       i_s = __ballot(idle && barrier == NONE && !want);
+              if (lane == 0) {
+                pc[12] += __popcll(i_b);
+                pc[13] += __popcll(i_n);
+                pc[14] += __popcll(i_r);
+                pc[15] += __popcll(i_s);
+              }
+            }
             if (wm) {
               // every lane takes part in the shuffles; the claim reads its chain's window slot
               const uint32_t cc = next_c + rank, src = cc & 63u;
@@ -628,6 +786,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               if (want && rank < avail) {
                 c = cc;
                 cstart = stg_w;
+                csteps = 0;
                 cnt0 = cnt1 = cnt2 = 0;
                 if (tag == cc) {
                   take_entry(ce);
@@ -670,7 +829,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               pc[9] += __popcll(b_act);
               pc[10] += __popcll(b_f);
               pc[11] += __popcll(b_t);
+              pc[25 + nbk] += __popcll(b_act);
             }
+            const unsigned long long b_e1 = __ballot(exp && k == l), b_t1 = __ballot(tail && xk == xl);
+            if (lane == 0) {
+              pc[30] += __popcll(b_e1);
+              pc[31] += __popcll(b_t1);
+            }
+            if (lst != L_IDLE) ++csteps;
           }
           const uint32_t qk = tail ? xk : k, ql = tail ? xl : l;
           const bool qkneg = qk == 0;
@@ -702,7 +868,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               end_chain(false, 0, 0);
             }
           } else if (exp) {
-            // ---- expansion (bwtgap.c:200-258); the match child continues the chain
+            // ---- expansion (bwtgap.c:200-258); the match child continues the chain.  The same steps as
+            // expand_node (k_coop_roots), kept inline: through the function this loop's registers
+            // spilled (16 -> 39 scratch accesses) and k_coop ran 10 % slower (same-box A/B)
             if (qshare) bk = bl;
             uint4 KK, LL;
             {
@@ -836,8 +1004,204 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     lap(5);
   }
   if (prof && lane == 0)
-    for (int q = 0; q < 12; ++q) atomicAdd(A.prof + q, (unsigned long long)pc[q]);
+    for (int q = 0; q < 40; ++q) atomicAdd(A.prof + q, (unsigned long long)pc[q]);
   if (prof && A.wave_t && lane == 0) A.wave_t[2 * wave + 1] = now();
+}
+
+// k_coop_roots -- level 0 of the heavy reads, before k_coop takes them.  Level 0 is the two root
+// chains (strand 1 popped first, bwtgap.c:126-127): each walks the read from its end while the
+// match child exists, staging the mismatch and gap children of every expansion.  They take about a
+// tenth of k_coop's iterations with two lanes of 64 running, so here each lane runs one root chain
+// on its own (chain u = 2 r + x of launch read r: x = 0 strand 1, x = 1 strand 0), from the read's
+// initial state, widths and symbols from global memory.  The two chains are independent unless
+// chain 0 ends in a hit (chain 1 would have to see it): then, or when the read is not for k_coop,
+// the record says so and k_coop runs level 0 itself.  A chain's children are staged in the lane's
+// ring (k_coop's staging rings, unused until it starts), then copied to the compact store pstore
+// at an offset reserved when the chain ends; proot[u] = {offset, cnt0 | cnt1 << 16,
+// cnt2 | children staged before its last pop << 16, flag}.
+__global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long long *counter) {
+  const int lane = threadIdx.x;
+  const AlnOpt o = A.o;
+  const bool comp = o.mode & MODE_COMPREAD;
+  const IndexView ixv0 = A.ix[0], ixv1 = A.ix[1];
+  const uint32_t SMASK = (1u << A.stg_log2) - 1u;
+  uint4 *const ring = A.stg + (((uint64_t)blockIdx.x * 64 + lane) << A.stg_log2);
+  const int t0 = o.s_mm, t1 = o.s_gape, t2 = o.s_gapo;  // the targets of level 0's children
+  const int q1 = t1 == t0 ? 0 : 1;
+  const int q2 = t2 == t0 ? 0 : (t2 == t1 ? q1 : 2);
+  constexpr int L_COPY = 4, L_END = 5;
+  int pst = L_IDLE;
+  uint64_t u = 0;
+  uint32_t pflag = 0, c0 = 0, c1 = 0, c2 = 0, pmpre = 0, pw = 0, ci = 0;
+  uint64_t off = 0;
+  Node nd = {};
+  int pa = 0, plen = 0, pmd = 0;
+  bool pseed = false;
+  const uint8_t *psq = nullptr;
+  const uint2 *pwb = nullptr, *pswb = nullptr;
+  uint32_t xk = 0, xl = 0, tcur = 0, snext = 0;
+  int xj = 0;
+  uint2 wim1 = make_uint2(0, 0);  // width[i-1] of the node about to be popped
+  auto psym = [&](int x) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t c = psq[x];
+    return pa && comp && c < 4 ? 3u - c : c;
+  };
+  auto record = [&]() __attribute__((always_inline)) {
+    A.proot[u] = make_uint4((uint32_t)off, c0 | c1 << 16, c2 | pmpre << 16, pflag);
+    pst = L_IDLE;
+  };
+  // the chain has ended without a hit: reserve its children's room in the store
+  auto finish = [&]() __attribute__((always_inline)) {
+    const uint32_t tot = c0 + c1 + c2;
+    off = 0;
+    if (tot) {
+      off = atomicAdd(A.pstore_next, (unsigned long long)tot);
+      if (off + tot > A.pstore_cap) pflag = PRO_SKIP;  // (cap < 2^32: offsets fit the record)
+    }
+    ci = 0;
+    if (tot && pflag == 0) pst = L_COPY;
+    else record();
+  };
+  // a pop of the chain (level 0: no differences, state M, m = max_diff; bwtgap.c:139-163)
+  auto ppop = [&]() __attribute__((always_inline)) {
+    pmpre = c0 + c1 + c2;
+    if (nd.i > 0 && pmd < (int)wim1.y) { finish(); return; }  // :155
+    if (nd.i == 0) { pflag = PRO_HIT; record(); return; }     // :159
+    if (pmd == 0) {                                            // :160
+      xj = nd.i - 1;
+      xk = nd.k;
+      xl = nd.l;
+      tcur = snext;
+      if (snext > 3) finish();
+      else pst = L_TAIL;
+      return;
+    }
+    pst = L_EXP;
+  };
+  for (;;) {
+    // ---- idle lanes take the next chains (one atomic per wave)
+    {
+      const bool want = pst == L_IDLE;
+      const unsigned long long wm = __ballot(want);
+      if (wm) {
+        unsigned long long base = 0;
+        if (lane == (int)__builtin_ctzll(wm)) base = atomicAdd(counter, (unsigned long long)__popcll(wm));
+        base = __shfl(base, (int)__builtin_ctzll(wm));
+        if (want) {
+          u = base + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
+          if (u >= 2ull * (uint64_t)A.n) {
+            pst = L_END;
+          } else {
+            const int64_t r = (int64_t)(u >> 1);
+            pa = (u & 1) ? 0 : 1;
+            const int64_t rr = A.ids ? A.ids[r] : r;
+            plen = (int)A.len[rr];
+            psq = A.seq + A.off[rr];
+            pmd = o.fnr_pos ? (int)A.maxdiff_tab[plen] : o.max_diff;
+            pseed = plen > o.seed_len;
+            const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
+            pwb = wb + (pa ? A.wlen1 : 0);
+            pswb = wb + 2 * A.wlen1 + (pa ? o.seed_len + 1 : 0);
+            c0 = c1 = c2 = pmpre = pw = off = 0;
+            if (plen < 1 || plen > COOP_MAXLEN || o.n_stacks > NSTK ||
+                (1u << A.stg_log2) < 9u * (uint32_t)(plen + 1) + 16u ||
+                (plen > o.seed_len && o.seed_len > COOP_SEEDMAX) || (int)A.nN[r] > pmd) {
+              pflag = PRO_SKIP;
+              record();
+            } else {
+              pflag = 0;
+              nd = {0u, ixv0.seq_len, plen, 0, 0, 0, 0, pa, STATE_M};
+              wim1 = pwb[plen - 1];
+              snext = psym(plen - 1);
+              pst = L_FETCH;  // the root's pop, once its width is in
+            }
+          }
+        }
+      }
+    }
+    if (__ballot(pst != L_END) == 0ull) break;
+    // ---- loads (one round trip)
+    const bool exp = pst == L_EXP, tail = pst == L_TAIL, copy = pst == L_COPY;
+    const IndexView ix = pa ? ixv0 : ixv1;  // strand a searches bwt[1-a]
+    const uint4 *ob = pa ? A.o64[0] : A.o64[1];
+    const uint32_t qk = tail ? xk : nd.k, ql = tail ? xl : nd.l;
+    const bool qkneg = qk == 0;
+    const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
+    Blk bk, bl;
+    load_blk(ob, ql, exp, bl);
+    load_blk(ob, qk - 1, exp && !qkneg && !qshare, bk);
+    uint4 tvl = make_uint4(0, 0, 0, 0), tvk = make_uint4(0, 0, 0, 0);
+    if (tail) tvl = ob[(size_t)(ql >> 6) * 4 + tcur];
+    if (tail && !qkneg && !qshare) tvk = ob[(size_t)((qk - 1) >> 6) * 4 + tcur];
+    const int ni = nd.i - 1;
+    ExpW w = {};
+    uint32_t csym = 0, snx = 0;
+    if (exp) {
+      csym = psym(ni);
+      if (ni > 0) {
+        w.im2 = pwb[ni - 1];
+        w.im1 = pwb[ni];
+        snx = psym(ni - 1);
+        const int ii = ni - (plen - o.seed_len);
+        if (pseed && ii > 0) {
+          w.slo = pswb[ii - 1];
+          w.shi = pswb[ii];
+        }
+      }
+    } else if (tail && xj > 0) {
+      snx = psym(xj - 1);
+    }
+    uint4 cv[4];
+    const uint32_t tot = c0 + c1 + c2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (copy && ci + q < tot) cv[q] = ring[ci + q];
+    // ---- consume
+    if (pst == L_FETCH) {
+      ppop();
+    } else if (copy) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (ci + q < tot) A.pstore[off + ci + q] = cv[q];
+      ci += 4;
+      if (ci >= tot) record();
+    } else if (tail) {
+      // one step of bwt_match_exact_alt (bwt.c:240-247)
+      if (qshare) tvk = tvl;
+      const uint32_t ok = qkneg ? 0u : occ_of(tvk, qk - 1), ol = occ_of(tvl, ql);
+      const uint32_t base = l2of(ix, tcur);
+      xk = base + ok + 1;
+      xl = base + ol;
+      tcur = snx;
+      if (xk > xl) finish();
+      else if (--xj < 0) { pflag = PRO_HIT; record(); }
+      else if (snx > 3) finish();
+    } else if (exp) {
+      uint32_t mk = 0, ml = 0;
+      if (expand_node(o, make_uint4(ix.L2[0], ix.L2[1], ix.L2[2], ix.L2[3]), bl, bk, qkneg, qshare, nd, pmd, pseed,
+                      plen, csym, w, t0, t1, q1, q2, ring, pw, SMASK,
+                      c0, c1, c2, mk, ml)) {
+        nd.k = mk;
+        nd.l = ml;
+        nd.i = ni;
+        wim1 = w.im2;  // width[ni - 1]
+        snext = snx;
+        ppop();
+      } else {
+        finish();
+      }
+    }
+  }
+}
+
+hipError_t launch_coop_roots(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {
+  if (g.n <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(g.pstore_next, 0, sizeof(unsigned long long), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_coop_roots, dim3(blocks), dim3(64), 0, st, g, d_counter);
+  return hipGetLastError();
 }
 
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {

@@ -151,9 +151,15 @@ struct CoopArgs {
   uint32_t *iters;
   unsigned long long *prof;  // diagnostics: per-phase wave cycles (IBWA_PROF_PHASES), may be null
   unsigned long long *wave_t;  // diagnostics: per wave {start, end} shader clock (with prof)
+  uint4 *proot;              // root chain records of k_coop_roots [2 n] (nullptr: k_coop runs level 0)
+  uint4 *pstore;             // their children, compact
+  unsigned long long *pstore_next;  // bump pointer into pstore (entries)
+  uint64_t pstore_cap;       // pstore capacity (entries)
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);
+// level 0 of the heavy reads, one root chain per lane (g.proot / g.pstore set), before launch_coop
+hipError_t launch_coop_roots(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);
 // ids (in input order) and statuses of the reads whose status is non-zero (select.hip); tmp == nullptr
 // only sizes the rocPRIM scratch into *tmp_bytes
 hipError_t select_handed_on(const uint32_t *status, int64_t n, int64_t *ids, uint32_t *sel_status,

@@ -73,7 +73,7 @@ struct DBuf {
 struct ibwa_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[8] = {};
   // index
   DBuf idx[2];
   IndexView ix[2] = {};
@@ -96,6 +96,7 @@ struct ibwa_ctx {
   DBuf d_selst, d_seltmp;                           // statuses of the handed-on reads, select scratch
   DBuf d_ordk, d_ordi, d_ordids, d_ordtmp;          // the coop pass's order (largest first-pass stack first)
   int coop_order = 1;                               // option
+  int coop_roots = 1;                               // option: level 0 of the heavy reads by k_coop_roots
   uint32_t aln_cap_used = 0;
   // sampled suffix arrays kept by ibwa_ctx_build_index
   DBuf sa_s[2];
@@ -138,7 +139,7 @@ struct ibwa_ctx {
   DBuf d_cw, d_ptabg;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
   int coop_pool_gb = 16;             // bucket page pool
-  DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb;
+  DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb, c_proot, c_pstore;
   bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
   bool verbose = getenv("IBWA_VERBOSE") != nullptr;
   bool prof_phases = getenv("IBWA_PROF_PHASES") != nullptr;  // diagnostics kernel variant
@@ -354,6 +355,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_early_entries" && value >= 0) c->gap_early_entries = (uint32_t)value;
   else if (k == "gap_lw" && (value == 0 || value == 1)) c->gap_lw = (int)value;
   else if (k == "coop_order" && (value == 0 || value == 1)) c->coop_order = (int)value;
+  else if (k == "coop_roots" && (value == 0 || value == 1)) c->coop_roots = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
   else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
   else if (k == "exact_jump") c->exact_jump = value != 0;
@@ -1059,6 +1061,23 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
     if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
     if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
+    // k_coop_roots: two chain records per read, their children in a compact store (a chain that
+    // finds it full leaves level 0 to k_coop).  A root chain stages ~190 children on a GRCh37-sized
+    // genome, so the store takes the first pass's page pool when there is one: nothing in it is
+    // live between the first pass and the retry passes, which set it up anew.
+    uint4 *pstore = nullptr;
+    uint64_t pcap = 0;
+    if (c->coop_roots) {
+      if (int rc = c->c_proot.ensure((uint64_t)lanes * 2 * 16)) return rc;
+      if (c->d_pool.cap >= (1ull << 30)) {
+        pstore = c->d_pool.as<uint4>();
+        pcap = std::min<uint64_t>(c->d_pool.cap / 16, 0xFFFFFFFFull);
+      } else {
+        pcap = std::min<uint64_t>(1ull << 31, std::max<uint64_t>(1ull << 24, (uint64_t)lanes * 2 * 256));
+        if (int rc = c->c_pstore.ensure(pcap * 16)) return rc;
+        pstore = c->c_pstore.as<uint4>();
+      }
+    }
     if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
     if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
     if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
@@ -1120,6 +1139,12 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     K.pool_next = c->c_next.as<uint32_t>();
     K.hits = c->c_hits.as<uint4>();
     K.recb = c->c_recb.as<uint4>();
+    if (c->coop_roots) {
+      K.proot = c->c_proot.as<uint4>();
+      K.pstore = pstore;
+      K.pstore_next = c->c_next.as<unsigned long long>() + 1;
+      K.pstore_cap = pcap;
+    }
     K.hcap = hcap;
     K.max_iters = 1u << 24;  // runaway guard; a read past it goes to the sequential kernel
     // hits go on the first pass's stream (a read out of room there is flagged and re-run below)
@@ -1135,19 +1160,22 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     }
     K.o = o;
     if (c->prof_phases) {
-      if (int rc = c->d_prof.ensure(128 + (uint64_t)blocks * 16)) return rc;
-      HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 128 + (uint64_t)blocks * 16, c->stream));
+      if (int rc = c->d_prof.ensure(512 + (uint64_t)blocks * 16)) return rc;
+      HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 512 + (uint64_t)blocks * 16, c->stream));
       K.prof = c->d_prof.as<unsigned long long>();
-      K.wave_t = K.prof + 16;
+      K.wave_t = K.prof + 64;
     }
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(launch_width(B, c->block, c->stream));
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    if (K.proot) HIPCHK(launch_coop_roots(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
+    HIPCHK(hipEventRecord(c->ev[6], c->stream));
     HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[4]));
     if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop kernel done\n", since());
     if (c->prof_phases) {
-      unsigned long long pf[12];
+      unsigned long long pf[40];
       HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
       const char *nm[6] = {"barriers", "commits", "claims", "loads+consume", "levels", "read set-up"};
       double tot = 0;
@@ -1158,6 +1186,22 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
               "%.1f running (%.1f fetching an entry, %.1f in an exact tail)\n", pf[6], pf[6] ? tot / pf[6] : 0.0, pf[7],
               pf[8], pf[6] ? (double)pf[9] / pf[6] : 0.0, pf[6] ? (double)pf[10] / pf[6] : 0.0,
               pf[6] ? (double)pf[11] / pf[6] : 0.0);
+      const double it = pf[6] ? (double)pf[6] : 1.0;
+      fprintf(stderr, "[ibwa_amd] k_coop idle lanes per iteration: barrier %.1f, level drained %.1f, ring %.1f, staging %.1f; "
+              "chains %llu (%.0f per level), %llu discarded at %llu barriers, %llu children committed\n",
+              pf[12] / it, pf[13] / it, pf[14] / it, pf[15] / it, pf[16], pf[8] ? (double)pf[16] / pf[8] : 0.0, pf[17],
+              pf[18], pf[19]);
+      fprintf(stderr, "[ibwa_amd] k_coop iterations (running lanes) by chains per level:");
+      const char *nb[5] = {"<=2", "<=16", "<=64", "<=256", ">256"};
+      for (int q = 0; q < 5; ++q)
+        fprintf(stderr, " %s: %.1f%% (%.1f)", nb[q], 100.0 * pf[20 + q] / it, pf[20 + q] ? (double)pf[25 + q] / pf[20 + q] : 0.0);
+      fprintf(stderr, "\n");
+      fprintf(stderr, "[ibwa_amd] k_coop one-row lane-steps: expanding %.1f%%, exact tail %.1f%% of running; chains by steps:",
+              100.0 * pf[30] / (pf[9] ? pf[9] : 1), 100.0 * pf[31] / (pf[9] ? pf[9] : 1));
+      const char *cb[4] = {"<4", "<16", "<64", ">=64"};
+      for (int q = 0; q < 4; ++q)
+        fprintf(stderr, " %s: %llu (%.1f%% of steps)", cb[q], pf[32 + q], 100.0 * pf[36 + q] / (pf[9] ? pf[9] : 1));
+      fprintf(stderr, "\n");
       // wave end times (shader clock) relative to the first wave start: the pass's tail
       std::vector<unsigned long long> wt((size_t)blocks * 2);
       HIPCHK(hipMemcpy(wt.data(), K.wave_t, wt.size() * 8, hipMemcpyDeviceToHost));
@@ -1208,10 +1252,28 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
               why[1], why[2], why[3], why[4], why[5]);
       fprintf(stderr, "[ibwa_amd] coop pass: %lld reads, %zu handed on, max %u wave iterations, %u pages, %.1f ms\n",
               (long long)lanes, next.size(), mx, pages, a);
+      if (K.proot) {
+        unsigned long long used = 0;
+        HIPCHK(hipMemcpy(&used, K.pstore_next, 8, hipMemcpyDeviceToHost));
+        std::vector<uint4> pr((size_t)lanes * 2);
+        HIPCHK(hipMemcpy(pr.data(), K.proot, pr.size() * 16, hipMemcpyDeviceToHost));
+        int64_t fl[3] = {0, 0, 0};
+        for (const uint4 &q : pr) ++fl[q.w < 3 ? q.w : 2];
+        fprintf(stderr, "[ibwa_amd] coop roots: %.1f children per chain stored (%llu of %llu entries), chains: %lld done, "
+                "%lld hit, %lld skipped\n", (double)used / (double)pr.size(), used, (unsigned long long)K.pstore_cap,
+                (long long)fl[0], (long long)fl[1], (long long)fl[2]);
+      }
     }
     if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop results on host\n", since());
     c->stats.n_coop = lanes - (int64_t)next.size();
     c->stats.ms_coop = a;
+    {
+      float w = 0, rt = 0;
+      HIPCHK(hipEventElapsedTime(&w, c->ev[3], c->ev[5]));
+      HIPCHK(hipEventElapsedTime(&rt, c->ev[5], c->ev[6]));
+      c->stats.ms_coop_width = w;
+      c->stats.ms_coop_roots = rt;
+    }
     todo.swap(next);
     where.swap(next_where);
   }

@@ -99,6 +99,12 @@ def test_exact_reads_round_trip(mid_genome):
     # ... including reads cut off by max_entries (bwtgap.c:138), which it resolves itself ...
     (["-m", "300"], 100, 0.02, 8_000, {"gap_iter_budget": 1}),
     (["-m", "2000"], 150, 0.02, 4_000, {"gap_iter_budget": 1}),
+    # ... with level 0 run by k_coop_roots (the default) or by k_coop itself, under other options
+    ([], 100, 0.01, 30_000, {"gap_iter_budget": 1, "coop_roots": 0}),
+    (["-m", "300"], 100, 0.02, 8_000, {"gap_iter_budget": 1, "coop_roots": 0}),
+    (["-N", "-n", "2"], 100, 0.01, 4_000, {"gap_iter_budget": 1}), (["-L"], 100, 0.02, 8_000, {"gap_iter_budget": 1}),
+    (["-c"], 100, 0.02, 8_000, {"gap_iter_budget": 1}), (["-l", "20", "-k", "1"], 100, 0.02, 8_000, {"gap_iter_budget": 1}),
+    (["-n", "1"], 100, 0.01, 8_000, {"gap_iter_budget": 1}), (["-i", "0", "-d", "0"], 70, 0.02, 8_000, {"gap_iter_budget": 1}),
     # ... or, with it off, to the sequential wide kernel
     ([], 100, 0.01, 8_000, {"gap_iter_budget": 1, "gap_coop": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
@@ -106,7 +112,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
     o, e = eopt(argv)
     defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
-                "gap_iter_budget": 8000, "gap_coop": 1}
+                "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
