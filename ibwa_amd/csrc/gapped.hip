@@ -50,6 +50,16 @@ namespace {
 
 constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_NONSTOP = 0x10;
 constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
+// Gap group (first pass): a gap-opening expansion pushes the insertion child and then the non-empty
+// deletion children into one bucket, consecutively (bwtgap.c:221-227), and measured on a
+// GRCh37-sized genome 95 % of them are never popped (they score a gap open above the first hit).
+// The group is stored as ONE entry: the insertion child with the deletions still pending (z bits
+// 16-19 by symbol, ldp = i), in state STATE_G.  Popping it materializes its top deletion (T before G
+// before C before A) from its own Occ blocks -- the deletions' intervals are the symbol steps of
+// the group's (k, l) -- as the new candidate on top of the group, which keeps the rest; once none
+// is left it is the plain insertion child.  Pop order and stack size (a group counts as all of its
+// entries) are the reference's; a write per deletion is saved for every group never popped.
+constexpr int STATE_G = 3;
 // per-lane LDS stack of popped slots awaiting reuse (the retry pass's heavy reads get more)
 constexpr int NARROW_FREE_DEPTH = 8;
 constexpr int LW_FREE_DEPTH = 4;  // LDS-width variant: 8 B per lane
@@ -306,6 +316,23 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   auto pleader = [&]() __attribute__((always_inline)) -> bool {
     return PROF && lane == __builtin_ctzll(__builtin_amdgcn_read_exec());
   };
+  // a free page of this workgroup's pool for the lane's next slots
+  auto take_page = [&]() __attribute__((always_inline)) -> bool {
+    for (int w = 0; w < bm_words; ++w) {
+      uint32_t x = bitmap[w];
+      while (x != 0xFFFFFFFFu) {
+        const uint32_t bit = (uint32_t)__builtin_ctz(~x);
+        const uint32_t old = atomicOr(&bitmap[w], 1u << bit);
+        if (!(old & (1u << bit))) {
+          ptab_at(n_pages) = (uint16_t)(w * 32 + bit);
+          ++n_pages;
+          return true;
+        }
+        x = old | (1u << bit);
+      }
+    }
+    return false;
+  };
   auto end_read = [&](uint32_t stat) __attribute__((always_inline)) {
     const bool pl_ = pleader();
     int na = stat ? 0 : n_aln;
@@ -474,7 +501,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     if (PROF && lane == 0) ++pf9;
     // ------------------------------------------------ decide this iteration's work
     // search lanes pop C; exact lanes advance one symbol
-    bool do_pop = false, finish = false;
+    bool do_pop = false, finish = false, do_mat = false;
     if (((A.max_iters && n_iter > A.max_iters) ||
          (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries)) &&
         (st == 1 || st == 2)) {
@@ -501,6 +528,8 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         const int e_score = (e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape) & 0x7ff;
         if (!(o.mode & MODE_NONSTOP) && (uint32_t)e_score > (uint32_t)(best_score + o.s_mm)) {
           finish = true;  // bwtgap.c:143 (after the pop; nothing else observes the stack)
+        } else if (!WIDE && state == STATE_G) {
+          do_mat = true;  // a gap group: its top deletion is the entry the reference pops
         } else {
           do_pop = true;
           m = max_diff - (e_mm + e_go);
@@ -574,7 +603,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     const IndexView ixq = st == 2 ? (xa ? ixv0 : ixv1) : ix;
     const uint4 *obq = st == 2 ? (xa ? A.o64[0] : A.o64[1]) : ob;
     const uint32_t qk = st == 2 ? xk : k, ql = st == 2 ? xl : l;
-    const bool qrun = (srch && i > 0) || (st == 2 && xj >= 0);
+    const bool qrun = (srch && i > 0) || (st == 2 && xj >= 0) || do_mat;
     const bool qkneg = qk == 0;
     const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
     Blk bk, bl;
@@ -716,6 +745,46 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       }
       continue;
     }
+    if (do_mat) {
+      // ---- the top deletion of gap group C, from C's blocks: the new candidate, on top of the
+      // group (kept in D with the deletions still pending); nothing is popped, the stack size stays
+      const uint32_t dm = (e.z >> 16) & 15u;
+      const uint32_t c = 31u - (uint32_t)__builtin_clz(dm);
+      const uint32_t dmr = dm & ~(1u << c);
+      // one slot: LDS free stack, free list (its successor is known here), else the bump region
+      uint32_t slot = 0;
+      if (n_free) {
+        --n_free;
+        slot = (uint32_t)free_slots[fsi(n_free)];
+      } else if (fl_head != NILH) {
+        slot = fl_head;
+        fl_head = fl_next;
+        fl_known = fl_head == NILH;
+      } else {
+        const uint32_t skip_at = P0 - HS;
+        slot = bump == skip_at ? bump + HS : bump;  // the bump region skips the hit area
+        const uint32_t b_end = slot + 1;
+        if (b_end > slot_end || (b_end > P0 && ((b_end - 1 - P0) >> LG) >= n_pages && !take_page())) {
+          end_stat = status | ST_STACK_OVERFLOW;
+          st = 3;
+          continue;
+        }
+        bump = b_end;
+      }
+      const uint32_t g_prev = E::prev(e);
+      const uint4 del = E::make(pick4(KK, c), pick4(LL, c), i + 1, i + 1, C_slot, e_mm, e_go, e_ge, a, STATE_D);
+      const uint4 grp = dmr ? E::make(k, l, i, (int)dmr, g_prev, e_mm, e_go, e_ge, a, STATE_G)
+                            : E::make(k, l, i, i, g_prev, e_mm, e_go, e_ge, a, STATE_I);
+      lds_heads[hidx(C_b)] = (H)slot;
+      if ((cfl & 6u) == 6u) *slot_ptr(D_slot) = D;
+      D = grp;  // memory holds the group with its old mask, if at all: dirty
+      D_slot = C_slot;
+      C = del;
+      C_slot = slot;
+      C_valid = true;
+      cfl = 7u;  // C dirty, D valid and dirty
+      continue;
+    }
     if (!do_pop) continue;
     if (m < 0) continue;                                   // bwtgap.c:147
     if (i > 0 && m < (int)bid1) continue;                 // bwtgap.c:155
@@ -774,9 +843,11 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       const uint32_t ner = ((ne4 >> rot) | (ne4 << (4 - rot))) & 15u;
       if (allow_diff && allow_M) vm |= ner << 5;
       else if (csym < 4) vm |= ner & 8u ? 1u << 8 : 0u;  // the match child only
+      // a gap-opening expansion's deletions go into its insertion child's gap group (narrow)
+      const uint32_t dmask = !WIDE && state == STATE_M && (vm & 1u) ? (vm >> 1) & 15u : 0u;
       // slots for all pushes of this expansion; one new page at most (popcount <= 9)
       if (vm) {
-        const uint32_t npush = (uint32_t)__builtin_popcount(vm);
+        const uint32_t npush = (uint32_t)__builtin_popcount(vm & ~(dmask << 1));
         const uint32_t reuse = n_free + (fl_head != NILH ? 1u : 0u);  // fl_known holds here
         const uint32_t nb = npush > reuse ? npush - reuse : 0u;
         uint32_t b_end = bump + nb;
@@ -784,27 +855,10 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         if (b_end > slot_end) {
           status |= ST_STACK_OVERFLOW;
           vm = 0;
-        } else if (b_end > P0 && ((b_end - 1 - P0) >> LG) >= n_pages) {
-          // the expansion reaches a new page: take a free page of this workgroup's pool
-          bool got = false;
-          for (int w = 0; w < bm_words && !got; ++w) {
-            uint32_t x = bitmap[w];
-            while (x != 0xFFFFFFFFu) {
-              const uint32_t bit = (uint32_t)__builtin_ctz(~x);
-              const uint32_t old = atomicOr(&bitmap[w], 1u << bit);
-              if (!(old & (1u << bit))) {
-                ptab_at(n_pages) = (uint16_t)(w * 32 + bit);
-                ++n_pages;
-                got = true;
-                break;
-              }
-              x = old | (1u << bit);
-            }
-          }
-          if (!got) {
-            status |= ST_STACK_OVERFLOW;
-            vm = 0;
-          }
+        } else if (b_end > P0 && ((b_end - 1 - P0) >> LG) >= n_pages && !take_page()) {
+          // the expansion reaches a new page and the workgroup's pool has none
+          status |= ST_STACK_OVERFLOW;
+          vm = 0;
         }
       }
       // push each child (bwtgap.c:216-258, in the reference's order): link it into its bucket and
@@ -827,7 +881,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           status |= ST_STACK_OVERFLOW;
           vm = 0;
         }
-        const uint32_t npush = (uint32_t)__builtin_popcount(vm);
+        const uint32_t npush = (uint32_t)__builtin_popcount(vm & ~(dmask << 1));
         const uint32_t n_fs = npush < n_free ? npush : n_free;  // from the LDS free stack, top down
         const bool use_fl = npush > n_fs && fl_head != NILH;    // one slot of the free list (fl_known)
         const uint32_t fs_top = n_free, fl_slot = fl_head, b0 = bump, skip_at = P0 - HS;
@@ -872,7 +926,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         uint32_t t = 0;
         // ---- gap children (bit 0 insertion, bits 1-4 deletion by A..T): bucket scG, stored in order,
         // each linked to the one before
-        const uint32_t vg = vm & 0x1Fu;
+        const uint32_t vg = vm & 0x1Fu & ~(dmask << 1);  // with a gap group: the group entry alone
         if (vg) {
           if (pleader()) ++pf5;
           const bool tk = !C_valid || scG <= C_b;
@@ -886,7 +940,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
               const uint32_t pk = j == 0 ? k : j == 1 ? KK.x : j == 2 ? KK.y : j == 3 ? KK.z : KK.w;
               const uint32_t pl = j == 0 ? l : j == 1 ? LL.x : j == 2 ? LL.y : j == 3 ? LL.z : LL.w;
               const int pi = j == 0 ? ni : ni + 1;
-              last = E::make(pk, pl, pi, pi, link, e_mm, n_gapo, n_gape, a, j == 0 ? STATE_I : STATE_D);
+              const bool grp = j == 0 && dmask;
+              last = E::make(pk, pl, pi, grp ? (int)dmask : pi, link, e_mm, n_gapo, n_gape, a,
+                             grp ? STATE_G : j == 0 ? STATE_I : STATE_D);
               *slot_ptr(slot) = last;
               link = slot;
             }
@@ -938,7 +994,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
           }
           const uint32_t nb = t - n_fs - fl_n;
           bump = b0 + nb + ((nb && b0 <= skip_at && b0 + nb > skip_at) ? HS : 0u);
-          n_entries += (int)t;
+          n_entries += (int)t + (vm ? __builtin_popcount(dmask) : 0);  // a group counts all its entries
           if (LW) {
             nonempty.m0 |= (has_match ? 1u << (sc_base & (GAP_RING - 1)) : 0u) |
                            (has_mm ? 1u << (scMM & (GAP_RING - 1)) : 0u) | (has_gap ? 1u << (scG & (GAP_RING - 1)) : 0u);

@@ -79,6 +79,7 @@ def lib():
         L.or_free.argtypes = [c.c_void_p]
         L.or_set_stats.argtypes = [c.c_void_p]
         L.or_set_width_touches.argtypes = [c.c_void_p]
+        L.or_push_kinds.argtypes = [c.c_void_p]
         L.or_exact_touches.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p, c.c_void_p,
                                        c.c_int, c.c_int, c.c_int, c.c_void_p]
         L.or_aln_local_core.restype = c.c_int
@@ -323,6 +324,21 @@ def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False
     L.or_free(ptr)
     alns = np.frombuffer(buf, dtype=ALN_DTYPE).copy()
     return n_aln, alns, tch
+
+
+PUSH_KINDS = ("root", "ins_open", "del_open", "ins_ext", "del_ext", "mismatch", "match")
+
+
+def push_kinds(reset=False):
+    """Instrumentation: {kind: (pushes, pops, expansions)} summed over the restated bwt_match_gap
+    calls since the last reset (which this call does after reading, with reset=True)."""
+    L = lib()
+    out = np.zeros(3 * len(PUSH_KINDS), dtype=np.uint64)
+    L.or_push_kinds(out.ctypes.data)
+    if reset:
+        L.or_push_kinds_reset()
+    n = len(PUSH_KINDS)
+    return {k: (int(out[i]), int(out[n + i]), int(out[2 * n + i])) for i, k in enumerate(PUSH_KINDS)}
 
 
 def exact_touches(bwt0, bwt1, seqs, offs, lens, mode, K=0, jump=False):

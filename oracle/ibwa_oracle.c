@@ -283,7 +283,28 @@ typedef struct {
 	int i, a, state, n_mm, n_gapo, n_gape, last_diff_pos, score;
 	int phantom; /* instrumentation: can never be expanded (see gs_push) */
 	int mc;      /* instrumentation: a match child (popped right after its parent's expansion) */
+	int kind;    /* instrumentation: what pushed it (OR_K_*) */
 } entry_t;
+
+/* instrumentation: pushes / pops / expansions by kind of entry, summed over all searches since the
+ * last or_push_kinds_reset (relaxed atomics; diagnostics for the GPU stack design) */
+enum { OR_K_ROOT, OR_K_INS_OPEN, OR_K_DEL_OPEN, OR_K_INS_EXT, OR_K_DEL_EXT, OR_K_MISMATCH, OR_K_MATCH, OR_K_N };
+static uint64_t g_kind_push[OR_K_N], g_kind_pop[OR_K_N], g_kind_exp[OR_K_N];
+void or_push_kinds_reset(void)
+{
+	memset(g_kind_push, 0, sizeof g_kind_push);
+	memset(g_kind_pop, 0, sizeof g_kind_pop);
+	memset(g_kind_exp, 0, sizeof g_kind_exp);
+}
+void or_push_kinds(uint64_t out[3 * OR_K_N])
+{
+	int i;
+	for (i = 0; i < OR_K_N; ++i) {
+		out[i] = __atomic_load_n(&g_kind_push[i], __ATOMIC_RELAXED);
+		out[OR_K_N + i] = __atomic_load_n(&g_kind_pop[i], __ATOMIC_RELAXED);
+		out[2 * OR_K_N + i] = __atomic_load_n(&g_kind_exp[i], __ATOMIC_RELAXED);
+	}
+}
 
 typedef struct { int n, m; entry_t *e; } bucket_t;
 #define OR_CHAIN_W 64
@@ -296,6 +317,7 @@ typedef struct {
 	/* match chains (a popped non-match-child entry and its run of match children + tail):
 	 * rounds = sum over windows of W consecutive chains of one level of the longest chain */
 	uint32_t chains, rounds, next_mc, ch_len, win_n, win_max, win_level;
+	int next_kind; /* instrumentation: kind of the next push (OR_K_*) */
 	uint32_t *chl, chl_n, chl_m; /* chain (length << 11 | level) in pop order, when stats are on */
 	uint64_t *hset; uint32_t hcap, hn; /* distinct (a,i,k,l) expansions, when stats are on */
 } gstack_t;
@@ -391,6 +413,8 @@ static void gs_push(gstack_t *s, int a, int i, uint32_t k, uint32_t l, int n_mm,
 	p->n_mm = n_mm & 0xff; p->n_gapo = n_gapo & 0xff; p->n_gape = n_gape & 0xff;
 	p->last_diff_pos = ldp;
 	p->mc = s->next_mc; s->next_mc = 0;
+	p->kind = s->next_kind; s->next_kind = OR_K_MISMATCH;
+	__atomic_add_fetch(&g_kind_push[p->kind], 1, __ATOMIC_RELAXED);
 	p->score = score & 0x7ff; /* info = score<<21 keeps 11 bits */
 	/* phantom: more diffs than the (non-increasing) max_diff allows, or a score the
 	 * search stops at once a hit has fixed best_score -- such entries are only counted */
@@ -409,6 +433,7 @@ static void gs_pop(gstack_t *s, entry_t *e)
 	bucket_t *q = s->b + s->best;
 	++s->pops;
 	*e = q->e[q->n - 1];
+	__atomic_add_fetch(&g_kind_pop[e->kind], 1, __ATOMIC_RELAXED);
 	if (!e->phantom) --s->n_real;
 	if (!e->mc && s->hset) { /* a chain starts: record the previous one */
 		if (s->chains) {
@@ -472,7 +497,9 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 	stack->md_now = max_diff;
 	stack->score_cap = 0x7fffffff;
 	stack->gape = (opt->mode & OR_MODE_GAPE) != 0;
+	stack->next_kind = OR_K_ROOT;
 	gs_push(stack, 0, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
+	stack->next_kind = OR_K_ROOT;
 	gs_push(stack, 1, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
 
 	while (stack->n_entries) {
@@ -548,6 +575,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 
 		--i;
 		++stack->expansions;
+		__atomic_add_fetch(&g_kind_exp[e.kind], 1, __ATOMIC_RELAXED);
 		gs_note_exp(stack, a, i, k, l);
 		twoocc4_t(bwt, k - 1, l, ck, cl, t);
 		occ = l - k + 1;
@@ -565,20 +593,25 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 		if (allow_diff && i >= opt->indel_end_skip + tmp && len - i >= opt->indel_end_skip + tmp) {
 			if (e.state == ST_M) {
 				if (e.n_gapo < opt->max_gapo) {
+					stack->next_kind = OR_K_INS_OPEN;
 					gs_push(stack, a, i, k, l, e.n_mm, e.n_gapo + 1, e.n_gape, ST_I, i, opt);
 					for (j = 0; j != 4; ++j) {
 						uint32_t kk = bwt->L2[j] + ck[j] + 1, ll = bwt->L2[j] + cl[j];
+						stack->next_kind = OR_K_DEL_OPEN;
 						if (kk <= ll) gs_push(stack, a, i + 1, kk, ll, e.n_mm, e.n_gapo + 1, e.n_gape, ST_D, i + 1, opt);
 					}
 				}
 			} else if (e.state == ST_I) {
-				if (e.n_gape < opt->max_gape)
+				if (e.n_gape < opt->max_gape) {
+					stack->next_kind = OR_K_INS_EXT;
 					gs_push(stack, a, i, k, l, e.n_mm, e.n_gapo, e.n_gape + 1, ST_I, i, opt);
+				}
 			} else if (e.state == ST_D) {
 				if (e.n_gape < opt->max_gape) {
 					if (e.n_gape + e.n_gapo < max_diff || occ < (uint32_t)opt->max_del_occ) {
 						for (j = 0; j != 4; ++j) {
 							uint32_t kk = bwt->L2[j] + ck[j] + 1, ll = bwt->L2[j] + cl[j];
+							stack->next_kind = OR_K_DEL_EXT;
 							if (kk <= ll) gs_push(stack, a, i + 1, kk, ll, e.n_mm, e.n_gapo, e.n_gape + 1, ST_D, i + 1, opt);
 						}
 					}
@@ -591,6 +624,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 				int is_mm = (j != 4 || str[i] > 3);
 				uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
 				stack->next_mc = !is_mm;
+				stack->next_kind = is_mm ? OR_K_MISMATCH : OR_K_MATCH;
 				if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm + is_mm, e.n_gapo, e.n_gape, ST_M,
 				                      is_mm ? i : e.last_diff_pos, opt);
 			}
@@ -598,6 +632,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 			int c = str[i] & 3;
 			uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
 			stack->next_mc = 1;
+			stack->next_kind = OR_K_MATCH;
 			if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm, e.n_gapo, e.n_gape, ST_M, e.last_diff_pos, opt);
 		}
 	}
