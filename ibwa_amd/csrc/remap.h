@@ -1,16 +1,14 @@
-// remap.h -- iBWA's compound-sequence remapping (`sampe -R`) and the multi-reference database set
-// of `sampe <pri> <1.sai> <2.sai> <1.fq> <2.fq> [<alt> <a1.sai> <a2.sai> ...]`, host side:
+// remap.h -- iBWA's compound-sequence remapping (`sampe -R`), host side:
 //   * the .remap table of an alternate reference (load_remappings / read_mapping_extract,
-//     bwaremap.cpp:42-127): per alternate sequence, its target sequence in the primary, the
-//     1-based region it replaces (or `exact`) and the alt-vs-primary CIGAR;
-//   * position projection (remap_cigar, bwa_remap_position[_with_seqid], bwaremap.cpp:170-311)
-//     and the "identical remapping" test (is_remapped_sequence_identical, :129-168);
-//   * CIGAR projection of a read aligned to an alternate sequence (translate_cigar,
-//     translate_cigar.cpp:1-356);
-//   * the database set: references concatenated at their offsets (dbset_restore, dbset.c:135-176),
-//     coord2idx / dbset_extract_sequence / dbset_extract_remapped / dbset_coor_pac2real
-//     (dbset.c:17-39, :248-325).
-// Reference quirks are kept, including the fatal errors (message + abort, as err_fatal).
+//     bwaremap.cpp:42-141): per alternate sequence, its target sequence in the primary, the
+//     1-based region it replaces (or `exact`) and the alternate-vs-primary CIGAR;
+//   * a walk over that CIGAR, run by run (walk_alt), which serves the position projection
+//     (remap_cigar, bwaremap.cpp:170-238) and the "identical remapping" test
+//     (is_remapped_sequence_identical, :129-168);
+//   * the CIGAR projection of a read aligned to an alternate sequence (translate_cigar,
+//     translate_cigar.cpp:342-356), a table-driven merge of the two CIGARs.
+// The reference's observable behaviour is kept, quirks included (noted where they occur), and its
+// fatal errors (message + abort, as err_fatal).
 #ifndef IBWA_REMAP_H
 #define IBWA_REMAP_H
 #include <errno.h>
@@ -20,8 +18,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <memory>
-#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -47,46 +45,42 @@ struct Mapping {
   int n_gapo = 0;
 };
 
-// can_remap (bwaremap.cpp:17-26): exactly one '-' and two '|'
-inline bool can_remap(const char *str) {
-  int ndash = 0, npipe = 0;
-  for (; *str; ++str) {
-    if (*str == '-') ++ndash;
-    if (*str == '|') ++npipe;
-  }
-  return ndash == 1 && npipe == 2;
-}
-
-// read_mapping_extract (bwaremap.cpp:102-141): "name-target|start|stop" or "name-target|exact..."
+// The header of a .remap entry, "<name>-<target>|<start>|<stop>" or "<name>-<target>|exact..."
+// (bwaremap.cpp:16-26, :102-141): the text must hold exactly one '-' and two '|'; the target runs
+// from after the '-' to the first '|' and may not be empty; start / stop are 1-based inclusive
+// (read with strtoul, so leading blanks and a sign pass as there) and end the text.
 inline bool read_mapping_extract(const char *str, Mapping &m) {
   m.exact = 0;
-  if (!can_remap(str)) return false;
-  const char *beg = strchr(str, '-');
-  if (!beg) return false;
-  ++beg;
-  const char *end = strchr(beg, '|');
-  if (beg == end || !end) return false;
-  m.seqname.assign(beg, end);
-  beg = end + 1;
-  if (strncmp("exact", beg, 5) == 0) {
+  const std::string h(str);
+  if (std::count(h.begin(), h.end(), '-') != 1 || std::count(h.begin(), h.end(), '|') != 2) return false;
+  const size_t t0 = h.find('-') + 1, t1 = h.find('|', t0);
+  if (t1 == std::string::npos || t1 == t0) return false;
+  m.seqname = h.substr(t0, t1 - t0);
+  const char *f = str + t1 + 1;  // the fields after the target
+  if (strncmp(f, "exact", 5) == 0) {
     m.exact = 1;
     m.start = m.stop = 0;
     m.has_cigar = false;
     return true;
   }
-  char *e = nullptr;
-  m.start = (uint32_t)strtoul(beg, &e, 10);
-  if (e == beg || *e != '|') return false;
-  --m.start;
-  beg = e + 1;
-  m.stop = (uint32_t)strtoul(beg, &e, 10) + 1;  // one past the last base
-  if (e == beg || *e != '\0') return false;
+  // two numeric fields, the first closed by '|', the second by the end of the text
+  uint32_t v[2];
+  const char closer[2] = {'|', '\0'};
+  for (int q = 0; q < 2; ++q) {
+    char *e = nullptr;
+    v[q] = (uint32_t)strtoul(f, &e, 10);
+    if (e == f || *e != closer[q]) return false;
+    f = e + 1;
+  }
+  m.start = v[0] - 1;  // 0-based first base
+  m.stop = v[1] + 1;   // one past the last base
   return true;
 }
 
-// load_remappings (bwaremap.cpp:42-100): -1 error, 0 no file, 1 loaded.  Entries are assigned to
-// the sequences in file order (the i-th entry is sequence i's mapping).  The std::getline /
-// eof() loop is emulated exactly: a last header line without a newline is not read.
+// load_remappings (bwaremap.cpp:42-100): -1 error, 0 no file, 1 loaded.  The file is a FASTA-like
+// list: a header per alternate sequence, in sequence order, then its CIGAR over any number of lines.
+// The reference reads it with std::getline and stops at end-of-file, so a header is taken only when
+// a newline ends it (a last header without one is ignored); a last CIGAR line counts either way.
 inline int load_remappings(const std::string &path, int n_seqs, std::vector<std::unique_ptr<Mapping>> &maps) {
   FILE *fp = fopen(path.c_str(), "r");
   if (!fp) {
@@ -102,344 +96,266 @@ inline int load_remappings(const std::string &path, int n_seqs, std::vector<std:
   }
   maps.clear();
   maps.resize(n_seqs);
-  size_t at = 0;
-  bool eofbit = false;
-  auto getline = [&](std::string &out) -> bool {  // std::getline on an ifstream
-    out.clear();
-    if (at >= data.size()) {
-      eofbit = true;
-      return false;  // nothing extracted: failbit
-    }
-    const size_t e = data.find('\n', at);
-    if (e == std::string::npos) {
-      out = data.substr(at);
-      at = data.size();
-      eofbit = true;
-      return true;
-    }
-    out = data.substr(at, e - at);
-    at = e + 1;
-    return true;
-  };
-  std::string line;
-  if (!getline(line)) {
+  if (data.empty()) {
     fprintf(stderr, "Empty remapping file '%s'\n", path.c_str());
     return -1;
   }
-  long lineNum = 0;
-  int i = 0;
-  while (!eofbit) {
-    ++lineNum;
-    const char c0 = line.empty() ? '\0' : line[0];
-    if (c0 != '>') {
-      fprintf(stderr, "Unexpected character '%c' at start of line %ld in file '%s'. Expected '>'.\n", c0, lineNum,
-              path.c_str());
+  // the lines, and whether a newline ends each
+  std::vector<std::pair<std::string, bool>> lines;
+  for (size_t at = 0; at < data.size();) {
+    const size_t e = data.find('\n', at);
+    const bool nl = e != std::string::npos;
+    lines.emplace_back(data.substr(at, (nl ? e : data.size()) - at), nl);
+    at = nl ? e + 1 : data.size();
+  }
+  auto is_header = [](const std::string &x) { return !x.empty() && x[0] == '>'; };
+  int n = 0;
+  for (size_t h = 0; h < lines.size() && lines[h].second;) {  // h: a header line
+    const std::string &hdr = lines[h].first;
+    if (!is_header(hdr)) {
+      fprintf(stderr, "Unexpected character '%c' at start of line %zu in file '%s'. Expected '>'.\n",
+              hdr.empty() ? '\0' : hdr[0], h + 1, path.c_str());
       return -1;
     }
-    if (i >= n_seqs) {  // the reference writes past its array here
+    if (n >= n_seqs) {  // the reference writes past its array here
       fprintf(stderr, "More remappings than sequences in '%s'\n", path.c_str());
       return -1;
     }
-    maps[i].reset(new Mapping);
-    if (!read_mapping_extract(line.c_str() + 1, *maps[i])) {
-      fprintf(stderr, "Failed to extract read mapping from string '%s' in file %s, line %ld\n", line.c_str() + 1,
-              path.c_str(), lineNum);
+    Mapping *m = new Mapping;
+    maps[n].reset(m);
+    if (!read_mapping_extract(hdr.c_str() + 1, *m)) {
+      fprintf(stderr, "Failed to extract read mapping from string '%s' in file %s, line %zu\n", hdr.c_str() + 1,
+              path.c_str(), h + 1);
       return -1;
     }
-    std::string cigar;
-    while (getline(line) && !(!line.empty() && line[0] == '>')) {
-      ++lineNum;
-      cigar += line;
-    }
-    maps[i]->cigar = cigar;  // also for `exact` entries (an empty string)
-    maps[i]->has_cigar = true;
-    ++lineNum;
-    int go = 0;
-    for (char ch : cigar) go += ch == 'I' || ch == 'D' || ch == 'N';  // cigar_gap_opens (bwaremap.cpp:28-36)
-    maps[i]->n_gapo = go;
-    ++i;
+    size_t nx = h + 1;  // the CIGAR: every line up to the next header
+    for (; nx < lines.size() && !is_header(lines[nx].first); ++nx) m->cigar += lines[nx].first;
+    m->has_cigar = true;  // also for `exact` entries (an empty string)
+    m->n_gapo = (int)std::count_if(m->cigar.begin(), m->cigar.end(),
+                                   [](char ch) { return ch == 'I' || ch == 'D' || ch == 'N'; });  // cigar_gap_opens
+    ++n;
+    h = nx;
   }
   return 1;
 }
 
-// is_remapped_sequence_identical (bwaremap.cpp:129-168)
-inline int is_remapped_sequence_identical(const Mapping &m, uint32_t start, uint32_t len) {
-  uint32_t pos = 0, last_len = 0;
-  const char *cigar = m.cigar.c_str();
-  char last_op = 0;
-  if (m.exact) return 1;
-  while (pos <= start && *cigar) {
-    char *end;
-    last_len = (uint32_t)strtoul(cigar, &end, 10);
-    if (end == cigar) {
-      fprintf(stderr, "[remap_coordinates] expected number in cigar string '%s' at pos %ld\n", m.cigar.c_str(),
-              (long)(cigar - m.cigar.c_str()));
-      return 0;
-    }
-    cigar = end;
-    last_op = *cigar;
-    switch (last_op) {
-      case 'M': case 'X': case '=': case 'N': case 'D': pos += last_len; break;
-      case 'I': break;
-      default: fprintf(stderr, "invalid cigar character '%c'\n", last_op); return 0;
-    }
-    cigar++;
+// ---------------------------------------------------------------- the alternate's CIGAR against the primary
+// Its text is read run by run ("<digits><op>", strtoul), lazily as the reference's loops read it: a
+// malformed run is an error only for a walk that gets to it.  Each op moves the position on the
+// alternate, on the primary, or both.
+enum : int { ADV_ALT = 1, ADV_PRI = 2 };
+inline int run_moves(char op) {
+  switch (op) {
+    case 'M': case 'X': case '=': return ADV_ALT | ADV_PRI;
+    case 'I': return ADV_ALT;
+    case 'N': case 'D': return ADV_PRI;
+    default: return -1;
   }
-  if (pos > start) return (last_op == 'M' || last_op == '=') && last_len - start > len;
-  if (pos == last_len) {
-    fprintf(stderr, "failed to parse cigar string '%s'\n", m.cigar.c_str());
-    return 0;
-  }
-  return 0;
 }
 
-// remap_cigar (bwaremap.cpp:170-238): the target offset of alternate position pos
-inline int remap_cigar(const char *cigar, uint32_t *result, uint32_t pos, uint32_t seqlen) {
-  const char *p = cigar;
-  uint32_t altpos = 0, refpos = 0, last_len = 0;
+// The runs of `text` taken while keep(walk) holds before a run (bwaremap.cpp:140-166, :180-207):
+// positions after them, and the last run taken.  error: a run did not parse (message printed).
+struct AltWalk {
+  uint32_t alt = 0, pri = 0, last_len = 0;
   char last_op = 0;
+  bool error = false;
+};
+template <class Keep>
+inline AltWalk walk_alt(const char *text, Keep keep) {
+  AltWalk w;
+  for (const char *p = text; *p && keep(w);) {
+    char *e;
+    const uint32_t n = (uint32_t)strtoul(p, &e, 10);
+    const int mv = e == p ? 0 : run_moves(*e);
+    if (e == p) fprintf(stderr, "[remap_coordinates] expected number in cigar string '%s' at pos %ld\n", text, (long)(p - text));
+    else if (mv < 0) fprintf(stderr, "invalid cigar character '%c'\n", *e);
+    if (mv <= 0) {
+      w.error = true;
+      return w;
+    }
+    w.last_len = n;
+    w.last_op = *e;
+    if (mv & ADV_ALT) w.alt += n;
+    if (mv & ADV_PRI) w.pri += n;
+    p = e + 1;
+  }
+  return w;
+}
+
+// is_remapped_sequence_identical (bwaremap.cpp:129-168): whether the alternate is the primary
+// unchanged over the read -- an exact remapping, or the run reaching past `start` on the primary
+// is a match run with last_len - start > len (the reference's own test, unsigned, kept as is)
+inline int is_remapped_sequence_identical(const Mapping &m, uint32_t start, uint32_t len) {
+  if (m.exact) return 1;
+  const AltWalk w = walk_alt(m.cigar.c_str(), [&](const AltWalk &x) { return x.pri <= start; });
+  if (w.error || w.pri <= start) return 0;
+  return (w.last_op == 'M' || w.last_op == '=') && w.last_len - start > len;
+}
+
+// remap_cigar (bwaremap.cpp:170-238): the primary offset of alternate position pos
+inline int remap_cigar(const char *cigar, uint32_t *result, uint32_t pos, uint32_t seqlen) {
   if (pos >= seqlen) {
     fprintf(stderr, "[remap_coordinates] requested pos %u > sequence length %u\n", pos, seqlen);
     return 0;
   }
-  while (altpos <= pos && *p) {
-    char *end;
-    last_len = (uint32_t)strtoul(p, &end, 10);
-    if (end == p) {
-      fprintf(stderr, "[remap_coordinates] expected number in cigar string '%s' at pos %ld\n", cigar, (long)(p - cigar));
-      return 0;
-    }
-    p = end;
-    last_op = *p;
-    switch (last_op) {
-      case 'M': case 'X': case '=': refpos += last_len; altpos += last_len; break;
-      case 'N': case 'D': refpos += last_len; break;
-      case 'I': altpos += last_len; break;
-      default: fprintf(stderr, "invalid cigar character '%c'\n", last_op); return 0;
-    }
-    p++;
-  }
-  if (altpos > seqlen) {
-    fprintf(stderr, "[remap_coordinates] cigar '%s' string implies length > read mapping (%u vs %u)\n", cigar, altpos,
+  const AltWalk w = walk_alt(cigar, [&](const AltWalk &x) { return x.alt <= pos; });
+  if (w.error) return 0;
+  if (w.alt > seqlen) {
+    fprintf(stderr, "[remap_coordinates] cigar '%s' string implies length > read mapping (%u vs %u)\n", cigar, w.alt,
             seqlen);
     return 0;
   }
-  if (altpos == pos) {
-    *result = refpos;
-    return 1;
-  } else if (altpos > pos) {
-    switch (last_op) {
-      case 'M': case 'X': case '=': *result = refpos - (altpos - pos); break;
-      case 'I': *result = refpos; break;
-      default: fprintf(stderr, "Error remapping cigar string %s:, pos=%u\n", cigar, pos); return 0;
-    }
-  } else {
+  if (w.alt < pos) {
     fprintf(stderr, "failed to parse cigar string '%s'\n", cigar);
+    return 0;
+  }
+  if (w.alt == pos) {
+    *result = w.pri;
+    return 1;
+  }
+  // pos lies inside the last run: a match run maps it base for base, an insertion to where it starts
+  const int mv = run_moves(w.last_op);
+  if (mv == (ADV_ALT | ADV_PRI)) *result = w.pri - (w.alt - pos);
+  else if (mv == ADV_ALT) *result = w.pri;
+  else {
+    fprintf(stderr, "Error remapping cigar string %s:, pos=%u\n", cigar, pos);
     return 0;
   }
   return 1;
 }
 
-// ---------------------------------------------------------------- translate_cigar (translate_cigar.cpp)
-// A read's CIGAR against an alternate sequence (starting at `start` on it) composed with the
-// alternate's CIGAR against the primary.  bwa_cigar_t: op << 29 | len, ops M I D S N = 0..4.
-class CigarTranslator {
- public:
-  CigarTranslator(const char *seq_cigar, uint32_t start_pos, const uint32_t *read_cigar, int n_cigar, int total_read_len)
-      : seq_cigar_(seq_cigar), p_(seq_cigar), start_pos_(start_pos), rc_(read_cigar), n_(n_cigar),
-        total_read_len_(total_read_len) {
-    seq_advance();
-    read_advance();
-  }
-  std::vector<uint32_t> out;
-
-  void exec() {
-    find_start_pos();
-    if (!rc_) {
-      int len = 0;
-      while (len < total_read_len_ && !eos()) {
-        const int dist = total_read_len_ - len;
-        if (seq_len_ < dist) {
-          push(tr_seqop(seq_op_), seq_len_);
-          len += seq_len_;
-          seq_advance();
-        } else {
-          push(tr_seqop(seq_op_), dist);
-          break;
-        }
-      }
-      return;
-    }
-    while (!eor() && !eos()) {
-      if (seq_len_ == 0) seq_advance();
-      if (read_len_ == 0) read_advance();
-      if (OPS[read_op_] == 'S') {
-        push(read_op_, read_len_);
-        read_len_ = 0;
-        if (!eor()) read_advance();
-        continue;
-      }
-      switch (seq_op_) {
-        case '=': case 'M': case 'X': in_match(); break;
-        case 'I': in_insertion(); break;
-        case 'N': case 'D': in_deletion(); break;
-        default: throw std::runtime_error(std::string("Invalid cigar character: ") + seq_op_);
-      }
-    }
-    while (!eor()) {
-      if (read_len_ == 0) read_advance();
-      if (OPS[read_op_] == 'M' || OPS[read_op_] == 'I' || OPS[read_op_] == 'S') push(tr_seqop('S'), read_len_);
-      read_len_ = 0;
-    }
-  }
-
- private:
-  static constexpr const char *OPS = "MIDSN";
-  const char *seq_cigar_, *p_;
-  uint32_t start_pos_;
-  const uint32_t *rc_;
-  int rci_ = 0, n_;
-  int total_read_len_;
-  uint32_t cpos_ = 0;
-  char seq_op_ = 0;
-  int seq_len_ = 0, read_op_ = 0, read_len_ = 0;
-
-  void push(int op, int len) {  // CigarBuilder::push: merges a run with the previous one
-    const uint32_t c = (uint32_t)op << 29 | (uint32_t)len;
-    if (!out.empty() && (out.back() >> 29) == (uint32_t)op)
-      out.back() = (uint32_t)op << 29 | ((out.back() & 0x1fffffffu) + (uint32_t)len);
-    else
-      out.push_back(c);
-  }
-  static int tr_seqop(char op) {
-    switch (op) {
-      case 'M': return 0;
-      case 'I': return 1;
-      case 'D': return 2;
-      case 'S': return 3;
-      case 'N': return 4;
-      default: throw std::runtime_error(std::string("Unknown cigar operation: ") + op);
-    }
-  }
-  void in_match() {
-    switch (OPS[read_op_]) {
-      case 'M': case 'N': case 'D':
-        if (seq_len_ >= read_len_) {
-          push(read_op_, read_len_);
-          seq_len_ -= read_len_;
-          read_len_ = 0;
-        } else {
-          push(read_op_, seq_len_);
-          read_len_ -= seq_len_;
-          seq_len_ = 0;
-        }
-        break;
-      case 'I':
-        push(read_op_, read_len_);
-        read_len_ = 0;
-        break;
-      default: throw std::runtime_error("Unknown cigar op in read");
-    }
-  }
-  void in_insertion() {
-    switch (OPS[read_op_]) {
-      case 'M':
-        if (seq_len_ < read_len_) {
-          push(1, seq_len_);
-          read_len_ -= seq_len_;
-          seq_len_ = 0;
-        } else {
-          push(1, read_len_);
-          seq_len_ -= read_len_;
-          read_len_ = 0;
-        }
-        break;
-      case 'I':
-        push(read_op_, read_len_);
-        read_len_ = 0;
-        break;
-      case 'N': case 'D':
-        if (seq_len_ > read_len_) {
-          seq_len_ -= read_len_;
-          read_len_ = 0;
-        } else {
-          read_len_ -= seq_len_;
-          seq_len_ = 0;
-        }
-        break;
-      default: throw std::runtime_error("Unknown cigar op in read");
-    }
-  }
-  void in_deletion() {
-    switch (OPS[read_op_]) {
-      case 'M':
-        push(tr_seqop(seq_op_), seq_len_);
-        seq_advance();
-        break;
-      case 'I':
-        push(tr_seqop(seq_op_), seq_len_);
-        seq_advance();
-        push(read_op_, read_len_);
-        read_advance();
-        break;
-      case 'N': case 'D':
-        push(tr_seqop(seq_op_), seq_len_);
-        seq_len_ = 0;
-        break;
-      default: throw std::runtime_error("Unknown cigar op in read");
-    }
-  }
-  void find_start_pos() {
-    while (cpos_ < start_pos_ && !eos()) {
-      if (seq_len_ == 0) seq_advance();
-      const int dist = (int)(start_pos_ - cpos_);
-      switch (seq_op_) {
-        case '=': case 'M': case 'X': case 'I':
-          if (seq_len_ > dist) {
-            seq_len_ -= (int)(start_pos_ - cpos_);
-            cpos_ = start_pos_;
-          } else {
-            cpos_ += (uint32_t)seq_len_;
-            seq_len_ = 0;
-          }
-          break;
-        case 'N': case 'D': seq_len_ = 0; break;
-        default: throw std::runtime_error(std::string("Invalid cigar character: ") + seq_op_);
-      }
-    }
-    if (cpos_ < start_pos_)
-      throw std::runtime_error("Failed to seek to position " + std::to_string(start_pos_) + " in cigar string '" +
-                               std::string(seq_cigar_) + "'");
-  }
-  bool eos() const { return seq_len_ == 0 && *p_ == 0; }
-  bool eor() const { return read_len_ == 0 && rci_ >= n_; }
-  void seq_advance() {
-    char *end;
-    seq_len_ = (int)strtoul(p_, &end, 10);
-    p_ = end;
-    seq_op_ = *p_;
-    if (*p_) ++p_;  // the reference steps past the terminating NUL too (never read again)
-  }
-  void read_advance() {
-    if (!rc_) return;
-    read_len_ = (int)(rc_[rci_] & 0x1fffffffu);
-    read_op_ = (int)(rc_[rci_++] >> 29);
-  }
+// ---------------------------------------------------------------- translate_cigar (translate_cigar.cpp:342-356)
+// A read's CIGAR (bwa_cigar_t: op << 29 | len, ops M I D S N = 0..4) against an alternate sequence,
+// from `start` on it, composed with the alternate's CIGAR against the primary.  The two are merged
+// run against run by the table below; what the reference does past either end (a zero-length run
+// of the last op, deletions counted against an ungapped read's length, the read cursor stepped
+// after an insertion without a bound check) is reproduced, since the SAM output shows it.
+namespace xlat {
+enum Act : uint8_t {
+  EMIT_READ_MIN,   // emit the read's op over min(both); both consume it
+  EMIT_READ_ALL,   // emit the read's op (an insertion) over the read run; the read run ends
+  EMIT_INS_MIN,    // emit an insertion over min(both); both consume it
+  SKIP_MIN,        // both consume min(both), nothing emitted
+  EMIT_ALT_NEXT,   // emit the alternate's op over its run; the next alternate run
+  EMIT_ALT_NEXT_I, // the same, then the read run as an insertion; the next read run
+  EMIT_ALT_END,    // emit the alternate's op over its run; the alternate run ends
+  BAD
 };
+// [alternate run: 0 match (M = X), 1 insertion (I), 2 deletion (D N)][read op M I D S N]; S never
+// reaches the table (a read clip is emitted before)
+constexpr Act ACT[3][5] = {
+    {EMIT_READ_MIN, EMIT_READ_ALL, EMIT_READ_MIN, BAD, EMIT_READ_MIN},
+    {EMIT_INS_MIN, EMIT_READ_ALL, SKIP_MIN, BAD, SKIP_MIN},
+    {EMIT_ALT_NEXT, EMIT_ALT_NEXT_I, EMIT_ALT_END, BAD, EMIT_ALT_END},
+};
+inline int alt_class(char op) { return op == 'M' || op == '=' || op == 'X' ? 0 : op == 'I' ? 1 : op == 'N' || op == 'D' ? 2 : -1; }
+inline int op_code(char op) {  // a CIGAR letter as a bwa_cigar_t op; -1 for '=' / 'X' and others
+  const char *c = strchr("MIDSN", op);
+  return op && c ? (int)(c - "MIDSN") : -1;
+}
+}  // namespace xlat
 
-// translate_cigar (translate_cigar.cpp:342-356): false (message printed) when the translation fails
 inline bool translate_cigar(const std::string &seq_cigar, uint32_t start, const uint32_t *read_cigar, int n_cigar,
                             int read_len, std::vector<uint32_t> &out) {
-  CigarTranslator ct(seq_cigar.c_str(), start, read_cigar, n_cigar, read_len);
-  try {
-    ct.exec();
-    out.swap(ct.out);
-    return true;
-  } catch (const std::exception &e) {
-    fprintf(stderr, "Error translating cigar string: %s\n", e.what());
+  using namespace xlat;
+  out.clear();
+  std::string err;
+  auto emit = [&](int op, int n) {  // runs of one op merge (the length within its 29 bits)
+    if (!out.empty() && (int)(out.back() >> 29) == op)
+      out.back() = (uint32_t)op << 29 | (((out.back() & 0x1fffffffu) + (uint32_t)n) & 0x1fffffffu);
+    else
+      out.push_back((uint32_t)op << 29 | (uint32_t)n);
+  };
+  // the alternate's runs: op '\0' and length 0 once its text is used up
+  const char *ap = seq_cigar.c_str();
+  char a_op = 0;
+  int a_left = 0;
+  auto a_next = [&]() {
+    char *e;
+    a_left = (int)strtoul(ap, &e, 10);
+    ap = e;
+    a_op = *ap;
+    if (*ap) ++ap;
+  };
+  auto a_done = [&]() { return a_left == 0 && *ap == 0; };
+  // the read's runs (the reference reads the next one without a bound check)
+  int r_i = 0, r_op = 0, r_left = 0;
+  auto r_next = [&]() {
+    if (!read_cigar) return;
+    r_left = (int)(read_cigar[r_i] & 0x1fffffffu);
+    r_op = (int)(read_cigar[r_i++] >> 29);
+  };
+  auto r_done = [&]() { return r_left == 0 && r_i >= n_cigar; };
+  auto fail = [&](const std::string &why) {
+    fprintf(stderr, "Error translating cigar string: %s\n", why.c_str());
     out.clear();
     return false;
+  };
+  a_next();
+  r_next();
+  // 1. the alternate's runs up to `start` (an insertion on it counts, a deletion does not)
+  uint32_t at = 0;
+  while (at < start && !a_done()) {
+    if (a_left == 0) a_next();
+    const int cl = alt_class(a_op);
+    if (cl < 0) return fail(std::string("Invalid cigar character: ") + a_op);
+    if (cl == 2) {
+      a_left = 0;
+    } else if ((uint32_t)a_left > start - at) {
+      a_left -= (int)(start - at);
+      at = start;
+    } else {
+      at += (uint32_t)a_left;
+      a_left = 0;
+    }
   }
+  if (at < start)
+    return fail("Failed to seek to position " + std::to_string(start) + " in cigar string '" + seq_cigar + "'");
+  // 2a. an ungapped read: the alternate's runs over the read length
+  if (!read_cigar) {
+    for (int len = 0; len < read_len && !a_done();) {
+      const int op = op_code(a_op);
+      if (op < 0) return fail(std::string("Unknown cigar operation: ") + a_op);
+      const int take = a_left < read_len - len ? a_left : read_len - len;
+      emit(op, take);
+      if (take < a_left) break;
+      len += a_left;
+      a_next();
+    }
+    return !out.empty();
+  }
+  // 2b. both CIGARs run against each other
+  while (!r_done() && !a_done()) {
+    if (a_left == 0) a_next();
+    if (r_left == 0) r_next();
+    if (r_op == 3) {  // a clip of the read passes through
+      emit(3, r_left);
+      r_left = 0;
+      if (!r_done()) r_next();
+      continue;
+    }
+    const int cl = alt_class(a_op);
+    if (cl < 0) return fail(std::string("Invalid cigar character: ") + a_op);
+    const Act act = r_op >= 0 && r_op < 5 ? ACT[cl][r_op] : BAD;
+    const int mn = a_left < r_left ? a_left : r_left;
+    switch (act) {
+      case EMIT_READ_MIN: emit(r_op, mn); a_left -= mn; r_left -= mn; break;
+      case EMIT_READ_ALL: emit(r_op, r_left); r_left = 0; break;
+      case EMIT_INS_MIN: emit(1, mn); a_left -= mn; r_left -= mn; break;
+      case SKIP_MIN: a_left -= mn; r_left -= mn; break;
+      case EMIT_ALT_NEXT: emit(op_code(a_op), a_left); a_next(); break;
+      case EMIT_ALT_NEXT_I: emit(op_code(a_op), a_left); a_next(); emit(r_op, r_left); r_next(); break;
+      case EMIT_ALT_END: emit(op_code(a_op), a_left); a_left = 0; break;
+      default: return fail("Unknown cigar op in read");
+    }
+  }
+  // 3. what is left of the read is clipped (its deletions dropped)
+  while (!r_done()) {
+    if (r_left == 0) r_next();
+    if (r_op == 0 || r_op == 1 || r_op == 3) emit(3, r_left);
+    r_left = 0;
+  }
+  return !out.empty();  // an empty translation is the reference's NULL as well
 }
 
 }  // namespace ibwa_sam

@@ -11,6 +11,13 @@
 //       bns_restore (.ann/.amb/.pac), then coor_pac2real / pac_at over a grid of positions.
 //   host_check chunks <n> <threads>
 //       parallel_chunks coverage: every index visited exactly once.
+//   host_check remap < cases
+//       remap.h (the -R remapping of sampe) on one case per line, one result line each:
+//         H <header>                               read_mapping_extract
+//         R <cigar> <pos> <seqlen>                 remap_cigar
+//         I <cigar> <exact> <start> <len>          is_remapped_sequence_identical
+//         T <cigar> <start> <read cigar|-> <len>   translate_cigar (read CIGAR as text, - for none)
+//         L <file> <n_seqs>                        load_remappings
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -21,6 +28,7 @@
 
 #include "readers.h"
 #include "sam_common.h"
+#include "remap.h"
 
 using namespace ibwa_sam;
 
@@ -93,6 +101,58 @@ int main(int argc, char **argv) {
     for (int64_t i = 0; i < n; ++i)
       if (seen[i] != 1) return 1;
     printf("ok %lld\n", (long long)n);
+    return 0;
+  }
+  if (argc >= 2 && !strcmp(argv[1], "remap")) {
+    char buf[4096];
+    while (fgets(buf, sizeof buf, stdin)) {
+      char kind = buf[0], a[1024] = "", b[1024] = "", c[1024] = "";
+      long x = 0, y = 0, z = 0;
+      if (kind == 'H' && sscanf(buf + 2, "%1023[^\n]", a) >= 0) {
+        Mapping m;
+        if (read_mapping_extract(a, m)) printf("%s %d %u %u\n", m.seqname.c_str(), m.exact, m.start, m.stop);
+        else printf("fail\n");
+      } else if (kind == 'R' && sscanf(buf + 2, "%1023s %ld %ld", a, &x, &y) == 3) {
+        uint32_t r = 0;
+        const int ok = remap_cigar(a[0] == '-' ? "" : a, &r, (uint32_t)x, (uint32_t)y);
+        if (ok) printf("%u\n", r);
+        else printf("fail\n");
+      } else if (kind == 'I' && sscanf(buf + 2, "%1023s %ld %ld %ld", a, &x, &y, &z) == 4) {
+        Mapping m;
+        m.cigar = a[0] == '-' ? "" : a;
+        m.exact = (int)x;
+        printf("%d\n", is_remapped_sequence_identical(m, (uint32_t)y, (uint32_t)z));
+      } else if (kind == 'T' && sscanf(buf + 2, "%1023s %ld %1023s %ld", a, &x, b, &y) == 4) {
+        std::vector<uint32_t> rc;  // the read CIGAR as bwa_cigar_t runs, then one zero run of slack
+        for (const char *p = b; *p && *p != '-';) {
+          char *e;
+          const uint32_t n = (uint32_t)strtoul(p, &e, 10);
+          rc.push_back((uint32_t)(strchr("MIDSN", *e) - "MIDSN") << 29 | n);
+          p = e + 1;
+        }
+        const int n_rc = (int)rc.size();
+        rc.push_back(0);
+        std::vector<uint32_t> out;
+        if (!translate_cigar(a[0] == '-' ? std::string() : std::string(a), (uint32_t)x, b[0] == '-' ? nullptr : rc.data(),
+                             n_rc, (int)y, out)) {
+          printf("fail\n");
+        } else {
+          for (uint32_t v : out) printf("%u%c", v & 0x1fffffffu, "MIDSN"[v >> 29]);
+          printf("\n");
+        }
+      } else if (kind == 'L' && sscanf(buf + 2, "%1023s %ld", c, &x) == 2) {
+        std::vector<std::unique_ptr<Mapping>> maps;
+        const int rv = load_remappings(c, (int)x, maps);
+        printf("%d", rv);
+        if (rv == 1)
+          for (auto &m : maps)
+            if (m) printf(" [%s %d %u %u %s %d]", m->seqname.c_str(), m->exact, m->start, m->stop, m->cigar.c_str(), m->n_gapo);
+            else printf(" []");
+        printf("\n");
+      } else {
+        printf("?\n");
+      }
+    }
     return 0;
   }
   fprintf(stderr, "usage: host_check reads <file> <mode> <trim> [bam_which] | bns <prefix> | chunks <n> <threads>\n");

@@ -33,7 +33,7 @@ def bins():
     out = {}
     for name, flags in FLAVOURS.items():
         exe = os.path.join(OUT, f"host_check_{name}")
-        deps = [SRC] + [os.path.join(ROOT, "ibwa_amd", "csrc", f) for f in ("readers.h", "sam_common.h")]
+        deps = [SRC] + [os.path.join(ROOT, "ibwa_amd", "csrc", f) for f in ("readers.h", "sam_common.h", "remap.h")]
         if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(d) for d in deps):
             subprocess.run(["g++", "-std=c++17", "-g", "-pthread", *flags, "-I", os.path.join(ROOT, "include"),
                             "-I", os.path.join(ROOT, "ibwa_amd", "csrc"), SRC, "-o", exe, "-lz"], check=True)
@@ -122,3 +122,35 @@ def test_bns_and_chunks(bins):
         for n, t in [(0, 4), (1, 8), (255, 3), (100000, 8), (12345, 0)]:
             r = run(exe, "chunks", n, t)
             assert r.returncode == 0 and r.stdout.startswith(b"ok"), (name, n, t)
+
+
+def test_remap_known_answers(bins, tmp_path):
+    """remap.h (sampe -R: read_mapping_extract, remap_cigar, is_remapped_sequence_identical,
+    translate_cigar) on 9 015 cases answered by the reference's own functions
+    (tools/make_remap_unit.py over oracle/_ref/libibwa_ref.so, bwaremap.cpp / translate_cigar.cpp),
+    in the plain, ASan/UBSan and TSan builds."""
+    rows = [ln.rstrip("\n").split("\t") for ln in open(os.path.join(GOLD, "remap_unit.tsv"))]
+    cases = "".join(c + "\n" for c, _ in rows).encode()
+    for name, exe in bins.items():
+        r = subprocess.run([exe, "remap"], input=cases, capture_output=True, env=ENV, timeout=300)
+        assert r.returncode == 0 and b"Sanitizer" not in r.stderr and b"runtime error" not in r.stderr, \
+            (name, r.stderr.decode()[-2000:])
+        got = r.stdout.decode().splitlines()
+        assert len(got) == len(rows)
+        bad = [(c, a, g) for (c, a), g in zip(rows, got) if a != g]
+        assert not bad, (name, bad[:5])
+
+
+@pytest.mark.parametrize("text,n_seqs,expect", [
+    (">a-chr1|1|10\n5M2I3M\n>b-chr1|exact|\n", 2, "1 [chr1 0 0 11 5M2I3M 1] [chr1 1 0 0  0]"),
+    (">a-chr1|1|10\n5M\n2D3M\n>b-chr2|3|4", 2, "1 [chr1 0 0 11 5M2D3M 1] []"),  # an unterminated last header
+    (">a-chr1|1|10\n5M\n3M", 1, "1 [chr1 0 0 11 5M3M 0]"),                       # an unterminated last CIGAR line
+    ("", 1, "-1"), ("x\n", 1, "-1"), (">a-chr1|1|10\n>b-c|1|2\n", 1, "-1"), (">bad\n", 1, "-1"),
+    (">a-chr1|1|10", 1, "1 []")])
+def test_remap_file(bins, tmp_path, text, n_seqs, expect):
+    """load_remappings (bwaremap.cpp:42-100) on .remap texts: headers, multi-line CIGARs, the
+    std::getline end-of-file behaviour, the errors."""
+    f = tmp_path / "x.remap"
+    f.write_text(text)
+    r = subprocess.run([bins["plain"], "remap"], input=f"L {f} {n_seqs}\n".encode(), capture_output=True, timeout=60)
+    assert r.stdout.decode().strip() == expect
