@@ -290,8 +290,10 @@ typedef struct {
  * last or_push_kinds_reset (relaxed atomics; diagnostics for the GPU stack design) */
 enum { OR_K_ROOT, OR_K_INS_OPEN, OR_K_DEL_OPEN, OR_K_INS_EXT, OR_K_DEL_EXT, OR_K_MISMATCH, OR_K_MATCH, OR_K_N };
 static uint64_t g_kind_push[OR_K_N], g_kind_pop[OR_K_N], g_kind_exp[OR_K_N];
+static int g_kinds_on; /* counting is off until the first reset: shared counters would serialise the threads */
 void or_push_kinds_reset(void)
 {
+	g_kinds_on = 1;
 	memset(g_kind_push, 0, sizeof g_kind_push);
 	memset(g_kind_pop, 0, sizeof g_kind_pop);
 	memset(g_kind_exp, 0, sizeof g_kind_exp);
@@ -414,7 +416,7 @@ static void gs_push(gstack_t *s, int a, int i, uint32_t k, uint32_t l, int n_mm,
 	p->last_diff_pos = ldp;
 	p->mc = s->next_mc; s->next_mc = 0;
 	p->kind = s->next_kind; s->next_kind = OR_K_MISMATCH;
-	__atomic_add_fetch(&g_kind_push[p->kind], 1, __ATOMIC_RELAXED);
+	if (g_kinds_on) __atomic_add_fetch(&g_kind_push[p->kind], 1, __ATOMIC_RELAXED);
 	p->score = score & 0x7ff; /* info = score<<21 keeps 11 bits */
 	/* phantom: more diffs than the (non-increasing) max_diff allows, or a score the
 	 * search stops at once a hit has fixed best_score -- such entries are only counted */
@@ -433,7 +435,7 @@ static void gs_pop(gstack_t *s, entry_t *e)
 	bucket_t *q = s->b + s->best;
 	++s->pops;
 	*e = q->e[q->n - 1];
-	__atomic_add_fetch(&g_kind_pop[e->kind], 1, __ATOMIC_RELAXED);
+	if (g_kinds_on) __atomic_add_fetch(&g_kind_pop[e->kind], 1, __ATOMIC_RELAXED);
 	if (!e->phantom) --s->n_real;
 	if (!e->mc && s->hset) { /* a chain starts: record the previous one */
 		if (s->chains) {
@@ -575,7 +577,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 
 		--i;
 		++stack->expansions;
-		__atomic_add_fetch(&g_kind_exp[e.kind], 1, __ATOMIC_RELAXED);
+		if (g_kinds_on) __atomic_add_fetch(&g_kind_exp[e.kind], 1, __ATOMIC_RELAXED);
 		gs_note_exp(stack, a, i, k, l);
 		twoocc4_t(bwt, k - 1, l, ck, cl, t);
 		occ = l - k + 1;

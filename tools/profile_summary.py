@@ -17,7 +17,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-HOT = ("k_exact", "k_pack_reads", "k_gapped", "k_width", "k_search", "k_sw", "k_coop", "k_sa2pos", "k_expand_sa")
+HOT = ("k_exact", "k_pack_reads", "k_gapped", "k_width", "k_search", "k_sw", "k_coop_roots", "k_coop", "k_sa2pos", "k_expand_sa")
 
 
 def short(name):

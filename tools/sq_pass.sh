@@ -17,10 +17,11 @@ n = collections.Counter()
 for f in glob.glob(f"{out}/pmc/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        for h in ("k_gapped", "k_coop", "k_width", "k_exact", "k_sw"):
+        for h in ("k_gapped", "k_coop_roots", "k_coop", "k_width", "k_exact", "k_sw"):
             if h in name:
                 agg[h][r["Counter_Name"]] += float(r["Counter_Value"])
                 n[(h, r["Counter_Name"])] += 1
+                break
 for h, d in agg.items():
     print(h, {k: f"{v:.3g}" for k, v in sorted(d.items())})
 PY
