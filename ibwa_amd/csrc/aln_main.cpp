@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <string>
 #include <thread>
+#include <atomic>
 #include <type_traits>
 #include <vector>
 
@@ -64,6 +65,7 @@ struct Batch {
   std::vector<uint64_t> off;
   std::vector<uint32_t> len;
   int max_len = 0;
+  std::vector<std::pair<long, long>> trims;  // per 0x40000-read batch: bases trimmed, bases read
   int64_t n() const { return (int64_t)len.size(); }
 };
 
@@ -159,9 +161,10 @@ void take_bulk(const FastqBulk &fb, size_t i0, size_t i1, const ReadForm &f, Bat
 
 // Returns 1 with a batch, 0 at the end of the input, -1 on bad options.
 template <class Reader>
-int read_batch(Reader &rd, FastqBulk *fb, int mode, int trim_qual, Batch &b, long *n_trimmed, long *n_tot,
-               bool *eof) {
-  b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0;
+int read_batch(Reader &rd, FastqBulk *fb, int mode, int trim_qual, Batch &b, bool *eof) {
+  b.seq.clear(); b.off.clear(); b.len.clear(); b.max_len = 0; b.trims.clear();
+  long trimmed = 0, total = 0;
+  long *n_trimmed = &trimmed, *n_tot = &total;
   const bool bam = std::is_same<Reader, BamReader>::value;
   const ReadForm f{bam, !bam && (mode & IBWA_MODE_IL13) != 0, bam ? 0 : (int)((unsigned)mode >> 24), trim_qual};
   if (((unsigned)mode >> 24) > 15) {
@@ -185,6 +188,7 @@ int read_batch(Reader &rd, FastqBulk *fb, int mode, int trim_qual, Batch &b, lon
     }
   }
   if ((int)b.len.size() < kSub) read_serial(rd, f, b, n_trimmed, n_tot, eof);
+  b.trims.emplace_back(trimmed, total);
   return b.len.empty() ? 0 : 1;
 }
 
@@ -197,8 +201,8 @@ int batch_key(const ibwa_gap_opt_t &opt, int max_len) {
 // left in `carry` for the next group.  Returns the batches read (0 at the end), -1 on bad input.
 template <class Reader>
 int read_group(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, Batch &g, Batch &sub, Batch &carry,
-               bool &has_carry, long *n_trimmed, long *n_tot, bool *eof) {
-  g.seq.clear(); g.off.clear(); g.len.clear(); g.max_len = 0;
+               bool &has_carry, bool *eof) {
+  g.seq.clear(); g.off.clear(); g.len.clear(); g.max_len = 0; g.trims.clear();
   int nb = 0, key = 0;
   auto append = [&](const Batch &x) {
     const uint64_t base = g.seq.size();
@@ -206,6 +210,7 @@ int read_group(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, Batch &g, B
     for (uint64_t o : x.off) g.off.push_back(base + o);
     g.len.insert(g.len.end(), x.len.begin(), x.len.end());
     g.max_len = std::max(g.max_len, x.max_len);
+    g.trims.insert(g.trims.end(), x.trims.begin(), x.trims.end());
   };
   if (has_carry) {
     std::swap(g, carry);
@@ -214,7 +219,7 @@ int read_group(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, Batch &g, B
     nb = 1;
   }
   while (nb < kGroup) {
-    const int r = read_batch(rd, fb, opt.mode, opt.trim_qual, sub, n_trimmed, n_tot, eof);
+    const int r = read_batch(rd, fb, opt.mode, opt.trim_qual, sub, eof);
     if (r < 0) return -1;
     if (r == 0) break;
     const int k = batch_key(opt, sub.max_len);
@@ -358,10 +363,24 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   for (int g = 0; g < n_gpus; ++g) prep.emplace_back([&, g]() { prep_rc[g] = ibwa_ctx_prepare(ctx[g], &opt); });
   Batch cur, nxt, sub, carry;
   bool has_carry = false;
-  long n_trim = 0, n_tot = 0;
-  int64_t tot_seqs = 0;
   bool eof = false;
-  int have = read_group(rd, fb, opt, cur, sub, carry, has_carry, &n_trim, &n_tot, &eof);
+  double parse_s = 0;  // wall time of the FASTQ parse (all host threads)
+  auto timed_read = [&](Batch &into) {
+    const auto t = std::chrono::steady_clock::now();
+    const int r = read_group(rd, fb, opt, into, sub, carry, has_carry, &eof);
+    parse_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+    return r;
+  };
+  int64_t tot_seqs = 0;
+  std::thread writer;
+  std::atomic<bool> write_failed{false};
+  struct JoinAtExit {  // an early return still waits for the write in flight
+    std::thread &t;
+    ~JoinAtExit() {
+      if (t.joinable()) t.join();
+    }
+  } join_writer{writer};
+  int have = timed_read(cur);
   for (auto &t : prep) t.join();
   for (int g = 0; g < n_gpus; ++g)
     if (prep_rc[g]) return die("prepare the index");
@@ -370,9 +389,9 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     auto t0 = std::chrono::steady_clock::now();
     const int64_t n = cur.n();
     tot_seqs += n;
-    if (opt.trim_qual >= 1 && n_tot)
-      fprintf(stderr, "[bwa_read_seq] %.1f%% bases are trimmed.\n", 100.0f * n_trim / n_tot);
-    n_trim = n_tot = 0;
+    if (opt.trim_qual >= 1)  // once per 0x40000-read batch, as bwa_read_seq (bwaseqio.c:206)
+      for (const auto &t : cur.trims)
+        if (t.second) fprintf(stderr, "[bwa_read_seq] %.1f%% bases are trimmed.\n", 100.0f * t.first / t.second);
     fprintf(stderr, "[bwa_aln_core] calculate SA coordinate... ");
     std::vector<std::vector<int32_t>> g_naln(n_gpus);
     std::vector<ibwa_aln1_t *> g_aln(n_gpus, nullptr);
@@ -408,7 +427,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       });
     }
     // overlap: parse the next batch while the GPUs work
-    int more = read_group(rd, fb, opt, nxt, sub, carry, has_carry, &n_trim, &n_tot, &eof);
+    int more = timed_read(nxt);
     for (auto &t : th) t.join();
     for (int g = 0; g < n_gpus; ++g)
       if (g_rc[g]) return die("aln");
@@ -416,34 +435,50 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fprintf(stderr, "%.2f sec\n", sec);
     fprintf(stderr, "[bwa_aln_core] write to the disk... ");
-    for (int g = 0; g < n_gpus; ++g) {  // bwtaln.c:227-231, input order; one write per slice
-      const ibwa_aln1_t *p = g_aln[g];
-      size_t bytes = 0;
-      for (int32_t k : g_naln[g]) bytes += 4 + (size_t)k * sizeof(ibwa_aln1_t);
-      std::vector<char> buf(bytes);
-      char *w = buf.data();
-      for (int32_t k : g_naln[g]) {
-        memcpy(w, &k, 4);
-        w += 4;
-        if (k) memcpy(w, p, (size_t)k * sizeof(ibwa_aln1_t));
-        w += (size_t)k * sizeof(ibwa_aln1_t);
-        p += k;
-      }
-      if (bytes && fwrite(buf.data(), 1, bytes, out) != bytes) {
-        fprintf(stderr, "[ibwa-amd aln] write failed\n");
-        return 1;
-      }
-      ibwa_free(g_aln[g]);
+    // write-behind: this group's records go out (bwtaln.c:227-231, input order, one write per
+    // slice) while the next group aligns; the previous group's write has finished first
+    if (writer.joinable()) writer.join();
+    if (write_failed) {
+      fprintf(stderr, "[ibwa-amd aln] write failed\n");
+      return 1;
     }
+    writer = std::thread([out, &write_failed, naln = std::move(g_naln), aln = std::move(g_aln)]() {
+      for (size_t g = 0; g < naln.size(); ++g) {
+        const ibwa_aln1_t *p = aln[g];
+        size_t bytes = 0;
+        for (int32_t k : naln[g]) bytes += 4 + (size_t)k * sizeof(ibwa_aln1_t);
+        std::vector<char> buf(bytes);
+        char *w = buf.data();
+        for (int32_t k : naln[g]) {
+          memcpy(w, &k, 4);
+          w += 4;
+          if (k) memcpy(w, p, (size_t)k * sizeof(ibwa_aln1_t));
+          w += (size_t)k * sizeof(ibwa_aln1_t);
+          p += k;
+        }
+        if (bytes && fwrite(buf.data(), 1, bytes, out) != bytes) write_failed = true;
+        ibwa_free(aln[g]);
+      }
+    });
     ph.mark("write");
     fprintf(stderr, "0.00 sec\n");
     fprintf(stderr, "[bwa_aln_core] %lld sequences have been processed.\n", (long long)tot_seqs);
     std::swap(cur, nxt);
     have = more;
   }
+  if (writer.joinable()) writer.join();
+  if (write_failed) {
+    fprintf(stderr, "[ibwa-amd aln] write failed\n");
+    return 1;
+  }
   if (out != stdout) fclose(out);
   for (auto *x : ctx) ibwa_ctx_destroy(x);
   if (have < 0) return 1;
   ph.print("ibwa-amd aln");
+  if (parse_s > 0) {
+    const int nt = fb ? ibwa_sam::host_threads() : 1;
+    fprintf(stderr, "[ibwa-amd aln] input parse: %lld reads in %.2f s on %d host threads = %.2f M reads/s (%.3f M per thread)\n",
+            (long long)tot_seqs, parse_s, nt, tot_seqs / parse_s / 1e6, tot_seqs / parse_s / 1e6 / nt);
+  }
   return 0;
 }

@@ -260,9 +260,30 @@ struct PacSeg {
   const uint8_t *pac;
   uint64_t offset, l_pac;
 };
+int host_threads_c() {  // as ibwa_sam::host_threads
+  const char *e = getenv("OMP_NUM_THREADS");
+  int n = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(n, 32));
+}
+
 struct PacSet {
   std::vector<PacSeg> seg;
   uint64_t l_pac = 0;
+  // bases [x, x + n) as 2-bit codes: unpacked from one reference's .pac when the window lies in it
+  void extract(uint64_t x, uint32_t n, uint8_t *out) const {
+    size_t j = seg.size() - 1;
+    while (j > 0 && seg[j].offset > x) --j;
+    const uint64_t p0 = x - seg[j].offset;
+    if (p0 + n > seg[j].l_pac) {  // crosses into a hole or the next reference: base by base
+      for (uint32_t t = 0; t < n; ++t) out[t] = at(x + t);
+      return;
+    }
+    const uint8_t *pac = seg[j].pac;
+    for (uint32_t t = 0; t < n; ++t) {
+      const uint64_t p = p0 + t;
+      out[t] = (pac[p >> 2] >> ((~p & 3) << 1)) & 3;  // bns_pac (bntseq.h)
+    }
+  }
   uint8_t at(uint64_t x) const {
     size_t j = seg.size() - 1;
     while (j > 0 && seg[j].offset > x) --j;
@@ -344,66 +365,110 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
   n_tot[0] = n_tot[1] = n_mapped[0] = n_mapped[1] = 0;
   if (!popt->is_sw || ii->avg < 0.0) return 0;  // bwasw.c:279
   const bool std_pe = popt->type == IBWA_PET_STD;
-  // ---- pass 1: eligible pairs, candidate windows (bwasw.c:157-219)
+  // ---- pass 1: eligible pairs, candidate windows (bwasw.c:157-219), in contiguous pair ranges on
+  // the host threads, then concatenated in pair order
   struct Cand {
     int pair, k;
   };
+  struct Part {
+    std::vector<Cand> cand;
+    std::vector<uint8_t> qbuf, rbuf;
+    std::vector<uint64_t> qoff, roff;
+    std::vector<uint32_t> qlen, rlen;
+    std::vector<int32_t> reglen;
+    std::vector<int64_t> beg;
+    uint64_t n_tot[2] = {0, 0};
+  };
+  std::vector<int8_t> single(std::max(n_seqs, 0), -1);
+  const int nt = std::max(1, std::min<int>(host_threads_c(), n_seqs / 1024 + 1));
+  std::vector<Part> part(nt);
+  auto scan = [&](int t) {
+    Part &P = part[t];
+    const int i0 = (int)((int64_t)n_seqs * t / nt), i1 = (int)((int64_t)n_seqs * (t + 1) / nt);
+    for (int i = i0; i < i1; ++i) {
+      ibwa_ref_seq_t *p[2] = {seqs[0] + i, seqs[1] + i};
+      if (!((p[0]->mapQ >= 17 || p[1]->mapQ >= 17) && (p[0]->extra_flag & IBWA_SAM_FPP) == 0)) continue;
+      single[i] = (p[0]->type == IBWA_TYPE_NO_MATCH || p[1]->type == IBWA_TYPE_NO_MATCH) ? 1 : 0;
+      ++P.n_tot[single[i]];
+      if (popt->type != IBWA_PET_STD && popt->type != IBWA_PET_SOLID) continue;
+      for (int k = 0; k < 2; ++k) {
+        const ibwa_ref_seq_t *ref = p[1 - k], *mate = p[k];
+        if (ref->type == IBWA_TYPE_NO_MATCH) continue;
+        const int L = (int)mate->len;
+        int64_t b, e;
+        // set_right_coordinate / set_left_coordinate (bwasw.c:114-143), in the reference's double arithmetic
+        auto right = [&]() {
+          b = (int64_t)((int64_t)ref->remapped_pos + ii->avg - 3 * ii->std - mate->len * 1.5);
+          e = (int64_t)(b + 6 * ii->std + 2 * mate->len);
+          if (b < (int64_t)ref->remapped_pos + (int64_t)ref->len) b = ref->remapped_pos + ref->len;
+          if (e > (int64_t)l_pac) e = (int64_t)l_pac;
+        };
+        auto left = [&]() {
+          b = (int64_t)((int64_t)ref->remapped_pos + ref->len - ii->avg - 3 * ii->std - mate->len * 0.5);
+          e = (int64_t)(b + 6 * ii->std + 2 * mate->len);
+          if (b < 0) b = 0;
+          if (e > (int64_t)ref->remapped_pos) e = (int64_t)ref->remapped_pos;
+        };
+        // the read as bwa_sw_core sees it: a copy (the reference reverses p[k]->seq in place and back)
+        const size_t q0 = P.qbuf.size();
+        P.qbuf.resize(q0 + L);
+        uint8_t *q = P.qbuf.data() + q0;
+        if (std_pe) {
+          if (ref->strand == 0) { right(); memcpy(q, mate->rseq, L); }
+          else { left(); rev_copy(mate->seq, L, false, q); }
+        } else {
+          if (ref->strand == 0) { if (k == 0) left(); else right(); rev_copy(mate->rseq, L, false, q); }
+          else { if (k == 0) right(); else left(); memcpy(q, mate->seq, L); }
+        }
+        const int rl = (int)(e - b);
+        // dbset_extract_sequence (dbset.c:306-325), only for windows bwa_sw_core would extract (bwasw.c:40)
+        const size_t r0 = P.rbuf.size();
+        uint32_t got = 0;
+        if (rl >= 20 && b >= 0 && (uint64_t)b < l_pac) {
+          got = (uint32_t)std::min<uint64_t>((uint64_t)rl, l_pac - (uint64_t)b);
+          P.rbuf.resize(r0 + got);
+          ps.extract((uint64_t)b, got, P.rbuf.data() + r0);
+        }
+        P.cand.push_back({i, k});
+        P.qoff.push_back(q0); P.qlen.push_back((uint32_t)L);
+        P.roff.push_back(r0); P.rlen.push_back(got);
+        P.reglen.push_back(rl);
+        P.beg.push_back(b);
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(scan, t);
+    scan(0);
+    for (auto &x : th) x.join();
+  }
   std::vector<Cand> cand;
   std::vector<uint8_t> qbuf, rbuf;
   std::vector<uint64_t> qoff, roff;
   std::vector<uint32_t> qlen, rlen;
   std::vector<int32_t> reglen;
   std::vector<int64_t> beg;
-  std::vector<int8_t> single(std::max(n_seqs, 0), -1);
-  for (int i = 0; i < n_seqs; ++i) {
-    ibwa_ref_seq_t *p[2] = {seqs[0] + i, seqs[1] + i};
-    if (!((p[0]->mapQ >= 17 || p[1]->mapQ >= 17) && (p[0]->extra_flag & IBWA_SAM_FPP) == 0)) continue;
-    single[i] = (p[0]->type == IBWA_TYPE_NO_MATCH || p[1]->type == IBWA_TYPE_NO_MATCH) ? 1 : 0;
-    ++n_tot[single[i]];
-    if (popt->type != IBWA_PET_STD && popt->type != IBWA_PET_SOLID) continue;
-    for (int k = 0; k < 2; ++k) {
-      const ibwa_ref_seq_t *ref = p[1 - k], *mate = p[k];
-      if (ref->type == IBWA_TYPE_NO_MATCH) continue;
-      const int L = (int)mate->len;
-      int64_t b, e;
-      // set_right_coordinate / set_left_coordinate (bwasw.c:114-143), in the reference's double arithmetic
-      auto right = [&]() {
-        b = (int64_t)((int64_t)ref->remapped_pos + ii->avg - 3 * ii->std - mate->len * 1.5);
-        e = (int64_t)(b + 6 * ii->std + 2 * mate->len);
-        if (b < (int64_t)ref->remapped_pos + (int64_t)ref->len) b = ref->remapped_pos + ref->len;
-        if (e > (int64_t)l_pac) e = (int64_t)l_pac;
-      };
-      auto left = [&]() {
-        b = (int64_t)((int64_t)ref->remapped_pos + ref->len - ii->avg - 3 * ii->std - mate->len * 0.5);
-        e = (int64_t)(b + 6 * ii->std + 2 * mate->len);
-        if (b < 0) b = 0;
-        if (e > (int64_t)ref->remapped_pos) e = (int64_t)ref->remapped_pos;
-      };
-      // the read as bwa_sw_core sees it: a copy (the reference reverses p[k]->seq in place and back)
-      const size_t q0 = qbuf.size();
-      qbuf.resize(q0 + L);
-      uint8_t *q = qbuf.data() + q0;
-      if (std_pe) {
-        if (ref->strand == 0) { right(); memcpy(q, mate->rseq, L); }
-        else { left(); rev_copy(mate->seq, L, false, q); }
-      } else {
-        if (ref->strand == 0) { if (k == 0) left(); else right(); rev_copy(mate->rseq, L, false, q); }
-        else { if (k == 0) right(); else left(); memcpy(q, mate->seq, L); }
-      }
-      const int rl = (int)(e - b);
-      // dbset_extract_sequence (dbset.c:306-325), only for windows bwa_sw_core would extract (bwasw.c:40)
-      const size_t r0 = rbuf.size();
-      uint32_t got = 0;
-      if (rl >= 20 && b >= 0 && (uint64_t)b < l_pac) {
-        got = (uint32_t)std::min<uint64_t>((uint64_t)rl, l_pac - (uint64_t)b);
-        rbuf.resize(r0 + got);
-        for (uint32_t j = 0; j < got; ++j) rbuf[r0 + j] = ps.at((uint64_t)b + j);
-      }
-      cand.push_back({i, k});
-      qoff.push_back(q0); qlen.push_back((uint32_t)L);
-      roff.push_back(r0); rlen.push_back(got);
-      reglen.push_back(rl);
-      beg.push_back(b);
+  {
+    size_t nc = 0, nq = 0, nr = 0;
+    for (const Part &P : part) { nc += P.cand.size(); nq += P.qbuf.size(); nr += P.rbuf.size(); }
+    cand.reserve(nc); qoff.reserve(nc); roff.reserve(nc); qlen.reserve(nc); rlen.reserve(nc);
+    reglen.reserve(nc); beg.reserve(nc);
+    qbuf.reserve(nq + 1); rbuf.reserve(nr + 1);
+    for (Part &P : part) {
+      const uint64_t qb = qbuf.size(), rb = rbuf.size();
+      cand.insert(cand.end(), P.cand.begin(), P.cand.end());
+      for (uint64_t x : P.qoff) qoff.push_back(qb + x);
+      for (uint64_t x : P.roff) roff.push_back(rb + x);
+      qlen.insert(qlen.end(), P.qlen.begin(), P.qlen.end());
+      rlen.insert(rlen.end(), P.rlen.begin(), P.rlen.end());
+      reglen.insert(reglen.end(), P.reglen.begin(), P.reglen.end());
+      beg.insert(beg.end(), P.beg.begin(), P.beg.end());
+      qbuf.insert(qbuf.end(), P.qbuf.begin(), P.qbuf.end());
+      rbuf.insert(rbuf.end(), P.rbuf.begin(), P.rbuf.end());
+      n_tot[0] += P.n_tot[0];
+      n_tot[1] += P.n_tot[1];
+      P = Part();
     }
   }
   // ---- pass 2: every bwa_sw_core of the batch in one launch

@@ -59,6 +59,12 @@ namespace {
 
 constexpr int MODE_GAPE = 0x01, MODE_COMPREAD = 0x02, MODE_LOGGAP = 0x04, MODE_NONSTOP = 0x10;
 constexpr int STATE_M = 0, STATE_I = 1, STATE_D = 2;
+// Gap group: a gap-opening expansion stages its insertion child with its deletion children pending
+// (ldp field = their symbols; the group's ldp is its i) as one entry in STATE_G.  95 % of gap-open
+// children on a GRCh37-sized genome are never popped, so the deletions are spelled out only when
+// the group's level is reached (expand_groups); until then the group counts as all its entries in
+// the stack size (bwtgap.c:138).
+constexpr int STATE_G = 3;
 constexpr int RREC = COOP_RREC;      // chain records in flight (ring)
 constexpr int MAXP = COOP_MAXP;      // pages per bucket
 constexpr int NSTK = COOP_NSTK;      // buckets
@@ -151,7 +157,7 @@ __device__ __forceinline__ bool expand_node(const AlnOpt &o, uint4 L2, const Blk
                                             bool qshare, const Node &nd, int max_diff, bool seeded, int len,
                                             uint32_t csym, const ExpW &w, int t0, int t1, int q1, int q2, uint4 *stg,
                                             uint32_t &stg_w, uint32_t smask, uint32_t &cnt0, uint32_t &cnt1,
-                                            uint32_t &cnt2, uint32_t &mk, uint32_t &ml) {
+                                            uint32_t &cnt2, uint32_t &cex, uint32_t &cgq, uint32_t &mk, uint32_t &ml) {
   const bool gape = o.mode & MODE_GAPE;
   const uint32_t qk = nd.k, ql = nd.l;
   if (qshare) bk = bl;
@@ -206,6 +212,9 @@ __device__ __forceinline__ bool expand_node(const AlnOpt &o, uint4 L2, const Blk
   if (match) vm &= ~(1u << 8);
   const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
   const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
+  // a gap-opening expansion's deletions ride on its insertion child (gap group)
+  const uint32_t gdm = state == STATE_M && (vm & 1u) ? (vm >> 1) & 15u : 0u;
+  vm &= ~(gdm << 1);
   while (vm) {
     const uint32_t j = (uint32_t)__builtin_ctz(vm);
     vm &= vm - 1;
@@ -221,7 +230,13 @@ __device__ __forceinline__ bool expand_node(const AlnOpt &o, uint4 L2, const Blk
     const int sc = sc_base + (is_sym ? o.s_mm : sc_gap);
     const int q = sc == t0 ? 0 : sc == t1 ? q1 : q2;
     const uint32_t rk = q == 0 ? cnt0++ : q == 1 ? cnt1++ : cnt2++;
-    stg[(stg_w++) & smask] = mk_ent(pk, pl, pi, pi, n_mm, n_gapo, n_gape, nd.a, pstate, (uint32_t)q, rk);
+    const bool grp = is_ins && gdm;
+    stg[(stg_w++) & smask] = mk_ent(pk, pl, pi, grp ? (int)gdm : pi, n_mm, n_gapo, n_gape, nd.a, grp ? STATE_G : pstate,
+                                    (uint32_t)q, rk);
+    if (grp) {
+      cex += (uint32_t)__builtin_popcount(gdm);
+      cgq |= 1u << q;
+    }
   }
   if (match) {
     mk = pick4(KK, csym);
@@ -230,9 +245,93 @@ __device__ __forceinline__ bool expand_node(const AlnOpt &o, uint4 L2, const Blk
   return match;
 }
 
+// Level start with gap groups (bucket s, N entries on the pages of dirc0): spell each group out as
+// the reference pushed it (bwtgap.c:221-227: the insertion, then the deletions A..T, bottom to top)
+// into new pages, whose ids go to dir_s (the bucket's global directory row) and dirc0.  The
+// deletions' intervals are the symbol steps of the group's own (k, l).  Returns {entries, n_free},
+// entries >= GRP_FAIL | why on a page shortage.  Out of line: inlined into k_coop its registers
+// spilled into the chain loop (k_coop +40 %, same-box A/B); it runs once per such level.
+constexpr uint32_t GRP_FAIL = 0xFFFFFFF0u;
+
+__device__ __noinline__ uint2 expand_groups(uint4 *pool, const uint4 *o0, const uint4 *o1, uint4 L2, uint32_t *dir_s,
+                                            uint32_t *dirc0, uint32_t *freel, uint32_t n_free, uint32_t freecap,
+                                            uint32_t *pool_next, uint32_t pool_pages, uint32_t N, uint32_t old_np,
+                                            int lane) {
+  auto ent_at = [&](uint32_t j) -> uint4 {
+    return pool[((uint64_t)dirc0[j >> COOP_PG_LOG2] << COOP_PG_LOG2) + (j & (COOP_PG - 1))];
+  };
+  auto size_of = [](const uint4 &e) -> uint32_t {
+    return ((e.w >> 25) & 3u) == (uint32_t)STATE_G ? 1u + (uint32_t)__builtin_popcount((e.z >> 10) & 15u) : 1u;
+  };
+  uint32_t nvt = 0;
+  for (uint32_t b0 = 0; b0 < N; b0 += 64) {
+    const uint32_t j = b0 + (uint32_t)lane;
+    uint32_t t = 0;
+    wave_excl(j < N ? size_of(ent_at(j)) : 0u, lane, t);
+    nvt += t;
+  }
+  const uint32_t npv = (nvt + COOP_PG - 1) >> COOP_PG_LOG2;
+  if (npv > MAXP) return make_uint2(GRP_FAIL | 4u, n_free);
+  for (uint32_t pq = 0; pq < npv; ++pq) {  // the new pages: the wave's free stack, else the global pool
+    uint32_t p;
+    if (n_free) {
+      p = freel[--n_free];
+    } else {
+      uint32_t q = 0;
+      if (lane == 0) q = atomicAdd(pool_next, 1u);
+      q = __shfl(q, 0);
+      if (q >= pool_pages) return make_uint2(GRP_FAIL | 3u, n_free);
+      p = q;
+    }
+    if (lane == 0) dir_s[pq] = p;
+  }
+  __threadfence_block();
+  __syncthreads();
+  auto put = [&](uint32_t vpos, const uint4 &x) {
+    pool[((uint64_t)dir_s[vpos >> COOP_PG_LOG2] << COOP_PG_LOG2) + (vpos & (COOP_PG - 1))] = x;
+  };
+  uint32_t vbase = 0;
+  for (uint32_t b0 = 0; b0 < N; b0 += 64) {
+    const uint32_t j = b0 + (uint32_t)lane;
+    const uint4 e = j < N ? ent_at(j) : make_uint4(0, 0, 0, 0);
+    const bool grp = j < N && ((e.w >> 25) & 3u) == (uint32_t)STATE_G;
+    uint32_t t = 0;
+    const uint32_t vo = vbase + wave_excl(j < N ? size_of(e) : 0u, lane, t);
+    vbase += t;
+    if (j < N && !grp) put(vo, e);
+    if (grp) {
+      const uint4 *ob = (e.w >> 24) & 1u ? o0 : o1;  // strand a searches bwt[1-a]
+      const uint32_t gi = e.z & 0x3ffu, dm = (e.z >> 10) & 15u;
+      // the insertion child: the group itself, its deletions spelled out
+      put(vo, make_uint4(e.x, e.y, gi | gi << 10, (e.w & ~(3u << 25)) | (uint32_t)STATE_I << 25));
+      uint32_t r = 1;
+      for (uint32_t cc = 0; cc < 4; ++cc) {
+        if (dm & (1u << cc)) {
+          const uint32_t l2 = pick4(L2, cc);
+          const uint32_t dl = l2 + occ_of(ob[(size_t)(e.y >> 6) * 4 + cc], e.y);
+          uint32_t dk = l2 + 1u;
+          if (e.x != 0) dk += occ_of(ob[(size_t)((e.x - 1) >> 6) * 4 + cc], e.x - 1);
+          put(vo + r, make_uint4(dk, dl, (gi + 1) | (gi + 1) << 10, (e.w & ~(3u << 25)) | (uint32_t)STATE_D << 25));
+          ++r;
+        }
+      }
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  // the old pages back (beyond the free stack's room they are dropped), the new directory in
+  const uint32_t room = freecap - n_free, nf = old_np < room ? old_np : room;
+  for (uint32_t j = lane; j < nf; j += 64) freel[n_free + j] = dirc0[j];
+  n_free += nf;
+  __syncthreads();
+  for (uint32_t j = lane; j < npv; j += 64) dirc0[j] = dir_s[j];
+  return make_uint2(nvt, n_free);
+}
+
 struct Shm {
-  uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | ring << 16 | hit << 24,
-                      //  done (1) | children staged before the chain's last pop << 1}
+  uint4 recA[RREC];   // {staging start, cnt0 | cnt1 << 16, cnt2 | ring << 16 | hit << 24 | gap-group categories << 25,
+                      //  done (1) | stack growth before the chain's last pop << 1 (16 bits) |
+                      //  deletions pending in its gap groups << 17}
   uint32_t dirc[4][MAXP];  // page ids of the level's bucket and of its (up to) three target buckets
   uint32_t nb[NSTK];       // entries per bucket
   uint16_t np[NSTK];       // pages per bucket (<= MAXP)
@@ -244,6 +343,8 @@ struct Shm {
   uint16_t Wb[2][COOP_MAXLEN + 2];
   uint16_t SWb[2][COOP_SEEDMAX + 1];
   uint8_t str[COOP_MAXLEN];      // bwa_seq_t.seq; strand 1 reads it complemented (COMPREAD)
+  uint32_t gm[NSTK / 32];        // buckets holding gap groups
+  uint32_t gq;                   // target categories (bit q) that this level's commits gave gap groups
   uint32_t head[64];             // per-lane staging ring: first uncommitted slot
   uint32_t rb[64];               // per-lane staging rollback point (discarded chains)
 };
@@ -264,7 +365,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     return a && comp && c < 4 ? 3u - c : c;
   };
   const bool gape = o.mode & MODE_GAPE;
-  const IndexView ixv0 = A.ix[0], ixv1 = A.ix[1];
+  const IndexView ixv0 = A.ix[0];  // L2 only: the same for both strands (checked at launch)
   uint4 *const stg_base = A.stg + ((wave * 64) << A.stg_log2);
   uint4 *const stg = stg_base + ((uint64_t)lane << A.stg_log2);
   const uint32_t SMASK = (1u << A.stg_log2) - 1u;
@@ -344,7 +445,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       // ---------------------------------------------- per-read setup
       const bool seeded = len > o.seed_len;
       // level 0 done by k_coop_roots: the records of its two chains (A.proot[2 r], [2 r + 1])
-      bool pro = A.proot && A.proot[2 * r].w == 0u && A.proot[2 * r + 1].w == 0u;
+      bool pro = A.proot && (A.proot[2 * r].w & 0xFFu) == 0u && (A.proot[2 * r + 1].w & 0xFFu) == 0u;
       const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
       for (int j = lane; j < len; j += 64) {
         const uint32_t c = sq[j];
@@ -367,11 +468,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       }
       S.head[lane] = 0;
       S.rb[lane] = NONE;
+      if (lane == 0) S.gq = 0;
       for (int j = lane; j < RREC; j += 64) S.recA[j].w = 0;
       if (pro && lane < 2) {
         // the finished chains 0 and 1 of level 0: staging start = their offset in A.pstore (ring 64)
         const uint4 q = A.proot[2 * r + lane];
-        S.recA[lane] = make_uint4(q.x, q.y, (q.z & 0xffffu) | 64u << 16, 1u | (q.z >> 16) << 1);
+        S.recA[lane] = make_uint4(q.x, q.y, (q.z & 0xffffu) | 64u << 16 | ((q.w >> 24) & 7u) << 25,
+                                  1u | (q.z >> 16) << 1 | ((q.w >> 8) & 0xFFFFu) << 17);
       }
       __syncthreads();
       // roots (bwtgap.c:126-127): strand 0 then strand 1, both in bucket 0
@@ -393,6 +496,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       }
       int best_score = (opt_max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape;
       int max_diff = opt_max_diff, best_cnt = 0;
+      // buckets holding gap groups: bit b of S.gm[b >> 5]
+      if (lane < 4) S.gm[lane] = 0;
       uint32_t n_live = 2;  // entries on the stack (bwtgap.c n_entries)
       uint32_t stg_w = 0;   // this lane's staging write counter
       int s = 0;            // level (score bucket)
@@ -404,7 +509,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         if (s >= o.n_stacks) break;                                              // stack empty
         if (n_live > (uint32_t)o.max_entries) break;                            // :138, before the level's first pop
         if (!(o.mode & MODE_NONSTOP) && s > best_score + o.s_mm) break;         // :143
-        const uint32_t N = S.nb[s];
+        uint32_t N = S.nb[s];
         // targets: mismatch, gap extension, gap open (deduplicated when penalties coincide)
         const int t0 = s + o.s_mm;
         const int t1 = s + o.s_gape;
@@ -419,6 +524,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           if (tg(q) < o.n_stacks)
             for (uint32_t j = lane; j < S.np[tg(q)]; j += 64) S.dirc[1 + q][j] = dir[tg(q) * MAXP + j];
         __syncthreads();
+        {
+          if ((S.gm[(uint32_t)s >> 5] >> (s & 31)) & 1u) {
+            // the level holds gap groups: spell them out first
+            const uint2 g = expand_groups(A.pool, A.o64[0], A.o64[1],
+                                          make_uint4(ixv0.L2[0], ixv0.L2[1], ixv0.L2[2], ixv0.L2[3]), dir + s * MAXP,
+                                          S.dirc[0], freel, n_free, A.freecap, A.pool_next, A.pool_pages, N, S.np[s], lane);
+            n_free = g.y;
+            if (g.x >= GRP_FAIL) {
+              status = ST_STACK_OVERFLOW | (g.x & 15u) << 8;
+              done = true;
+              break;
+            }
+            if (lane == 0) {
+              S.np[s] = (uint16_t)((g.x + COOP_PG - 1) >> COOP_PG_LOG2);
+              S.nb[s] = g.x;
+            }
+            N = g.x;
+            __syncthreads();
+          }
+        }
         const int nbk = N <= 2 ? 0 : N <= 16 ? 1 : N <= 64 ? 2 : N <= 256 ? 3 : 4;
         if (prof && lane == 0) {
           ++pc[8];
@@ -429,11 +554,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         // lane chain state
         int lst = L_IDLE;
         uint32_t c = 0, cstart = 0, cnt0 = 0, cnt1 = 0, cnt2 = 0;
-        uint32_t mpre = 0;  // children staged before the chain's latest pop
+        uint32_t mpre = 0;  // stack growth (children staged, a group counting all) before the chain's latest pop
         uint32_t k = 0, l = 0;
-        int i = 0, ldp = 0, e_mm = 0, e_go = 0, e_ge = 0, a = 0, state = 0;
-        int xj = 0;
-        uint32_t xk = 0, xl = 0;
+        int i = 0, ldp = 0;  // an exact tail steps k, l, i down to the hit
+        // the node's entry word, fields unpacked where used (registers are the loop's limit):
+        // n_mm | n_gapo << 8 | n_gape << 16 | a << 24 | state << 25
+        uint32_t ew = 0;
         uint32_t ent_page = 0, ent_off = 0;
         // Entry window: lane x holds the entry of chain wh (wh = x mod 64), loaded with an earlier
         // iteration's round trip, so a chain claimed inside the window starts expanding in the
@@ -463,12 +589,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             uint32_t *hr = reinterpret_cast<uint32_t *>(A.recb + wave * RREC + slot);
             __hip_atomic_store(hr + 0, hk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(hr + 1, hl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(hr + 2, (uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(hr + 2, ew & 0x1FFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(hr + 3, (uint32_t)ldp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
-          S.recA[slot] = make_uint4(cstart, cnt0 | cnt1 << 16, cnt2 | (uint32_t)lane << 16 | (hit ? 1u << 24 : 0u),
-                                    1u | mpre << 1);
+          S.recA[slot] = make_uint4(cstart, cnt0 | cnt1 << 16,
+                                    (cnt2 & 0xFFFFu) | (uint32_t)lane << 16 | (hit ? 1u << 24 : 0u) | (cnt2 >> 28) << 25,
+                                    1u | mpre << 1 | ((cnt2 >> 16) & 0xFFFu) << 17);
           if (hit) hit_c = c;
           lst = L_IDLE;
         };
@@ -477,29 +603,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           l = ent.y;
           i = (int)(ent.z & 0x3ff);
           ldp = (int)((ent.z >> 10) & 0x3ff);
-          e_mm = (int)(ent.w & 0xff);
-          e_go = (int)((ent.w >> 8) & 0xff);
-          e_ge = (int)((ent.w >> 16) & 0xff);
-          a = (int)((ent.w >> 24) & 1);
-          state = (int)((ent.w >> 25) & 3);
+          ew = ent.w & 0x7FFFFFFu;
         };
         // the pops of bwtgap.c:139-163 for the node in registers: prune, hit, tail or expand
         auto pop_node = [&]() __attribute__((always_inline)) {
-          mpre = cnt0 + cnt1 + cnt2;
+          mpre = cnt0 + cnt1 + (cnt2 & 0xFFFFu) + ((cnt2 >> 16) & 0xFFFu);
+          const int e_mm = (int)(ew & 0xffu), e_go = (int)((ew >> 8) & 0xffu), e_ge = (int)((ew >> 16) & 0xffu);
+          const int a = (int)((ew >> 24) & 1u), state = (int)((ew >> 25) & 3u);
           int m = max_diff - (e_mm + e_go);
           if (gape) m -= e_ge;
-          if (m < 0) { end_chain(false, 0, 0); return; }                                  // :147
-          if (i > 0 && m < (int)S.Wb[a][i - 1]) { end_chain(false, 0, 0); return; }      // :155
-          if (i == 0) { end_chain(true, k, l); return; }                                   // :159
-          if (m == 0 && (state == STATE_M || gape || e_ge == o.max_gape)) {              // :160
-            xj = i - 1;
-            xk = k;
-            xl = l;
-            if (sym_of(a, xj) > 3) { end_chain(false, 0, 0); return; }
-            lst = L_TAIL;
-            return;
+          // one end_chain call site: with several, the calls were merged across the lambdas before
+          // inlining and the chain state went to scratch
+          int end = 0;  // 1 no hit, 2 hit
+          if (m < 0) end = 1;                                                                // :147
+          else if (i > 0 && m < (int)S.Wb[a][i - 1]) end = 1;                                // :155
+          else if (i == 0) end = 2;                                                          // :159
+          else if (m == 0 && (state == STATE_M || gape || e_ge == o.max_gape)) {             // :160
+            --i;  // the tail's next symbol
+            if (sym_of(a, i) > 3) end = 1;
+            else lst = L_TAIL;
+          } else {
+            lst = L_EXP;
           }
-          lst = L_EXP;
+          if (end) end_chain(end == 2, k, l);
         };
 
         for (;;) {
@@ -584,18 +710,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               const bool v = base + lane < lim;
               const uint4 ra = v ? S.recA[cc & (RREC - 1)] : make_uint4(0, 0, 0, 0);
               const uint32_t n0 = ra.y & 0xffffu, n1 = ra.y >> 16, n2 = ra.z & 0xffffu;
-              const uint32_t tot = n0 + n1 + n2;
+              const uint32_t tot = n0 + n1 + n2;  // entries staged (a gap group is one)
               // stack size before this chain's first pop; its largest before any of its pops is
-              // nc + (children staged before its last pop) (bwtgap.c:138)
-              uint32_t dsum = 0;
+              // nc + (its stack growth before its last pop) (bwtgap.c:138); a gap group counts all
+              // its entries
+              uint32_t dsum = 0, vsum = 0;
               const uint32_t pre = wave_excl(v ? tot : 0u, lane, dsum);
-              const uint32_t nc = n_live + pre - (uint32_t)lane;  // each earlier chain popped one entry
-              if (__ballot(v && nc + (ra.w >> 1) > (uint32_t)o.max_entries)) {
+              const uint32_t vpre = wave_excl(v ? tot + (ra.w >> 17) : 0u, lane, vsum);
+              const uint32_t nc = n_live + vpre - (uint32_t)lane;  // each earlier chain popped one entry
+              if (__ballot(v && nc + ((ra.w >> 1) & 0xFFFFu) > (uint32_t)o.max_entries)) {
                 done = true;  // the search breaks inside the first such chain: the hits so far stand
                 break;
               }
               const uint32_t nv = (lim - base) < 64 ? (lim - base) : 64;
-              n_live = n_live + dsum - nv;
+              n_live = n_live + vsum - nv;
+              // target categories that now hold gap groups (buckets marked at the level's end)
+              if (v && ((ra.z >> 25) & 7u)) atomicOr(&S.gq, (ra.z >> 25) & 7u);
               if (prof && lane == 0) pc[19] += dsum;
               uint32_t T0 = 0, T1 = 0, T2 = 0;
               const uint32_t o0 = wave_excl(n0, lane, T0);
@@ -810,10 +940,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           }
           lap(2);
           // ============================================ loads of this iteration (one round trip)
-          const IndexView ix = a ? ixv0 : ixv1;  // strand a searches bwt[1-a]
+          // L2 (symbol counts) is the same for bwt and rbwt -- one text, reversed (checked at launch):
+          // the uniform copy keeps it out of the loop's vector registers
+          const IndexView &ix = ixv0;
+          const int a = (int)((ew >> 24) & 1u);
           const uint4 *ob = a ? A.o64[0] : A.o64[1];
-          uint4 ent = make_uint4(0, 0, 0, 0);
-          if (lst == L_FETCH) ent = A.pool[((uint64_t)ent_page << COOP_PG_LOG2) + ent_off];
           if (wreq) {
             const uint32_t widx = N - 1u - wh;
             wen = A.pool[((uint64_t)S.dirc[0][widx >> COOP_PG_LOG2] << COOP_PG_LOG2) + (widx & (COOP_PG - 1))];
@@ -831,40 +962,59 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               pc[11] += __popcll(b_t);
               pc[25 + nbk] += __popcll(b_act);
             }
-            const unsigned long long b_e1 = __ballot(exp && k == l), b_t1 = __ballot(tail && xk == xl);
+            const unsigned long long b_e1 = __ballot(exp && k == l), b_t1 = __ballot(tail && k == l);
             if (lane == 0) {
               pc[30] += __popcll(b_e1);
               pc[31] += __popcll(b_t1);
             }
             if (lst != L_IDLE) ++csteps;
           }
-          const uint32_t qk = tail ? xk : k, ql = tail ? xl : l;
+          const uint32_t qk = k, ql = l;
           const bool qkneg = qk == 0;
           const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
+          const uint32_t tsym = tail ? sym_of(a, i) : 0u;
+          // One set of load registers: a lane fetches its chain's entry (bl.v0), takes an exact-tail
+          // step (the tail symbol's Occ words of both rows: bl.v0, bk.v0) or expands (both whole
+          // blocks) -- never two of these, so the round trip holds 8 uint4s, not 14
           Blk bk, bl;
-          load_blk(ob, ql, exp, bl);
-          load_blk(ob, qk - 1, exp && !qkneg && !qshare, bk);
-          const uint32_t tsym = tail ? sym_of(a, xj) : 0u;
-          uint4 tvl = make_uint4(0, 0, 0, 0), tvk = make_uint4(0, 0, 0, 0);
-          if (tail) tvl = ob[(size_t)(ql >> 6) * 4 + tsym];
-          if (tail && !qkneg && !qshare) tvk = ob[(size_t)((qk - 1) >> 6) * 4 + tsym];
+          {
+            const bool fetch = lst == L_FETCH;
+            const bool kld = (exp || tail) && !qkneg && !qshare;
+            const uint4 *pl = fetch ? A.pool + (((uint64_t)ent_page << COOP_PG_LOG2) + ent_off)
+                                    : ob + ((size_t)(ql >> 6) * 4 + tsym);
+            const uint4 *pk = ob + ((size_t)((qk - 1) >> 6) * 4 + tsym);
+            if (fetch || exp || tail) bl.v0 = pl[0];
+            if (exp) {
+              bl.v1 = pl[1];
+              bl.v2 = pl[2];
+              bl.v3 = pl[3];
+            }
+            if (kld) bk.v0 = pk[0];
+            if (exp && kld) {
+              bk.v1 = pk[1];
+              bk.v2 = pk[2];
+              bk.v3 = pk[3];
+            }
+          }
 
           // ============================================ consume
           if (lst == L_FETCH) {
-            take_entry(ent);
+            take_entry(bl.v0);
             pop_node();
           } else if (tail) {
             // one step of bwt_match_exact_alt (bwt.c:240-247)
+            const uint4 tvl = bl.v0;
+            uint4 tvk = bk.v0;
             if (qshare) tvk = tvl;
             const uint32_t ok = qkneg ? 0u : occ_of(tvk, qk - 1), ol = occ_of(tvl, ql);
             const uint32_t base = l2of(ix, tsym);
-            xk = base + ok + 1;
-            xl = base + ol;
-            if (xk > xl) {
+            k = base + ok + 1;
+            l = base + ol;
+            if (k > l) {
               end_chain(false, 0, 0);
-            } else if (--xj < 0) {
-              end_chain(true, xk, xl);
-            } else if (sym_of(a, xj) > 3) {
+            } else if (--i < 0) {
+              end_chain(true, k, l);
+            } else if (sym_of(a, i) > 3) {
               end_chain(false, 0, 0);
             }
           } else if (exp) {
@@ -872,6 +1022,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             // expand_node (k_coop_roots), kept inline: through the function this loop's registers
             // spilled (16 -> 39 scratch accesses) and k_coop ran 10 % slower (same-box A/B)
             if (qshare) bk = bl;
+            const int e_mm = (int)(ew & 0xffu), e_go = (int)((ew >> 8) & 0xffu), e_ge = (int)((ew >> 16) & 0xffu);
+            const int state = (int)((ew >> 25) & 3u);
             uint4 KK, LL;
             {
               const uint4 cl4 = make_uint4(occ_of(bl.v0, ql), occ_of(bl.v1, ql), occ_of(bl.v2, ql), occ_of(bl.v3, ql));
@@ -927,6 +1079,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             if (match) vm &= ~(1u << 8);
             const int sc_base = e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape;
             const int sc_gap = state == STATE_M ? o.s_gapo : o.s_gape;
+            // a gap-opening expansion's deletions ride on its insertion child (gap group)
+            const uint32_t gdm = state == STATE_M && (vm & 1u) ? (vm >> 1) & 15u : 0u;
+            vm &= ~(gdm << 1);
             while (vm) {
               const uint32_t j = (uint32_t)__builtin_ctz(vm);
               vm &= vm - 1;
@@ -941,14 +1096,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               const int pstate = is_ins ? STATE_I : is_del ? STATE_D : STATE_M;
               const int sc = sc_base + (is_sym ? o.s_mm : sc_gap);
               const int q = sc == t0 ? 0 : sc == t1 ? q1 : q2;
-              const uint32_t rk = q == 0 ? cnt0++ : q == 1 ? cnt1++ : cnt2++;
-              stg[(stg_w++) & SMASK] = mk_ent(pk, pl, pi, pi, n_mm, n_gapo, n_gape, a, pstate, (uint32_t)q, rk);
+              const uint32_t rk = q == 0 ? cnt0++ : q == 1 ? cnt1++ : (cnt2++ & 0xFFFFu);
+              const bool grp = is_ins && gdm;
+              stg[(stg_w++) & SMASK] = mk_ent(pk, pl, pi, grp ? (int)gdm : pi, n_mm, n_gapo, n_gape, a,
+                                              grp ? STATE_G : pstate, (uint32_t)q, rk);
+              if (grp) cnt2 = (cnt2 + ((uint32_t)__builtin_popcount(gdm) << 16)) | 1u << (28 + q);
             }
             if (match) {
               k = pick4(KK, csym);
               l = pick4(LL, csym);
               i = ni;
-              state = STATE_M;
+              ew = (ew & ~(3u << 25)) | (uint32_t)STATE_M << 25;
               pop_node();
             } else {
               end_chain(false, 0, 0);
@@ -963,6 +1121,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         if (lane == 0) {
           S.nb[s] = 0;
           S.np[s] = 0;
+          for (int q = 0; q < 3; ++q)
+            if ((S.gq >> q) & 1u) {
+              const int b = q == 0 ? t0 : q == 1 ? t1 : t2;
+              if (b < o.n_stacks) S.gm[(uint32_t)b >> 5] |= 1u << (b & 31);
+            }
+          S.gq = 0;
         }
         __syncthreads();
         ++s;
@@ -1018,7 +1182,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
 // the record says so and k_coop runs level 0 itself.  A chain's children are staged in the lane's
 // ring (k_coop's staging rings, unused until it starts), then copied to the compact store pstore
 // at an offset reserved when the chain ends; proot[u] = {offset, cnt0 | cnt1 << 16,
-// cnt2 | children staged before its last pop << 16, flag}.
+// cnt2 | stack growth before its last pop << 16, flag | deletions pending in its gap groups << 8 |
+// categories holding a gap group << 24}.
 __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long long *counter) {
   const int lane = threadIdx.x;
   const AlnOpt o = A.o;
@@ -1032,7 +1197,7 @@ __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long lon
   constexpr int L_COPY = 4, L_END = 5;
   int pst = L_IDLE;
   uint64_t u = 0;
-  uint32_t pflag = 0, c0 = 0, c1 = 0, c2 = 0, pmpre = 0, pw = 0, ci = 0;
+  uint32_t pflag = 0, c0 = 0, c1 = 0, c2 = 0, pmpre = 0, pw = 0, ci = 0, pex = 0, pgq = 0;
   uint64_t off = 0;
   Node nd = {};
   int pa = 0, plen = 0, pmd = 0;
@@ -1047,7 +1212,7 @@ __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long lon
     return pa && comp && c < 4 ? 3u - c : c;
   };
   auto record = [&]() __attribute__((always_inline)) {
-    A.proot[u] = make_uint4((uint32_t)off, c0 | c1 << 16, c2 | pmpre << 16, pflag);
+    A.proot[u] = make_uint4((uint32_t)off, c0 | c1 << 16, c2 | pmpre << 16, pflag | pex << 8 | pgq << 24);
     pst = L_IDLE;
   };
   // the chain has ended without a hit: reserve its children's room in the store
@@ -1064,7 +1229,7 @@ __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long lon
   };
   // a pop of the chain (level 0: no differences, state M, m = max_diff; bwtgap.c:139-163)
   auto ppop = [&]() __attribute__((always_inline)) {
-    pmpre = c0 + c1 + c2;
+    pmpre = c0 + c1 + c2 + pex;  // the stack grew by the entries staged so far (a group counts all)
     if (nd.i > 0 && pmd < (int)wim1.y) { finish(); return; }  // :155
     if (nd.i == 0) { pflag = PRO_HIT; record(); return; }     // :159
     if (pmd == 0) {                                            // :160
@@ -1102,7 +1267,7 @@ __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long lon
             const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
             pwb = wb + (pa ? A.wlen1 : 0);
             pswb = wb + 2 * A.wlen1 + (pa ? o.seed_len + 1 : 0);
-            c0 = c1 = c2 = pmpre = pw = off = 0;
+            c0 = c1 = c2 = pmpre = pw = off = pex = pgq = 0;
             if (plen < 1 || plen > COOP_MAXLEN || o.n_stacks > NSTK ||
                 (1u << A.stg_log2) < 9u * (uint32_t)(plen + 1) + 16u ||
                 (plen > o.seed_len && o.seed_len > COOP_SEEDMAX) || (int)A.nN[r] > pmd) {
@@ -1180,7 +1345,7 @@ __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long lon
       uint32_t mk = 0, ml = 0;
       if (expand_node(o, make_uint4(ix.L2[0], ix.L2[1], ix.L2[2], ix.L2[3]), bl, bk, qkneg, qshare, nd, pmd, pseed,
                       plen, csym, w, t0, t1, q1, q2, ring, pw, SMASK,
-                      c0, c1, c2, mk, ml)) {
+                      c0, c1, c2, pex, pgq, mk, ml)) {
         nd.k = mk;
         nd.l = ml;
         nd.i = ni;
@@ -1206,6 +1371,8 @@ hipError_t launch_coop_roots(const CoopArgs &g, unsigned long long *d_counter, i
 
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {
   if (g.n <= 0) return hipSuccess;
+  for (int c = 0; c < 5; ++c)  // the kernel takes L2 from ix[0] for both strands
+    if (g.ix[0].L2[c] != g.ix[1].L2[c]) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(g.pool_next, 0, sizeof(uint32_t), st);

@@ -1258,7 +1258,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         std::vector<uint4> pr((size_t)lanes * 2);
         HIPCHK(hipMemcpy(pr.data(), K.proot, pr.size() * 16, hipMemcpyDeviceToHost));
         int64_t fl[3] = {0, 0, 0};
-        for (const uint4 &q : pr) ++fl[q.w < 3 ? q.w : 2];
+        for (const uint4 &q : pr) ++fl[(q.w & 0xFFu) < 3 ? (q.w & 0xFFu) : 2];
         fprintf(stderr, "[ibwa_amd] coop roots: %.1f children per chain stored (%llu of %llu entries), chains: %lld done, "
                 "%lld hit, %lld skipped\n", (double)used / (double)pr.size(), used, (unsigned long long)K.pstore_cap,
                 (long long)fl[0], (long long)fl[1], (long long)fl[2]);

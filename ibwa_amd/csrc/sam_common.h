@@ -5,6 +5,7 @@
 #ifndef IBWA_SAM_COMMON_H
 #define IBWA_SAM_COMMON_H
 #include <math.h>
+#include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -43,6 +44,37 @@ inline void parallel_chunks(int64_t n, const std::function<void(int64_t, int64_t
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t) th.emplace_back(f, n * t / nt, n * (t + 1) / nt, t);
   for (auto &x : th) x.join();
+}
+// Messages of per-read steps: printed at once, or inside parallel_ordered collected per chunk and
+// printed after the join in chunk order -- the stderr a sequential loop gives
+inline std::string *&msg_sink() {
+  static thread_local std::string *sink = nullptr;
+  return sink;
+}
+inline void msg(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+inline void msg(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (std::string *s = msg_sink()) s->append(buf);
+  else fputs(buf, stderr);
+}
+// parallel_chunks whose msg() output keeps the order of a sequential loop over [0, n)
+inline void parallel_ordered(int64_t n, const std::function<void(int64_t, int64_t, int)> &f, int nt = 0) {
+  if (nt <= 0) nt = host_threads();
+  nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 256 + 1));
+  std::vector<std::string> out(nt);
+  parallel_chunks(
+      n,
+      [&](int64_t lo, int64_t hi, int t) {
+        msg_sink() = &out[t];
+        f(lo, hi, t);
+        msg_sink() = nullptr;
+      },
+      nt);
+  for (const std::string &x : out) fputs(x.c_str(), stderr);
 }
 // a thread joined when it goes out of scope (the next batch's parser, on every return path)
 struct Background {
@@ -267,7 +299,7 @@ inline uint64_t remap_position_with_seqid(const RefDb &r, const Bns &target, uin
     uint32_t offset = 0;
     const uint32_t altpos = (uint32_t)(pac_coor - (uint64_t)r.bns.anns[seqid].offset);
     if (!remap_cigar(m->cigar.c_str(), &offset, altpos, (uint32_t)r.bns.anns[seqid].len)) {
-      fprintf(stderr, "Failed to remap coordinates to %s (coord=%lu)", r.bns.anns[seqid].name.c_str(), (unsigned long)pac_coor);
+      msg("Failed to remap coordinates to %s (coord=%lu)", r.bns.anns[seqid].name.c_str(), (unsigned long)pac_coor);
       return 0;
     }
     rv = m->start + offset;

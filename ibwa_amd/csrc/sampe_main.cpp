@@ -195,9 +195,20 @@ struct Aln {  // alignment_t (saiset.h:9-14)
   int dbidx;
 };
 
+// one read's alignments: a slice of the batch's flat array
+struct AlnSpan {
+  const Aln *p = nullptr;
+  size_t n = 0;
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const Aln &operator[](size_t i) const { return p[i]; }
+  const Aln *begin() const { return p; }
+  const Aln *end() const { return p + n; }
+};
+
 struct PairCtx {
   Read *p[2];
-  const std::vector<Aln> *aln[2];
+  const AlnSpan *aln[2];
   const PeOpt *opt;
   const Isize *ii;
   int s_mm;
@@ -468,8 +479,9 @@ struct Sampe {
 
   // alngrp_create (saiset.c:45-76): the read's records of every reference; with several
   // references sorted by score (klib's introsort, not stable) and cut at best + s_mm
-  bool read_alns(int j, std::vector<Aln> &v) {
-    v.clear();
+  bool read_alns(int j, std::vector<Aln> &flat) {
+    const size_t first = flat.size();
+    std::vector<Aln> &v = flat;
     for (size_t d = 0; d < fp_sai[j].size(); ++d) {
       uint32_t count = 0;
       if (fread(&count, 4, 1, fp_sai[j][d]) != 1) continue;  // past the end: nothing
@@ -485,12 +497,14 @@ struct Sampe {
         v[o + t].dbidx = (int)d;
       }
     }
-    if (fp_sai[j].size() > 1 && !v.empty()) {
-      ks_introsort(v.size(), v.data(), [](const Aln &x, const Aln &y) { return x.aln.score < y.aln.score; });
-      const int best = v[0].aln.score;
-      for (size_t t = 0; t < v.size(); ++t)
-        if (v[t].aln.score > best + gopt[0].s_mm) {
-          v.resize(t);
+    if (fp_sai[j].size() > 1 && v.size() > first) {
+      Aln *a = v.data() + first;
+      const size_t m = v.size() - first;
+      ks_introsort(m, a, [](const Aln &x, const Aln &y) { return x.aln.score < y.aln.score; });
+      const int best = a[0].aln.score;
+      for (size_t t = 0; t < m; ++t)
+        if (a[t].aln.score > best + gopt[0].s_mm) {
+          v.resize(first + t);
           break;
         }
     }
@@ -543,7 +557,7 @@ struct Sampe {
     int main_idx = 0;
     uint32_t start = 0, num = 0;
   };
-  bool select_sai(const std::vector<Aln> &ag, Read &s, Pick &pk) {
+  bool select_sai(const AlnSpan &ag, Read &s, Pick &pk) {
     if (ag.empty()) {
       unmap(s);
       return false;
@@ -626,55 +640,119 @@ struct Sampe {
   }
 
   int batch(std::vector<Read> seqs[2], int n, Out &o) {
-    std::vector<std::vector<Aln>> alns[2];
-    alns[0].resize(n);
-    alns[1].resize(n);
-    // ---- SE (bwa_cal_pac_pos_pe, bwape.c:366-385): hit choice in pair order, one SA->pos launch
-    // per reference, then remap(); a row whose remap fails moves to the next row (rare: per row)
-    std::vector<int> hd;
-    std::vector<uint8_t> hs;
-    std::vector<uint32_t> hk, hl;
-    std::vector<Read *> hr;
-    std::vector<Pick> hp;
-    std::vector<const std::vector<Aln> *> ha;
+    // every read's alignments in one flat array per end (alns[j][i] slices it)
+    std::vector<Aln> aflat[2];
+    std::vector<size_t> aoff[2];
+    std::vector<AlnSpan> alns[2];
+    // ---- SE (bwa_cal_pac_pos_pe, bwape.c:366-385): hit choice in pair order (the drand48 stream),
+    // one SA->pos launch per reference, then remap() on the host threads; the main alignment's other
+    // rows for the reads whose remap failed, in one more launch per reference
+    for (int j = 0; j < 2; ++j) {
+      aoff[j].assign(n + 1, 0);
+      aflat[j].reserve((size_t)n + n / 4);
+    }
+    std::vector<Pick> pick[2];
+    std::vector<uint8_t> chosen[2];
+    for (int j = 0; j < 2; ++j) {
+      pick[j].assign(n, Pick());
+      chosen[j].assign(n, 0);
+    }
+    for (int i = 0; i < n; ++i) {
+      for (int j = 0; j < 2; ++j) {
+        aoff[j][i] = aflat[j].size();
+        if (!read_alns(j, aflat[j])) return 1;
+      }
+      aoff[0][i + 1] = aflat[0].size();
+      aoff[1][i + 1] = aflat[1].size();
+    }
+    for (int j = 0; j < 2; ++j) {
+      alns[j].resize(n);
+      for (int i = 0; i < n; ++i) alns[j][i] = AlnSpan{aflat[j].data() + aoff[j][i], aoff[j][i + 1] - aoff[j][i]};
+    }
     for (int i = 0; i < n; ++i) {
       for (int j = 0; j < 2; ++j) {
         Read &p = seqs[j][i];
         p.multi.clear();
         p.extra_flag |= SAM_FPD | (j == 0 ? SAM_FR1 : SAM_FR2);
-        if (!read_alns(j, alns[j][i])) return 1;
-        Pick pk;
-        if (select_sai(alns[j][i], p, pk)) {
-          hd.push_back(alns[j][i][pk.main_idx].dbidx);
-          hs.push_back((uint8_t)p.strand); hk.push_back(p.sa); hl.push_back((uint32_t)p.len);
-          hr.push_back(&p);
-          hp.push_back(pk);
-          ha.push_back(&alns[j][i]);
-        }
+        chosen[j][i] = select_sai(alns[j][i], p, pick[j][i]) ? 1 : 0;
       }
     }
+    std::vector<int> hd;
+    std::vector<uint8_t> hs;
+    std::vector<uint32_t> hk, hl;
+    std::vector<int> hi;  // (pair, end) as 2 i + j
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < 2; ++j)
+        if (chosen[j][i]) {
+          const Read &p = seqs[j][i];
+          hd.push_back(alns[j][i][pick[j][i].main_idx].dbidx);
+          hs.push_back((uint8_t)p.strand); hk.push_back(p.sa); hl.push_back((uint32_t)p.len);
+          hi.push_back(2 * i + j);
+        }
     ph.mark("sai+hit choice");
     std::vector<uint64_t> pos;
     if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
-    for (size_t t = 0; t < hr.size(); ++t) {
-      Read &p = *hr[t];
-      const Aln &ma = (*ha[t])[hp[t].main_idx];
+    std::vector<uint8_t> ok(hi.size(), 0);
+    auto remap_main = [&](size_t t) {
+      const int i = hi[t] >> 1, j = hi[t] & 1;
+      Read &p = seqs[j][i];
+      const Aln &ma = alns[j][i][pick[j][i].main_idx];
       int status = 0;
       p.pos = pos[t];
       remap(p, p.pos, ma.dbidx, (uint64_t)p.len, (uint32_t)(p.n_gapo + p.n_gape), &status);
-      // the other rows of the main alignment, cyclically from the chosen one (bwape.c:336-357)
-      for (uint32_t step = 1; status != 1 && step < hp[t].num; ++step) {
-        const uint32_t aidx = (hp[t].start + step) % hp[t].num;
-        std::vector<int> d1{ma.dbidx};
-        std::vector<uint8_t> s1{(uint8_t)p.strand};
-        std::vector<uint32_t> k1{ma.aln.k + aidx}, l1{(uint32_t)p.len};
+      ok[t] = status == 1;
+    };
+    parallel_ordered((int64_t)hi.size(), [&](int64_t lo, int64_t hi_, int) {
+      for (int64_t t = lo; t < hi_; ++t) remap_main((size_t)t);
+    });
+    // the other rows of the main alignment, cyclically from the chosen one (bwape.c:336-357), for
+    // the reads whose remap failed: their rows in one launch per reference (bounded per launch)
+    {
+      std::vector<size_t> fail;
+      for (size_t t = 0; t < hi.size(); ++t)
+        if (!ok[t] && pick[hi[t] & 1][hi[t] >> 1].num > 1) fail.push_back(t);
+      size_t f0 = 0;
+      while (f0 < fail.size()) {
+        std::vector<int> d1;
+        std::vector<uint8_t> s1;
+        std::vector<uint32_t> k1, l1;
+        std::vector<size_t> first;
+        size_t f1 = f0;
+        for (; f1 < fail.size() && (f1 == f0 || k1.size() < ((size_t)1 << 22)); ++f1) {
+          const int i = hi[fail[f1]] >> 1, j = hi[fail[f1]] & 1;
+          const Read &p = seqs[j][i];
+          const Pick &pk = pick[j][i];
+          const Aln &ma = alns[j][i][pk.main_idx];
+          first.push_back(k1.size());
+          for (uint32_t step = 1; step < pk.num; ++step) {
+            d1.push_back(ma.dbidx); s1.push_back((uint8_t)p.strand);
+            k1.push_back(ma.aln.k + (pk.start + step) % pk.num); l1.push_back((uint32_t)p.len);
+          }
+        }
         std::vector<uint64_t> p1;
         if (int rc = sa2pos(d1, s1, k1, l1, p1)) return rc;
-        p.sa = ma.aln.k + aidx;
-        p.pos = p1[0];
-        remap(p, p.pos, ma.dbidx, (uint64_t)p.len, (uint32_t)(p.n_gapo + p.n_gape), &status);
+        parallel_ordered((int64_t)(f1 - f0), [&](int64_t lo, int64_t hi_, int) {
+          for (int64_t u = lo; u < hi_; ++u) {
+            const size_t t = fail[f0 + u];
+            const int i = hi[t] >> 1, j = hi[t] & 1;
+            Read &p = seqs[j][i];
+            const Pick &pk = pick[j][i];
+            const Aln &ma = alns[j][i][pk.main_idx];
+            int status = 0;
+            for (uint32_t step = 1; status != 1 && step < pk.num; ++step) {
+              p.sa = ma.aln.k + (pk.start + step) % pk.num;
+              p.pos = p1[first[u] + step - 1];
+              remap(p, p.pos, ma.dbidx, (uint64_t)p.len, (uint32_t)(p.n_gapo + p.n_gape), &status);
+            }
+            ok[t] = status == 1;
+          }
+        });
+        f0 = f1;
       }
-      if (status != 1) {
+    }
+    for (size_t t = 0; t < hi.size(); ++t) {
+      Read &p = seqs[hi[t] & 1][hi[t] >> 1];
+      if (!ok[t]) {
         unmap(p);
         fprintf(stderr, "Failed to select primary alignment for %s\n", p.name.c_str());
         continue;
@@ -736,74 +814,106 @@ struct Sampe {
       cache[f.first.first][f.first.second].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
     }
     ph.mark("sa2pos");
-    // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:238-297), pair by pair
-    PosArr arr;
-    std::vector<std::pair<uint64_t, int>> ps;
-    int cnt_chg = 0;
-    for (int i = 0; i < n; ++i) {
-      Read *p[2] = {&seqs[0][i], &seqs[1][i]};
-      arr.clear();
-      if (popt.remapping) {
-        for (int j = 0; j < 2; ++j) {
-          // compute_seq_coords_and_counts (filter_alignments.cpp:53-140): positions inside their
-          // reference, remapped; per distinct remapped position the lowest score seen there; c1 / c2
-          // count the positions whose lowest score is / is not the best
-          ps.clear();
-          int min_score = INT32_MAX;
-          const std::vector<Aln> &ag = alns[j][i];
+    // ---- select_sai_multi's rows that the -R pass did not compute (no -R, or a cached interval):
+    // for every read that can take the multi list (n_occ <= max(n, N) + 1), in one launch
+    std::vector<int64_t> mfirst[2];
+    std::vector<uint64_t> mpos;
+    if (popt.N_multi || popt.n_multi) {
+      const int cap = std::max(popt.n_multi, popt.N_multi) + 1;
+      hd.clear(); hs.clear(); hk.clear(); hl.clear();
+      for (int j = 0; j < 2; ++j) {
+        mfirst[j].assign(n, -1);
+        for (int i = 0; i < n; ++i) {
+          const AlnSpan &ag = alns[j][i];
+          int n_occ = 0;
+          for (const Aln &q : ag) n_occ += (int)(q.aln.l - q.aln.k + 1);
+          if (ag.empty() || n_occ > cap) continue;
+          mfirst[j][i] = (int64_t)hk.size();
+          const int64_t slot0 = row0[j].empty() ? -1 : row0[j][i];
           for (size_t k = 0; k < ag.size(); ++k) {
-            const ibwa_aln1_t &a = ag[k].aln;
-            const int d = ag[k].dbidx;
-            const RefDb &rdb = dbs.db[d];
-            min_score = std::min(min_score, a.score);
-            const uint32_t w = a.l - a.k + 1;
-            const int64_t slot = aslot[row0[j][i] + (int64_t)k];
-            const uint64_t *pp = slot < 0 ? cache[d][(uint64_t)a.k << 32 | a.l].data() : pos.data() + slot;
-            for (uint32_t r = 0; r < w; ++r) {
-              const uint64_t x = pp[r];
-              if (x < rdb.offset || x >= rdb.offset + (uint64_t)rdb.bns.l_pac) continue;
-              Position ap;
-              ap.pos = x;
-              ap.len = p[j]->len;
-              ap.n_gape = a.n_gape;
-              ap.n_gapo = a.n_gapo;
-              ap.score = a.score;
-              int status = 0;
-              remap(ap, x, d, (uint64_t)ap.len, (uint32_t)(ap.n_gapo + ap.n_gape), &status);
-              if (!status) continue;
-              ap.idx_and_end = (uint32_t)k << 1 | (uint32_t)j;
-              arr.push(ap);
-              ps.push_back({ap.remapped_pos, a.score});
+            if (slot0 >= 0 && aslot[slot0 + (int64_t)k] >= 0) continue;
+            const ibwa_aln1_t &q = ag[k].aln;
+            for (uint32_t r = 0; r < q.l - q.k + 1; ++r) {
+              hd.push_back(ag[k].dbidx); hs.push_back((uint8_t)q.a); hk.push_back(q.k + r);
+              hl.push_back((uint32_t)seqs[j][i].len);
             }
           }
-          std::sort(ps.begin(), ps.end());
-          size_t c[2] = {0, 0};
-          for (size_t t = 0; t < ps.size(); ++t)
-            if (t == 0 || ps[t].first != ps[t - 1].first) ++c[ps[t].second == min_score ? 0 : 1];
-          p[j]->c1 = (uint32_t)c[0] & 0xfffffffu;
-          p[j]->c2 = (uint32_t)c[1] & 0xfffffffu;
-          if (p[j]->c1 != 0) p[j]->type = p[j]->c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
         }
       }
-      for (int j = 0; j < 2; ++j)
-        if (p[j]->c1 || p[j]->c2) p[j]->seQ = p[j]->mapQ = approx_mapQ(*p[j], max_diff_of(*p[j])) & 0xff;
-      const bool m0 = p[0]->type == TYPE_UNIQUE || p[0]->type == TYPE_REPEAT;
-      const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
-      if (m0 && m1) {
-        PairCtx c{{p[0], p[1]}, {&alns[0][i], &alns[1][i]}, &popt, &ii, gopt[1].s_mm};
-        cnt_chg += find_optimal_pair(c, arr);
-      }
-      if (popt.N_multi || popt.n_multi) {
-        for (int j = 0; j < 2; ++j) {
-          if (p[j]->type == TYPE_NO_MATCH) continue;
-          int max_multi = popt.n_multi;
-          if (!(p[j]->extra_flag & SAM_FPP) && p[1 - j]->type != TYPE_NO_MATCH)
-            max_multi = (int)(p[j]->c1 + p[j]->c2) - 1 > popt.N_multi ? popt.n_multi : popt.N_multi;
-          if (int rc = select_sai_multi(alns[j][i], *p[j], max_multi, row0[j].empty() ? -1 : row0[j][i], aslot, pos))
-            return rc;
-        }
-      }
+      if (int rc = sa2pos(hd, hs, hk, hl, mpos)) return rc;
     }
+    // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:238-297), pair by pair on the host threads
+    std::vector<int> chg(host_threads(), 0);
+    parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
+      PosArr arr;
+      std::vector<std::pair<uint64_t, int>> ps;
+      for (int64_t i = lo; i < hi_; ++i) {
+        Read *p[2] = {&seqs[0][i], &seqs[1][i]};
+        arr.clear();
+        if (popt.remapping) {
+          for (int j = 0; j < 2; ++j) {
+            // compute_seq_coords_and_counts (filter_alignments.cpp:53-140): positions inside their
+            // reference, remapped; per distinct remapped position the lowest score seen there; c1 / c2
+            // count the positions whose lowest score is / is not the best
+            ps.clear();
+            int min_score = INT32_MAX;
+            const AlnSpan &ag = alns[j][i];
+            for (size_t k = 0; k < ag.size(); ++k) {
+              const ibwa_aln1_t &a = ag[k].aln;
+              const int d = ag[k].dbidx;
+              const RefDb &rdb = dbs.db[d];
+              min_score = std::min(min_score, a.score);
+              const uint32_t w = a.l - a.k + 1;
+              const int64_t slot = aslot[row0[j][i] + (int64_t)k];
+              const uint64_t *pp = slot < 0 ? cache[d].find((uint64_t)a.k << 32 | a.l)->second.data() : pos.data() + slot;
+              for (uint32_t r = 0; r < w; ++r) {
+                const uint64_t x = pp[r];
+                if (x < rdb.offset || x >= rdb.offset + (uint64_t)rdb.bns.l_pac) continue;
+                Position ap;
+                ap.pos = x;
+                ap.len = p[j]->len;
+                ap.n_gape = a.n_gape;
+                ap.n_gapo = a.n_gapo;
+                ap.score = a.score;
+                int status = 0;
+                remap(ap, x, d, (uint64_t)ap.len, (uint32_t)(ap.n_gapo + ap.n_gape), &status);
+                if (!status) continue;
+                ap.idx_and_end = (uint32_t)k << 1 | (uint32_t)j;
+                arr.push(ap);
+                ps.push_back({ap.remapped_pos, a.score});
+              }
+            }
+            std::sort(ps.begin(), ps.end());
+            size_t c[2] = {0, 0};
+            for (size_t t = 0; t < ps.size(); ++t)
+              if (t == 0 || ps[t].first != ps[t - 1].first) ++c[ps[t].second == min_score ? 0 : 1];
+            p[j]->c1 = (uint32_t)c[0] & 0xfffffffu;
+            p[j]->c2 = (uint32_t)c[1] & 0xfffffffu;
+            if (p[j]->c1 != 0) p[j]->type = p[j]->c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
+          }
+        }
+        for (int j = 0; j < 2; ++j)
+          if (p[j]->c1 || p[j]->c2) p[j]->seQ = p[j]->mapQ = approx_mapQ(*p[j], max_diff_of(*p[j])) & 0xff;
+        const bool m0 = p[0]->type == TYPE_UNIQUE || p[0]->type == TYPE_REPEAT;
+        const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
+        if (m0 && m1) {
+          PairCtx c{{p[0], p[1]}, {&alns[0][i], &alns[1][i]}, &popt, &ii, gopt[1].s_mm};
+          chg[th] += find_optimal_pair(c, arr);
+        }
+        if (popt.N_multi || popt.n_multi) {
+          for (int j = 0; j < 2; ++j) {
+            if (p[j]->type == TYPE_NO_MATCH) continue;
+            int max_multi = popt.n_multi;
+            if (!(p[j]->extra_flag & SAM_FPP) && p[1 - j]->type != TYPE_NO_MATCH)
+              max_multi = (int)(p[j]->c1 + p[j]->c2) - 1 > popt.N_multi ? popt.n_multi : popt.N_multi;
+            const uint64_t *mrow = mfirst[j][i] >= 0 ? mpos.data() + mfirst[j][i] : nullptr;
+            select_sai_multi(alns[j][i], *p[j], max_multi, row0[j].empty() ? -1 : row0[j][i], aslot, pos, mrow);
+          }
+        }
+      }
+    }, (int)chg.size());
+    int cnt_chg = 0;
+    for (int x : chg) cnt_chg += x;
     fprintf(stderr, "[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);
     ph.mark("pairing");
     // ---- mate rescue (bwa_paired_sw) over the concatenated references
@@ -850,8 +960,8 @@ struct Sampe {
 
   // select_sai_multi (saiset.c:124-163): every hit when there are at most n_multi + 1 of them
   // (positions as bwtdb_sa2seq gives them: not remapped)
-  int select_sai_multi(const std::vector<Aln> &ag, Read &s, int n_multi, int64_t slot0,
-                       const std::vector<int64_t> &aslot, const std::vector<uint64_t> &pos) {
+  int select_sai_multi(const AlnSpan &ag, Read &s, int n_multi, int64_t slot0, const std::vector<int64_t> &aslot,
+                       const std::vector<uint64_t> &pos, const uint64_t *mrow) {
     int n_occ = 0;
     for (const Aln &q : ag) n_occ += (int)(q.aln.l - q.aln.k + 1);
     s.multi.clear();
@@ -860,18 +970,14 @@ struct Sampe {
     for (size_t k = 0; k < ag.size(); ++k) {
       const ibwa_aln1_t &q = ag[k].aln;
       const uint32_t w = q.l - q.k + 1;
-      std::vector<uint64_t> own;
       const uint64_t *pp = nullptr;
       const int64_t slot = slot0 >= 0 ? aslot[slot0 + (int64_t)k] : -1;
       if (slot >= 0) {
         pp = pos.data() + slot;
-      } else {  // not on hand (no -R pass, or a cached interval): bwtdb_sa2seq for this read
-        std::vector<int> dd(w, ag[k].dbidx);
-        std::vector<uint8_t> st(w, (uint8_t)q.a);
-        std::vector<uint32_t> kk(w), ll(w, (uint32_t)s.len);
-        for (uint32_t r = 0; r < w; ++r) kk[r] = q.k + r;
-        if (int rc = sa2pos(dd, st, kk, ll, own)) return rc;
-        pp = own.data();
+      } else {  // not on hand (no -R pass, or a cached interval): this read's rows of the batch's
+                // one bwtdb_sa2seq launch for select_sai_multi (mrow, alignment by alignment)
+        pp = mrow;
+        mrow += w;
       }
       for (uint32_t r = 0; r < w; ++r) {
         Multi m;
