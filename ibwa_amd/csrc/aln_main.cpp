@@ -385,23 +385,50 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   for (int g = 0; g < n_gpus; ++g)
     if (prep_rc[g]) return die("prepare the index");
   ph.mark("read (index prepared meanwhile)");
-  while (have > 0) {
-    auto t0 = std::chrono::steady_clock::now();
-    const int64_t n = cur.n();
-    tot_seqs += n;
-    if (opt.trim_qual >= 1)  // once per 0x40000-read batch, as bwa_read_seq (bwaseqio.c:206)
-      for (const auto &t : cur.trims)
-        if (t.second) fprintf(stderr, "[bwa_read_seq] %.1f%% bases are trimmed.\n", 100.0f * t.first / t.second);
-    fprintf(stderr, "[bwa_aln_core] calculate SA coordinate... ");
-    std::vector<std::vector<int32_t>> g_naln(n_gpus);
-    std::vector<ibwa_aln1_t *> g_aln(n_gpus, nullptr);
-    std::vector<int> g_rc(n_gpus, 0);
+  // Overlapped groups: lane l's contexts (one per GPU) share lane 0's index and take every
+  // n_lanes-th group, so a group's staging, first pass and host work run while the previous group's
+  // cooperative pass drains.  Groups finish, and their records are written, in input order.
+  const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
+  std::vector<std::vector<ibwa_ctx_t *>> lctx(n_lanes);
+  lctx[0] = ctx;
+  for (int l = 1; l < n_lanes; ++l)
+    for (int g = 0; g < n_gpus; ++g) {
+      ibwa_ctx_t *x = nullptr;
+      if (ibwa_ctx_create(g, &x) || ibwa_ctx_share_index(x, ctx[g])) return die("a second context on the GPU");
+      lctx[l].push_back(x);
+    }
+  struct Job {
+    Batch b;
+    std::vector<std::vector<int32_t>> naln;
+    std::vector<ibwa_aln1_t *> aln;
+    std::vector<int> rc;
     std::vector<std::thread> th;
+    std::chrono::steady_clock::time_point t0;
+    bool active = false;
+  };
+  std::vector<Job> jobs(n_lanes);
+  struct JoinJobs {  // an early return still waits for the groups in flight
+    std::vector<Job> &j;
+    ~JoinJobs() {
+      for (auto &x : j)
+        for (auto &t : x.th)
+          if (t.joinable()) t.join();
+    }
+  } join_jobs{jobs};
+  auto launch = [&](Job &J, std::vector<ibwa_ctx_t *> &cx) {
+    const int64_t n = J.b.n();
+    J.naln.assign(n_gpus, {});
+    J.aln.assign(n_gpus, nullptr);
+    J.rc.assign(n_gpus, 0);
+    J.th.clear();
+    J.t0 = std::chrono::steady_clock::now();
+    J.active = true;
     const int64_t per = (n + n_gpus - 1) / n_gpus;
     for (int g = 0; g < n_gpus; ++g) {
-      th.emplace_back([&, g]() {
+      J.th.emplace_back([&J, &cx, &opt, g, n, per]() {
+        const Batch &cur = J.b;
         int64_t b = std::min<int64_t>(n, g * per), e = std::min<int64_t>(n, b + per);
-        g_naln[g].resize(e - b);
+        J.naln[g].resize(e - b);
         int64_t tot = 0;
         // each slice is staged from its own bytes only: offsets rebased to the slice's first read
         // (reads are contiguous in input order); the batch-level max length still applies
@@ -410,13 +437,13 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         for (auto &x : off) x -= base;
         // ibwa_aln_batch, in its three steps (IBWA_ALN_TIMES=1: their wall times per slice)
         auto c0 = std::chrono::steady_clock::now();
-        int rc = ibwa_batch_stage(ctx[g], e - b, cur.seq.data() + base, off.data(), cur.len.data() + b);
+        int rc = ibwa_batch_stage(cx[g], e - b, cur.seq.data() + base, off.data(), cur.len.data() + b);
         auto c1 = std::chrono::steady_clock::now();
-        if (!rc) rc = ibwa_batch_run(ctx[g], &opt, cur.max_len);
+        if (!rc) rc = ibwa_batch_run(cx[g], &opt, cur.max_len);
         auto c2 = std::chrono::steady_clock::now();
-        if (!rc) rc = ibwa_batch_fetch(ctx[g], g_naln[g].data(), &g_aln[g], &tot);
+        if (!rc) rc = ibwa_batch_fetch(cx[g], J.naln[g].data(), &J.aln[g], &tot);
         auto c3 = std::chrono::steady_clock::now();
-        g_rc[g] = rc;
+        J.rc[g] = rc;
         if (kTimes) {
           auto ms = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
             return std::chrono::duration<double, std::milli>(y - x).count();
@@ -426,23 +453,25 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         }
       });
     }
-    // overlap: parse the next batch while the GPUs work
-    int more = timed_read(nxt);
-    for (auto &t : th) t.join();
+  };
+  // wait for a group, then hand its records to the writer (bwtaln.c:227-231, input order, one write
+  // per slice); the previous group's write has finished first
+  auto finish = [&](Job &J) -> int {
+    for (auto &t : J.th) t.join();
+    J.th.clear();
+    J.active = false;
     for (int g = 0; g < n_gpus; ++g)
-      if (g_rc[g]) return die("aln");
-    ph.mark("align (next batch parsed meanwhile)");
-    double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    fprintf(stderr, "%.2f sec\n", sec);
+      if (J.rc[g]) return die("aln");
+    tot_seqs += J.b.n();
+    fprintf(stderr, "[bwa_aln_core] calculate SA coordinate... %.2f sec\n",
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - J.t0).count());
     fprintf(stderr, "[bwa_aln_core] write to the disk... ");
-    // write-behind: this group's records go out (bwtaln.c:227-231, input order, one write per
-    // slice) while the next group aligns; the previous group's write has finished first
     if (writer.joinable()) writer.join();
     if (write_failed) {
       fprintf(stderr, "[ibwa-amd aln] write failed\n");
       return 1;
     }
-    writer = std::thread([out, &write_failed, naln = std::move(g_naln), aln = std::move(g_aln)]() {
+    writer = std::thread([out, &write_failed, naln = std::move(J.naln), aln = std::move(J.aln)]() {
       for (size_t g = 0; g < naln.size(); ++g) {
         const ibwa_aln1_t *p = aln[g];
         size_t bytes = 0;
@@ -460,18 +489,35 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         ibwa_free(aln[g]);
       }
     });
-    ph.mark("write");
     fprintf(stderr, "0.00 sec\n");
     fprintf(stderr, "[bwa_aln_core] %lld sequences have been processed.\n", (long long)tot_seqs);
-    std::swap(cur, nxt);
-    have = more;
+    return 0;
+  };
+  int64_t k = 0;  // groups launched
+  while (have > 0) {
+    Job &J = jobs[k % n_lanes];
+    if (J.active)  // the oldest group in flight
+      if (int rc = finish(J)) return rc;
+    if (opt.trim_qual >= 1)  // once per 0x40000-read batch, as bwa_read_seq (bwaseqio.c:206)
+      for (const auto &t : cur.trims)
+        if (t.second) fprintf(stderr, "[bwa_read_seq] %.1f%% bases are trimmed.\n", 100.0f * t.first / t.second);
+    std::swap(J.b, cur);
+    launch(J, lctx[k % n_lanes]);
+    ++k;
+    have = timed_read(cur);  // the next group is parsed while the GPUs work
   }
+  for (int64_t q = std::max<int64_t>(0, k - n_lanes); q < k; ++q)
+    if (jobs[q % n_lanes].active)
+      if (int rc = finish(jobs[q % n_lanes])) return rc;
+  ph.mark("align (groups overlapped, next group parsed meanwhile)");
   if (writer.joinable()) writer.join();
   if (write_failed) {
     fprintf(stderr, "[ibwa-amd aln] write failed\n");
     return 1;
   }
   if (out != stdout) fclose(out);
+  for (int l = n_lanes - 1; l >= 1; --l)  // lanes sharing the index first
+    for (auto *x : lctx[l]) ibwa_ctx_destroy(x);
   for (auto *x : ctx) ibwa_ctx_destroy(x);
   if (have < 0) return 1;
   ph.print("ibwa-amd aln");

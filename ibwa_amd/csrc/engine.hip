@@ -45,8 +45,10 @@ int fail(int code, const char *fmt, ...) {
 struct DBuf {
   void *p = nullptr;
   size_t cap = 0;
+  bool borrowed = false;  // another context's buffer (ibwa_ctx_share_index): never freed or grown here
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
+    if (borrowed) return fail(IBWA_EINVAL, "a shared index buffer cannot grow (%zu > %zu bytes)", bytes, cap);
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
@@ -61,9 +63,17 @@ struct DBuf {
     return 0;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && !borrowed) (void)hipFree(p);
     p = nullptr;
     cap = 0;
+    borrowed = false;
+  }
+  DBuf borrow() const {
+    DBuf b;
+    b.p = p;
+    b.cap = cap;
+    b.borrowed = true;
+    return b;
   }
   template <class T> T *as() const { return (T *)p; }
 };
@@ -450,6 +460,41 @@ int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   }
   dst->jump_ready = false;
   dst->sa_expanded = false;
+  return 0;
+}
+
+int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
+  if (!dst || !src || dst == src) return fail(IBWA_EINVAL, "share_index: two distinct contexts");
+  if (dst->device != src->device) return fail(IBWA_EINVAL, "share_index: contexts on devices %d and %d", dst->device, src->device);
+  for (int s = 0; s < 2; ++s)
+    if (!src->loaded[s]) return fail(IBWA_ENOINDEX, "source index not loaded");
+  HIPCHK(hipSetDevice(dst->device));
+  HIPCHK(hipStreamSynchronize(src->stream));  // src's structures are complete
+  for (int s = 0; s < 2; ++s) {
+    for (DBuf *b : {&dst->idx[s], &dst->o64[s], &dst->kt[s], &dst->sa_s[s], &dst->sa_full[s], &dst->isa_full[s], &dst->txt2[s]})
+      b->release();
+    dst->idx[s] = src->idx[s].borrow();
+    dst->o64[s] = src->o64[s].borrow();
+    dst->kt[s] = src->kt[s].borrow();
+    dst->sa_s[s] = src->sa_s[s].borrow();
+    dst->sa_full[s] = src->sa_full[s].borrow();
+    dst->isa_full[s] = src->isa_full[s].borrow();
+    dst->txt2[s] = src->txt2[s].borrow();
+    dst->ix[s] = src->ix[s];
+    dst->loaded[s] = true;
+    dst->sa_loaded[s] = src->sa_loaded[s];
+    dst->build_rounds[s] = src->build_rounds[s];
+  }
+  dst->kmer_k = src->kmer_k;
+  dst->kmer_K = src->kmer_K;
+  dst->kmer_valid = src->kmer_valid;
+  dst->sa_intv = src->sa_intv;
+  dst->sa_expanded = src->sa_expanded;
+  dst->jump_ready = src->jump_ready;
+  dst->jump_derived = src->jump_derived;
+  dst->jump_derive = src->jump_derive;
+  dst->exact_jump = src->exact_jump;
+  dst->width_jump = src->width_jump;
   return 0;
 }
 

@@ -1001,32 +1001,32 @@ struct Sampe {
     std::vector<uint8_t> rev[2];
     for (int j = 0; j < 2; ++j) {
       ref[j].assign(n, ibwa_ref_seq_t());
-      size_t tot = 0;
-      for (int i = 0; i < n; ++i) tot += (size_t)seqs[j][i].len;
-      rev[j].resize(tot + 1);
-      size_t ro = 0;
-      for (int i = 0; i < n; ++i) {
-        Read &r = seqs[j][i];
-        ibwa_ref_seq_t &t = ref[j][i];
-        memset(&t, 0, sizeof t);
-        std::reverse_copy(r.seq.begin(), r.seq.begin() + r.len, rev[j].begin() + ro);  // bwa_seq_t.seq: reversed
-        t.seq = rev[j].data() + ro;
-        ro += (size_t)r.len;
-        t.rseq = r.rseq.data();
-        t.len = (uint32_t)r.len;
-        t.full_len = (uint32_t)r.full_len;
-        t.strand = (uint32_t)r.strand;
-        t.type = (uint32_t)r.type;
-        t.extra_flag = (uint32_t)r.extra_flag;
-        t.n_mm = (uint32_t)r.n_mm; t.n_gapo = (uint32_t)r.n_gapo; t.n_gape = (uint32_t)r.n_gape;
-        t.mapQ = (uint32_t)r.mapQ;
-        t.seQ = (uint64_t)r.seQ;
-        t.pos = r.pos;
-        t.remapped_pos = r.remapped_pos;
-        t.dbidx = (uint32_t)r.dbidx;
-        t.remapped_dbidx = (uint32_t)r.remapped_dbidx;
-        t.c1 = r.c1; t.c2 = r.c2;
-      }
+      std::vector<size_t> ro(n + 1, 0);
+      for (int i = 0; i < n; ++i) ro[i + 1] = ro[i] + (size_t)seqs[j][i].len;
+      rev[j].resize(ro[n] + 1);
+      parallel_chunks(n, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t i = lo; i < hi; ++i) {
+          Read &r = seqs[j][i];
+          ibwa_ref_seq_t &t = ref[j][i];
+          memset(&t, 0, sizeof t);
+          std::reverse_copy(r.seq.begin(), r.seq.begin() + r.len, rev[j].begin() + ro[i]);  // bwa_seq_t.seq: reversed
+          t.seq = rev[j].data() + ro[i];
+          t.rseq = r.rseq.data();
+          t.len = (uint32_t)r.len;
+          t.full_len = (uint32_t)r.full_len;
+          t.strand = (uint32_t)r.strand;
+          t.type = (uint32_t)r.type;
+          t.extra_flag = (uint32_t)r.extra_flag;
+          t.n_mm = (uint32_t)r.n_mm; t.n_gapo = (uint32_t)r.n_gapo; t.n_gape = (uint32_t)r.n_gape;
+          t.mapQ = (uint32_t)r.mapQ;
+          t.seQ = (uint64_t)r.seQ;
+          t.pos = r.pos;
+          t.remapped_pos = r.remapped_pos;
+          t.dbidx = (uint32_t)r.dbidx;
+          t.remapped_dbidx = (uint32_t)r.remapped_dbidx;
+          t.c1 = r.c1; t.c2 = r.c2;
+        }
+      });
     }
     ibwa_ref_pe_opt_t po;
     memset(&po, 0, sizeof po);
@@ -1052,25 +1052,27 @@ struct Sampe {
     fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 discordant pairs are fixed.\n", (unsigned long long)n_mapped[0],
             (unsigned long long)n_tot[0]);
     for (int j = 0; j < 2; ++j) {
-      for (int i = 0; i < n; ++i) {
-        Read &r = seqs[j][i];
-        ibwa_ref_seq_t &t = ref[j][i];
-        r.type = t.type;
-        r.strand = t.strand;
-        r.extra_flag = t.extra_flag;
-        r.n_mm = t.n_mm; r.n_gapo = t.n_gapo; r.n_gape = t.n_gape;
-        r.mapQ = t.mapQ;
-        r.seQ = (int)t.seQ;
-        r.pos = t.pos;
-        r.remapped_pos = t.remapped_pos;
-        r.dbidx = (int)t.dbidx;
-        r.remapped_dbidx = (int)t.remapped_dbidx;
-        if (t.cigar) {
-          r.cigar.assign(t.cigar, t.cigar + t.n_cigar);
-          r.has_cigar = true;
-          free(t.cigar);
+      parallel_chunks(n, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t i = lo; i < hi; ++i) {
+          Read &r = seqs[j][i];
+          ibwa_ref_seq_t &t = ref[j][i];
+          r.type = t.type;
+          r.strand = t.strand;
+          r.extra_flag = t.extra_flag;
+          r.n_mm = t.n_mm; r.n_gapo = t.n_gapo; r.n_gape = t.n_gape;
+          r.mapQ = t.mapQ;
+          r.seQ = (int)t.seQ;
+          r.pos = t.pos;
+          r.remapped_pos = t.remapped_pos;
+          r.dbidx = (int)t.dbidx;
+          r.remapped_dbidx = (int)t.remapped_dbidx;
+          if (t.cigar) {
+            r.cigar.assign(t.cigar, t.cigar + t.n_cigar);
+            r.has_cigar = true;
+            free(t.cigar);
+          }
         }
-      }
+      });
     }
     return 0;
   }

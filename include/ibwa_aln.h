@@ -81,6 +81,10 @@ int ibwa_ctx_load_bwt(ibwa_ctx_t *ctx, int strand, uint32_t primary, const uint3
 int ibwa_ctx_load_bwt_file(ibwa_ctx_t *ctx, int strand, const char *path);
 /* Copy the index of another context (same process) device-to-device (xGMI peer copy when possible). */
 int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src);
+/* Use the index of another context on the same device without a copy: its BWT and the structures
+ * ibwa_ctx_prepare built (call after it).  Two contexts then align different batches concurrently on
+ * one GPU (the CLI's overlapped groups).  src must outlive dst. */
+int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src);
 
 /*
  * Batched aln over flat arrays -- the body of bwa_cal_sa_reg_gap

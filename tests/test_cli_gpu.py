@@ -76,6 +76,18 @@ def test_cli_grouped_batches_equal_one_at_a_time(golden_dir, argv, tmp_path):
     assert one[64:] == grp[64:]
 
 
+@pytest.mark.parametrize("key", ["r100.default", "r36.n0"])
+def test_cli_overlapped_groups(golden_dir, sai_manifest, key, tmp_path):
+    """Consecutive groups overlapped on 1, 2 or 3 contexts sharing one index (IBWA_ALN_LANES,
+    ibwa_ctx_share_index): the .sai keeps input order and equals the reference's."""
+    m = sai_manifest[key]
+    exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+    for lanes in ("1", "2", "3"):
+        got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path,
+                          {"IBWA_ALN_SUBBATCH": "64", "IBWA_ALN_GROUP": "2", "IBWA_ALN_LANES": lanes}, f"l{lanes}.sai")
+        assert oracle.sai_body_equal(got, exp), lanes
+
+
 @pytest.mark.parametrize("argv", [[], ["-q", "15"], ["-B", "4"], ["-I"]])
 def test_cli_bulk_parse_equals_serial(golden_dir, argv, tmp_path):
     """The threaded FASTQ path (readers.h FastqBulk) and its hand-off to the serial reader: a file

@@ -78,10 +78,10 @@ def write_fastq(path, reads, first=0, count=None):
             f.write(buf.tobytes())
 
 
-def run(argv, timeout=1800):
+def run(argv, timeout=1800, env=None):
     t = time.perf_counter()
     r = subprocess.run(argv, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout,
-                       env=dict(os.environ, IBWA_ALN_TIMES="1"))
+                       env=dict(os.environ, IBWA_ALN_TIMES="1", **(env or {})))
     dt = time.perf_counter() - t
     err = r.stderr.decode(errors="replace")
     if r.returncode != 0:
@@ -93,6 +93,12 @@ def run(argv, timeout=1800):
         if "wall s:" in ln:
             for name, v in re.findall(r"([a-z][a-z .()]*?) (\d+\.\d+)", ln.split("wall s:", 1)[1]):
                 phases[name.strip()] = float(v)
+        m = re.search(r"input parse: (\d+) reads in ([\d.]+) s on (\d+) host threads", ln)
+        if m:
+            log("  cli:", ln.strip())
+            n_, s_, t_ = int(m.group(1)), float(m.group(2)), int(m.group(3))
+            phases["input parse"] = {"reads": n_, "wall_s": s_, "threads": t_, "reads_per_s": n_ / s_,
+                                     "reads_per_s_per_thread": n_ / s_ / t_}
     return dt, phases
 
 
@@ -131,6 +137,7 @@ def main():
     ap.add_argument("--check", type=int, default=20000, help="first reads checked against the CPU restatement")
     ap.add_argument("--ref-sample", type=int, default=200_000, help="reads the reference binary aligns (0: skip)")
     ap.add_argument("--threads", type=int, default=bench.host_threads())
+    ap.add_argument("--lanes", default="2", help="IBWA_ALN_LANES values to run (overlapped groups), e.g. 2,1")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
@@ -162,15 +169,26 @@ def main():
             del reads
             log(f"{name}: {a.reads} reads written in {time.perf_counter() - t:.1f} s")
             sai = os.path.join(tmp, f"c{cid}.sai")
-            wall, ph = run([CLI, "aln"] + opts + ["-f", sai, P, fq])
-            load = ph.get("load index", 0.0)
-            c = {"workload": f"{name}: {a.reads} x {a.read_len} bp SE FASTQ, aln {' '.join(opts) or 'defaults'}",
-                 "wall_s": wall, "phases_s": ph, "reads_per_s": a.reads / wall,
-                 "reads_per_s_excl_index_load": a.reads / max(wall - load, 1e-9),
-                 "note": "wall clock of the CLI process incl. FASTQ parsing (overlapped with the GPU) and .sai "
-                         "writes; index load (phase 'load index') excluded in reads_per_s_excl_index_load"}
-            log(f"{name}: aln {wall:.1f} s wall, phases {ph} -> {c['reads_per_s_excl_index_load']:.0f} reads/s "
-                f"excl. index load")
+            c = None
+            for li, lanes in enumerate(int(x) for x in a.lanes.split(",")):
+                out_sai = sai if li == 0 else os.path.join(tmp, f"c{cid}_l{lanes}.sai")
+                wall, ph = run([CLI, "aln"] + opts + ["-f", out_sai, P, fq], env={"IBWA_ALN_LANES": str(lanes)})
+                load = ph.get("load index", 0.0)
+                r_ = {"lanes": lanes, "wall_s": wall, "phases_s": ph, "reads_per_s": a.reads / wall,
+                      "reads_per_s_excl_index_load": a.reads / max(wall - load, 1e-9)}
+                log(f"{name}: aln (lanes {lanes}) {wall:.1f} s wall, phases {ph} -> "
+                    f"{r_['reads_per_s_excl_index_load']:.0f} reads/s excl. index load")
+                if c is None:
+                    c = {"workload": f"{name}: {a.reads} x {a.read_len} bp SE FASTQ, aln {' '.join(opts) or 'defaults'}",
+                         **r_, "runs": [],
+                         "note": "wall clock of the CLI process incl. FASTQ parsing (overlapped with the GPU) and .sai "
+                                 "writes; index load (phase 'load index') excluded in reads_per_s_excl_index_load; "
+                                 "lanes = IBWA_ALN_LANES (consecutive groups overlapped on that many contexts)"}
+                else:
+                    r_["sai_equal_first_run"] = open(out_sai, "rb").read() == open(sai, "rb").read()
+                    log(f"{name}: lanes {lanes} .sai equal to lanes {c['lanes']}: {r_['sai_equal_first_run']}")
+                    os.unlink(out_sai)
+                c["runs"].append(r_)
             t = time.perf_counter()
             c["parity_first_reads"] = a.check
             c["parity_ok"] = bool(oracle_check(P, cfq, sai, opts, a.check))
