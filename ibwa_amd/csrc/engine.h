@@ -209,6 +209,9 @@ struct SwArgs {
   int gap_end;
 };
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st);
+// row p's n_cigar[p] CIGAR words (at cig + p * cap) to out + first[p]
+hipError_t launch_pack_cigar(const uint32_t *cig, int cap, const int32_t *n_cigar, const uint64_t *first, int64_t n,
+                             uint32_t *out, hipStream_t st);
 uint64_t sw_words_per_lane(int max_len1, int max_len2);
 uint64_t sw_tb_per_lane(int max_len1, int max_len2);
 

@@ -170,6 +170,7 @@ struct ibwa_ctx {
   int kmer_K = 0;   // K of the built tables
   bool kmer_valid = false;
   ibwa_run_stats_t stats = {};
+  DBuf sw[15];  // sw_batch's buffers (kept between calls)
 };
 
 namespace {
@@ -343,6 +344,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
                   &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
                   &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1]})
     b->release();
+  for (auto &b : c->sw) b.release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1603,10 +1605,12 @@ int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1,
     end2 = std::max<uint64_t>(end2, off2[p] + len2[p]);
   }
   const int cap = std::max(1, max1 + max2);
-  DBuf s1, s2, o1, o2, l1, l2, sc, pl, nc, en, cg, scr, tbb;
-  auto release = [&]() {
-    for (DBuf *b : {&s1, &s2, &o1, &o2, &l1, &l2, &sc, &pl, &nc, &en, &cg, &scr, &tbb}) b->release();
-  };
+  // the context's SW buffers, grown as needed and kept (a per-call hipMalloc / hipFree of the DP
+  // scratch cost more than the kernel on a sampe batch)
+  DBuf &s1 = c->sw[0], &s2 = c->sw[1], &o1 = c->sw[2], &o2 = c->sw[3], &l1 = c->sw[4], &l2 = c->sw[5], &sc = c->sw[6],
+       &pl = c->sw[7], &nc = c->sw[8], &en = c->sw[9], &cg = c->sw[10], &scr = c->sw[11], &tbb = c->sw[12],
+       &cf = c->sw[13], &cc = c->sw[14];
+  auto release = [&]() {};
   const uint64_t wpl = sw_words_per_lane(max1, max2), tpl = sw_tb_per_lane(max1, max2);
   const uint64_t per_wave = (wpl * 4 + tpl) * 64;
   // a persistent grid within ~32 GiB of DP scratch (5 waves per SIMD at most: 94 VGPRs)
@@ -1618,7 +1622,7 @@ int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1,
       (rc = l1.ensure(n * 4)) || (rc = l2.ensure(n * 4)) || (rc = sc.ensure(n * 4)) || (rc = pl.ensure(n * 4)) ||
       (rc = nc.ensure(n * 4)) || (rc = en.ensure(n * 16)) || (rc = cg.ensure((uint64_t)n * cap * 4)) ||
       (rc = scr.ensure((uint64_t)blocks * 4 * wpl * 4 * 64)) || (rc = tbb.ensure((uint64_t)blocks * 4 * tpl * 64)) ||
-      (rc = c->d_counter.ensure(64))) {
+      (rc = c->d_counter.ensure(64)) || (rc = cf.ensure(n * 8))) {
     release();
     return rc;
   }
@@ -1651,28 +1655,33 @@ int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1,
     chk(launch_sw(A, c->d_counter.as<unsigned long long>(), blocks, c->stream), "k_sw");
     chk(hipEventRecord(c->ev[1], c->stream), "event");
   }
-  std::vector<uint32_t> hc;
   if (!rc) {
-    hc.resize((uint64_t)n * cap);
     chk(hipMemcpyAsync(score, sc.p, n * 4, hipMemcpyDeviceToHost, c->stream), "D2H score");
     chk(hipMemcpyAsync(path_len, pl.p, n * 4, hipMemcpyDeviceToHost, c->stream), "D2H path_len");
     chk(hipMemcpyAsync(n_cigar, nc.p, n * 4, hipMemcpyDeviceToHost, c->stream), "D2H n_cigar");
     chk(hipMemcpyAsync(ends, en.p, n * 16, hipMemcpyDeviceToHost, c->stream), "D2H ends");
-    chk(hipMemcpyAsync(hc.data(), cg.p, (uint64_t)n * cap * 4, hipMemcpyDeviceToHost, c->stream), "D2H cigar");
     chk(hipStreamSynchronize(c->stream), "sync");
     float ms = 0;
     if (!rc && hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->stats.ms_sw = ms;
   }
-  release();
   if (rc) return rc;
+  // the CIGARs packed on the device (row p's n_cigar[p] words at its prefix offset), one copy back
+  std::vector<uint64_t> first(n);
   int64_t tot = 0;
-  for (int64_t p = 0; p < n; ++p) tot += n_cigar[p];
+  for (int64_t p = 0; p < n; ++p) {
+    first[p] = (uint64_t)tot;
+    tot += n_cigar[p];
+  }
   uint32_t *o = (uint32_t *)malloc(std::max<int64_t>(tot, 1) * 4);
   if (!o) return fail(IBWA_EINVAL, "out of host memory");
-  int64_t q = 0;
-  for (int64_t p = 0; p < n; ++p) {
-    memcpy(o + q, hc.data() + (uint64_t)p * cap, (size_t)n_cigar[p] * 4);
-    q += n_cigar[p];
+  if (tot) {
+    if ((rc = cc.ensure((uint64_t)tot * 4))) { free(o); return rc; }
+    chk(hipMemcpyAsync(cf.p, first.data(), n * 8, hipMemcpyHostToDevice, c->stream), "H2D cigar offsets");
+    chk(launch_pack_cigar(cg.as<uint32_t>(), cap, nc.as<int32_t>(), cf.as<uint64_t>(), n, cc.as<uint32_t>(), c->stream),
+        "k_pack_cigar");
+    chk(hipMemcpyAsync(o, cc.p, (uint64_t)tot * 4, hipMemcpyDeviceToHost, c->stream), "D2H cigar");
+    chk(hipStreamSynchronize(c->stream), "sync");
+    if (rc) { free(o); return rc; }
   }
   *cigar = o;
   if (n_cigar_total) *n_cigar_total = tot;

@@ -464,7 +464,7 @@ struct Sampe {
   PeOpt popt;
   ibwa_gap_opt_t gopt[2];
   std::vector<FILE *> fp_sai[2];  // per end, per reference
-  std::vector<ibwa_aln1_t> sai_tmp;
+  std::vector<ibwa_aln1_t> sai_tmp[2];  // per end (the ends are read on two threads)
   Drand48 rnd;
   Isize last_ii;
   // bwtcache (bwtcache.c:27-45), one per reference: positions of an interval of >= 1000 rows,
@@ -487,13 +487,13 @@ struct Sampe {
       if (fread(&count, 4, 1, fp_sai[j][d]) != 1) continue;  // past the end: nothing
       const size_t o = v.size();
       v.resize(o + count);
-      sai_tmp.resize(count);  // the read's records in one read
-      if (count && fread(sai_tmp.data(), sizeof(ibwa_aln1_t), count, fp_sai[j][d]) != count) {
+      sai_tmp[j].resize(count);  // the read's records in one read
+      if (count && fread(sai_tmp[j].data(), sizeof(ibwa_aln1_t), count, fp_sai[j][d]) != count) {
         fprintf(stderr, "[ibwa-amd sampe] truncated .sai\n");
         return false;
       }
       for (uint32_t t = 0; t < count; ++t) {
-        v[o + t].aln = sai_tmp[t];
+        v[o + t].aln = sai_tmp[j][t];
         v[o + t].dbidx = (int)d;
       }
     }
@@ -600,38 +600,64 @@ struct Sampe {
     return true;
   }
 
+  // The next batch of 0x40000 pairs (bwa_read_seq twice, bwape.c:466-468) and its .sai records,
+  // end 1 and end 2 on two threads, in the background: the first batch while the index loads, each
+  // later one while the batch before it is processed.
+  std::vector<Read> nxt[2];
+  std::vector<Aln> nflat[2];
+  std::vector<size_t> noff[2];
+  bool nxt_ok[2] = {true, true};
+  Background reader;
+  void read_next(Source *src) {
+    auto rd = [this, src](int j) {
+      nxt[j].clear();
+      nxt[j].reserve(0x40000);
+      Read r;
+      while ((int)nxt[j].size() < 0x40000 && src[j].next(r)) nxt[j].push_back(std::move(r));
+      // alngrp_create per read, in read order (saiset.c:45-76)
+      const size_t n = nxt[j].size();
+      nflat[j].clear();
+      nflat[j].reserve(n + n / 4);
+      noff[j].assign(n + 1, 0);
+      nxt_ok[j] = true;
+      for (size_t i = 0; i < n && nxt_ok[j]; ++i) {
+        noff[j][i] = nflat[j].size();
+        nxt_ok[j] = read_alns((int)j, nflat[j]);
+        noff[j][i + 1] = nflat[j].size();
+      }
+    };
+    std::thread t1(rd, 1);
+    rd(0);
+    t1.join();
+  }
+  void start_reading(Source *src) {
+    reader.start([this, src]() { read_next(src); });
+  }
+
   int run(Source src[2], FILE *out) {
     Out o{out, {}};
     long tot = 0;
-    // batches of 0x40000 pairs (bwa_read_seq twice, bwape.c:466-468): the two files are parsed
-    // concurrently, and the next batch while this one is processed
-    std::vector<Read> seqs[2], nxt[2];
-    auto read_batch = [&]() {
-      auto rd = [&](int j) {
-        nxt[j].clear();
-        nxt[j].reserve(0x40000);
-        Read r;
-        while ((int)nxt[j].size() < 0x40000 && src[j].next(r)) nxt[j].push_back(std::move(r));
-      };
-      std::thread t1(rd, 1);
-      rd(0);
-      t1.join();
-    };
-    read_batch();
+    std::vector<Read> seqs[2];
+    std::vector<Aln> flat[2];
+    std::vector<size_t> offs[2];
     for (;;) {
-      seqs[0].swap(nxt[0]);
-      seqs[1].swap(nxt[1]);
+      reader.wait();
+      for (int j = 0; j < 2; ++j) {
+        seqs[j].swap(nxt[j]);
+        flat[j].swap(nflat[j]);
+        offs[j].swap(noff[j]);
+      }
       ph.mark("read (wait)");
       if (seqs[0].empty()) break;
-      Background bg;
-      bg.start(read_batch);
+      if (!nxt_ok[0] || !nxt_ok[1]) return 1;
+      start_reading(src);
       if (seqs[1].size() != seqs[0].size()) {
         fprintf(stderr, "[ibwa-amd sampe] the two read files hold different numbers of reads\n");
         return 1;
       }
       const int n = (int)seqs[0].size();
       tot += n;
-      if (int rc = batch(seqs, n, o)) return rc;
+      if (int rc = batch(seqs, flat, offs, n, o)) return rc;
       fprintf(stderr, "[bwa_sai2sam_pe_core] %ld sequences have been processed.\n", tot);
     }
     o.flush();
@@ -639,31 +665,17 @@ struct Sampe {
     return 0;
   }
 
-  int batch(std::vector<Read> seqs[2], int n, Out &o) {
-    // every read's alignments in one flat array per end (alns[j][i] slices it)
-    std::vector<Aln> aflat[2];
-    std::vector<size_t> aoff[2];
+  int batch(std::vector<Read> seqs[2], std::vector<Aln> aflat[2], std::vector<size_t> aoff[2], int n, Out &o) {
+    // every read's alignments in one flat array per end (alns[j][i] slices it), read with the batch
     std::vector<AlnSpan> alns[2];
     // ---- SE (bwa_cal_pac_pos_pe, bwape.c:366-385): hit choice in pair order (the drand48 stream),
     // one SA->pos launch per reference, then remap() on the host threads; the main alignment's other
     // rows for the reads whose remap failed, in one more launch per reference
-    for (int j = 0; j < 2; ++j) {
-      aoff[j].assign(n + 1, 0);
-      aflat[j].reserve((size_t)n + n / 4);
-    }
     std::vector<Pick> pick[2];
     std::vector<uint8_t> chosen[2];
     for (int j = 0; j < 2; ++j) {
       pick[j].assign(n, Pick());
       chosen[j].assign(n, 0);
-    }
-    for (int i = 0; i < n; ++i) {
-      for (int j = 0; j < 2; ++j) {
-        aoff[j][i] = aflat[j].size();
-        if (!read_alns(j, aflat[j])) return 1;
-      }
-      aoff[0][i + 1] = aflat[0].size();
-      aoff[1][i + 1] = aflat[1].size();
     }
     for (int j = 0; j < 2; ++j) {
       alns[j].resize(n);
@@ -1082,6 +1094,7 @@ struct Sampe {
 
 int sampe_main(int argc, char *argv[]) {
   init_tables();
+  Source src[2];  // before S: the background reader S holds uses it until S is gone
   Sampe S;
   int c;
   const char *fn_out = nullptr;
@@ -1143,13 +1156,13 @@ int sampe_main(int argc, char *argv[]) {
       return 1;
     }
   }
-  Source src[2];
   for (int j = 0; j < 2; ++j) {
     if (!src[j].open(fq[j], S.gopt[j])) {
       fprintf(stderr, "[ibwa-amd sampe] cannot open %s\n", fq[j]);
       return 1;
     }
   }
+  S.start_reading(src);
   // dbset_restore (dbset.c:135-176): references at cumulative offsets, each with its index on the
   // GPU, and (-R) its .remap table when it has one
   S.dbs.db.resize(count);
@@ -1198,8 +1211,9 @@ int sampe_main(int argc, char *argv[]) {
   head += "@PG\tID:bwa\tPN:bwa\tVN:ibwa-amd\n";
   fwrite(head.data(), 1, head.size(), out);
   Source *sp = src;
-  S.ph.mark("load index");
+  S.ph.mark("load index (first batch read meanwhile)");
   const int rc = S.run(sp, out);
+  S.reader.wait();  // a batch read ahead on an error return
   for (int j = 0; j < 2; ++j)
     for (FILE *fp : S.fp_sai[j]) fclose(fp);
   if (out != stdout) fclose(out);

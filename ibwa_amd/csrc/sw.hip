@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "engine.h"
 
 namespace ibwa {
@@ -486,6 +488,26 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
     A.n_cigar[p] = n_cig;
     A.ends[p] = make_int4(s_i, s_j, e_i, e_j);
   }
+}
+
+__global__ void __launch_bounds__(256) k_pack_cigar(const uint32_t *cig, int cap, const int32_t *n_cigar,
+                                                    const uint64_t *first, int64_t n, uint32_t *out) {
+  // one lane per CIGAR word slot of a row: a wave reads a row's words as one segment
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * 64; t += stride) {
+    const int64_t p = t >> 6;
+    const int w = (int)(t & 63);
+    const int m = n_cigar[p];
+    for (int x = w; x < m; x += 64) out[first[p] + x] = cig[(uint64_t)p * cap + x];
+  }
+}
+
+hipError_t launch_pack_cigar(const uint32_t *cig, int cap, const int32_t *n_cigar, const uint64_t *first, int64_t n,
+                             uint32_t *out, hipStream_t st) {
+  const int64_t lanes = n * 64;
+  const int blocks = (int)std::min<int64_t>((lanes + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_pack_cigar, dim3(blocks), dim3(256), 0, st, cig, cap, n_cigar, first, n, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st) {

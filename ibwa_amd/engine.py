@@ -79,6 +79,7 @@ CAPI = {
     "ibwa_ctx_load_bwt": (_i, [_vp, _i, _u32, c.POINTER(_u32), _vp, _u64]),
     "ibwa_ctx_load_bwt_file": (_i, [_vp, _i, c.c_char_p]),
     "ibwa_ctx_clone_index": (_i, [_vp, _vp]),
+    "ibwa_ctx_share_index": (_i, [_vp, _vp]),
     "ibwa_aln_batch": (_i, [_vp, c.POINTER(GapOpt), _i64, _vp, _vp, _vp, _i, _vp, c.POINTER(_vp),
                             c.POINTER(_i64)]),
     "ibwa_batch_stage": (_i, [_vp, _i64, _vp, _vp, _vp]),
