@@ -648,11 +648,7 @@ struct Refine {
 // job's reference / read slices
 inline bool refine_prepare(const Dbs &b, Read &s, uint64_t pos, int ext, Refine &j, std::vector<uint8_t> &rbuf,
                            std::vector<uint64_t> &roff, std::vector<uint32_t> &rlen) {
-  if (pos > b.l_pac) {
-    fprintf(stderr, "[refine_gapped_core] position=%llu > l_pac=%llu\n", (unsigned long long)pos,
-            (unsigned long long)b.l_pac);
-    return false;
-  }
+  if (pos > b.l_pac) return false;  // the caller reports it (bwase.c:175-178)
   const int64_t p = (int64_t)pos;
   int64_t ref_len = s.len + abs(ext), ref_start;
   if (ext > 0) {
@@ -712,38 +708,74 @@ inline void refine_finish(const Dbs &b, const Refine &j, const uint32_t *c32, in
 // each read's remapped_pos as the reference has it at that point (bwase.c:401) and the
 // trimmed-read correction.  Returns 0, 1 on a bad position (message printed), -1 on a GPU error.
 inline int refine_gapped(ibwa_ctx_t *ctx, const Dbs &b, std::vector<Read *> &reads) {
+  // the jobs in read order, gathered in contiguous read ranges on the host threads and concatenated
+  struct Part {
+    std::vector<Refine> jobs;
+    std::vector<uint8_t> rbuf, qbuf;
+    std::vector<uint64_t> roff, qoff;
+    std::vector<uint32_t> rlen, qlen;
+    int64_t bad = -1;  // the first read whose window is out of range
+    uint64_t bad_pos = 0;
+  };
+  const int nt = std::max(1, std::min<int>(host_threads(), (int)(reads.size() / 1024) + 1));
+  std::vector<Part> part(nt);
+  parallel_chunks((int64_t)reads.size(), [&](int64_t lo, int64_t hi, int t) {
+    Part &P = part[t];
+    auto add_job = [&](Read &p, Multi *q, uint64_t ps, int ext, int strand, int dbidx, int seqid) -> bool {
+      Refine j;
+      j.s = &p;
+      j.q = q;
+      j.dbidx = dbidx;
+      j.seqid = seqid;
+      if (ps > b.l_pac) {
+        P.bad_pos = ps;
+        return false;
+      }
+      if (!refine_prepare(b, p, ps, ext, j, P.rbuf, P.roff, P.rlen)) return false;
+      const std::vector<uint8_t> &sq = strand ? p.rseq : p.seq;
+      P.qoff.push_back(P.qbuf.size());
+      P.qlen.push_back((uint32_t)p.len);
+      P.qbuf.insert(P.qbuf.end(), sq.begin(), sq.begin() + p.len);
+      P.jobs.push_back(j);
+      return true;
+    };
+    for (int64_t i = lo; i < hi && P.bad < 0; ++i) {
+      Read &p = *reads[i];
+      // remapped sequences can also have gaps (bwase.c:341-347)
+      int remapped_gapo = 0;
+      const RefDb &r = b.db[p.dbidx];
+      if (r.remap && p.remapped_seqid >= 0 && p.remapped_seqid < (int)r.mappings.size() && r.mappings[p.remapped_seqid])
+        remapped_gapo += r.mappings[p.remapped_seqid]->n_gapo;
+      bool ok = true;
+      for (Multi &q : p.multi) {  // bwt_multi1_t.dbidx / remapped_seqid are 0 (select_sai_multi)
+        if (q.gap == 0) continue;
+        if (!(ok = add_job(p, &q, q.pos, (q.strand ? 1 : -1) * q.gap, q.strand, 0, 0))) break;
+      }
+      if (ok && !(p.type == TYPE_NO_MATCH || p.type == TYPE_MATESW || (p.n_gapo == 0 && remapped_gapo == 0)))
+        ok = add_job(p, nullptr, p.pos, (p.strand ? 1 : -1) * (p.n_gapo + p.n_gape), p.strand, p.dbidx, p.remapped_seqid);
+      if (!ok) P.bad = i;
+    }
+  }, nt);
+  for (const Part &P : part)
+    if (P.bad >= 0) {
+      fprintf(stderr, "[refine_gapped_core] position=%llu > l_pac=%llu\n", (unsigned long long)P.bad_pos,
+              (unsigned long long)b.l_pac);
+      return 1;
+    }
   std::vector<Refine> jobs;
   std::vector<uint8_t> rbuf, qbuf;
   std::vector<uint64_t> roff, qoff;
   std::vector<uint32_t> rlen, qlen;
-  auto add_job = [&](Read &p, Multi *q, uint64_t ps, int ext, int strand, int dbidx, int seqid) -> bool {
-    Refine j;
-    j.s = &p;
-    j.q = q;
-    j.dbidx = dbidx;
-    j.seqid = seqid;
-    if (!refine_prepare(b, p, ps, ext, j, rbuf, roff, rlen)) return false;
-    const std::vector<uint8_t> &sq = strand ? p.rseq : p.seq;
-    qoff.push_back(qbuf.size());
-    qlen.push_back((uint32_t)p.len);
-    qbuf.insert(qbuf.end(), sq.begin(), sq.begin() + p.len);
-    jobs.push_back(j);
-    return true;
-  };
-  for (Read *pp : reads) {
-    Read &p = *pp;
-    // remapped sequences can also have gaps (bwase.c:341-347)
-    int remapped_gapo = 0;
-    const RefDb &r = b.db[p.dbidx];
-    if (r.remap && p.remapped_seqid >= 0 && p.remapped_seqid < (int)r.mappings.size() && r.mappings[p.remapped_seqid])
-      remapped_gapo += r.mappings[p.remapped_seqid]->n_gapo;
-    for (Multi &q : p.multi) {  // bwt_multi1_t.dbidx / remapped_seqid are 0 (select_sai_multi)
-      if (q.gap == 0) continue;
-      if (!add_job(p, &q, q.pos, (q.strand ? 1 : -1) * q.gap, q.strand, 0, 0)) return 1;
-    }
-    if (p.type == TYPE_NO_MATCH || p.type == TYPE_MATESW || (p.n_gapo == 0 && remapped_gapo == 0)) continue;
-    if (!add_job(p, nullptr, p.pos, (p.strand ? 1 : -1) * (p.n_gapo + p.n_gape), p.strand, p.dbidx, p.remapped_seqid))
-      return 1;
+  for (Part &P : part) {
+    const uint64_t rb = rbuf.size(), qb = qbuf.size();
+    jobs.insert(jobs.end(), P.jobs.begin(), P.jobs.end());
+    for (uint64_t x : P.roff) roff.push_back(rb + x);
+    for (uint64_t x : P.qoff) qoff.push_back(qb + x);
+    rlen.insert(rlen.end(), P.rlen.begin(), P.rlen.end());
+    qlen.insert(qlen.end(), P.qlen.begin(), P.qlen.end());
+    rbuf.insert(rbuf.end(), P.rbuf.begin(), P.rbuf.end());
+    qbuf.insert(qbuf.end(), P.qbuf.begin(), P.qbuf.end());
+    P = Part();
   }
   if (!jobs.empty()) {
     rbuf.push_back(0);
@@ -782,10 +814,16 @@ inline int refine_gapped(ibwa_ctx_t *ctx, const Dbs &b, std::vector<Read *> &rea
 struct Out {
   FILE *fp;
   std::string b;
+  std::thread w;  // print_parallel's write-behind of a batch's lines
+  void wait() {
+    if (w.joinable()) w.join();
+  }
   void flush() {
+    wait();
     if (!b.empty()) fwrite(b.data(), 1, b.size(), fp);
     b.clear();
   }
+  ~Out() { wait(); }
   Out &s(const char *x) { b += x; return *this; }
   Out &s(const std::string &x) { b += x; return *this; }
   Out &c(char x) { b += x; return *this; }
@@ -936,8 +974,11 @@ inline void print_parallel(Out &o, int64_t n, const std::function<void(Out &, in
     for (int64_t i = lo; i < hi; ++i) fmt(ob, i);
     bufs[t].swap(ob.b);
   }, nt);
-  for (auto &x : bufs)
-    if (!x.empty()) fwrite(x.data(), 1, x.size(), o.fp);
+  // written while the next batch is worked on (Out::flush / the next call / ~Out wait for it)
+  o.w = std::thread([fp = o.fp, bufs = std::move(bufs)]() {
+    for (auto &x : bufs)
+      if (!x.empty()) fwrite(x.data(), 1, x.size(), fp);
+  });
 }
 
 // bwa_escape / bwa_set_rg (bwase.c:608-641)

@@ -394,7 +394,13 @@ int infer_isize(const std::vector<Read> &s0, const std::vector<Read> &s1, Isize 
     fprintf(stderr, "[infer_isize] fail to infer insert size: too few good pairs\n");
     return -1;
   }
-  std::sort(isizes.begin(), isizes.end());
+  {  // sorted by counting (every kept size is < 100000): the order the sums below need
+    std::vector<uint32_t> cnt(100000, 0);
+    for (uint64_t v : isizes) ++cnt[v];
+    size_t q = 0;
+    for (uint32_t v = 0; v < 100000; ++v)
+      for (uint32_t c = cnt[v]; c; --c) isizes[q++] = v;
+  }
   const int p25 = (int)isizes[(int)(tot * 0.25 + 0.5)];
   const int p50 = (int)isizes[(int)(tot * 0.50 + 0.5)];
   const int p75 = (int)isizes[(int)(tot * 0.75 + 0.5)];
@@ -965,7 +971,6 @@ struct Sampe {
       print_sam1(ob, dbs, *p[1], p[0], gopt[1].mode, gopt[1].max_top2, rg_id);
     });
     ph.mark("print");
-    o.flush();
     last_ii = ii;
     return 0;
   }
