@@ -63,6 +63,19 @@ def test_sw_restatement_matches_reference_vectors(golden_dir):
     assert not bad, bad[:5]
 
 
+def test_sw_restatement_matches_reference_ties(golden_dir):
+    """... and on 1 080 score-tie pairs (tools/make_sw_ties_golden.py): tandem copies, periods
+    1-5 / 31-33, N runs -- the first maximum in row-major order."""
+    vecs = oracle.read_sw_vectors(os.path.join(golden_dir, "sw_ties.tsv"))
+    assert len(vecs) > 1000
+    bad = []
+    for k, (ref, rd, score, pl, start, end, cig) in enumerate(vecs):
+        got = oracle.sw_local(oracle.nt4(ref), oracle.nt4(rd))
+        if got != (score, pl, start, end, cig):
+            bad.append((k, got, (score, pl, start, end, cig)))
+    assert not bad, bad[:5]
+
+
 def test_sa2pos_restatement_matches_reference_vectors(golden_dir):
     """bwt_sa (bwt.c:69) + bwtdb_sa2seq (dbset.c:240) restated == the reference on 10 755 rows."""
     g = os.path.join(golden_dir, "g1m")

@@ -52,6 +52,66 @@ def test_sw_random_shapes_vs_oracle(gpu_engine):
     assert not bad, bad[:5]
 
 
+def test_sw_tie_vectors(golden_dir, gpu_engine):
+    """The reference's outputs on 1 080 score-tie pairs (tools/make_sw_ties_golden.py)."""
+    vecs = oracle.read_sw_vectors(os.path.join(golden_dir, "sw_ties.tsv"))
+    got = gpu_engine.sw([oracle.nt4(v[0]) for v in vecs], [oracle.nt4(v[1]) for v in vecs])
+    bad = [(k, g, v[2:]) for k, (g, v) in enumerate(zip(got, vecs)) if g != tuple(v[2:])]
+    assert not bad, (len(bad), bad[:5])
+
+
+def test_sw_adversarial_ties(gpu_engine):
+    """Inputs whose best local score is reached by many cells: tandem copies of the read in the
+    window (equal maxima in different rows and strips), homopolymers and short-period repeats
+    (equal maxima along diagonals, across the 32-column strip edges), N runs, and reads that match
+    two windows places equally.  The reference keeps the first maximum in row-major order
+    (stdaln.c:615-626, `if (h > score_f)`); the strip-mined forward pass must find the same cell."""
+    rng = random.Random(2024)
+    refs, reads = [], []
+
+    def push(ref, rd):
+        refs.append(np.array(ref, np.uint8))
+        reads.append(np.array(rd, np.uint8))
+
+    for _ in range(400):
+        l2 = rng.choice([7, 16, 31, 32, 33, 36, 64, 100, 150])
+        rd = [rng.randrange(4) for _ in range(l2)]
+        k = rng.choice([2, 3, 4])
+        gap = [rng.randrange(4) for _ in range(rng.choice([0, 1, 5, 31, 32, 33]))]
+        ref = []
+        for _c in range(k):
+            ref += rd + gap
+        push(ref[:800], rd)
+        # the read's halves swapped in the window: two equal partial maxima
+        h = l2 // 2
+        push(rd[h:] + gap + rd[:h] + gap + rd[h:], rd)
+    for period in (1, 2, 3, 4, 5, 31, 32, 33):
+        unit = [rng.randrange(4) for _ in range(period)]
+        for l1, l2 in ((64, 36), (510, 150), (300, 100), (33, 33), (96, 64)):
+            ref = (unit * (l1 // period + 1))[:l1]
+            rd = (unit * (l2 // period + 2))[rng.randrange(period):][:l2]
+            push(ref, rd)
+            rd2 = list(rd)
+            rd2[l2 // 2] = (rd2[l2 // 2] + 1) % 4  # one mismatch: many equal-score local hits
+            push(ref, rd2)
+    for _ in range(200):  # N runs in the window and the read
+        l1, l2 = rng.choice([(510, 150), (200, 100), (64, 36)])
+        ref = [rng.randrange(4) for _ in range(l1)]
+        a0 = rng.randrange(0, l1 - l2)
+        rd = ref[a0:a0 + l2]
+        for _n in range(rng.randrange(1, 6)):
+            q = rng.randrange(l2)
+            for t in range(q, min(l2, q + rng.randrange(1, 8))):
+                rd[t] = 4
+        q = rng.randrange(l1)
+        for t in range(q, min(l1, q + rng.randrange(1, 40))):
+            ref[t] = 4
+        push(ref, rd)
+    got = gpu_engine.sw(refs, reads)
+    bad = [(k, got[k], exp) for k, (a, b) in enumerate(zip(refs, reads)) if got[k] != (exp := oracle.sw_local(a, b))]
+    assert not bad, (len(bad), bad[:3])
+
+
 def test_sw_rejects_overflowing_lengths(gpu_engine):
     from ibwa_amd import engine as E
     with pytest.raises(E.IbwaError):
