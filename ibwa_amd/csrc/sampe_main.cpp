@@ -178,6 +178,28 @@ struct PosArr {
   }
 };
 
+// One pair's position array as find_optimal_pair sees it when the batch's pairs share one kvec in
+// pair order (the reference's single-threaded loop): slots [0, n) are this pair's, a slot past them
+// holds what the most recent earlier pair with more positions left there -- found by walking the
+// nearest-previous-greater chain of the pairs' counts -- and a slot no pair wrote is zero.
+struct PosView {
+  const Position *const *arr;  // every pair's final array (sorted when find_optimal_pair ran)
+  const uint32_t *cnt;         // every pair's count
+  const int32_t *pg;           // nearest earlier pair with a larger count (-1: none)
+  int64_t i;                   // this pair
+  size_t n;
+  const Position *a;
+  PosView(const Position *const *arr_, const uint32_t *cnt_, const int32_t *pg_, int64_t i_)
+      : arr(arr_), cnt(cnt_), pg(pg_), i(i_), n(cnt_[i_]), a(arr_[i_]) {}
+  const Position &at(size_t idx) const {
+    static const Position zero;
+    if (idx < n) return a[idx];
+    int64_t j = pg[i];
+    while (j >= 0 && cnt[j] <= idx) j = pg[j];
+    return j >= 0 ? arr[j][idx] : zero;
+  }
+};
+
 inline uint64_t hash_64(uint64_t key) {  // bwapair.c:31-41
   key += ~(key << 32);
   key ^= (key >> 22);
@@ -212,7 +234,14 @@ struct PairCtx {
   const PeOpt *opt;
   const Isize *ii;
   int s_mm;
-  const ibwa_aln1_t &al(const Position &x) const { return (*aln[x.idx_and_end & 1])[x.idx_and_end >> 1].aln; }
+  const ibwa_aln1_t &al(const Position &x) const {
+    // a position left by an earlier pair (PosView) may index past this pair's alignments: the
+    // reference reads whatever lies there; here a zero record
+    static const ibwa_aln1_t none = {};
+    const AlnSpan &s = *aln[x.idx_and_end & 1];
+    const size_t k = x.idx_and_end >> 1;
+    return k < s.size() ? s[k].aln : none;
+  }
 };
 
 struct Pint {  // pairing_internals_t (bwapair.c:8-17)
@@ -273,7 +302,7 @@ void pairing_aux2(const PairCtx &c, Pint &pi, Read &r, const Position &pos) {
 // select_mapping (bwapair.c:64-90): the first lowest-score position of a run that maps to the same
 // place, skipping a remapped position identical to a primary one already seen (the set is seeded
 // from the array's first element, as the reference does)
-const Position &select_mapping(const PairCtx &c, const PosArr &arr, size_t begin, size_t end) {
+const Position &select_mapping(const PairCtx &c, const PosView &arr, size_t begin, size_t end) {
   const Position *best = &arr.at(begin);
   std::vector<uint64_t> seen;
   auto has = [&](uint64_t x) { return std::find(seen.begin(), seen.end(), x) != seen.end(); };
@@ -290,12 +319,12 @@ const Position &select_mapping(const PairCtx &c, const PosArr &arr, size_t begin
   return *best;
 }
 
-// find_optimal_pair (bwapair.c:166-279), BWA_PET_STD
-int find_optimal_pair(const PairCtx &c, PosArr &arr) {
+// find_optimal_pair (bwapair.c:166-279), BWA_PET_STD, on the pair's array already sorted by
+// ks_introsort (bwapair.c:188)
+int find_optimal_pair(const PairCtx &c, const PosView &arr) {
   Read **p = (Read **)c.p;
   Pint pi;
   pi.max_len = std::max(p[0]->full_len, p[1]->full_len);
-  ks_introsort(arr.n, arr.a.data(), position_lt);
   for (int j = 0; j < 2; ++j)
     for (int t = 0; t < 2; ++t) pi.last_pos[j][t].pos = pi.last_pos[j][t].remapped_pos = ~0ull;
   // mappings_overlap (bwapair.c:43-62)
@@ -860,8 +889,16 @@ struct Sampe {
       }
       if (int rc = sa2pos(hd, hs, hk, hl, mpos)) return rc;
     }
-    // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:238-297), pair by pair on the host threads
-    std::vector<int> chg(host_threads(), 0);
+    // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:238-297) on the host threads, in three passes so
+    // that find_optimal_pair's look-ahead past a pair's positions sees what the reference's one
+    // shared array holds there: (A) every pair's positions, counts and sort; (B) each pair's nearest
+    // earlier pair with more positions; (C) the pairing itself and select_sai_multi.
+    const int nth = host_threads();
+    std::vector<std::vector<Position>> pstore(nth);
+    std::vector<uint32_t> pcnt(n, 0);
+    std::vector<uint64_t> poff(n, 0);
+    std::vector<int> pth(n, 0);
+    std::vector<uint8_t> paired(n, 0);
     parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
       PosArr arr;
       std::vector<std::pair<uint64_t, int>> ps;
@@ -914,9 +951,32 @@ struct Sampe {
           if (p[j]->c1 || p[j]->c2) p[j]->seQ = p[j]->mapQ = approx_mapQ(*p[j], max_diff_of(*p[j])) & 0xff;
         const bool m0 = p[0]->type == TYPE_UNIQUE || p[0]->type == TYPE_REPEAT;
         const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
-        if (m0 && m1) {
+        paired[i] = m0 && m1;
+        if (paired[i]) ks_introsort(arr.n, arr.a.data(), position_lt);  // find_optimal_pair's sort
+        pth[i] = th;
+        poff[i] = pstore[th].size();
+        pcnt[i] = (uint32_t)arr.n;
+        pstore[th].insert(pstore[th].end(), arr.a.begin(), arr.a.begin() + arr.n);
+      }
+    }, nth);
+    std::vector<const Position *> parr(n);
+    for (int i = 0; i < n; ++i) parr[i] = pstore[pth[i]].data() + poff[i];
+    std::vector<int32_t> pg(n, -1);
+    {
+      std::vector<int32_t> st;
+      for (int i = 0; i < n; ++i) {
+        while (!st.empty() && pcnt[st.back()] <= pcnt[i]) st.pop_back();
+        pg[i] = st.empty() ? -1 : st.back();
+        st.push_back(i);
+      }
+    }
+    std::vector<int> chg(nth, 0);
+    parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
+      for (int64_t i = lo; i < hi_; ++i) {
+        Read *p[2] = {&seqs[0][i], &seqs[1][i]};
+        if (paired[i]) {
           PairCtx c{{p[0], p[1]}, {&alns[0][i], &alns[1][i]}, &popt, &ii, gopt[1].s_mm};
-          chg[th] += find_optimal_pair(c, arr);
+          chg[th] += find_optimal_pair(c, PosView(parr.data(), pcnt.data(), pg.data(), i));
         }
         if (popt.N_multi || popt.n_multi) {
           for (int j = 0; j < 2; ++j) {
@@ -929,7 +989,7 @@ struct Sampe {
           }
         }
       }
-    }, (int)chg.size());
+    }, nth);
     int cnt_chg = 0;
     for (int x : chg) cnt_chg += x;
     fprintf(stderr, "[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);

@@ -117,7 +117,11 @@ CAPI = {
 
 
 def declare(L):
+    import os
+    older = bool(os.environ.get("IBWA_LIB"))  # an A/B build (tools/) may predate newer entry points
     for name, (res, args) in CAPI.items():
+        if older and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
