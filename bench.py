@@ -426,10 +426,25 @@ def sw_leg(eng, refs, reads, do_cpu, steps=3):
     eng.set_option("sw_stop", 0)
     out["value"] = n / (out["full_kernel_ms"] * 1e-3)
     out["unit"] = "alignments/s"
-    ach = out["forward_GCUPS"] * 1e9 * SW_OPS_PER_CELL
-    out["roofline"] = {"bound": "valu", "kernel": "k_sw forward pass", "achieved": ach / 1e12,
-                       "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T lane-ops/s", "frac": ach / VALU_PEAK_LANE_OPS,
-                       "ops_per_cell": SW_OPS_PER_CELL}
+    # the VALU work per alignment measured by SQ_INSTS_VALU on this workload shape (the latest
+    # profiles/*_sw_pmc.json, tools/r03_sw_pmc.sh) over the live kernel time: whole k_sw
+    import glob
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sw_pmc.json")), reverse=True)
+    if pmc:
+        with open(pmc[0]) as f:
+            sp = json.load(f)
+        ach = sp["valu_wave_insts_per_alignment"] * 64 * n / (out["full_kernel_ms"] * 1e-3)
+        out["roofline"] = {"bound": "valu", "kernel": "k_sw (whole kernel)", "achieved": ach / 1e12,
+                           "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T lane-ops/s", "frac": ach / VALU_PEAK_LANE_OPS,
+                           "valu_wave_insts_per_alignment": sp["valu_wave_insts_per_alignment"],
+                           "source": os.path.basename(pmc[0]) + " (SQ_INSTS_VALU per alignment) x live alignments/s"}
+    est = out["forward_GCUPS"] * 1e9 * SW_OPS_PER_CELL
+    out["forward_pass_estimate"] = {"achieved": est / 1e12, "unit": "T lane-ops/s", "frac": est / VALU_PEAK_LANE_OPS,
+                                    "ops_per_cell": SW_OPS_PER_CELL,
+                                    "note": "forward pass alone, ops per cell from its gfx950 asm (not a counter)"}
+    if "roofline" not in out:
+        out["roofline"] = dict(out["forward_pass_estimate"], bound="valu", kernel="k_sw forward pass",
+                               peak=VALU_PEAK_LANE_OPS / 1e12)
     if do_cpu:
         import oracle
         s = min(1000, n)
