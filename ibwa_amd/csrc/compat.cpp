@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -365,6 +366,8 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
   n_tot[0] = n_tot[1] = n_mapped[0] = n_mapped[1] = 0;
   if (!popt->is_sw || ii->avg < 0.0) return 0;  // bwasw.c:279
   const bool std_pe = popt->type == IBWA_PET_STD;
+  static const bool stats = getenv("IBWA_SAMPE_STATS") != nullptr;
+  const auto c0 = std::chrono::steady_clock::now();
   // ---- pass 1: eligible pairs, candidate windows (bwasw.c:157-219), in contiguous pair ranges on
   // the host threads, then concatenated in pair order
   struct Cand {
@@ -473,6 +476,7 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
   }
   // ---- pass 2: every bwa_sw_core of the batch in one launch
   const int64_t m = (int64_t)cand.size();
+  const auto c1 = std::chrono::steady_clock::now();
   std::vector<int32_t> ncig(m);
   std::vector<uint32_t> cnt(m);
   uint32_t *cig = nullptr;
@@ -483,6 +487,7 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
                                     reglen.data(), beg.data(), (int64_t)l_pac, ncig.data(), cnt.data(), &cig))
       return rc;
   }
+  const auto c2 = std::chrono::steady_clock::now();
   // ---- pass 3: acceptance and fix-up in pair order (bwasw.c:220-265)
   std::vector<uint64_t> cfirst(m);
   for (int64_t j = 0, acc = 0; j < m; ++j) { cfirst[j] = acc; acc += ncig[j]; }
@@ -557,6 +562,13 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
     rf->extra_flag |= IBWA_SAM_FPP;
   }
   ibwa_free(cig);
+  if (stats) {
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    fprintf(stderr, "[ibwa-amd paired_sw] %d pairs, %lld rescues: windows %.1f, SW %.1f, fix-up %.1f ms\n", n_seqs,
+            (long long)m, ms(c0, c1), ms(c1, c2), ms(c2, std::chrono::steady_clock::now()));
+  }
   return 0;
 }
 

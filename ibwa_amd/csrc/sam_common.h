@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <functional>
 #include <string>
@@ -61,20 +62,32 @@ inline void msg(const char *fmt, ...) {
   if (std::string *s = msg_sink()) s->append(buf);
   else fputs(buf, stderr);
 }
-// parallel_chunks whose msg() output keeps the order of a sequential loop over [0, n)
-inline void parallel_ordered(int64_t n, const std::function<void(int64_t, int64_t, int)> &f, int nt = 0) {
+// f(begin, end, thread) over [0, n) in chunks of `grain` claimed dynamically by the host threads
+// (a few costly items do not hold one thread's whole share back), with msg() output kept in the
+// order of a sequential loop: each chunk's messages are printed after the join, chunk by chunk
+inline void parallel_ordered(int64_t n, const std::function<void(int64_t, int64_t, int)> &f, int nt = 0,
+                             int64_t grain = 256) {
+  if (n <= 0) return;
   if (nt <= 0) nt = host_threads();
-  nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 256 + 1));
-  std::vector<std::string> out(nt);
-  parallel_chunks(
-      n,
-      [&](int64_t lo, int64_t hi, int t) {
-        msg_sink() = &out[t];
-        f(lo, hi, t);
-        msg_sink() = nullptr;
-      },
-      nt);
-  for (const std::string &x : out) fputs(x.c_str(), stderr);
+  const int64_t nch = (n + grain - 1) / grain;
+  nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, nch));
+  std::vector<std::string> out(nch);
+  std::atomic<int64_t> next{0};
+  auto work = [&](int t) {
+    for (;;) {
+      const int64_t ch = next.fetch_add(1);
+      if (ch >= nch) break;
+      msg_sink() = &out[ch];
+      f(ch * grain, std::min(n, (ch + 1) * grain), t);
+      msg_sink() = nullptr;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+  for (const std::string &x : out)
+    if (!x.empty()) fputs(x.c_str(), stderr);
 }
 // a thread joined when it goes out of scope (the next batch's parser, on every return path)
 struct Background {

@@ -592,23 +592,37 @@ struct Sampe {
     int main_idx = 0;
     uint32_t start = 0, num = 0;
   };
-  bool select_sai(const AlnSpan &ag, Read &s, Pick &pk) {
-    if (ag.empty()) {
-      unmap(s);
-      return false;
-    }
-    int main_idx = 0, i, cnt;
-    double rng_cache = 0.0;
+  // the drand48 decisions of select_sai_ibwa (bwape.c:305-318): the main alignment and the draw
+  // that picks its row.  The only sequential part of the hit choice.
+  void select_rng(const AlnSpan &ag, int &main_idx, double &rng_cache) {
+    main_idx = 0;
+    rng_cache = 0.0;
+    if (ag.empty()) return;
     const int best = ag[0].aln.score;
-    for (i = cnt = 0; i < (int)ag.size(); ++i) {
+    int cnt = 0;
+    for (int i = 0; i < (int)ag.size(); ++i) {
       const ibwa_aln1_t &p = ag[i].aln;
-      const int naln = (int)(p.l - p.k + 1);
       if (p.score > best) break;
       if (rnd.next() * (double)(uint32_t)(p.l - p.k + 1 + (uint32_t)cnt) > (double)cnt) {
         main_idx = i;
         rng_cache = rnd.next();
       }
-      cnt += naln;
+      cnt += (int)(p.l - p.k + 1);
+    }
+  }
+  // the rest of select_sai_ibwa up to the coordinate (bwape.c:319-335): counts, type, the main
+  // alignment's fields and first SA row; false when the read is unmapped without a try
+  bool select_sai(const AlnSpan &ag, Read &s, Pick &pk, int main_idx, double rng_cache) {
+    if (ag.empty()) {
+      unmap(s);
+      return false;
+    }
+    int i, cnt;
+    const int best = ag[0].aln.score;
+    for (i = cnt = 0; i < (int)ag.size(); ++i) {
+      const ibwa_aln1_t &p = ag[i].aln;
+      if (p.score > best) break;
+      cnt += (int)(p.l - p.k + 1);
     }
     s.c1 = (uint32_t)cnt & 0xfffffffu;
     for (int t = i; t < (int)ag.size(); ++t) cnt += (int)(ag[t].aln.l - ag[t].aln.k + 1);
@@ -625,7 +639,7 @@ struct Sampe {
       s.remapped_dbidx = 0;
       s.remapped_seqid = -1;
       unmap(s);
-      fprintf(stderr, "Failed to select primary alignment for %s\n", s.name.c_str());
+      msg("Failed to select primary alignment for %s\n", s.name.c_str());
       return false;
     }
     s.sa = p.k + start;
@@ -716,13 +730,20 @@ struct Sampe {
       alns[j].resize(n);
       for (int i = 0; i < n; ++i) alns[j][i] = AlnSpan{aflat[j].data() + aoff[j][i], aoff[j][i + 1] - aoff[j][i]};
     }
-    for (int i = 0; i < n; ++i) {
-      for (int j = 0; j < 2; ++j) {
-        Read &p = seqs[j][i];
-        p.multi.clear();
-        p.extra_flag |= SAM_FPD | (j == 0 ? SAM_FR1 : SAM_FR2);
-        chosen[j][i] = select_sai(alns[j][i], p, pick[j][i]) ? 1 : 0;
-      }
+    {
+      std::vector<int> midx(2 * (size_t)n);
+      std::vector<double> rcache(2 * (size_t)n);
+      for (int i = 0; i < n; ++i)  // the drand48 stream, in pair order
+        for (int j = 0; j < 2; ++j) select_rng(alns[j][i], midx[2 * i + j], rcache[2 * i + j]);
+      parallel_ordered(n, [&](int64_t lo, int64_t hi_, int) {
+        for (int64_t i = lo; i < hi_; ++i)
+          for (int j = 0; j < 2; ++j) {
+            Read &p = seqs[j][i];
+            p.multi.clear();
+            p.extra_flag |= SAM_FPD | (j == 0 ? SAM_FR1 : SAM_FR2);
+            chosen[j][i] = select_sai(alns[j][i], p, pick[j][i], midx[2 * i + j], rcache[2 * i + j]) ? 1 : 0;
+          }
+      }, 0, 1024);
     }
     std::vector<int> hd;
     std::vector<uint8_t> hs;
@@ -889,6 +910,7 @@ struct Sampe {
       }
       if (int rc = sa2pos(hd, hs, hk, hl, mpos)) return rc;
     }
+    ph.mark("multi rows");
     // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:238-297) on the host threads, in three passes so
     // that find_optimal_pair's look-ahead past a pair's positions sees what the reference's one
     // shared array holds there: (A) every pair's positions, counts and sort; (B) each pair's nearest
@@ -959,6 +981,7 @@ struct Sampe {
         pstore[th].insert(pstore[th].end(), arr.a.begin(), arr.a.begin() + arr.n);
       }
     }, nth);
+    ph.mark("pairing: positions");
     std::vector<const Position *> parr(n);
     for (int i = 0; i < n; ++i) parr[i] = pstore[pth[i]].data() + poff[i];
     std::vector<int32_t> pg(n, -1);
@@ -969,6 +992,12 @@ struct Sampe {
         pg[i] = st.empty() ? -1 : st.back();
         st.push_back(i);
       }
+    }
+    if (getenv("IBWA_SAMPE_STATS")) {
+      uint64_t tot = 0, mx = 0;
+      for (int i = 0; i < n; ++i) { tot += pcnt[i]; mx = std::max<uint64_t>(mx, pcnt[i]); }
+      fprintf(stderr, "[ibwa-amd sampe] batch of %d pairs: %llu positions (max %llu per pair), %zu rows computed\n", n,
+              (unsigned long long)tot, (unsigned long long)mx, pos.size());
     }
     std::vector<int> chg(nth, 0);
     parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {

@@ -12,7 +12,7 @@ for cfg in "$@"; do
   opts=()
   IFS=, read -ra kv <<< "$cfg"
   for x in "${kv[@]}"; do [ -n "$x" ] && opts+=(--opt "$x"); done
-  timeout -k 10 400 python bench.py --reads $N --steps 1 --warmup 1 --no-cpu --exact-leg 0 --sa2pos 0 "${opts[@]}" \
+  timeout -k 10 400 python bench.py --reads $N --steps 1 --warmup 1 --no-cpu --exact-leg 0 --sa2pos 0 --sw-leg 0 "${opts[@]}" \
     > gpurun_out/sweep_$i.json 2> gpurun_out/sweep_$i.log || { tail -5 gpurun_out/sweep_$i.log; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/sweep_$i.json')); e=d['extra']; print('[$cfg]', round(d['ms_per_step']), 'heavy', e['n_heavy'], {k: round(v) for k, v in e['kernel_ms_per_step'].items()}, flush=True)"
 done
