@@ -349,6 +349,127 @@ struct Shm {
   uint32_t rb[64];               // per-lane staging rollback point (discarded chains)
 };
 
+// Resume a read from the first pass's state at a level boundary (GapArgs::rdump): {entries, hits,
+// lowest score, stack size}, {best_score, best_cnt, max_diff}, the live entries in slot order (per
+// bucket bottom to top), the hits in the order they were added.  gap_shadow (bwtgap.c:81-91) of
+// each hit is replayed, in order, on the widths k_width computed afresh; each entry goes to the top
+// of its bucket.  Out of line: k_coop's chain loop keeps its registers.
+struct ResumeOut {
+  int s, best_score, best_cnt, max_diff, n_aln;
+  uint32_t n_live, status, n_free;
+};
+__device__ __noinline__ ResumeOut resume_state(const uint4 *rs, Shm *S, uint4 *pool, uint32_t *dir, uint4 *hitv,
+                                               uint32_t hcap, uint32_t *freel, uint32_t n_free, uint32_t *pool_next,
+                                               uint32_t pool_pages, uint32_t seq_len, int s_mm, int s_gapo, int s_gape,
+                                               int n_stacks, int lane) {
+  ResumeOut R;
+  __syncthreads();
+  const uint4 h0 = rs[0], h1 = rs[1];
+  const uint32_t ne = h0.x, nh = h0.y;
+  R.s = (int)h0.z;
+  R.n_live = h0.w;
+  R.best_score = (int)h1.x;
+  R.best_cnt = (int)h1.y;
+  R.max_diff = (int)h1.z;
+  R.status = 0;
+  for (uint32_t j = 0; j < nh && j < hcap; ++j) {
+    const uint4 h = rs[RD_HDR + ne + j];
+    const int h_a = (int)((h.x >> 24) & 1u), h_ldp = (int)(h.w >> 16);
+    const uint32_t x = h.z - h.y + 1u;
+    uint32_t jrun = 0;
+    for (int base = 0; base < h_ldp; base += 64) {
+      const int q = base + lane;
+      uint2 w = q < h_ldp ? make_uint2(S->Ww[h_a][q], S->Wb[h_a][q]) : make_uint2(0, 0);
+      const bool eq = q < h_ldp && w.x == x;
+      const unsigned long long em = __ballot(eq);
+      if (q < h_ldp) {
+        if (w.x > x) {
+          S->Ww[h_a][q] = w.x - x;
+        } else if (eq) {
+          S->Ww[h_a][q] = seq_len - (jrun + (uint32_t)__popcll(em & ((1ull << lane) - 1ull)) + 1u);
+          S->Wb[h_a][q] = 1u;
+        }
+      }
+      jrun += (uint32_t)__popcll(em);
+    }
+    if (lane == 0) hitv[j] = make_uint4(h.x, h.y, h.z, h.w & 0xFFFFu);
+  }
+  R.n_aln = (int)nh;
+  if (nh > hcap) R.status = ST_ALN_OVERFLOW;
+  // a bucket's page ids also in LDS (S->dirc, free until the levels start: 8 pages of 8192 entries
+  // per bucket cover the first pass's 64 k slots)
+  uint32_t *const pc8 = &S->dirc[0][0];
+  for (uint32_t b0 = 0; b0 < ne && R.status == 0; b0 += 64) {
+    const uint32_t j = b0 + (uint32_t)lane;
+    uint4 ce = make_uint4(0, 0, 0, 0);
+    int b = -1;
+    bool grp = false;
+    if (j < ne) {
+      const uint4 e = rs[RD_HDR + j];
+      const int e_mm = (int)((e.w >> 16) & 31u), e_go = (int)((e.w >> 21) & 7u), e_ge = (int)((e.w >> 24) & 15u);
+      const int est = (int)((e.w >> 29) & 3u);
+      ce = mk_ent(e.x, e.y, (int)(e.z & 0xFFFFu), (int)(e.z >> 16), e_mm, e_go, e_ge, (int)((e.w >> 28) & 1u), est);
+      b = e_mm * s_mm + e_go * s_gapo + e_ge * s_gape;
+      grp = est == STATE_G;
+      if (b >= n_stacks) b = NSTK;  // not from the first pass; fails below
+    }
+    unsigned long long pend = __ballot(b >= 0);
+    while (pend) {
+      const int bb = __shfl(b, (int)__builtin_ctzll(pend));
+      const unsigned long long mm = __ballot(b == bb);
+      pend &= ~mm;
+      if (bb >= n_stacks) {
+        R.status = ST_STACK_OVERFLOW | 1u << 8;
+        break;
+      }
+      const uint32_t base = S->nb[bb], tot = (uint32_t)__popcll(mm);
+      const uint32_t need_p = (base + tot + COOP_PG - 1u) >> COOP_PG_LOG2;
+      uint32_t npb = S->np[bb];
+      while (npb < need_p) {
+        uint32_t p = NONE;
+        if (npb < 8u) {
+          if (n_free) {
+            --n_free;
+            p = freel[n_free];
+          } else {
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(pool_next, 1u);
+            q = __shfl(q, 0);
+            p = q < pool_pages ? q : NONE;
+          }
+        }
+        if (p == NONE) {
+          R.status = ST_STACK_OVERFLOW | 3u << 8;
+          break;
+        }
+        if (lane == 0) {
+          pc8[bb * 8 + npb] = p;
+          dir[bb * MAXP + npb] = p;
+        }
+        ++npb;
+      }
+      __syncthreads();
+      if (R.status) break;
+      if (b == bb) {
+        const uint32_t pos = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
+        pool[((uint64_t)pc8[bb * 8 + (pos >> COOP_PG_LOG2)] << COOP_PG_LOG2) + (pos & (COOP_PG - 1u))] = ce;
+      }
+      const bool g = __ballot(b == bb && grp) != 0ull;
+      __syncthreads();
+      if (lane == 0) {
+        S->np[bb] = (uint16_t)npb;
+        S->nb[bb] = base + tot;
+        if (g) S->gm[(uint32_t)bb >> 5] |= 1u << (bb & 31);
+      }
+      __syncthreads();
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  R.n_free = n_free;
+  return R;
+}
+
 }  // namespace
 
 template <bool PROF>
@@ -444,8 +565,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     } else {
       // ---------------------------------------------- per-read setup
       const bool seeded = len > o.seed_len;
+      // a first-pass search state to resume from (GapArgs::rdump), 1 + its offset
+      const uint64_t rof = A.roff ? A.roff[rr] : 0ull;
       // level 0 done by k_coop_roots: the records of its two chains (A.proot[2 r], [2 r + 1])
-      bool pro = A.proot && (A.proot[2 * r].w & 0xFFu) == 0u && (A.proot[2 * r + 1].w & 0xFFu) == 0u;
+      bool pro = !rof && A.proot && (A.proot[2 * r].w & 0xFFu) == 0u && (A.proot[2 * r + 1].w & 0xFFu) == 0u;
       const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
       for (int j = lane; j < len; j += 64) {
         const uint32_t c = sq[j];
@@ -478,7 +601,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       }
       __syncthreads();
       // roots (bwtgap.c:126-127): strand 0 then strand 1, both in bucket 0
-      {
+      if (!rof) {
         const uint32_t p = alloc_page();
         if (p == NONE) {
           status = ST_STACK_OVERFLOW | 3u << 8;
@@ -501,6 +624,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       uint32_t n_live = 2;  // entries on the stack (bwtgap.c n_entries)
       uint32_t stg_w = 0;   // this lane's staging write counter
       int s = 0;            // level (score bucket)
+      if (rof) {
+        const ResumeOut ro_ = resume_state(A.rdump + (rof - 1), &S, A.pool, dir, hitv, A.hcap, freel, n_free, A.pool_next,
+                                           A.pool_pages, ixv0.seq_len, o.s_mm, o.s_gapo, o.s_gape, o.n_stacks, lane);
+        s = ro_.s;
+        n_live = ro_.n_live;
+        best_score = ro_.best_score;
+        best_cnt = ro_.best_cnt;
+        max_diff = ro_.max_diff;
+        n_aln = ro_.n_aln;
+        status = ro_.status;
+        n_free = ro_.n_free;
+      }
       bool done = status != 0;
       lap(5);
       // ---------------------------------------------- levels
@@ -1270,7 +1405,8 @@ __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long lon
             c0 = c1 = c2 = pmpre = pw = off = pex = pgq = 0;
             if (plen < 1 || plen > COOP_MAXLEN || o.n_stacks > NSTK ||
                 (1u << A.stg_log2) < 9u * (uint32_t)(plen + 1) + 16u ||
-                (plen > o.seed_len && o.seed_len > COOP_SEEDMAX) || (int)A.nN[r] > pmd) {
+                (plen > o.seed_len && o.seed_len > COOP_SEEDMAX) || (int)A.nN[r] > pmd ||
+                (A.roff && A.roff[rr])) {  // resumed reads start past level 0
               pflag = PRO_SKIP;
               record();
             } else {

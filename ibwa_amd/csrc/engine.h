@@ -91,6 +91,8 @@ struct GapArgs {
   uint32_t max_iters;        // iteration budget per read (0: none); over it -> ST_HEAVY
   uint32_t early_iters;      // early hand-off: past this many iterations (0: off) a read whose
   uint32_t early_entries;    //   stack holds more than early_entries entries -> ST_HEAVY
+  uint32_t early2_iters;     // a second such rule (0: off), e.g. an earlier check with a larger stack
+  uint32_t early2_entries;
   int lanes_per_wave;        // reads a wave runs at once (64; 1 for heavy reads)
   int free_depth;            // LDS free-slot stack per read (wide kernel)
   // LDS-resident widths (first pass, when they fit): the k_width records (AlnArgs::cw) copied into
@@ -98,8 +100,18 @@ struct GapArgs {
   const uint32_t *cw;        // nullptr: widths from wbuf, heads per bucket, page table in LDS
   uint32_t cw_words, cw_rw;
   uint16_t *ptab_g;          // [lane][GAP_MAX_PAGES]
+  // Resume (LDS-width variant): a read past an early hand-off rule runs on to the next score-level
+  // boundary and leaves its search state for the cooperative pass instead of being re-run from the
+  // start there.  rdump: the states, RD_HDR header records + the live entries in slot order + the
+  // hits; rd_next / rd_cap: fill counter and capacity (16 B records); roff[read]: 1 + the state's
+  // first record (0: none).  nullptr: every hand-off re-runs from the start.
+  uint4 *rdump;
+  unsigned long long *rd_next;
+  unsigned long long rd_cap;
+  uint64_t *roff;
   AlnOpt o;
 };
+constexpr int RD_HDR = 2;  // resume state header: {entries, hits, lowest score, stack size}, {best_score, best_cnt, max_diff, 0}
 constexpr int GAP_RING = 16;      // bucket heads of the LDS-width variant: live scores span <= 16
 constexpr int GAP_MAX_PAGES = 8;  // page-table entries per lane (global table)
 size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int pages_per_block, int lanes_per_wave,
@@ -155,6 +167,8 @@ struct CoopArgs {
   uint4 *pstore;             // their children, compact
   unsigned long long *pstore_next;  // bump pointer into pstore (entries)
   uint64_t pstore_cap;       // pstore capacity (entries)
+  const uint4 *rdump;        // first-pass search states (GapArgs::rdump), roff[read] 1 + offset, 0: none
+  const uint64_t *roff;
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);
@@ -164,6 +178,15 @@ hipError_t launch_coop_roots(const CoopArgs &g, unsigned long long *d_counter, i
 // only sizes the rocPRIM scratch into *tmp_bytes
 hipError_t select_handed_on(const uint32_t *status, int64_t n, int64_t *ids, uint32_t *sel_status,
                             unsigned long long *d_count, void *tmp, size_t *tmp_bytes, hipStream_t st);
+// ids (base + i, in order) and statuses of the reads in [base, base + n) that left a resume state
+// (roff != 0); tmp == nullptr only sizes the scratch
+hipError_t select_resumed(const uint64_t *roff, int64_t base, int64_t n, const uint32_t *status, int64_t *ids,
+                          uint32_t *sel_status, unsigned long long *d_count, void *tmp, size_t *tmp_bytes,
+                          hipStream_t st);
+// after a cooperative launch over resumed reads ids[0, n): status[id] = 0 where it resolved the read,
+// else roff[id] = 0 (the read starts over in the later passes)
+hipError_t resume_fixup(const uint32_t *r_status, const int64_t *ids, int64_t n, uint32_t *status, uint64_t *roff,
+                        hipStream_t st);
 // the order in which the cooperative pass takes the handed-on reads: largest first-pass stack first
 // (status bits 16-31); idx[0, n) gets the permutation of the selection, ids_out the ids in that order
 hipError_t order_heavy_first(const uint32_t *sel_status, const int64_t *ids, unsigned long long n, uint32_t *keys,

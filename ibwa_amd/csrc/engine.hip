@@ -141,12 +141,17 @@ struct ibwa_ctx {
   // early hand-off to the coop pass: a read past 3000 iterations whose stack holds > 1000 entries
   // (swept at 10M reads: 2.28 -> 2.14 s per step; budget 6000-16000 with it: within noise)
   uint32_t gap_early_iters = 3000, gap_early_entries = 1000;
+  uint32_t gap_early2_iters = 0, gap_early2_entries = 0;  // a second early hand-off rule (0: off)
   uint32_t gap_iter_budget = 8000;   // first-pass iterations per read before handing it to the coop pass (swept 1000-8000 at 50M reads: 8000 best)
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
   int gap_coop = 1;
   int gap_lw = 1;                    // first pass with its widths in LDS (gapped.hip LW) when they fit
+  int gap_resume = 1;                // early hand-offs leave their search state for the coop pass (LW)
+  int gap_resume_gb = 48;            // state buffer (GiB, at most ~4 KiB per read of the batch)
+  int64_t gap_resume_records = 0;    // tests: state buffer of this many 16 B records (0: by gap_resume_gb)
   DBuf d_cw, d_ptabg;
+  DBuf d_rdump, d_roff;  // resume states (GapArgs::rdump) and per-read offsets
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
   int coop_pool_gb = 16;             // bucket page pool
   DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb, c_proot, c_pstore;
@@ -365,7 +370,12 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
   else if (k == "gap_early_iters" && value >= 0) c->gap_early_iters = (uint32_t)value;
   else if (k == "gap_early_entries" && value >= 0) c->gap_early_entries = (uint32_t)value;
+  else if (k == "gap_early2_iters" && value >= 0) c->gap_early2_iters = (uint32_t)value;
+  else if (k == "gap_early2_entries" && value >= 0) c->gap_early2_entries = (uint32_t)value;
   else if (k == "gap_lw" && (value == 0 || value == 1)) c->gap_lw = (int)value;
+  else if (k == "gap_resume" && (value == 0 || value == 1)) c->gap_resume = (int)value;
+  else if (k == "gap_resume_gb" && value >= 1 && value <= 256) c->gap_resume_gb = (int)value;
+  else if (k == "gap_resume_records" && value >= 0) c->gap_resume_records = (int64_t)value;
   else if (k == "coop_order" && (value == 0 || value == 1)) c->coop_order = (int)value;
   else if (k == "coop_roots" && (value == 0 || value == 1)) c->coop_roots = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
@@ -871,6 +881,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                   gapped_lds_bytes(o.n_stacks, 64, true, 0, 0, 1, 4096) <= 65536 && max_len <= 65535;
   float ms_w = 0, ms_s = 0;
   c->stream_out = v2;
+  bool resume_states = false;  // the first pass left resume states (GapArgs::rdump)
+  float res_ms = 0, res_w = 0;  // the cooperative launches over resumed reads (after each chunk)
+  int64_t res_ok = 0;           // reads they resolved
+  c->stats.n_resumed = 0;
+  c->stats.resume_records = 0;
   if (v2) {
     if (int rc = ensure_kmer(c)) return rc;
     c->stats.path = 2;
@@ -911,6 +926,18 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (int rc = c->d_cw.ensure(chunk * (uint64_t)cw_words * 4)) return rc;
       if (int rc = c->d_ptabg.ensure(lanes * GAP_MAX_PAGES * 2)) return rc;
     }
+    // resume states of the early hand-offs: per read 1 + the state's offset (0: none), then the
+    // buffer's fill counter and the count of states stored
+    const bool resume = lw && c->gap_resume && c->gap_coop && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK;
+    uint64_t rd_cap = 0;
+    if (resume) {
+      rd_cap = std::min<uint64_t>((uint64_t)c->gap_resume_gb << 30, (uint64_t)n * 4096 + (1u << 20)) / 16;
+      if (c->gap_resume_records > 0) rd_cap = (uint64_t)c->gap_resume_records;
+      if (int rc = c->d_rdump.ensure(rd_cap * 16)) return rc;
+      if (int rc = c->d_roff.ensure(((uint64_t)n + 2) * 8)) return rc;
+      HIPCHK(hipMemsetAsync(c->d_roff.p, 0, ((uint64_t)n + 2) * 8, c->stream));
+      resume_states = true;
+    }
     if (int rc = c->d_ent.ensure(lanes * P0 * 16)) return rc;
     if (int rc = c->d_pool.ensure((uint64_t)blocks * ppb * (16ull << LG))) return rc;
     if (int rc = c->d_aln.ensure(aln_total * 16)) return rc;
@@ -919,6 +946,128 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (int rc = c->d_status.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
     if (int rc = c->d_counter.ensure(64)) return rc;
     HIPCHK(hipMemsetAsync(c->d_counter.as<unsigned long long>() + 1, 0, 8, c->stream));
+    // The reads of chunk [b0, b0 + cnt) that left a resume state go through the cooperative pass right
+    // after their chunk's first pass, so the state buffer holds one chunk's states at a time: a read
+    // it resolves is done (status 0), one it hands on starts over in the passes below.
+    auto coop_resumed = [&](int64_t b0, int64_t cnt) -> int {
+      size_t tb = 0;
+      HIPCHK(select_resumed(c->d_roff.as<uint64_t>(), b0, cnt, c->d_status.as<uint32_t>(), nullptr, nullptr, nullptr,
+                            nullptr, &tb, c->stream));
+      if (int rc = c->d_seltmp.ensure(tb + 16)) return rc;
+      if (int rc = c->d_ids.ensure(cnt * 8)) return rc;
+      if (int rc = c->d_selst.ensure(cnt * 4)) return rc;
+      unsigned long long *d_cnt = c->d_counter.as<unsigned long long>() + 5;
+      HIPCHK(select_resumed(c->d_roff.as<uint64_t>(), b0, cnt, c->d_status.as<uint32_t>(), c->d_ids.as<int64_t>(),
+                            c->d_selst.as<uint32_t>(), d_cnt, c->d_seltmp.p, &tb, c->stream));
+      unsigned long long lanes_u = 0;
+      HIPCHK(hipMemcpyAsync(&lanes_u, d_cnt, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      const int64_t lanes = (int64_t)lanes_u;
+      if (lanes > 0) {
+        uint32_t stg_log2 = 10;
+        while ((1u << stg_log2) < 2u * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
+        const int full_blocks = c->n_cus * c->coop_waves_per_cu;
+        const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
+        const uint32_t freecap = 4096, hcap = 4096;
+        const uint64_t pool_bytes = std::min<uint64_t>(
+            (uint64_t)c->coop_pool_gb << 30,
+            std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
+        const uint32_t pool_pages = (uint32_t)(pool_bytes / (COOP_PG * 16ull));
+        if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
+        if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
+        if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
+        if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
+        if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
+        if (int rc = c->c_recb.ensure((uint64_t)blocks * COOP_RREC * 16)) return rc;
+        if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
+        if (int rc = c->c_next.ensure(64)) return rc;
+        if (int rc = c->r_status.ensure(lanes * 4)) return rc;
+        // largest first-pass stack first, as in the main cooperative pass below
+        const int64_t *ids = c->d_ids.as<int64_t>();
+        if (c->coop_order && lanes > 1) {
+          size_t ob = 0;
+          HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &ob, c->stream));
+          if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;
+          if (int rc = c->d_ordi.ensure(lanes * 8)) return rc;
+          if (int rc = c->d_ordids.ensure(lanes * 8)) return rc;
+          if (int rc = c->d_ordtmp.ensure(ob + 16)) return rc;
+          HIPCHK(order_heavy_first(c->d_selst.as<uint32_t>(), c->d_ids.as<int64_t>(), lanes, c->d_ordk.as<uint32_t>(),
+                                   c->d_ordi.as<uint32_t>(), c->d_ordids.as<int64_t>(), c->d_ordtmp.p, &ob, c->stream));
+          ids = c->d_ordids.as<int64_t>();
+        }
+        // the reads' widths afresh (their first-pass rows carry its gap_shadow updates; the coop
+        // pass replays them from the states)
+        AlnArgs W = A;
+        W.ids = ids;
+        W.n = lanes;
+        W.wbuf = c->d_wbuf.as<uint2>();
+        W.nN = c->d_nN.as<uint16_t>();
+        CoopArgs K = {};
+        K.ix[0] = c->ix[0];
+        K.ix[1] = c->ix[1];
+        K.o64[0] = c->o64[0].as<uint4>();
+        K.o64[1] = c->o64[1].as<uint4>();
+        K.seq = A.seq;
+        K.off = A.off;
+        K.len = A.len;
+        K.ids = ids;
+        K.n = lanes;
+        K.out_by_id = 1;
+        K.maxdiff_tab = A.maxdiff_tab;
+        K.wbuf = W.wbuf;
+        K.wstride = A.wstride;
+        K.wlen1 = A.wlen1;
+        K.nN = W.nN;
+        K.stg = c->c_stg.as<uint4>();
+        K.stg_log2 = stg_log2;
+        K.dir = c->c_dir.as<uint32_t>();
+        K.freel = c->c_free.as<uint32_t>();
+        K.freecap = freecap;
+        K.pool = c->c_pool.as<uint4>();
+        K.pool_pages = pool_pages;
+        K.pool_next = c->c_next.as<uint32_t>();
+        K.hits = c->c_hits.as<uint4>();
+        K.recb = c->c_recb.as<uint4>();
+        K.rdump = c->d_rdump.as<uint4>();
+        K.roff = c->d_roff.as<uint64_t>();
+        K.hcap = hcap;
+        K.max_iters = 1u << 24;
+        K.aln = c->d_aln.as<uint4>();
+        K.aln_total = c->stream_total;
+        K.aln_next = c->d_counter.as<unsigned long long>() + 1;
+        K.aln_off = c->d_aoff.as<uint64_t>();
+        K.n_aln = c->d_naln.as<int32_t>();
+        K.status = c->r_status.as<uint32_t>();
+        K.o = o;
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        HIPCHK(launch_width(W, c->block, c->stream));
+        HIPCHK(hipEventRecord(c->ev[5], c->stream));
+        HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
+        HIPCHK(hipEventRecord(c->ev[4], c->stream));
+        HIPCHK(resume_fixup(c->r_status.as<uint32_t>(), ids, lanes, c->d_status.as<uint32_t>(), c->d_roff.as<uint64_t>(),
+                            c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[4]));
+        float t_all = 0, t_w = 0;
+        HIPCHK(hipEventElapsedTime(&t_all, c->ev[3], c->ev[4]));
+        HIPCHK(hipEventElapsedTime(&t_w, c->ev[3], c->ev[5]));
+        std::vector<uint32_t> rs(lanes);
+        HIPCHK(hipMemcpy(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost));
+        int64_t ok = 0;
+        for (uint32_t v : rs) ok += v == 0;
+        res_ms += t_all;
+        res_w += t_w;
+        res_ok += ok;
+        if (c->verbose)
+          fprintf(stderr, "[ibwa_amd] chunk at %lld: %lld resumed reads through the cooperative pass, %.1f ms\n",
+                  (long long)b0, (long long)lanes, t_all);
+      }
+      // the next chunk's states start at the front of the buffer (the stored counts stay)
+      unsigned long long used = 0;
+      HIPCHK(hipMemcpy(&used, c->d_roff.as<unsigned long long>() + n, 8, hipMemcpyDeviceToHost));
+      c->stats.resume_records += (int64_t)used;
+      HIPCHK(hipMemsetAsync(c->d_roff.as<unsigned long long>() + n, 0, 8, c->stream));
+      return 0;
+    };
     for (int64_t b0 = 0; b0 < n; b0 += chunk) {
       const int64_t cnt = std::min(chunk, n - b0);
       AlnArgs B = A;
@@ -953,6 +1102,14 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.max_iters = c->gap_iter_budget;
       G.early_iters = c->gap_early_iters;
       G.early_entries = c->gap_early_entries;
+      G.early2_iters = c->gap_early2_iters;
+      G.early2_entries = c->gap_early2_entries;
+      if (resume) {
+        G.rdump = c->d_rdump.as<uint4>();
+        G.rd_next = c->d_roff.as<unsigned long long>() + n;
+        G.rd_cap = rd_cap;
+        G.roff = c->d_roff.as<uint64_t>() + b0;
+      }
       if (c->verbose || c->diag) {
         if (int rc = c->d_iters.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
         G.iters = c->d_iters.as<uint32_t>() + b0;
@@ -1006,6 +1163,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                 "seed widths %.3f candidate %.3f; exact steps %.3f (unique interval %.3f) (%.3g live lane-iterations)\n",
                 pf[11] / li, pf[12] / li, pf[13] / li, pf[14] / li, pf[15] / li, pf[17] / li, pf[18] / li, (double)pf[16]);
       }
+      if (resume_states)
+        if (int rc = coop_resumed(b0, cnt)) return rc;
     }
   }
   // first pass, in chunks of lanes_per_chunk reads
@@ -1079,6 +1238,15 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->stats.n_stack_overflow += (s_ & ST_STACK_OVERFLOW) != 0;
     c->stats.n_aln_overflow += (s_ & ST_ALN_OVERFLOW) != 0;
     c->stats.n_heavy += (s_ & ST_HEAVY) != 0;
+  }
+  if (resume_states) {
+    unsigned long long rs[2] = {0, 0};
+    HIPCHK(hipMemcpy(rs, c->d_roff.as<unsigned long long>() + n, 16, hipMemcpyDeviceToHost));
+    c->stats.n_resumed = (int64_t)rs[1];
+    c->stats.n_heavy += res_ok;  // handed on and resolved by the per-chunk cooperative launches
+    c->stats.n_coop += res_ok;
+    c->stats.ms_coop += res_ms;
+    c->stats.ms_coop_width += res_w;
   }
   if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: handed-on reads selected, %zu to retry\n", since(), c->retry_ids.size());
   // retry pass: larger stacks / hit arrays for the few reads that overflowed
@@ -1186,6 +1354,10 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     K.pool_next = c->c_next.as<uint32_t>();
     K.hits = c->c_hits.as<uint4>();
     K.recb = c->c_recb.as<uint4>();
+    if (resume_states) {
+      K.rdump = c->d_rdump.as<uint4>();
+      K.roff = c->d_roff.as<uint64_t>();
+    }
     if (c->coop_roots) {
       K.proot = c->c_proot.as<uint4>();
       K.pstore = pstore;
@@ -1312,13 +1484,13 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       }
     }
     if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop results on host\n", since());
-    c->stats.n_coop = lanes - (int64_t)next.size();
-    c->stats.ms_coop = a;
+    c->stats.n_coop += lanes - (int64_t)next.size();
+    c->stats.ms_coop += a;
     {
       float w = 0, rt = 0;
       HIPCHK(hipEventElapsedTime(&w, c->ev[3], c->ev[5]));
       HIPCHK(hipEventElapsedTime(&rt, c->ev[5], c->ev[6]));
-      c->stats.ms_coop_width = w;
+      c->stats.ms_coop_width += w;
       c->stats.ms_coop_roots = rt;
     }
     todo.swap(next);
@@ -1470,8 +1642,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(hipStreamSynchronize(c->stream));
     c->stream_len = std::min<unsigned long long>(c->stream_len, c->stream_total);
   }
-  c->stats.ms_retry = ms_r;
-  c->stats.n_retry = (int64_t)c->retry_ids.size();
+  c->stats.ms_retry = ms_r + res_ms;
+  c->stats.n_retry = (int64_t)c->retry_ids.size() + res_ok;
   c->stats.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return 0;

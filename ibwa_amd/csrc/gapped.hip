@@ -348,7 +348,11 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         stat |= ST_ALN_OVERFLOW;
         na = 0;
       } else {
-        for (int j = 0; j < na; ++j) ka->aln[pos + j] = ent1[P0 - 1 - j];
+        for (int j = 0; j < na; ++j) {
+          uint4 h = ent1[P0 - 1 - j];
+          h.w &= 0xFFFFu;  // the hit's last_diff_pos rides in bits 16-31 (resume states replay gap_shadow)
+          ka->aln[pos + j] = h;
+        }
         ka->aln_off[ro] = pos;
       }
     }
@@ -362,6 +366,84 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     n_pages = 0;
     st = 0;
     if (pl_) ++pf7;
+  };
+
+  // Resume states (LW, GapArgs::rdump): the lanes in `me` are between two pops; the whole wave copies
+  // each one's live stack, its hits and its search variables to the state buffer, and the lane hands
+  // its read on.  C (score minsc, slot cs, link cp) is the top of the lowest non-empty bucket.  Pops
+  // come in score order, so every stored entry scoring above minsc is live and every one below is
+  // dead.  At minsc the live entries are C and the list below it: the ones that were in the bucket
+  // when its level started, minus those popped from the top since, all in slots below any pushed
+  // since (the bump region only grows past live slots) -- i.e. every entry at minsc in a slot <= cp
+  // is live and every other one but C is dead.  So the state is the stored entries (after the dirty
+  // register entries are written back) that pass that test, in slot order: per bucket bottom to top.
+  auto dump_states = [&](bool me, int minsc, uint32_t cs, uint32_t cp) __attribute__((always_inline)) {
+    if (me) {
+      if (cfl & 1u) *slot_ptr(C_slot) = C;
+      if ((cfl & 6u) == 6u) *slot_ptr(D_slot) = D;
+    }
+    __threadfence_block();
+    KArgs *ka = args();
+    unsigned long long dm = __ballot(me);
+    while (dm) {
+      const int src = __builtin_ctzll(dm);
+      dm &= dm - 1;
+      const uint32_t sbump = (uint32_t)__shfl((int)bump, src), sna = (uint32_t)__shfl(n_aln, src);
+      const uint32_t sne = (uint32_t)__shfl(n_entries, src);
+      const int smin = __shfl(minsc, src);
+      const uint32_t scs = (uint32_t)__shfl((int)cs, src), scp = (uint32_t)__shfl((int)cp, src);
+      // the first pass runs 64 reads per wave: lane x's static region is region gtid
+      const uint64_t sg = gtid - (uint64_t)lane + (uint64_t)src;
+      const uint4 *const se1 = A.ent + sg * P0;
+      const uint16_t *const spt = ka->ptab_g + sg * GAP_MAX_PAGES;
+      // two sweeps over the slots: count the live entries, then (room reserved) copy them
+      auto sweep = [&](uint4 *out) __attribute__((always_inline)) -> uint32_t {
+        uint32_t cnt = 0;
+        for (uint32_t b0 = 0; b0 < sbump; b0 += 128) {
+          const uint32_t s0 = b0 + (uint32_t)lane, s1 = s0 + 64u;
+          const bool ok0 = s0 < sbump && (s0 < P0 - HS || s0 >= P0), ok1 = s1 < sbump && (s1 < P0 - HS || s1 >= P0);
+          auto sp = [&](uint32_t x) __attribute__((always_inline)) -> const uint4 * {
+            if (x < P0) return se1 + x;
+            return pool + ((uint64_t)spt[(x - P0) >> LG] << LG) + ((x - P0) & ((1u << LG) - 1u));
+          };
+          uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
+          if (ok0) e0 = *sp(s0);
+          if (ok1) e1 = *sp(s1);
+          auto live = [&](const uint4 &x, uint32_t slot) __attribute__((always_inline)) {
+            const int sc = (int)(((x.w >> 16) & 31u) * (uint32_t)o.s_mm + ((x.w >> 21) & 7u) * (uint32_t)o.s_gapo +
+                                 ((x.w >> 24) & 15u) * (uint32_t)o.s_gape);
+            return sc > smin || (sc == smin && (slot == scs || (scp != NILH && slot <= scp)));
+          };
+          const bool l0 = ok0 && live(e0, s0), l1 = ok1 && live(e1, s1);
+          const unsigned long long m0 = __ballot(l0), m1 = __ballot(l1);
+          if (out && l0) out[RD_HDR + cnt + (uint32_t)__popcll(m0 & lt_mask)] = e0;
+          cnt += (uint32_t)__popcll(m0);
+          if (out && l1) out[RD_HDR + cnt + (uint32_t)__popcll(m1 & lt_mask)] = e1;
+          cnt += (uint32_t)__popcll(m1);
+        }
+        return cnt;
+      };
+      const uint32_t nlive = sweep(nullptr);
+      const unsigned long long need = (unsigned long long)RD_HDR + nlive + sna;
+      unsigned long long off = 0;
+      if (lane == src) off = atomicAdd(ka->rd_next, need);
+      off = __shfl(off, src);
+      if (off + need <= ka->rd_cap) {
+        uint4 *const out = ka->rdump + off;
+        const uint32_t cnt = sweep(out);
+        for (uint32_t j = (uint32_t)lane; j < sna; j += 64) out[RD_HDR + cnt + j] = se1[P0 - 1 - j];
+        if (lane == src) {
+          out[0] = make_uint4(cnt, sna, (uint32_t)smin, sne);
+          out[1] = make_uint4((uint32_t)best_score, (uint32_t)best_cnt, (uint32_t)max_diff, 0u);
+          ka->roff[ro] = off + 1;
+          atomicAdd(ka->rd_next + 1, 1ull);  // states stored
+        }
+      }
+    }
+    if (me) {
+      status |= ST_HEAVY | (uint32_t)(n_entries < 0xFFFF ? n_entries : 0xFFFF) << 16;
+      n_entries = 0;
+    }
   };
 
   for (;;) {
@@ -399,6 +481,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       C_valid = true;
       C_load = false;
       cfl = 0;
+      end_stat = 0;  // LW: bit 31 = leave a resume state at the next pop
       st = 1;
     };
     // LW: reads claimed last iteration -- their records reached LDS with that iteration's loads
@@ -506,15 +589,23 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     if (PROF && lane == 0) ++pf9;
     // ------------------------------------------------ decide this iteration's work
     // search lanes pop C; exact lanes advance one symbol
-    bool do_pop = false, finish = false, do_mat = false;
-    if (((A.max_iters && n_iter > A.max_iters) ||
-         (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries)) &&
+    bool do_pop = false, finish = false, do_mat = false, dump_now = false;
+    const bool over_budget = A.max_iters && n_iter > A.max_iters;
+    if ((over_budget || (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries) ||
+         (A.early2_iters && n_iter > A.early2_iters && n_entries > (int)A.early2_entries)) &&
         (st == 1 || st == 2)) {
-      // a long search: the retry pass re-runs it from the start; bits 16-31 keep the stack size
-      // (the cooperative pass takes the biggest first, so its longest reads do not start last)
-      status |= ST_HEAVY | (uint32_t)(n_entries < 0xFFFF ? n_entries : 0xFFFF) << 16;
-      st = 1;
-      n_entries = 0;
+      if (LW && A.rdump && !over_budget && st == 1) {
+        // resume: the read leaves its search state at this pop (below)
+        end_stat |= 0x80000000u;
+      } else if (LW && A.rdump && !over_budget) {
+        // resume: the exact sub-search ends first
+      } else {
+        // a long search: the retry pass re-runs it from the start; bits 16-31 keep the stack size
+        // (the cooperative pass takes the biggest first, so its longest reads do not start last)
+        status |= ST_HEAVY | (uint32_t)(n_entries < 0xFFFF ? n_entries : 0xFFFF) << 16;
+        st = 1;
+        n_entries = 0;
+      }
     }
     uint4 e = make_uint4(0, 0, 0, 0);
     int a = 0, i = 0, ldp = 0, e_mm = 0, e_go = 0, e_ge = 0, state = 0, m = 0, m_seed = 0;
@@ -533,6 +624,10 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         const int e_score = (e_mm * o.s_mm + e_go * o.s_gapo + e_ge * o.s_gape) & 0x7ff;
         if (!(o.mode & MODE_NONSTOP) && (uint32_t)e_score > (uint32_t)(best_score + o.s_mm)) {
           finish = true;  // bwtgap.c:143 (after the pop; nothing else observes the stack)
+        } else if (LW && (end_stat >> 31)) {
+          // resume state (dump_states): C is the top of the lowest non-empty bucket
+          dump_now = true;
+          m = e_score;
         } else if (!WIDE && state == STATE_G) {
           do_mat = true;  // a gap group: its top deletion is the entry the reference pops
         } else {
@@ -548,6 +643,10 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     }
     // pop bookkeeping (no memory round trip): unlink C, choose the next candidate
     uint32_t load_slot = 0;
+    if (LW && __ballot(dump_now)) {
+      dump_states(dump_now, m, C_slot, E::prev(C));
+      if (dump_now) finish = true;  // handed on (status set), with or without a stored state
+    }
     if (do_pop) {
       const uint32_t prev = E::prev(e);
       lds_heads[hidx(C_b)] = (H)prev;
@@ -1086,7 +1185,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         continue;
       }
       ent1[P0 - 1 - n_aln] = make_uint4((uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
-                                        k, l, (uint32_t)score);
+                                        k, l, (uint32_t)score | (uint32_t)ldp << 16);
       ++n_aln;
     }
     

@@ -20,6 +20,20 @@ namespace {
 struct NonZero {
   __host__ __device__ bool operator()(uint32_t s) const { return s != 0u; }
 };
+struct NonZero64 {
+  __host__ __device__ bool operator()(uint64_t s) const { return s != 0u; }
+};
+
+// after a cooperative launch over resumed reads: a resolved read is done (status 0); one the pass
+// handed on loses its state (the later passes run it from the start)
+__global__ void k_resume_fixup(const uint32_t *r_status, const int64_t *ids, int64_t n, uint32_t *status,
+                               uint64_t *roff) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = ids[i];
+    if (r_status[i] == 0u) status[r] = 0u;
+    else roff[r] = 0u;
+  }
+}
 
 __global__ void k_gather_status(const uint32_t *status, const int64_t *ids, const unsigned long long *count,
                                 uint32_t *out) {
@@ -41,6 +55,25 @@ __global__ void k_gather_ids(const int64_t *ids, const uint32_t *perm, unsigned 
 }
 
 }  // namespace
+
+hipError_t select_resumed(const uint64_t *roff, int64_t base, int64_t n, const uint32_t *status, int64_t *ids,
+                          uint32_t *sel_status, unsigned long long *d_count, void *tmp, size_t *tmp_bytes,
+                          hipStream_t st) {
+  auto in = rocprim::make_counting_iterator<int64_t>(base);
+  auto flags = rocprim::make_transform_iterator(roff + base, NonZero64());
+  if (!tmp) return rocprim::select(nullptr, *tmp_bytes, in, flags, ids, d_count, (size_t)n, st);
+  hipError_t e = rocprim::select(tmp, *tmp_bytes, in, flags, ids, d_count, (size_t)n, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gather_status, dim3(1024), dim3(256), 0, st, status, ids, d_count, sel_status);
+  return hipGetLastError();
+}
+
+hipError_t resume_fixup(const uint32_t *r_status, const int64_t *ids, int64_t n, uint32_t *status, uint64_t *roff,
+                        hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_resume_fixup, dim3(1024), dim3(256), 0, st, r_status, ids, n, status, roff);
+  return hipGetLastError();
+}
 
 hipError_t order_heavy_first(const uint32_t *sel_status, const int64_t *ids, unsigned long long n, uint32_t *keys,
                              uint32_t *idx, int64_t *ids_out, void *tmp, size_t *tmp_bytes, hipStream_t st) {

@@ -31,7 +31,8 @@ class RunStats(c.Structure):
                 ("n_launch_search", c.c_int64), ("path", c.c_int), ("kmer_k", c.c_int),
                 ("n_stack_overflow", c.c_int64), ("n_aln_overflow", c.c_int64), ("n_heavy", c.c_int64), ("ms_sw", c.c_double),
                 ("n_coop", c.c_int64), ("ms_coop", c.c_double), ("ms_sa2pos", c.c_double),
-                ("sa2pos_full", c.c_int), ("ms_coop_width", c.c_double), ("ms_coop_roots", c.c_double)]
+                ("sa2pos_full", c.c_int), ("ms_coop_width", c.c_double), ("ms_coop_roots", c.c_double),
+                ("n_resumed", c.c_int64), ("resume_records", c.c_int64)]
 
 
 class RefSeq(c.Structure):

@@ -141,6 +141,10 @@ typedef struct {
 	int sa2pos_full;           /* 1: it gathered from a full SA, 0: it walked the sampled SA */
 	double ms_coop_width;      /* of ms_coop: the heavy reads' widths (k_width) */
 	double ms_coop_roots;      /* of ms_coop: their level 0 (k_coop_roots); the rest is k_coop */
+	int64_t n_resumed;         /* heavy reads handed on with their search state (the cooperative
+	                              pass resumes them instead of starting over) */
+	int64_t resume_records;    /* 16 B records those states took (requested, incl. any that did not fit);
+	                              the cooperative pass runs them chunk by chunk (part of ms_coop) */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 
@@ -162,6 +166,11 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "gap_iter_budget" (8000)       first-pass iterations before a read goes to the cooperative pass
  *   "gap_early_iters", "gap_early_entries" (3000, 1000)
  *                                  earlier hand-off of a read whose stack holds that many entries
+ *   "gap_early2_iters", "gap_early2_entries" (0, 0)  a second such rule (0: off)
+ *   "gap_resume" (0/1, default 1), "gap_resume_gb" (48)  an early hand-off leaves the read's search
+ *                                  state (at the next score-level boundary) for the cooperative pass,
+ *                                  which resumes it instead of starting over; state buffer size
+ *                                  ("gap_resume_records": the buffer in 16 B records, for tests)
  *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 

@@ -72,6 +72,8 @@ def main():
     print(json.dumps({k: v for k, v in res.items() if k != "features"}), flush=True)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
+    # raw per-read arrays for offline analysis (first-pass iterations, features, handed on)
+    np.savez_compressed(a.out.rsplit(".", 1)[0] + ".npz", it=it, ft=ft, heavy=heavy, ids=ids, ps=ps)
     eng.close()
 
 
