@@ -183,17 +183,18 @@ def cpu_and_parity(eng, eopt, seq, off, lns, n_aln, alns, budget_s, check, heavy
                      f"oracle/ibwa_oracle.c)"}
     # heavy reads: resolved outside the first pass
     ids, ps = eng.retry_info()
-    by_pass = {int(k): int((ps == k).sum()) for k in (1, 2, 3)}
+    by_pass = {int(k): int((ps == k).sum()) for k in (1, 2, 3, 4)}
     sel = []
     for k, cap in ((2, 2000), (3, 2000), (1, 1 << 30)):
-        cand = ids[(ps == k) & (ids >= n_s)]
+        # the cooperative pass: from the start (1) or resuming the first pass's state (4)
+        cand = ids[(np.isin(ps, (1, 4)) if k == 1 else ps == k) & (ids >= n_s)]
         if cand.size > cap:
             cand = cand[np.linspace(0, cand.size - 1, cap).astype(np.int64)]
         sel.append(cand)
     # wide/general first (few), then coop reads spread evenly over the batch
     coop = sel[2]
     order = np.concatenate([sel[0], sel[1], coop[np.argsort(np.arange(coop.size) % 64, kind="stable")]])
-    checked = {1: 0, 2: 0, 3: 0}
+    checked = {1: 0, 2: 0, 3: 0, 4: 0}
     bad = []
     t0 = time.perf_counter()
     pass_of = dict(zip(ids.tolist(), ps.tolist()))
@@ -210,15 +211,16 @@ def cpu_and_parity(eng, eopt, seq, off, lns, n_aln, alns, budget_s, check, heavy
             if got[j] != exp[j] or n_aln[i] != hn[j]:
                 bad.append(int(i))
     parity = {"first_reads": n_s, "first_reads_ok": ok_first,
-              "handed_on_reads": int(ids.size), "handed_on_by_pass": {"coop": by_pass[1], "wide": by_pass[2],
-                                                                       "general": by_pass[3]},
-              "handed_on_checked": {"coop": checked[1], "wide": checked[2], "general": checked[3]},
+              "handed_on_reads": int(ids.size), "handed_on_by_pass": {"coop": by_pass[1], "coop_resumed": by_pass[4],
+                                                                       "wide": by_pass[2], "general": by_pass[3]},
+              "handed_on_checked": {"coop": checked[1], "coop_resumed": checked[4], "wide": checked[2],
+                                    "general": checked[3]},
               "handed_on_mismatches": bad[:20], "handed_on_ok": not bad,
               "heavy_check_s": time.perf_counter() - t0}
     parity["ok"] = ok_first and not bad and n_s + sum(checked.values()) >= 200_000
     # which of the sampled first reads the cooperative pass resolved (for the per-kernel roofline)
     coop_first = np.zeros(n_s, dtype=bool)
-    cid = ids[(ps == 1) & (ids < n_s)]
+    cid = ids[np.isin(ps, (1, 4)) & (ids < n_s)]
     coop_first[cid] = True
     return cpu, (tch, wtch, coop_first), parity
 
@@ -650,6 +652,12 @@ def main():
                      "k_gapped": (float(mg[~coop_first].sum()) * scale, ms_s / launches, ["k_gapped"]),
                      "k_coop": (float(mg[coop_first].sum()) * scale, (ms_c - ms_cw) / launches,
                                 ["k_coop", "k_coop_roots"])}
+            if int(stl.n_resumed) > 0:
+                # a resumed heavy read's search is split between the two kernels at its hand-off (the
+                # first pass's part is not re-run), so bwt_match_gap's touches price them together
+                per_k = {"k_width": per_k["k_width"],
+                         "k_gapped+k_coop": (float(mg.sum()) * scale, (ms_s + ms_c - ms_cw) / launches,
+                                             ["k_gapped", "k_coop"])}
             pk = {}
             for name, (tt, ms, kn) in per_k.items():
                 ab = tt * 64.0
@@ -667,7 +675,7 @@ def main():
                                   "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None}}
             dom = max(pk, key=lambda x: pk[x]["kernel_ms_per_step"])
             d_ = pk[dom]
-            result["roofline"] = {"bound": "hbm", "kernel": dom + (" (+ k_coop_roots)" if dom == "k_coop" else ""),
+            result["roofline"] = {"bound": "hbm", "kernel": dom + (" (+ k_coop_roots)" if dom.endswith("k_coop") else ""),
                                   "achieved": d_["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d_["frac"],
                                   "traffic": d_["traffic"], "traffic_source": d_["traffic_source"],
                                   "algorithmic_bytes_per_step": d_["algorithmic_bytes_per_step"],

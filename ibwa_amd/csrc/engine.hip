@@ -150,6 +150,9 @@ struct ibwa_ctx {
   int gap_resume = 1;                // early hand-offs leave their search state for the coop pass (LW)
   int gap_resume_gb = 48;            // state buffer (GiB, at most ~4 KiB per read of the batch)
   int64_t gap_resume_records = 0;    // tests: state buffer of this many 16 B records (0: by gap_resume_gb)
+  // the early hand-off rule when the read leaves a resume state (nothing is re-run, so it pays to hand
+  // on earlier: swept at 50M reads, flat optimum, profiles/r03_resume_sweep*.log)
+  uint32_t gap_resume_iters = 2000, gap_resume_entries = 300;
   DBuf d_cw, d_ptabg;
   DBuf d_rdump, d_roff;  // resume states (GapArgs::rdump) and per-read offsets
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
@@ -168,6 +171,7 @@ struct ibwa_ctx {
   uint64_t gap_stream_min = 1u << 20;   // ... and at least this many in total
   std::vector<uint64_t> h_aoff;
   std::vector<uint8_t> retry_pass;  // per retry_ids entry: 1 coop, 2 wide, 3 general kernels
+  std::vector<int64_t> resumed_ids; // reads the cooperative pass resolved from a resume state (retry_info pass 4)
   bool naln_on_host = true;  // h_naln mirrors d_naln
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
@@ -376,6 +380,8 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_resume" && (value == 0 || value == 1)) c->gap_resume = (int)value;
   else if (k == "gap_resume_gb" && value >= 1 && value <= 256) c->gap_resume_gb = (int)value;
   else if (k == "gap_resume_records" && value >= 0) c->gap_resume_records = (int64_t)value;
+  else if (k == "gap_resume_iters" && value >= 0) c->gap_resume_iters = (uint32_t)value;
+  else if (k == "gap_resume_entries" && value >= 0) c->gap_resume_entries = (uint32_t)value;
   else if (k == "coop_order" && (value == 0 || value == 1)) c->coop_order = (int)value;
   else if (k == "coop_roots" && (value == 0 || value == 1)) c->coop_roots = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
@@ -882,6 +888,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   float ms_w = 0, ms_s = 0;
   c->stream_out = v2;
   bool resume_states = false;  // the first pass left resume states (GapArgs::rdump)
+  c->resumed_ids.clear();
   float res_ms = 0, res_w = 0;  // the cooperative launches over resumed reads (after each chunk)
   int64_t res_ok = 0;           // reads they resolved
   c->stats.n_resumed = 0;
@@ -1051,9 +1058,15 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         HIPCHK(hipEventElapsedTime(&t_all, c->ev[3], c->ev[4]));
         HIPCHK(hipEventElapsedTime(&t_w, c->ev[3], c->ev[5]));
         std::vector<uint32_t> rs(lanes);
+        std::vector<int64_t> rid(lanes);
         HIPCHK(hipMemcpy(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(rid.data(), ids, lanes * 8, hipMemcpyDeviceToHost));
         int64_t ok = 0;
-        for (uint32_t v : rs) ok += v == 0;
+        for (int64_t j = 0; j < lanes; ++j)
+          if (rs[j] == 0) {
+            ++ok;
+            c->resumed_ids.push_back(rid[j]);
+          }
         res_ms += t_all;
         res_w += t_w;
         res_ok += ok;
@@ -1100,8 +1113,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.n_aln = c->d_naln.as<int32_t>() + b0;
       G.status = c->d_status.as<uint32_t>() + b0;
       G.max_iters = c->gap_iter_budget;
-      G.early_iters = c->gap_early_iters;
-      G.early_entries = c->gap_early_entries;
+      G.early_iters = resume ? c->gap_resume_iters : c->gap_early_iters;
+      G.early_entries = resume ? c->gap_resume_entries : c->gap_early_entries;
       G.early2_iters = c->gap_early2_iters;
       G.early2_entries = c->gap_early2_entries;
       if (resume) {
@@ -1650,10 +1663,10 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
 }
 
 int ibwa_batch_retry_info(const ibwa_ctx_t *c, int64_t *ids, uint8_t *pass, int64_t cap, int64_t *n) {
-  const int64_t m = (int64_t)c->retry_ids.size();
+  const int64_t m0 = (int64_t)c->retry_ids.size(), m = m0 + (int64_t)c->resumed_ids.size();
   for (int64_t j = 0; j < std::min(m, cap); ++j) {
-    if (ids) ids[j] = c->retry_ids[j];
-    if (pass) pass[j] = j < (int64_t)c->retry_pass.size() ? c->retry_pass[j] : 0;
+    if (ids) ids[j] = j < m0 ? c->retry_ids[j] : c->resumed_ids[j - m0];
+    if (pass) pass[j] = j >= m0 ? 4 : j < (int64_t)c->retry_pass.size() ? c->retry_pass[j] : 0;
   }
   if (n) *n = m;
   return 0;

@@ -234,7 +234,7 @@ class Engine:
 
     def retry_info(self):
         """(read ids, pass) of the reads the last run's first pass handed on; pass 1 = coop,
-        2 = sequential wide, 3 = general kernels."""
+        2 = sequential wide, 3 = general kernels, 4 = coop resuming the first pass's state."""
         n = c.c_int64()
         _chk(lib().ibwa_batch_retry_info(self.h, None, None, 0, c.byref(n)))
         ids = np.zeros(n.value, np.int64)

@@ -171,6 +171,7 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *                                  state (at the next score-level boundary) for the cooperative pass,
  *                                  which resumes it instead of starting over; state buffer size
  *                                  ("gap_resume_records": the buffer in 16 B records, for tests)
+ *   "gap_resume_iters", "gap_resume_entries" (2000, 300)  the early hand-off rule when states are left
  *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
@@ -190,7 +191,8 @@ int ibwa_aln_parse_args(int argc, char *const *argv, ibwa_gap_opt_t *opt, int *n
 /*
  * Reads of the last ibwa_batch_run that the first pass handed on, and the pass that resolved
  * each: 1 the wave-cooperative pass (coop.hip), 2 the sequential wide pass (gapped.hip, one
- * read per wave), 3 the general kernels (aln.hip).  Writes min(cap, n) entries; *n = their count.
+ * read per wave), 3 the general kernels (aln.hip), 4 the wave-cooperative pass resuming the first
+ * pass's search state (after the read's chunk).  Writes min(cap, n) entries; *n = their count.
  */
 int ibwa_batch_retry_info(const ibwa_ctx_t *ctx, int64_t *ids, uint8_t *pass, int64_t cap, int64_t *n);
 

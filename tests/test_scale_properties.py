@@ -111,21 +111,21 @@ def test_exact_reads_round_trip(mid_genome):
     # pass resumes them (gap_resume), under the options above, with paged first-pass stacks and with a
     # state buffer too small for some of them (those start over); the LDS-width first pass, which
     # leaves the states, takes reads up to ~100 bp (its LDS records) with max_diff <= 6
-    ([], 100, 0.01, 30_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    ([], 90, 0.02, 8_000, {"gap_early_iters": 60, "gap_early_entries": 16}),
-    (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    (["-m", "300"], 100, 0.02, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    (["-m", "2000"], 100, 0.03, 4_000, {"gap_early_iters": 40, "gap_early_entries": 8}),
-    (["-N", "-n", "2"], 100, 0.01, 4_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    (["-L"], 100, 0.02, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    (["-c"], 100, 0.02, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    (["-l", "20", "-k", "1"], 100, 0.02, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    (["-n", "1"], 100, 0.01, 8_000, {"gap_early_iters": 5, "gap_early_entries": 2}),
-    (["-i", "0", "-d", "0"], 70, 0.02, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4}),
-    ([], 100, 0.01, 30_000, {"gap_early_iters": 20, "gap_early_entries": 4, "coop_roots": 0}),
-    ([], 100, 0.02, 20_000, {"gap_early_iters": 100, "gap_early_entries": 50, "gap_cap1": 256,
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    ([], 90, 0.02, 8_000, {"gap_resume_iters": 60, "gap_resume_entries": 16}),
+    (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-m", "300"], 100, 0.02, 8_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-m", "2000"], 100, 0.03, 4_000, {"gap_resume_iters": 40, "gap_resume_entries": 8}),
+    (["-N", "-n", "2"], 100, 0.01, 4_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-L"], 100, 0.02, 8_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-c"], 100, 0.02, 8_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-l", "20", "-k", "1"], 100, 0.02, 8_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-n", "1"], 100, 0.01, 8_000, {"gap_resume_iters": 5, "gap_resume_entries": 2}),
+    (["-i", "0", "-d", "0"], 70, 0.02, 8_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "coop_roots": 0}),
+    ([], 100, 0.02, 20_000, {"gap_resume_iters": 100, "gap_resume_entries": 50, "gap_cap1": 256,
                              "gap_pages_per_block": 8}),
-    ([], 100, 0.01, 30_000, {"gap_early_iters": 20, "gap_early_entries": 4, "gap_resume_records": 20_000}),
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_resume_records": 20_000}),
     ([], 100, 0.01, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4, "gap_resume": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
@@ -133,7 +133,8 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     o, e = eopt(argv)
     defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
-                "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0}
+                "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
+                "gap_resume_entries": 300}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
@@ -144,7 +145,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
             eng.set_option(k, defaults[k])
     if "-m" in argv:
         assert st.n_heavy > 0 and st.n_coop == st.n_heavy  # nothing handed on to the sequential kernel
-    if "gap_early_iters" in tune and tune.get("gap_resume", 1):
+    if "gap_resume_iters" in tune and tune.get("gap_resume", 1):
         assert st.n_resumed > 0  # the resume path ran
         if "gap_resume_records" in tune:
             assert st.resume_records > tune["gap_resume_records"]  # ... and some states did not fit
