@@ -352,8 +352,8 @@ struct Shm {
 // Resume a read from the first pass's state at a level boundary (GapArgs::rdump): {entries, hits,
 // lowest score, stack size}, {best_score, best_cnt, max_diff}, the live entries in slot order (per
 // bucket bottom to top), the hits in the order they were added.  gap_shadow (bwtgap.c:81-91) of
-// each hit is replayed, in order, on the widths k_width computed afresh; each entry goes to the top
-// of its bucket.  Out of line: k_coop's chain loop keeps its registers.
+// each hit is replayed, in order, on widths k_width computed afresh (replay; else the widths are
+// the first pass's own, already shadowed); each entry goes to the top of its bucket.  Out of line: k_coop's chain loop keeps its registers.
 struct ResumeOut {
   int s, best_score, best_cnt, max_diff, n_aln;
   uint32_t n_live, status, n_free;
@@ -361,7 +361,7 @@ struct ResumeOut {
 __device__ __noinline__ ResumeOut resume_state(const uint4 *rs, Shm *S, uint4 *pool, uint32_t *dir, uint4 *hitv,
                                                uint32_t hcap, uint32_t *freel, uint32_t n_free, uint32_t *pool_next,
                                                uint32_t pool_pages, uint32_t seq_len, int s_mm, int s_gapo, int s_gape,
-                                               int n_stacks, int lane) {
+                                               int n_stacks, int lane, bool replay) {
   ResumeOut R;
   __syncthreads();
   const uint4 h0 = rs[0], h1 = rs[1];
@@ -374,7 +374,7 @@ __device__ __noinline__ ResumeOut resume_state(const uint4 *rs, Shm *S, uint4 *p
   R.status = 0;
   for (uint32_t j = 0; j < nh && j < hcap; ++j) {
     const uint4 h = rs[RD_HDR + ne + j];
-    const int h_a = (int)((h.x >> 24) & 1u), h_ldp = (int)(h.w >> 16);
+    const int h_a = (int)((h.x >> 24) & 1u), h_ldp = replay ? (int)(h.w >> 16) : 0;
     const uint32_t x = h.z - h.y + 1u;
     uint32_t jrun = 0;
     for (int base = 0; base < h_ldp; base += 64) {
@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     if (len > COOP_MAXLEN || o.n_stacks > NSTK || (1u << A.stg_log2) < 9u * (uint32_t)(len + 1) + 16u ||
         (len > o.seed_len && o.seed_len > COOP_SEEDMAX)) {
       status = ST_STACK_OVERFLOW | 1u << 8;  // not for this kernel: the sequential kernel takes it
-    } else if ((int)A.nN[r] > opt_max_diff) {
+    } else if ((int)A.nN[A.wb_base >= 0 ? rr - A.wb_base : r] > opt_max_diff) {
       // bwtgap.c:116-122: no hit
     } else {
       // ---------------------------------------------- per-read setup
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       const uint64_t rof = A.roff ? A.roff[rr] : 0ull;
       // level 0 done by k_coop_roots: the records of its two chains (A.proot[2 r], [2 r + 1])
       bool pro = !rof && A.proot && (A.proot[2 * r].w & 0xFFu) == 0u && (A.proot[2 * r + 1].w & 0xFFu) == 0u;
-      const uint2 *wb = A.wbuf + (uint64_t)r * A.wstride;
+      const uint2 *wb = A.wbuf + (uint64_t)(A.wb_base >= 0 ? rr - A.wb_base : r) * A.wstride;
       for (int j = lane; j < len; j += 64) {
         const uint32_t c = sq[j];
         S.str[j] = (uint8_t)c;
@@ -626,7 +626,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
       int s = 0;            // level (score bucket)
       if (rof) {
         const ResumeOut ro_ = resume_state(A.rdump + (rof - 1), &S, A.pool, dir, hitv, A.hcap, freel, n_free, A.pool_next,
-                                           A.pool_pages, ixv0.seq_len, o.s_mm, o.s_gapo, o.s_gape, o.n_stacks, lane);
+                                           A.pool_pages, ixv0.seq_len, o.s_mm, o.s_gapo, o.s_gape, o.n_stacks, lane,
+                                           A.wb_base < 0);
         s = ro_.s;
         n_live = ro_.n_live;
         best_score = ro_.best_score;

@@ -169,6 +169,10 @@ struct CoopArgs {
   uint64_t pstore_cap;       // pstore capacity (entries)
   const uint4 *rdump;        // first-pass search states (GapArgs::rdump), roff[read] 1 + offset, 0: none
   const uint64_t *roff;
+  // >= 0: the widths and N counts are the first pass's own, of read (id - wb_base) of its chunk (right
+  // after it: its gap_shadow updates are in them, so a resumed read does not replay them); -1: per
+  // launch read (k_width run for this launch)
+  int64_t wb_base;
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);

@@ -980,7 +980,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
             (uint64_t)c->coop_pool_gb << 30,
             std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
         const uint32_t pool_pages = (uint32_t)(pool_bytes / (COOP_PG * 16ull));
-        if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
         if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
         if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
         if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
@@ -1002,13 +1001,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                                    c->d_ordi.as<uint32_t>(), c->d_ordids.as<int64_t>(), c->d_ordtmp.p, &ob, c->stream));
           ids = c->d_ordids.as<int64_t>();
         }
-        // the reads' widths afresh (their first-pass rows carry its gap_shadow updates; the coop
-        // pass replays them from the states)
-        AlnArgs W = A;
-        W.ids = ids;
-        W.n = lanes;
-        W.wbuf = c->d_wbuf.as<uint2>();
-        W.nN = c->d_nN.as<uint16_t>();
+        // the widths and N counts are the chunk's own first-pass rows, still in place (their gap_shadow
+        // updates included: the pass does not replay them)
         CoopArgs K = {};
         K.ix[0] = c->ix[0];
         K.ix[1] = c->ix[1];
@@ -1021,10 +1015,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         K.n = lanes;
         K.out_by_id = 1;
         K.maxdiff_tab = A.maxdiff_tab;
-        K.wbuf = W.wbuf;
+        K.wbuf = c->d_wbuf.as<uint2>();
+        K.wb_base = b0;
         K.wstride = A.wstride;
         K.wlen1 = A.wlen1;
-        K.nN = W.nN;
+        K.nN = c->d_nN.as<uint16_t>();
         K.stg = c->c_stg.as<uint4>();
         K.stg_log2 = stg_log2;
         K.dir = c->c_dir.as<uint32_t>();
@@ -1047,7 +1042,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         K.status = c->r_status.as<uint32_t>();
         K.o = o;
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
-        HIPCHK(launch_width(W, c->block, c->stream));
         HIPCHK(hipEventRecord(c->ev[5], c->stream));
         HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
         HIPCHK(hipEventRecord(c->ev[4], c->stream));
@@ -1342,6 +1336,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     B.wbuf = c->d_wbuf.as<uint2>();
     B.nN = c->d_nN.as<uint16_t>();
     CoopArgs K = {};
+    K.wb_base = -1;  // widths from this launch's k_width
     K.ix[0] = c->ix[0];
     K.ix[1] = c->ix[1];
     K.o64[0] = c->o64[0].as<uint4>();
