@@ -126,6 +126,8 @@ def test_exact_reads_round_trip(mid_genome):
     ([], 100, 0.02, 20_000, {"gap_resume_iters": 100, "gap_resume_entries": 50, "gap_cap1": 256,
                              "gap_pages_per_block": 8}),
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_resume_records": 20_000}),
+    # a 1 GiB page pool: resumed reads that run out of pages start over in the later passes
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "coop_pool_gb": 1}),
     ([], 100, 0.01, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4, "gap_resume": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
@@ -134,7 +136,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
-                "gap_resume_entries": 300}
+                "gap_resume_entries": 300, "coop_pool_gb": 16}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
