@@ -109,6 +109,8 @@ struct GapArgs {
   unsigned long long *rd_next;
   unsigned long long rd_cap;
   uint64_t *roff;
+  uint32_t tail_lanes;       // resume also when no read is left to claim and <= tail_lanes of the wave
+  uint32_t tail_iters;       //   are busy, for a read past tail_iters iterations (0: off)
   AlnOpt o;
 };
 constexpr int RD_HDR = 2;  // resume state header: {entries, hits, lowest score, stack size}, {best_score, best_cnt, max_diff, 0}

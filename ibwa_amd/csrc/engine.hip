@@ -153,6 +153,9 @@ struct ibwa_ctx {
   // the early hand-off rule when the read leaves a resume state (nothing is re-run, so it pays to hand
   // on earlier: swept at 50M reads, flat optimum, profiles/r03_resume_sweep*.log)
   uint32_t gap_resume_iters = 2000, gap_resume_entries = 300;
+  // resume in a launch's tail (GapArgs::tail_lanes): 16 / 200 measured 5868 vs 5884 ms per 50M-read
+  // step (profiles/r03_tail_sweep.log; 8, 32, 4 / 500 in between)
+  uint32_t gap_tail_lanes = 16, gap_tail_iters = 200;
   DBuf d_cw, d_ptabg;
   DBuf d_rdump, d_roff;  // resume states (GapArgs::rdump) and per-read offsets
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
@@ -382,6 +385,8 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_resume_records" && value >= 0) c->gap_resume_records = (int64_t)value;
   else if (k == "gap_resume_iters" && value >= 0) c->gap_resume_iters = (uint32_t)value;
   else if (k == "gap_resume_entries" && value >= 0) c->gap_resume_entries = (uint32_t)value;
+  else if (k == "gap_tail_lanes" && value >= 0 && value <= 64) c->gap_tail_lanes = (uint32_t)value;
+  else if (k == "gap_tail_iters" && value >= 0) c->gap_tail_iters = (uint32_t)value;
   else if (k == "coop_order" && (value == 0 || value == 1)) c->coop_order = (int)value;
   else if (k == "coop_roots" && (value == 0 || value == 1)) c->coop_roots = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
@@ -1116,6 +1121,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         G.rd_next = c->d_roff.as<unsigned long long>() + n;
         G.rd_cap = rd_cap;
         G.roff = c->d_roff.as<uint64_t>() + b0;
+        G.tail_lanes = c->gap_tail_lanes;
+        G.tail_iters = c->gap_tail_iters;
       }
       if (c->verbose || c->diag) {
         if (int rc = c->d_iters.ensure(std::max<int64_t>(n, 1) * 4)) return rc;

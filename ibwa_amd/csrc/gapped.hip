@@ -591,7 +591,11 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     // search lanes pop C; exact lanes advance one symbol
     bool do_pop = false, finish = false, do_mat = false, dump_now = false;
     const bool over_budget = A.max_iters && n_iter > A.max_iters;
-    if ((over_budget || (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries) ||
+    // the launch's tail: no read left to claim and few lanes of this wave still busy -- their reads
+    // leave their states for the cooperative pass instead of holding the wave (and the launch) open
+    const bool tail = LW && A.rdump && A.tail_lanes && !more && (uint32_t)__popcll(__ballot(st != 0)) <= A.tail_lanes &&
+                      n_iter > A.tail_iters;
+    if ((over_budget || tail || (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries) ||
          (A.early2_iters && n_iter > A.early2_iters && n_entries > (int)A.early2_entries)) &&
         (st == 1 || st == 2)) {
       if (LW && A.rdump && !over_budget && st == 1) {

@@ -126,6 +126,9 @@ def test_exact_reads_round_trip(mid_genome):
     ([], 100, 0.02, 20_000, {"gap_resume_iters": 100, "gap_resume_entries": 50, "gap_cap1": 256,
                              "gap_pages_per_block": 8}),
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_resume_records": 20_000}),
+    # every read past 5 iterations in the launch's tail (here: from the start) leaves its state
+    ([], 100, 0.01, 30_000, {"gap_tail_lanes": 64, "gap_tail_iters": 5}),
+    (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_tail_lanes": 64, "gap_tail_iters": 1}),
     # a 1 GiB page pool: resumed reads that run out of pages start over in the later passes
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "coop_pool_gb": 1}),
     ([], 100, 0.01, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4, "gap_resume": 0})])
@@ -136,7 +139,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
-                "gap_resume_entries": 300, "coop_pool_gb": 16}
+                "gap_resume_entries": 300, "coop_pool_gb": 16, "gap_tail_lanes": 16, "gap_tail_iters": 200}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
@@ -147,7 +150,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
             eng.set_option(k, defaults[k])
     if "-m" in argv:
         assert st.n_heavy > 0 and st.n_coop == st.n_heavy  # nothing handed on to the sequential kernel
-    if "gap_resume_iters" in tune and tune.get("gap_resume", 1):
+    if ("gap_resume_iters" in tune or "gap_tail_lanes" in tune) and tune.get("gap_resume", 1):
         assert st.n_resumed > 0  # the resume path ran
         if "gap_resume_records" in tune:
             assert st.resume_records > tune["gap_resume_records"]  # ... and some states did not fit
