@@ -156,6 +156,8 @@ struct ibwa_ctx {
   // resume in a launch's tail (GapArgs::tail_lanes): 16 / 200 measured 5868 vs 5884 ms per 50M-read
   // step (profiles/r03_tail_sweep.log; 8, 32, 4 / 500 in between)
   uint32_t gap_tail_lanes = 16, gap_tail_iters = 200;
+  int gap_resume_ppb = 96;           // first-pass pages per 256-lane pool when states are left (<= gap_pages_per_block)
+  uint32_t gap_resume_cap1 = 4096;   // first-pass static slots per lane when states are left (<= gap_cap1)
   DBuf d_cw, d_ptabg;
   DBuf d_rdump, d_roff;  // resume states (GapArgs::rdump) and per-read offsets
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
@@ -387,6 +389,8 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_resume_entries" && value >= 0) c->gap_resume_entries = (uint32_t)value;
   else if (k == "gap_tail_lanes" && value >= 0 && value <= 64) c->gap_tail_lanes = (uint32_t)value;
   else if (k == "gap_tail_iters" && value >= 0) c->gap_tail_iters = (uint32_t)value;
+  else if (k == "gap_resume_ppb" && value >= 1 && value <= 65536) c->gap_resume_ppb = (int)value;
+  else if (k == "gap_resume_cap1" && value >= 16 && value <= 65536) c->gap_resume_cap1 = (uint32_t)value;
   else if (k == "coop_order" && (value == 0 || value == 1)) c->coop_order = (int)value;
   else if (k == "coop_roots" && (value == 0 || value == 1)) c->coop_roots = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
@@ -950,8 +954,14 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       HIPCHK(hipMemsetAsync(c->d_roff.p, 0, ((uint64_t)n + 2) * 8, c->stream));
       resume_states = true;
     }
-    if (int rc = c->d_ent.ensure(lanes * P0 * 16)) return rc;
-    if (int rc = c->d_pool.ensure((uint64_t)blocks * ppb * (16ull << LG))) return rc;
+    // and smaller static slot regions (4096: 5859 -> 5840 ms per 50M-read step, hits identical,
+    // profiles/r03_pool_cap_sweep.log; the page table and max_pages are the same for both sizes)
+    const uint32_t P0r = resume ? std::min<uint32_t>(P0, c->gap_resume_cap1) : P0;
+    if (int rc = c->d_ent.ensure(lanes * P0r * 16)) return rc;
+    // with resume states a read leaves the first pass by 2 000 iterations, so few stacks outgrow the
+    // static slots: a smaller page pool (same time at 50M reads, profiles/r03_pool_chunk_sweep.log)
+    const int ppb_run = resume ? std::min(ppb, std::max(1, c->gap_resume_ppb * block / 256)) : ppb;
+    if (int rc = c->d_pool.ensure((uint64_t)blocks * ppb_run * (16ull << LG))) return rc;
     if (int rc = c->d_aln.ensure(aln_total * 16)) return rc;
     if (int rc = c->d_aoff.ensure(std::max<int64_t>(n, 1) * 8)) return rc;
     if (int rc = c->d_naln.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
@@ -1099,12 +1109,12 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         G.ptab_g = c->d_ptabg.as<uint16_t>();
       }
       G.ent = c->d_ent.as<uint4>();
-      G.cap1 = P0;
-      G.hit_slots = std::min<uint32_t>(c->gap_hit_slots, P0 / 2);
+      G.cap1 = P0r;
+      G.hit_slots = std::min<uint32_t>(c->gap_hit_slots, P0r / 2);
       G.pool = c->d_pool.as<uint4>();
       G.page_log2 = LG;
       G.max_pages = max_pages;
-      G.pages_per_block = ppb;
+      G.pages_per_block = ppb_run;
       G.aln = c->d_aln.as<uint4>();
       G.aln_total = aln_total;
       c->stream_total = aln_total;

@@ -172,6 +172,8 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *                                  which resumes it instead of starting over; state buffer size
  *                                  ("gap_resume_records": the buffer in 16 B records, for tests)
  *   "gap_resume_iters", "gap_resume_entries" (2000, 300)  the early hand-off rule when states are left
+ *   "gap_resume_ppb" (96), "gap_resume_cap1" (4096)  first-pass pool pages per 256 lanes and static
+ *                                  slots per lane when states are left (at most the values above)
  *   "gap_tail_lanes", "gap_tail_iters" (16, 200)  also leave a state when no read is left to claim and
  *                                  at most that many lanes of the wave are busy (0: off)
  *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
