@@ -25,7 +25,8 @@ from ibwa_amd import engine as E  # noqa: E402
 DEFAULTS = {"gap_early_iters": 3000, "gap_early_entries": 1000, "gap_iter_budget": 8000,
             "gap_early2_iters": 0, "gap_early2_entries": 0, "gap_resume": 1, "gap_resume_gb": 48,
             "coop_roots": 1, "gap_reads_per_chunk": 16 << 20,
-            "gap_resume_iters": 2000, "gap_resume_entries": 300, "gap_tail_lanes": 16, "gap_tail_iters": 200}
+            "gap_resume_iters": 2000, "gap_resume_entries": 300, "gap_tail_lanes": 16, "gap_tail_iters": 200,
+            "gap_pages_per_block": 384, "gap_cap1": 8192}
 
 
 def main():
