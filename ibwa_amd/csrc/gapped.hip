@@ -35,7 +35,9 @@
 // use track the live entries (the reference's stack size).  At read end the
 // hits are appended to a compact per-batch stream (one atomic per read).  A
 // read that needs more (or options that do not fit the bit fields) is re-run,
-// exactly, by the retry pass.
+// exactly, by the retry pass -- or, past the early hand-off rule in the
+// LDS-width variant, leaves its search state (dump_states: live stack, hits,
+// best score) for the cooperative pass to continue from (coop.hip resume_state).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
