@@ -172,9 +172,12 @@ def cpu_and_parity(eng, eopt, seq, off, lns, n_aln, alns, budget_s, check, heavy
     dt = time.perf_counter() - t
     n_s = int(min(n, max(check, n_cal * budget_s / max(dt, 1e-3))))
     wtch = np.zeros(n_s, dtype=np.uint32)
+    # where each resumed read left the first pass (pops made, from the GPU) -> its touches up to there
+    hpop = np.ascontiguousarray(eng.handoff_pops()[:n_s])
+    stch = np.zeros(n_s, dtype=np.uint32)
     t = time.perf_counter()
     rn, ra, tch = oracle.cal_sa_reg_gap(b0, b1, seq, off[:n_s], lns[:n_s], opt, n_threads=threads, touches=True,
-                                        width_touches=wtch)
+                                        width_touches=wtch, split_pops=hpop, split_touches=stch)
     dt = time.perf_counter() - t
     p = int(rn.sum())
     ok_first = bool((n_aln[:n_s] == rn).all() and alns[:p].tobytes() == ra.tobytes())
@@ -218,11 +221,12 @@ def cpu_and_parity(eng, eopt, seq, off, lns, n_aln, alns, budget_s, check, heavy
               "handed_on_mismatches": bad[:20], "handed_on_ok": not bad,
               "heavy_check_s": time.perf_counter() - t0}
     parity["ok"] = ok_first and not bad and n_s + sum(checked.values()) >= 200_000
-    # which of the sampled first reads the cooperative pass resolved (for the per-kernel roofline)
-    coop_first = np.zeros(n_s, dtype=bool)
-    cid = ids[np.isin(ps, (1, 4)) & (ids < n_s)]
-    coop_first[cid] = True
-    return cpu, (tch, wtch, coop_first), parity
+    # which pass resolved each sampled first read (0: the first pass; retry_info's 1-4), for the
+    # per-kernel roofline, and the touches of a resumed read (pass 4) before its hand-off
+    pass_first = np.zeros(n_s, dtype=np.uint8)
+    sel_ = ids < n_s
+    pass_first[ids[sel_]] = ps[sel_]
+    return cpu, (tch, wtch, pass_first, stch, hpop), parity
 
 
 REF = os.path.join(ROOT, "oracle", "_ref", "ibwa_ref")
@@ -430,11 +434,19 @@ def sw_leg(eng, refs, reads, do_cpu, steps=3):
     out["unit"] = "alignments/s"
     # the VALU work per alignment measured by SQ_INSTS_VALU on this workload shape (the latest
     # profiles/*_sw_pmc.json, tools/r03_sw_pmc.sh) over the live kernel time: whole k_sw
+    # Only a counter file of this build (its build_id) and of this workload shape counts; otherwise the
+    # forward-pass estimate below stands in.
     import glob
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sw_pmc.json")), reverse=True)
-    if pmc:
-        with open(pmc[0]) as f:
-            sp = json.load(f)
+    from ibwa_amd import engine as E
+    bid = E.lib().ibwa_build_id().decode()
+    pmc, sp = [], None
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sw_pmc.json")), reverse=True):
+        with open(fn) as f:
+            d = json.load(f)
+        if d.get("build_id") == bid and d.get("window") == 510 and d.get("read_len") == 150:
+            pmc, sp = [fn], d
+            break
+    if sp is not None:
         ach = sp["valu_wave_insts_per_alignment"] * 64 * n / (out["full_kernel_ms"] * 1e-3)
         out["roofline"] = {"bound": "valu", "kernel": "k_sw (whole kernel)", "achieved": ach / 1e12,
                            "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T lane-ops/s", "frac": ach / VALU_PEAK_LANE_OPS,
@@ -621,7 +633,7 @@ def main():
         k_ms = (ms_w + ms_s + ms_r) / launches
         if do_cpu:
             tc = time.perf_counter()
-            cpu, (tch, wtch, coop_first), parity = cpu_and_parity(eng, opt, seq, off, lns, n_aln, alns, args.cpu_budget,
+            cpu, (tch, wtch, pass_first, stch, hpop), parity = cpu_and_parity(eng, opt, seq, off, lns, n_aln, alns, args.cpu_budget,
                                                                   args.check, args.heavy_budget, threads)
             log(f"CPU baseline + parity {time.perf_counter()-tc:.1f} s: {cpu['value']:.0f} reads/s, parity {parity}")
             result["cpu_baseline"] = cpu
@@ -635,6 +647,9 @@ def main():
                         extra["cpu_port"] = cpu
                         result["cpu_baseline"] = ref
                         extra["parity"]["reference_sample_ok"] = ref["sai_equals_gpu"]
+                        # the reference binary's .sai on the same reads is part of the parity verdict
+                        extra["parity"]["ok"] = bool(extra["parity"]["ok"] and ref["sai_equals_gpu"])
+                        extra["parity_sample_ok"] = extra["parity"]["ok"]
                 except Exception as e:  # the headline line is printed regardless
                     extra["cpu_reference_error"] = repr(e)[:500]
                 log(f"reference CPU baseline {time.perf_counter()-tr_:.1f} s: {result['cpu_baseline']}")
@@ -642,22 +657,29 @@ def main():
             touches = float(tch.mean())
             # algorithmic bytes: 64 B per Occ-interval touch of the reference algorithm, counted by
             # the CPU restatement on the sampled first reads and split per kernel -- bwt_cal_width's touches
-            # (k_width), bwt_match_gap's of the reads the first pass resolves (k_gapped) and of the heavy reads
-            # (k_coop with its level-0 prologue k_coop_roots; it re-runs them from the start, so the first
-            # pass's partial work on them and their second k_width are not algorithmic bytes)
+            # (k_width); bwt_match_gap's of the reads the first pass resolves (k_gapped); of a read that left
+            # its resume state after p pops (ibwa_batch_diag 2), the touches before pop p + 1 (k_gapped) and
+            # the rest (k_coop); of a read the cooperative pass re-ran from the start, all of them (k_coop
+            # with its level-0 prologue k_coop_roots: the first pass's partial work on it and its second
+            # k_width are not algorithmic bytes)
             ns_ = tch.size
             scale = args.reads / ns_
             mg = tch.astype(np.float64) - wtch
+            resumed = pass_first == 4
+            scratch = pass_first == 1
+            first = pass_first == 0
+            g_t = float(mg[first].sum() + (stch[resumed].astype(np.float64) - wtch[resumed]).sum())
+            c_t = float(mg[scratch].sum() + (tch[resumed].astype(np.float64) - stch[resumed]).sum())
             per_k = {"k_width": (float(wtch.sum()) * scale, ms_w / launches, ["k_width"]),
-                     "k_gapped": (float(mg[~coop_first].sum()) * scale, ms_s / launches, ["k_gapped"]),
-                     "k_coop": (float(mg[coop_first].sum()) * scale, (ms_c - ms_cw) / launches,
-                                ["k_coop", "k_coop_roots"])}
-            if int(stl.n_resumed) > 0:
-                # a resumed heavy read's search is split between the two kernels at its hand-off (the
-                # first pass's part is not re-run), so bwt_match_gap's touches price them together
-                per_k = {"k_width": per_k["k_width"],
-                         "k_gapped+k_coop": (float(mg.sum()) * scale, (ms_s + ms_c - ms_cw) / launches,
-                                             ["k_gapped", "k_coop"])}
+                     "k_gapped": (g_t * scale, ms_s / launches, ["k_gapped"]),
+                     "k_coop": (c_t * scale, (ms_c - ms_cw) / launches, ["k_coop", "k_coop_roots"])}
+            extra["touch_split"] = {"sample_reads": int(ns_), "resumed": int(resumed.sum()),
+                                    "coop_from_start": int(scratch.sum()),
+                                    "wide_or_general": int(((pass_first == 2) | (pass_first == 3)).sum()),
+                                    "resumed_pops_mean": float(hpop[resumed].mean()) if resumed.any() else None,
+                                    "resumed_touches_first_pass": float((stch[resumed].astype(np.float64) - wtch[resumed]).sum()),
+                                    "resumed_touches_coop": float((tch[resumed].astype(np.float64) - stch[resumed]).sum()),
+                                    "unsplit_resumed": int((resumed & (hpop == 0)).sum())}
             pk = {}
             for name, (tt, ms, kn) in per_k.items():
                 ab = tt * 64.0
@@ -686,8 +708,10 @@ def main():
                                            "kernel_ms": k_ms, "touches_per_read": touches,
                                            "traffic": pmc[0] if pmc else None,
                                            "traffic_source": pmc[1] if pmc else None},
-                                  "touches_sample": f"first {ns_} reads ({int(coop_first.sum())} of them resolved by the "
-                                                    f"cooperative pass), oracle/ibwa_oracle.c touch counter"}
+                                  "touches_sample": f"first {ns_} reads ({int(resumed.sum())} of them resumed and "
+                                                    f"{int(scratch.sum())} re-run by the cooperative pass), "
+                                                    f"oracle/ibwa_oracle.c touch counter split at each resumed "
+                                                    f"read's hand-off pop"}
         # the extra legs cannot cost the headline line: a failure is recorded as extra.<leg>.error
         def leg(name, fn):
             t_ = time.perf_counter()

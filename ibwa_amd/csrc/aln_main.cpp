@@ -25,13 +25,16 @@
 #include <vector>
 
 #include "ibwa_aln.h"
+#include "ingest.h"
 #include "readers.h"
 #include "sam_common.h"
 
 namespace {
 
 using ibwa_cli::BamReader;
+using ibwa_cli::DevGroup;
 using ibwa_cli::FastqBulk;
+using ibwa_cli::FastqGpu;
 using ibwa_cli::SeqReader;
 
 const int kBatch = 0x40000;  // bwtaln.c:193
@@ -67,6 +70,16 @@ struct Batch {
   int max_len = 0;
   std::vector<std::pair<long, long>> trims;  // per 0x40000-read batch: bases trimmed, bases read
   int64_t n() const { return (int64_t)len.size(); }
+};
+
+// A GPU run's reads: host-parsed (b) or parsed on the GPUs, staged device to device (dg)
+struct Group {
+  Batch b;
+  DevGroup dg;
+  bool dev = false;
+  int64_t n() const { return dev ? dg.n : b.n(); }
+  int max_len() const { return dev ? dg.max_len : b.max_len; }
+  const std::vector<std::pair<long, long>> &trims() const { return dev ? dg.trims : b.trims; }
 };
 
 // bwa_read_seq (bwaseqio.c:145-208) for FASTQ/FASTA input, bwa_read_bam (:89-143) for BAM: one
@@ -270,7 +283,7 @@ int die(const char *what) {
 
 template <class Reader>
 int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out,
-            int n_gpus);
+            int n_gpus, const char *fq_dev);
 
 int samse_main(int argc, char *argv[]);  // samse_main.cpp
 int sampe_main(int argc, char *argv[]);  // sampe_main.cpp
@@ -322,21 +335,25 @@ int main(int argc, char *argv[]) {
       fprintf(stderr, "[ibwa-amd aln] cannot open %s as BAM\n", argv[first_arg + 1]);
       return 1;
     }
-    return run_aln(rd, nullptr, opt, prefix, fn_out, n_gpus);
+    return run_aln(rd, nullptr, opt, prefix, fn_out, n_gpus, nullptr);
   }
   SeqReader rd;
   if (!rd.open(argv[first_arg + 1])) {
     fprintf(stderr, "[ibwa-amd aln] cannot open %s\n", argv[first_arg + 1]);
     return 1;
   }
-  // IBWA_ALN_SERIAL_READ=1: the serial reader only (tests compare the two)
+  // IBWA_ALN_SERIAL_READ=1: the serial reader only (tests compare the two); an uncompressed FASTQ
+  // file is parsed on the GPUs (ingest.h) unless IBWA_ALN_GPU_PARSE=0
   FastqBulk fb(rd);
-  return run_aln(rd, env_int("IBWA_ALN_SERIAL_READ", 0) ? nullptr : &fb, opt, prefix, fn_out, n_gpus);
+  const bool serial = env_int("IBWA_ALN_SERIAL_READ", 0) != 0;
+  const char *gp = getenv("IBWA_ALN_GPU_PARSE");
+  const bool dev_parse = !serial && !(gp && atoi(gp) == 0) && FastqGpu::usable(argv[first_arg + 1]);
+  return run_aln(rd, serial ? nullptr : &fb, opt, prefix, fn_out, n_gpus, dev_parse ? argv[first_arg + 1] : nullptr);
 }
 
 template <class Reader>
 int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out,
-            int n_gpus) {
+            int n_gpus, const char *fq_dev) {
   FILE *out = fn_out ? fopen(fn_out, "wb") : stdout;
   if (!out) {
     fprintf(stderr, "[ibwa-amd aln] cannot write %s\n", fn_out);
@@ -344,9 +361,42 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   }
   if (n_gpus < 1) n_gpus = 1;
   ibwa_sam::Phases ph;
+  // GPU slice g runs on device g mod (visible devices): more slices than devices rehearse the
+  // multi-GPU path on fewer GPUs (index replication, the slice split, the ordered writer)
+  int n_dev = 0;
+  if (ibwa_device_count(&n_dev) || n_dev < 1) return die("no HIP device");
+  if (n_gpus > n_dev)
+    fprintf(stderr, "[ibwa-amd aln] -G %d on %d visible device(s): slice g runs on device g mod %d\n", n_gpus, n_dev, n_dev);
+  // FASTQ parsed on the GPUs: one ingest context per GPU (its own stream and buffers); the first
+  // region is read from the file while the index loads
+  std::vector<ibwa_ctx_t *> ing;
+  std::unique_ptr<FastqGpu> fg;
+  struct Destroy {
+    std::vector<ibwa_ctx_t *> &v;
+    std::unique_ptr<FastqGpu> &f;
+    ~Destroy() {
+      f.reset();
+      for (auto *x : v) ibwa_ctx_destroy(x);
+    }
+  } destroy_ing{ing, fg};
+  if (fq_dev) {
+    for (int g = 0; g < n_gpus; ++g) {
+      ibwa_ctx_t *x = nullptr;
+      if (ibwa_ctx_create(g % n_dev, &x)) return die("ibwa_ctx_create (ingest)");
+      ing.push_back(x);
+    }
+    const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
+    const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)1 << 30;
+    const uint64_t carry = cm && atoll(cm) > 0 ? (uint64_t)atoll(cm) : (uint64_t)256 << 20;
+    fg.reset(new FastqGpu(fq_dev, ing, opt.mode, opt.trim_qual, kSub, piece, carry));
+    if (!fg->ok()) {
+      fprintf(stderr, "[ibwa-amd aln] cannot read %s for the device parse\n", fq_dev);
+      return 1;
+    }
+  }
   std::vector<ibwa_ctx_t *> ctx(n_gpus, nullptr);
   for (int g = 0; g < n_gpus; ++g) {
-    if (ibwa_ctx_create(g, &ctx[g])) return die("ibwa_ctx_create");
+    if (ibwa_ctx_create(g % n_dev, &ctx[g])) return die("ibwa_ctx_create");
     if (g == 0) {
       if (ibwa_ctx_load_bwt_file(ctx[0], 0, (prefix + ".bwt").c_str())) return die("load .bwt");
       if (ibwa_ctx_load_bwt_file(ctx[0], 1, (prefix + ".rbwt").c_str())) return die("load .rbwt");
@@ -361,13 +411,33 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   std::vector<int> prep_rc(n_gpus, 0);
   std::vector<std::thread> prep;
   for (int g = 0; g < n_gpus; ++g) prep.emplace_back([&, g]() { prep_rc[g] = ibwa_ctx_prepare(ctx[g], &opt); });
-  Batch cur, nxt, sub, carry;
+  Group cur;
+  Batch sub, carry;
   bool has_carry = false;
   bool eof = false;
-  double parse_s = 0;  // wall time of the FASTQ parse (all host threads)
-  auto timed_read = [&](Batch &into) {
+  double parse_s = 0;  // wall time of the FASTQ parse (all host threads, or waiting for the GPUs')
+  bool dev_active = fg != nullptr;
+  auto key_of = [&](int max_len) { return batch_key(opt, max_len); };
+  auto timed_read = [&](Group &into) {
     const auto t = std::chrono::steady_clock::now();
-    const int r = read_group(rd, fb, opt, into, sub, carry, has_carry, &eof);
+    int r = 0;
+    into.dev = false;
+    if (dev_active) {
+      if (fg->next(into.dg, key_of)) {
+        into.dev = true;
+        r = 1;
+      } else {
+        dev_active = false;
+        if (fg->handoff()) {  // the host readers from the first batch the device path did not take
+          fprintf(stderr, "[ibwa-amd aln] the host readers take over at byte %llu\n",
+                  (unsigned long long)fg->handoff_offset());
+          if (gzseek(rd.fp, (z_off_t)fg->handoff_offset(), SEEK_SET) < 0) r = -1;
+        } else {
+          eof = true;
+        }
+      }
+    }
+    if (!into.dev && r == 0) r = read_group(rd, fb, opt, into.b, sub, carry, has_carry, &eof);
     parse_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
     return r;
   };
@@ -394,11 +464,11 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   for (int l = 1; l < n_lanes; ++l)
     for (int g = 0; g < n_gpus; ++g) {
       ibwa_ctx_t *x = nullptr;
-      if (ibwa_ctx_create(g, &x) || ibwa_ctx_share_index(x, ctx[g])) return die("a second context on the GPU");
+      if (ibwa_ctx_create(g % n_dev, &x) || ibwa_ctx_share_index(x, ctx[g])) return die("a second context on the GPU");
       lctx[l].push_back(x);
     }
   struct Job {
-    Batch b;
+    Group b;
     std::vector<std::vector<int32_t>> naln;
     std::vector<ibwa_aln1_t *> aln;
     std::vector<int> rc;
@@ -424,22 +494,36 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     J.t0 = std::chrono::steady_clock::now();
     J.active = true;
     const int64_t per = (n + n_gpus - 1) / n_gpus;
+    // a group parsed on the GPUs is staged here, device to device, before the next region's parse
+    // reuses the ingest buffers; its slices are the group's reads in each GPU's piece
+    std::vector<double> stage_ms(n_gpus, 0.0);
+    if (J.b.dev)
+      for (int g = 0; g < n_gpus; ++g) {
+        const auto s0 = std::chrono::steady_clock::now();
+        J.rc[g] = ibwa_batch_stage_fq(cx[g], ing[g], J.b.dg.first[g], J.b.dg.count[g], J.b.dg.max_len);
+        stage_ms[g] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s0).count();
+      }
     for (int g = 0; g < n_gpus; ++g) {
-      J.th.emplace_back([&J, &cx, &opt, g, n, per]() {
-        const Batch &cur = J.b;
+      J.th.emplace_back([&J, &cx, &opt, g, n, per, sms = stage_ms[g]]() {
+        const Group &cur = J.b;
         int64_t b = std::min<int64_t>(n, g * per), e = std::min<int64_t>(n, b + per);
+        if (cur.dev) b = 0, e = cur.dg.count[g];
         J.naln[g].resize(e - b);
         int64_t tot = 0;
-        // each slice is staged from its own bytes only: offsets rebased to the slice's first read
-        // (reads are contiguous in input order); the batch-level max length still applies
-        const uint64_t base = b < e ? cur.off[b] : 0;
-        std::vector<uint64_t> off(cur.off.begin() + b, cur.off.begin() + e);
-        for (auto &x : off) x -= base;
-        // ibwa_aln_batch, in its three steps (IBWA_ALN_TIMES=1: their wall times per slice)
         auto c0 = std::chrono::steady_clock::now();
-        int rc = ibwa_batch_stage(cx[g], e - b, cur.seq.data() + base, off.data(), cur.len.data() + b);
+        int rc = J.rc[g];
+        if (!cur.dev) {
+          // each slice is staged from its own bytes only: offsets rebased to the slice's first read
+          // (reads are contiguous in input order); the batch-level max length still applies
+          const Batch &hb = cur.b;
+          const uint64_t base = b < e ? hb.off[b] : 0;
+          std::vector<uint64_t> off(hb.off.begin() + b, hb.off.begin() + e);
+          for (auto &x : off) x -= base;
+          // ibwa_aln_batch, in its three steps (IBWA_ALN_TIMES=1: their wall times per slice)
+          rc = ibwa_batch_stage(cx[g], e - b, hb.seq.data() + base, off.data(), hb.len.data() + b);
+        }
         auto c1 = std::chrono::steady_clock::now();
-        if (!rc) rc = ibwa_batch_run(cx[g], &opt, cur.max_len);
+        if (!rc) rc = ibwa_batch_run(cx[g], &opt, cur.max_len());
         auto c2 = std::chrono::steady_clock::now();
         if (!rc) rc = ibwa_batch_fetch(cx[g], J.naln[g].data(), &J.aln[g], &tot);
         auto c3 = std::chrono::steady_clock::now();
@@ -449,7 +533,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
             return std::chrono::duration<double, std::milli>(y - x).count();
           };
           fprintf(stderr, "[ibwa-amd aln] slice %d: %lld reads, stage %.1f run %.1f fetch %.1f ms\n", g,
-                  (long long)(e - b), ms(c0, c1), ms(c1, c2), ms(c2, c3));
+                  (long long)(e - b), ms(c0, c1) + sms, ms(c1, c2), ms(c2, c3));
         }
       });
     }
@@ -499,7 +583,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     if (J.active)  // the oldest group in flight
       if (int rc = finish(J)) return rc;
     if (opt.trim_qual >= 1)  // once per 0x40000-read batch, as bwa_read_seq (bwaseqio.c:206)
-      for (const auto &t : cur.trims)
+      for (const auto &t : cur.trims())
         if (t.second) fprintf(stderr, "[bwa_read_seq] %.1f%% bases are trimmed.\n", 100.0f * t.first / t.second);
     std::swap(J.b, cur);
     launch(J, lctx[k % n_lanes]);
@@ -521,6 +605,11 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   for (auto *x : ctx) ibwa_ctx_destroy(x);
   if (have < 0) return 1;
   ph.print("ibwa-amd aln");
+  if (fg) {
+    fprintf(stderr, "[ibwa-amd aln] input parsed on the GPUs: %lld records, %.2f s waiting for the parse (%.0f ms of device "
+                    "time: H2D copies + kernels)%s\n",
+            (long long)fg->records(), fg->parse_s(), fg->dev_ms(), fg->handoff() ? "; the host readers took the rest" : "");
+  }
   if (parse_s > 0) {
     const int nt = fb ? ibwa_sam::host_threads() : 1;
     fprintf(stderr, "[ibwa-amd aln] input parse: %lld reads in %.2f s on %d host threads = %.2f M reads/s (%.3f M per thread)\n",

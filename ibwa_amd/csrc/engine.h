@@ -109,11 +109,12 @@ struct GapArgs {
   unsigned long long *rd_next;
   unsigned long long rd_cap;
   uint64_t *roff;
+  uint32_t *hpop;            // optional: per read, the pops (bwtgap.c:129) made before its state was left
   uint32_t tail_lanes;       // resume also when no read is left to claim and <= tail_lanes of the wave
   uint32_t tail_iters;       //   are busy, for a read past tail_iters iterations (0: off)
   AlnOpt o;
 };
-constexpr int RD_HDR = 2;  // resume state header: {entries, hits, lowest score, stack size}, {best_score, best_cnt, max_diff, 0}
+constexpr int RD_HDR = 2;  // resume state header: {entries, hits, lowest score, stack size}, {best_score, best_cnt, max_diff, pops}
 constexpr int GAP_RING = 16;      // bucket heads of the LDS-width variant: live scores span <= 16
 constexpr int GAP_MAX_PAGES = 8;  // page-table entries per lane (global table)
 size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int pages_per_block, int lanes_per_wave,
@@ -284,5 +285,33 @@ hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_
                         hipStream_t st);
 hipError_t pack_text2(const uint8_t *T, uint64_t n, uint32_t *out, uint64_t out_words, hipStream_t st);
 hipError_t reverse_text(uint8_t *T, uint64_t n, hipStream_t st);
+
+// FASTQ ingest on the device (fastq.hip): strict 4-line records of a raw block -> kept reads
+constexpr int FQ_MIN_RDLEN = 35;  // BWA_MIN_RDLEN (bwtaln.h:23): bwa_trim_read keeps at least this
+struct FqOpt {
+  int l_bc;       // -B barcode length (mode >> 24)
+  int trim_qual;  // -q
+  int is_64;      // -I: qualities - 31 before trimming
+};
+struct FqBufs {
+  const uint8_t *raw;   // the block, fq_padded_bytes(n) bytes, zero past n
+  uint32_t *tile_cnt, *tile_base;
+  uint32_t *nl;         // newline positions, cap_lines entries
+  uint32_t cap_lines;
+  uint32_t *n_lines;    // lines found (at most cap_lines)
+  uint32_t *bad;        // first record that is not strict (0xFFFFFFFF: none)
+  int32_t *rec_len;     // per record (cap_lines / 4 + 1): kept length, -1 skipped or not strict
+  uint32_t *rec_L;      // per record: sequence line length (0: not strict)
+  uint64_t *rec_key;    // per record: kept rank << 40 | code offset (exclusive scan)
+  uint8_t *codes;       // kept reads' reversed nt4 codes, concatenated
+  uint64_t *offk;       // per kept read: code offset
+  uint32_t *lenk;       // per kept read: length
+};
+uint64_t fq_padded_bytes(uint64_t n);
+// tmp == nullptr: *tmp_bytes = the scans' scratch size
+hipError_t fq_parse_launch(const FqBufs &b, uint64_t n, const FqOpt &o, void *tmp, size_t *tmp_bytes, hipStream_t st);
+// kept reads [first, first + n) of a parsed block as a batch: offsets from the first one's codes
+hipError_t fq_rebase(const uint64_t *offk, const uint32_t *lenk, int64_t first, int64_t n, uint64_t *off, uint32_t *len,
+                     hipStream_t st);
 
 }  // namespace ibwa

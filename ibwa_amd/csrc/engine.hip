@@ -160,6 +160,8 @@ struct ibwa_ctx {
   uint32_t gap_resume_cap1 = 4096;   // first-pass static slots per lane when states are left (<= gap_cap1)
   DBuf d_cw, d_ptabg;
   DBuf d_rdump, d_roff;  // resume states (GapArgs::rdump) and per-read offsets
+  DBuf d_hpop;           // per read: first-pass pops before its resume state (0: none; ibwa_batch_diag 2)
+  bool hpop_valid = false;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
   int coop_pool_gb = 16;             // bucket page pool
   DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb, c_proot, c_pstore;
@@ -185,12 +187,28 @@ struct ibwa_ctx {
   bool kmer_valid = false;
   ibwa_run_stats_t stats = {};
   DBuf sw[15];  // sw_batch's buffers (kept between calls)
+  // ibwa_ctx_share_index: the context whose index structures this one borrows, and how many
+  // contexts borrow this one's; neither side may rebuild or replace them while shared
+  ibwa_ctx *share_src = nullptr;
+  int n_borrowers = 0;
+  // FASTQ ingest (fastq.hip, ibwa_fq_parse): the last parsed block and its kept reads
+  DBuf fq_raw, fq_tile, fq_nl, fq_cnt, fq_len, fq_L, fq_key, fq_codes, fq_offk, fq_lenk, fq_tmp;
+  int64_t fq_kept = 0;
+  double fq_ms = 0;  // device time of the last parse (H2D copy + kernels), HIP events
 };
 
 namespace {
+// An operation that would rebuild or replace index structures shared by ibwa_ctx_share_index
+// (borrowed buffers are written in place or cannot grow, and the other context may be aligning).
+int refuse_shared(const ibwa_ctx *c, const char *what) {
+  if (c->share_src) return fail(IBWA_EINVAL, "%s: this context shares another context's index", what);
+  if (c->n_borrowers) return fail(IBWA_EINVAL, "%s: %d other context(s) share this context's index", what, c->n_borrowers);
+  return 0;
+}
 // (Re)build the K-mer tables for the resident index if needed.
 int ensure_kmer(ibwa_ctx *c) {
   if (c->kmer_valid) return 0;
+  if (int rc = refuse_shared(c, "K-mer tables")) return rc;
   int K = c->kmer_k;
   if (K < 0) {
     // auto: K ~ log4(2n) (past that most K-mers are absent), up to 15 (2 x 8.6 GB for a
@@ -232,6 +250,7 @@ int ensure_kmer(ibwa_ctx *c) {
 // (a scatter) and the text (a gather through the ISA).  Skipped when HBM is short: the exact path
 // then runs without the jump (same results).
 int derive_sa_locked(ibwa_ctx *c, uint32_t intv) {
+  if (c->share_src) return fail(IBWA_EINVAL, "sampled SA: this context shares another context's index");
   HIPCHK(hipSetDevice(c->device));
   for (int s = 0; s < 2; ++s) {
     const uint64_t n_nodes = ((uint64_t)c->ix[s].seq_len + intv) / intv;
@@ -251,6 +270,9 @@ int derive_sa_locked(ibwa_ctx *c, uint32_t intv) {
 
 int ensure_jump(ibwa_ctx *c) {
   if (c->jump_ready || !c->exact_jump || !c->jump_derive) return 0;
+  // a context sharing another's index runs without the jump unless the source had it when shared
+  // (the same results; the jump only saves rank queries)
+  if (c->share_src) return 0;
   const uint64_t n = c->ix[0].seq_len;
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
@@ -329,6 +351,14 @@ int ibwa_cal_maxdiff(int l, double err, double thres) {  // bwtaln.c:39-51
   return 2;
 }
 
+int ibwa_device_count(int *n) {
+  int d = 0;
+  hipError_t e = hipGetDeviceCount(&d);
+  if (e != hipSuccess) return fail(IBWA_EHIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  if (n) *n = d;
+  return 0;
+}
+
 int ibwa_ctx_create(int device, ibwa_ctx_t **out) {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
@@ -353,6 +383,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->share_src) --c->share_src->n_borrowers;
   for (DBuf *b : {&c->h2p_in, &c->h2p_out, &c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
                   &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
@@ -367,7 +398,12 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
 int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   std::string k = key ? key : "";
   if (k == "exact_path") c->exact_path = value != 0;
-  else if (k == "kmer_k" && value >= -1 && value <= 16) { c->kmer_k = (int)value; c->kmer_valid = false; }
+  else if (k == "kmer_k" && value >= -1 && value <= 16) {
+    if (value != c->kmer_k)
+      if (int rc = refuse_shared(c, "option kmer_k")) return rc;
+    c->kmer_k = (int)value;
+    c->kmer_valid = false;
+  }
   else if (k == "exact_blocks" && value > 0) c->exact_blocks = (int)value;
   else if (k == "lanes_per_chunk" && value > 0) c->lanes_per_chunk = value;
   else if (k == "gapped_v2") c->gapped_v2 = value != 0;
@@ -421,6 +457,7 @@ int ibwa_ctx_set_tuning(ibwa_ctx_t *c, int stack_cap, int aln_cap, int block) {
 int ibwa_ctx_load_bwt(ibwa_ctx_t *c, int strand, uint32_t primary, const uint32_t L2[4], const uint32_t *bwt,
                       uint64_t bwt_size) {
   if (strand < 0 || strand > 1) return fail(IBWA_EINVAL, "strand must be 0 (.bwt) or 1 (.rbwt)");
+  if (int rc = refuse_shared(c, "load_bwt")) return rc;
   HIPCHK(hipSetDevice(c->device));
   const uint32_t seq_len = L2[3];
   const uint64_t n_blocks = ((uint64_t)seq_len + 127) / 128 + 1;
@@ -468,6 +505,7 @@ int ibwa_ctx_load_bwt_file(ibwa_ctx_t *c, int strand, const char *path) {  // bw
 }
 
 int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
+  if (int rc = refuse_shared(dst, "clone_index")) return rc;
   for (int s = 0; s < 2; ++s) {
     if (!src->loaded[s]) return fail(IBWA_ENOINDEX, "source index not loaded");
     HIPCHK(hipSetDevice(dst->device));
@@ -495,6 +533,8 @@ int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   if (dst->device != src->device) return fail(IBWA_EINVAL, "share_index: contexts on devices %d and %d", dst->device, src->device);
   for (int s = 0; s < 2; ++s)
     if (!src->loaded[s]) return fail(IBWA_ENOINDEX, "source index not loaded");
+  if (int rc = refuse_shared(dst, "share_index (destination)")) return rc;
+  if (src->share_src) return fail(IBWA_EINVAL, "share_index: the source shares another context's index; share that one");
   HIPCHK(hipSetDevice(dst->device));
   HIPCHK(hipStreamSynchronize(src->stream));  // src's structures are complete
   for (int s = 0; s < 2; ++s) {
@@ -522,12 +562,15 @@ int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   dst->jump_derive = src->jump_derive;
   dst->exact_jump = src->exact_jump;
   dst->width_jump = src->width_jump;
+  dst->share_src = const_cast<ibwa_ctx *>(src);
+  ++dst->share_src->n_borrowers;
   return 0;
 }
 
 int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa_intv) {
   if (n == 0 || n >= 0xFFFFFFFEull) return fail(IBWA_EINVAL, "text length %llu outside [1, 2^32-2)", (unsigned long long)n);
   if (sa_intv < 0) return fail(IBWA_EINVAL, "sa_intv < 0");
+  if (int rc = refuse_shared(c, "build_index")) return rc;
   HIPCHK(hipSetDevice(c->device));
   DBuf T;
   if (int rc = T.ensure(n)) return rc;
@@ -638,6 +681,7 @@ int ibwa_ctx_export_sa(const ibwa_ctx_t *c, int strand, uint32_t *out, uint64_t 
 int ibwa_ctx_load_sa(ibwa_ctx_t *c, int strand, uint32_t sa_intv, const uint32_t *sa, uint64_t n_sa) {
   if (strand < 0 || strand > 1 || !c->loaded[strand]) return fail(IBWA_ENOINDEX, "index not loaded");
   if (sa_intv == 0) return fail(IBWA_EINVAL, "sa_intv == 0");
+  if (int rc = refuse_shared(c, "load_sa")) return rc;
   const uint64_t n = c->ix[strand].seq_len;
   if (n_sa != (n + sa_intv) / sa_intv)
     return fail(IBWA_EINVAL, "n_sa %llu != (seq_len + intv) / intv", (unsigned long long)n_sa);
@@ -681,6 +725,7 @@ int ibwa_ctx_derive_sa(ibwa_ctx_t *c, uint32_t sa_intv) {
 int ibwa_ctx_expand_sa(ibwa_ctx_t *c) {
   if (!c->sa_loaded[0] || !c->sa_loaded[1]) return fail(IBWA_ENOINDEX, "sampled SA of both strands needed");
   if (c->jump_ready || c->sa_expanded) return 0;  // full SA already resident
+  if (c->share_src) return fail(IBWA_EINVAL, "expand_sa: this context shares another context's index");
   HIPCHK(hipSetDevice(c->device));
   for (int s = 0; s < 2; ++s) {
     if (int rc = c->sa_full[s].ensure(((uint64_t)c->ix[s].seq_len + 1) * 4)) return rc;
@@ -733,6 +778,142 @@ int ibwa_sa2pos(ibwa_ctx_t *c, int64_t n, const uint8_t *strand, const uint32_t 
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->stats.ms_sa2pos = ms;
   c->stats.sa2pos_full = full;
+  return 0;
+}
+
+int ibwa_host_alloc(uint64_t bytes, void **p) {
+  if (!p) return fail(IBWA_EINVAL, "null pointer");
+  hipError_t e = hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(IBWA_EHIP, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+  return 0;
+}
+
+int ibwa_host_free(void *p) {
+  if (p) HIPCHK(hipHostFree(p));
+  return 0;
+}
+
+int ibwa_fq_parse(ibwa_ctx_t *c, const void *raw, uint64_t nbytes, int mode, int trim_qual, int64_t *n_rec,
+                  uint64_t *consumed, int *not_strict, int32_t *rec_len, uint32_t *rec_L, int64_t cap) {
+  if (!c || !raw || !n_rec || !consumed || !not_strict || cap < 0) return fail(IBWA_EINVAL, "fq_parse: bad arguments");
+  if (nbytes >= 0xFFFF0000ull) return fail(IBWA_EINVAL, "fq_parse: a block of %llu bytes (< 4 GiB)", (unsigned long long)nbytes);
+  if (((unsigned)mode >> 24) > 15) return fail(IBWA_EINVAL, "the maximum barcode length is 15");
+  *n_rec = 0;
+  *consumed = 0;
+  *not_strict = 0;
+  c->fq_kept = 0;
+  c->fq_ms = 0;
+  if (nbytes == 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  const uint64_t padded = fq_padded_bytes(nbytes);
+  // a strict line holds >= 2 bytes, and records of real reads far more: past cap_lines the block
+  // simply ends earlier (the caller parses on from *consumed)
+  const uint64_t cap_lines = std::min<uint64_t>(nbytes / 12 + 64, 0xFFFFFF00ull);
+  const uint64_t max_rec = cap_lines / 4 + 1, n_tiles = padded / 16384;
+  if (int rc = c->fq_raw.ensure(padded)) return rc;
+  if (int rc = c->fq_tile.ensure(n_tiles * 8 + 8)) return rc;
+  if (int rc = c->fq_nl.ensure(cap_lines * 4)) return rc;
+  if (int rc = c->fq_cnt.ensure(16)) return rc;
+  if (int rc = c->fq_len.ensure(max_rec * 4)) return rc;
+  if (int rc = c->fq_L.ensure(max_rec * 4)) return rc;
+  if (int rc = c->fq_key.ensure(max_rec * 8)) return rc;
+  if (int rc = c->fq_codes.ensure(nbytes + 16)) return rc;
+  if (int rc = c->fq_offk.ensure(max_rec * 8)) return rc;
+  if (int rc = c->fq_lenk.ensure(max_rec * 4)) return rc;
+  FqBufs B;
+  B.raw = c->fq_raw.as<uint8_t>();
+  B.tile_cnt = c->fq_tile.as<uint32_t>();
+  B.tile_base = B.tile_cnt + n_tiles;
+  B.nl = c->fq_nl.as<uint32_t>();
+  B.cap_lines = (uint32_t)cap_lines;
+  B.n_lines = c->fq_cnt.as<uint32_t>();
+  B.bad = B.n_lines + 1;
+  B.rec_len = c->fq_len.as<int32_t>();
+  B.rec_L = c->fq_L.as<uint32_t>();
+  B.rec_key = c->fq_key.as<uint64_t>();
+  B.codes = c->fq_codes.as<uint8_t>();
+  B.offk = c->fq_offk.as<uint64_t>();
+  B.lenk = c->fq_lenk.as<uint32_t>();
+  const FqOpt o{(int)((unsigned)mode >> 24), trim_qual, (mode & IBWA_MODE_IL13) ? 1 : 0};
+  size_t tb = 0;
+  HIPCHK(fq_parse_launch(B, nbytes, o, nullptr, &tb, c->stream));
+  if (int rc = c->fq_tmp.ensure(tb + 256)) return rc;
+  HIPCHK(hipEventRecord(c->ev[6], c->stream));
+  HIPCHK(hipMemcpyAsync(c->fq_raw.p, raw, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->fq_raw.as<uint8_t>() + nbytes, 0, padded - nbytes, c->stream));
+  HIPCHK(fq_parse_launch(B, nbytes, o, c->fq_tmp.p, &tb, c->stream));
+  HIPCHK(hipEventRecord(c->ev[7], c->stream));
+  uint32_t cnt[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(cnt, c->fq_cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
+  c->fq_ms = ms;
+  const uint64_t complete = cnt[0] / 4;
+  uint64_t n = std::min<uint64_t>(complete, cnt[1]);
+  *not_strict = cnt[1] < complete && n == cnt[1];
+  if (n > (uint64_t)cap) {  // the caller takes at most cap records: the block ends at the last of them
+    n = (uint64_t)cap;
+    *not_strict = 0;
+  }
+  if (n == 0) return 0;
+  uint32_t last_nl = 0;
+  HIPCHK(hipMemcpy(&last_nl, c->fq_nl.as<uint32_t>() + 4 * n - 1, 4, hipMemcpyDeviceToHost));
+  if (rec_len) HIPCHK(hipMemcpy(rec_len, c->fq_len.p, n * 4, hipMemcpyDeviceToHost));
+  if (rec_L) HIPCHK(hipMemcpy(rec_L, c->fq_L.p, n * 4, hipMemcpyDeviceToHost));
+  uint64_t key = 0;
+  int32_t ll = 0;
+  HIPCHK(hipMemcpy(&key, c->fq_key.as<uint64_t>() + n - 1, 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&ll, c->fq_len.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost));
+  c->fq_kept = (int64_t)(key >> 40) + (ll >= 0 ? 1 : 0);
+  *n_rec = (int64_t)n;
+  *consumed = (uint64_t)last_nl + 1;
+  return 0;
+}
+
+int ibwa_fq_offset(const ibwa_ctx_t *c, int64_t r, uint64_t *off) {
+  if (!c || !off || r < 0) return fail(IBWA_EINVAL, "fq_offset: bad arguments");
+  *off = 0;
+  if (r == 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  uint32_t x = 0;
+  HIPCHK(hipMemcpy(&x, c->fq_nl.as<uint32_t>() + 4 * r - 1, 4, hipMemcpyDeviceToHost));
+  *off = (uint64_t)x + 1;
+  return 0;
+}
+
+int ibwa_fq_stats(const ibwa_ctx_t *c, int64_t *kept, double *ms) {
+  if (kept) *kept = c->fq_kept;
+  if (ms) *ms = c->fq_ms;
+  return 0;
+}
+
+int ibwa_batch_stage_fq(ibwa_ctx_t *c, const ibwa_ctx_t *src, int64_t first, int64_t n, int max_len) {
+  if (!c || !src || first < 0 || n < 0 || first + n > src->fq_kept)
+    return fail(IBWA_EINVAL, "stage_fq: reads [%lld, %lld) outside the %lld kept reads of the parsed block",
+                (long long)first, (long long)(first + n), (long long)(src ? src->fq_kept : 0));
+  if (c->device != src->device) return fail(IBWA_EINVAL, "stage_fq: contexts on devices %d and %d", c->device, src->device);
+  if (max_len > 65535) return fail(IBWA_EINVAL, "read length %d > 65535 is not supported", max_len);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(src->stream));  // the block is parsed
+  uint64_t b0 = 0, b1 = 0;
+  uint32_t l1 = 0;
+  if (n) {
+    HIPCHK(hipMemcpy(&b0, src->fq_offk.as<uint64_t>() + first, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&b1, src->fq_offk.as<uint64_t>() + first + n - 1, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&l1, src->fq_lenk.as<uint32_t>() + first + n - 1, 4, hipMemcpyDeviceToHost));
+  }
+  const uint64_t bytes = n ? b1 + l1 - b0 : 0;
+  if (int rc = c->d_seq.ensure(bytes + 16)) return rc;
+  if (int rc = c->d_off.ensure(n * 8 + 8)) return rc;
+  if (int rc = c->d_len.ensure(n * 4 + 4)) return rc;
+  if (bytes) HIPCHK(hipMemcpyAsync(c->d_seq.p, src->fq_codes.as<uint8_t>() + b0, bytes, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(fq_rebase(src->fq_offk.as<uint64_t>(), src->fq_lenk.as<uint32_t>(), first, n, c->d_off.as<uint64_t>(),
+                   c->d_len.as<uint32_t>(), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->n = n;
+  c->seq_bytes = bytes;
+  c->max_len = max_len;
   return 0;
 }
 
@@ -897,6 +1078,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   float ms_w = 0, ms_s = 0;
   c->stream_out = v2;
   bool resume_states = false;  // the first pass left resume states (GapArgs::rdump)
+  c->hpop_valid = false;
   c->resumed_ids.clear();
   float res_ms = 0, res_w = 0;  // the cooperative launches over resumed reads (after each chunk)
   int64_t res_ok = 0;           // reads they resolved
@@ -947,12 +1129,16 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const bool resume = lw && c->gap_resume && c->gap_coop && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK;
     uint64_t rd_cap = 0;
     if (resume) {
-      rd_cap = std::min<uint64_t>((uint64_t)c->gap_resume_gb << 30, (uint64_t)n * 4096 + (1u << 20)) / 16;
+      // the buffer holds one first-pass chunk's states at a time (cleared after each chunk)
+      rd_cap = std::min<uint64_t>((uint64_t)c->gap_resume_gb << 30, (uint64_t)chunk * 4096 + (1u << 20)) / 16;
       if (c->gap_resume_records > 0) rd_cap = (uint64_t)c->gap_resume_records;
       if (int rc = c->d_rdump.ensure(rd_cap * 16)) return rc;
       if (int rc = c->d_roff.ensure(((uint64_t)n + 2) * 8)) return rc;
       HIPCHK(hipMemsetAsync(c->d_roff.p, 0, ((uint64_t)n + 2) * 8, c->stream));
+      if (int rc = c->d_hpop.ensure(((uint64_t)n + 1) * 4)) return rc;
+      HIPCHK(hipMemsetAsync(c->d_hpop.p, 0, ((uint64_t)n + 1) * 4, c->stream));
       resume_states = true;
+      c->hpop_valid = true;
     }
     // and smaller static slot regions (4096: 5859 -> 5840 ms per 50M-read step, hits identical,
     // profiles/r03_pool_cap_sweep.log; the page table and max_pages are the same for both sizes)
@@ -1131,6 +1317,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         G.rd_next = c->d_roff.as<unsigned long long>() + n;
         G.rd_cap = rd_cap;
         G.roff = c->d_roff.as<uint64_t>() + b0;
+        G.hpop = c->d_hpop.as<uint32_t>() + b0;
         G.tail_lanes = c->gap_tail_lanes;
         G.tail_iters = c->gap_tail_iters;
       }
@@ -1685,6 +1872,18 @@ int ibwa_batch_retry_info(const ibwa_ctx_t *c, int64_t *ids, uint8_t *pass, int6
 }
 
 int ibwa_batch_diag(const ibwa_ctx_t *c, int what, void *out, uint64_t cap_bytes) {
+  if (what == 2) {
+    const uint64_t need2 = (uint64_t)c->n * 4;
+    if (cap_bytes < need2) return fail(IBWA_EINVAL, "diag buffer too small");
+    if (!c->hpop_valid) {  // no resume states in the last run
+      memset(out, 0, need2);
+      return 0;
+    }
+    if (c->n == 0) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(out, c->d_hpop.p, need2, hipMemcpyDeviceToHost));
+    return 0;
+  }
   const uint64_t need = what == 0 ? (uint64_t)c->n * 4 : (uint64_t)c->n * 8;
   if (!c->diag || (what != 0 && what != 1)) return fail(IBWA_EINVAL, "set option diag=1 before the run; what = 0 or 1");
   if (cap_bytes < need) return fail(IBWA_EINVAL, "diag buffer too small");

@@ -265,6 +265,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   int len = 0, opt_max_diff = 0, max_diff = 0, best_score = 0, n_aln = 0;
   int best_cnt = 0, n_entries = 0;
   uint32_t bump = 0, status = 0, n_free = 0, n_pages = 0, n_iter = 0;
+  uint32_t n_pops = 0;  // pops made (bwtgap.c:129): where a resume state splits the read's work
   // freed slots beyond the LDS stack: a list threaded through the slots themselves (x = next);
   // fl_next is the head's successor once known (loaded with an iteration's other loads)
   uint32_t fl_head = 0, fl_next = 0;
@@ -391,7 +392,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       const int src = __builtin_ctzll(dm);
       dm &= dm - 1;
       const uint32_t sbump = (uint32_t)__shfl((int)bump, src), sna = (uint32_t)__shfl(n_aln, src);
-      const uint32_t sne = (uint32_t)__shfl(n_entries, src);
+      const uint32_t sne = (uint32_t)__shfl(n_entries, src), spops = (uint32_t)__shfl((int)n_pops, src);
       const int smin = __shfl(minsc, src);
       const uint32_t scs = (uint32_t)__shfl((int)cs, src), scp = (uint32_t)__shfl((int)cp, src);
       // the first pass runs 64 reads per wave: lane x's static region is region gtid
@@ -436,8 +437,9 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
         for (uint32_t j = (uint32_t)lane; j < sna; j += 64) out[RD_HDR + cnt + j] = se1[P0 - 1 - j];
         if (lane == src) {
           out[0] = make_uint4(cnt, sna, (uint32_t)smin, sne);
-          out[1] = make_uint4((uint32_t)best_score, (uint32_t)best_cnt, (uint32_t)max_diff, 0u);
+          out[1] = make_uint4((uint32_t)best_score, (uint32_t)best_cnt, (uint32_t)max_diff, spops);
           ka->roff[ro] = off + 1;
+          if (ka->hpop) ka->hpop[ro] = spops;
           atomicAdd(ka->rd_next + 1, 1ull);  // states stored
         }
       }
@@ -477,6 +479,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       fl_known = true;
       n_pages = 0;
       n_iter = 0;
+      n_pops = 0;
       n_entries = 2;
       C_slot = 1;
       C_b = 0;
@@ -657,6 +660,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       const uint32_t prev = E::prev(e);
       lds_heads[hidx(C_b)] = (H)prev;
       --n_entries;
+      ++n_pops;
       if (C_slot + 1 == bump) {
         bump = C_slot;
       } else if (REUSE && n_free < FREE_DEPTH) {

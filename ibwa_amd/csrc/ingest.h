@@ -1,0 +1,338 @@
+// ingest.h -- `ibwa-amd aln`'s FASTQ input parsed on the GPUs (fastq.hip, ibwa_fq_parse).
+//
+// bwa_aln_core (bwtaln.c:199-231) reads batches of 0x40000 kept reads with bwa_read_seq
+// (bwaseqio.c:145-208).  For an uncompressed FASTQ file the host here only moves bytes: host
+// threads pread() the file into pinned buffers, one region at a time (the next region is read
+// while the current one is parsed and aligned), and each GPU's ingest context parses its piece of
+// the region -- strict 4-line records split, checked, barcode / -q trimmed, nt4-encoded and
+// reversed on the device (ibwa_fq_parse) -- and keeps the kept reads in HBM.  From the per-record
+// lengths the host forms the reference's batches (kSub kept reads each, the records bwa_read_seq
+// skips included) and from them groups: consecutive complete batches with the same batch-level
+// max_diff (bwtaln.c:86-88), whose slices -- the group's reads in each GPU's piece -- are staged
+// device to device (ibwa_batch_stage_fq).  A region's last, incomplete batch is parsed again at
+// the start of the next region (its bytes move to the front of the next buffer), except at the
+// end of the file.  At the first record that is not strict (FASTA, multi-line, CRLF, a truncated
+// tail) -- or a batch whose bytes exceed the carry room -- the rest of the file, from the start
+// of the incomplete batch, goes to the host readers (readers.h), whose records are then the
+// reference's as before.
+#pragma once
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ibwa_aln.h"
+#include "readers.h"
+#include "sam_common.h"
+
+namespace ibwa_cli {
+
+// A group the GPUs align: per GPU the kept reads [first, first + count) of its parsed piece.
+struct DevGroup {
+  int64_t n = 0;
+  int max_len = 0;
+  std::vector<std::pair<long, long>> trims;  // per batch: bases trimmed, bases read (bwaseqio.c:206)
+  std::vector<int64_t> first, count;
+};
+
+class FastqGpu {
+ public:
+  // true when `fn` is a regular, uncompressed file this path can take
+  static bool usable(const char *fn) {
+    if (!strcmp(fn, "-")) return false;
+    struct stat st;
+    if (stat(fn, &st) != 0 || !S_ISREG(st.st_mode)) return false;
+    FILE *f = fopen(fn, "rb");
+    if (!f) return false;
+    unsigned char m[2] = {0, 0};
+    const size_t got = fread(m, 1, 2, f);
+    fclose(f);
+    return !(got == 2 && m[0] == 0x1f && m[1] == 0x8b);  // gzip: the host readers inflate it
+  }
+
+  FastqGpu(const char *fn, std::vector<ibwa_ctx_t *> ing, int mode, int trim_qual, int sub, uint64_t piece_bytes,
+           uint64_t carry_bytes)
+      : ing_(std::move(ing)), mode_(mode), trim_(trim_qual), sub_(sub), l_bc_((int)((unsigned)mode >> 24)) {
+    fd_ = open(fn, O_RDONLY);
+    struct stat st;
+    fsize_ = fd_ >= 0 && fstat(fd_, &st) == 0 ? (uint64_t)st.st_size : 0;
+    piece_ = std::max<uint64_t>(piece_bytes, 4096);
+    carry_ = std::max<uint64_t>(carry_bytes, 4096);
+    chunk_ = piece_ * ing_.size();
+    for (auto &b : buf_) {
+      void *p = nullptr;
+      if (ibwa_host_alloc(carry_ + chunk_ + 64, &p)) { ok_ = false; return; }
+      b = static_cast<char *>(p);
+    }
+    ok_ = fd_ >= 0;
+    if (ok_) start_read(0);
+  }
+  ~FastqGpu() {
+    if (reader_.joinable()) reader_.join();
+    for (char *b : buf_) ibwa_host_free(b);
+    if (fd_ >= 0) close(fd_);
+  }
+  bool ok() const { return ok_; }
+  // the host readers take over at this file offset (valid once next() returned false with handoff())
+  bool handoff() const { return handoff_; }
+  uint64_t handoff_offset() const { return handoff_off_; }
+  double parse_s() const { return parse_s_; }
+  double dev_ms() const { return dev_ms_; }
+  int64_t records() const { return n_records_; }
+
+  // The next group, false when the GPU path is over (the input ended, or handoff()).  All of the
+  // previous region's groups must have been staged before the call that parses a new region.
+  template <class KeyFn>
+  bool next(DevGroup &g, KeyFn key_of) {
+    for (;;) {
+      if (gi_ < groups_.size()) {
+        g = std::move(groups_[gi_++]);
+        return true;
+      }
+      if (after_ != NEXT) {
+        handoff_ = after_ == HANDOFF;
+        return false;
+      }
+      after_ = parse_region(key_of);
+    }
+  }
+
+ private:
+  std::vector<ibwa_ctx_t *> ing_;
+  int mode_, trim_, sub_, l_bc_;
+  int fd_ = -1;
+  uint64_t fsize_ = 0, piece_ = 0, carry_ = 0, chunk_ = 0;
+  char *buf_[2] = {nullptr, nullptr};
+  bool ok_ = false, handoff_ = false;
+  uint64_t handoff_off_ = 0;
+  int cur_ = 0;                 // buffer of the region being parsed
+  uint64_t tail_ = 0;           // carried bytes in front of the chunk in buf_[cur_]
+  uint64_t tail_file_off_ = 0;  // file offset of the carried bytes' first byte
+  uint64_t next_off_ = 0;       // file offset of the next chunk
+  uint64_t got_[2] = {0, 0};
+  std::thread reader_;
+  std::vector<DevGroup> groups_;
+  size_t gi_ = 0;
+  double parse_s_ = 0, dev_ms_ = 0;
+  int64_t n_records_ = 0;
+
+  // chunk at file offset next_off_ into buf_[b] + carry_, by several threads
+  void start_read(int b) {
+    const uint64_t off = next_off_, want = off < fsize_ ? std::min<uint64_t>(chunk_, fsize_ - off) : 0;
+    next_off_ = off + want;
+    char *dst = buf_[b] + carry_;
+    reader_ = std::thread([this, b, off, want, dst]() {
+      const int nt = std::max(1, std::min<int>(ibwa_sam::host_threads(), (int)(want >> 24) + 1));
+      std::vector<uint64_t> got(nt, 0);
+      std::vector<std::thread> th;
+      for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() {
+          const uint64_t lo = want * t / nt, hi = want * (t + 1) / nt;
+          uint64_t p = lo;
+          while (p < hi) {
+            const ssize_t r = pread(fd_, dst + p, (size_t)std::min<uint64_t>(hi - p, 1u << 30), (off_t)(off + p));
+            if (r <= 0) break;
+            p += (uint64_t)r;
+          }
+          got[t] = p - lo;
+        });
+      for (auto &x : th) x.join();
+      uint64_t tot = 0;
+      for (int t = 0; t < nt; ++t) {
+        if (got[t] != want * (t + 1) / nt - want * t / nt) { tot += got[t]; break; }  // short read: stop there
+        tot += got[t];
+      }
+      got_[b] = tot;
+    });
+  }
+
+  // Parse the region in buf_[cur_] and form its groups; after them: 1 the next region, 0 the end
+  // of the input, -1 the host readers from handoff_off_.
+  enum { NEXT = 1, END = 0, HANDOFF = -1 };
+  int after_ = NEXT;
+
+  template <class KeyFn>
+  int parse_region(KeyFn key_of) {
+    reader_.join();
+    const uint64_t got = got_[cur_];
+    const bool eof = next_off_ >= fsize_;
+    char *const base = buf_[cur_] + carry_ - tail_;
+    const uint64_t n = tail_ + got;
+    groups_.clear();
+    gi_ = 0;
+    if (n == 0) return END;
+    // pieces: one per GPU, split at strict record starts (readers.h FastqBulk::rec_at)
+    const int G = (int)ing_.size();
+    std::vector<uint64_t> cut(G + 1, n);
+    cut[0] = 0;
+    for (int g = 1; g < G; ++g) {
+      uint64_t x = std::max<uint64_t>(cut[g - 1], n * (uint64_t)g / (uint64_t)G);
+      cut[g] = n;
+      while (x < n) {
+        const char *nl = static_cast<const char *>(memchr(base + x, '\n', n - x));
+        if (!nl) break;
+        x = (uint64_t)(nl + 1 - base);
+        FastqBulk::Rec r;
+        if (x < n && base[x] == '@' && FastqBulk::rec_at(base + x, base + n, eof, base, r) > 0) { cut[g] = x; break; }
+      }
+      if (cut[g] < cut[g - 1]) cut[g] = cut[g - 1];
+    }
+    // each GPU parses its piece (in parallel)
+    struct Piece {
+      int64_t n_rec = 0;
+      uint64_t consumed = 0;
+      int not_strict = 0, rc = 0;
+      std::vector<int32_t> len;
+      std::vector<uint32_t> L;
+    };
+    std::vector<Piece> pc(G);
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+      std::vector<std::thread> th;
+      for (int g = 0; g < G; ++g)
+        th.emplace_back([&, g]() {
+          Piece &p = pc[g];
+          const uint64_t bytes = cut[g + 1] - cut[g];
+          if (!bytes) return;
+          const int64_t cap = (int64_t)(bytes / 8 + 1);  // a strict record holds >= 8 bytes
+          p.len.resize(cap);
+          p.L.resize(cap);
+          p.rc = ibwa_fq_parse(ing_[g], base + cut[g], bytes, mode_, trim_, &p.n_rec, &p.consumed, &p.not_strict,
+                               p.len.data(), p.L.data(), cap);
+        });
+      for (auto &x : th) x.join();
+    }
+    parse_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int g = 0; g < G; ++g) {
+      if (pc[g].rc) {
+        fprintf(stderr, "[ibwa-amd aln] FASTQ parse on GPU %d: %s\n", g, ibwa_last_error());
+        handoff_off_ = tail_file_off_;
+        return HANDOFF;
+      }
+      double ms = 0;
+      if (cut[g + 1] > cut[g]) ibwa_fq_stats(ing_[g], nullptr, &ms);
+      dev_ms_ += ms;
+    }
+    // the region's records: pieces in order, up to the first one that does not end on its cut
+    int g_end = 0;
+    bool strict_stop = false;
+    uint64_t end_byte = 0;
+    for (int g = 0; g < G; ++g) {
+      g_end = g + 1;
+      end_byte = cut[g] + pc[g].consumed;
+      if (end_byte != cut[g + 1] || pc[g].not_strict) {
+        strict_stop = pc[g].not_strict != 0;
+        break;
+      }
+    }
+    // batches of sub_ kept reads (bwa_read_seq's n_needed; skipped records ride along)
+    struct Bt {
+      int g0 = 0;
+      int64_t r0 = 0, kept = 0;
+      int max_len = 0;
+      long trimmed = 0, total = 0;
+    };
+    std::vector<Bt> bts;
+    Bt cb;
+    bool open_batch = false;
+    std::vector<int64_t> kept_before(G + 1, 0);
+    int64_t kept_tot = 0, recs = 0;
+    for (int g = 0; g < G; ++g) {
+      kept_before[g] = kept_tot;
+      if (g >= g_end) continue;
+      for (int64_t r = 0; r < pc[g].n_rec; ++r) {
+        if (!open_batch) {
+          cb = Bt();
+          cb.g0 = g;
+          cb.r0 = r;
+          open_batch = true;
+        }
+        const int32_t len = pc[g].len[r];
+        if (len >= 0) {  // bwaseqio.c:176-180, bwa_trim_read
+          const long full = (long)pc[g].L[r] - l_bc_;
+          cb.total += full;
+          cb.trimmed += full - len;
+          cb.max_len = std::max<int>(cb.max_len, len);
+          ++cb.kept;
+          ++kept_tot;
+        }
+        ++recs;
+        if (cb.kept == sub_) {
+          bts.push_back(cb);
+          open_batch = false;
+        }
+      }
+    }
+    kept_before[G] = kept_tot;
+    const bool input_end = eof && !strict_stop && end_byte == n;
+    uint64_t rewind = end_byte;  // region offset where what follows these groups starts
+    if (open_batch) {
+      if (input_end) {
+        if (cb.kept > 0) bts.push_back(cb);  // the input's last batch
+      } else {
+        uint64_t off = 0;
+        if (cb.r0 > 0 && ibwa_fq_offset(ing_[cb.g0], cb.r0, &off)) {
+          fprintf(stderr, "[ibwa-amd aln] FASTQ parse: %s\n", ibwa_last_error());
+          handoff_off_ = tail_file_off_;
+          return HANDOFF;
+        }
+        rewind = cut[cb.g0] + off;
+        for (int64_t r = cb.r0; r < pc[cb.g0].n_rec; ++r) --recs;  // parsed again
+        for (int g = cb.g0 + 1; g < g_end; ++g) recs -= pc[g].n_rec;
+      }
+    }
+    // groups: consecutive batches with the same batch-level key; per GPU the kept reads they hold
+    int64_t k0 = 0;
+    for (size_t b = 0; b < bts.size();) {
+      const int key = key_of(bts[b].max_len);
+      DevGroup dg;
+      dg.first.assign(G, 0);
+      dg.count.assign(G, 0);
+      const int64_t ka = k0;
+      size_t e = b;
+      while (e < bts.size() && key_of(bts[e].max_len) == key) {
+        dg.max_len = std::max(dg.max_len, bts[e].max_len);
+        dg.trims.emplace_back(bts[e].trimmed, bts[e].total);
+        k0 += bts[e].kept;
+        ++e;
+      }
+      dg.n = k0 - ka;
+      for (int g = 0; g < G; ++g) {
+        const int64_t lo = std::max(ka, kept_before[g]), hi = std::min(k0, kept_before[g + 1]);
+        dg.first[g] = hi > lo ? lo - kept_before[g] : 0;
+        dg.count[g] = hi > lo ? hi - lo : 0;
+      }
+      groups_.push_back(std::move(dg));
+      b = e;
+    }
+    n_records_ += recs;
+    const uint64_t file_rewind = tail_file_off_ + rewind;
+    if (input_end) return END;
+    if (strict_stop || eof) {  // a record the host readers must see (not strict, truncated, ...)
+      handoff_off_ = file_rewind;
+      return HANDOFF;
+    }
+    const uint64_t carry = n - rewind;
+    if (carry > carry_) {
+      handoff_off_ = file_rewind;
+      return HANDOFF;
+    }
+    // the next region: the carried bytes in front of the next chunk, read meanwhile
+    const int nb = cur_ ^ 1;
+    memcpy(buf_[nb] + carry_ - carry, base + rewind, carry);
+    tail_ = carry;
+    tail_file_off_ = file_rewind;
+    start_read(nb);
+    cur_ = nb;
+    return NEXT;
+  }
+};
+
+}  // namespace ibwa_cli

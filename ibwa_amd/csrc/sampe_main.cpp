@@ -984,13 +984,20 @@ struct Sampe {
     ph.mark("pairing: positions");
     std::vector<const Position *> parr(n);
     for (int i = 0; i < n; ++i) parr[i] = pstore[pth[i]].data() + poff[i];
+    // `sampe -t T`: the reference's thread t (threadblock_exec, bwape.c:249-253) takes pairs t, t+T,
+    // t+2T, ... into its own position array, so the slots past a pair's positions hold what the
+    // earlier pairs of its residue class mod T left there: one nearest-greater chain per class
     std::vector<int32_t> pg(n, -1);
     {
+      const int T = popt.n_threads > 1 ? popt.n_threads : 1;
       std::vector<int32_t> st;
-      for (int i = 0; i < n; ++i) {
-        while (!st.empty() && pcnt[st.back()] <= pcnt[i]) st.pop_back();
-        pg[i] = st.empty() ? -1 : st.back();
-        st.push_back(i);
+      for (int c = 0; c < T && c < n; ++c) {
+        st.clear();
+        for (int i = c; i < n; i += T) {
+          while (!st.empty() && pcnt[st.back()] <= pcnt[i]) st.pop_back();
+          pg[i] = st.empty() ? -1 : st.back();
+          st.push_back(i);
+        }
       }
     }
     if (getenv("IBWA_SAMPE_STATS")) {

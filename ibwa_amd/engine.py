@@ -76,6 +76,14 @@ CAPI = {
     "ibwa_gap_init_opt": (None, [c.POINTER(GapOpt)]),
     "ibwa_cal_maxdiff": (_i, [_i, c.c_double, c.c_double]),
     "ibwa_ctx_create": (_i, [_i, c.POINTER(_vp)]),
+    "ibwa_device_count": (_i, [c.POINTER(_i)]),
+    "ibwa_fq_parse": (_i, [_vp, _vp, c.c_uint64, _i, _i, c.POINTER(c.c_int64), c.POINTER(c.c_uint64), c.POINTER(_i),
+                           _vp, _vp, c.c_int64]),
+    "ibwa_fq_stats": (_i, [_vp, c.POINTER(c.c_int64), c.POINTER(c.c_double)]),
+    "ibwa_fq_offset": (_i, [_vp, c.c_int64, c.POINTER(c.c_uint64)]),
+    "ibwa_batch_stage_fq": (_i, [_vp, _vp, c.c_int64, c.c_int64, _i]),
+    "ibwa_host_alloc": (_i, [c.c_uint64, c.POINTER(_vp)]),
+    "ibwa_host_free": (_i, [_vp]),
     "ibwa_ctx_destroy": (None, [_vp]),
     "ibwa_ctx_load_bwt": (_i, [_vp, _i, _u32, c.POINTER(_u32), _vp, _u64]),
     "ibwa_ctx_load_bwt_file": (_i, [_vp, _i, c.c_char_p]),
@@ -207,6 +215,11 @@ class Engine:
         arr = (c.c_uint32 * 4)(*[int(x) for x in L2])
         _chk(lib().ibwa_ctx_load_bwt(self.h, strand, int(primary), arr, words.ctypes.data, words.size))
 
+    def share_index(self, src):
+        """Borrow src's resident index (ibwa_ctx_share_index); src must outlive this engine."""
+        _chk(lib().ibwa_ctx_share_index(self.h, src.h))
+        self._share_src = src
+
     def set_tuning(self, stack_cap=0, aln_cap=0, block=0):
         _chk(lib().ibwa_ctx_set_tuning(self.h, stack_cap, aln_cap, block))
 
@@ -249,6 +262,12 @@ class Engine:
         _chk(lib().ibwa_batch_diag(self.h, 0, it.ctypes.data, it.nbytes))
         _chk(lib().ibwa_batch_diag(self.h, 1, ft.ctypes.data, ft.nbytes))
         return it, ft
+
+    def handoff_pops(self):
+        """Per read: pops the first pass made before leaving its resume state (0: none), ibwa_batch_diag 2."""
+        hp = np.zeros(self.n, np.uint32)
+        _chk(lib().ibwa_batch_diag(self.h, 2, hp.ctypes.data, hp.nbytes))
+        return hp
 
     def stats(self):
         st = RunStats()

@@ -68,6 +68,8 @@ int ibwa_cal_maxdiff(int len, double err, double thres);
 
 /* One engine per GPU (device ordinal).  Owns a HIP stream and device buffers. */
 int ibwa_ctx_create(int device, ibwa_ctx_t **out);
+/* Visible HIP devices (the CLI's -G maps GPU slice g to device g mod this count). */
+int ibwa_device_count(int *n);
 void ibwa_ctx_destroy(ibwa_ctx_t *ctx);
 
 /*
@@ -83,7 +85,9 @@ int ibwa_ctx_load_bwt_file(ibwa_ctx_t *ctx, int strand, const char *path);
 int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src);
 /* Use the index of another context on the same device without a copy: its BWT and the structures
  * ibwa_ctx_prepare built (call after it).  Two contexts then align different batches concurrently on
- * one GPU (the CLI's overlapped groups).  src must outlive dst. */
+ * one GPU (the CLI's overlapped groups).  src must outlive dst.  While shared, neither context may
+ * rebuild or replace the index (load_bwt, build_index, load_sa, clone_index into it, option kmer_k,
+ * K-mer tables or a sampled SA the destination would have to build): those return IBWA_EINVAL. */
 int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src);
 
 /*
@@ -107,6 +111,31 @@ int ibwa_aln_batch(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt, int64_t n_seqs, c
  */
 int ibwa_batch_stage(ibwa_ctx_t *ctx, int64_t n_seqs, const uint8_t *seq, const uint64_t *off,
                      const uint32_t *len);
+
+/*
+ * FASTQ ingest on the device -- bwa_read_seq (bwaseqio.c:145-208) over kseq_read (kseq.h:156-195)
+ * for strict 4-line records ("@header", one line of sequence bytes: isgraph, none of '>' '+' '@';
+ * a line starting with '+'; one line of quality bytes 33..127 as long as the sequence), with the
+ * barcode strip (-B: mode >> 24), -I and bwa_trim_read (-q, :74-87), nst_nt4_table codes and the
+ * reversal (:197).  raw[0, nbytes) must begin at a record.  Out: *n_rec strict records from its
+ * start (at most cap), the *consumed bytes they span, *not_strict = 1 when the next complete
+ * record is not strict (the serial kseq reader takes over there; else the block ended inside a
+ * record), per record the kept length (-1: not longer than the barcode, skipped as bwaseqio.c:162)
+ * and the sequence line's length (rec_len / rec_L may be null).  The kept reads stay in the
+ * context (one block at a time) for ibwa_batch_stage_fq.  raw may be pinned (ibwa_host_alloc).
+ */
+int ibwa_fq_parse(ibwa_ctx_t *ctx, const void *raw, uint64_t nbytes, int mode, int trim_qual, int64_t *n_rec,
+                  uint64_t *consumed, int *not_strict, int32_t *rec_len, uint32_t *rec_L, int64_t cap);
+/* byte offset (in the block) of record r of the last ibwa_fq_parse (r <= its n_rec) */
+int ibwa_fq_offset(const ibwa_ctx_t *ctx, int64_t r, uint64_t *off);
+/* kept reads and device time (H2D copy + kernels, ms) of the last ibwa_fq_parse */
+int ibwa_fq_stats(const ibwa_ctx_t *ctx, int64_t *kept, double *ms);
+/* ibwa_batch_stage from src's last parsed block (same device): its kept reads [first, first + n),
+ * copied device to device; max_len = their longest */
+int ibwa_batch_stage_fq(ibwa_ctx_t *ctx, const ibwa_ctx_t *src, int64_t first, int64_t n, int max_len);
+/* pinned host memory for the raw blocks */
+int ibwa_host_alloc(uint64_t bytes, void **p);
+int ibwa_host_free(void *p);
 int ibwa_batch_run(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt, int batch_max_len);
 int ibwa_batch_fetch(ibwa_ctx_t *ctx, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total);
 
@@ -203,7 +232,9 @@ int ibwa_batch_retry_info(const ibwa_ctx_t *ctx, int64_t *ids, uint8_t *pass, in
 /* Diagnostics of the last ibwa_batch_run with option "diag" = 1 (gapped path): what 0 = first-pass
  * iterations per read (uint32[n]); 1 = k_width's search-cost features per read (uint16[n][4]:
  * sum of log2 width over both full-length chains, the same over the seed chains, the smaller
- * restart count of the two full chains, of the two seed chains). */
+ * restart count of the two full chains, of the two seed chains).  what 2 (no option needed): per
+ * read the pops (bwtgap.c:129) the first pass made before leaving its resume state, 0 if it left
+ * none (uint32[n]): the point where the read's search moves from k_gapped to k_coop. */
 int ibwa_batch_diag(const ibwa_ctx_t *ctx, int what, void *out, uint64_t cap_bytes);
 
 /* Tuning knobs (0 = default): per-lane stack entries, per-read hit slots, block size */

@@ -79,6 +79,7 @@ def lib():
         L.or_free.argtypes = [c.c_void_p]
         L.or_set_stats.argtypes = [c.c_void_p]
         L.or_set_width_touches.argtypes = [c.c_void_p]
+        L.or_set_touch_split.argtypes = [c.c_void_p, c.c_void_p]
         L.or_push_kinds.argtypes = [c.c_void_p]
         L.or_exact_touches.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p, c.c_void_p,
                                        c.c_int, c.c_int, c.c_int, c.c_void_p]
@@ -298,13 +299,21 @@ STATS_DTYPE = np.dtype([("pushes", "<u4"), ("pops", "<u4"), ("peak_entries", "<u
                         ("rounds_g4", "<u4"), ("rounds_g16", "<u4"), ("rounds_lvl", "<u4")])
 
 
-def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False, stats=None, width_touches=None):
+def cal_sa_reg_gap(bwt0, bwt1, seqs, offs, lens, opt, n_threads=1, touches=False, stats=None, width_touches=None,
+                   split_pops=None, split_touches=None):
     """Run the restated bwa_cal_sa_reg_gap.  Returns (n_aln int32[n], alns ALN_DTYPE[...], touches).
     `stats`: optional STATS_DTYPE[n] array filled with per-read search statistics.
     `width_touches`: optional uint32[n] array filled with the touches of each read's bwt_cal_width
-    calls (bwtaln.c:123-130) alone; touches - width_touches are bwt_match_gap's."""
+    calls (bwtaln.c:123-130) alone; touches - width_touches are bwt_match_gap's.
+    `split_pops` / `split_touches`: optional uint32[n] arrays; split_touches[r] gets the touches counted
+    before pop split_pops[r] + 1 of read r (its total if split_pops[r] is 0 or never reached) -- the
+    GPU first pass's share of a read that left its resume state after that many pops."""
     L = lib()
     n = len(lens)
+    if split_pops is not None:
+        assert split_pops.dtype == np.uint32 and split_pops.size >= n and split_pops.flags.c_contiguous
+        assert split_touches.dtype == np.uint32 and split_touches.size >= n and split_touches.flags.c_contiguous
+        L.or_set_touch_split(ctypes.c_void_p(split_pops.ctypes.data), ctypes.c_void_p(split_touches.ctypes.data))
     if width_touches is not None:
         assert width_touches.dtype == np.uint32 and width_touches.size >= n and width_touches.flags.c_contiguous
         L.or_set_width_touches(ctypes.c_void_p(width_touches.ctypes.data))

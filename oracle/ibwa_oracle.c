@@ -322,6 +322,7 @@ typedef struct {
 	int next_kind; /* instrumentation: kind of the next push (OR_K_*) */
 	uint32_t *chl, chl_n, chl_m; /* chain (length << 11 | level) in pop order, when stats are on */
 	uint64_t *hset; uint32_t hcap, hn; /* distinct (a,i,k,l) expansions, when stats are on */
+	uint32_t split_pop, touch_at_split; /* touches counted before pop number split_pop + 1 (0: off) */
 } gstack_t;
 
 /* per-read search statistics (test/bench instrumentation only) */
@@ -336,6 +337,12 @@ void or_set_stats(or_stats_t *buf) { g_stats_next = buf; }
  * touches are bwt_match_gap's), consumed by the next or_cal_sa_reg_gap call */
 static uint32_t *g_wtouch_next;
 void or_set_width_touches(uint32_t *buf) { g_wtouch_next = buf; }
+/* per read a pop count p (0: none) and the touches counted before pop p + 1 -- where the GPU's first
+ * pass left the read's resume state after p pops (gapped.hip dump_states) -- consumed by the next
+ * or_cal_sa_reg_gap call; the bench splits bwt_match_gap's touches of a resumed read there */
+static const uint32_t *g_split_pops_next;
+static uint32_t *g_split_touch_next;
+void or_set_touch_split(const uint32_t *pops, uint32_t *touches) { g_split_pops_next = pops; g_split_touch_next = touches; }
 
 #define SCORE(m, o, e, p) ((m) * (p)->s_mm + (o) * (p)->s_gapo + (e) * (p)->s_gape)
 #define ST_M 0
@@ -514,6 +521,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 		width_t *width;
 
 		if (stack->n_entries > opt->max_entries) break;
+		if (stack->split_pop && stack->pops == stack->split_pop) stack->touch_at_split = *t;
 		gs_pop(stack, &e);
 		k = e.k; l = e.l;
 		a = e.a; i = e.i;
@@ -717,6 +725,8 @@ typedef struct {
 	int32_t *n_aln;
 	or_aln1_t **per_read;
 	uint32_t *touches, *wtouches;
+	const uint32_t *split_pops;
+	uint32_t *split_touches;
 	or_stats_t *stats;
 	int64_t next;  /* dynamic claim of THREAD_BLOCK reads (bwtaln.c:100-113) */
 	pthread_mutex_t lock;
@@ -764,6 +774,8 @@ static void *worker(void *data)
 			}
 			if (B->wtouches) B->wtouches[r] = t;
 			stack->pushes = stack->pops = stack->peak = stack->peak_bucket = 0;
+			stack->split_pop = B->split_pops ? B->split_pops[r] : 0;
+			stack->touch_at_split = t;
 			match_gap(B->bwt, L, seq, w, L <= opt->seed_len ? 0 : sw, &local, &out, stack, &t);
 			B->n_aln[r] = out.n;
 			if (B->stats) {
@@ -808,6 +820,7 @@ static void *worker(void *data)
 				memcpy(B->per_read[r], out.a, out.n * sizeof(or_aln1_t));
 			} else B->per_read[r] = 0;
 			if (B->touches) B->touches[r] = t;
+			if (B->split_touches) B->split_touches[r] = stack->split_pop ? stack->touch_at_split : t;
 		}
 	}
 	free(out.a); free(rseq);
@@ -833,6 +846,10 @@ int64_t or_cal_sa_reg_gap(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_
 	g_stats_next = 0;
 	B.wtouches = g_wtouch_next;
 	g_wtouch_next = 0;
+	B.split_pops = g_split_pops_next;
+	B.split_touches = g_split_touch_next;
+	g_split_pops_next = 0;
+	g_split_touch_next = 0;
 	B.per_read = (or_aln1_t**)calloc(n_seqs > 0 ? n_seqs : 1, sizeof(or_aln1_t*));
 	pthread_mutex_init(&B.lock, 0);
 	for (i = 0; i < n_seqs; ++i) if ((int)len[i] > B.max_len) B.max_len = (int)len[i];

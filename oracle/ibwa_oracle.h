@@ -81,6 +81,9 @@ int64_t or_cal_sa_reg_gap(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_
                           const or_gap_opt_t *opt, int n_threads,
                           int32_t *n_aln, or_aln1_t **alns_out, uint32_t *touches_out);
 void or_free(void *p);
+/* next or_cal_sa_reg_gap only: per read a pop count p (0: none) -> touches[r] = the touches counted
+ * before pop p + 1 (the read's total when p is 0 or never reached) */
+void or_set_touch_split(const uint32_t *pops, uint32_t *touches);
 void or_exact_touches(const or_bwt_t *bwt0, const or_bwt_t *bwt1, int64_t n_seqs, const uint8_t *seq,
                       const uint64_t *off, const uint32_t *len, int mode, int K, int jump, uint32_t *touches);
 

@@ -120,3 +120,80 @@ def test_cli_truncated_last_record(golden_dir, key, tmp_path):
     assert oracle.sai_body_equal(got, gold)
     got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path, {"IBWA_ALN_SERIAL_READ": "1"}, "s.sai")
     assert oracle.sai_body_equal(got, gold)
+
+
+@pytest.mark.parametrize("key", ["r100.default", "mixed.default", "r36.n0"])
+def test_cli_multi_gpu_rehearsal(golden_dir, sai_manifest, key, tmp_path):
+    """`aln -G 2` / `-G 3` on one GPU (slice g runs on device g mod the visible devices,
+    aln_main.cpp): the index replicated device to device (ibwa_ctx_clone_index), each group split
+    into per-GPU slices that keep the batch-level options (bwtaln.c:89-93), the slices' records
+    written in input order, with two overlapped lanes per slice.  Small groups so that every slice
+    holds reads.  The .sai equals -G 1's and the reference's."""
+    m = sai_manifest[key]
+    gold = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+    env = {"IBWA_ALN_SUBBATCH": "96", "IBWA_ALN_GROUP": "2", "IBWA_ALN_LANES": "2"}
+    one = run_cli_env(m["argv"] + ["-G", "1"], golden_dir, m["reads"], tmp_path, env, "g1.sai")
+    assert oracle.sai_body_equal(one, gold)
+    for g in ("2", "3"):
+        got = run_cli_env(m["argv"] + ["-G", g], golden_dir, m["reads"], tmp_path, env, f"g{g}.sai")
+        assert got[64:] == one[64:], g
+
+
+def _variety_fastq(path, n, seed, crlf_at=None, truncate=False):
+    """Strict 4-line FASTQ of reads drawn from the golden genome with what bwa_read_seq branches on:
+    lengths 20-160 (some not longer than a barcode), lower case, N, '-', low-quality tails, long and
+    empty headers; optionally CRLF records from crlf_at on (the host readers take over there) and a
+    truncated last record."""
+    import random
+    from tests.synth_util import golden_genome_ascii
+    g, _, _ = golden_genome_ascii()
+    rng = random.Random(seed)
+    out = []
+    for i in range(n):
+        L = rng.choice([20, 36, 70, 100, 100, 100, 150, 160, 4, 8])
+        p = rng.randrange(0, len(g) - L)
+        s = list(g[p:p + L].replace("N", "A"))
+        for _ in range(rng.randrange(0, 4)):
+            s[rng.randrange(L)] = rng.choice("ACGTacgtN-")
+        if rng.random() < 0.2:
+            s = [c.lower() for c in s]
+        q = [chr(33 + rng.randint(25, 40)) for _ in range(L)]
+        if rng.random() < 0.3:
+            for j in range(max(0, L - rng.randint(5, 40)), L):
+                q[j] = chr(33 + rng.randint(2, 12))
+        name = "" if rng.random() < 0.02 else f"v{i} some comment {rng.random()}"
+        eol = "\r\n" if crlf_at is not None and i >= crlf_at else "\n"
+        out.append(f"@{name}{eol}{''.join(s)}{eol}+{eol}{''.join(q)}{eol}")
+    text = "".join(out)
+    if truncate:
+        text = text[:-7]
+    path.write_text(text)
+
+
+@pytest.mark.parametrize("argv", [[], ["-B", "5"], ["-q", "20"], ["-I", "-q", "15"], ["-n", "0"], ["-B", "3", "-q", "10"]])
+@pytest.mark.parametrize("shape", ["plain", "crlf", "truncated"])
+def test_cli_gpu_parse_equals_host(golden_dir, argv, shape, tmp_path):
+    """FASTQ parsed on the GPU (ingest.h, fastq.hip) == the host readers (IBWA_ALN_GPU_PARSE=0) ==
+    the serial kseq reader: small regions (IBWA_FQ_PIECE_BYTES) so that batches straddle regions and
+    are parsed again, a second GPU slice (-G 2 on one device: pieces split at record starts), CRLF
+    records in the middle (the host readers take over at the first batch they fall in) and a
+    truncated last record."""
+    fq = tmp_path / "v.fq"
+    _variety_fastq(fq, 3000, 7, crlf_at=1700 if shape == "crlf" else None, truncate=shape == "truncated")
+    env = {"IBWA_ALN_SUBBATCH": "200", "IBWA_ALN_GROUP": "3"}
+    host = run_cli_env(argv, golden_dir, str(fq), tmp_path, dict(env, IBWA_ALN_GPU_PARSE="0"), "host.sai")
+    ser = run_cli_env(argv, golden_dir, str(fq), tmp_path, dict(env, IBWA_ALN_SERIAL_READ="1"), "ser.sai")
+    assert len(host) > 64 and host[64:] == ser[64:]
+    for extra, piece in (([], "1000000000"), ([], "40000"), (["-G", "2"], "30000")):
+        dev = run_cli_env(argv + extra, golden_dir, str(fq), tmp_path, dict(env, IBWA_FQ_PIECE_BYTES=piece), "dev.sai")
+        assert dev[64:] == host[64:], (extra, piece)
+
+
+def test_cli_gpu_parse_carry_overflow(golden_dir, sai_manifest, tmp_path):
+    """A batch whose bytes do not fit the carry room hands the rest to the host readers; the .sai is
+    still the reference's."""
+    m = sai_manifest["r100.default"]
+    gold = open(os.path.join(golden_dir, "r100.default.sai"), "rb").read()
+    got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path,
+                      {"IBWA_ALN_SUBBATCH": "500", "IBWA_FQ_PIECE_BYTES": "20000", "IBWA_FQ_CARRY_BYTES": "4096"}, "c.sai")
+    assert oracle.sai_body_equal(got, gold)

@@ -233,3 +233,33 @@ def test_sai_goldens_lds_widths(golden_dir, sai_manifest, gpu_engine, gap_lw):
             bad.append(key)
     gpu_engine.set_option("gap_lw", 1)
     assert not bad, bad
+
+
+def test_shared_index_is_frozen(golden_dir, sai_manifest):
+    """ibwa_ctx_share_index: a context borrowing another's index aligns the goldens bit-exact, and
+    while the index is shared neither side may rebuild or replace it (borrowed buffers would be
+    written in place under the other context, or could not grow): option kmer_k and load_bwt fail
+    with IBWA_EINVAL on both; once the borrower is gone the source may again."""
+    src = E.Engine(0)
+    src.load_index_files(os.path.join(golden_dir, "g1m"))
+    m = sai_manifest["r100.default"]
+    opt, _ = oracle.parse_aln_args(m["argv"])
+    src.prepare(_eopt(opt))
+    dst = E.Engine(0)
+    dst.share_index(src)
+    recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+    seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+    n_aln, alns = dst.aln(seqs, offs, lens, _eopt(opt))
+    assert oracle.sai_body_equal(oracle.sai_bytes(opt, n_aln, alns), open(os.path.join(golden_dir, "r100.default.sai"), "rb").read())
+    for eng in (dst, src):
+        with pytest.raises(E.IbwaError, match="share"):
+            eng.set_option("kmer_k", 5)
+        with pytest.raises(E.IbwaError, match="share"):
+            eng.load_index_files(os.path.join(golden_dir, "g1m"))
+    with pytest.raises(E.IbwaError, match="share"):
+        E.Engine(0).share_index(dst)
+    dst.close()
+    src.set_option("kmer_k", 5)
+    n2, a2 = src.aln(seqs, offs, lens, _eopt(opt))
+    assert (n2 == n_aln).all() and a2.tobytes() == alns.tobytes()
+    src.close()

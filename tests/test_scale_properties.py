@@ -145,6 +145,8 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
             eng.set_option(k, v)
         n_aln, alns = eng.aln(seq, off, lns, e)
         st = eng.stats()
+        hpop = eng.handoff_pops()
+        ids, ps = eng.retry_info()
     finally:
         for k in tune:
             eng.set_option(k, defaults[k])
@@ -154,6 +156,14 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
         assert st.n_resumed > 0  # the resume path ran
         if "gap_resume_records" in tune:
             assert st.resume_records > tune["gap_resume_records"]  # ... and some states did not fit
-    rn, ra, _ = oracle.cal_sa_reg_gap(b0, b1, seq, off, lns, o, n_threads=8)
+    ost = np.zeros(len(lns), dtype=oracle.STATS_DTYPE)
+    rn, ra, _ = oracle.cal_sa_reg_gap(b0, b1, seq, off, lns, o, n_threads=8, stats=ost)
     assert (n_aln == rn).all()
     assert alns.tobytes() == ra.tobytes()
+    # the pops a resumed read made before its hand-off (the bench's touch split): every read the
+    # cooperative pass resumed has them, and the reference's search went on past them
+    res = ids[ps == 4]
+    assert (hpop[res] > 0).all()
+    assert (hpop[res] < ost["pops"][res]).all()
+    if st.n_resumed == 0:
+        assert not hpop.any()

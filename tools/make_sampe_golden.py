@@ -49,6 +49,9 @@ CASES = {
     "pe150.default": ("pe150", [], ["-R"]),
     "pe150.o1000": ("pe150", [], ["-R", "-o", "1000"]),
     "pe70few.default": ("pe70few", [], ["-R"]),
+    # sampe -t T: thread t pairs t, t+T, ... in its own position array (bwape.c:249-253), so
+    # find_optimal_pair's look-ahead reads what the pair's residue class mod T left there
+    "pe100.t4": ("pe100", [], ["-R", "-t", "4"]),
 }
 
 
@@ -183,7 +186,8 @@ def tandem_case():
     write_fq(os.path.join(GOLD, "tandem_2.fq"), "td_", r2s, 2)
     prefix = os.path.join(GOLD, "tandem")
     out = {}
-    for key, argv in (("tandem.R", ["-R"]), ("tandem.R.n2000", ["-R", "-n", "2000", "-N", "3000"])):
+    for key, argv in (("tandem.R", ["-R"]), ("tandem.R.n2000", ["-R", "-n", "2000", "-N", "3000"]),
+                      ("tandem.R.t2", ["-R", "-t", "2"]), ("tandem.R.t3", ["-R", "-t", "3"])):
         sai = []
         for end in (1, 2):
             fn = f"tandem_{end}.sai"
@@ -197,6 +201,54 @@ def tandem_case():
             with gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:
                 f.write(res.stdout)
         out[key] = {"prefix": "tandem", "sai": sai, "reads": ["tandem_1.fq", "tandem_2.fq"], "aln_argv": [],
+                    "argv": argv, "sam": f"sampe_{key}.sam.gz"}
+        print(key, len(res.stdout.splitlines()), "lines")
+    return out
+
+
+def tandem_threads_case():
+    """`sampe -t T` on the tandem genome: pairs from inside the array, each followed T pairs later (T = 2
+    or 3) by a copy of itself, so the reference's thread-local position arrays (thread t pairs t, t+T, ...,
+    bwape.c:249-253) hold the copy's own positions past its end, while one shared array would hold the
+    pair just before it.  The same reads with -t 1 give other SAM lines, which is what pins the
+    residue-class look-ahead (sampe_main.cpp PosView)."""
+    rng = random.Random(33)
+    prefix = os.path.join(GOLD, "tandem")
+    g = "".join(ln.strip() for ln in open(os.path.join(GOLD, "tandem.fa")) if not ln.startswith(">"))
+    L = 100
+    r1s, r2s = [], []
+    while len(r1s) < 600:
+        ins = max(L + 10, int(rng.gauss(300, 30)))
+        f0 = rng.randrange(50000, 50000 + 60000 - ins) if rng.random() < 0.8 else rng.randrange(0, 45000)
+        seg = g[f0:f0 + ins]
+        a, b = mutate(rng, seg[:L], 0.01), mutate(rng, rc(seg[-L:]), 0.01)
+        if len(a) != L or len(b) != L:
+            continue
+        if rng.random() < 0.5:
+            a, b = b, a
+        r1s.append((a, "I" * L))
+        r2s.append((b, "I" * L))
+        if len(r1s) >= 3 and rng.random() < 0.3:  # the pair T = 2 or 3 before, again
+            t = rng.choice([2, 3])
+            r1s.append(r1s[-t])
+            r2s.append(r2s[-t])
+    write_fq(os.path.join(GOLD, "tandemt_1.fq"), "tt_", r1s, 1)
+    write_fq(os.path.join(GOLD, "tandemt_2.fq"), "tt_", r2s, 2)
+    sai = []
+    for end in (1, 2):
+        fn = f"tandemt_{end}.sai"
+        subprocess.run([REF, "aln", "-f", os.path.join(GOLD, fn), prefix, os.path.join(GOLD, f"tandemt_{end}.fq")],
+                       check=True, capture_output=True)
+        sai.append(fn)
+    out = {}
+    for key, argv in (("tandemt.R", ["-R"]), ("tandemt.R.t2", ["-R", "-t", "2"]), ("tandemt.R.t3", ["-R", "-t", "3"])):
+        res = subprocess.run([REF, "sampe"] + argv + [prefix] + [os.path.join(GOLD, x) for x in sai] +
+                             [os.path.join(GOLD, "tandemt_1.fq"), os.path.join(GOLD, "tandemt_2.fq")],
+                             check=True, capture_output=True)
+        with open(os.path.join(GOLD, f"sampe_{key}.sam.gz"), "wb") as raw:
+            with gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:
+                f.write(res.stdout)
+        out[key] = {"prefix": "tandem", "sai": sai, "reads": ["tandemt_1.fq", "tandemt_2.fq"], "aln_argv": [],
                     "argv": argv, "sam": f"sampe_{key}.sam.gz"}
         print(key, len(res.stdout.splitlines()), "lines")
     return out
@@ -234,6 +286,7 @@ def main():
                          "argv": sampe_argv, "sam": f"sampe_{key}.sam.gz"}
         print(key, len(out.stdout.splitlines()), "lines")
     manifest.update(tandem_case())
+    manifest.update(tandem_threads_case())
     with open(os.path.join(GOLD, "sampe_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
 
