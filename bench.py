@@ -594,6 +594,10 @@ def main():
     if args.dump:
         n_d, a_d = eng.fetch()
         np.savez(f"{args.dump}.rank{rank}.npz", n_aln=n_d, alns=a_d.view(np.uint32))
+    # device memory held once the timed steps ran (index, tables and this context's search buffers)
+    free_b, total_b = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b))
+    dev_mem_gb = (total_b.value - free_b.value) / 1e9
     total_reads = args.reads * world * args.steps
     value = total_reads / dt
     ms_step = dt * 1e3 / args.steps
@@ -622,6 +626,9 @@ def main():
                                         "k_coop_roots": ms_cr / launches,
                                         "k_coop": (ms_c - ms_cw - ms_cr) / launches,
                                         "wide+general retry": (ms_r - ms_c) / launches},
+                 "device_memory_gb": {"in_use_after_steps": dev_mem_gb, "total": total_b.value / 1e9,
+                                      "note": "hipMemGetInfo after the timed steps: index + tables + one context's "
+                                              "search buffers (sized for this batch)"},
                  "host_cores": threads, "cpu_model": cpu_model(),
                  # digest of the sources libibwa_amd.so was built from (checked against this tree on load)
                  "build_id": E.lib().ibwa_build_id().decode()}

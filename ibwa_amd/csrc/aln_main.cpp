@@ -578,6 +578,18 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     return 0;
   };
   int64_t k = 0;  // groups launched
+  // IBWA_ALN_PARSE_ONLY=1 (measurement): the input is read and parsed into groups, nothing is aligned
+  const bool parse_only = env_int("IBWA_ALN_PARSE_ONLY", 0) != 0;
+  const auto t_parse_only = std::chrono::steady_clock::now();
+  while (have > 0 && parse_only) {
+    tot_seqs += cur.n();
+    have = timed_read(cur);
+  }
+  if (parse_only) {
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_parse_only).count();
+    fprintf(stderr, "[ibwa-amd aln] parse only: %lld reads, %.3f s parsing (%.3f s after the first group) = %.2f M reads/s (%s)\n",
+            (long long)tot_seqs, parse_s, s, tot_seqs / std::max(parse_s, 1e-9) / 1e6, fg ? "GPU parse" : "host parse");
+  }
   while (have > 0) {
     Job &J = jobs[k % n_lanes];
     if (J.active)  // the oldest group in flight

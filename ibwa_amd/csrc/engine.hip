@@ -147,6 +147,7 @@ struct ibwa_ctx {
   // wave-cooperative heavy-read pass (coop.hip)
   int gap_coop = 1;
   int gap_lw = 1;                    // first pass with its widths in LDS (gapped.hip LW) when they fit
+  int gap_lw_min_waves = 8;          // ... in a workgroup size that keeps at least this many waves per CU
   int gap_resume = 1;                // early hand-offs leave their search state for the coop pass (LW)
   int gap_resume_gb = 48;            // state buffer (GiB, at most ~4 KiB per read of the batch)
   int64_t gap_resume_records = 0;    // tests: state buffer of this many 16 B records (0: by gap_resume_gb)
@@ -418,6 +419,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_early2_iters" && value >= 0) c->gap_early2_iters = (uint32_t)value;
   else if (k == "gap_early2_entries" && value >= 0) c->gap_early2_entries = (uint32_t)value;
   else if (k == "gap_lw" && (value == 0 || value == 1)) c->gap_lw = (int)value;
+  else if (k == "gap_lw_min_waves" && value >= 1 && value <= 32) c->gap_lw_min_waves = (int)value;
   else if (k == "gap_resume" && (value == 0 || value == 1)) c->gap_resume = (int)value;
   else if (k == "gap_resume_gb" && value >= 1 && value <= 256) c->gap_resume_gb = (int)value;
   else if (k == "gap_resume_records" && value >= 0) c->gap_resume_records = (int64_t)value;
@@ -1101,14 +1103,22 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const uint32_t cw_rw = (uint32_t)(max_len + 15) / 16;
     const uint32_t cw_sb = max_len > o.seed_len ? (uint32_t)o.seed_len + 1u : 0u;
     const uint32_t cw_words = 1u + cw_rw + ((uint32_t)max_len + 1u + cw_sb + 3u) / 4u;
+    // The LDS rows grow with the read (100 bp: 208 B per lane, 3 workgroups of 256 lanes per CU); longer
+    // reads take the workgroup size that keeps the most waves per CU (150 bp: 9 of 64 lanes) as long
+    // as that is at least gap_lw_min_waves
+    int lw_block = 256, lw_waves = 0;
+    for (int blk : {256, 128, 64}) {
+      const size_t b = gapped_lds_bytes(o.n_stacks, blk, false, max_pages, ppb_of(blk), 64, 0, (int)cw_words);
+      if (b > 65536) continue;
+      const int waves = std::min<int>(c->gap_blocks_per_cu * 4, (int)(160 * 1024 / b) * (blk / 64));
+      if (waves > lw_waves) lw_waves = waves, lw_block = blk;
+    }
     const bool lw = c->gap_lw && !c->diag && batch_md <= 6 && o.max_seed_diff >= 0 && o.max_seed_diff <= 2 && maxpen <= 15 &&
-                    max_pages <= GAP_MAX_PAGES &&
-                    gapped_lds_bytes(o.n_stacks, 256, false, max_pages, ppb_of(256), 64, 0, (int)cw_words) * 3 <=
-                        160 * 1024;
+                    max_pages <= GAP_MAX_PAGES && lw_waves >= c->gap_lw_min_waves;
     auto lds_of = [&](int blk) {
       return gapped_lds_bytes(o.n_stacks, blk, false, max_pages, ppb_of(blk), 64, 0, lw ? (int)cw_words : 0);
     };
-    const int block = lds_of(256) <= 65536 ? 256 : lds_of(128) <= 65536 ? 128 : 64;
+    const int block = lw ? lw_block : lds_of(256) <= 65536 ? 256 : lds_of(128) <= 65536 ? 128 : 64;
     const int ppb = ppb_of(block);
     const size_t lds = lds_of(block);
     const int per_cu = std::max<int>(

@@ -195,8 +195,8 @@ size_t gapped_lds_bytes(int n_stacks, int block, bool wide, int max_pages, int p
 // the same kernel): 0 claim, 1 pop, 2 wait for the loads, 3 rest; then wave-level event
 // counts (the wave executes a block once for all its lanes in it): 4 exact steps, 5 push-loop
 // trips, 6 hit blocks, 7 read ends, 8 expansions, 9 wave iterations, 10 read claims.
-template <bool WIDE, bool PROF, bool LW>
-__global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *counter) {
+template <bool WIDE, bool PROF, bool LW, int NBL>
+__device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long *counter) {
   static_assert(!(WIDE && LW), "the LDS-width variant is a first-pass kernel");
   using E = Ent<WIDE>;
   using H = typename E::Head;
@@ -208,8 +208,10 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   const int NB = blockDim.x;
   // LDS lanes: the lanes that run reads; LDS index (x << nbl) + ltid (powers of two)
-  const int LNB = (NB >> 6) * A.lanes_per_wave;
-  const int nbl = 31 - __builtin_clz(LNB);
+  // NBL > 0: log2 of the LDS lanes known at compile time (the LW first pass, one instantiation per
+  // workgroup size), so a row's LDS address is the lane's plus an immediate offset
+  const int LNB = NBL ? (1 << NBL) : (NB >> 6) * A.lanes_per_wave;
+  const int nbl = NBL ? NBL : 31 - __builtin_clz(LNB);
   const int ltid = (tid >> 6) * A.lanes_per_wave + (lane < A.lanes_per_wave ? lane : 0);
   const AlnOpt o = A.o;
   H *const lds_heads = reinterpret_cast<H *>(lds_raw);
@@ -710,11 +712,11 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
     pf1 += t_issue - t_pop;
     // ------------------------------------------------ issue every load of this iteration
     const bool srch = do_pop && m >= 0;
-    const IndexView ix = a ? ixv0 : ixv1;  // strand a searches bwt[1-a]
+    // strand a searches bwt[1-a]; the two BWTs have the same L2 and length (a text and its reverse,
+    // checked at launch), so those are uniform: no per-lane select of an IndexView
     const uint4 *ob = a ? A.o64[0] : A.o64[1];
     uint32_t k = e.x, l = e.y;
     // exact lanes query (xk-1, xl) on bwt[1-xa]
-    const IndexView ixq = st == 2 ? (xa ? ixv0 : ixv1) : ix;
     const uint4 *obq = st == 2 ? (xa ? A.o64[0] : A.o64[1]) : ob;
     const uint32_t qk = st == 2 ? xk : k, ql = st == 2 ? xl : l;
     const bool qrun = (srch && i > 0) || (st == 2 && xj >= 0) || do_mat;
@@ -823,8 +825,8 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
                                            occ_of(qshare ? bl.v1 : bk.v1, qk - 1),
                                            occ_of(qshare ? bl.v2 : bk.v2, qk - 1),
                                            occ_of(qshare ? bl.v3 : bk.v3, qk - 1));
-      KK = make_uint4(ixq.L2[0] + ck4.x + 1, ixq.L2[1] + ck4.y + 1, ixq.L2[2] + ck4.z + 1, ixq.L2[3] + ck4.w + 1);
-      LL = make_uint4(ixq.L2[0] + cl4.x, ixq.L2[1] + cl4.y, ixq.L2[2] + cl4.z, ixq.L2[3] + cl4.w);
+      KK = make_uint4(ixv0.L2[0] + ck4.x + 1, ixv0.L2[1] + ck4.y + 1, ixv0.L2[2] + ck4.z + 1, ixv0.L2[3] + ck4.w + 1);
+      LL = make_uint4(ixv0.L2[0] + cl4.x, ixv0.L2[1] + cl4.y, ixv0.L2[2] + cl4.z, ixv0.L2[3] + cl4.w);
     }
 
     if (st == 2) {
@@ -1157,7 +1159,7 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
       // (8 positions per round trip: a load-modify-store per position would cost one HBM
       // round trip each, and a wave waits for its longest lane)
       uint2 *width = const_cast<uint2 *>(a ? W1 : W0);
-      const uint32_t x = l - k + 1, mx = ix.seq_len;
+      const uint32_t x = l - k + 1, mx = ixv0.seq_len;
       uint32_t jj = 0;
       // LW: the LDS nibbles of strand a follow -- bid (clamped) of every changed position and the
       // "equals the previous width" bit of positions 1..ldp
@@ -1210,24 +1212,46 @@ __global__ void __launch_bounds__(256) k_gapped(GapArgs A, unsigned long long *c
   }
 }
 
+// The search kernels hold 3 waves per SIMD (<= 168 VGPRs; the register allocator otherwise drifts
+// a few registers past it); the PROF diagnostics build keeps its own allocation.
+template <bool WIDE, bool LW, int NBL = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_gapped(GapArgs A, unsigned long long *counter) {
+  gapped_body<WIDE, false, LW, NBL>(A, counter);
+}
+template <bool WIDE, bool LW, int NBL = 0>
+__global__ void __launch_bounds__(256) k_gapped_prof(GapArgs A, unsigned long long *counter) {
+  gapped_body<WIDE, true, LW, NBL>(A, counter);
+}
+
 hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int blocks, int block, bool wide,
                          hipStream_t st) {
   if (g.n <= 0) return hipSuccess;
+  for (int c = 0; c < 5; ++c)  // the kernel takes L2 and seq_len from ix[0] for both strands
+    if (g.ix[0].L2[c] != g.ix[1].L2[c]) return hipErrorInvalidValue;
+  if (g.ix[0].seq_len != g.ix[1].seq_len) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
   const bool lw = !wide && g.cw != nullptr;
   const size_t lds = gapped_lds_bytes(g.o.n_stacks, block, wide, g.max_pages, g.pages_per_block, g.lanes_per_wave,
                                       g.free_depth, lw ? (int)g.cw_words : 0);
   if (wide)
-    hipLaunchKernelGGL((k_gapped<true, false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<true, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+  else if (lw && g.lanes_per_wave != 64)
+    return hipErrorInvalidValue;  // the LW first pass runs 64 reads per wave
   else if (lw && g.prof)
-    hipLaunchKernelGGL((k_gapped<false, true, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped_prof<false, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+  else if (lw && block == 256)
+    hipLaunchKernelGGL((k_gapped<false, true, 8>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+  else if (lw && block == 128)
+    hipLaunchKernelGGL((k_gapped<false, true, 7>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+  else if (lw && block == 64)
+    hipLaunchKernelGGL((k_gapped<false, true, 6>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   else if (lw)
-    hipLaunchKernelGGL((k_gapped<false, false, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<false, true>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   else if (g.prof)
-    hipLaunchKernelGGL((k_gapped<false, true, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped_prof<false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   else
-    hipLaunchKernelGGL((k_gapped<false, false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
+    hipLaunchKernelGGL((k_gapped<false, false>), dim3(blocks), dim3(block), lds, st, g, d_counter);
   return hipGetLastError();
 }
 

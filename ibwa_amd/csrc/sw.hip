@@ -7,7 +7,7 @@
 // One alignment per lane, persistent grid with per-wave claiming.  The forward
 // pass and the global fill are strip-mined (a strip's columns of the row above in
 // registers, one boundary per row through scratch); the reverse pass walks its
-// lane-major eh row by aligned 16-word blocks; all three are branch free per cell.
+// lane-major eh row by aligned 32-word blocks (whole 128 B lines); all three are branch free per cell.
 // Scratch that the lanes touch in step (strip boundaries, packed reference codes,
 // traceback bytes) is interleaved lane-minor inside each wave, so a wave's access
 // is one contiguous segment.  The passes are integer VALU work (roofline: VALU,
@@ -29,8 +29,14 @@ constexpr int STRIP = 32;  // forward-pass columns held in registers
 constexpr int GS = 16;      // global-fill columns held in registers (strip width; 32: 296 VGPRs)
 // traceback bytes per row: whole strips, so a strip's junk columns past len1 stay in their row
 __host__ __device__ inline uint32_t sw_tb_width(int max_len1) { return (uint32_t)((max_len1 + GS) / GS * GS); }
-// the reverse pass's eh row per lane: eh[0 .. l1+1] in whole 64 B blocks (its 16-word block accesses)
-__host__ __device__ inline uint32_t sw_eh_words(int max_len1) { return (uint32_t)((max_len1 + 2 + 15) / 16 * 16); }
+// the reverse pass walks its eh row by aligned blocks of RB words (16: 64 B, 32: whole 128 B lines)
+#ifndef IBWA_SW_RB
+#define IBWA_SW_RB 32
+#endif
+constexpr int RB = IBWA_SW_RB;
+static_assert(RB == 16 || RB == 32, "reverse-pass block of 16 or 32 words");
+// the reverse pass's eh row per lane: eh[0 .. l1+1] in whole blocks
+__host__ __device__ inline uint32_t sw_eh_words(int max_len1) { return (uint32_t)((max_len1 + 2 + RB - 1) / RB * RB); }
 constexpr int NEG_INF = -1073741823;  // MINOR_INF (stdaln.h:84)
 constexpr int FM = 0, FI = 1, FD = 2;  // FROM_M / FROM_I / FROM_D
 
@@ -391,32 +397,37 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
           int last_h = 0, f = 0, i = start;
           bool found = false;
           int nxt = (int)L.v(eEH + i + 1);  // eh[i+1] of the row below (old value)
-          // cells start, start-1, ..., end+1 (start > end >= 0 always) by aligned 16-word blocks of
-          // the eh row: block q = eh[16q .. 16q+15] is loaded (4 x 16 B) before its cells are
-          // updated (a cell writes eh[i+1] only, and cells go down, so every loaded value is still
-          // the row below's) and stored back whole: cells outside [end+1, i], or after the start
-          // was found, keep their word; cell 16q+15 writes the next block's first word.  The
-          // block's reference codes are three packed words of the forward pass's eREF.
+          // cells start, start-1, ..., end+1 (start > end >= 0 always) by aligned RB-word blocks of
+          // the eh row: block q = eh[RB q .. RB q + RB-1] is loaded (RB / 4 x 16 B) before its cells
+          // are updated (a cell writes eh[i+1] only, and cells go down, so every loaded value is
+          // still the row below's) and stored back whole: cells outside [end+1, i], or after the
+          // start was found, keep their word; cell RB q + RB-1 writes the next block's first word.
+          // The block's reference codes are packed words of the forward pass's eREF (8 per word:
+          // cell RB q + m reads a[RB q + m - 1]).
+          constexpr int RW = RB / 8;  // eREF words per block
           while (i > end && !found) {
-            const int q = i >> 4;
-            int blk[16];
+            const int q = i / RB;
+            int blk[RB];
 #pragma unroll
-            for (int x = 0; x < 4; ++x) {
-              const uint4 v = L.v4((uint32_t)q * 4 + x);
+            for (int x = 0; x < RB / 4; ++x) {
+              const uint4 v = L.v4((uint32_t)q * (RB / 4) + x);
               blk[4 * x] = (int)v.x; blk[4 * x + 1] = (int)v.y; blk[4 * x + 2] = (int)v.z; blk[4 * x + 3] = (int)v.w;
             }
-            const uint32_t r0 = q > 0 ? L.u(eREF + 2 * q - 1) : 0u, r1 = L.u(eREF + 2 * q), r2 = L.u(eREF + 2 * q + 1);
-            uint32_t out[16];
+            const uint32_t r0 = q > 0 ? L.u(eREF + RW * q - 1) : 0u;
+            uint32_t rw[RW];
+#pragma unroll
+            for (int x = 0; x < RW; ++x) rw[x] = L.u(eREF + RW * q + x);
+            uint32_t out[RB];
             out[0] = (uint32_t)blk[0];
             uint32_t top = 0;
             bool top_act = false;
             int ii = i;
 #pragma unroll
-            for (int m = 15; m >= 0; --m) {
-              const int ik = 16 * q + m;
+            for (int m = RB - 1; m >= 0; --m) {
+              const int ik = RB * q + m;
               const bool act = ik <= i && ik > end && !found;
-              const int nx = m == 15 ? nxt : blk[m + 1];
-              const uint32_t code = m == 0 ? r0 >> 28 : m <= 8 ? (r1 >> (4 * (m - 1))) & 15u : (r2 >> (4 * (m - 9))) & 15u;
+              const int nx = m == RB - 1 ? nxt : blk[m + 1];
+              const uint32_t code = m == 0 ? r0 >> 28 : (rw[(m - 1) >> 3] >> (4 * ((m - 1) & 7))) & 15u;
               const uint32_t ca = (code < 4u ? code : 4u) * 6u;
               const int hd = (nx >> 16) + (int)__builtin_amdgcn_ubfe(rp, ca, 6) - 32;
               const int fn = max(f - R, last_h - QR);
@@ -426,7 +437,7 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
               const int e = max(max(e_old - R, above - QR), 0);
               const int h = max(max(hd, fm), e);  // >= 0: e is
               const uint32_t val = (uint32_t)last_h << 16 | (uint32_t)e;
-              if (m < 15) {
+              if (m < RB - 1) {
                 out[m + 1] = act ? val : (uint32_t)blk[m + 1];
               } else {
                 top = val;
@@ -446,9 +457,9 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
               if (act && !found) ii = ik - 1;
             }
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
-              L.v4((uint32_t)q * 4 + x) = make_uint4(out[4 * x], out[4 * x + 1], out[4 * x + 2], out[4 * x + 3]);
-            if (top_act) L.v(eEH + (uint32_t)(16 * q + 16)) = top;
+            for (int x = 0; x < RB / 4; ++x)
+              L.v4((uint32_t)q * (RB / 4) + x) = make_uint4(out[4 * x], out[4 * x + 1], out[4 * x + 2], out[4 * x + 3]);
+            if (top_act) L.v(eEH + (uint32_t)(RB * q + RB)) = top;
             nxt = blk[0];
             i = ii;
           }

@@ -192,6 +192,9 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "gap_cap1", "gap_pages_per_block", "gap_hit_slots", "gap_blocks_per_cu", "gap_reads_per_chunk"
  *                                  its per-lane static slots, 128 KiB pages per workgroup pool,
  *                                  first-pass hit slots, residency and batch slice size
+ *   "gap_lw" (0/1, default 1), "gap_lw_min_waves" (8)  first pass with its width records in LDS
+ *                                  (and resume states), in the workgroup size that keeps the most
+ *                                  waves per CU (100 bp: 12, 150 bp: 9) when that is at least the minimum
  *   "gap_iter_budget" (8000)       first-pass iterations before a read goes to the cooperative pass
  *   "gap_early_iters", "gap_early_entries" (3000, 1000)
  *                                  earlier hand-off of a read whose stack holds that many entries

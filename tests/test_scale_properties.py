@@ -87,6 +87,7 @@ def test_exact_reads_round_trip(mid_genome):
 @pytest.mark.parametrize("argv,ln,sub,n,tune", [
     ([], 100, 0.01, 30_000, {}), (["-n", "0"], 100, 0.01, 100_000, {}),
     ([], 150, 0.02, 8_000, {}), (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {}),
+    ([], 150, 0.02, 8_000, {"gap_lw_min_waves": 12}),  # 150 bp through the first pass without LDS widths
     # small static regions: many reads take pages from their workgroup pool, some exhaust it
     ([], 100, 0.02, 20_000, {"gap_cap1": 256, "gap_pages_per_block": 2}),
     (["-n", "0"], 100, 0.01, 20_000, {"exact_path": 0}),
@@ -126,6 +127,10 @@ def test_exact_reads_round_trip(mid_genome):
     ([], 100, 0.02, 20_000, {"gap_resume_iters": 100, "gap_resume_entries": 50, "gap_cap1": 256,
                              "gap_pages_per_block": 8}),
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_resume_records": 20_000}),
+    # 150 bp (and 120 bp) reads: the LDS-width first pass in 64-lane workgroups, with resume states
+    ([], 150, 0.02, 8_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
+    ([], 120, 0.02, 8_000, {"gap_resume_iters": 40, "gap_resume_entries": 8}),
+    (["-n", "3", "-o", "2", "-e", "3"], 150, 0.02, 4_000, {"gap_resume_iters": 20, "gap_resume_entries": 4}),
     # every read past 5 iterations in the launch's tail (here: from the start) leaves its state
     ([], 100, 0.01, 30_000, {"gap_tail_lanes": 64, "gap_tail_iters": 5}),
     (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_tail_lanes": 64, "gap_tail_iters": 1}),
@@ -139,7 +144,8 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
-                "gap_resume_entries": 300, "coop_pool_gb": 16, "gap_tail_lanes": 16, "gap_tail_iters": 200}
+                "gap_resume_entries": 300, "coop_pool_gb": 16, "gap_tail_lanes": 16, "gap_tail_iters": 200,
+                "gap_lw_min_waves": 8}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)

@@ -93,6 +93,15 @@ def run(argv, timeout=1800, env=None):
         if "wall s:" in ln:
             for name, v in re.findall(r"([a-z][a-z .()]*?) (\d+\.\d+)", ln.split("wall s:", 1)[1]):
                 phases[name.strip()] = float(v)
+        m = re.search(r"parse only: (\d+) reads, ([\d.]+) s parsing", ln)
+        if m:
+            log("  cli:", ln.strip())
+            phases["parse only"] = {"reads": int(m.group(1)), "parse_s": float(m.group(2)),
+                                    "reads_per_s": int(m.group(1)) / max(float(m.group(2)), 1e-9)}
+        m = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s waiting for the parse \((\d+) ms of device", ln)
+        if m:
+            log("  cli:", ln.strip())
+            phases["gpu parse"] = {"records": int(m.group(1)), "wait_s": float(m.group(2)), "device_ms": int(m.group(3))}
         m = re.search(r"input parse: (\d+) reads in ([\d.]+) s on (\d+) host threads", ln)
         if m:
             log("  cli:", ln.strip())
@@ -138,6 +147,9 @@ def main():
     ap.add_argument("--ref-sample", type=int, default=200_000, help="reads the reference binary aligns (0: skip)")
     ap.add_argument("--threads", type=int, default=bench.host_threads())
     ap.add_argument("--lanes", default="2", help="IBWA_ALN_LANES values to run (overlapped groups), e.g. 2,1")
+    ap.add_argument("--parse", default="dev,host", help="input parse modes to time alone first (IBWA_ALN_PARSE_ONLY): "
+                                                        "dev = on the GPU (default path), host = IBWA_ALN_GPU_PARSE=0")
+    ap.add_argument("--host-parse-run", type=int, default=1, help="also align with the host parse and compare the .sai")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
@@ -169,6 +181,12 @@ def main():
             del reads
             log(f"{name}: {a.reads} reads written in {time.perf_counter() - t:.1f} s")
             sai = os.path.join(tmp, f"c{cid}.sai")
+            parse = {}
+            for mode in [x for x in a.parse.split(",") if x]:
+                env = {"IBWA_ALN_PARSE_ONLY": "1", "IBWA_ALN_GPU_PARSE": "1" if mode == "dev" else "0"}
+                wall, ph = run([CLI, "aln"] + opts + ["-f", os.path.join(tmp, "p.sai"), P, fq], env=env)
+                parse[mode] = {"wall_s": wall, "phases_s": ph, **ph.get("parse only", {})}
+                log(f"{name}: parse only ({mode}): {parse[mode]}")
             c = None
             for li, lanes in enumerate(int(x) for x in a.lanes.split(",")):
                 out_sai = sai if li == 0 else os.path.join(tmp, f"c{cid}_l{lanes}.sai")
@@ -189,6 +207,16 @@ def main():
                     log(f"{name}: lanes {lanes} .sai equal to lanes {c['lanes']}: {r_['sai_equal_first_run']}")
                     os.unlink(out_sai)
                 c["runs"].append(r_)
+            c["parse_only"] = parse
+            if a.host_parse_run:
+                hsai = os.path.join(tmp, f"c{cid}_h.sai")
+                wall, ph = run([CLI, "aln"] + opts + ["-f", hsai, P, fq], env={"IBWA_ALN_GPU_PARSE": "0"})
+                load = ph.get("load index", 0.0)
+                c["host_parse"] = {"wall_s": wall, "phases_s": ph, "reads_per_s_excl_index_load": a.reads / max(wall - load, 1e-9),
+                                   "sai_equal_gpu_parse": open(hsai, "rb").read() == open(sai, "rb").read()}
+                log(f"{name}: host parse: {wall:.1f} s wall -> {c['host_parse']['reads_per_s_excl_index_load']:.0f} reads/s "
+                    f"excl. index load; .sai equal to the GPU parse's: {c['host_parse']['sai_equal_gpu_parse']}")
+                os.unlink(hsai)
             t = time.perf_counter()
             c["parity_first_reads"] = a.check
             c["parity_ok"] = bool(oracle_check(P, cfq, sai, opts, a.check))
