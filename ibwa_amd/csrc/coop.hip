@@ -103,25 +103,33 @@ __device__ __forceinline__ uint32_t pick4(uint4 v, uint32_t c) {
 
 __device__ __forceinline__ int int_log2(uint32_t v) { return v ? 31 - __builtin_clz(v) : 0; }
 
-// wave-wide exclusive prefix sum and total (64 lanes)
+// wave-wide exclusive prefix sum and total (64 lanes, all active): DPP row shifts within the rows
+// of 16 lanes, then the row broadcasts of lanes 15 and 31 -- six VALU steps instead of six
+// ds_bpermute round trips through the LDS crossbar
 __device__ __forceinline__ uint32_t wave_excl(uint32_t v, int lane, uint32_t &total) {
+  (void)lane;
   uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
-  total = __shfl(x, 63);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   return x - v;
 }
 
+// wave-wide minimum (64 lanes, all active), the same DPP steps as wave_excl; lane 63 ends with it
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t y = __shfl_xor(v, d);
-    v = y < v ? y : v;
-  }
-  return v;
+  const int NO = -1;  // 0xFFFFFFFF: the identity for lanes with no source
+  auto mn = [](uint32_t a, int b) __attribute__((always_inline)) { return a < (uint32_t)b ? a : (uint32_t)b; };
+  v = mn(v, __builtin_amdgcn_update_dpp(NO, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = mn(v, __builtin_amdgcn_update_dpp(NO, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = mn(v, __builtin_amdgcn_update_dpp(NO, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = mn(v, __builtin_amdgcn_update_dpp(NO, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = mn(v, __builtin_amdgcn_update_dpp(NO, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = mn(v, __builtin_amdgcn_update_dpp(NO, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // entry (uint4): {k, l, i | ldp << 10 | rank << 20, n_mm | n_gapo << 8 | n_gape << 16 | a << 24 | state << 25
