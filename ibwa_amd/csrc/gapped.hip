@@ -1040,13 +1040,20 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
           }
         };
         uint32_t t = 0;
+        // the three target buckets' heads, read together (one LDS wait, not one per group); the
+        // gap and mismatch buckets coincide when their penalties do, the match child's never does
+        const uint32_t vg = vm & 0x1Fu & ~(dmask << 1);  // with a gap group: the group entry alone
+        const uint32_t vmm = vm & vm_mm;
+        const bool has_match_ch = has_match && vm;
+        const uint32_t hG = vg ? (uint32_t)lds_heads[hidx(scG)] : 0u;
+        uint32_t hM = vmm ? (uint32_t)lds_heads[hidx(scMM)] : 0u;
+        const uint32_t hB = has_match_ch ? (uint32_t)lds_heads[hidx(sc_base)] : 0u;
         // ---- gap children (bit 0 insertion, bits 1-4 deletion by A..T): bucket scG, stored in order,
         // each linked to the one before
-        const uint32_t vg = vm & 0x1Fu & ~(dmask << 1);  // with a gap group: the group entry alone
         if (vg) {
           if (pleader()) ++pf5;
           const bool tk = !C_valid || scG <= C_b;
-          uint32_t link = (uint32_t)lds_heads[hidx(scG)];
+          uint32_t link = hG;
           const int n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (open ? 0 : 1);
           uint4 last = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -1065,13 +1072,13 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
           }
           lds_heads[hidx(scG)] = (H)link;
           group_take(tk, last, link, scG);
+          if (scMM == scG) hM = link;
         }
         // ---- mismatch children (bits 5-8 but the match child): bucket scMM
-        const uint32_t vmm = vm & vm_mm;
         if (vmm) {
           if (pleader()) ++pf5;
           const bool tk = !C_valid || scMM <= C_b;
-          uint32_t link = (uint32_t)lds_heads[hidx(scMM)];
+          uint32_t link = hM;
           uint4 last = make_uint4(0, 0, 0, 0);
 #pragma unroll
           for (int j = 5; j < 9; ++j) {
@@ -1088,9 +1095,9 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
         }
         // ---- the match child (bucket sc_base <= C_b: always the new candidate): kept in C, not
         // stored; C moves to D, the old D is stored if memory lacks it
-        if (has_match && vm) {
+        if (has_match_ch) {
           const uint32_t slot = slot_at(t++);
-          const uint32_t hd = (uint32_t)lds_heads[hidx(sc_base)];
+          const uint32_t hd = hB;
           const uint4 ne = E::make(pick4(KK, csym), pick4(LL, csym), ni, ldp, hd, e_mm, e_go, e_ge, a, STATE_M);
           lds_heads[hidx(sc_base)] = (H)slot;
           if ((cfl & 6u) == 6u) *slot_ptr(D_slot) = D;

@@ -165,6 +165,9 @@ class FastqGpu {
     const bool eof = next_off_ >= fsize_;
     char *const base = buf_[cur_] + carry_ - tail_;
     const uint64_t n = tail_ + got;
+    // the next chunk is read into the other buffer, behind its carry room, while this region is
+    // parsed and aligned (that buffer's previous region went to the GPUs with its parse)
+    if (!eof) start_read(cur_ ^ 1);
     groups_.clear();
     gi_ = 0;
     if (n == 0) return END;
@@ -329,7 +332,6 @@ class FastqGpu {
     memcpy(buf_[nb] + carry_ - carry, base + rewind, carry);
     tail_ = carry;
     tail_file_off_ = file_rewind;
-    start_read(nb);
     cur_ = nb;
     return NEXT;
   }
