@@ -478,6 +478,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reads", type=int, default=50_000_000, help="reads per GPU")
     ap.add_argument("--read-len", type=int, default=100)
+    ap.add_argument("--sub", type=float, default=0.01, help="substitution rate of the synthetic reads "
+                                                           "(configs[4]'s 2 x 150 bp: 0.02)")
+    ap.add_argument("--indel", type=float, default=0.05, help="fraction of reads with one 1-3 bp indel")
     ap.add_argument("--scale", type=float, default=1.0, help="genome size as a fraction of GRCh37")
     ap.add_argument("--aln", default="", help="aln options (reference syntax); default: gap_init_opt's")
     ap.add_argument("--seed", type=int, default=3, help="reads seed (SURVEY §8d: configs[2] = 3)")
@@ -529,7 +532,7 @@ def main():
     log(f"genome {codes.size/1e9:.3f} Gbp ({n_amb} N->random), {time.perf_counter()-tg:.1f} s")
     tr = time.perf_counter()
     keep = 1_000_000 if world == 1 and rank == 0 and not args.no_cpu and args.ref_budget > 0 else 0
-    parts = [make_reads(ascii_, lens, shard_seed(r, args.seed), args.reads, args.read_len, 0.01, 0.05, threads,
+    parts = [make_reads(ascii_, lens, shard_seed(r, args.seed), args.reads, args.read_len, args.sub, args.indel, threads,
                         keep_raw=keep if j == 0 else 0)
              for j, r in enumerate([rank] if world > 1 else range(max(1, args.shards)))]
     raw_sample = None
@@ -606,15 +609,20 @@ def main():
     path = stl.path
     exact_cfg = opt.max_diff == 0 and opt.fnr <= 0
     cfg_name = "configs[1]" if exact_cfg else "configs[2]" if world == 1 else "configs[3]"
+    if args.read_len == 150 and not exact_cfg:
+        cfg_name = "configs[4] aln shape"  # one end of 2 x 150 bp pairs
+    reads_desc = "" if (args.sub, args.indel) == (0.01, 0.05) else \
+        f" ({args.sub:.0%} substitutions, {args.indel:.0%} with a 1-3 bp indel)"
     result = {
         "metric": "reads/s `ibwa aln` GRCh37-sized 100bp, achieved HBM GB/s vs peak",
         "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic",
         "config": {"workload": f"{cfg_name}: GRCh37-sized synthetic genome ({sum(lens)/1e9:.2f} Gbp, index built on "
-                               f"device), {args.reads} x {args.read_len} bp SE reads per GPU, aln "
+                               f"device), {args.reads} x {args.read_len} bp SE reads per GPU{reads_desc}, aln "
                                f"{args.aln or 'defaults (-n 0.04 -o 1)'}",
-                   "reads_per_gpu": args.reads, "read_len": args.read_len, "aln_options": args.aln or "defaults",
+                   "reads_per_gpu": args.reads, "read_len": args.read_len, "substitution_rate": args.sub,
+                   "indel_read_fraction": args.indel, "aln_options": args.aln or "defaults",
                    "parallelism": f"replicated index, reads sharded x{world}"},
     }
     if rank == 0:

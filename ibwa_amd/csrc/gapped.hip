@@ -246,7 +246,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     bitmap[w] = hi - lo >= 32 ? 0u : ~((1u << (hi - lo)) - 1u);  // bits past the pool stay taken
   }
   __syncthreads();
-  const IndexView ixv0 = A.ix[0], ixv1 = A.ix[1];
+  const IndexView ixv0 = A.ix[0];  // L2 and seq_len of both strands (checked at launch)
   const bool comp = o.mode & MODE_COMPREAD;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + tid;
   const uint32_t P0 = A.cap1;                  // static slots per lane

@@ -63,9 +63,11 @@ class FastqGpu {
     fd_ = open(fn, O_RDONLY);
     struct stat st;
     fsize_ = fd_ >= 0 && fstat(fd_, &st) == 0 ? (uint64_t)st.st_size : 0;
+    // pinned buffers no larger than the file needs (a small input must not pin GBs)
+    const uint64_t fs = std::max<uint64_t>((fsize_ + 4095) / 4096 * 4096, 4096);
     piece_ = std::max<uint64_t>(piece_bytes, 4096);
-    carry_ = std::max<uint64_t>(carry_bytes, 4096);
-    chunk_ = piece_ * ing_.size();
+    carry_ = std::min<uint64_t>(std::max<uint64_t>(carry_bytes, 4096), fs);
+    chunk_ = std::min<uint64_t>(piece_ * ing_.size(), fs);
     for (auto &b : buf_) {
       void *p = nullptr;
       if (ibwa_host_alloc(carry_ + chunk_ + 64, &p)) { ok_ = false; return; }
