@@ -416,7 +416,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   bool has_carry = false;
   bool eof = false;
   double parse_s = 0;  // wall time of the FASTQ parse (all host threads, or waiting for the GPUs')
-  bool dev_active = fg != nullptr;
+  bool dev_active = fg != nullptr, dev_done = false;
   auto key_of = [&](int max_len) { return batch_key(opt, max_len); };
   auto timed_read = [&](Group &into) {
     const auto t = std::chrono::steady_clock::now();
@@ -433,11 +433,11 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
                   (unsigned long long)fg->handoff_offset());
           if (gzseek(rd.fp, (z_off_t)fg->handoff_offset(), SEEK_SET) < 0) r = -1;
         } else {
-          eof = true;
+          dev_done = true;  // the input ended on the GPU path
         }
       }
     }
-    if (!into.dev && r == 0) r = read_group(rd, fb, opt, into.b, sub, carry, has_carry, &eof);
+    if (!into.dev && r == 0 && !dev_done) r = read_group(rd, fb, opt, into.b, sub, carry, has_carry, &eof);
     parse_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
     return r;
   };
