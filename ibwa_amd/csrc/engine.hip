@@ -983,6 +983,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   if (int rc = check_opt(opt)) return rc;
   HIPCHK(hipSetDevice(c->device));
   memset(&c->stats, 0, sizeof(c->stats));
+  c->hpop_valid = false;  // set again by a gapped run that leaves resume states
   const int64_t n = c->n;
   const int max_len = std::max(batch_max_len, c->max_len);
 
@@ -1885,7 +1886,7 @@ int ibwa_batch_diag(const ibwa_ctx_t *c, int what, void *out, uint64_t cap_bytes
   if (what == 2) {
     const uint64_t need2 = (uint64_t)c->n * 4;
     if (cap_bytes < need2) return fail(IBWA_EINVAL, "diag buffer too small");
-    if (!c->hpop_valid) {  // no resume states in the last run
+    if (!c->hpop_valid || c->d_hpop.cap < need2) {  // no resume states in the last run
       memset(out, 0, need2);
       return 0;
     }
