@@ -1070,6 +1070,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->patch_ids.clear();
     c->patch_alns.clear();
     c->retry_pass.clear();
+    c->resumed_ids.clear();
     c->stats.ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return 0;
