@@ -601,6 +601,7 @@ def main():
     free_b, total_b = ctypes.c_size_t(0), ctypes.c_size_t(0)
     hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b))
     dev_mem_gb = (total_b.value - free_b.value) / 1e9
+    lib_now, lib_peak = E.Engine.device_bytes()
     total_reads = args.reads * world * args.steps
     value = total_reads / dt
     ms_step = dt * 1e3 / args.steps
@@ -635,8 +636,14 @@ def main():
                                         "k_coop": (ms_c - ms_cw - ms_cr) / launches,
                                         "wide+general retry": (ms_r - ms_c) / launches},
                  "device_memory_gb": {"in_use_after_steps": dev_mem_gb, "total": total_b.value / 1e9,
+                                      "library_buffers": lib_now / 1e9, "library_peak": lib_peak / 1e9,
                                       "note": "hipMemGetInfo after the timed steps: index + tables + one context's "
-                                              "search buffers (sized for this batch)"},
+                                              "search buffers (sized for this batch); library_*: the engine's own "
+                                              "device buffers now and at their high-water mark (ibwa_device_bytes)"},
+                 "buffer_use": {"resume_records_peak": int(stl.resume_records_peak),
+                                "resume_records_cap": int(stl.resume_records_cap),
+                                "resume_records_per_step": int(stl.resume_records), "n_resumed": int(stl.n_resumed),
+                                "coop_pages_peak": int(stl.coop_pages_peak), "coop_pages_cap": int(stl.coop_pages_cap)},
                  "host_cores": threads, "cpu_model": cpu_model(),
                  # digest of the sources libibwa_amd.so was built from (checked against this tree on load)
                  "build_id": E.lib().ibwa_build_id().decode()}

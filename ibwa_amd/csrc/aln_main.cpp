@@ -612,11 +612,15 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     return 1;
   }
   if (out != stdout) fclose(out);
+  int64_t dev_now = 0, dev_peak = 0;
+  ibwa_device_bytes(&dev_now, &dev_peak);
   for (int l = n_lanes - 1; l >= 1; --l)  // lanes sharing the index first
     for (auto *x : lctx[l]) ibwa_ctx_destroy(x);
   for (auto *x : ctx) ibwa_ctx_destroy(x);
   if (have < 0) return 1;
   ph.print("ibwa-amd aln");
+  fprintf(stderr, "[ibwa-amd aln] device memory: peak %.1f GB of engine buffers on %d GPU(s) (%d context(s) per GPU, "
+                  "index shared)\n", dev_peak / 1e9, n_gpus, n_lanes);
   if (fg) {
     fprintf(stderr, "[ibwa-amd aln] input parsed on the GPUs: %lld records, %.2f s waiting for the parse (%.0f ms of device "
                     "time: H2D copies + kernels)%s\n",

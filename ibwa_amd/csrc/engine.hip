@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <chrono>
 #include <string>
@@ -41,6 +42,15 @@ int fail(int code, const char *fmt, ...) {
     if (e_ != hipSuccess) return fail(IBWA_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
   } while (0)
 
+// Device bytes the library's buffers hold (all contexts of the process) and their high-water mark.
+std::atomic<int64_t> g_dev_bytes{0}, g_dev_peak{0};
+void dev_bytes_add(int64_t d) {
+  const int64_t now = g_dev_bytes.fetch_add(d) + d;
+  int64_t pk = g_dev_peak.load();
+  while (now > pk && !g_dev_peak.compare_exchange_weak(pk, now)) {
+  }
+}
+
 // A growable device buffer.
 struct DBuf {
   void *p = nullptr;
@@ -49,7 +59,10 @@ struct DBuf {
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     if (borrowed) return fail(IBWA_EINVAL, "a shared index buffer cannot grow (%zu > %zu bytes)", bytes, cap);
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipFree(p);
+      dev_bytes_add(-(int64_t)cap);
+    }
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 256);
@@ -60,10 +73,14 @@ struct DBuf {
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (verbose && ms > 20.0) fprintf(stderr, "[ibwa_amd] hipMalloc(%.2f GB) took %.0f ms\n", want / 1e9, ms);
     cap = want;
+    dev_bytes_add((int64_t)want);
     return 0;
   }
   void release() {
-    if (p && !borrowed) (void)hipFree(p);
+    if (p && !borrowed) {
+      (void)hipFree(p);
+      dev_bytes_add(-(int64_t)cap);
+    }
     p = nullptr;
     cap = 0;
     borrowed = false;
@@ -199,6 +216,14 @@ struct ibwa_ctx {
 };
 
 namespace {
+
+// the pages a cooperative launch took from its pool (a bump counter: freed pages go to per-wave lists)
+void note_coop_pages(ibwa_ctx *c, uint32_t pool_pages) {
+  uint32_t used = 0;
+  if (hipMemcpy(&used, c->c_next.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return;
+  c->stats.coop_pages_peak = std::max<int64_t>(c->stats.coop_pages_peak, std::min<uint32_t>(used, pool_pages));
+  c->stats.coop_pages_cap = pool_pages;
+}
 // An operation that would rebuild or replace index structures shared by ibwa_ctx_share_index
 // (borrowed buffers are written in place or cannot grow, and the other context may be aligning).
 int refuse_shared(const ibwa_ctx *c, const char *what) {
@@ -357,6 +382,12 @@ int ibwa_device_count(int *n) {
   hipError_t e = hipGetDeviceCount(&d);
   if (e != hipSuccess) return fail(IBWA_EHIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
   if (n) *n = d;
+  return 0;
+}
+
+int ibwa_device_bytes(int64_t *now, int64_t *peak) {
+  if (now) *now = g_dev_bytes.load();
+  if (peak) *peak = g_dev_peak.load();
   return 0;
 }
 
@@ -1088,6 +1119,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   int64_t res_ok = 0;           // reads they resolved
   c->stats.n_resumed = 0;
   c->stats.resume_records = 0;
+  c->stats.resume_records_peak = c->stats.resume_records_cap = 0;
+  c->stats.coop_pages_peak = c->stats.coop_pages_cap = 0;
   if (v2) {
     if (int rc = ensure_kmer(c)) return rc;
     c->stats.path = 2;
@@ -1145,6 +1178,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       rd_cap = std::min<uint64_t>((uint64_t)c->gap_resume_gb << 30, (uint64_t)chunk * 4096 + (1u << 20)) / 16;
       if (c->gap_resume_records > 0) rd_cap = (uint64_t)c->gap_resume_records;
       if (int rc = c->d_rdump.ensure(rd_cap * 16)) return rc;
+      c->stats.resume_records_cap = (int64_t)rd_cap;
       if (int rc = c->d_roff.ensure(((uint64_t)n + 2) * 8)) return rc;
       HIPCHK(hipMemsetAsync(c->d_roff.p, 0, ((uint64_t)n + 2) * 8, c->stream));
       if (int rc = c->d_hpop.ensure(((uint64_t)n + 1) * 4)) return rc;
@@ -1261,6 +1295,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         HIPCHK(resume_fixup(c->r_status.as<uint32_t>(), ids, lanes, c->d_status.as<uint32_t>(), c->d_roff.as<uint64_t>(),
                             c->stream));
         HIPCHK(hipEventSynchronize(c->ev[4]));
+        note_coop_pages(c, pool_pages);
         float t_all = 0, t_w = 0;
         HIPCHK(hipEventElapsedTime(&t_all, c->ev[3], c->ev[4]));
         HIPCHK(hipEventElapsedTime(&t_w, c->ev[3], c->ev[5]));
@@ -1285,6 +1320,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       unsigned long long used = 0;
       HIPCHK(hipMemcpy(&used, c->d_roff.as<unsigned long long>() + n, 8, hipMemcpyDeviceToHost));
       c->stats.resume_records += (int64_t)used;
+      c->stats.resume_records_peak = std::max<int64_t>(c->stats.resume_records_peak, (int64_t)used);
       HIPCHK(hipMemsetAsync(c->d_roff.as<unsigned long long>() + n, 0, 8, c->stream));
       return 0;
     };
@@ -1616,6 +1652,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[4]));
+    note_coop_pages(c, pool_pages);
     if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop kernel done\n", since());
     if (c->prof_phases) {
       unsigned long long pf[40];

@@ -32,7 +32,9 @@ class RunStats(c.Structure):
                 ("n_stack_overflow", c.c_int64), ("n_aln_overflow", c.c_int64), ("n_heavy", c.c_int64), ("ms_sw", c.c_double),
                 ("n_coop", c.c_int64), ("ms_coop", c.c_double), ("ms_sa2pos", c.c_double),
                 ("sa2pos_full", c.c_int), ("ms_coop_width", c.c_double), ("ms_coop_roots", c.c_double),
-                ("n_resumed", c.c_int64), ("resume_records", c.c_int64)]
+                ("n_resumed", c.c_int64), ("resume_records", c.c_int64),
+                ("resume_records_peak", c.c_int64), ("resume_records_cap", c.c_int64),
+                ("coop_pages_peak", c.c_int64), ("coop_pages_cap", c.c_int64)]
 
 
 class RefSeq(c.Structure):
@@ -77,6 +79,7 @@ CAPI = {
     "ibwa_cal_maxdiff": (_i, [_i, c.c_double, c.c_double]),
     "ibwa_ctx_create": (_i, [_i, c.POINTER(_vp)]),
     "ibwa_device_count": (_i, [c.POINTER(_i)]),
+    "ibwa_device_bytes": (_i, [c.POINTER(c.c_int64), c.POINTER(c.c_int64)]),
     "ibwa_fq_parse": (_i, [_vp, _vp, c.c_uint64, _i, _i, c.POINTER(c.c_int64), c.POINTER(c.c_uint64), c.POINTER(_i),
                            _vp, _vp, c.c_int64]),
     "ibwa_fq_stats": (_i, [_vp, c.POINTER(c.c_int64), c.POINTER(c.c_double)]),
@@ -268,6 +271,13 @@ class Engine:
         hp = np.zeros(self.n, np.uint32)
         _chk(lib().ibwa_batch_diag(self.h, 2, hp.ctypes.data, hp.nbytes))
         return hp
+
+    @staticmethod
+    def device_bytes():
+        """(bytes held now, high-water mark) of the library's device buffers, all contexts of the process."""
+        now, peak = c.c_int64(), c.c_int64()
+        _chk(lib().ibwa_device_bytes(c.byref(now), c.byref(peak)))
+        return now.value, peak.value
 
     def stats(self):
         st = RunStats()

@@ -70,6 +70,10 @@ int ibwa_cal_maxdiff(int len, double err, double thres);
 int ibwa_ctx_create(int device, ibwa_ctx_t **out);
 /* Visible HIP devices (the CLI's -G maps GPU slice g to device g mod this count). */
 int ibwa_device_count(int *n);
+/* Device memory the library's buffers hold now, and their high-water mark, in bytes, summed over
+ * every context of the process (a context borrowing another's index counts only its own buffers).
+ * No reference counterpart: the footprint report of bench.py and the CLI's stats line. */
+int ibwa_device_bytes(int64_t *now, int64_t *peak);
 void ibwa_ctx_destroy(ibwa_ctx_t *ctx);
 
 /*
@@ -174,6 +178,11 @@ typedef struct {
 	                              pass resumes them instead of starting over) */
 	int64_t resume_records;    /* 16 B records those states took (requested, incl. any that did not fit);
 	                              the cooperative pass runs them chunk by chunk (part of ms_coop) */
+	int64_t resume_records_peak; /* the most records one first-pass chunk's states requested (the
+	                              state buffer holds one chunk's states at a time) */
+	int64_t resume_records_cap;  /* the state buffer's capacity in 16 B records */
+	int64_t coop_pages_peak;     /* the most bucket pages one cooperative launch took from its pool */
+	int64_t coop_pages_cap;      /* the pool's capacity in pages (COOP_PG 16 B entries each) */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
 
