@@ -72,7 +72,7 @@ struct Batch {
   int64_t n() const { return (int64_t)len.size(); }
 };
 
-// A GPU run's reads: host-parsed (b) or parsed on the GPUs, staged device to device (dg)
+// A GPU run's reads: host-parsed (b) or parsed on the GPUs, staged as views of the parsed block (dg)
 struct Group {
   Batch b;
   DevGroup dg;
@@ -367,8 +367,8 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   if (ibwa_device_count(&n_dev) || n_dev < 1) return die("no HIP device");
   if (n_gpus > n_dev)
     fprintf(stderr, "[ibwa-amd aln] -G %d on %d visible device(s): slice g runs on device g mod %d\n", n_gpus, n_dev, n_dev);
-  // FASTQ parsed on the GPUs: one ingest context per GPU (its own stream and buffers); the first
-  // region is read from the file while the index loads
+  // FASTQ parsed on the GPUs: n_lanes + 1 ingest contexts per GPU (their own streams and buffers;
+  // ingest.h's slots); the first region is read and parsed while the index loads
   std::vector<ibwa_ctx_t *> ing;
   std::unique_ptr<FastqGpu> fg;
   struct Destroy {
@@ -379,16 +379,21 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       for (auto *x : v) ibwa_ctx_destroy(x);
     }
   } destroy_ing{ing, fg};
+  const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
   if (fq_dev) {
-    for (int g = 0; g < n_gpus; ++g) {
-      ibwa_ctx_t *x = nullptr;
-      if (ibwa_ctx_create(g % n_dev, &x)) return die("ibwa_ctx_create (ingest)");
-      ing.push_back(x);
-    }
+    // one slot per group a lane can hold, and one more that is parsed ahead
+    const int n_slots = n_lanes + 1;
+    for (int sl = 0; sl < n_slots; ++sl)
+      for (int g = 0; g < n_gpus; ++g) {
+        ibwa_ctx_t *x = nullptr;
+        if (ibwa_ctx_create(g % n_dev, &x)) return die("ibwa_ctx_create (ingest)");
+        ing.push_back(x);
+      }
     const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
     const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)1 << 30;
     const uint64_t carry = cm && atoll(cm) > 0 ? (uint64_t)atoll(cm) : (uint64_t)256 << 20;
-    fg.reset(new FastqGpu(fq_dev, ing, opt.mode, opt.trim_qual, kSub, piece, carry));
+    fg.reset(new FastqGpu(fq_dev, ing, n_gpus, opt.mode, opt.trim_qual, kSub, piece, carry,
+                          [opt](int max_len) { return batch_key(opt, max_len); }));
     if (!fg->ok()) {
       fprintf(stderr, "[ibwa-amd aln] cannot read %s for the device parse\n", fq_dev);
       return 1;
@@ -417,13 +422,12 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   bool eof = false;
   double parse_s = 0;  // wall time of the FASTQ parse (all host threads, or waiting for the GPUs')
   bool dev_active = fg != nullptr, dev_done = false;
-  auto key_of = [&](int max_len) { return batch_key(opt, max_len); };
   auto timed_read = [&](Group &into) {
     const auto t = std::chrono::steady_clock::now();
     int r = 0;
     into.dev = false;
     if (dev_active) {
-      if (fg->next(into.dg, key_of)) {
+      if (fg->next(into.dg)) {
         into.dev = true;
         r = 1;
       } else {
@@ -458,7 +462,6 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   // Overlapped groups: lane l's contexts (one per GPU) share lane 0's index and take every
   // n_lanes-th group, so a group's staging, first pass and host work run while the previous group's
   // cooperative pass drains.  Groups finish, and their records are written, in input order.
-  const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
   std::vector<std::vector<ibwa_ctx_t *>> lctx(n_lanes);
   lctx[0] = ctx;
   for (int l = 1; l < n_lanes; ++l)
@@ -494,13 +497,13 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     J.t0 = std::chrono::steady_clock::now();
     J.active = true;
     const int64_t per = (n + n_gpus - 1) / n_gpus;
-    // a group parsed on the GPUs is staged here, device to device, before the next region's parse
-    // reuses the ingest buffers; its slices are the group's reads in each GPU's piece
+    // a group parsed on the GPUs is staged as a view of its ingest slot (released in finish());
+    // its slices are the group's reads in each GPU's piece
     std::vector<double> stage_ms(n_gpus, 0.0);
     if (J.b.dev)
       for (int g = 0; g < n_gpus; ++g) {
         const auto s0 = std::chrono::steady_clock::now();
-        J.rc[g] = ibwa_batch_stage_fq(cx[g], ing[g], J.b.dg.first[g], J.b.dg.count[g], J.b.dg.max_len);
+        J.rc[g] = ibwa_batch_stage_fq(cx[g], fg->ctx_of(J.b.dg, g), J.b.dg.first[g], J.b.dg.count[g], J.b.dg.max_len);
         stage_ms[g] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s0).count();
       }
     for (int g = 0; g < n_gpus; ++g) {
@@ -544,6 +547,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     for (auto &t : J.th) t.join();
     J.th.clear();
     J.active = false;
+    if (J.b.dev) fg->release(J.b.dg);  // its ingest slot may be parsed over
     for (int g = 0; g < n_gpus; ++g)
       if (J.rc[g]) return die("aln");
     tot_seqs += J.b.n();
@@ -583,6 +587,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   const auto t_parse_only = std::chrono::steady_clock::now();
   while (have > 0 && parse_only) {
     tot_seqs += cur.n();
+    if (cur.dev) fg->release(cur.dg);
     have = timed_read(cur);
   }
   if (parse_only) {
@@ -622,8 +627,8 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   fprintf(stderr, "[ibwa-amd aln] device memory: peak %.1f GB of engine buffers on %d GPU(s) (%d context(s) per GPU, "
                   "index shared)\n", dev_peak / 1e9, n_gpus, n_lanes);
   if (fg) {
-    fprintf(stderr, "[ibwa-amd aln] input parsed on the GPUs: %lld records, %.2f s waiting for the parse (%.0f ms of device "
-                    "time: H2D copies + kernels)%s\n",
+    fprintf(stderr, "[ibwa-amd aln] input parsed on the GPUs: %lld records, %.2f s parsing ahead of the alignment (%.0f ms "
+                    "of device time: H2D copies + kernels)%s\n",
             (long long)fg->records(), fg->parse_s(), fg->dev_ms(), fg->handoff() ? "; the host readers took the rest" : "");
   }
   if (parse_s > 0) {

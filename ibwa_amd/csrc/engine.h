@@ -310,8 +310,5 @@ struct FqBufs {
 uint64_t fq_padded_bytes(uint64_t n);
 // tmp == nullptr: *tmp_bytes = the scans' scratch size
 hipError_t fq_parse_launch(const FqBufs &b, uint64_t n, const FqOpt &o, void *tmp, size_t *tmp_bytes, hipStream_t st);
-// kept reads [first, first + n) of a parsed block as a batch: offsets from the first one's codes
-hipError_t fq_rebase(const uint64_t *offk, const uint32_t *lenk, int64_t first, int64_t n, uint64_t *off, uint32_t *len,
-                     hipStream_t st);
 
 }  // namespace ibwa

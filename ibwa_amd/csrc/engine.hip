@@ -107,6 +107,10 @@ struct ibwa_ctx {
   bool loaded[2] = {false, false};
   // staged batch
   DBuf d_seq, d_off, d_len;
+  // the staged batch: d_seq / d_off / d_len, or (ibwa_batch_stage_fq) a parsed block's kept reads
+  const uint8_t *v_seq = nullptr;
+  const uint64_t *v_off = nullptr;
+  const uint32_t *v_len = nullptr;
   int64_t n = 0;
   uint64_t seq_bytes = 0;
   int max_len = 0;
@@ -166,7 +170,13 @@ struct ibwa_ctx {
   int gap_lw = 1;                    // first pass with its widths in LDS (gapped.hip LW) when they fit
   int gap_lw_min_waves = 8;          // ... in a workgroup size that keeps at least this many waves per CU
   int gap_resume = 1;                // early hand-offs leave their search state for the coop pass (LW)
-  int gap_resume_gb = 48;            // state buffer (GiB, at most ~4 KiB per read of the batch)
+  int gap_resume_gb = 48;            // state buffer: at most this many GiB ...
+  // ... sized per read of a first-pass chunk: this many 16 B records (100 bp reads at 1 % need ~160
+  // per read at the busiest chunk), or the most an earlier run's chunk needed (x 1.15) if more --
+  // states that do not fit are not lost work only: their reads start over in the cooperative pass
+  uint32_t gap_resume_recs = 192;
+  double resume_need = 0;            // the most records per chunk read a run of this context requested
+  int coop_stg_room = 1;             // k_coop's per-lane staging ring: this many chains' children (2: same time)
   int64_t gap_resume_records = 0;    // tests: state buffer of this many 16 B records (0: by gap_resume_gb)
   // the early hand-off rule when the read leaves a resume state (nothing is re-run, so it pays to hand
   // on earlier: swept at 50M reads, flat optimum, profiles/r03_resume_sweep*.log)
@@ -174,7 +184,9 @@ struct ibwa_ctx {
   // resume in a launch's tail (GapArgs::tail_lanes): 16 / 200 measured 5868 vs 5884 ms per 50M-read
   // step (profiles/r03_tail_sweep.log; 8, 32, 4 / 500 in between)
   uint32_t gap_tail_lanes = 16, gap_tail_iters = 200;
-  int gap_resume_ppb = 96;           // first-pass pages per 256-lane pool when states are left (<= gap_pages_per_block)
+  // first-pass pages per 256-lane pool when states are left (<= gap_pages_per_block): 96 -> 48 cost
+  // nothing measurable at 100 or 150 bp (profiles/r04_sweep_mem*.jsonl)
+  int gap_resume_ppb = 48;
   uint32_t gap_resume_cap1 = 4096;   // first-pass static slots per lane when states are left (<= gap_cap1)
   DBuf d_cw, d_ptabg;
   DBuf d_rdump, d_roff;  // resume states (GapArgs::rdump) and per-read offsets
@@ -182,6 +194,7 @@ struct ibwa_ctx {
   bool hpop_valid = false;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
   int coop_pool_gb = 16;             // bucket page pool
+  uint32_t coop_pool_pages = 0;      // tests: the pool in pages (0: by coop_pool_gb)
   DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb, c_proot, c_pstore;
   bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
   bool verbose = getenv("IBWA_VERBOSE") != nullptr;
@@ -472,6 +485,9 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_coop") c->gap_coop = value != 0;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
   else if (k == "coop_pool_gb" && value > 0 && value <= 256) c->coop_pool_gb = (int)value;
+  else if (k == "coop_stg_room" && value >= 1 && value <= 4) c->coop_stg_room = (int)value;
+  else if (k == "coop_pool_pages" && value >= 0 && value <= (1l << 24)) c->coop_pool_pages = (uint32_t)value;
+  else if (k == "gap_resume_recs" && value >= 1 && value <= 65536) c->gap_resume_recs = (uint32_t)value;
   else if (k == "sw_stop" && value >= 0 && value <= 2) c->sw_stop_after = (int)value;  // SW phase timing
   else return fail(IBWA_EINVAL, "unknown option %s", k.c_str());
   return 0;
@@ -929,23 +945,14 @@ int ibwa_batch_stage_fq(ibwa_ctx_t *c, const ibwa_ctx_t *src, int64_t first, int
   if (max_len > 65535) return fail(IBWA_EINVAL, "read length %d > 65535 is not supported", max_len);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(src->stream));  // the block is parsed
-  uint64_t b0 = 0, b1 = 0;
-  uint32_t l1 = 0;
-  if (n) {
-    HIPCHK(hipMemcpy(&b0, src->fq_offk.as<uint64_t>() + first, 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&b1, src->fq_offk.as<uint64_t>() + first + n - 1, 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&l1, src->fq_lenk.as<uint32_t>() + first + n - 1, 4, hipMemcpyDeviceToHost));
-  }
-  const uint64_t bytes = n ? b1 + l1 - b0 : 0;
-  if (int rc = c->d_seq.ensure(bytes + 16)) return rc;
-  if (int rc = c->d_off.ensure(n * 8 + 8)) return rc;
-  if (int rc = c->d_len.ensure(n * 4 + 4)) return rc;
-  if (bytes) HIPCHK(hipMemcpyAsync(c->d_seq.p, src->fq_codes.as<uint8_t>() + b0, bytes, hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(fq_rebase(src->fq_offk.as<uint64_t>(), src->fq_lenk.as<uint32_t>(), first, n, c->d_off.as<uint64_t>(),
-                   c->d_len.as<uint32_t>(), c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  // no copy: the batch is a view of the parsed block's kept reads (their codes, offsets into them
+  // and lengths), which must stay as they are until this context's runs over it are over -- a
+  // copy would be a kernel waiting for CUs that the other contexts' persistent searches hold
+  c->v_seq = src->fq_codes.as<uint8_t>();
+  c->v_off = src->fq_offk.as<uint64_t>() + first;
+  c->v_len = src->fq_lenk.as<uint32_t>() + first;
   c->n = n;
-  c->seq_bytes = bytes;
+  c->seq_bytes = 0;
   c->max_len = max_len;
   return 0;
 }
@@ -972,6 +979,9 @@ int ibwa_batch_stage(ibwa_ctx_t *c, int64_t n, const uint8_t *seq, const uint64_
   c->n = n;
   c->seq_bytes = bytes;
   c->max_len = max_len;
+  c->v_seq = c->d_seq.as<uint8_t>();
+  c->v_off = c->d_off.as<uint64_t>();
+  c->v_len = c->d_len.as<uint32_t>();
   return 0;
 }
 
@@ -1040,9 +1050,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   AlnArgs A = {};
   A.ix[0] = c->ix[0];
   A.ix[1] = c->ix[1];
-  A.seq = c->d_seq.as<uint8_t>();
-  A.off = c->d_off.as<uint64_t>();
-  A.len = c->d_len.as<uint32_t>();
+  A.seq = c->v_seq;
+  A.off = c->v_off;
+  A.len = c->v_len;
   A.maxdiff_tab = c->d_tab.as<int16_t>();
   A.wlen1 = (uint32_t)max_len + 1;
   A.wstride = 2ull * A.wlen1 + 2ull * ((uint64_t)std::max(opt->seed_len, 0) + 1);
@@ -1125,8 +1135,15 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (int rc = ensure_kmer(c)) return rc;
     c->stats.path = 2;
     // equal chunks of at most gap_reads_per_chunk reads: every launch ends with a tail in which
-    // only its slowest reads still run, so fewer (and balanced) launches waste less
-    const int64_t n_chunks = (std::max<int64_t>(n, 1) + c->gap_reads_per_chunk - 1) / c->gap_reads_per_chunk;
+    // only its slowest reads still run, so fewer (and balanced) launches waste less -- but no more
+    // reads than an earlier run's resume states per read let the state buffer hold (150 bp at 2 %:
+    // 3 chunks of 6.7 M instead of 2 of 10 M, whose overflowing states start over: 5160 -> 4972 ms
+    // per 20 M reads, profiles/r04_sweep_mem150.jsonl)
+    int64_t per_chunk = c->gap_reads_per_chunk;
+    if (c->resume_need > 0)
+      per_chunk = std::max<int64_t>(65536, std::min<int64_t>(per_chunk, (int64_t)((double)(((uint64_t)c->gap_resume_gb << 30) / 16) /
+                                                                                   (1.15 * c->resume_need))));
+    const int64_t n_chunks = (std::max<int64_t>(n, 1) + per_chunk - 1) / per_chunk;
     const int64_t chunk = (std::max<int64_t>(n, 1) + n_chunks - 1) / n_chunks;
     // LDS: bucket heads + free slots + page table per lane, the page bitmap per workgroup
     const uint32_t LG = 13, P0 = c->gap_cap1;
@@ -1175,7 +1192,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     uint64_t rd_cap = 0;
     if (resume) {
       // the buffer holds one first-pass chunk's states at a time (cleared after each chunk)
-      rd_cap = std::min<uint64_t>((uint64_t)c->gap_resume_gb << 30, (uint64_t)chunk * 4096 + (1u << 20)) / 16;
+      const double per_read = std::max<double>(c->gap_resume_recs, 1.15 * c->resume_need);
+      rd_cap = std::min<uint64_t>(((uint64_t)c->gap_resume_gb << 30) / 16, (uint64_t)((double)chunk * per_read) + (1u << 16));
       if (c->gap_resume_records > 0) rd_cap = (uint64_t)c->gap_resume_records;
       if (int rc = c->d_rdump.ensure(rd_cap * 16)) return rc;
       c->stats.resume_records_cap = (int64_t)rd_cap;
@@ -1219,14 +1237,14 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       const int64_t lanes = (int64_t)lanes_u;
       if (lanes > 0) {
         uint32_t stg_log2 = 10;
-        while ((1u << stg_log2) < 2u * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
+        while ((1u << stg_log2) < (uint32_t)c->coop_stg_room * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
         const int full_blocks = c->n_cus * c->coop_waves_per_cu;
         const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
         const uint32_t freecap = 4096, hcap = 4096;
         const uint64_t pool_bytes = std::min<uint64_t>(
             (uint64_t)c->coop_pool_gb << 30,
             std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
-        const uint32_t pool_pages = (uint32_t)(pool_bytes / (COOP_PG * 16ull));
+        const uint32_t pool_pages = c->coop_pool_pages ? c->coop_pool_pages : (uint32_t)(pool_bytes / (COOP_PG * 16ull));
         if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
         if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
         if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
@@ -1321,6 +1339,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       HIPCHK(hipMemcpy(&used, c->d_roff.as<unsigned long long>() + n, 8, hipMemcpyDeviceToHost));
       c->stats.resume_records += (int64_t)used;
       c->stats.resume_records_peak = std::max<int64_t>(c->stats.resume_records_peak, (int64_t)used);
+      if (cnt >= 65536) c->resume_need = std::max(c->resume_need, (double)used / (double)cnt);
       HIPCHK(hipMemsetAsync(c->d_roff.as<unsigned long long>() + n, 0, 8, c->stream));
       return 0;
     };
@@ -1520,242 +1539,254 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   // heavy and overflowing reads: the wave-cooperative kernel first (exact; whatever it cannot
   // hold is flagged and continues below)
   if (v2 && c->gap_coop && !todo.empty() && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK) {
-    const int64_t lanes = (int64_t)todo.size();
-    uint32_t stg_log2 = 10;
-    while ((1u << stg_log2) < 2u * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
-    // one heavy read per wave at a time: no more waves than heavy reads, and the page pool in
-    // proportion (at least 1 GiB; a read that runs out of pages goes on to the wide kernel)
-    const int full_blocks = c->n_cus * c->coop_waves_per_cu;
-    const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
-    const uint32_t freecap = 4096, hcap = 4096;
-    const uint64_t pool_bytes = std::min<uint64_t>(
-        (uint64_t)c->coop_pool_gb << 30, std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
-    const uint32_t pool_pages = (uint32_t)(pool_bytes / (COOP_PG * 16ull));
-    if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
-    if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
-    if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
-    if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
-    // k_coop_roots: two chain records per read, their children in a compact store (a chain that
-    // finds it full leaves level 0 to k_coop).  A root chain stages ~190 children on a GRCh37-sized
-    // genome, so the store takes the first pass's page pool when there is one: nothing in it is
-    // live between the first pass and the retry passes, which set it up anew.
-    uint4 *pstore = nullptr;
-    uint64_t pcap = 0;
-    if (c->coop_roots) {
-      if (int rc = c->c_proot.ensure((uint64_t)lanes * 2 * 16)) return rc;
-      if (c->d_pool.cap >= (1ull << 30)) {
-        pstore = c->d_pool.as<uint4>();
-        pcap = std::min<uint64_t>(c->d_pool.cap / 16, 0xFFFFFFFFull);
-      } else {
-        pcap = std::min<uint64_t>(1ull << 31, std::max<uint64_t>(1ull << 24, (uint64_t)lanes * 2 * 256));
-        if (int rc = c->c_pstore.ensure(pcap * 16)) return rc;
-        pstore = c->c_pstore.as<uint4>();
+    std::vector<int64_t> wide_todo, wide_where;
+    for (int round = 0; round < 3 && !todo.empty(); ++round) {
+      const int64_t lanes = (int64_t)todo.size();
+      const size_t wide0 = wide_todo.size();
+      uint32_t stg_log2 = 10;
+      while ((1u << stg_log2) < (uint32_t)c->coop_stg_room * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
+      // one heavy read per wave at a time: no more waves than heavy reads, and the page pool in
+      // proportion (at least 1 GiB; the reads that run out of pages run again with all of it)
+      const int full_blocks = c->n_cus * c->coop_waves_per_cu;
+      const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
+      const uint32_t freecap = 4096, hcap = 4096;
+      const uint64_t pool_bytes =
+          round ? (uint64_t)c->coop_pool_gb << 30
+                : std::min<uint64_t>((uint64_t)c->coop_pool_gb << 30,
+                                     std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
+      const uint32_t pool_pages = c->coop_pool_pages ? c->coop_pool_pages : (uint32_t)(pool_bytes / (COOP_PG * 16ull));
+      if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
+      if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;
+      if (int rc = c->d_nN.ensure(lanes * 2 + 2)) return rc;
+      if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
+      // k_coop_roots: two chain records per read, their children in a compact store (a chain that
+      // finds it full leaves level 0 to k_coop).  A root chain stages ~190 children on a GRCh37-sized
+      // genome, so the store takes the first pass's page pool when there is one: nothing in it is
+      // live between the first pass and the retry passes, which set it up anew.
+      uint4 *pstore = nullptr;
+      uint64_t pcap = 0;
+      if (c->coop_roots) {
+        if (int rc = c->c_proot.ensure((uint64_t)lanes * 2 * 16)) return rc;
+        if (c->d_pool.cap >= (1ull << 30)) {
+          pstore = c->d_pool.as<uint4>();
+          pcap = std::min<uint64_t>(c->d_pool.cap / 16, 0xFFFFFFFFull);
+        } else {
+          pcap = std::min<uint64_t>(1ull << 31, std::max<uint64_t>(1ull << 24, (uint64_t)lanes * 2 * 256));
+          if (int rc = c->c_pstore.ensure(pcap * 16)) return rc;
+          pstore = c->c_pstore.as<uint4>();
+        }
       }
-    }
-    if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
-    if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
-    if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
-    if (int rc = c->c_recb.ensure((uint64_t)blocks * COOP_RREC * 16)) return rc;
-    if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
-    if (int rc = c->c_next.ensure(64)) return rc;
-    if (int rc = c->r_status.ensure(lanes * 4)) return rc;
-    if (int rc = c->d_counter.ensure(64)) return rc;
-    // d_ids holds todo (select_handed_on, input order); the pass takes the reads with the largest
-    // first-pass stacks first (its longest reads then do not start near its end) -- which pass or
-    // which order resolves a read changes nothing in its results
-    const int64_t *coop_ids = c->d_ids.as<int64_t>();
-    if (c->coop_order && lanes > 1) {
-      size_t tb = 0;
-      HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &tb, c->stream));
-      if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;
-      if (int rc = c->d_ordi.ensure(lanes * 8)) return rc;
-      if (int rc = c->d_ordids.ensure(lanes * 8)) return rc;
-      if (int rc = c->d_ordtmp.ensure(tb + 16)) return rc;
-      HIPCHK(order_heavy_first(c->d_selst.as<uint32_t>(), c->d_ids.as<int64_t>(), lanes, c->d_ordk.as<uint32_t>(),
-                               c->d_ordi.as<uint32_t>(), c->d_ordids.as<int64_t>(), c->d_ordtmp.p, &tb, c->stream));
-      std::vector<uint32_t> perm(lanes);
-      HIPCHK(hipMemcpyAsync(perm.data(), c->d_ordi.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
+      if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
+      if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
+      if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
+      if (int rc = c->c_recb.ensure((uint64_t)blocks * COOP_RREC * 16)) return rc;
+      if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
+      if (int rc = c->c_next.ensure(64)) return rc;
+      if (int rc = c->r_status.ensure(lanes * 4)) return rc;
+      if (int rc = c->d_counter.ensure(64)) return rc;
+      // d_ids holds todo (select_handed_on, input order); the pass takes the reads with the largest
+      // first-pass stacks first (its longest reads then do not start near its end) -- which pass or
+      // which order resolves a read changes nothing in its results
+      if (round) HIPCHK(hipMemcpy(c->d_ids.p, todo.data(), lanes * 8, hipMemcpyHostToDevice));
+      const int64_t *coop_ids = c->d_ids.as<int64_t>();
+      if (!round && c->coop_order && lanes > 1) {
+        size_t tb = 0;
+        HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &tb, c->stream));
+        if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;
+        if (int rc = c->d_ordi.ensure(lanes * 8)) return rc;
+        if (int rc = c->d_ordids.ensure(lanes * 8)) return rc;
+        if (int rc = c->d_ordtmp.ensure(tb + 16)) return rc;
+        HIPCHK(order_heavy_first(c->d_selst.as<uint32_t>(), c->d_ids.as<int64_t>(), lanes, c->d_ordk.as<uint32_t>(),
+                                 c->d_ordi.as<uint32_t>(), c->d_ordids.as<int64_t>(), c->d_ordtmp.p, &tb, c->stream));
+        std::vector<uint32_t> perm(lanes);
+        HIPCHK(hipMemcpyAsync(perm.data(), c->d_ordi.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int64_t j = 0; j < lanes; ++j) {
+          todo[j] = c->retry_ids[perm[j]];
+          where[j] = perm[j];
+        }
+        coop_ids = c->d_ordids.as<int64_t>();
+      }
+      AlnArgs B = A;
+      B.ids = coop_ids;
+      B.n = lanes;
+      B.wbuf = c->d_wbuf.as<uint2>();
+      B.nN = c->d_nN.as<uint16_t>();
+      CoopArgs K = {};
+      K.wb_base = -1;  // widths from this launch's k_width
+      K.ix[0] = c->ix[0];
+      K.ix[1] = c->ix[1];
+      K.o64[0] = c->o64[0].as<uint4>();
+      K.o64[1] = c->o64[1].as<uint4>();
+      K.seq = A.seq;
+      K.off = A.off;
+      K.len = A.len;
+      K.ids = B.ids;
+      K.n = lanes;
+      K.out_by_id = 1;  // n_aln / aln_off of the input read; status per launch read
+      K.maxdiff_tab = A.maxdiff_tab;
+      K.wbuf = B.wbuf;
+      K.wstride = A.wstride;
+      K.wlen1 = A.wlen1;
+      K.nN = B.nN;
+      K.stg = c->c_stg.as<uint4>();
+      K.stg_log2 = stg_log2;
+      K.dir = c->c_dir.as<uint32_t>();
+      K.freel = c->c_free.as<uint32_t>();
+      K.freecap = freecap;
+      K.pool = c->c_pool.as<uint4>();
+      K.pool_pages = pool_pages;
+      K.pool_next = c->c_next.as<uint32_t>();
+      K.hits = c->c_hits.as<uint4>();
+      K.recb = c->c_recb.as<uint4>();
+      if (resume_states) {
+        K.rdump = c->d_rdump.as<uint4>();
+        K.roff = c->d_roff.as<uint64_t>();
+      }
+      if (c->coop_roots) {
+        K.proot = c->c_proot.as<uint4>();
+        K.pstore = pstore;
+        K.pstore_next = c->c_next.as<unsigned long long>() + 1;
+        K.pstore_cap = pcap;
+      }
+      K.hcap = hcap;
+      K.max_iters = 1u << 24;  // runaway guard; a read past it goes to the sequential kernel
+      // hits go on the first pass's stream (a read out of room there is flagged and re-run below)
+      K.aln = c->d_aln.as<uint4>();
+      K.aln_total = c->stream_total;
+      K.aln_next = c->d_counter.as<unsigned long long>() + 1;
+      K.aln_off = c->d_aoff.as<uint64_t>();
+      K.n_aln = c->d_naln.as<int32_t>();
+      K.status = c->r_status.as<uint32_t>();
+      if (c->verbose) {
+        if (int rc = c->d_iters.ensure(lanes * 4)) return rc;
+        K.iters = c->d_iters.as<uint32_t>();
+      }
+      K.o = o;
+      if (c->prof_phases) {
+        if (int rc = c->d_prof.ensure(512 + (uint64_t)blocks * 16)) return rc;
+        HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 512 + (uint64_t)blocks * 16, c->stream));
+        K.prof = c->d_prof.as<unsigned long long>();
+        K.wave_t = K.prof + 64;
+      }
+      HIPCHK(hipEventRecord(c->ev[3], c->stream));
+      HIPCHK(launch_width(B, c->block, c->stream));
+      HIPCHK(hipEventRecord(c->ev[5], c->stream));
+      if (K.proot) HIPCHK(launch_coop_roots(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
+      HIPCHK(hipEventRecord(c->ev[6], c->stream));
+      HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
+      HIPCHK(hipEventRecord(c->ev[4], c->stream));
+      HIPCHK(hipEventSynchronize(c->ev[4]));
+      note_coop_pages(c, pool_pages);
+      if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop kernel done\n", since());
+      if (c->prof_phases) {
+        unsigned long long pf[40];
+        HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
+        const char *nm[6] = {"barriers", "commits", "claims", "loads+consume", "levels", "read set-up"};
+        double tot = 0;
+        for (int q = 0; q < 6; ++q) tot += (double)pf[q];
+        fprintf(stderr, "[ibwa_amd] k_coop phases (wave cycles):");
+        for (int q = 0; q < 6; ++q) fprintf(stderr, " %s %.1f%%", nm[q], tot > 0 ? 100.0 * pf[q] / tot : 0.0);
+        fprintf(stderr, "; %llu iterations (%.0f cycles each), %llu commits, %llu levels; lanes per iteration: "
+                "%.1f running (%.1f fetching an entry, %.1f in an exact tail)\n", pf[6], pf[6] ? tot / pf[6] : 0.0, pf[7],
+                pf[8], pf[6] ? (double)pf[9] / pf[6] : 0.0, pf[6] ? (double)pf[10] / pf[6] : 0.0,
+                pf[6] ? (double)pf[11] / pf[6] : 0.0);
+        const double it = pf[6] ? (double)pf[6] : 1.0;
+        fprintf(stderr, "[ibwa_amd] k_coop idle lanes per iteration: barrier %.1f, level drained %.1f, ring %.1f, staging %.1f; "
+                "chains %llu (%.0f per level), %llu discarded at %llu barriers, %llu children committed\n",
+                pf[12] / it, pf[13] / it, pf[14] / it, pf[15] / it, pf[16], pf[8] ? (double)pf[16] / pf[8] : 0.0, pf[17],
+                pf[18], pf[19]);
+        fprintf(stderr, "[ibwa_amd] k_coop iterations (running lanes) by chains per level:");
+        const char *nb[5] = {"<=2", "<=16", "<=64", "<=256", ">256"};
+        for (int q = 0; q < 5; ++q)
+          fprintf(stderr, " %s: %.1f%% (%.1f)", nb[q], 100.0 * pf[20 + q] / it, pf[20 + q] ? (double)pf[25 + q] / pf[20 + q] : 0.0);
+        fprintf(stderr, "\n");
+        fprintf(stderr, "[ibwa_amd] k_coop one-row lane-steps: expanding %.1f%%, exact tail %.1f%% of running; chains by steps:",
+                100.0 * pf[30] / (pf[9] ? pf[9] : 1), 100.0 * pf[31] / (pf[9] ? pf[9] : 1));
+        const char *cb[4] = {"<4", "<16", "<64", ">=64"};
+        for (int q = 0; q < 4; ++q)
+          fprintf(stderr, " %s: %llu (%.1f%% of steps)", cb[q], pf[32 + q], 100.0 * pf[36 + q] / (pf[9] ? pf[9] : 1));
+        fprintf(stderr, "\n");
+        // wave end times (shader clock) relative to the first wave start: the pass's tail
+        std::vector<unsigned long long> wt((size_t)blocks * 2);
+        HIPCHK(hipMemcpy(wt.data(), K.wave_t, wt.size() * 8, hipMemcpyDeviceToHost));
+        // each wave's own duration (the clock is per XCD; the persistent grid starts together)
+        std::vector<double> ends;
+        for (int w = 0; w < blocks; ++w) ends.push_back((double)(wt[2 * w + 1] - wt[2 * w]));
+        std::sort(ends.begin(), ends.end());
+        const double last = ends.back() > 0 ? ends.back() : 1.0;
+        fprintf(stderr, "[ibwa_amd] k_coop wave durations (fraction of the longest): p10 %.3f p50 %.3f p90 %.3f p99 %.3f\n",
+                ends[ends.size() / 10] / last, ends[ends.size() / 2] / last, ends[ends.size() * 9 / 10] / last,
+                ends[ends.size() * 99 / 100] / last);
+      }
+      float a = 0;
+      HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
+      ms_r += a;
+      std::vector<uint32_t> rs(lanes);
+      HIPCHK(hipMemcpyAsync(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
+      // reads out of pool pages (reason 3: the pool is shared by the launch's waves) run again in a
+      // launch of their own with the whole pool; the others go on to the wide kernel
+      std::vector<int64_t> next, next_where;
       for (int64_t j = 0; j < lanes; ++j) {
-        todo[j] = c->retry_ids[perm[j]];
-        where[j] = perm[j];
+        if (rs[j] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "score outside the stack range");
+        if (rs[j]) {
+          const bool again = ((rs[j] >> 8) & 7u) == 3u && round < 2;
+          (again ? next : wide_todo).push_back(todo[j]);
+          (again ? next_where : wide_where).push_back(where[j]);
+          continue;
+        }
+        found_by[where[j]] = 1;
       }
-      coop_ids = c->d_ordids.as<int64_t>();
-    }
-    AlnArgs B = A;
-    B.ids = coop_ids;
-    B.n = lanes;
-    B.wbuf = c->d_wbuf.as<uint2>();
-    B.nN = c->d_nN.as<uint16_t>();
-    CoopArgs K = {};
-    K.wb_base = -1;  // widths from this launch's k_width
-    K.ix[0] = c->ix[0];
-    K.ix[1] = c->ix[1];
-    K.o64[0] = c->o64[0].as<uint4>();
-    K.o64[1] = c->o64[1].as<uint4>();
-    K.seq = A.seq;
-    K.off = A.off;
-    K.len = A.len;
-    K.ids = B.ids;
-    K.n = lanes;
-    K.out_by_id = 1;  // n_aln / aln_off of the input read; status per launch read
-    K.maxdiff_tab = A.maxdiff_tab;
-    K.wbuf = B.wbuf;
-    K.wstride = A.wstride;
-    K.wlen1 = A.wlen1;
-    K.nN = B.nN;
-    K.stg = c->c_stg.as<uint4>();
-    K.stg_log2 = stg_log2;
-    K.dir = c->c_dir.as<uint32_t>();
-    K.freel = c->c_free.as<uint32_t>();
-    K.freecap = freecap;
-    K.pool = c->c_pool.as<uint4>();
-    K.pool_pages = pool_pages;
-    K.pool_next = c->c_next.as<uint32_t>();
-    K.hits = c->c_hits.as<uint4>();
-    K.recb = c->c_recb.as<uint4>();
-    if (resume_states) {
-      K.rdump = c->d_rdump.as<uint4>();
-      K.roff = c->d_roff.as<uint64_t>();
-    }
-    if (c->coop_roots) {
-      K.proot = c->c_proot.as<uint4>();
-      K.pstore = pstore;
-      K.pstore_next = c->c_next.as<unsigned long long>() + 1;
-      K.pstore_cap = pcap;
-    }
-    K.hcap = hcap;
-    K.max_iters = 1u << 24;  // runaway guard; a read past it goes to the sequential kernel
-    // hits go on the first pass's stream (a read out of room there is flagged and re-run below)
-    K.aln = c->d_aln.as<uint4>();
-    K.aln_total = c->stream_total;
-    K.aln_next = c->d_counter.as<unsigned long long>() + 1;
-    K.aln_off = c->d_aoff.as<uint64_t>();
-    K.n_aln = c->d_naln.as<int32_t>();
-    K.status = c->r_status.as<uint32_t>();
-    if (c->verbose) {
-      if (int rc = c->d_iters.ensure(lanes * 4)) return rc;
-      K.iters = c->d_iters.as<uint32_t>();
-    }
-    K.o = o;
-    if (c->prof_phases) {
-      if (int rc = c->d_prof.ensure(512 + (uint64_t)blocks * 16)) return rc;
-      HIPCHK(hipMemsetAsync(c->d_prof.p, 0, 512 + (uint64_t)blocks * 16, c->stream));
-      K.prof = c->d_prof.as<unsigned long long>();
-      K.wave_t = K.prof + 64;
-    }
-    HIPCHK(hipEventRecord(c->ev[3], c->stream));
-    HIPCHK(launch_width(B, c->block, c->stream));
-    HIPCHK(hipEventRecord(c->ev[5], c->stream));
-    if (K.proot) HIPCHK(launch_coop_roots(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
-    HIPCHK(hipEventRecord(c->ev[6], c->stream));
-    HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
-    HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    HIPCHK(hipEventSynchronize(c->ev[4]));
-    note_coop_pages(c, pool_pages);
-    if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop kernel done\n", since());
-    if (c->prof_phases) {
-      unsigned long long pf[40];
-      HIPCHK(hipMemcpy(pf, c->d_prof.p, sizeof pf, hipMemcpyDeviceToHost));
-      const char *nm[6] = {"barriers", "commits", "claims", "loads+consume", "levels", "read set-up"};
-      double tot = 0;
-      for (int q = 0; q < 6; ++q) tot += (double)pf[q];
-      fprintf(stderr, "[ibwa_amd] k_coop phases (wave cycles):");
-      for (int q = 0; q < 6; ++q) fprintf(stderr, " %s %.1f%%", nm[q], tot > 0 ? 100.0 * pf[q] / tot : 0.0);
-      fprintf(stderr, "; %llu iterations (%.0f cycles each), %llu commits, %llu levels; lanes per iteration: "
-              "%.1f running (%.1f fetching an entry, %.1f in an exact tail)\n", pf[6], pf[6] ? tot / pf[6] : 0.0, pf[7],
-              pf[8], pf[6] ? (double)pf[9] / pf[6] : 0.0, pf[6] ? (double)pf[10] / pf[6] : 0.0,
-              pf[6] ? (double)pf[11] / pf[6] : 0.0);
-      const double it = pf[6] ? (double)pf[6] : 1.0;
-      fprintf(stderr, "[ibwa_amd] k_coop idle lanes per iteration: barrier %.1f, level drained %.1f, ring %.1f, staging %.1f; "
-              "chains %llu (%.0f per level), %llu discarded at %llu barriers, %llu children committed\n",
-              pf[12] / it, pf[13] / it, pf[14] / it, pf[15] / it, pf[16], pf[8] ? (double)pf[16] / pf[8] : 0.0, pf[17],
-              pf[18], pf[19]);
-      fprintf(stderr, "[ibwa_amd] k_coop iterations (running lanes) by chains per level:");
-      const char *nb[5] = {"<=2", "<=16", "<=64", "<=256", ">256"};
-      for (int q = 0; q < 5; ++q)
-        fprintf(stderr, " %s: %.1f%% (%.1f)", nb[q], 100.0 * pf[20 + q] / it, pf[20 + q] ? (double)pf[25 + q] / pf[20 + q] : 0.0);
-      fprintf(stderr, "\n");
-      fprintf(stderr, "[ibwa_amd] k_coop one-row lane-steps: expanding %.1f%%, exact tail %.1f%% of running; chains by steps:",
-              100.0 * pf[30] / (pf[9] ? pf[9] : 1), 100.0 * pf[31] / (pf[9] ? pf[9] : 1));
-      const char *cb[4] = {"<4", "<16", "<64", ">=64"};
-      for (int q = 0; q < 4; ++q)
-        fprintf(stderr, " %s: %llu (%.1f%% of steps)", cb[q], pf[32 + q], 100.0 * pf[36 + q] / (pf[9] ? pf[9] : 1));
-      fprintf(stderr, "\n");
-      // wave end times (shader clock) relative to the first wave start: the pass's tail
-      std::vector<unsigned long long> wt((size_t)blocks * 2);
-      HIPCHK(hipMemcpy(wt.data(), K.wave_t, wt.size() * 8, hipMemcpyDeviceToHost));
-      // each wave's own duration (the clock is per XCD; the persistent grid starts together)
-      std::vector<double> ends;
-      for (int w = 0; w < blocks; ++w) ends.push_back((double)(wt[2 * w + 1] - wt[2 * w]));
-      std::sort(ends.begin(), ends.end());
-      const double last = ends.back() > 0 ? ends.back() : 1.0;
-      fprintf(stderr, "[ibwa_amd] k_coop wave durations (fraction of the longest): p10 %.3f p50 %.3f p90 %.3f p99 %.3f\n",
-              ends[ends.size() / 10] / last, ends[ends.size() / 2] / last, ends[ends.size() * 9 / 10] / last,
-              ends[ends.size() * 99 / 100] / last);
-    }
-    float a = 0;
-    HIPCHK(hipEventElapsedTime(&a, c->ev[3], c->ev[4]));
-    ms_r += a;
-    std::vector<uint32_t> rs(lanes);
-    HIPCHK(hipMemcpyAsync(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    std::vector<int64_t> next, next_where;
-    for (int64_t j = 0; j < lanes; ++j) {
-      if (rs[j] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "score outside the stack range");
-      if (rs[j]) {
-        next.push_back(todo[j]);
-        next_where.push_back(where[j]);
-        continue;
+      if (c->verbose) {
+        uint32_t mx = 0;
+        if (K.iters) {
+          std::vector<uint32_t> it(lanes);
+          HIPCHK(hipMemcpy(it.data(), K.iters, lanes * 4, hipMemcpyDeviceToHost));
+          mx = *std::max_element(it.begin(), it.end());
+          double sum = 0;
+          for (uint32_t v : it) sum += v;
+          std::sort(it.begin(), it.end());
+          fprintf(stderr, "[ibwa_amd] coop wave-iterations: sum %.3g (%.0f per wave of %d), p50 %u p99 %u p99.9 %u max %u\n",
+                  sum, sum / blocks, blocks, it[it.size() / 2], it[(size_t)(it.size() * 0.99)],
+                  it[(size_t)(it.size() * 0.999)], mx);
+        }
+        uint32_t pages = 0;
+        HIPCHK(hipMemcpy(&pages, K.pool_next, 4, hipMemcpyDeviceToHost));
+        int why[8] = {0};
+        for (int64_t j = 0; j < lanes; ++j)
+          if (rs[j]) ++why[(rs[j] >> 8) & 7];
+        fprintf(stderr, "[ibwa_amd] coop hand-on reasons: len %d, max_entries %d, pool %d, bucket pages %d, guard %d\n",
+                why[1], why[2], why[3], why[4], why[5]);
+        fprintf(stderr, "[ibwa_amd] coop pass: %lld reads, %zu handed on, max %u wave iterations, %u pages, %.1f ms\n",
+                (long long)lanes, next.size(), mx, pages, a);
+        if (K.proot) {
+          unsigned long long used = 0;
+          HIPCHK(hipMemcpy(&used, K.pstore_next, 8, hipMemcpyDeviceToHost));
+          std::vector<uint4> pr((size_t)lanes * 2);
+          HIPCHK(hipMemcpy(pr.data(), K.proot, pr.size() * 16, hipMemcpyDeviceToHost));
+          int64_t fl[3] = {0, 0, 0};
+          for (const uint4 &q : pr) ++fl[(q.w & 0xFFu) < 3 ? (q.w & 0xFFu) : 2];
+          fprintf(stderr, "[ibwa_amd] coop roots: %.1f children per chain stored (%llu of %llu entries), chains: %lld done, "
+                  "%lld hit, %lld skipped\n", (double)used / (double)pr.size(), used, (unsigned long long)K.pstore_cap,
+                  (long long)fl[0], (long long)fl[1], (long long)fl[2]);
+        }
       }
-      found_by[where[j]] = 1;
-    }
-    if (c->verbose) {
-      uint32_t mx = 0;
-      if (K.iters) {
-        std::vector<uint32_t> it(lanes);
-        HIPCHK(hipMemcpy(it.data(), K.iters, lanes * 4, hipMemcpyDeviceToHost));
-        mx = *std::max_element(it.begin(), it.end());
-        double sum = 0;
-        for (uint32_t v : it) sum += v;
-        std::sort(it.begin(), it.end());
-        fprintf(stderr, "[ibwa_amd] coop wave-iterations: sum %.3g (%.0f per wave of %d), p50 %u p99 %u p99.9 %u max %u\n",
-                sum, sum / blocks, blocks, it[it.size() / 2], it[(size_t)(it.size() * 0.99)],
-                it[(size_t)(it.size() * 0.999)], mx);
+      if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop results on host\n", since());
+      c->stats.n_coop += lanes - (int64_t)next.size() - (int64_t)(wide_todo.size() - wide0);
+      c->stats.ms_coop += a;
+      {
+        float w = 0, rt = 0;
+        HIPCHK(hipEventElapsedTime(&w, c->ev[3], c->ev[5]));
+        HIPCHK(hipEventElapsedTime(&rt, c->ev[5], c->ev[6]));
+        c->stats.ms_coop_width += w;
+        c->stats.ms_coop_roots = rt;
       }
-      uint32_t pages = 0;
-      HIPCHK(hipMemcpy(&pages, K.pool_next, 4, hipMemcpyDeviceToHost));
-      int why[8] = {0};
-      for (int64_t j = 0; j < lanes; ++j)
-        if (rs[j]) ++why[(rs[j] >> 8) & 7];
-      fprintf(stderr, "[ibwa_amd] coop hand-on reasons: len %d, max_entries %d, pool %d, bucket pages %d, guard %d\n",
-              why[1], why[2], why[3], why[4], why[5]);
-      fprintf(stderr, "[ibwa_amd] coop pass: %lld reads, %zu handed on, max %u wave iterations, %u pages, %.1f ms\n",
-              (long long)lanes, next.size(), mx, pages, a);
-      if (K.proot) {
-        unsigned long long used = 0;
-        HIPCHK(hipMemcpy(&used, K.pstore_next, 8, hipMemcpyDeviceToHost));
-        std::vector<uint4> pr((size_t)lanes * 2);
-        HIPCHK(hipMemcpy(pr.data(), K.proot, pr.size() * 16, hipMemcpyDeviceToHost));
-        int64_t fl[3] = {0, 0, 0};
-        for (const uint4 &q : pr) ++fl[(q.w & 0xFFu) < 3 ? (q.w & 0xFFu) : 2];
-        fprintf(stderr, "[ibwa_amd] coop roots: %.1f children per chain stored (%llu of %llu entries), chains: %lld done, "
-                "%lld hit, %lld skipped\n", (double)used / (double)pr.size(), used, (unsigned long long)K.pstore_cap,
-                (long long)fl[0], (long long)fl[1], (long long)fl[2]);
-      }
+      todo.swap(next);
+      where.swap(next_where);
     }
-    if (c->verbose) fprintf(stderr, "[ibwa_amd] t %.1f ms: coop results on host\n", since());
-    c->stats.n_coop += lanes - (int64_t)next.size();
-    c->stats.ms_coop += a;
-    {
-      float w = 0, rt = 0;
-      HIPCHK(hipEventElapsedTime(&w, c->ev[3], c->ev[5]));
-      HIPCHK(hipEventElapsedTime(&rt, c->ev[5], c->ev[6]));
-      c->stats.ms_coop_width += w;
-      c->stats.ms_coop_roots = rt;
-    }
-    todo.swap(next);
-    where.swap(next_where);
+    todo.insert(todo.end(), wide_todo.begin(), wide_todo.end());
+    where.insert(where.end(), wide_where.begin(), wide_where.end());
   }
   // first two retry rounds: the persistent gapped kernel with 24-bit slot links and one
   // large static region per read (4 MiB, then 64 MiB; reads < 4096 bp); then the general kernels

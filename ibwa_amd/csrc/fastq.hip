@@ -172,15 +172,6 @@ __global__ void __launch_bounds__(FQ_BLOCK) k_fq_encode(const uint8_t *buf, cons
   }
 }
 
-__global__ void k_fq_rebase(const uint64_t *offk, const uint32_t *lenk, int64_t first, int64_t n, uint64_t *off,
-                            uint32_t *len) {
-  const uint64_t b = offk[first];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    off[i] = offk[first + i] - b;
-    len[i] = lenk[first + i];
-  }
-}
-
 }  // namespace
 
 uint64_t fq_padded_bytes(uint64_t n) { return (n + FQ_TILE - 1) / FQ_TILE * FQ_TILE + FQ_TILE; }
@@ -214,13 +205,6 @@ hipError_t fq_parse_launch(const FqBufs &B, uint64_t n, const FqOpt &o, void *tm
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_fq_encode, dim3(grid), dim3(FQ_BLOCK), 0, st, B.raw, B.nl, B.n_lines, B.bad, B.rec_len, B.rec_key,
                      o.l_bc, B.codes, B.offk, B.lenk);
-  return hipGetLastError();
-}
-
-hipError_t fq_rebase(const uint64_t *offk, const uint32_t *lenk, int64_t first, int64_t n, uint64_t *off, uint32_t *len,
-                     hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fq_rebase, dim3(1024), dim3(256), 0, st, offk, lenk, first, n, off, len);
   return hipGetLastError();
 }
 

@@ -3,13 +3,17 @@
 // bwa_aln_core (bwtaln.c:199-231) reads batches of 0x40000 kept reads with bwa_read_seq
 // (bwaseqio.c:145-208).  For an uncompressed FASTQ file the host here only moves bytes: host
 // threads pread() the file into pinned buffers, one region at a time (the next region is read
-// while the current one is parsed and aligned), and each GPU's ingest context parses its piece of
-// the region -- strict 4-line records split, checked, barcode / -q trimmed, nt4-encoded and
-// reversed on the device (ibwa_fq_parse) -- and keeps the kept reads in HBM.  From the per-record
-// lengths the host forms the reference's batches (kSub kept reads each, the records bwa_read_seq
-// skips included) and from them groups: consecutive complete batches with the same batch-level
-// max_diff (bwtaln.c:86-88), whose slices -- the group's reads in each GPU's piece -- are staged
-// device to device (ibwa_batch_stage_fq).  A region's last, incomplete batch is parsed again at
+// while the current one is parsed), and each GPU's ingest context parses its piece of the region
+// -- strict 4-line records split, checked, barcode / -q trimmed, nt4-encoded and reversed on the
+// device (ibwa_fq_parse) -- and keeps the kept reads in HBM.  From the per-record lengths the host
+// forms the reference's batches (kSub kept reads each, the records bwa_read_seq skips included) and
+// from them groups: consecutive complete batches with the same batch-level max_diff
+// (bwtaln.c:86-88), whose slices -- the group's reads in each GPU's piece -- the aligning contexts
+// take as views of the parsed block (ibwa_batch_stage_fq, no copy).  A producer thread parses ahead:
+// the regions rotate over `slots` ingest contexts per GPU, and a slot is parsed over only once
+// every group of its previous region has been released (aligned) -- the parse kernels wait for
+// CUs that the searches' persistent grids hold, so they must not sit on the launching thread's
+// path.  A region's last, incomplete batch is parsed again at
 // the start of the next region (its bytes move to the front of the next buffer), except at the
 // end of the file.  At the first record that is not strict (FASTA, multi-line, CRLF, a truncated
 // tail) -- or a batch whose bytes exceed the carry room -- the rest of the file, from the start
@@ -24,6 +28,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -38,6 +46,7 @@ namespace ibwa_cli {
 struct DevGroup {
   int64_t n = 0;
   int max_len = 0;
+  int slot = 0;  // the ingest contexts (one per GPU) that hold its reads
   std::vector<std::pair<long, long>> trims;  // per batch: bases trimmed, bases read (bwaseqio.c:206)
   std::vector<int64_t> first, count;
 };
@@ -57,9 +66,14 @@ class FastqGpu {
     return !(got == 2 && m[0] == 0x1f && m[1] == 0x8b);  // gzip: the host readers inflate it
   }
 
-  FastqGpu(const char *fn, std::vector<ibwa_ctx_t *> ing, int mode, int trim_qual, int sub, uint64_t piece_bytes,
-           uint64_t carry_bytes)
-      : ing_(std::move(ing)), mode_(mode), trim_(trim_qual), sub_(sub), l_bc_((int)((unsigned)mode >> 24)) {
+  // ing: n_slots x G ingest contexts, slot-major (ing[slot * G + g] on GPU g); key_of(max_len): the
+  // batch-level key that groups share
+  FastqGpu(const char *fn, std::vector<ibwa_ctx_t *> ing, int G, int mode, int trim_qual, int sub,
+           uint64_t piece_bytes, uint64_t carry_bytes, std::function<int(int)> key_of)
+      : all_(std::move(ing)), G_(G), mode_(mode), trim_(trim_qual), sub_(sub), l_bc_((int)((unsigned)mode >> 24)),
+        key_of_(std::move(key_of)) {
+    n_slots_ = G_ > 0 ? (int)all_.size() / G_ : 0;
+    busy_.assign(std::max(n_slots_, 1), 0);
     fd_ = open(fn, O_RDONLY);
     struct stat st;
     fsize_ = fd_ >= 0 && fstat(fd_, &st) == 0 ? (uint64_t)st.st_size : 0;
@@ -67,16 +81,24 @@ class FastqGpu {
     const uint64_t fs = std::max<uint64_t>((fsize_ + 4095) / 4096 * 4096, 4096);
     piece_ = std::max<uint64_t>(piece_bytes, 4096);
     carry_ = std::min<uint64_t>(std::max<uint64_t>(carry_bytes, 4096), fs);
-    chunk_ = std::min<uint64_t>(piece_ * ing_.size(), fs);
+    chunk_ = std::min<uint64_t>(piece_ * G_, fs);
     for (auto &b : buf_) {
       void *p = nullptr;
       if (ibwa_host_alloc(carry_ + chunk_ + 64, &p)) { ok_ = false; return; }
       b = static_cast<char *>(p);
     }
-    ok_ = fd_ >= 0;
-    if (ok_) start_read(0);
+    ok_ = fd_ >= 0 && n_slots_ >= 1;
+    if (!ok_) return;
+    start_read(0);
+    producer_ = std::thread([this]() { produce(); });
   }
   ~FastqGpu() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (producer_.joinable()) producer_.join();
     if (reader_.joinable()) reader_.join();
     for (char *b : buf_) ibwa_host_free(b);
     if (fd_ >= 0) close(fd_);
@@ -88,27 +110,40 @@ class FastqGpu {
   double parse_s() const { return parse_s_; }
   double dev_ms() const { return dev_ms_; }
   int64_t records() const { return n_records_; }
+  // GPU g's ingest context of a group
+  ibwa_ctx_t *ctx_of(const DevGroup &d, int g) const { return all_[(size_t)d.slot * G_ + g]; }
 
-  // The next group, false when the GPU path is over (the input ended, or handoff()).  All of the
-  // previous region's groups must have been staged before the call that parses a new region.
-  template <class KeyFn>
-  bool next(DevGroup &g, KeyFn key_of) {
-    for (;;) {
-      if (gi_ < groups_.size()) {
-        g = std::move(groups_[gi_++]);
-        return true;
-      }
-      if (after_ != NEXT) {
-        handoff_ = after_ == HANDOFF;
-        return false;
-      }
-      after_ = parse_region(key_of);
+  // The next group in input order, false when the GPU path is over (the input ended, or handoff()).
+  bool next(DevGroup &g) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&]() { return !queue_.empty() || finished_; });
+    if (queue_.empty()) return false;
+    g = std::move(queue_.front());
+    queue_.pop_front();
+    return true;
+  }
+  // a group's reads are no longer used (its alignment has been fetched): its slot may be parsed over
+  // once all of its region's groups are released
+  void release(const DevGroup &g) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      --busy_[g.slot];
     }
+    cv_.notify_all();
   }
 
  private:
-  std::vector<ibwa_ctx_t *> ing_;
+  std::vector<ibwa_ctx_t *> all_;  // slot-major ingest contexts
+  std::vector<ibwa_ctx_t *> ing_;  // the slot being parsed
+  int G_ = 1, n_slots_ = 0;
   int mode_, trim_, sub_, l_bc_;
+  std::function<int(int)> key_of_;
+  std::thread producer_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<DevGroup> queue_;
+  std::vector<int> busy_;  // per slot: groups of its region not yet released
+  bool stop_ = false, finished_ = false;
   int fd_ = -1;
   uint64_t fsize_ = 0, piece_ = 0, carry_ = 0, chunk_ = 0;
   char *buf_[2] = {nullptr, nullptr};
@@ -121,9 +156,40 @@ class FastqGpu {
   uint64_t got_[2] = {0, 0};
   std::thread reader_;
   std::vector<DevGroup> groups_;
-  size_t gi_ = 0;
   double parse_s_ = 0, dev_ms_ = 0;
   int64_t n_records_ = 0;
+
+  // regions in turn, slot r % n_slots, each once the slot's previous region is released
+  void produce() {
+    int after = NEXT;
+    for (int64_t region = 0; after == NEXT; ++region) {
+      const int slot = (int)(region % n_slots_);
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&]() { return stop_ || busy_[slot] == 0; });
+        if (stop_) break;
+      }
+      ing_.assign(all_.begin() + (size_t)slot * G_, all_.begin() + (size_t)(slot + 1) * G_);
+      after = parse_region();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        busy_[slot] = (int)groups_.size();
+        for (auto &g : groups_) {
+          g.slot = slot;
+          queue_.push_back(std::move(g));
+        }
+        groups_.clear();
+        if (after != NEXT) {
+          handoff_ = after == HANDOFF;
+          finished_ = true;
+        }
+      }
+      cv_.notify_all();
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    finished_ = true;
+    cv_.notify_all();
+  }
 
   // chunk at file offset next_off_ into buf_[b] + carry_, by several threads
   void start_read(int b) {
@@ -158,10 +224,9 @@ class FastqGpu {
   // Parse the region in buf_[cur_] and form its groups; after them: 1 the next region, 0 the end
   // of the input, -1 the host readers from handoff_off_.
   enum { NEXT = 1, END = 0, HANDOFF = -1 };
-  int after_ = NEXT;
 
-  template <class KeyFn>
-  int parse_region(KeyFn key_of) {
+  int parse_region() {
+    auto key_of = key_of_;
     reader_.join();
     const uint64_t got = got_[cur_];
     const bool eof = next_off_ >= fsize_;
@@ -171,7 +236,6 @@ class FastqGpu {
     // parsed and aligned (that buffer's previous region went to the GPUs with its parse)
     if (!eof) start_read(cur_ ^ 1);
     groups_.clear();
-    gi_ = 0;
     if (n == 0) return END;
     // pieces: one per GPU, split at strict record starts (readers.h FastqBulk::rec_at)
     const int G = (int)ing_.size();

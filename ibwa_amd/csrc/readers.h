@@ -164,7 +164,7 @@ struct SeqReader {
 // byte, looking for the next '@' or '>' -- is the one kseq_read would be in.
 struct FastqBulk {
   struct Rec {
-    uint64_t s, q;  // offsets of the sequence and quality lines in blk
+    uint64_t h, s, q;  // offsets of the header (its '@'), the sequence and the quality lines in blk
     uint32_t len;
   };
   SeqReader &rd;
@@ -209,6 +209,7 @@ struct FastqBulk {
       if (c < 33 || c > 127) return -1;
     }
     if (u[L] != '\n') return -1;
+    r.h = (uint64_t)(p - base);
     r.s = (uint64_t)(sq - base);
     r.q = (uint64_t)(u - base);
     r.len = (uint32_t)L;

@@ -469,8 +469,46 @@ int infer_isize(const std::vector<Read> &s0, const std::vector<Read> &s1, Isize 
 }
 
 // ---------------------------------------------------------------- read sources (bwa_open_reads, bwtaln.c:159-171)
+// next_read's record (bwa_read_seq, bwaseqio.c:145-208) from a strict FASTQ record of the bulk
+// parser: false for a record bwa_read_seq skips (not longer than the barcode)
+inline bool rec_to_read(const char *base, const ibwa_cli::FastqBulk::Rec &r, int mode, int trim_qual, Read &p) {
+  const bool is_comp = mode & IBWA_MODE_COMPREAD;
+  const bool is_64 = mode & IBWA_MODE_IL13;
+  const int l_bc = (int)((unsigned)mode >> 24);
+  const int L = (int)r.len;
+  if (L <= l_bc) return false;
+  const char *s = base + r.s, *q = base + r.q;
+  p = Read();
+  auto qv = [&](int i) { return is_64 ? (char)(q[i] - 31) : q[i]; };
+  if (l_bc) {
+    for (int i = 0; i < l_bc; ++i) p.bc[i] = qv(i) - 33 < 13 ? (char)tolower(s[i]) : (char)toupper(s[i]);
+    p.bc[l_bc] = 0;
+  }
+  const int n = L - l_bc;
+  p.full_len = p.clip_len = p.len = n;
+  p.seq.resize(n);
+  for (int i = 0; i < n; ++i) p.seq[i] = nt4[(unsigned char)s[l_bc + i]];
+  p.qual.resize(n);
+  for (int i = 0; i < n; ++i) p.qual[i] = qv(l_bc + i);
+  p.has_qual = true;
+  if (trim_qual >= 1) trim_read(trim_qual, p);
+  p.rseq.assign(n, 0);
+  for (int i = 0; i < p.len; ++i) {
+    const uint8_t c = p.seq[p.len - 1 - i];
+    p.rseq[i] = is_comp && c < 4 ? 3 - c : c;
+  }
+  // kseq's name: the header up to its first white space; then /[12]$ trimmed
+  const char *h = base + r.h + 1, *e = h;
+  while (*e != '\n' && !isspace((unsigned char)*e)) ++e;
+  size_t t = (size_t)(e - h);
+  if (t > 2 && h[t - 2] == '/' && (h[t - 1] == '1' || h[t - 1] == '2')) t -= 2;
+  p.name.assign(h, t);
+  return true;
+}
+
 struct Source {
   std::unique_ptr<ibwa_cli::SeqReader> fq;
+  std::unique_ptr<ibwa_cli::FastqBulk> fb;  // strict FASTQ records in bulk, before the serial reader
   std::unique_ptr<ibwa_cli::BamReader> bam;
   int mode = 0, trim_qual = 0;
   bool open(const char *fn, const ibwa_gap_opt_t &opt) {
@@ -486,9 +524,41 @@ struct Source {
       return bam->open(fn, which);
     }
     fq.reset(new ibwa_cli::SeqReader);
-    return fq->open(fn);
+    if (!fq->open(fn)) return false;
+    if (!getenv("IBWA_SAMPE_SERIAL_READ")) fb.reset(new ibwa_cli::FastqBulk(*fq));
+    return true;
   }
   bool next(Read &r) { return bam ? next_read(*bam, mode, trim_qual, r) : next_read(*fq, mode, trim_qual, r); }
+  // reads appended to out up to n_max: the bulk parser's records on nt threads, then record by
+  // record (the same reads in the same order as next() alone)
+  void take(std::vector<Read> &out, size_t n_max, int nt) {
+    auto par = [](int k, const std::function<void(int)> &g) {
+      std::vector<std::thread> th;
+      for (int t = 1; t < k; ++t) th.emplace_back(g, t);
+      g(0);
+      for (auto &x : th) x.join();
+    };
+    while (fb && out.size() < n_max && fb->more(nt, par)) {
+      const size_t i0 = fb->qi, m = std::min(fb->recs.size() - i0, n_max - out.size());
+      const size_t o = out.size();
+      out.resize(o + m);
+      std::vector<uint8_t> keep(m);
+      const char *base = fb->blk.data();
+      parallel_chunks((int64_t)m, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t k = lo; k < hi; ++k) keep[k] = rec_to_read(base, fb->recs[i0 + k], mode, trim_qual, out[o + k]);
+      }, nt);
+      size_t w = o;
+      for (size_t k = 0; k < m; ++k)
+        if (keep[k]) {
+          if (w != o + k) out[w] = std::move(out[o + k]);
+          ++w;
+        }
+      out.resize(w);
+      fb->qi = i0 + m;
+    }
+    Read r;
+    while (out.size() < n_max && next(r)) out.push_back(std::move(r));
+  }
 };
 
 // ---------------------------------------------------------------- the batch loop (bwa_sai2sam_pe_core)
@@ -661,8 +731,7 @@ struct Sampe {
     auto rd = [this, src](int j) {
       nxt[j].clear();
       nxt[j].reserve(0x40000);
-      Read r;
-      while ((int)nxt[j].size() < 0x40000 && src[j].next(r)) nxt[j].push_back(std::move(r));
+      src[j].take(nxt[j], 0x40000, std::max(1, host_threads() / 2));
       // alngrp_create per read, in read order (saiset.c:45-76)
       const size_t n = nxt[j].size();
       nflat[j].clear();
@@ -735,6 +804,7 @@ struct Sampe {
       std::vector<double> rcache(2 * (size_t)n);
       for (int i = 0; i < n; ++i)  // the drand48 stream, in pair order
         for (int j = 0; j < 2; ++j) select_rng(alns[j][i], midx[2 * i + j], rcache[2 * i + j]);
+      ph.mark("hit choice: drand48");
       parallel_ordered(n, [&](int64_t lo, int64_t hi_, int) {
         for (int64_t i = lo; i < hi_; ++i)
           for (int j = 0; j < 2; ++j) {
@@ -744,6 +814,7 @@ struct Sampe {
             chosen[j][i] = select_sai(alns[j][i], p, pick[j][i], midx[2 * i + j], rcache[2 * i + j]) ? 1 : 0;
           }
       }, 0, 1024);
+      ph.mark("hit choice: select");
     }
     std::vector<int> hd;
     std::vector<uint8_t> hs;
@@ -757,9 +828,10 @@ struct Sampe {
           hs.push_back((uint8_t)p.strand); hk.push_back(p.sa); hl.push_back((uint32_t)p.len);
           hi.push_back(2 * i + j);
         }
-    ph.mark("sai+hit choice");
+    ph.mark("hit choice: row lists");
     std::vector<uint64_t> pos;
     if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
+    ph.mark("sa2pos: kernel");
     std::vector<uint8_t> ok(hi.size(), 0);
     auto remap_main = [&](size_t t) {
       const int i = hi[t] >> 1, j = hi[t] & 1;
@@ -773,6 +845,7 @@ struct Sampe {
     parallel_ordered((int64_t)hi.size(), [&](int64_t lo, int64_t hi_, int) {
       for (int64_t t = lo; t < hi_; ++t) remap_main((size_t)t);
     });
+    ph.mark("sa2pos: remap");
     // the other rows of the main alignment, cyclically from the chosen one (bwape.c:336-357), for
     // the reads whose remap failed: their rows in one launch per reference (bounded per launch)
     {
@@ -837,6 +910,7 @@ struct Sampe {
       ii.low = ii.high = 0;
       ii.avg = ii.std = -1.0;
     }
+    ph.mark("isize");
     // ---- every row of every interval (compute_seq_coords_and_counts): one SA->pos launch per
     // reference.  Rows of intervals narrower than kMinHashWidth are computed per (read, alignment);
     // wider ones come from the reference's cache, filled on first use with that caller's strand
@@ -875,13 +949,14 @@ struct Sampe {
         }
       }
     }
-    ph.mark("isize+rows");
+    ph.mark("rows");
     if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
+    ph.mark("rows: sa2pos kernel");
     for (auto &f : fill) {
       const uint32_t k = (uint32_t)(f.first.second >> 32), l = (uint32_t)f.first.second;
       cache[f.first.first][f.first.second].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
     }
-    ph.mark("sa2pos");
+    ph.mark("rows: cache");
     // ---- select_sai_multi's rows that the -R pass did not compute (no -R, or a cached interval):
     // for every read that can take the multi list (n_occ <= max(n, N) + 1), in one launch
     std::vector<int64_t> mfirst[2];
@@ -921,12 +996,19 @@ struct Sampe {
     std::vector<uint64_t> poff(n, 0);
     std::vector<int> pth(n, 0);
     std::vector<uint8_t> paired(n, 0);
+    static const bool pstats = getenv("IBWA_SAMPE_STATS") != nullptr;
+    std::atomic<int64_t> t_pos{0}, t_cnt{0}, t_sort{0};  // ns in the rows' remap, the c1 / c2 count, the sort
+    auto now_ns = []() {
+      return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
     parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
       PosArr arr;
       std::vector<std::pair<uint64_t, int>> ps;
+      int64_t a_pos = 0, a_cnt = 0, a_sort = 0;
       for (int64_t i = lo; i < hi_; ++i) {
         Read *p[2] = {&seqs[0][i], &seqs[1][i]};
         arr.clear();
+        int64_t t0 = pstats ? now_ns() : 0;
         if (popt.remapping) {
           for (int j = 0; j < 2; ++j) {
             // compute_seq_coords_and_counts (filter_alignments.cpp:53-140): positions inside their
@@ -960,6 +1042,8 @@ struct Sampe {
                 ps.push_back({ap.remapped_pos, a.score});
               }
             }
+            const int64_t t1 = pstats ? now_ns() : 0;
+            if (pstats) a_pos += t1 - t0;
             std::sort(ps.begin(), ps.end());
             size_t c[2] = {0, 0};
             for (size_t t = 0; t < ps.size(); ++t)
@@ -967,6 +1051,11 @@ struct Sampe {
             p[j]->c1 = (uint32_t)c[0] & 0xfffffffu;
             p[j]->c2 = (uint32_t)c[1] & 0xfffffffu;
             if (p[j]->c1 != 0) p[j]->type = p[j]->c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
+            if (pstats) {
+              const int64_t t2 = now_ns();
+              a_cnt += t2 - t1;
+              t0 = t2;
+            }
           }
         }
         for (int j = 0; j < 2; ++j)
@@ -975,11 +1064,15 @@ struct Sampe {
         const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
         paired[i] = m0 && m1;
         if (paired[i]) ks_introsort(arr.n, arr.a.data(), position_lt);  // find_optimal_pair's sort
+        if (pstats) a_sort += now_ns() - t0;
         pth[i] = th;
         poff[i] = pstore[th].size();
         pcnt[i] = (uint32_t)arr.n;
         pstore[th].insert(pstore[th].end(), arr.a.begin(), arr.a.begin() + arr.n);
       }
+      t_pos += a_pos;
+      t_cnt += a_cnt;
+      t_sort += a_sort;
     }, nth);
     ph.mark("pairing: positions");
     std::vector<const Position *> parr(n);
@@ -1003,8 +1096,9 @@ struct Sampe {
     if (getenv("IBWA_SAMPE_STATS")) {
       uint64_t tot = 0, mx = 0;
       for (int i = 0; i < n; ++i) { tot += pcnt[i]; mx = std::max<uint64_t>(mx, pcnt[i]); }
-      fprintf(stderr, "[ibwa-amd sampe] batch of %d pairs: %llu positions (max %llu per pair), %zu rows computed\n", n,
-              (unsigned long long)tot, (unsigned long long)mx, pos.size());
+      fprintf(stderr, "[ibwa-amd sampe] batch of %d pairs: %llu positions (max %llu per pair), %zu rows computed; "
+              "positions pass thread-ms: rows %.0f, c1/c2 %.0f, sort %.0f\n", n, (unsigned long long)tot,
+              (unsigned long long)mx, pos.size(), t_pos * 1e-6, t_cnt * 1e-6, t_sort * 1e-6);
     }
     std::vector<int> chg(nth, 0);
     parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
@@ -1038,6 +1132,7 @@ struct Sampe {
     for (int j = 0; j < 2; ++j)
       for (Read &r : seqs[j]) rp.push_back(&r);
     if (int rc = refine_gapped(ctx[0], dbs, rp)) return rc == 1 ? 1 : die("global alignment");
+    ph.mark("refine");
     for (int j = 0; j < 2; ++j) {
       for (Read &r : seqs[j]) {
         int status = 0;
@@ -1048,7 +1143,7 @@ struct Sampe {
         }
       }
     }
-    ph.mark("refine+md");
+    ph.mark("remap after refine");
     // ---- print: with -R the remapped (primary) coordinates, the original ones as ZR
     print_parallel(o, n, [&](Out &ob, int64_t i) {
       Read *p[2] = {&seqs[0][i], &seqs[1][i]};
@@ -1141,6 +1236,7 @@ struct Sampe {
         }
       });
     }
+    ph.mark("paired SW: mirrors");
     ibwa_ref_pe_opt_t po;
     memset(&po, 0, sizeof po);
     po.max_isize = popt.max_isize; po.force_isize = popt.force_isize; po.max_occ = popt.max_occ;
@@ -1160,6 +1256,7 @@ struct Sampe {
     if (ibwa_paired_sw_dbs(ctx[0], n, sp, &po, &ri, (int)pacs.size(), pacs.data(), offs.data(), lens.data(), n_tot,
                            n_mapped))
       return die("paired SW");
+    ph.mark("paired SW: windows+SW+fix-up");
     fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 singletons are mated.\n", (unsigned long long)n_mapped[1],
             (unsigned long long)n_tot[1]);
     fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 discordant pairs are fixed.\n", (unsigned long long)n_mapped[0],

@@ -135,7 +135,8 @@ int ibwa_fq_offset(const ibwa_ctx_t *ctx, int64_t r, uint64_t *off);
 /* kept reads and device time (H2D copy + kernels, ms) of the last ibwa_fq_parse */
 int ibwa_fq_stats(const ibwa_ctx_t *ctx, int64_t *kept, double *ms);
 /* ibwa_batch_stage from src's last parsed block (same device): its kept reads [first, first + n),
- * copied device to device; max_len = their longest */
+ * max_len = their longest.  Nothing is copied: the batch is a view of src's block, which must not be
+ * parsed over (ibwa_fq_parse on src) or destroyed while this context runs or fetches the batch. */
 int ibwa_batch_stage_fq(ibwa_ctx_t *ctx, const ibwa_ctx_t *src, int64_t first, int64_t n, int max_len);
 /* pinned host memory for the raw blocks */
 int ibwa_host_alloc(uint64_t bytes, void **p);
@@ -210,14 +211,21 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "gap_early2_iters", "gap_early2_entries" (0, 0)  a second such rule (0: off)
  *   "gap_resume" (0/1, default 1), "gap_resume_gb" (48)  an early hand-off leaves the read's search
  *                                  state (at the next score-level boundary) for the cooperative pass,
- *                                  which resumes it instead of starting over; state buffer size
+ *                                  which resumes it instead of starting over; state buffer size cap
  *                                  ("gap_resume_records": the buffer in 16 B records, for tests)
+ *   "gap_resume_recs" (192)        state buffer records per read of a first-pass chunk, or 1.15 x the
+ *                                  most an earlier run of the context needed, if more (states that do
+ *                                  not fit start over in the cooperative pass: same hits)
  *   "gap_resume_iters", "gap_resume_entries" (2000, 300)  the early hand-off rule when states are left
- *   "gap_resume_ppb" (96), "gap_resume_cap1" (4096)  first-pass pool pages per 256 lanes and static
+ *   "gap_resume_ppb" (48), "gap_resume_cap1" (4096)  first-pass pool pages per 256 lanes and static
  *                                  slots per lane when states are left (at most the values above)
  *   "gap_tail_lanes", "gap_tail_iters" (16, 200)  also leave a state when no read is left to claim and
  *                                  at most that many lanes of the wave are busy (0: off)
- *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool */
+ *   "coop_waves_per_cu" (12), "coop_pool_gb" (16)  cooperative pass residency and page pool (reads
+ *                                  that run out of its pages run again in up to two more launches with
+ *                                  the whole pool, then the wide kernel; "coop_pool_pages": the pool
+ *                                  in pages, for tests)
+ *   "coop_stg_room" (1)            its per-lane staging ring holds this many chains' children (1..4) */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
 /* The sources this library was built from: the first 16 hex digits of the SHA-256 of the

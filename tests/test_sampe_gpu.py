@@ -85,3 +85,39 @@ def test_aln_pe_reads_match_reference_sai(golden_dir, key, tmp_path):
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-2000:]
         assert oracle.sai_body_equal(out.read_bytes(), open(os.path.join(golden_dir, sai), "rb").read())
+
+
+@pytest.mark.parametrize("aln_opts", [["-B", "5"], ["-I", "-q", "15"], []])
+def test_sampe_bulk_reader_equals_serial(golden_dir, aln_opts, tmp_path):
+    """sampe's reads come from the bulk FASTQ parser on host threads (sampe_main.cpp Source::take,
+    rec_to_read) until the first record it does not take, then from the serial kseq reader
+    (bwaseqio.c:145-208).  With barcodes (-B), Illumina 1.3 qualities (-I) and trimming (-q) in the
+    .sai header's mode, and end 2 holding a multi-line record midway (the hand-over), the SAM equals
+    the one of the serial reader alone (IBWA_SAMPE_SERIAL_READ=1) byte for byte."""
+    g = lambda x: os.path.join(golden_dir, x)  # noqa: E731
+    recs = open(g("pe100_2.fq")).read().split("\n")
+    k = 4 * (len(recs) // 8)  # a record in the middle: its sequence over two lines
+    s = recs[k + 1]
+    recs[k + 1] = s[:40] + "\n" + s[40:]
+    fq2 = tmp_path / "r2.fq"
+    fq2.write_text("\n".join(recs))
+    fq = [g("pe100_1.fq"), str(fq2)]
+    sai = []
+    for j, f in enumerate(fq):
+        out = tmp_path / f"{j}.sai"
+        r = subprocess.run([CLI, "aln"] + aln_opts + ["-f", str(out), g("g1m"), f], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        sai.append(str(out))
+    outs = []
+    for serial in (False, True):
+        out = tmp_path / f"out{int(serial)}.sam"
+        env = dict(os.environ)
+        if serial:
+            env["IBWA_SAMPE_SERIAL_READ"] = "1"
+        r = subprocess.run([CLI, "sampe", "-R", "-f", str(out), g("g1m"), *sai, *fq], capture_output=True, text=True,
+                           timeout=120, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(_body(out.read_text()))
+    assert len(outs[0]) > 1000
+    assert outs[0] == outs[1]

@@ -136,6 +136,10 @@ def test_exact_reads_round_trip(mid_genome):
     (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_tail_lanes": 64, "gap_tail_iters": 1}),
     # a 1 GiB page pool: resumed reads that run out of pages start over in the later passes
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "coop_pool_gb": 1}),
+    # pools of a few pages: the reads out of pages run again in launches of their own, then go on to
+    # the wide kernel
+    ([], 100, 0.02, 4_000, {"gap_iter_budget": 1, "coop_pool_pages": 48}),
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "coop_pool_pages": 256}),
     ([], 100, 0.01, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4, "gap_resume": 0})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
@@ -145,7 +149,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
                 "gap_resume_entries": 300, "coop_pool_gb": 16, "gap_tail_lanes": 16, "gap_tail_iters": 200,
-                "gap_lw_min_waves": 8}
+                "gap_lw_min_waves": 8, "coop_pool_pages": 0}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)

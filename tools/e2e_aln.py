@@ -98,10 +98,14 @@ def run(argv, timeout=1800, env=None):
             log("  cli:", ln.strip())
             phases["parse only"] = {"reads": int(m.group(1)), "parse_s": float(m.group(2)),
                                     "reads_per_s": int(m.group(1)) / max(float(m.group(2)), 1e-9)}
-        m = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s waiting for the parse \((\d+) ms of device", ln)
+        m = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s parsing ahead of the alignment \((\d+) ms of device", ln)
         if m:
             log("  cli:", ln.strip())
-            phases["gpu parse"] = {"records": int(m.group(1)), "wait_s": float(m.group(2)), "device_ms": int(m.group(3))}
+            phases["gpu parse"] = {"records": int(m.group(1)), "producer_s": float(m.group(2)), "device_ms": int(m.group(3))}
+        m = re.search(r"device memory: peak ([\d.]+) GB", ln)
+        if m:
+            log("  cli:", ln.strip())
+            phases["device_memory_peak_gb"] = float(m.group(1))
         m = re.search(r"input parse: (\d+) reads in ([\d.]+) s on (\d+) host threads", ln)
         if m:
             log("  cli:", ln.strip())

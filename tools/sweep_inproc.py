@@ -26,7 +26,9 @@ DEFAULTS = {"gap_early_iters": 3000, "gap_early_entries": 1000, "gap_iter_budget
             "gap_early2_iters": 0, "gap_early2_entries": 0, "gap_resume": 1, "gap_resume_gb": 48,
             "coop_roots": 1, "gap_reads_per_chunk": 16 << 20,
             "gap_resume_iters": 2000, "gap_resume_entries": 300, "gap_tail_lanes": 16, "gap_tail_iters": 200,
-            "gap_pages_per_block": 384, "gap_cap1": 8192}
+            "gap_pages_per_block": 384, "gap_cap1": 8192, "gap_resume_ppb": 48, "gap_resume_cap1": 4096,
+            "coop_pool_gb": 16, "gap_lw_min_waves": 8, "coop_waves_per_cu": 12,
+            "coop_stg_room": 1, "gap_resume_recs": 192}
 
 
 def main():
@@ -34,6 +36,9 @@ def main():
     ap.add_argument("--reads", type=int, default=50_000_000)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--read-len", type=int, default=100)
+    ap.add_argument("--sub", type=float, default=0.01)
+    ap.add_argument("--indel", type=float, default=0.05)
     ap.add_argument("--out", default="gpurun_out/sweep_inproc.jsonl")
     ap.add_argument("configs", nargs="*", default=[""])
     a = ap.parse_args()
@@ -44,7 +49,7 @@ def main():
     th = bench.host_threads()
     t0 = time.perf_counter()
     ascii_, codes, lens, _ = bench.make_genome(int(a.scale * 1e6), 1_000_000, 37, th)
-    seq, off, lns = bench.make_reads(ascii_, lens, 3, a.reads, 100, 0.01, 0.05, th)
+    seq, off, lns = bench.make_reads(ascii_, lens, 3, a.reads, a.read_len, a.sub, a.indel, th)
     del ascii_
     eng = E.Engine(0)
     eng.build_index(codes, sa_intv=0)
@@ -75,7 +80,9 @@ def main():
             rec = {"config": cfg, "ms_per_step": float(np.mean(ms)), "ms": ms, "n_heavy": int(st.n_heavy),
                    "width": st.ms_width, "gapped": st.ms_search, "coop": st.ms_coop, "retry": st.ms_retry,
                    "coop_roots": st.ms_coop_roots, "coop_width": st.ms_coop_width, "n_resumed": int(st.n_resumed),
-                   "resume_records": int(st.resume_records),
+                   "resume_records": int(st.resume_records), "resume_records_peak": int(st.resume_records_peak),
+                   "coop_pages_peak": int(st.coop_pages_peak), "coop_pages_cap": int(st.coop_pages_cap),
+                   "lib_bytes": E.Engine.device_bytes(),
                    "hits_equal_first_config": same}
             print(json.dumps(rec), flush=True)
             fo.write(json.dumps(rec) + "\n")
