@@ -840,10 +840,16 @@ struct Out {
   Out &s(const char *x) { b += x; return *this; }
   Out &s(const std::string &x) { b += x; return *this; }
   Out &c(char x) { b += x; return *this; }
-  Out &i(long long v) {
-    char t[32];
-    snprintf(t, sizeof t, "%lld", v);
-    b += t;
+  Out &i(long long v) {  // %lld
+    char t[24];
+    char *e = t + sizeof t, *q = e;
+    unsigned long long u = v < 0 ? 0ull - (unsigned long long)v : (unsigned long long)v;
+    do {
+      *--q = (char)('0' + u % 10);
+      u /= 10;
+    } while (u);
+    if (v < 0) *--q = '-';
+    b.append(q, (size_t)(e - q));
     return *this;
   }
 };

@@ -156,6 +156,10 @@ struct Position {  // position_t (bwapair.h:13-25)
   int dbidx = 0, remapped_dbidx = 0, remapped_seqid = 0, remap_identical = 0;
   int n_gapo = 0, n_gape = 0, len = 0, score = 0;
 };
+struct PosKey {  // a position's sort key (position_lt's fields) and its index
+  uint64_t rp, p;
+  uint32_t idx;
+};
 inline bool position_lt(const Position &a, const Position &b) {  // bwapair.c:22-28
   if (a.remapped_pos == b.remapped_pos) return a.pos < b.pos;
   return a.remapped_pos < b.remapped_pos;
@@ -627,6 +631,11 @@ struct Sampe {
   int sa2pos(const std::vector<int> &db, const std::vector<uint8_t> &st, const std::vector<uint32_t> &k,
              const std::vector<uint32_t> &len, std::vector<uint64_t> &pos) {
     pos.assign(k.size(), 0);
+    if (ctx.size() == 1) {  // one reference: the lists as they are
+      if (!k.empty() && ibwa_sa2pos(ctx[0], (int64_t)k.size(), st.data(), k.data(), len.data(), dbs.db[0].offset, pos.data()))
+        return die("sa2pos");
+      return 0;
+    }
     for (size_t d = 0; d < ctx.size(); ++d) {
       std::vector<size_t> idx;
       for (size_t t = 0; t < k.size(); ++t)
@@ -920,34 +929,63 @@ struct Sampe {
     hd.clear(); hs.clear(); hk.clear(); hl.clear();
     std::vector<std::pair<std::pair<int, uint64_t>, int64_t>> fill;  // new cache keys -> first row
     if (popt.remapping) {
+      // alignment slots in (pair, end, alignment) order; the narrow intervals' rows at offsets from
+      // per-pair counts, filled on the host threads; then the wide ones in pair order (the first use
+      // of an interval fills the cache), behind them
       for (int j = 0; j < 2; ++j) row0[j].assign(n + 1, 0);
-      for (int i = 0; i < n; ++i) {
+      int64_t na = 0;
+      for (int i = 0; i < n; ++i)
         for (int j = 0; j < 2; ++j) {
-          row0[j][i] = (int64_t)aslot.size();
-          for (const Aln &al : alns[j][i]) {
-            const ibwa_aln1_t &a = al.aln;
-            const uint32_t w = a.l - a.k + 1;
-            auto rows = [&]() {
-              for (uint32_t r = 0; r < w; ++r) {
-                hd.push_back(al.dbidx); hs.push_back((uint8_t)a.a); hk.push_back(a.k + r);
-                hl.push_back((uint32_t)seqs[j][i].len);
+          row0[j][i] = na;
+          na += (int64_t)alns[j][i].size();
+        }
+      aslot.assign(na, -1);
+      std::vector<int64_t> r0(n + 1, 0);
+      parallel_chunks(n, [&](int64_t lo, int64_t hi_, int) {
+        for (int64_t i = lo; i < hi_; ++i) {
+          int64_t c = 0;
+          for (int j = 0; j < 2; ++j)
+            for (const Aln &al : alns[j][i]) {
+              const uint32_t w = al.aln.l - al.aln.k + 1;
+              if (w < kMinHashWidth) c += w;
+            }
+          r0[i + 1] = c;
+        }
+      });
+      for (int i = 0; i < n; ++i) r0[i + 1] += r0[i];
+      hd.resize(r0[n]); hs.resize(r0[n]); hk.resize(r0[n]); hl.resize(r0[n]);
+      parallel_chunks(n, [&](int64_t lo, int64_t hi_, int) {
+        for (int64_t i = lo; i < hi_; ++i) {
+          int64_t o = r0[i];
+          for (int j = 0; j < 2; ++j) {
+            const AlnSpan &ag = alns[j][i];
+            for (size_t k = 0; k < ag.size(); ++k) {
+              const ibwa_aln1_t &a = ag[k].aln;
+              const uint32_t w = a.l - a.k + 1;
+              if (w >= kMinHashWidth) continue;
+              aslot[row0[j][i] + (int64_t)k] = o;
+              for (uint32_t r = 0; r < w; ++r, ++o) {
+                hd[o] = ag[k].dbidx; hs[o] = (uint8_t)a.a; hk[o] = a.k + r; hl[o] = (uint32_t)seqs[j][i].len;
               }
-            };
-            if (w >= kMinHashWidth) {
-              const uint64_t key = (uint64_t)a.k << 32 | a.l;
-              if (!cache[al.dbidx].count(key)) {
-                fill.push_back({{al.dbidx, key}, (int64_t)hk.size()});
-                cache[al.dbidx][key];  // reserve: later uses in this batch share it
-                rows();
-              }
-              aslot.push_back(-1);
-            } else {
-              aslot.push_back((int64_t)hk.size());
-              rows();
             }
           }
         }
-      }
+      });
+      for (int i = 0; i < n; ++i)
+        for (int j = 0; j < 2; ++j)
+          for (const Aln &al : alns[j][i]) {
+            const ibwa_aln1_t &a = al.aln;
+            const uint32_t w = a.l - a.k + 1;
+            if (w < kMinHashWidth) continue;
+            const uint64_t key = (uint64_t)a.k << 32 | a.l;
+            if (cache[al.dbidx].count(key)) continue;
+            fill.push_back({{al.dbidx, key}, (int64_t)hk.size()});
+            cache[al.dbidx][key];  // reserve: later uses in this batch share it
+            for (uint32_t r = 0; r < w; ++r) {
+              hd.push_back(al.dbidx); hs.push_back((uint8_t)a.a); hk.push_back(a.k + r);
+              hl.push_back((uint32_t)seqs[j][i].len);
+            }
+          }
     }
     ph.mark("rows");
     if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
@@ -1004,6 +1042,8 @@ struct Sampe {
     parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
       PosArr arr;
       std::vector<std::pair<uint64_t, int>> ps;
+      std::vector<PosKey> pk;
+      std::vector<Position> tmp;
       int64_t a_pos = 0, a_cnt = 0, a_sort = 0;
       for (int64_t i = lo; i < hi_; ++i) {
         Read *p[2] = {&seqs[0][i], &seqs[1][i]};
@@ -1063,7 +1103,22 @@ struct Sampe {
         const bool m0 = p[0]->type == TYPE_UNIQUE || p[0]->type == TYPE_REPEAT;
         const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
         paired[i] = m0 && m1;
-        if (paired[i]) ks_introsort(arr.n, arr.a.data(), position_lt);  // find_optimal_pair's sort
+        if (paired[i]) {  // find_optimal_pair's sort
+          if (arr.n > 32) {
+            // on 24-byte keys with the positions' indices: the introsort's moves depend only on the
+            // comparisons, so the permutation -- ties included -- is the one of the positions themselves
+            pk.resize(arr.n);
+            for (size_t t = 0; t < arr.n; ++t) pk[t] = {arr.a[t].remapped_pos, arr.a[t].pos, (uint32_t)t};
+            ks_introsort(arr.n, pk.data(), [](const PosKey &a, const PosKey &b) {
+              return a.rp == b.rp ? a.p < b.p : a.rp < b.rp;
+            });
+            tmp.resize(arr.n);
+            for (size_t t = 0; t < arr.n; ++t) tmp[t] = arr.a[pk[t].idx];
+            std::copy(tmp.begin(), tmp.end(), arr.a.begin());
+          } else {
+            ks_introsort(arr.n, arr.a.data(), position_lt);
+          }
+        }
         if (pstats) a_sort += now_ns() - t0;
         pth[i] = th;
         poff[i] = pstore[th].size();
@@ -1133,16 +1188,18 @@ struct Sampe {
       for (Read &r : seqs[j]) rp.push_back(&r);
     if (int rc = refine_gapped(ctx[0], dbs, rp)) return rc == 1 ? 1 : die("global alignment");
     ph.mark("refine");
-    for (int j = 0; j < 2; ++j) {
-      for (Read &r : seqs[j]) {
-        int status = 0;
-        remap(r, r.pos, r.dbidx, (uint64_t)r.len, (uint32_t)(r.n_gapo + r.n_gape), &status);
-        if (status == 0) {
-          fprintf(stderr, "Failed to remap read %s after refining gaps.\n", r.name.c_str());
-          unmap(r);
+    for (int j = 0; j < 2; ++j)
+      parallel_ordered(n, [&](int64_t lo, int64_t hi_, int) {
+        for (int64_t i = lo; i < hi_; ++i) {
+          Read &r = seqs[j][i];
+          int status = 0;
+          remap(r, r.pos, r.dbidx, (uint64_t)r.len, (uint32_t)(r.n_gapo + r.n_gape), &status);
+          if (status == 0) {
+            msg("Failed to remap read %s after refining gaps.\n", r.name.c_str());
+            unmap(r);
+          }
         }
-      }
-    }
+      }, 0, 4096);
     ph.mark("remap after refine");
     // ---- print: with -R the remapped (primary) coordinates, the original ones as ZR
     print_parallel(o, n, [&](Out &ob, int64_t i) {
