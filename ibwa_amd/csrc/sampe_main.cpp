@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "ibwa_bwa_compat.h"
+#include "ksort.h"
 #include "sam_common.h"
 
 using namespace ibwa_sam;
@@ -60,93 +61,6 @@ struct Isize {  // isize_info_t (bwapair.h:8-11)
 int die(const char *what) {
   fprintf(stderr, "[ibwa-amd sampe] %s: %s\n", what, ibwa_last_error());
   return 1;
-}
-
-// ---------------------------------------------------------------- klib ks_introsort (ksort.h:142-219)
-// Restated because the order of equal keys (not stable) decides which position find_optimal_pair
-// sees first.
-template <class T, class Lt>
-void ks_insertsort(T *s, T *t, Lt lt) {
-  for (T *i = s + 1; i < t; ++i)
-    for (T *j = i; j > s && lt(*j, *(j - 1)); --j) std::swap(*j, *(j - 1));
-}
-template <class T, class Lt>
-void ks_combsort(size_t n, T *a, Lt lt) {
-  const double shrink = 1.2473309501039786540366528676643;
-  bool do_swap;
-  size_t gap = n;
-  do {
-    if (gap > 2) {
-      gap = (size_t)(gap / shrink);
-      if (gap == 9 || gap == 10) gap = 11;
-    }
-    do_swap = false;
-    for (T *i = a; i < a + n - gap; ++i) {
-      T *j = i + gap;
-      if (lt(*j, *i)) {
-        std::swap(*i, *j);
-        do_swap = true;
-      }
-    }
-  } while (do_swap || gap > 2);
-  if (gap != 1) ks_insertsort(a, a + n, lt);
-}
-template <class T, class Lt>
-void ks_introsort(size_t n, T *a, Lt lt) {
-  struct Frame {
-    T *left, *right;
-    int depth;
-  };
-  if (n < 1) return;
-  if (n == 2) {
-    if (lt(a[1], a[0])) std::swap(a[0], a[1]);
-    return;
-  }
-  int d;
-  for (d = 2; 1ul << d < n; ++d) {}
-  std::vector<Frame> stack;
-  T *s = a, *t = a + (n - 1);
-  d <<= 1;
-  for (;;) {
-    if (s < t) {
-      if (--d == 0) {
-        ks_combsort((size_t)(t - s + 1), s, lt);
-        t = s;
-        continue;
-      }
-      T *i = s, *j = t, *k = i + ((j - i) >> 1) + 1;
-      if (lt(*k, *i)) {
-        if (lt(*k, *j)) k = j;
-      } else {
-        k = lt(*j, *i) ? i : j;
-      }
-      const T rp = *k;
-      if (k != t) std::swap(*k, *t);
-      for (;;) {
-        do ++i; while (lt(*i, rp));
-        do --j; while (i <= j && lt(rp, *j));
-        if (j <= i) break;
-        std::swap(*i, *j);
-      }
-      std::swap(*i, *t);
-      if (i - s > t - i) {
-        if (i - s > 16) stack.push_back({s, i - 1, d});
-        s = t - i > 16 ? i + 1 : t;
-      } else {
-        if (t - i > 16) stack.push_back({i + 1, t, d});
-        t = i - s > 16 ? i - 1 : s;
-      }
-    } else {
-      if (stack.empty()) {
-        ks_insertsort(a, a + n, lt);
-        return;
-      }
-      s = stack.back().left;
-      t = stack.back().right;
-      d = stack.back().depth;
-      stack.pop_back();
-    }
-  }
 }
 
 // ---------------------------------------------------------------- pairing (bwapair.c)
@@ -1262,20 +1176,21 @@ struct Sampe {
   // bwa_paired_sw through the C-ABI (compat.cpp) on bwa_seq_t mirrors of the batch
   int paired_sw(std::vector<Read> seqs[2], int n, const Isize &ii) {
     if (!popt.is_sw || ii.avg < 0.0) return 0;
-    std::vector<ibwa_ref_seq_t> ref[2];
-    std::vector<uint8_t> rev[2];
+    // the mirrors are filled in parallel below: no zero-filled allocation of a batch's worth first
+    std::unique_ptr<ibwa_ref_seq_t[]> ref[2];
+    std::unique_ptr<uint8_t[]> rev[2];
     for (int j = 0; j < 2; ++j) {
-      ref[j].assign(n, ibwa_ref_seq_t());
+      ref[j].reset(new ibwa_ref_seq_t[std::max(n, 1)]);
       std::vector<size_t> ro(n + 1, 0);
       for (int i = 0; i < n; ++i) ro[i + 1] = ro[i] + (size_t)seqs[j][i].len;
-      rev[j].resize(ro[n] + 1);
+      rev[j].reset(new uint8_t[ro[n] + 1]);
       parallel_chunks(n, [&](int64_t lo, int64_t hi, int) {
         for (int64_t i = lo; i < hi; ++i) {
           Read &r = seqs[j][i];
           ibwa_ref_seq_t &t = ref[j][i];
           memset(&t, 0, sizeof t);
-          std::reverse_copy(r.seq.begin(), r.seq.begin() + r.len, rev[j].begin() + ro[i]);  // bwa_seq_t.seq: reversed
-          t.seq = rev[j].data() + ro[i];
+          std::reverse_copy(r.seq.begin(), r.seq.begin() + r.len, rev[j].get() + ro[i]);  // bwa_seq_t.seq: reversed
+          t.seq = rev[j].get() + ro[i];
           t.rseq = r.rseq.data();
           t.len = (uint32_t)r.len;
           t.full_len = (uint32_t)r.full_len;
@@ -1301,7 +1216,7 @@ struct Sampe {
     po.type = popt.type; po.is_sw = popt.is_sw; po.is_preload = popt.is_preload; po.remapping = popt.remapping;
     po.ap_prior = popt.ap_prior;
     ibwa_ref_isize_info_t ri{ii.avg, ii.std, ii.ap_prior, ii.low, ii.high, ii.high_bayesian};
-    ibwa_ref_seq_t *sp[2] = {ref[0].data(), ref[1].data()};
+    ibwa_ref_seq_t *sp[2] = {ref[0].get(), ref[1].get()};
     uint64_t n_tot[2], n_mapped[2];
     std::vector<const uint8_t *> pacs;
     std::vector<uint64_t> offs, lens;
