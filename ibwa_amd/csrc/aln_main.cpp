@@ -535,8 +535,10 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
           auto ms = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
             return std::chrono::duration<double, std::milli>(y - x).count();
           };
-          fprintf(stderr, "[ibwa-amd aln] slice %d: %lld reads, stage %.1f run %.1f fetch %.1f ms\n", g,
-                  (long long)(e - b), ms(c0, c1) + sms, ms(c1, c2), ms(c2, c3));
+          ibwa_run_stats_t st;
+          ibwa_batch_stats(cx[g], &st);
+          fprintf(stderr, "[ibwa-amd aln] slice %d: %lld reads, stage %.1f run %.1f (of which allocating %.1f) fetch %.1f ms\n",
+                  g, (long long)(e - b), ms(c0, c1) + sms, ms(c1, c2), st.ms_alloc, ms(c2, c3));
         }
       });
     }

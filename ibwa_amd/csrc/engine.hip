@@ -42,6 +42,8 @@ int fail(int code, const char *fmt, ...) {
     if (e_ != hipSuccess) return fail(IBWA_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
   } while (0)
 
+// hipMalloc wall time of this thread (a run reports what it spent: ibwa_run_stats_t.ms_alloc)
+thread_local double g_alloc_ms = 0;
 // Device bytes the library's buffers hold (all contexts of the process) and their high-water mark.
 std::atomic<int64_t> g_dev_bytes{0}, g_dev_peak{0};
 void dev_bytes_add(int64_t d) {
@@ -71,6 +73,7 @@ struct DBuf {
     hipError_t e = hipMalloc(&p, want);
     if (e != hipSuccess) return fail(IBWA_EHIP, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    g_alloc_ms += ms;
     if (verbose && ms > 20.0) fprintf(stderr, "[ibwa_amd] hipMalloc(%.2f GB) took %.0f ms\n", want / 1e9, ms);
     cap = want;
     dev_bytes_add((int64_t)want);
@@ -1024,6 +1027,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   if (int rc = check_opt(opt)) return rc;
   HIPCHK(hipSetDevice(c->device));
   memset(&c->stats, 0, sizeof(c->stats));
+  g_alloc_ms = 0;
   c->hpop_valid = false;  // set again by a gapped run that leaves resume states
   const int64_t n = c->n;
   const int max_len = std::max(batch_max_len, c->max_len);
@@ -1114,6 +1118,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->resumed_ids.clear();
     c->stats.ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->stats.ms_alloc = g_alloc_ms;
     return 0;
   }
 
@@ -1938,6 +1943,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   c->stats.n_retry = (int64_t)c->retry_ids.size() + res_ok;
   c->stats.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->stats.ms_alloc = g_alloc_ms;
   return 0;
 }
 

@@ -34,7 +34,7 @@ class RunStats(c.Structure):
                 ("sa2pos_full", c.c_int), ("ms_coop_width", c.c_double), ("ms_coop_roots", c.c_double),
                 ("n_resumed", c.c_int64), ("resume_records", c.c_int64),
                 ("resume_records_peak", c.c_int64), ("resume_records_cap", c.c_int64),
-                ("coop_pages_peak", c.c_int64), ("coop_pages_cap", c.c_int64)]
+                ("coop_pages_peak", c.c_int64), ("coop_pages_cap", c.c_int64), ("ms_alloc", c.c_double)]
 
 
 class RefSeq(c.Structure):
