@@ -5,6 +5,8 @@
 // permutation as sorting the records themselves (tests/test_ksort.py).
 #pragma once
 #include <stddef.h>
+#include <stdint.h>
+#include <string.h>
 
 #include <utility>
 #include <vector>
@@ -92,6 +94,43 @@ void ks_introsort(size_t n, T *a, Lt lt) {
       d = stack.back().depth;
       stack.pop_back();
     }
+  }
+}
+
+// LSD radix sort of 64-bit keys, each with a 32-bit payload (vals may be null), in 11-bit digits
+// over the bits in which the keys differ; tk / tv are scratch.  Stable, so for keys without
+// duplicates it leaves what any sort leaves.
+inline void radix_sort_u64(size_t n, uint64_t *keys, uint32_t *vals, std::vector<uint64_t> &tk, std::vector<uint32_t> &tv) {
+  if (n < 2) return;
+  uint64_t diff = 0;
+  for (size_t i = 1; i < n; ++i) diff |= keys[i] ^ keys[0];
+  if (!diff) return;
+  const int lo = __builtin_ctzll(diff), hi = 64 - __builtin_clzll(diff);
+  tk.resize(n);
+  if (vals) tv.resize(n);
+  uint64_t *ka = keys, *kb = tk.data();
+  uint32_t *va = vals, *vb = vals ? tv.data() : nullptr;
+  size_t cnt[2048];
+  for (int sh = lo; sh < hi; sh += 11) {
+    memset(cnt, 0, sizeof cnt);
+    for (size_t i = 0; i < n; ++i) ++cnt[(ka[i] >> sh) & 2047];
+    size_t sum = 0;
+    for (size_t &c : cnt) {
+      const size_t x = c;
+      c = sum;
+      sum += x;
+    }
+    for (size_t i = 0; i < n; ++i) {
+      const size_t d = cnt[(ka[i] >> sh) & 2047]++;
+      kb[d] = ka[i];
+      if (va) vb[d] = va[i];
+    }
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  if (ka != keys) {
+    memcpy(keys, ka, n * sizeof *keys);
+    if (vals) memcpy(vals, va, n * sizeof *vals);
   }
 }
 

@@ -646,15 +646,18 @@ struct Sampe {
   // end 1 and end 2 on two threads, in the background: the first batch while the index loads, each
   // later one while the batch before it is processed.
   std::vector<Read> nxt[2];
+  double rd_s[2][2] = {{0, 0}, {0, 0}};  // per end: seconds reading reads, reading .sai records
   std::vector<Aln> nflat[2];
   std::vector<size_t> noff[2];
   bool nxt_ok[2] = {true, true};
   Background reader;
   void read_next(Source *src) {
     auto rd = [this, src](int j) {
+      const auto t0 = std::chrono::steady_clock::now();
       nxt[j].clear();
       nxt[j].reserve(0x40000);
       src[j].take(nxt[j], 0x40000, std::max(1, host_threads() / 2));
+      const auto t1 = std::chrono::steady_clock::now();
       // alngrp_create per read, in read order (saiset.c:45-76)
       const size_t n = nxt[j].size();
       nflat[j].clear();
@@ -666,6 +669,9 @@ struct Sampe {
         nxt_ok[j] = read_alns((int)j, nflat[j]);
         noff[j][i + 1] = nflat[j].size();
       }
+      const auto t2 = std::chrono::steady_clock::now();
+      rd_s[j][0] += std::chrono::duration<double>(t1 - t0).count();
+      rd_s[j][1] += std::chrono::duration<double>(t2 - t1).count();
     };
     std::thread t1(rd, 1);
     rd(0);
@@ -703,6 +709,8 @@ struct Sampe {
     }
     o.flush();
     ph.print("ibwa-amd sampe");
+    fprintf(stderr, "[ibwa-amd sampe] read-ahead thread s: end 1 reads %.2f .sai %.2f, end 2 reads %.2f .sai %.2f\n",
+            rd_s[0][0], rd_s[0][1], rd_s[1][0], rd_s[1][1]);
     return 0;
   }
 
@@ -743,14 +751,33 @@ struct Sampe {
     std::vector<uint8_t> hs;
     std::vector<uint32_t> hk, hl;
     std::vector<int> hi;  // (pair, end) as 2 i + j
-    for (int i = 0; i < n; ++i)
-      for (int j = 0; j < 2; ++j)
-        if (chosen[j][i]) {
-          const Read &p = seqs[j][i];
-          hd.push_back(alns[j][i][pick[j][i].main_idx].dbidx);
-          hs.push_back((uint8_t)p.strand); hk.push_back(p.sa); hl.push_back((uint32_t)p.len);
-          hi.push_back(2 * i + j);
+    {
+      // the chosen hits in (pair, end) order: counts per block of pairs, then filled in place
+      const int64_t nb = (n + 4095) / 4096;
+      std::vector<int64_t> c0(nb + 1, 0);
+      parallel_chunks(nb, [&](int64_t lo, int64_t hi_, int) {
+        for (int64_t b = lo; b < hi_; ++b) {
+          int64_t c = 0;
+          for (int64_t i = b * 4096; i < std::min<int64_t>(n, (b + 1) * 4096); ++i) c += chosen[0][i] + chosen[1][i];
+          c0[b + 1] = c;
         }
+      });
+      for (int64_t b = 0; b < nb; ++b) c0[b + 1] += c0[b];
+      hd.resize(c0[nb]); hs.resize(c0[nb]); hk.resize(c0[nb]); hl.resize(c0[nb]); hi.resize(c0[nb]);
+      parallel_chunks(nb, [&](int64_t lo, int64_t hi_, int) {
+        for (int64_t b = lo; b < hi_; ++b) {
+          int64_t o = c0[b];
+          for (int64_t i = b * 4096; i < std::min<int64_t>(n, (b + 1) * 4096); ++i)
+            for (int j = 0; j < 2; ++j)
+              if (chosen[j][i]) {
+                const Read &p = seqs[j][i];
+                hd[o] = alns[j][i][pick[j][i].main_idx].dbidx;
+                hs[o] = (uint8_t)p.strand; hk[o] = p.sa; hl[o] = (uint32_t)p.len;
+                hi[o++] = (int)(2 * i + j);
+              }
+        }
+      });
+    }
     ph.mark("hit choice: row lists");
     std::vector<uint64_t> pos;
     if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
@@ -814,15 +841,17 @@ struct Sampe {
         f0 = f1;
       }
     }
-    for (size_t t = 0; t < hi.size(); ++t) {
-      Read &p = seqs[hi[t] & 1][hi[t] >> 1];
-      if (!ok[t]) {
-        unmap(p);
-        fprintf(stderr, "Failed to select primary alignment for %s\n", p.name.c_str());
-        continue;
+    parallel_ordered((int64_t)hi.size(), [&](int64_t lo, int64_t hi_, int) {
+      for (int64_t t = lo; t < hi_; ++t) {
+        Read &p = seqs[hi[t] & 1][hi[t] >> 1];
+        if (!ok[t]) {
+          unmap(p);
+          msg("Failed to select primary alignment for %s\n", p.name.c_str());
+          continue;
+        }
+        p.seQ = p.mapQ = approx_mapQ(p, max_diff_of(p)) & 0xff;
       }
-      p.seQ = p.mapQ = approx_mapQ(p, max_diff_of(p)) & 0xff;
-    }
+    }, 0, 4096);
     ph.mark("sa2pos");
     // ---- insert size
     Isize ii;
@@ -949,6 +978,7 @@ struct Sampe {
     std::vector<int> pth(n, 0);
     std::vector<uint8_t> paired(n, 0);
     static const bool pstats = getenv("IBWA_SAMPE_STATS") != nullptr;
+    const bool fit32 = dbs.l_pac < (1ull << 32);  // positions (and remapped ones) in 32 bits: radix keys
     std::atomic<int64_t> t_pos{0}, t_cnt{0}, t_sort{0};  // ns in the rows' remap, the c1 / c2 count, the sort
     auto now_ns = []() {
       return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -958,6 +988,8 @@ struct Sampe {
       std::vector<std::pair<uint64_t, int>> ps;
       std::vector<PosKey> pk;
       std::vector<Position> tmp;
+      std::vector<uint64_t> kk, tk;
+      std::vector<uint32_t> ki, tv;
       int64_t a_pos = 0, a_cnt = 0, a_sort = 0;
       for (int64_t i = lo; i < hi_; ++i) {
         Read *p[2] = {&seqs[0][i], &seqs[1][i]};
@@ -998,7 +1030,18 @@ struct Sampe {
             }
             const int64_t t1 = pstats ? now_ns() : 0;
             if (pstats) a_pos += t1 - t0;
-            std::sort(ps.begin(), ps.end());
+            // c1 / c2 below need the positions grouped, each group's lowest score first: a sort
+            // by (remapped position, score), on one 64-bit key when the values fit
+            bool sc20 = true;
+            for (const auto &x : ps) sc20 = sc20 && (unsigned)x.second < (1u << 20);
+            if (ps.size() > 256 && fit32 && sc20) {
+              kk.resize(ps.size());
+              for (size_t t = 0; t < ps.size(); ++t) kk[t] = ps[t].first << 20 | (uint64_t)(ps[t].second & 0xFFFFF);
+              radix_sort_u64(kk.size(), kk.data(), nullptr, tk, tv);
+              for (size_t t = 0; t < ps.size(); ++t) ps[t] = {kk[t] >> 20, (int)(kk[t] & 0xFFFFF)};
+            } else {
+              std::sort(ps.begin(), ps.end());
+            }
             size_t c[2] = {0, 0};
             for (size_t t = 0; t < ps.size(); ++t)
               if (t == 0 || ps[t].first != ps[t - 1].first) ++c[ps[t].second == min_score ? 0 : 1];
@@ -1018,7 +1061,27 @@ struct Sampe {
         const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
         paired[i] = m0 && m1;
         if (paired[i]) {  // find_optimal_pair's sort
-          if (arr.n > 32) {
+          bool done = false;
+          if (arr.n > 256 && fit32) {
+            // no two positions with the same (remapped position, position): then the sorted order is
+            // unique and a radix sort gives the introsort's; with such ties the introsort decides
+            kk.resize(arr.n);
+            ki.resize(arr.n);
+            for (size_t t = 0; t < arr.n; ++t) {
+              kk[t] = arr.a[t].remapped_pos << 32 | arr.a[t].pos;
+              ki[t] = (uint32_t)t;
+            }
+            radix_sort_u64(arr.n, kk.data(), ki.data(), tk, tv);
+            done = true;
+            for (size_t t = 1; t < arr.n && done; ++t) done = kk[t] != kk[t - 1];
+            if (done) {
+              tmp.resize(arr.n);
+              for (size_t t = 0; t < arr.n; ++t) tmp[t] = arr.a[ki[t]];
+              std::copy(tmp.begin(), tmp.end(), arr.a.begin());
+            }
+          }
+          if (done) {
+          } else if (arr.n > 32) {
             // on 24-byte keys with the positions' indices: the introsort's moves depend only on the
             // comparisons, so the permutation -- ties included -- is the one of the positions themselves
             pk.resize(arr.n);

@@ -4,7 +4,8 @@ follows from it (bwapair.c:188).  sampe_main.cpp sorts a pair's positions throug
 (remapped_pos, pos, index) and gathers the records after: the permutation must be the one that
 sorting the records themselves gives, ties included.  Checked here on the CPU by a small C++ driver
 compiled against the header: many ties, all the size regimes (pairs, insertion sort, quicksort
-partitions, the depth-limit combsort)."""
+partitions, the depth-limit combsort); and the LSD radix sort sampe uses when no two keys tie
+(radix_sort_u64) against a stable sort."""
 import os
 import subprocess
 
@@ -15,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRIVER = r'''
 #include <stdint.h>
 #include <stdio.h>
+#include <algorithm>
 #include <random>
 #include "ksort.h"
 using namespace ibwa_sam;
@@ -41,8 +43,27 @@ int main() {
       ++cases;
     }
   }
-  printf("%ld %ld\n", cases, bad);
-  return bad != 0;
+  // radix_sort_u64: a stable sort of the keys (payloads follow), any key range
+  long rbad = 0;
+  std::vector<uint64_t> tk;
+  std::vector<uint32_t> tv;
+  for (int n : {2, 3, 300, 5000, 100000}) {
+    for (int rep = 0; rep < 6; ++rep) {
+      const int sh = rep * 11;
+      std::vector<uint64_t> k(n);
+      std::vector<uint32_t> v(n);
+      for (int i = 0; i < n; ++i) { k[i] = (g() % (rep % 2 ? 7 : 1000000)) << sh; v[i] = (uint32_t)i; }
+      std::vector<std::pair<uint64_t, uint32_t>> e(n);
+      for (int i = 0; i < n; ++i) e[i] = {k[i], v[i]};
+      std::stable_sort(e.begin(), e.end(), [](const std::pair<uint64_t, uint32_t> &x, const std::pair<uint64_t, uint32_t> &y) {
+        return x.first < y.first; });
+      radix_sort_u64(n, k.data(), v.data(), tk, tv);
+      for (int i = 0; i < n; ++i) rbad += k[i] != e[i].first || v[i] != e[i].second;
+      ++cases;
+    }
+  }
+  printf("%ld %ld\n", cases, bad + rbad);
+  return bad + rbad != 0;
 }
 '''
 
@@ -57,4 +78,4 @@ def test_key_sort_permutation_equals_record_sort(tmp_path):
         pytest.fail(r.stderr[-2000:])
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     cases, bad = map(int, r.stdout.split())
-    assert cases == 220 and bad == 0
+    assert cases == 250 and bad == 0

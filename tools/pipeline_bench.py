@@ -44,7 +44,7 @@ def run(argv, stdout=None, timeout=1200):
     if r.returncode != 0:
         raise RuntimeError(f"{argv[:2]} failed ({r.returncode}): {r.stderr.decode()[-1500:]}")
     for ln in r.stderr.decode(errors="replace").splitlines():
-        if "wall s:" in ln or "[ibwa-amd aln]" in ln or "hipMalloc" in ln or "coop pass" in ln or "retry" in ln or "batch of" in ln or "paired_sw]" in ln:
+        if "wall s:" in ln or "[ibwa-amd aln]" in ln or "hipMalloc" in ln or "coop pass" in ln or "retry" in ln or "batch of" in ln or "paired_sw]" in ln or "read-ahead" in ln:
             log(f"  {os.path.basename(argv[0])} {argv[1]}: {ln}")
     return dt
 
