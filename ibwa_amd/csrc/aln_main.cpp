@@ -367,7 +367,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   if (ibwa_device_count(&n_dev) || n_dev < 1) return die("no HIP device");
   if (n_gpus > n_dev)
     fprintf(stderr, "[ibwa-amd aln] -G %d on %d visible device(s): slice g runs on device g mod %d\n", n_gpus, n_dev, n_dev);
-  // FASTQ parsed on the GPUs: n_lanes + 1 ingest contexts per GPU (their own streams and buffers;
+  // FASTQ parsed on the GPUs: n_lanes + 3 ingest contexts per GPU (their own streams and buffers;
   // ingest.h's slots); the first region is read and parsed while the index loads
   std::vector<ibwa_ctx_t *> ing;
   std::unique_ptr<FastqGpu> fg;
@@ -381,8 +381,10 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   } destroy_ing{ing, fg};
   const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
   if (fq_dev) {
-    // one slot per group a lane can hold, and one more that is parsed ahead
-    const int n_slots = n_lanes + 1;
+    // one slot per group a lane can hold and the group being launched, and two more parsed ahead:
+    // a parse waits for launch boundaries of the searches (their grids hold every CU), so with one
+    // slot ahead the launching thread still waited (6.9 s of waits at 50 M reads, r04_e2e_50m_v2)
+    const int n_slots = n_lanes + 3;
     for (int sl = 0; sl < n_slots; ++sl)
       for (int g = 0; g < n_gpus; ++g) {
         ibwa_ctx_t *x = nullptr;

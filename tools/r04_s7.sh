@@ -10,8 +10,8 @@ for e in "X=0" "GPU_BLIT_ENGINE_TYPE=1" "GPU_BLIT_ENGINE_TYPE=2" "GPU_CP_DMA_COP
   env $e timeout -k 10 90 ./tools/copy_under_load > gpurun_out/cul_$e.txt 2>&1 || { cat gpurun_out/cul_$e.txt; exit 1; }
   grep "under load" gpurun_out/cul_$e.txt
 done
-echo "=== sampe tests $(date +%T)"
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_sampe_gpu.py tests/test_samse_gpu.py > gpurun_out/sampe_tests.log 2>&1 || { tail -30 gpurun_out/sampe_tests.log; exit 1; }
+echo "=== gpu tests $(date +%T)"
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/sampe_tests.log 2>&1 || { tail -30 gpurun_out/sampe_tests.log; exit 1; }
 tail -2 gpurun_out/sampe_tests.log
 echo "=== pipe $(date +%T)"
 bash tools/r04_pipe1.sh
