@@ -292,6 +292,11 @@ int fa2pac_main(int argc, char *argv[]);
 int pac_rev_main(int argc, char *argv[]);
 
 int main(int argc, char *argv[]) {
+  // Before the HIP runtime starts: host <-> device copies of every size go through the copy engines.
+  // By default the runtime does small ones with shader kernels, which wait until a search grid that
+  // holds every CU (the other lane's, or this lane's next one) ends: 1.4 s for an 8-byte copy next
+  // to a 1.5 s grid, 0.02 ms with this setting (tools/copy_under_load.hip, profiles/r04_cul_*.txt)
+  setenv("GPU_FORCE_BLIT_COPY_SIZE", "0", 0);
   if (argc >= 2 && strcmp(argv[1], "samse") == 0) return samse_main(argc - 1, argv + 1);
   if (argc >= 2 && strcmp(argv[1], "sampe") == 0) return sampe_main(argc - 1, argv + 1);
   if (argc >= 2 && strcmp(argv[1], "index") == 0) return index_main(argc - 1, argv + 1);
