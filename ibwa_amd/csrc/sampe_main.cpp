@@ -389,6 +389,16 @@ int infer_isize(const std::vector<Read> &s0, const std::vector<Read> &s1, Isize 
 // ---------------------------------------------------------------- read sources (bwa_open_reads, bwtaln.c:159-171)
 // next_read's record (bwa_read_seq, bwaseqio.c:145-208) from a strict FASTQ record of the bulk
 // parser: false for a record bwa_read_seq skips (not longer than the barcode)
+// a Read back to its defaults, keeping its strings' and vectors' buffers (a batch's reads are
+// refilled in place: no allocation per read in the steady state)
+inline void reset_read(Read &p) {
+  Read t;
+  t.name.swap(p.name); t.qual.swap(p.qual); t.seq.swap(p.seq); t.rseq.swap(p.rseq);
+  t.cigar.swap(p.cigar); t.multi.swap(p.multi); t.md.swap(p.md);
+  t.name.clear(); t.qual.clear(); t.seq.clear(); t.rseq.clear(); t.cigar.clear(); t.multi.clear(); t.md.clear();
+  p = std::move(t);
+}
+
 inline bool rec_to_read(const char *base, const ibwa_cli::FastqBulk::Rec &r, int mode, int trim_qual, Read &p) {
   const bool is_comp = mode & IBWA_MODE_COMPREAD;
   const bool is_64 = mode & IBWA_MODE_IL13;
@@ -396,7 +406,7 @@ inline bool rec_to_read(const char *base, const ibwa_cli::FastqBulk::Rec &r, int
   const int L = (int)r.len;
   if (L <= l_bc) return false;
   const char *s = base + r.s, *q = base + r.q;
-  p = Read();
+  reset_read(p);
   auto qv = [&](int i) { return is_64 ? (char)(q[i] - 31) : q[i]; };
   if (l_bc) {
     for (int i = 0; i < l_bc; ++i) p.bc[i] = qv(i) - 33 < 13 ? (char)tolower(s[i]) : (char)toupper(s[i]);
@@ -456,26 +466,31 @@ struct Source {
       g(0);
       for (auto &x : th) x.join();
     };
-    while (fb && out.size() < n_max && fb->more(nt, par)) {
-      const size_t i0 = fb->qi, m = std::min(fb->recs.size() - i0, n_max - out.size());
-      const size_t o = out.size();
-      out.resize(o + m);
+    size_t have = 0;  // out's elements (a batch before this one) are refilled in place
+    while (fb && have < n_max && fb->more(nt, par)) {
+      const size_t i0 = fb->qi, m = std::min(fb->recs.size() - i0, n_max - have);
+      if (out.size() < have + m) out.resize(have + m);
       std::vector<uint8_t> keep(m);
       const char *base = fb->blk.data();
       parallel_chunks((int64_t)m, [&](int64_t lo, int64_t hi, int) {
-        for (int64_t k = lo; k < hi; ++k) keep[k] = rec_to_read(base, fb->recs[i0 + k], mode, trim_qual, out[o + k]);
+        for (int64_t k = lo; k < hi; ++k) keep[k] = rec_to_read(base, fb->recs[i0 + k], mode, trim_qual, out[have + k]);
       }, nt);
-      size_t w = o;
+      size_t w = have;
       for (size_t k = 0; k < m; ++k)
         if (keep[k]) {
-          if (w != o + k) out[w] = std::move(out[o + k]);
+          if (w != have + k) std::swap(out[w], out[have + k]);
           ++w;
         }
-      out.resize(w);
+      have = w;
       fb->qi = i0 + m;
     }
     Read r;
-    while (out.size() < n_max && next(r)) out.push_back(std::move(r));
+    while (have < n_max && next(r)) {
+      if (have < out.size()) out[have] = std::move(r);
+      else out.push_back(std::move(r));
+      ++have;
+    }
+    out.resize(have);
   }
 };
 
@@ -502,16 +517,45 @@ struct Sampe {
 
   // alngrp_create (saiset.c:45-76): the read's records of every reference; with several
   // references sorted by score (klib's introsort, not stable) and cut at best + s_mm
+  // a .sai read in 16 MiB blocks (one fread per block, not two per read)
+  struct SaiIn {
+    FILE *fp = nullptr;
+    std::vector<char> b;
+    size_t p = 0, e = 0;
+    size_t read(void *dst, size_t n) {  // bytes copied (< n: the file ended)
+      size_t got = 0;
+      char *d = static_cast<char *>(dst);
+      while (got < n) {
+        if (p == e) {
+          if (b.empty()) b.resize((size_t)16 << 20);
+          p = 0;
+          e = fread(b.data(), 1, b.size(), fp);
+          if (e == 0) break;
+        }
+        const size_t k = std::min(n - got, e - p);
+        memcpy(d + got, b.data() + p, k);
+        p += k;
+        got += k;
+      }
+      return got;
+    }
+  };
+  std::vector<SaiIn> sai_in[2];  // per end, per reference: over fp_sai
+
   bool read_alns(int j, std::vector<Aln> &flat) {
     const size_t first = flat.size();
     std::vector<Aln> &v = flat;
+    if (sai_in[j].size() != fp_sai[j].size()) {
+      sai_in[j].resize(fp_sai[j].size());
+      for (size_t d = 0; d < fp_sai[j].size(); ++d) sai_in[j][d].fp = fp_sai[j][d];
+    }
     for (size_t d = 0; d < fp_sai[j].size(); ++d) {
       uint32_t count = 0;
-      if (fread(&count, 4, 1, fp_sai[j][d]) != 1) continue;  // past the end: nothing
+      if (sai_in[j][d].read(&count, 4) != 4) continue;  // past the end: nothing
       const size_t o = v.size();
       v.resize(o + count);
       sai_tmp[j].resize(count);  // the read's records in one read
-      if (count && fread(sai_tmp[j].data(), sizeof(ibwa_aln1_t), count, fp_sai[j][d]) != count) {
+      if (count && sai_in[j][d].read(sai_tmp[j].data(), sizeof(ibwa_aln1_t) * count) != sizeof(ibwa_aln1_t) * count) {
         fprintf(stderr, "[ibwa-amd sampe] truncated .sai\n");
         return false;
       }
@@ -654,7 +698,6 @@ struct Sampe {
   void read_next(Source *src) {
     auto rd = [this, src](int j) {
       const auto t0 = std::chrono::steady_clock::now();
-      nxt[j].clear();
       nxt[j].reserve(0x40000);
       src[j].take(nxt[j], 0x40000, std::max(1, host_threads() / 2));
       const auto t1 = std::chrono::steady_clock::now();
