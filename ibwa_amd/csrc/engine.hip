@@ -238,7 +238,7 @@ void note_coop_pages(ibwa_ctx *c, uint32_t pool_pages) {
   uint32_t used = 0;
   if (hipMemcpy(&used, c->c_next.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return;
   c->stats.coop_pages_peak = std::max<int64_t>(c->stats.coop_pages_peak, std::min<uint32_t>(used, pool_pages));
-  c->stats.coop_pages_cap = pool_pages;
+  c->stats.coop_pages_cap = std::max<int64_t>(c->stats.coop_pages_cap, pool_pages);  // the largest launch's pool
 }
 // An operation that would rebuild or replace index structures shared by ibwa_ctx_share_index
 // (borrowed buffers are written in place or cannot grow, and the other context may be aligning).

@@ -183,7 +183,7 @@ typedef struct {
 	                              state buffer holds one chunk's states at a time) */
 	int64_t resume_records_cap;  /* the state buffer's capacity in 16 B records */
 	int64_t coop_pages_peak;     /* the most bucket pages one cooperative launch took from its pool */
-	int64_t coop_pages_cap;      /* the pool's capacity in pages (COOP_PG 16 B entries each) */
+	int64_t coop_pages_cap;      /* the largest launch's pool in pages (COOP_PG 16 B entries each) */
 	double ms_alloc;             /* wall time the run spent allocating device buffers (hipMalloc) */
 } ibwa_run_stats_t;
 int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
