@@ -308,7 +308,11 @@ struct FqBufs {
   uint32_t *lenk;       // per kept read: length
 };
 uint64_t fq_padded_bytes(uint64_t n);
+constexpr uint32_t FQ_PAD_MAX = 16384;  // fq_padded_bytes(n) - n <= 2 * FQ_PAD_MAX (one tile + the rounding)
 // tmp == nullptr: *tmp_bytes = the scans' scratch size
-hipError_t fq_parse_launch(const FqBufs &b, uint64_t n, const FqOpt &o, void *tmp, size_t *tmp_bytes, hipStream_t st);
+// h_init (pinned host, may be null): {0, 0xFFFFFFFF} for the line and first-bad counters, copied in
+// instead of two memsets (a memset is a kernel, which waits for CUs another context's grid holds)
+hipError_t fq_parse_launch(const FqBufs &b, uint64_t n, const FqOpt &o, void *tmp, size_t *tmp_bytes, hipStream_t st,
+                           const uint32_t *h_init = nullptr);
 
 }  // namespace ibwa

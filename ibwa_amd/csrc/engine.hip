@@ -229,6 +229,7 @@ struct ibwa_ctx {
   DBuf fq_raw, fq_tile, fq_nl, fq_cnt, fq_len, fq_L, fq_key, fq_codes, fq_offk, fq_lenk, fq_tmp;
   int64_t fq_kept = 0;
   double fq_ms = 0;  // device time of the last parse (H2D copy + kernels), HIP events
+  uint32_t *fq_hinit = nullptr;  // pinned: the parse counters' initial values, then zeros for the padding
 };
 
 namespace {
@@ -435,10 +436,15 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   for (DBuf *b : {&c->h2p_in, &c->h2p_out, &c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
                   &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
-                  &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1]})
+                  &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1], &c->c_dir, &c->c_free, &c->c_hits,
+                  &c->c_next, &c->c_pool, &c->c_proot, &c->c_pstore, &c->c_recb, &c->c_stg, &c->d_cw, &c->d_feat,
+                  &c->d_hpop, &c->d_ordi, &c->d_ordids, &c->d_ordk, &c->d_ordtmp, &c->d_ptabg, &c->d_rdump, &c->d_roff,
+                  &c->d_selst, &c->d_seltmp, &c->fq_L, &c->fq_cnt, &c->fq_codes, &c->fq_key, &c->fq_len, &c->fq_lenk,
+                  &c->fq_nl, &c->fq_offk, &c->fq_raw, &c->fq_tile, &c->fq_tmp})
     b->release();
   for (auto &b : c->sw) b.release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
+  if (c->fq_hinit) (void)hipHostFree(c->fq_hinit);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -891,9 +897,21 @@ int ibwa_fq_parse(ibwa_ctx_t *c, const void *raw, uint64_t nbytes, int mode, int
   HIPCHK(fq_parse_launch(B, nbytes, o, nullptr, &tb, c->stream));
   if (int rc = c->fq_tmp.ensure(tb + 256)) return rc;
   HIPCHK(hipEventRecord(c->ev[6], c->stream));
+  // the padding and the counters' initial values come from pinned host memory (copy engine), not
+  // from memsets (kernels)
+  if (!c->fq_hinit) {
+    void *h = nullptr;
+    HIPCHK(hipHostMalloc(&h, 8 + 2 * FQ_PAD_MAX, 0));
+    memset(h, 0, 8 + 2 * FQ_PAD_MAX);
+    static_cast<uint32_t *>(h)[1] = 0xFFFFFFFFu;
+    c->fq_hinit = static_cast<uint32_t *>(h);
+  }
   HIPCHK(hipMemcpyAsync(c->fq_raw.p, raw, nbytes, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(c->fq_raw.as<uint8_t>() + nbytes, 0, padded - nbytes, c->stream));
-  HIPCHK(fq_parse_launch(B, nbytes, o, c->fq_tmp.p, &tb, c->stream));
+  if (padded - nbytes <= 2 * FQ_PAD_MAX)
+    HIPCHK(hipMemcpyAsync(c->fq_raw.as<uint8_t>() + nbytes, c->fq_hinit + 2, padded - nbytes, hipMemcpyHostToDevice, c->stream));
+  else
+    HIPCHK(hipMemsetAsync(c->fq_raw.as<uint8_t>() + nbytes, 0, padded - nbytes, c->stream));
+  HIPCHK(fq_parse_launch(B, nbytes, o, c->fq_tmp.p, &tb, c->stream, c->fq_hinit));
   HIPCHK(hipEventRecord(c->ev[7], c->stream));
   uint32_t cnt[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(cnt, c->fq_cnt.p, 8, hipMemcpyDeviceToHost, c->stream));

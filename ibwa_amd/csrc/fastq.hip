@@ -176,7 +176,8 @@ __global__ void __launch_bounds__(FQ_BLOCK) k_fq_encode(const uint8_t *buf, cons
 
 uint64_t fq_padded_bytes(uint64_t n) { return (n + FQ_TILE - 1) / FQ_TILE * FQ_TILE + FQ_TILE; }
 
-hipError_t fq_parse_launch(const FqBufs &B, uint64_t n, const FqOpt &o, void *tmp, size_t *tmp_bytes, hipStream_t st) {
+hipError_t fq_parse_launch(const FqBufs &B, uint64_t n, const FqOpt &o, void *tmp, size_t *tmp_bytes, hipStream_t st,
+                           const uint32_t *h_init) {
   const uint32_t n_tiles = (uint32_t)((n + FQ_TILE - 1) / FQ_TILE);
   const uint64_t max_rec = (uint64_t)B.cap_lines / 4 + 1;  // every record holds 4 newlines
   auto keys = rocprim::make_transform_iterator(B.rec_len, KeptKey());
@@ -188,9 +189,13 @@ hipError_t fq_parse_launch(const FqBufs &B, uint64_t n, const FqOpt &o, void *tm
     *tmp_bytes = a > b ? a : b;
     return e;
   }
-  hipError_t e = hipMemsetAsync(B.n_lines, 0, 4, st);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(B.bad, 0xFF, 4, st);
+  hipError_t e = hipSuccess;
+  if (h_init && B.bad == B.n_lines + 1) {
+    e = hipMemcpyAsync(B.n_lines, h_init, 8, hipMemcpyHostToDevice, st);
+  } else {
+    e = hipMemsetAsync(B.n_lines, 0, 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(B.bad, 0xFF, 4, st);
+  }
   if (e != hipSuccess) return e;
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_fq_count, dim3(n_tiles), dim3(FQ_BLOCK), 0, st, (const uint4 *)B.raw, B.tile_cnt);
