@@ -691,6 +691,7 @@ struct Sampe {
   // later one while the batch before it is processed.
   std::vector<Read> nxt[2];
   double rd_s[2][2] = {{0, 0}, {0, 0}};  // per end: seconds reading reads, reading .sai records
+  std::vector<std::vector<Position>> pstore_;  // batch()'s per-thread position stores (capacity kept)
   std::vector<Aln> nflat[2];
   std::vector<size_t> noff[2];
   bool nxt_ok[2] = {true, true};
@@ -1015,7 +1016,11 @@ struct Sampe {
     // shared array holds there: (A) every pair's positions, counts and sort; (B) each pair's nearest
     // earlier pair with more positions; (C) the pairing itself and select_sai_multi.
     const int nth = host_threads();
-    std::vector<std::vector<Position>> pstore(nth);
+    // every pair's positions, per host thread; kept across batches (a batch holds ~10 M positions,
+    // 0.5 GB: allocating, faulting in and freeing that each batch cost about as much as filling it)
+    std::vector<std::vector<Position>> &pstore = pstore_;
+    pstore.resize(std::max<size_t>(pstore.size(), (size_t)nth));
+    for (auto &v : pstore) v.clear();
     std::vector<uint32_t> pcnt(n, 0);
     std::vector<uint64_t> poff(n, 0);
     std::vector<int> pth(n, 0);
