@@ -387,53 +387,6 @@ int infer_isize(const std::vector<Read> &s0, const std::vector<Read> &s1, Isize 
 }
 
 // ---------------------------------------------------------------- read sources (bwa_open_reads, bwtaln.c:159-171)
-// next_read's record (bwa_read_seq, bwaseqio.c:145-208) from a strict FASTQ record of the bulk
-// parser: false for a record bwa_read_seq skips (not longer than the barcode)
-// a Read back to its defaults, keeping its strings' and vectors' buffers (a batch's reads are
-// refilled in place: no allocation per read in the steady state)
-inline void reset_read(Read &p) {
-  Read t;
-  t.name.swap(p.name); t.qual.swap(p.qual); t.seq.swap(p.seq); t.rseq.swap(p.rseq);
-  t.cigar.swap(p.cigar); t.multi.swap(p.multi); t.md.swap(p.md);
-  t.name.clear(); t.qual.clear(); t.seq.clear(); t.rseq.clear(); t.cigar.clear(); t.multi.clear(); t.md.clear();
-  p = std::move(t);
-}
-
-inline bool rec_to_read(const char *base, const ibwa_cli::FastqBulk::Rec &r, int mode, int trim_qual, Read &p) {
-  const bool is_comp = mode & IBWA_MODE_COMPREAD;
-  const bool is_64 = mode & IBWA_MODE_IL13;
-  const int l_bc = (int)((unsigned)mode >> 24);
-  const int L = (int)r.len;
-  if (L <= l_bc) return false;
-  const char *s = base + r.s, *q = base + r.q;
-  reset_read(p);
-  auto qv = [&](int i) { return is_64 ? (char)(q[i] - 31) : q[i]; };
-  if (l_bc) {
-    for (int i = 0; i < l_bc; ++i) p.bc[i] = qv(i) - 33 < 13 ? (char)tolower(s[i]) : (char)toupper(s[i]);
-    p.bc[l_bc] = 0;
-  }
-  const int n = L - l_bc;
-  p.full_len = p.clip_len = p.len = n;
-  p.seq.resize(n);
-  for (int i = 0; i < n; ++i) p.seq[i] = nt4[(unsigned char)s[l_bc + i]];
-  p.qual.resize(n);
-  for (int i = 0; i < n; ++i) p.qual[i] = qv(l_bc + i);
-  p.has_qual = true;
-  if (trim_qual >= 1) trim_read(trim_qual, p);
-  p.rseq.assign(n, 0);
-  for (int i = 0; i < p.len; ++i) {
-    const uint8_t c = p.seq[p.len - 1 - i];
-    p.rseq[i] = is_comp && c < 4 ? 3 - c : c;
-  }
-  // kseq's name: the header up to its first white space; then /[12]$ trimmed
-  const char *h = base + r.h + 1, *e = h;
-  while (*e != '\n' && !isspace((unsigned char)*e)) ++e;
-  size_t t = (size_t)(e - h);
-  if (t > 2 && h[t - 2] == '/' && (h[t - 1] == '1' || h[t - 1] == '2')) t -= 2;
-  p.name.assign(h, t);
-  return true;
-}
-
 struct Source {
   std::unique_ptr<ibwa_cli::SeqReader> fq;
   std::unique_ptr<ibwa_cli::FastqBulk> fb;  // strict FASTQ records in bulk, before the serial reader
@@ -460,37 +413,7 @@ struct Source {
   // reads appended to out up to n_max: the bulk parser's records on nt threads, then record by
   // record (the same reads in the same order as next() alone)
   void take(std::vector<Read> &out, size_t n_max, int nt) {
-    auto par = [](int k, const std::function<void(int)> &g) {
-      std::vector<std::thread> th;
-      for (int t = 1; t < k; ++t) th.emplace_back(g, t);
-      g(0);
-      for (auto &x : th) x.join();
-    };
-    size_t have = 0;  // out's elements (a batch before this one) are refilled in place
-    while (fb && have < n_max && fb->more(nt, par)) {
-      const size_t i0 = fb->qi, m = std::min(fb->recs.size() - i0, n_max - have);
-      if (out.size() < have + m) out.resize(have + m);
-      std::vector<uint8_t> keep(m);
-      const char *base = fb->blk.data();
-      parallel_chunks((int64_t)m, [&](int64_t lo, int64_t hi, int) {
-        for (int64_t k = lo; k < hi; ++k) keep[k] = rec_to_read(base, fb->recs[i0 + k], mode, trim_qual, out[have + k]);
-      }, nt);
-      size_t w = have;
-      for (size_t k = 0; k < m; ++k)
-        if (keep[k]) {
-          if (w != have + k) std::swap(out[w], out[have + k]);
-          ++w;
-        }
-      have = w;
-      fb->qi = i0 + m;
-    }
-    Read r;
-    while (have < n_max && next(r)) {
-      if (have < out.size()) out[have] = std::move(r);
-      else out.push_back(std::move(r));
-      ++have;
-    }
-    out.resize(have);
+    take_reads(fb.get(), mode, trim_qual, out, n_max, nt, [this](Read &r) { return next(r); });
   }
 };
 

@@ -17,7 +17,9 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "sam_common.h"
@@ -62,12 +64,15 @@ int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::str
   std::vector<ibwa_aln1_t> aln;
   long tot = 0;
   ph.mark("load index");
-  // batches of 0x40000 reads (bwa_read_seq); the next one is parsed while this one is processed
+  // batches of 0x40000 reads (bwa_read_seq); the next one is parsed while this one is processed --
+  // strict FASTQ in bulk on host threads (IBWA_SAMSE_SERIAL_READ=1: the serial reader alone)
+  std::unique_ptr<ibwa_cli::FastqBulk> fb;
+  if constexpr (std::is_same<Reader, ibwa_cli::SeqReader>::value)
+    if (!getenv("IBWA_SAMSE_SERIAL_READ")) fb.reset(new ibwa_cli::FastqBulk(rd));
   auto read_batch = [&](std::vector<Read> &v) {
-    v.clear();
     v.reserve(0x40000);
-    Read r;
-    while ((int)v.size() < 0x40000 && next_read(rd, opt.mode, opt.trim_qual, r)) v.push_back(std::move(r));
+    take_reads(fb.get(), opt.mode, opt.trim_qual, v, 0x40000, host_threads(),
+               [&](Read &r) { return next_read(rd, opt.mode, opt.trim_qual, r); });
   };
   std::vector<Read> seqs, nxt;
   read_batch(nxt);

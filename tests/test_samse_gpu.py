@@ -41,3 +41,33 @@ def test_samse_rejects_bad_rg(golden_dir, tmp_path):
                         os.path.join(golden_dir, "r36.default.sai"), os.path.join(golden_dir, "reads_r36.fq")],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "@RG" in r.stderr
+
+
+@pytest.mark.parametrize("aln_opts", [["-B", "5"], ["-I", "-q", "15"]])
+def test_samse_bulk_reader_equals_serial(golden_dir, aln_opts, tmp_path):
+    """samse's reads come from the bulk FASTQ parser on host threads (sam_common.h take_reads) up to
+    the first record it does not take, then from the serial kseq reader: with a multi-line record
+    midway, barcodes / Illumina 1.3 qualities / trimming in the .sai header's mode, the SAM equals the
+    serial reader's alone (IBWA_SAMSE_SERIAL_READ=1) byte for byte."""
+    g = lambda x: os.path.join(golden_dir, x)  # noqa: E731
+    recs = open(g("pe100_1.fq")).read().split("\n")
+    k = 4 * (len(recs) // 8)
+    recs[k + 1] = recs[k + 1][:40] + "\n" + recs[k + 1][40:]
+    fq = tmp_path / "r.fq"
+    fq.write_text("\n".join(recs))
+    sai = tmp_path / "r.sai"
+    r = subprocess.run([CLI, "aln"] + aln_opts + ["-f", str(sai), g("g1m"), str(fq)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    outs = []
+    for serial in (False, True):
+        out = tmp_path / f"out{int(serial)}.sam"
+        env = dict(os.environ)
+        if serial:
+            env["IBWA_SAMSE_SERIAL_READ"] = "1"
+        r = subprocess.run([CLI, "samse", "-f", str(out), g("g1m"), str(sai), str(fq)], capture_output=True, text=True,
+                           timeout=120, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(_body(out.read_text()))
+    assert len(outs[0]) > 1000
+    assert outs[0] == outs[1]
