@@ -10,7 +10,7 @@
 // from them groups: consecutive complete batches with the same batch-level max_diff
 // (bwtaln.c:86-88), whose slices -- the group's reads in each GPU's piece -- the aligning contexts
 // take as views of the parsed block (ibwa_batch_stage_fq, no copy).  A producer thread parses ahead:
-// the regions rotate over `slots` ingest contexts per GPU, and a slot is parsed over only once
+// each region goes to the lowest free of `slots` ingest contexts per GPU: a slot is parsed over once
 // every group of its previous region has been released (aligned) -- the parse kernels wait for
 // CUs that the searches' persistent grids hold, so they must not sit on the launching thread's
 // path.  A region's last, incomplete batch is parsed again at
@@ -159,14 +159,22 @@ class FastqGpu {
   double parse_s_ = 0, dev_ms_ = 0;
   int64_t n_records_ = 0;
 
-  // regions in turn, slot r % n_slots, each once the slot's previous region is released
+  // regions in turn, each into a slot whose previous region has been released
   void produce() {
     int after = NEXT;
-    for (int64_t region = 0; after == NEXT; ++region) {
-      const int slot = (int)(region % n_slots_);
+    while (after == NEXT) {
+      // the lowest free slot: a slot's buffers are allocated at its first parse, and an allocation
+      // can wait long (a process started after one that held most of the HBM), so a short input
+      // touches as few slots as it needs
+      int slot = -1;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&]() { return stop_ || busy_[slot] == 0; });
+        cv_.wait(lk, [&]() {
+          if (stop_) return true;
+          for (int q = 0; q < n_slots_; ++q)
+            if (busy_[q] == 0) { slot = q; return true; }
+          return false;
+        });
         if (stop_) break;
       }
       ing_.assign(all_.begin() + (size_t)slot * G_, all_.begin() + (size_t)(slot + 1) * G_);
