@@ -615,6 +615,9 @@ struct Sampe {
   std::vector<Read> nxt[2];
   double rd_s[2][2] = {{0, 0}, {0, 0}};  // per end: seconds reading reads, reading .sai records
   std::vector<std::vector<Position>> pstore_;  // batch()'s per-thread position stores (capacity kept)
+  std::unique_ptr<ibwa_ref_seq_t[]> sw_ref_[2];  // paired_sw's bwa_seq_t mirrors per end (capacity kept)
+  std::unique_ptr<uint8_t[]> sw_rev_[2];
+  size_t sw_ref_cap_[2] = {0, 0}, sw_rev_cap_[2] = {0, 0};
   std::vector<Aln> nflat[2];
   std::vector<size_t> noff[2];
   bool nxt_ok[2] = {true, true};
@@ -1210,14 +1213,21 @@ struct Sampe {
   // bwa_paired_sw through the C-ABI (compat.cpp) on bwa_seq_t mirrors of the batch
   int paired_sw(std::vector<Read> seqs[2], int n, const Isize &ii) {
     if (!popt.is_sw || ii.avg < 0.0) return 0;
-    // the mirrors are filled in parallel below: no zero-filled allocation of a batch's worth first
-    std::unique_ptr<ibwa_ref_seq_t[]> ref[2];
-    std::unique_ptr<uint8_t[]> rev[2];
+    // the mirrors are filled in parallel below, in buffers kept across batches (allocating, faulting
+    // in and freeing a batch's worth each time cost ~25 ms per batch)
+    std::unique_ptr<ibwa_ref_seq_t[]> *ref = sw_ref_;
+    std::unique_ptr<uint8_t[]> *rev = sw_rev_;
     for (int j = 0; j < 2; ++j) {
-      ref[j].reset(new ibwa_ref_seq_t[std::max(n, 1)]);
+      if (sw_ref_cap_[j] < (size_t)std::max(n, 1)) {
+        sw_ref_cap_[j] = (size_t)std::max(n, 1);
+        ref[j].reset(new ibwa_ref_seq_t[sw_ref_cap_[j]]);
+      }
       std::vector<size_t> ro(n + 1, 0);
       for (int i = 0; i < n; ++i) ro[i + 1] = ro[i] + (size_t)seqs[j][i].len;
-      rev[j].reset(new uint8_t[ro[n] + 1]);
+      if (sw_rev_cap_[j] < ro[n] + 1) {
+        sw_rev_cap_[j] = ro[n] + 1;
+        rev[j].reset(new uint8_t[sw_rev_cap_[j]]);
+      }
       parallel_chunks(n, [&](int64_t lo, int64_t hi, int) {
         for (int64_t i = lo; i < hi; ++i) {
           Read &r = seqs[j][i];
