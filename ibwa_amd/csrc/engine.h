@@ -302,7 +302,7 @@ struct FqBufs {
   uint32_t *bad;        // first record that is not strict (0xFFFFFFFF: none)
   int32_t *rec_len;     // per record (cap_lines / 4 + 1): kept length, -1 skipped or not strict
   uint32_t *rec_L;      // per record: sequence line length (0: not strict)
-  uint64_t *rec_key;    // per record: kept rank << 40 | code offset (exclusive scan)
+  uint64_t *rec_key;    // per record: kept rank << 32 | code offset (exclusive scan; the block is < 4 GiB)
   uint8_t *codes;       // kept reads' reversed nt4 codes, concatenated
   uint64_t *offk;       // per kept read: code offset
   uint32_t *lenk;       // per kept read: length

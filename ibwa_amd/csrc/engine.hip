@@ -225,6 +225,7 @@ struct ibwa_ctx {
   // contexts borrow this one's; neither side may rebuild or replace them while shared
   ibwa_ctx *share_src = nullptr;
   int n_borrowers = 0;
+  bool destroy_pending = false;  // destroyed while borrowed: freed with its last borrower
   // FASTQ ingest (fastq.hip, ibwa_fq_parse): the last parsed block and its kept reads
   DBuf fq_raw, fq_tile, fq_nl, fq_cnt, fq_len, fq_L, fq_key, fq_codes, fq_offk, fq_lenk, fq_tmp;
   int64_t fq_kept = 0;
@@ -432,7 +433,16 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  if (c->share_src) --c->share_src->n_borrowers;
+  // a context whose index other contexts still borrow (ibwa_ctx_share_index) stays alive until the
+  // last of them is destroyed: its index buffers are theirs too
+  if (c->n_borrowers > 0) {
+    c->destroy_pending = true;
+    return;
+  }
+  if (ibwa_ctx *src = c->share_src) {
+    c->share_src = nullptr;
+    if (--src->n_borrowers == 0 && src->destroy_pending) ibwa_ctx_destroy(src);
+  }
   for (DBuf *b : {&c->h2p_in, &c->h2p_out, &c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
                   &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
@@ -935,7 +945,7 @@ int ibwa_fq_parse(ibwa_ctx_t *c, const void *raw, uint64_t nbytes, int mode, int
   int32_t ll = 0;
   HIPCHK(hipMemcpy(&key, c->fq_key.as<uint64_t>() + n - 1, 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(&ll, c->fq_len.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost));
-  c->fq_kept = (int64_t)(key >> 40) + (ll >= 0 ? 1 : 0);
+  c->fq_kept = (int64_t)(key >> 32) + (ll >= 0 ? 1 : 0);
   *n_rec = (int64_t)n;
   *consumed = (uint64_t)last_nl + 1;
   return 0;

@@ -13,7 +13,8 @@
 //   k_fq_lines   every newline's position, in order (block scan of per-thread counts)
 //   k_fq_rec     one wavefront per record: the strict-shape checks over its lines, its kept length
 //                (barcode / trim); the first record that is not strict ends the block's records
-//   (scan)       kept-read rank and code offset of every record, one 64-bit key
+//   (scan)       kept-read rank and code offset of every record, one 64-bit key (32 bits each:
+//                a block is < 4 GiB, so neither the rank nor the offset can overflow its half)
 //   k_fq_encode  one wavefront per record: the reversed nt4 codes, coalesced stores
 // The host hands the rest of the input, from the first record that is not strict, to the serial
 // kseq-semantics reader, exactly as FastqBulk does; the kept reads of the block stay in HBM and
@@ -140,9 +141,9 @@ __global__ void __launch_bounds__(FQ_BLOCK) k_fq_rec(const uint8_t *buf, const u
   }
 }
 
-struct KeptKey {  // kept-read count << 40 | code bytes
+struct KeptKey {  // kept-read count << 32 | code bytes
   __host__ __device__ uint64_t operator()(int32_t len) const {
-    return len >= 0 ? (1ull << 40) | (uint64_t)len : 0ull;
+    return len >= 0 ? (1ull << 32) | (uint64_t)len : 0ull;
   }
 };
 
@@ -158,7 +159,7 @@ __global__ void __launch_bounds__(FQ_BLOCK) k_fq_encode(const uint8_t *buf, cons
     const int32_t len = rec_len[r];
     if (len < 0) continue;
     const uint64_t key = rec_key[r];
-    const uint64_t kr = key >> 40, co = key & ((1ull << 40) - 1ull);
+    const uint64_t kr = key >> 32, co = key & 0xFFFFFFFFull;
     if (lane == 0) {
       offk[kr] = co;
       lenk[kr] = (uint32_t)len;

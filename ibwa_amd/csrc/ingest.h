@@ -156,6 +156,14 @@ class FastqGpu {
   uint64_t got_[2] = {0, 0};
   std::thread reader_;
   std::vector<DevGroup> groups_;
+  struct Piece {  // one GPU's piece of a region: its records' kept / sequence lengths
+    int64_t n_rec = 0;
+    uint64_t consumed = 0;
+    int not_strict = 0, rc = 0;
+    std::vector<int32_t> len;
+    std::vector<uint32_t> L;
+  };
+  std::vector<Piece> pc_;  // per GPU, reused by every region
   double parse_s_ = 0, dev_ms_ = 0;
   int64_t n_records_ = 0;
 
@@ -262,25 +270,26 @@ class FastqGpu {
       if (cut[g] < cut[g - 1]) cut[g] = cut[g - 1];
     }
     // each GPU parses its piece (in parallel)
-    struct Piece {
-      int64_t n_rec = 0;
-      uint64_t consumed = 0;
-      int not_strict = 0, rc = 0;
-      std::vector<int32_t> len;
-      std::vector<uint32_t> L;
-    };
-    std::vector<Piece> pc(G);
+    if ((int)pc_.size() < G) pc_.resize(G);
+    std::vector<Piece> &pc = pc_;
     const auto t0 = std::chrono::steady_clock::now();
     {
       std::vector<std::thread> th;
       for (int g = 0; g < G; ++g)
         th.emplace_back([&, g]() {
           Piece &p = pc[g];
+          p.n_rec = 0;
+          p.consumed = 0;
+          p.not_strict = p.rc = 0;
           const uint64_t bytes = cut[g + 1] - cut[g];
           if (!bytes) return;
-          const int64_t cap = (int64_t)(bytes / 8 + 1);  // a strict record holds >= 8 bytes
-          p.len.resize(cap);
-          p.L.resize(cap);
+          // ibwa_fq_parse returns at most cap_lines / 4 + 1 = bytes / 48 + 17 records; the arrays are
+          // kept across regions and only ever grow
+          const int64_t cap = (int64_t)(bytes / 48 + 17);
+          if ((int64_t)p.len.size() < cap) {
+            p.len.resize(cap);
+            p.L.resize(cap);
+          }
           p.rc = ibwa_fq_parse(ing_[g], base + cut[g], bytes, mode_, trim_, &p.n_rec, &p.consumed, &p.not_strict,
                                p.len.data(), p.L.data(), cap);
         });

@@ -483,8 +483,6 @@ inline bool next_read(Reader &rd, int mode, int trim_qual, Read &p) {
   }
 }
 
-// next_read's record (bwa_read_seq, bwaseqio.c:145-208) from a strict FASTQ record of the bulk
-// parser: false for a record bwa_read_seq skips (not longer than the barcode)
 // a Read back to its defaults, keeping its strings' and vectors' buffers (a batch's reads are
 // refilled in place: no allocation per read in the steady state)
 inline void reset_read(Read &p) {
@@ -495,6 +493,8 @@ inline void reset_read(Read &p) {
   p = std::move(t);
 }
 
+// next_read's record (bwa_read_seq, bwaseqio.c:145-208) from a strict FASTQ record of the bulk
+// parser: false for a record bwa_read_seq skips (not longer than the barcode)
 inline bool rec_to_read(const char *base, const ibwa_cli::FastqBulk::Rec &r, int mode, int trim_qual, Read &p) {
   const bool is_comp = mode & IBWA_MODE_COMPREAD;
   const bool is_64 = mode & IBWA_MODE_IL13;

@@ -74,6 +74,8 @@ int ibwa_device_count(int *n);
  * every context of the process (a context borrowing another's index counts only its own buffers).
  * No reference counterpart: the footprint report of bench.py and the CLI's stats line. */
 int ibwa_device_bytes(int64_t *now, int64_t *peak);
+/* Frees a context.  A context whose index others still borrow (ibwa_ctx_share_index) is freed with
+ * its last borrower, so the destroy order of a source and its borrowers does not matter. */
 void ibwa_ctx_destroy(ibwa_ctx_t *ctx);
 
 /*

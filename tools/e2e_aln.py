@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--parse", default="dev,host", help="input parse modes to time alone first (IBWA_ALN_PARSE_ONLY): "
                                                         "dev = on the GPU (default path), host = IBWA_ALN_GPU_PARSE=0")
     ap.add_argument("--host-parse-run", type=int, default=1, help="also align with the host parse and compare the .sai")
+    ap.add_argument("--variants", default="", help="JSON list of {name: {ENV: value}}: extra aln runs of the same FASTQ "
+                                                   "with these environment settings (.sai compared with the first run)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
@@ -211,6 +213,18 @@ def main():
                     log(f"{name}: lanes {lanes} .sai equal to lanes {c['lanes']}: {r_['sai_equal_first_run']}")
                     os.unlink(out_sai)
                 c["runs"].append(r_)
+            for vv in (json.loads(a.variants) if a.variants else []):
+                for vname, venv in vv.items():
+                    vsai = os.path.join(tmp, f"c{cid}_v.sai")
+                    wall, ph = run([CLI, "aln"] + opts + ["-f", vsai, P, fq], env={k: str(v) for k, v in venv.items()})
+                    load = ph.get("load index", 0.0)
+                    r_ = {"variant": vname, "env": venv, "wall_s": wall, "phases_s": ph,
+                          "reads_per_s_excl_index_load": a.reads / max(wall - load, 1e-9),
+                          "sai_equal_first_run": open(vsai, "rb").read() == open(sai, "rb").read()}
+                    log(f"{name}: variant {vname} {venv}: {wall:.1f} s wall -> {r_['reads_per_s_excl_index_load']:.0f} "
+                        f"reads/s excl. index load, .sai equal {r_['sai_equal_first_run']}")
+                    os.unlink(vsai)
+                    c["runs"].append(r_)
             c["parse_only"] = parse
             if a.host_parse_run:
                 hsai = os.path.join(tmp, f"c{cid}_h.sai")
