@@ -24,6 +24,8 @@ Extra JSON fields (rank 0, N=1):
   extra.parity  -- GPU == CPU restatement on >= 200k reads plus reads the cooperative / wide /
                    general passes resolved
   extra.exact_leg -- configs[1] (10M reads, -n 0) on the same index, with its own roofline
+  extra.e2e     -- the same reads end to end through the CLI (`ibwa-amd aln`: FASTQ file in, .sai out,
+                   index load excluded), .sai == the timed step's hits for every read
   extra.sw_leg  -- k_sw on 200k mate-rescue pairs (510 bp window x 150 bp read, configs[4]'s SW
                    shape) from the same genome: alignments/s, GCUPS over the forward cells, the
                    forward pass alone (engine option sw_stop=1) against its VALU roofline
@@ -386,6 +388,89 @@ def exact_leg(eng, ascii_, lens, args, threads, hip, do_cpu):
     return out
 
 
+CLI = os.path.join(ROOT, "ibwa_amd", "bin", "ibwa-amd")
+
+
+def e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns):
+    """configs[2] end to end through the product CLI: the timed step's own 50M reads
+    (same generator and seed) written as a FASTQ file, the device-built index written as .bwt / .rbwt
+    (bwt_dump_bwt, bwtio.c:7-15), then `ibwa-amd aln -f out.sai <prefix> <reads.fq>` as a child
+    process -- file in, .sai out: FASTQ parsed on the GPU, groups of 0x40000-read batches aligned on
+    two overlapped lanes, records written in input order (bwa_aln_core, bwtaln.c:173-241).  The
+    bench's engine is closed first (the CLI needs the HBM).  Reported: the CLI's wall clock, its
+    phases (index load, with the device arena reserved meanwhile; align), reads/s with and without
+    them, and parity: the CLI's .sai must equal the timed step's hits for every read."""
+    import subprocess
+    import tempfile
+    from ibwa_amd import _native
+    L = _native.lib()
+    out = {"workload": f"configs[2] end to end: {args.reads} x {args.read_len} bp FASTQ -> .sai, `ibwa-amd aln` "
+                       f"(defaults), one GPU"}
+    d = tempfile.mkdtemp(prefix="ibwa_e2e_", dir=os.environ.get("IBWA_E2E_DIR", "/tmp"))
+    try:
+        pre = os.path.join(d, "g")
+        for s_, ext in ((0, ".bwt"), (1, ".rbwt")):
+            p_, L2, w = eng.export_bwt(s_)
+            with open(pre + ext, "wb") as f:
+                np.array([p_] + list(L2), dtype=np.uint32).tofile(f)
+                w.astype(np.uint32, copy=False).tofile(f)
+        eng.close()
+        t = time.perf_counter()
+        c_lens = (ctypes.c_uint64 * len(lens))(*lens)
+        fq = os.path.join(d, "reads.fq")
+        n = args.reads
+        # the same call make_reads() made for the timed step (splitmix64 keyed by (seed, stream, index))
+        raw = np.empty(n * args.read_len, dtype=np.uint8)
+        pos = np.empty(n, dtype=np.uint64)
+        strand = np.empty(n, dtype=np.uint8)
+        L.ibwa_synth_reads(shard_seed(0, args.seed), ascii_.ctypes.data, ascii_.size, len(lens), c_lens, n,
+                           args.read_len, args.sub, args.indel, raw.ctypes.data, pos.ctypes.data,
+                           strand.ctypes.data, threads)
+        del pos, strand
+        if L.ibwa_synth_write_fastq(fq.encode(), raw.ctypes.data, 0, n, args.read_len, threads) != 0:
+            raise RuntimeError(f"cannot write {fq}")
+        del raw
+        out["fastq_bytes"] = os.path.getsize(fq)
+        out["fastq_write_s"] = time.perf_counter() - t
+        sai = os.path.join(d, "reads.sai")
+        env = dict(os.environ, IBWA_ALN_TIMES="1")
+        t = time.perf_counter()
+        r = subprocess.run([CLI, "aln", *args.aln.split(), "-f", sai, pre, fq], stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE, env=env, timeout=900)
+        wall = time.perf_counter() - t
+        err = r.stderr.decode(errors="replace")
+        if r.returncode != 0:
+            raise RuntimeError(f"ibwa-amd aln failed ({r.returncode}): {err[-800:]}")
+        import re
+        phases = {}
+        for ln in err.splitlines():
+            if "wall s:" in ln:
+                for name, v in re.findall(r"([a-z][a-z .()]*?) (\d+\.\d+)", ln.split("wall s:", 1)[1]):
+                    phases[name.strip()] = float(v)
+            m_ = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s parsing ahead.*\((\d+) ms of device", ln)
+            if m_:
+                out["gpu_parse"] = {"records": int(m_.group(1)), "producer_s": float(m_.group(2)),
+                                    "device_ms": int(m_.group(3)),
+                                    "records_per_s": int(m_.group(1)) / max(float(m_.group(2)), 1e-3)}
+            m_ = re.search(r"arena on GPU 0: ([\d.]+) GB, peak use ([\d.]+) GB", ln)
+            if m_:
+                out["arena_gb"], out["arena_peak_use_gb"] = float(m_.group(1)), float(m_.group(2))
+        load = phases.get("load index", 0.0)
+        out.update({"wall_s": wall, "phases_s": phases, "value": n / max(wall - load, 1e-9), "unit": "reads/s",
+                    "value_incl_index_load": n / wall,
+                    "note": "wall clock of the child process (FASTQ parse, alignment and .sai writes overlapped); "
+                            "`value` excludes its 'load index' phase (.bwt/.rbwt read and relaid out on the GPU, "
+                            "the device arena reserved meanwhile)"})
+        t = time.perf_counter()
+        first_bad = L.ibwa_sai_diff(sai.encode(), n, np.ascontiguousarray(n_aln, dtype=np.int32).ctypes.data,
+                                    np.ascontiguousarray(alns).ctypes.data)
+        out["parity"] = {"reads": n, "sai_equals_timed_step_hits": first_bad == -1,
+                         "first_differing_read": int(first_bad), "check_s": time.perf_counter() - t}
+        return out
+    finally:
+        subprocess.run(["rm", "-rf", d])
+
+
 SW_OPS_PER_CELL = 18  # VALU instructions per cell of k_sw's branch-free forward strip (gfx950 asm)
 VALU_PEAK_LANE_OPS = 256 * 64 * 2.4e9  # MI355X_MICROARCH.md: 256 CUs x 64 lanes/clk x 2.4 GHz
 
@@ -494,6 +579,8 @@ def main():
     ap.add_argument("--exact-reads", type=int, default=10_000_000)
     ap.add_argument("--exact-steps", type=int, default=5)
     ap.add_argument("--sa2pos", type=int, default=1, help="also time SA->coordinate of every read's first hit")
+    ap.add_argument("--e2e-leg", type=int, default=1, help="also run the CLI end to end on the same reads as a "
+                                                          "FASTQ file (extra.e2e)")
     ap.add_argument("--sw-leg", type=int, default=200_000, help="SW mate-rescue pairs for extra.sw_leg (0: off)")
     ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
     ap.add_argument("--shards", type=int, default=1,
@@ -751,6 +838,9 @@ def main():
         if args.exact_leg and world == 1 and not exact_cfg:
             del seq, off, lns
             leg("exact_leg", lambda: exact_leg(eng, ascii_, lens, args, threads, hip, do_cpu))
+        if args.e2e_leg and world == 1 and not exact_cfg and n_aln is not None and os.path.exists(CLI):
+            # last: it closes the engine (the CLI process needs the HBM)
+            leg("e2e", lambda: e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns))
         result["extra"] = extra
         print(json.dumps(result), flush=True)
     eng.close()

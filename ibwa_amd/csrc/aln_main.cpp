@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <zlib.h>
 
 #include <chrono>
@@ -51,6 +52,7 @@ const int kGroup = env_int("IBWA_ALN_GROUP", 16);
 const int kSub = env_int("IBWA_ALN_SUBBATCH", kBatch);
 const int kMinRdLen = 35;    // BWA_MIN_RDLEN, bwtaln.h:23
 const bool kTimes = env_int("IBWA_ALN_TIMES", 0) != 0;
+const double kArenaMaxGb = 232.0, kArenaMarginGb = 6.0;  // default device arena (run_aln)
 
 unsigned char nt4[256];
 
@@ -283,7 +285,7 @@ int die(const char *what) {
 
 template <class Reader>
 int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out,
-            int n_gpus, const char *fq_dev);
+            int n_gpus, const char *fq_dev, const char *fq_path);
 
 int samse_main(int argc, char *argv[]);  // samse_main.cpp
 int sampe_main(int argc, char *argv[]);  // sampe_main.cpp
@@ -340,7 +342,7 @@ int main(int argc, char *argv[]) {
       fprintf(stderr, "[ibwa-amd aln] cannot open %s as BAM\n", argv[first_arg + 1]);
       return 1;
     }
-    return run_aln(rd, nullptr, opt, prefix, fn_out, n_gpus, nullptr);
+    return run_aln(rd, nullptr, opt, prefix, fn_out, n_gpus, nullptr, argv[first_arg + 1]);
   }
   SeqReader rd;
   if (!rd.open(argv[first_arg + 1])) {
@@ -353,12 +355,13 @@ int main(int argc, char *argv[]) {
   const bool serial = env_int("IBWA_ALN_SERIAL_READ", 0) != 0;
   const char *gp = getenv("IBWA_ALN_GPU_PARSE");
   const bool dev_parse = !serial && !(gp && atoi(gp) == 0) && FastqGpu::usable(argv[first_arg + 1]);
-  return run_aln(rd, serial ? nullptr : &fb, opt, prefix, fn_out, n_gpus, dev_parse ? argv[first_arg + 1] : nullptr);
+  return run_aln(rd, serial ? nullptr : &fb, opt, prefix, fn_out, n_gpus, dev_parse ? argv[first_arg + 1] : nullptr,
+                 argv[first_arg + 1]);
 }
 
 template <class Reader>
 int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::string &prefix, const char *fn_out,
-            int n_gpus, const char *fq_dev) {
+            int n_gpus, const char *fq_dev, const char *fq_path) {
   FILE *out = fn_out ? fopen(fn_out, "wb") : stdout;
   if (!out) {
     fprintf(stderr, "[ibwa-amd aln] cannot write %s\n", fn_out);
@@ -372,6 +375,46 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   if (ibwa_device_count(&n_dev) || n_dev < 1) return die("no HIP device");
   if (n_gpus > n_dev)
     fprintf(stderr, "[ibwa-amd aln] -G %d on %d visible device(s): slice g runs on device g mod %d\n", n_gpus, n_dev, n_dev);
+  // One device arena per GPU, reserved before anything else is allocated (engine.hip Arena): every
+  // buffer -- index, ingest slots, the lanes' search scratch -- is carved from it, so no allocation
+  // in the middle of the alignment waits for the driver to wipe memory a previous process released.
+  // IBWA_ARENA_GB: its size per GPU (0: none); default: the free memory less a margin, at most
+  // kArenaMaxGb.
+  const int n_used = std::min(n_gpus, n_dev);
+  {
+    // the default arena follows the inputs: the index structures (bit planes, relaid-out BWT, K-mer
+    // tables: ~17x the two .bwt files at GRCh37 size), the ingest slots and the lanes' search scratch
+    // (both grow with the reads a group holds: ~16x the FASTQ bytes at 100 bp, capped at kArenaMaxGb)
+    auto fbytes = [](const std::string &f) -> double {
+      struct stat st;
+      return stat(f.c_str(), &st) == 0 ? (double)st.st_size : 0.0;
+    };
+    const double need_gb = (24.0 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) +
+                            16.0 * (fq_path ? fbytes(fq_path) : 0.0)) / (1u << 30) + 2.0;
+    const char *ag = getenv("IBWA_ARENA_GB");
+    std::vector<std::thread> th;
+    std::vector<int> rc(n_used, 0);
+    std::vector<double> want_gb(n_used, 0.0), ms(n_used, 0.0);
+    for (int d = 0; d < n_used; ++d)
+      th.emplace_back([&, d]() {
+        const auto t0 = std::chrono::steady_clock::now();
+        uint64_t fr = 0, tot = 0;
+        double gb = ag ? atof(ag) : 0.0;
+        if (!ag && ibwa_device_memory(d, &fr, &tot) == 0)
+          gb = std::min(std::min(kArenaMaxGb, (double)fr / (1u << 30) - kArenaMarginGb), need_gb);
+        want_gb[d] = gb;
+        if (gb >= 1.0) rc[d] = ibwa_reserve(d, (uint64_t)(gb * (1u << 30)));
+        ms[d] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      });
+    for (auto &t : th) t.join();
+    for (int d = 0; d < n_used; ++d) {
+      if (rc[d])
+        fprintf(stderr, "[ibwa-amd aln] warning: no arena on GPU %d (%s); buffers are allocated one by one\n", d,
+                ibwa_last_error());
+      else if (kTimes && want_gb[d] >= 1.0)
+        fprintf(stderr, "[ibwa-amd aln] arena on GPU %d: %.1f GiB reserved in %.0f ms\n", d, want_gb[d], ms[d]);
+    }
+  }
   // FASTQ parsed on the GPUs: n_lanes + 3 ingest contexts per GPU (their own streams and buffers;
   // ingest.h's slots); the first region is read and parsed while the index loads
   std::vector<ibwa_ctx_t *> ing;
@@ -635,6 +678,11 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   ph.print("ibwa-amd aln");
   fprintf(stderr, "[ibwa-amd aln] device memory: peak %.1f GB of engine buffers on %d GPU(s) (%d context(s) per GPU, "
                   "index shared)\n", dev_peak / 1e9, n_gpus, n_lanes);
+  for (int d = 0; d < n_used; ++d) {
+    uint64_t asz = 0, aused = 0, apeak = 0;
+    if (ibwa_arena_stats(d, &asz, &aused, &apeak) == 0 && asz)
+      fprintf(stderr, "[ibwa-amd aln] arena on GPU %d: %.1f GB, peak use %.1f GB\n", d, asz / 1e9, apeak / 1e9);
+  }
   if (fg) {
     fprintf(stderr, "[ibwa-amd aln] input parsed on the GPUs: %lld records, %.2f s parsing ahead of the alignment (%.0f ms "
                     "of device time: H2D copies + kernels)%s\n",

@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <thread>
 #include <chrono>
 #include <string>
@@ -53,7 +55,65 @@ void dev_bytes_add(int64_t d) {
   }
 }
 
-// A growable device buffer.
+// Device arena (ibwa_reserve): one hipMalloc per device, made once, from which every buffer of the
+// process's contexts on that device is carved (first fit, 4 KiB granules, freed ranges coalesce).
+// A hipMalloc right after another process released a lot of HBM waits until the driver has wiped
+// that memory (measured: 0.5-2.7 s for single allocations of `aln` end 2, profiles/r05_alloc.jsonl);
+// a CLI that reserves its arena while it loads the index pays that once, overlapped, instead of in
+// the middle of its first groups.  Without a reservation buffers are plain hipMallocs.
+struct Arena {
+  std::mutex mu;
+  char *base = nullptr;
+  size_t size = 0, used = 0, peak = 0;
+  std::map<size_t, size_t> free_;  // offset -> bytes
+  void *alloc(size_t n) {
+    n = (n + 4095) & ~(size_t)4095;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto it = free_.begin(); it != free_.end(); ++it) {
+      if (it->second < n) continue;
+      const size_t off = it->first, rest = it->second - n;
+      free_.erase(it);
+      if (rest) free_[off + n] = rest;
+      used += n;
+      peak = std::max(peak, used);
+      return base + off;
+    }
+    return nullptr;
+  }
+  bool owns(const void *p) const {
+    return base && static_cast<const char *>(p) >= base && static_cast<const char *>(p) < base + size;
+  }
+  void release(void *p, size_t n) {
+    n = (n + 4095) & ~(size_t)4095;
+    std::lock_guard<std::mutex> lk(mu);
+    size_t off = (size_t)(static_cast<char *>(p) - base);
+    used -= n;
+    auto nx = free_.lower_bound(off);
+    if (nx != free_.end() && off + n == nx->first) {  // merge with the next free range
+      n += nx->second;
+      nx = free_.erase(nx);
+    }
+    if (nx != free_.begin()) {
+      auto pv = std::prev(nx);
+      if (pv->first + pv->second == off) {  // and with the previous one
+        pv->second += n;
+        return;
+      }
+    }
+    free_[off] = n;
+  }
+};
+thread_local hipStream_t g_stream = nullptr;  // the stream of the context this thread's API call works on
+constexpr int MAX_DEV = 64;
+Arena g_arena[MAX_DEV];
+
+Arena *arena_here() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEV) return nullptr;
+  return g_arena[d].base ? &g_arena[d] : nullptr;
+}
+
+// A growable device buffer (carved from the device's arena when one is reserved).
 struct DBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -61,17 +121,17 @@ struct DBuf {
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     if (borrowed) return fail(IBWA_EINVAL, "a shared index buffer cannot grow (%zu > %zu bytes)", bytes, cap);
-    if (p) {
-      (void)hipFree(p);
-      dev_bytes_add(-(int64_t)cap);
-    }
+    if (p) free_dev(p, cap);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 256);
     static const bool verbose = getenv("IBWA_VERBOSE") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    hipError_t e = hipMalloc(&p, want);
-    if (e != hipSuccess) return fail(IBWA_EHIP, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+    if (Arena *a = arena_here()) p = a->alloc(want);
+    if (!p) {
+      hipError_t e = hipMalloc(&p, want);
+      if (e != hipSuccess) return fail(IBWA_EHIP, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+    }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     g_alloc_ms += ms;
     if (verbose && ms > 20.0) fprintf(stderr, "[ibwa_amd] hipMalloc(%.2f GB) took %.0f ms\n", want / 1e9, ms);
@@ -79,11 +139,24 @@ struct DBuf {
     dev_bytes_add((int64_t)want);
     return 0;
   }
+  static void free_dev(void *q, size_t n) {
+    for (Arena &a : g_arena)
+      if (a.owns(q)) {
+        // the range may still be used by work queued on the owning context's stream (the API call
+        // in progress on this thread: g_stream); other contexts never touch it (an index a context
+        // lends is never freed while borrowed, and an ingest slot is not parsed over while a lane
+        // still reads it)
+        if (g_stream) (void)hipStreamSynchronize(g_stream);
+        else (void)hipDeviceSynchronize();
+        a.release(q, n);
+        dev_bytes_add(-(int64_t)n);
+        return;
+      }
+    (void)hipFree(q);
+    dev_bytes_add(-(int64_t)n);
+  }
   void release() {
-    if (p && !borrowed) {
-      (void)hipFree(p);
-      dev_bytes_add(-(int64_t)cap);
-    }
+    if (p && !borrowed) free_dev(p, cap);
     p = nullptr;
     cap = 0;
     borrowed = false;
@@ -235,6 +308,12 @@ struct ibwa_ctx {
 
 namespace {
 
+// An API call's entry: the context's device, and its stream for the arena (DBuf::free_dev).
+hipError_t enter(const ibwa_ctx *c) {
+  g_stream = c->stream;
+  return hipSetDevice(c->device);
+}
+
 // the pages a cooperative launch took from its pool (a bump counter: freed pages go to per-wave lists)
 void note_coop_pages(ibwa_ctx *c, uint32_t pool_pages) {
   uint32_t used = 0;
@@ -295,7 +374,7 @@ int ensure_kmer(ibwa_ctx *c) {
 // then runs without the jump (same results).
 int derive_sa_locked(ibwa_ctx *c, uint32_t intv) {
   if (c->share_src) return fail(IBWA_EINVAL, "sampled SA: this context shares another context's index");
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   for (int s = 0; s < 2; ++s) {
     const uint64_t n_nodes = ((uint64_t)c->ix[s].seq_len + intv) / intv;
     DBuf tmp;
@@ -403,6 +482,45 @@ int ibwa_device_count(int *n) {
   return 0;
 }
 
+int ibwa_device_memory(int device, uint64_t *free_b, uint64_t *total_b) {
+  HIPCHK(hipSetDevice(device));
+  size_t f = 0, t = 0;
+  HIPCHK(hipMemGetInfo(&f, &t));
+  if (free_b) *free_b = f;
+  if (total_b) *total_b = t;
+  return 0;
+}
+
+int ibwa_reserve(int device, uint64_t bytes) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return fail(IBWA_EHIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= n || device >= MAX_DEV) return fail(IBWA_EINVAL, "device %d out of range (%d devices)", device, n);
+  Arena &a = g_arena[device];
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (a.base) return fail(IBWA_EINVAL, "device %d already has an arena of %zu bytes", device, a.size);
+  if (bytes == 0) return 0;
+  HIPCHK(hipSetDevice(device));
+  const size_t want = ((size_t)bytes + 4095) & ~(size_t)4095;
+  void *p = nullptr;
+  e = hipMalloc(&p, want);
+  if (e != hipSuccess) return fail(IBWA_EHIP, "hipMalloc(%zu) for the arena: %s", want, hipGetErrorString(e));
+  a.base = static_cast<char *>(p);
+  a.size = want;
+  a.free_[0] = want;
+  return 0;
+}
+
+int ibwa_arena_stats(int device, uint64_t *size, uint64_t *used, uint64_t *peak) {
+  if (device < 0 || device >= MAX_DEV) return fail(IBWA_EINVAL, "device %d out of range", device);
+  Arena &a = g_arena[device];
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (size) *size = a.size;
+  if (used) *used = a.used;
+  if (peak) *peak = a.peak;
+  return 0;
+}
+
 int ibwa_device_bytes(int64_t *now, int64_t *peak) {
   if (now) *now = g_dev_bytes.load();
   if (peak) *peak = g_dev_peak.load();
@@ -431,7 +549,7 @@ int ibwa_ctx_create(int device, ibwa_ctx_t **out) {
 
 void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  (void)enter(c);
   (void)hipStreamSynchronize(c->stream);
   // a context whose index other contexts still borrow (ibwa_ctx_share_index) stays alive until the
   // last of them is destroyed: its index buffers are theirs too
@@ -526,7 +644,7 @@ int ibwa_ctx_load_bwt(ibwa_ctx_t *c, int strand, uint32_t primary, const uint32_
                       uint64_t bwt_size) {
   if (strand < 0 || strand > 1) return fail(IBWA_EINVAL, "strand must be 0 (.bwt) or 1 (.rbwt)");
   if (int rc = refuse_shared(c, "load_bwt")) return rc;
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   const uint32_t seq_len = L2[3];
   const uint64_t n_blocks = ((uint64_t)seq_len + 127) / 128 + 1;
   // expected reference size: 4 words per 128 symbols (+1 final count block) + ceil(n/16) words
@@ -576,7 +694,7 @@ int ibwa_ctx_clone_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   if (int rc = refuse_shared(dst, "clone_index")) return rc;
   for (int s = 0; s < 2; ++s) {
     if (!src->loaded[s]) return fail(IBWA_ENOINDEX, "source index not loaded");
-    HIPCHK(hipSetDevice(dst->device));
+    HIPCHK(enter(dst));
     uint64_t bytes = ((uint64_t)src->ix[s].seq_len + 127) / 128 * 64 + 64;
     if (int rc = dst->idx[s].ensure(bytes)) return rc;
     if (src->device == dst->device) {
@@ -603,7 +721,7 @@ int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
     if (!src->loaded[s]) return fail(IBWA_ENOINDEX, "source index not loaded");
   if (int rc = refuse_shared(dst, "share_index (destination)")) return rc;
   if (src->share_src) return fail(IBWA_EINVAL, "share_index: the source shares another context's index; share that one");
-  HIPCHK(hipSetDevice(dst->device));
+  HIPCHK(enter(dst));
   HIPCHK(hipStreamSynchronize(src->stream));  // src's structures are complete
   for (int s = 0; s < 2; ++s) {
     for (DBuf *b : {&dst->idx[s], &dst->o64[s], &dst->kt[s], &dst->sa_s[s], &dst->sa_full[s], &dst->isa_full[s], &dst->txt2[s]})
@@ -639,7 +757,7 @@ int ibwa_ctx_build_index(ibwa_ctx_t *c, const uint8_t *codes, uint64_t n, int sa
   if (n == 0 || n >= 0xFFFFFFFEull) return fail(IBWA_EINVAL, "text length %llu outside [1, 2^32-2)", (unsigned long long)n);
   if (sa_intv < 0) return fail(IBWA_EINVAL, "sa_intv < 0");
   if (int rc = refuse_shared(c, "build_index")) return rc;
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   DBuf T;
   if (int rc = T.ensure(n)) return rc;
   HIPCHK(hipMemcpyAsync(T.p, codes, n, hipMemcpyHostToDevice, c->stream));
@@ -717,7 +835,7 @@ int ibwa_ctx_export_bwt(const ibwa_ctx_t *c, int strand, uint32_t *words, uint64
   if (int rc = ibwa_ctx_bwt_info(c, strand, nullptr, nullptr, &need)) return rc;
   if (cap < need) return fail(IBWA_EINVAL, "export buffer too small (%llu < %llu)", (unsigned long long)cap,
                               (unsigned long long)need);
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   const uint64_t n = c->ix[strand].seq_len, nb = (n + 127) / 128;
   std::vector<uint4> blk((nb + 1) * 4);
   HIPCHK(hipMemcpy(blk.data(), c->idx[strand].p, blk.size() * 16, hipMemcpyDeviceToHost));
@@ -740,7 +858,7 @@ int ibwa_ctx_export_sa(const ibwa_ctx_t *c, int strand, uint32_t *out, uint64_t 
   if (strand < 0 || strand > 1 || !c->loaded[strand] || !c->sa_intv) return fail(IBWA_ENOINDEX, "no sampled SA");
   const uint64_t n = c->ix[strand].seq_len, n_sa = (n + c->sa_intv) / c->sa_intv;
   if (cap < n_sa) return fail(IBWA_EINVAL, "export buffer too small");
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   HIPCHK(hipMemcpy(out, c->sa_s[strand].p, n_sa * 4, hipMemcpyDeviceToHost));
   out[0] = 0xFFFFFFFFu;  // bwt.c:66
   return 0;
@@ -755,7 +873,7 @@ int ibwa_ctx_load_sa(ibwa_ctx_t *c, int strand, uint32_t sa_intv, const uint32_t
     return fail(IBWA_EINVAL, "n_sa %llu != (seq_len + intv) / intv", (unsigned long long)n_sa);
   if (c->sa_loaded[1 - strand] && c->sa_intv != sa_intv)
     return fail(IBWA_EINVAL, "sa_intv %u differs from the other strand's %u", sa_intv, c->sa_intv);
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   if (int rc = c->sa_s[strand].ensure(n_sa * 4)) return rc;
   HIPCHK(hipMemcpy(c->sa_s[strand].p, sa, n_sa * 4, hipMemcpyHostToDevice));
   c->sa_intv = sa_intv;
@@ -794,7 +912,7 @@ int ibwa_ctx_expand_sa(ibwa_ctx_t *c) {
   if (!c->sa_loaded[0] || !c->sa_loaded[1]) return fail(IBWA_ENOINDEX, "sampled SA of both strands needed");
   if (c->jump_ready || c->sa_expanded) return 0;  // full SA already resident
   if (c->share_src) return fail(IBWA_EINVAL, "expand_sa: this context shares another context's index");
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   for (int s = 0; s < 2; ++s) {
     if (int rc = c->sa_full[s].ensure(((uint64_t)c->ix[s].seq_len + 1) * 4)) return rc;
     HIPCHK(expand_sa(c->ix[s], c->sa_s[s].as<uint32_t>(), c->sa_intv, c->sa_full[s].as<uint32_t>(), c->stream));
@@ -816,7 +934,7 @@ int ibwa_sa2pos(ibwa_ctx_t *c, int64_t n, const uint8_t *strand, const uint32_t 
   }
   c->stats.ms_sa2pos = 0;
   if (n == 0) return 0;
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   // one staging buffer: strand bytes, rows, lengths in; positions + walk lengths out
   const uint64_t o_k = (n + 15) / 16 * 16, o_len = o_k + n * 4, in_bytes = o_len + n * 4;
   if (int rc = c->h2p_in.ensure(in_bytes)) return rc;
@@ -872,7 +990,7 @@ int ibwa_fq_parse(ibwa_ctx_t *c, const void *raw, uint64_t nbytes, int mode, int
   c->fq_kept = 0;
   c->fq_ms = 0;
   if (nbytes == 0) return 0;
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   const uint64_t padded = fq_padded_bytes(nbytes);
   // a strict line holds >= 2 bytes, and records of real reads far more: past cap_lines the block
   // simply ends earlier (the caller parses on from *consumed)
@@ -955,7 +1073,7 @@ int ibwa_fq_offset(const ibwa_ctx_t *c, int64_t r, uint64_t *off) {
   if (!c || !off || r < 0) return fail(IBWA_EINVAL, "fq_offset: bad arguments");
   *off = 0;
   if (r == 0) return 0;
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   uint32_t x = 0;
   HIPCHK(hipMemcpy(&x, c->fq_nl.as<uint32_t>() + 4 * r - 1, 4, hipMemcpyDeviceToHost));
   *off = (uint64_t)x + 1;
@@ -974,7 +1092,7 @@ int ibwa_batch_stage_fq(ibwa_ctx_t *c, const ibwa_ctx_t *src, int64_t first, int
                 (long long)first, (long long)(first + n), (long long)(src ? src->fq_kept : 0));
   if (c->device != src->device) return fail(IBWA_EINVAL, "stage_fq: contexts on devices %d and %d", c->device, src->device);
   if (max_len > 65535) return fail(IBWA_EINVAL, "read length %d > 65535 is not supported", max_len);
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   HIPCHK(hipStreamSynchronize(src->stream));  // the block is parsed
   // no copy: the batch is a view of the parsed block's kept reads (their codes, offsets into them
   // and lengths), which must stay as they are until this context's runs over it are over -- a
@@ -990,7 +1108,7 @@ int ibwa_batch_stage_fq(ibwa_ctx_t *c, const ibwa_ctx_t *src, int64_t first, int
 
 int ibwa_batch_stage(ibwa_ctx_t *c, int64_t n, const uint8_t *seq, const uint64_t *off, const uint32_t *len) {
   if (n < 0) return fail(IBWA_EINVAL, "n < 0");
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   uint64_t bytes = 0;
   int max_len = 0;
   for (int64_t i = 0; i < n; ++i) {
@@ -1053,7 +1171,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   if (!c->loaded[0] || !c->loaded[1]) return fail(IBWA_ENOINDEX, "load both .bwt and .rbwt first");
   if (c->ix[0].seq_len != c->ix[1].seq_len) return fail(IBWA_EINVAL, ".bwt and .rbwt lengths differ");
   if (int rc = check_opt(opt)) return rc;
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   memset(&c->stats, 0, sizeof(c->stats));
   g_alloc_ms = 0;
   c->hpop_valid = false;  // set again by a gapped run that leaves resume states
@@ -1573,15 +1691,20 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   // hold is flagged and continues below)
   if (v2 && c->gap_coop && !todo.empty() && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK) {
     std::vector<int64_t> wide_todo, wide_where;
-    for (int round = 0; round < 3 && !todo.empty(); ++round) {
+    const int coop_rounds = 4;
+    for (int round = 0; round < coop_rounds && !todo.empty(); ++round) {
       const int64_t lanes = (int64_t)todo.size();
       const size_t wide0 = wide_todo.size();
       uint32_t stg_log2 = 10;
       while ((1u << stg_log2) < (uint32_t)c->coop_stg_room * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
       // one heavy read per wave at a time: no more waves than heavy reads, and the page pool in
-      // proportion (at least 1 GiB; the reads that run out of pages run again with all of it)
+      // proportion (at least 1 GiB).  The reads that run out of pages run again with all of it,
+      // shared by 8x fewer concurrent waves each round (the pool is taken page by page, so each of
+      // them can grow into the room the others leave): a read whose stack outgrew its share of a
+      // busy pool is still resolved cooperatively, instead of by the sequential wide kernel (at
+      // coop_pool_gb=10, 150 bp reads at 2 %: minutes, r04_sweep_mem150)
       const int full_blocks = c->n_cus * c->coop_waves_per_cu;
-      const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
+      const int blocks = (int)std::min<int64_t>(std::max(1, full_blocks >> (3 * round)), lanes);
       const uint32_t freecap = 4096, hcap = 4096;
       const uint64_t pool_bytes =
           round ? (uint64_t)c->coop_pool_gb << 30
@@ -1764,7 +1887,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       for (int64_t j = 0; j < lanes; ++j) {
         if (rs[j] & ST_BAD_SCORE) return fail(IBWA_EINVAL, "score outside the stack range");
         if (rs[j]) {
-          const bool again = ((rs[j] >> 8) & 7u) == 3u && round < 2;
+          const bool again = ((rs[j] >> 8) & 7u) == 3u && round < coop_rounds - 1;
           (again ? next : wide_todo).push_back(todo[j]);
           (again ? next_where : wide_where).push_back(where[j]);
           continue;
@@ -1994,7 +2117,7 @@ int ibwa_batch_diag(const ibwa_ctx_t *c, int what, void *out, uint64_t cap_bytes
       return 0;
     }
     if (c->n == 0) return 0;
-    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(enter(c));
     HIPCHK(hipMemcpy(out, c->d_hpop.p, need2, hipMemcpyDeviceToHost));
     return 0;
   }
@@ -2002,7 +2125,7 @@ int ibwa_batch_diag(const ibwa_ctx_t *c, int what, void *out, uint64_t cap_bytes
   if (!c->diag || (what != 0 && what != 1)) return fail(IBWA_EINVAL, "set option diag=1 before the run; what = 0 or 1");
   if (cap_bytes < need) return fail(IBWA_EINVAL, "diag buffer too small");
   if (c->n == 0) return 0;
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   HIPCHK(hipMemcpy(out, (what == 0 ? c->d_iters : c->d_feat).p, need, hipMemcpyDeviceToHost));
   return 0;
 }
@@ -2014,7 +2137,7 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
   const uint64_t n_slots = c->stream_out ? c->stream_len : (uint64_t)n * cap;
   c->h_aln.resize(std::max<uint64_t>(n_slots, 1));
   if (n) {
-    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(enter(c));
     if (!c->naln_on_host) {
       c->h_naln.resize(n);
       HIPCHK(hipMemcpyAsync(c->h_naln.data(), c->d_naln.p, n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -2066,7 +2189,7 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
 
 int ibwa_ctx_prepare(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt) {
   if (!c) return fail(IBWA_EINVAL, "null context");
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   if (int rc = ensure_kmer(c)) return rc;
   // the condition of ibwa_batch_run's exact path
   if (opt && c->exact_path && !(opt->fnr > 0.0f) && opt->max_diff == 0 && opt->max_entries >= 2)
@@ -2101,7 +2224,7 @@ int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1,
     *cigar = (uint32_t *)malloc(4);
     return 0;
   }
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   int max1 = 0, max2 = 0;
   uint64_t end1 = 0, end2 = 0;
   for (int64_t p = 0; p < n; ++p) {
@@ -2218,7 +2341,7 @@ int ibwa_global_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64
 
 int ibwa_occ4(ibwa_ctx_t *c, int strand, int64_t n, const uint32_t *k, uint32_t *cnt) {
   if (!c->loaded[strand]) return fail(IBWA_ENOINDEX, "index not loaded");
-  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(enter(c));
   DBuf dk, dc;
   if (int rc = dk.ensure(n * 4 + 4)) return rc;
   if (int rc = dc.ensure(n * 16 + 16)) { dk.release(); return rc; }

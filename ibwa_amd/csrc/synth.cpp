@@ -12,6 +12,8 @@
 // srand48(11).  ibwa_pack_nt4() restates that with the POSIX 48-bit LCG so
 // the repo-owned index builder produces the same .pac as `bwa index`.
 #include <cstdint>
+#include <cstdio>
+#include <unistd.h>
 #include <cstring>
 #include <cstdlib>
 #include <vector>
@@ -360,6 +362,80 @@ void ibwa_synth_reads(uint64_t seed, const char *ascii, uint64_t n, int n_contig
   std::vector<std::thread> th;
   for (int t = 0; t < n_threads; ++t) th.emplace_back(work, t);
   for (auto &x : th) x.join();
+}
+
+// Write n fixed-length reads (ASCII, stride len) as FASTQ records "@r%010d", bases, "+", 'I'
+// qualities -- the same bytes tools/e2e_aln.py and bench.py's write_fastq produce -- with n_threads
+// formatting and writing their share of records at fixed file offsets.  The reads with index
+// [first, first + n) are numbered from `first`.  Returns 0, or -1 if the file cannot be written.
+int ibwa_synth_write_fastq(const char *path, const char *seqs, uint64_t first, uint64_t n, int len, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  FILE *f = fopen(path, "wb");
+  if (!f) return -1;
+  const int fd = fileno(f);
+  const uint64_t rec = 12 + 1 + (uint64_t)len + 3 + (uint64_t)len + 1;
+  std::vector<int> bad(n_threads, 0);
+  auto work = [&](int t) {
+    const uint64_t lo = n * t / n_threads, hi = n * (t + 1) / n_threads;
+    const uint64_t step = 1u << 16;
+    std::vector<char> buf(step * rec);
+    for (uint64_t a = lo; a < hi; a += step) {
+      const uint64_t b = std::min(hi, a + step);
+      char *w = buf.data();
+      for (uint64_t r = a; r < b; ++r) {
+        uint64_t id = first + r;
+        w[0] = '@';
+        w[1] = 'r';
+        for (int d = 11; d >= 2; --d, id /= 10) w[d] = (char)('0' + id % 10);
+        w[12] = '\n';
+        memcpy(w + 13, seqs + r * (uint64_t)len, len);
+        memcpy(w + 13 + len, "\n+\n", 3);
+        memset(w + 16 + len, 'I', len);
+        w[16 + 2 * len] = '\n';
+        w += rec;
+      }
+      const uint64_t bytes = (b - a) * rec;
+      uint64_t done = 0;
+      while (done < bytes) {
+        const ssize_t x = pwrite(fd, buf.data() + done, bytes - done, (off_t)(a * rec + done));
+        if (x <= 0) { bad[t] = 1; return; }
+        done += (uint64_t)x;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < n_threads; ++t) th.emplace_back(work, t);
+  for (auto &x : th) x.join();
+  const bool ok = fclose(f) == 0 && std::find(bad.begin(), bad.end(), 1) == bad.end();
+  return ok ? 0 : -1;
+}
+
+// A .sai file (bwtaln.c:192, :227-231: 64 B header, then per read int32 n_aln and n_aln 16 B
+// records) against per-read hit counts and the concatenated 16 B records of n reads.  Returns the
+// first read whose records differ, n if the file holds more than those reads, or -1 if they are
+// equal (-2: the file cannot be read).
+int64_t ibwa_sai_diff(const char *path, uint64_t n, const int32_t *n_aln, const uint8_t *alns) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return -2;
+  std::vector<char> io(1 << 24);
+  setvbuf(f, io.data(), _IOFBF, io.size());
+  char hdr[64];
+  if (fread(hdr, 1, 64, f) != 64) { fclose(f); return 0; }
+  std::vector<uint8_t> rec;
+  uint64_t p = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    int32_t k = 0;
+    if (fread(&k, 4, 1, f) != 1 || k != n_aln[i]) { fclose(f); return (int64_t)i; }
+    rec.resize((size_t)k * 16);
+    if (k && (fread(rec.data(), 16, (size_t)k, f) != (size_t)k || memcmp(rec.data(), alns + p * 16, (size_t)k * 16))) {
+      fclose(f);
+      return (int64_t)i;
+    }
+    p += (uint64_t)k;
+  }
+  const int extra = fgetc(f);
+  fclose(f);
+  return extra == EOF ? -1 : (int64_t)n;
 }
 
 }  // extern "C"

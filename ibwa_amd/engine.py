@@ -80,6 +80,9 @@ CAPI = {
     "ibwa_ctx_create": (_i, [_i, c.POINTER(_vp)]),
     "ibwa_device_count": (_i, [c.POINTER(_i)]),
     "ibwa_device_bytes": (_i, [c.POINTER(c.c_int64), c.POINTER(c.c_int64)]),
+    "ibwa_device_memory": (_i, [_i, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64)]),
+    "ibwa_reserve": (_i, [_i, c.c_uint64]),
+    "ibwa_arena_stats": (_i, [_i, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64), c.POINTER(c.c_uint64)]),
     "ibwa_fq_parse": (_i, [_vp, _vp, c.c_uint64, _i, _i, c.POINTER(c.c_int64), c.POINTER(c.c_uint64), c.POINTER(_i),
                            _vp, _vp, c.c_int64]),
     "ibwa_fq_stats": (_i, [_vp, c.POINTER(c.c_int64), c.POINTER(c.c_double)]),

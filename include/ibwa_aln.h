@@ -74,6 +74,18 @@ int ibwa_device_count(int *n);
  * every context of the process (a context borrowing another's index counts only its own buffers).
  * No reference counterpart: the footprint report of bench.py and the CLI's stats line. */
 int ibwa_device_bytes(int64_t *now, int64_t *peak);
+/* Device arena: one allocation of `bytes` on `device`, made once, from which every later buffer of
+ * the process's contexts on that device is carved (a buffer that does not fit is a plain
+ * allocation).  Replaces the per-batch scratch allocation of bwa_cal_sa_reg_gap (bwtaln.c:88-97,
+ * 139: gap_init_stack / gap_destroy_stack per thread) with memory taken once per process.  A
+ * hipMalloc right after another process released much of the HBM waits for the driver to wipe it;
+ * reserving the arena while the index loads pays that once, overlapped.  IBWA_EINVAL if the device
+ * already has one (the arena lives until the process exits). */
+int ibwa_reserve(int device, uint64_t bytes);
+/* Free and total device memory of `device` (hipMemGetInfo), for sizing an arena. */
+int ibwa_device_memory(int device, uint64_t *free_b, uint64_t *total_b);
+/* The arena of `device`: its size, the bytes its buffers use now, and their high-water mark. */
+int ibwa_arena_stats(int device, uint64_t *size, uint64_t *used, uint64_t *peak);
 /* Frees a context.  A context whose index others still borrow (ibwa_ctx_share_index) is freed with
  * its last borrower, so the destroy order of a source and its borrowers does not matter. */
 void ibwa_ctx_destroy(ibwa_ctx_t *ctx);

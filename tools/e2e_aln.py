@@ -110,8 +110,8 @@ def run(argv, timeout=1800, env=None):
         if m:
             log("  cli:", ln.strip())
             n_, s_, t_ = int(m.group(1)), float(m.group(2)), int(m.group(3))
-            phases["input parse"] = {"reads": n_, "wall_s": s_, "threads": t_, "reads_per_s": n_ / s_,
-                                     "reads_per_s_per_thread": n_ / s_ / t_}
+            phases["input parse"] = {"reads": n_, "wall_s": s_, "threads": t_, "reads_per_s": n_ / max(s_, 1e-3),
+                                     "reads_per_s_per_thread": n_ / max(s_, 1e-3) / t_}
     return dt, phases
 
 
