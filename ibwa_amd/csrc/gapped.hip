@@ -261,7 +261,9 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
   int64_t cur = 0, cend = 0;
   bool more = true;
   // ---- lane state
-  int st = 0;  // 0 idle, 1 search (C valid or empty), 2 exact sub-search, 3 ended (retire), 4 (LW) record loading
+  // 0 idle, 1 search (C valid or empty), 2 exact sub-search, 3 ended (retire), 4 (LW) record loading,
+  // 5 gap_shadow of the lane's latest hit (16 width positions per iteration)
+  int st = 0;
   uint32_t end_stat = 0;
   int64_t r = 0, ro = 0;  // read of this launch, its output index
   int len = 0, opt_max_diff = 0, max_diff = 0, best_score = 0, n_aln = 0;
@@ -294,6 +296,13 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
   uint32_t xk = 0, xl = 0;
   int xj = 0, xa = 0;
   uint4 xe = make_uint4(0, 0, 0, 0);  // the entry that went down the exact path
+  // gap_shadow sub-state (st 5, bwtgap.c:81-91 after a hit is added): a lane is never in both
+  // sub-states, so it reuses the exact sub-search's registers -- the interval size x of the hit,
+  // the new width of the position before the chunk, the chunk's first position, the hit's strand,
+  // and (xe) the widths equal to x so far and last_diff_pos
+  uint32_t &sh_x = xk, &sh_prevx = xl;
+  int &sh_q = xj, &sh_a = xa;
+  uint32_t &sh_jj = xe.x, &sh_ldp = xe.y;
 
   // The per-read argument pointers are re-read from the kernel-argument segment where they are used
   // (read claim, read end) instead of staying live in SGPRs through the loop, where the compiler
@@ -723,8 +732,11 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     const bool qkneg = qk == 0;
     const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
     Blk bk, bl;
-    load_blk(obq, ql, qrun, bl);
-    load_blk(obq, qk - 1, qrun && !qkneg && !qshare, bk);
+    // a shadowing lane loads 16 width positions of its hit's strand into the block registers
+    const bool shd = st == 5;
+    const uint4 *shp = reinterpret_cast<const uint4 *>((sh_a ? W1 : W0) + sh_q);
+    load_blk(shd ? shp : obq, shd ? 0u : ql, qrun || shd, bl);
+    load_blk(shd ? shp + 4 : obq, shd ? 0u : qk - 1, (qrun && !qkneg && !qshare) || shd, bk);
     // width bounds of strand a at positions i-2, i-1 and the seed pair
     const uint2 *Wa = a ? W1 : W0;
     const uint2 *SWa = a ? SW1 : SW0;
@@ -812,6 +824,47 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     if (finish) {
       end_stat = status;
       st = 3;
+      continue;
+    }
+    if (shd) {
+      // ---- gap_shadow (bwtgap.c:81-91) of positions sh_q .. sh_q + 15 (< ldp) of strand sh_a: the
+      // hit's interval size is taken off every width above it, and a width equal to it becomes the
+      // jj-th largest row with bid 1.  LW: the LDS nibbles follow (the bid, clamped, and "equals the
+      // previous position's width" of every position up to ldp).
+      uint2 *width = const_cast<uint2 *>(sh_a ? W1 : W0);
+      const uint32_t mx = ixv0.seq_len, cf = (uint32_t)opt_max_diff + 1u;
+      const int ldp_ = (int)sh_ldp;
+      const uint4 wq[8] = {bl.v0, bl.v1, bl.v2, bl.v3, bk.v0, bk.v1, bk.v2, bk.v3};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int pp = sh_q + u;
+        const uint4 &h = wq[u >> 1];
+        uint2 w = (u & 1) ? make_uint2(h.z, h.w) : make_uint2(h.x, h.y);
+        if (pp < ldp_) {
+          if (w.x > sh_x) {
+            w.x -= sh_x;
+            width[pp] = w;
+          } else if (w.x == sh_x) {
+            ++sh_jj;
+            w = make_uint2(mx - sh_jj, 1u);
+            width[pp] = w;
+          }
+          if (LW) {
+            const uint32_t eq = pp > 0 && sh_prevx == w.x;
+            const uint32_t wd = 1u + CWR + ((uint32_t)pp >> 2), sh = 8u * ((uint32_t)pp & 3u) + 4u * (uint32_t)sh_a;
+            uint32_t &cell = cwl[(wd << nbl) + ltid];
+            cell = (cell & ~(0xFu << sh)) | (((w.y < cf ? w.y : cf) | eq << 3) << sh);
+          }
+          sh_prevx = w.x;
+        } else if (LW && pp == ldp_ && ldp_ > 0 && ldp_ <= len) {
+          // the position after the shadowed ones: only its "equal to the previous width" bit
+          const uint32_t wd = 1u + CWR + ((uint32_t)pp >> 2), sh = 8u * ((uint32_t)pp & 3u) + 4u * (uint32_t)sh_a;
+          uint32_t &cell = cwl[(wd << nbl) + ltid];
+          cell = (cell & ~(0x8u << sh)) | ((sh_prevx == w.x ? 1u : 0u) << 3 << sh);
+        }
+      }
+      sh_q += 16;
+      if (sh_q > ldp_) st = 1;  // every position up to ldp seen: back to popping
       continue;
     }
     const uint32_t csym = (st == 2 ? xa : a) == 1 && comp && sym < 4 ? 3u - sym : sym;
@@ -1162,43 +1215,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
       }
     }
     if (do_add) {
-      // gap_shadow (bwtgap.c:81-91) on this strand's width array
-      // (8 positions per round trip: a load-modify-store per position would cost one HBM
-      // round trip each, and a wave waits for its longest lane)
-      uint2 *width = const_cast<uint2 *>(a ? W1 : W0);
-      const uint32_t x = l - k + 1, mx = ixv0.seq_len;
-      uint32_t jj = 0;
-      // LW: the LDS nibbles of strand a follow -- bid (clamped) of every changed position and the
-      // "equals the previous width" bit of positions 1..ldp
-      const uint32_t cf = (uint32_t)opt_max_diff + 1u;
-      const uint32_t w_ldp = LW && ldp <= len ? width[ldp].x : 0u;
-      uint32_t prevx = 0;
-      auto set_nib = [&](int p, uint32_t nib, uint32_t keep) __attribute__((always_inline)) {
-        const uint32_t w = 1u + CWR + ((uint32_t)p >> 2), sh = 8u * ((uint32_t)p & 3u) + 4u * (uint32_t)a;
-        uint32_t &cell = cwl[(w << nbl) + ltid];
-        cell = (cell & ~(keep << sh)) | (nib << sh);
-      };
-      for (int q0 = 0; q0 < ldp; q0 += 8) {
-        uint2 wv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) wv[u] = q0 + u < ldp ? width[q0 + u] : make_uint2(0u, 0u);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (q0 + u >= ldp) break;
-          uint2 w = wv[u];
-          if (w.x > x) { w.x -= x; width[q0 + u] = w; }
-          else if (w.x == x) { ++jj; w = make_uint2(mx - jj, 1u); width[q0 + u] = w; }
-          if (LW) {
-            const int p = q0 + u;
-            const uint32_t eq = p > 0 && prevx == w.x;
-            set_nib(p, (w.y < cf ? w.y : cf) | eq << 3, 0xFu);
-            prevx = w.x;
-          }
-        }
-      }
-      if (LW && ldp > 0 && ldp <= len) set_nib(ldp, (prevx == w_ldp ? 1u : 0u) << 3, 0x8u);
       if ((uint32_t)n_aln >= HS) {
-        
         end_stat = ST_ALN_OVERFLOW;  // hit area full
         st = 3;
         continue;
@@ -1206,6 +1223,19 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
       ent1[P0 - 1 - n_aln] = make_uint4((uint32_t)e_mm | (uint32_t)e_go << 8 | (uint32_t)e_ge << 16 | (uint32_t)a << 24,
                                         k, l, (uint32_t)score | (uint32_t)ldp << 16);
       ++n_aln;
+      // gap_shadow (bwtgap.c:81-91) on this strand's widths [0, ldp): a sub-state of the lane, 16
+      // positions per iteration in the iteration's one round trip (st 5), so the wave does not wait
+      // on a chain of width loads while its other lanes could pop; the lane pops again only once
+      // every width is updated, as the reference does
+      if (ldp > 0) {
+        sh_x = l - k + 1;
+        sh_prevx = 0;
+        sh_q = 0;
+        sh_a = a;
+        sh_jj = 0;
+        sh_ldp = (uint32_t)ldp;
+        st = 5;
+      }
     }
     
     continue;

@@ -64,6 +64,40 @@ def test_sampe_several_references_and_remap(golden_dir, key, tmp_path):
         assert any("\tZR:Z:" in ln for ln in got)
 
 
+STALE = json.load(open(os.path.join(ROOT, "tests", "golden", "stale_manifest.json")))
+
+
+def test_stale_fixture_separates_thread_counts(golden_dir):
+    """The fixture pins something: the reference wrote different SAM with -t 1 and -t 3."""
+    sams = {k: _body(gzip.open(os.path.join(golden_dir, m["sam"]), "rt").read()) for k, m in STALE.items()}
+    assert len(sams["stale.R.t1"]) == len(sams["stale.R.t3"])
+    assert sams["stale.R.t1"] != sams["stale.R.t3"]
+
+
+@pytest.mark.parametrize("key", sorted(STALE))
+def test_sampe_stale_slots_per_thread_count(golden_dir, key, tmp_path):
+    """`sampe -R -t T`: find_optimal_pair's overlap run reads past the pair's own positions into what
+    the last pair of the same reference thread left there (bwapair.c:197, bwape.c:249-253), and
+    select_mapping looks that stale slot's alignment index up in the current pair's alignments
+    (tools/make_sampe_stale_golden.py: with -t 1 the mate of pair B takes the record of its exact
+    hit elsewhere, with -t 2 / -t 3 its own one-mismatch record).  sampe_main.cpp's PosView follows
+    the nearest-greater chain of the pair's residue class mod T; byte for byte except @PG."""
+    m = STALE[key]
+    g = lambda x: os.path.join(golden_dir, x)  # noqa: E731
+    args = [g(m["prefixes"][0]), *map(g, m["sai"][0]), *map(g, m["reads"])]
+    for pre, sai in zip(m["prefixes"][1:], m["sai"][1:]):
+        args += [g(pre), *map(g, sai)]
+    out = tmp_path / "out.sam"
+    r = subprocess.run([CLI, "sampe"] + m["argv"] + ["-f", str(out)] + args, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = _body(gzip.open(g(m["sam"]), "rt").read())
+    got = _body(out.read_text())
+    assert len(got) == len(want)
+    bad = [(i, gl, w) for i, (gl, w) in enumerate(zip(got, want)) if gl != w]
+    assert not bad, f"{len(bad)} lines differ; first:\n got {bad[0][1]}\nwant {bad[0][2]}"
+
+
 def test_sampe_incomplete_reference_group(golden_dir):
     """A trailing reference without both .sai files is refused (pe_inputs_parse)."""
     g = lambda x: os.path.join(golden_dir, x)  # noqa: E731

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 A=$1; B=$2; R=${3:-2}
 mkdir -p gpurun_out/ab
-ARGS="--reads ${READS:-10000000} --steps 2 --warmup 1 --no-cpu --exact-leg 0 --sa2pos 0 --sw-leg 0 $EXTRA"
+ARGS="--reads ${READS:-10000000} --steps 2 --warmup 1 --no-cpu --exact-leg 0 --sa2pos 0 --sw-leg 0 --e2e-leg 0 $EXTRA"
 for r in $(seq 1 $R); do
   for v in A B; do
     lib=$A; [ $v = B ] && lib=$B

@@ -210,8 +210,9 @@ def tandem_threads_case():
     """`sampe -t T` on the tandem genome: pairs from inside the array, each followed T pairs later (T = 2
     or 3) by a copy of itself, so the reference's thread-local position arrays (thread t pairs t, t+T, ...,
     bwape.c:249-253) hold the copy's own positions past its end, while one shared array would hold the
-    pair just before it.  The same reads with -t 1 give other SAM lines, which is what pins the
-    residue-class look-ahead (sampe_main.cpp PosView)."""
+    pair just before it.  (Measured with the reference: -t 1, -t 2 and -t 3 give the same SAM here,
+    because no look-ahead run reaches past a pair's own positions on this genome; the fixture that
+    separates them is tools/make_sampe_stale_golden.py.)"""
     rng = random.Random(33)
     prefix = os.path.join(GOLD, "tandem")
     g = "".join(ln.strip() for ln in open(os.path.join(GOLD, "tandem.fa")) if not ln.startswith(">"))
