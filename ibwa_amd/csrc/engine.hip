@@ -177,6 +177,10 @@ struct ibwa_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
+  // the cooperative pass over a chunk's resumed reads, overlapped with the next chunk's first pass
+  // (gap_overlap): its own stream and events, created at the first such run
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev2[6] = {};
   // index
   DBuf idx[2];
   IndexView ix[2] = {};
@@ -243,6 +247,11 @@ struct ibwa_ctx {
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
   int gap_coop = 1;
+  // overlap each first-pass chunk's cooperative pass over its resumed reads with the next chunk's
+  // first pass (two streams, two resume-state buffers), in at least gap_overlap_chunks chunks
+  int gap_overlap = 1;
+  int gap_overlap_chunks = 4;
+  int64_t gap_overlap_min = 8 << 20;  // reads per chunk at least (a smaller launch is mostly tail)
   int gap_lw = 1;                    // first pass with its widths in LDS (gapped.hip LW) when they fit
   int gap_lw_min_waves = 8;          // ... in a workgroup size that keeps at least this many waves per CU
   int gap_resume = 1;                // early hand-offs leave their search state for the coop pass (LW)
@@ -265,7 +274,8 @@ struct ibwa_ctx {
   int gap_resume_ppb = 48;
   uint32_t gap_resume_cap1 = 4096;   // first-pass static slots per lane when states are left (<= gap_cap1)
   DBuf d_cw, d_ptabg;
-  DBuf d_rdump, d_roff;  // resume states (GapArgs::rdump) and per-read offsets
+  DBuf d_rdump, d_roff;
+  DBuf d_rdump2, c_wbuf, c_nN;  // gap_overlap: the second state buffer; the overlapped pass's own widths / N counts  // resume states (GapArgs::rdump) and per-read offsets
   DBuf d_hpop;           // per read: first-pass pops before its resume state (0: none; ibwa_batch_diag 2)
   bool hpop_valid = false;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
@@ -567,11 +577,14 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
                   &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1], &c->c_dir, &c->c_free, &c->c_hits,
                   &c->c_next, &c->c_pool, &c->c_proot, &c->c_pstore, &c->c_recb, &c->c_stg, &c->d_cw, &c->d_feat,
                   &c->d_hpop, &c->d_ordi, &c->d_ordids, &c->d_ordk, &c->d_ordtmp, &c->d_ptabg, &c->d_rdump, &c->d_roff,
-                  &c->d_selst, &c->d_seltmp, &c->fq_L, &c->fq_cnt, &c->fq_codes, &c->fq_key, &c->fq_len, &c->fq_lenk,
+                  &c->d_selst, &c->d_seltmp, &c->d_rdump2, &c->c_wbuf, &c->c_nN, &c->fq_L, &c->fq_cnt, &c->fq_codes, &c->fq_key, &c->fq_len, &c->fq_lenk,
                   &c->fq_nl, &c->fq_offk, &c->fq_raw, &c->fq_tile, &c->fq_tmp})
     b->release();
   for (auto &b : c->sw) b.release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
+  for (auto &x : c->ev2)
+    if (x) (void)hipEventDestroy(x);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->fq_hinit) (void)hipHostFree(c->fq_hinit);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -620,6 +633,9 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "diag") c->diag = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
+  else if (k == "gap_overlap") c->gap_overlap = value != 0;
+  else if (k == "gap_overlap_chunks" && value >= 2 && value <= 64) c->gap_overlap_chunks = (int)value;
+  else if (k == "gap_overlap_min" && value >= 1) c->gap_overlap_min = value;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
   else if (k == "coop_pool_gb" && value > 0 && value <= 256) c->coop_pool_gb = (int)value;
   else if (k == "coop_stg_room" && value >= 1 && value <= 4) c->coop_stg_room = (int)value;
@@ -1290,12 +1306,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     // reads than an earlier run's resume states per read let the state buffer hold (150 bp at 2 %:
     // 3 chunks of 6.7 M instead of 2 of 10 M, whose overflowing states start over: 5160 -> 4972 ms
     // per 20 M reads, profiles/r04_sweep_mem150.jsonl)
-    int64_t per_chunk = c->gap_reads_per_chunk;
-    if (c->resume_need > 0)
-      per_chunk = std::max<int64_t>(65536, std::min<int64_t>(per_chunk, (int64_t)((double)(((uint64_t)c->gap_resume_gb << 30) / 16) /
-                                                                                   (1.15 * c->resume_need))));
-    const int64_t n_chunks = (std::max<int64_t>(n, 1) + per_chunk - 1) / per_chunk;
-    const int64_t chunk = (std::max<int64_t>(n, 1) + n_chunks - 1) / n_chunks;
     // LDS: bucket heads + free slots + page table per lane, the page bitmap per workgroup
     const uint32_t LG = 13, P0 = c->gap_cap1;
     const int max_pages = (int)std::min<uint32_t>(7, (65536u - P0) >> LG);
@@ -1326,6 +1336,21 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const size_t lds = lds_of(block);
     const int per_cu = std::max<int>(
         1, std::min<int>(c->gap_blocks_per_cu * 256 / block, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
+    const bool resume = lw && c->gap_resume && c->gap_coop && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK;
+    // Overlap (gap_overlap): chunk j's cooperative pass over its resumed reads runs on a second
+    // stream while chunk j+1's first pass runs -- the first pass fills the tail of the cooperative
+    // pass (its longest heavy reads) instead of the chip idling in it.  It needs two state buffers,
+    // so the chunks are smaller (at least gap_overlap_chunks of them); batches too small to gain are
+    // not split.
+    const int64_t ovl_chunks = std::min<int64_t>(c->gap_overlap_chunks, n / std::max<int64_t>(c->gap_overlap_min, 1));
+    const bool ovl = resume && c->gap_overlap && ovl_chunks >= 2;
+    int64_t per_chunk = c->gap_reads_per_chunk;
+    if (ovl) per_chunk = std::min<int64_t>(per_chunk, (n + ovl_chunks - 1) / ovl_chunks);
+    if (c->resume_need > 0)
+      per_chunk = std::max<int64_t>(65536, std::min<int64_t>(per_chunk, (int64_t)((double)(((uint64_t)c->gap_resume_gb << 30) / 16) /
+                                                                                   (1.15 * c->resume_need))));
+    const int64_t n_chunks = (std::max<int64_t>(n, 1) + per_chunk - 1) / per_chunk;
+    const int64_t chunk = (std::max<int64_t>(n, 1) + n_chunks - 1) / n_chunks;
     // persistent grid: fills the chip, but a small batch gets only the lanes it can use, so
     // its per-lane scratch and page pools are sized by the batch, not the worst case
     const int blocks = (int)std::min<int64_t>((int64_t)c->n_cus * per_cu, (chunk + block - 1) / block);
@@ -1337,9 +1362,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (int rc = c->d_cw.ensure(chunk * (uint64_t)cw_words * 4)) return rc;
       if (int rc = c->d_ptabg.ensure(lanes * GAP_MAX_PAGES * 2)) return rc;
     }
-    // resume states of the early hand-offs: per read 1 + the state's offset (0: none), then the
-    // buffer's fill counter and the count of states stored
-    const bool resume = lw && c->gap_resume && c->gap_coop && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK;
+    // resume states of the early hand-offs: per read 1 + the state's offset (0: none), then per state
+    // buffer its fill counter and the count of states stored
     uint64_t rd_cap = 0;
     if (resume) {
       // the buffer holds one first-pass chunk's states at a time (cleared after each chunk)
@@ -1347,9 +1371,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       rd_cap = std::min<uint64_t>(((uint64_t)c->gap_resume_gb << 30) / 16, (uint64_t)((double)chunk * per_read) + (1u << 16));
       if (c->gap_resume_records > 0) rd_cap = (uint64_t)c->gap_resume_records;
       if (int rc = c->d_rdump.ensure(rd_cap * 16)) return rc;
+      if (ovl)
+        if (int rc = c->d_rdump2.ensure(rd_cap * 16)) return rc;
       c->stats.resume_records_cap = (int64_t)rd_cap;
-      if (int rc = c->d_roff.ensure(((uint64_t)n + 2) * 8)) return rc;
-      HIPCHK(hipMemsetAsync(c->d_roff.p, 0, ((uint64_t)n + 2) * 8, c->stream));
+      if (int rc = c->d_roff.ensure(((uint64_t)n + 4) * 8)) return rc;
+      HIPCHK(hipMemsetAsync(c->d_roff.p, 0, ((uint64_t)n + 4) * 8, c->stream));
       if (int rc = c->d_hpop.ensure(((uint64_t)n + 1) * 4)) return rc;
       HIPCHK(hipMemsetAsync(c->d_hpop.p, 0, ((uint64_t)n + 1) * 4, c->stream));
       resume_states = true;
@@ -1372,108 +1398,152 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     // The reads of chunk [b0, b0 + cnt) that left a resume state go through the cooperative pass right
     // after their chunk's first pass, so the state buffer holds one chunk's states at a time: a read
     // it resolves is done (status 0), one it hands on starts over in the passes below.
-    auto coop_resumed = [&](int64_t b0, int64_t cnt) -> int {
+    // Launch part: select the resumed reads of chunk [b0, b0 + cnt) (state buffer p), order them
+    // largest stack first, then k_coop on stream st.  Without overlap the widths and N counts are the
+    // chunk's own first-pass rows, still in place (their gap_shadow updates included); with overlap the
+    // next chunk's k_width overwrites those rows, so the pass runs its own k_width over the selected
+    // reads (c_wbuf, c_nN) and replays gap_shadow hit by hit from the states (wb_base < 0).
+    struct CoopRun {
+      int64_t lanes = 0, b0 = 0, cnt = 0;
+      int p = 0;
+      uint32_t pool_pages = 0;
+      const int64_t *ids = nullptr;
+    };
+    auto coop_launch = [&](int64_t b0, int64_t cnt, int p, hipStream_t st, hipEvent_t *evs, bool own_widths,
+                           CoopRun &R) -> int {
+      R = CoopRun();
+      R.b0 = b0;
+      R.cnt = cnt;
+      R.p = p;
       size_t tb = 0;
       HIPCHK(select_resumed(c->d_roff.as<uint64_t>(), b0, cnt, c->d_status.as<uint32_t>(), nullptr, nullptr, nullptr,
-                            nullptr, &tb, c->stream));
+                            nullptr, &tb, st));
       if (int rc = c->d_seltmp.ensure(tb + 16)) return rc;
       if (int rc = c->d_ids.ensure(cnt * 8)) return rc;
       if (int rc = c->d_selst.ensure(cnt * 4)) return rc;
       unsigned long long *d_cnt = c->d_counter.as<unsigned long long>() + 5;
       HIPCHK(select_resumed(c->d_roff.as<uint64_t>(), b0, cnt, c->d_status.as<uint32_t>(), c->d_ids.as<int64_t>(),
-                            c->d_selst.as<uint32_t>(), d_cnt, c->d_seltmp.p, &tb, c->stream));
+                            c->d_selst.as<uint32_t>(), d_cnt, c->d_seltmp.p, &tb, st));
       unsigned long long lanes_u = 0;
-      HIPCHK(hipMemcpyAsync(&lanes_u, d_cnt, 8, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
+      HIPCHK(hipMemcpyAsync(&lanes_u, d_cnt, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
       const int64_t lanes = (int64_t)lanes_u;
-      if (lanes > 0) {
-        uint32_t stg_log2 = 10;
-        while ((1u << stg_log2) < (uint32_t)c->coop_stg_room * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
-        const int full_blocks = c->n_cus * c->coop_waves_per_cu;
-        const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
-        const uint32_t freecap = 4096, hcap = 4096;
-        const uint64_t pool_bytes = std::min<uint64_t>(
-            (uint64_t)c->coop_pool_gb << 30,
-            std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
-        const uint32_t pool_pages = c->coop_pool_pages ? c->coop_pool_pages : (uint32_t)(pool_bytes / (COOP_PG * 16ull));
-        if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
-        if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
-        if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
-        if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
-        if (int rc = c->c_recb.ensure((uint64_t)blocks * COOP_RREC * 16)) return rc;
-        if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
-        if (int rc = c->c_next.ensure(64)) return rc;
-        if (int rc = c->r_status.ensure(lanes * 4)) return rc;
-        // largest first-pass stack first, as in the main cooperative pass below
-        const int64_t *ids = c->d_ids.as<int64_t>();
-        if (c->coop_order && lanes > 1) {
-          size_t ob = 0;
-          HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &ob, c->stream));
-          if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;
-          if (int rc = c->d_ordi.ensure(lanes * 8)) return rc;
-          if (int rc = c->d_ordids.ensure(lanes * 8)) return rc;
-          if (int rc = c->d_ordtmp.ensure(ob + 16)) return rc;
-          HIPCHK(order_heavy_first(c->d_selst.as<uint32_t>(), c->d_ids.as<int64_t>(), lanes, c->d_ordk.as<uint32_t>(),
-                                   c->d_ordi.as<uint32_t>(), c->d_ordids.as<int64_t>(), c->d_ordtmp.p, &ob, c->stream));
-          ids = c->d_ordids.as<int64_t>();
-        }
-        // the widths and N counts are the chunk's own first-pass rows, still in place (their gap_shadow
-        // updates included: the pass does not replay them)
-        CoopArgs K = {};
-        K.ix[0] = c->ix[0];
-        K.ix[1] = c->ix[1];
-        K.o64[0] = c->o64[0].as<uint4>();
-        K.o64[1] = c->o64[1].as<uint4>();
-        K.seq = A.seq;
-        K.off = A.off;
-        K.len = A.len;
-        K.ids = ids;
-        K.n = lanes;
-        K.out_by_id = 1;
-        K.maxdiff_tab = A.maxdiff_tab;
+      R.lanes = lanes;
+      if (lanes <= 0) return 0;
+      uint32_t stg_log2 = 10;
+      while ((1u << stg_log2) < (uint32_t)c->coop_stg_room * (9u * (uint32_t)(max_len + 1) + 16u)) ++stg_log2;
+      const int full_blocks = c->n_cus * c->coop_waves_per_cu;
+      const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
+      const uint32_t freecap = 4096, hcap = 4096;
+      const uint64_t pool_bytes = std::min<uint64_t>(
+          (uint64_t)c->coop_pool_gb << 30,
+          std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
+      const uint32_t pool_pages = c->coop_pool_pages ? c->coop_pool_pages : (uint32_t)(pool_bytes / (COOP_PG * 16ull));
+      R.pool_pages = pool_pages;
+      if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
+      if (int rc = c->c_dir.ensure((uint64_t)blocks * COOP_NSTK * COOP_MAXP * 4)) return rc;
+      if (int rc = c->c_free.ensure((uint64_t)blocks * freecap * 4)) return rc;
+      if (int rc = c->c_hits.ensure((uint64_t)blocks * hcap * 16)) return rc;
+      if (int rc = c->c_recb.ensure((uint64_t)blocks * COOP_RREC * 16)) return rc;
+      if (int rc = c->c_pool.ensure((uint64_t)pool_pages * COOP_PG * 16)) return rc;
+      if (int rc = c->c_next.ensure(64)) return rc;
+      if (int rc = c->r_status.ensure(lanes * 4)) return rc;
+      // largest first-pass stack first, as in the main cooperative pass below
+      const int64_t *ids = c->d_ids.as<int64_t>();
+      if (c->coop_order && lanes > 1) {
+        size_t ob = 0;
+        HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &ob, st));
+        if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;
+        if (int rc = c->d_ordi.ensure(lanes * 8)) return rc;
+        if (int rc = c->d_ordids.ensure(lanes * 8)) return rc;
+        if (int rc = c->d_ordtmp.ensure(ob + 16)) return rc;
+        HIPCHK(order_heavy_first(c->d_selst.as<uint32_t>(), c->d_ids.as<int64_t>(), lanes, c->d_ordk.as<uint32_t>(),
+                                 c->d_ordi.as<uint32_t>(), c->d_ordids.as<int64_t>(), c->d_ordtmp.p, &ob, st));
+        ids = c->d_ordids.as<int64_t>();
+      }
+      R.ids = ids;
+      CoopArgs K = {};
+      K.ix[0] = c->ix[0];
+      K.ix[1] = c->ix[1];
+      K.o64[0] = c->o64[0].as<uint4>();
+      K.o64[1] = c->o64[1].as<uint4>();
+      K.seq = A.seq;
+      K.off = A.off;
+      K.len = A.len;
+      K.ids = ids;
+      K.n = lanes;
+      K.out_by_id = 1;
+      K.maxdiff_tab = A.maxdiff_tab;
+      K.wstride = A.wstride;
+      K.wlen1 = A.wlen1;
+      if (own_widths) {
+        if (int rc = c->c_wbuf.ensure((uint64_t)lanes * A.wstride * 8)) return rc;
+        if (int rc = c->c_nN.ensure((uint64_t)lanes * 2 + 2)) return rc;
+        K.wbuf = c->c_wbuf.as<uint2>();
+        K.wb_base = -1;
+        K.nN = c->c_nN.as<uint16_t>();
+      } else {
         K.wbuf = c->d_wbuf.as<uint2>();
         K.wb_base = b0;
-        K.wstride = A.wstride;
-        K.wlen1 = A.wlen1;
         K.nN = c->d_nN.as<uint16_t>();
-        K.stg = c->c_stg.as<uint4>();
-        K.stg_log2 = stg_log2;
-        K.dir = c->c_dir.as<uint32_t>();
-        K.freel = c->c_free.as<uint32_t>();
-        K.freecap = freecap;
-        K.pool = c->c_pool.as<uint4>();
-        K.pool_pages = pool_pages;
-        K.pool_next = c->c_next.as<uint32_t>();
-        K.hits = c->c_hits.as<uint4>();
-        K.recb = c->c_recb.as<uint4>();
-        K.rdump = c->d_rdump.as<uint4>();
-        K.roff = c->d_roff.as<uint64_t>();
-        K.hcap = hcap;
-        K.max_iters = 1u << 24;
-        K.aln = c->d_aln.as<uint4>();
-        K.aln_total = c->stream_total;
-        K.aln_next = c->d_counter.as<unsigned long long>() + 1;
-        K.aln_off = c->d_aoff.as<uint64_t>();
-        K.n_aln = c->d_naln.as<int32_t>();
-        K.status = c->r_status.as<uint32_t>();
-        K.o = o;
-        HIPCHK(hipEventRecord(c->ev[3], c->stream));
-        HIPCHK(hipEventRecord(c->ev[5], c->stream));
-        HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, c->stream));
-        HIPCHK(hipEventRecord(c->ev[4], c->stream));
-        HIPCHK(resume_fixup(c->r_status.as<uint32_t>(), ids, lanes, c->d_status.as<uint32_t>(), c->d_roff.as<uint64_t>(),
-                            c->stream));
-        HIPCHK(hipEventSynchronize(c->ev[4]));
-        note_coop_pages(c, pool_pages);
+      }
+      K.stg = c->c_stg.as<uint4>();
+      K.stg_log2 = stg_log2;
+      K.dir = c->c_dir.as<uint32_t>();
+      K.freel = c->c_free.as<uint32_t>();
+      K.freecap = freecap;
+      K.pool = c->c_pool.as<uint4>();
+      K.pool_pages = pool_pages;
+      K.pool_next = c->c_next.as<uint32_t>();
+      K.hits = c->c_hits.as<uint4>();
+      K.recb = c->c_recb.as<uint4>();
+      K.rdump = (p ? c->d_rdump2 : c->d_rdump).as<uint4>();
+      K.roff = c->d_roff.as<uint64_t>();
+      K.hcap = hcap;
+      K.max_iters = 1u << 24;
+      K.aln = c->d_aln.as<uint4>();
+      K.aln_total = c->stream_total;
+      K.aln_next = c->d_counter.as<unsigned long long>() + 1;
+      K.aln_off = c->d_aoff.as<uint64_t>();
+      K.n_aln = c->d_naln.as<int32_t>();
+      K.status = c->r_status.as<uint32_t>();
+      K.o = o;
+      HIPCHK(hipEventRecord(evs[0], st));
+      if (own_widths) {
+        AlnArgs B = A;
+        B.ids = ids;
+        B.n = lanes;
+        B.wbuf = c->c_wbuf.as<uint2>();
+        B.nN = c->c_nN.as<uint16_t>();
+        B.cw = nullptr;  // the cooperative pass reads the full widths
+        B.feat = nullptr;
+        HIPCHK(launch_width(B, c->block, st));
+      }
+      HIPCHK(hipEventRecord(evs[2], st));
+      // its own claim counter: the first pass of the next chunk claims with d_counter[0] meanwhile
+      HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>() + (own_widths ? 6 : 0), blocks, st));
+      HIPCHK(hipEventRecord(evs[1], st));
+      HIPCHK(resume_fixup(c->r_status.as<uint32_t>(), ids, lanes, c->d_status.as<uint32_t>(), c->d_roff.as<uint64_t>(),
+                          st));
+      return 0;
+    };
+    // Finish part (after the launch's kernels): the reads it resolved, the state buffer's use, and the
+    // buffer's fill counter back to 0 for the chunk after next.
+    auto coop_finish = [&](CoopRun &R, hipStream_t st, hipEvent_t *evs) -> int {
+      unsigned long long *rdn = c->d_roff.as<unsigned long long>() + n + 2 * R.p;
+      if (R.lanes > 0) {
+        HIPCHK(hipEventSynchronize(evs[1]));
+        note_coop_pages(c, R.pool_pages);
         float t_all = 0, t_w = 0;
-        HIPCHK(hipEventElapsedTime(&t_all, c->ev[3], c->ev[4]));
-        HIPCHK(hipEventElapsedTime(&t_w, c->ev[3], c->ev[5]));
-        std::vector<uint32_t> rs(lanes);
-        std::vector<int64_t> rid(lanes);
-        HIPCHK(hipMemcpy(rs.data(), c->r_status.p, lanes * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(rid.data(), ids, lanes * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipEventElapsedTime(&t_all, evs[0], evs[1]));
+        HIPCHK(hipEventElapsedTime(&t_w, evs[0], evs[2]));
+        std::vector<uint32_t> rs(R.lanes);
+        std::vector<int64_t> rid(R.lanes);
+        HIPCHK(hipMemcpyAsync(rs.data(), c->r_status.p, R.lanes * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(rid.data(), R.ids, R.lanes * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
         int64_t ok = 0;
-        for (int64_t j = 0; j < lanes; ++j)
+        for (int64_t j = 0; j < R.lanes; ++j)
           if (rs[j] == 0) {
             ++ok;
             c->resumed_ids.push_back(rid[j]);
@@ -1483,19 +1553,36 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         res_ok += ok;
         if (c->verbose)
           fprintf(stderr, "[ibwa_amd] chunk at %lld: %lld resumed reads through the cooperative pass, %.1f ms\n",
-                  (long long)b0, (long long)lanes, t_all);
+                  (long long)R.b0, (long long)R.lanes, t_all);
       }
-      // the next chunk's states start at the front of the buffer (the stored counts stay)
       unsigned long long used = 0;
-      HIPCHK(hipMemcpy(&used, c->d_roff.as<unsigned long long>() + n, 8, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpyAsync(&used, rdn, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
       c->stats.resume_records += (int64_t)used;
       c->stats.resume_records_peak = std::max<int64_t>(c->stats.resume_records_peak, (int64_t)used);
-      if (cnt >= 65536) c->resume_need = std::max(c->resume_need, (double)used / (double)cnt);
-      HIPCHK(hipMemsetAsync(c->d_roff.as<unsigned long long>() + n, 0, 8, c->stream));
+      if (R.cnt >= 65536) c->resume_need = std::max(c->resume_need, (double)used / (double)R.cnt);
+      HIPCHK(hipMemsetAsync(rdn, 0, 8, st));
+      HIPCHK(hipEventRecord(evs[3], st));  // the state buffer may be written again
       return 0;
     };
-    for (int64_t b0 = 0; b0 < n; b0 += chunk) {
+    auto coop_resumed = [&](int64_t b0, int64_t cnt) -> int {
+      CoopRun R;
+      hipEvent_t evs[4] = {c->ev[3], c->ev[4], c->ev[5], c->ev[6]};
+      if (int rc = coop_launch(b0, cnt, 0, c->stream, evs, false, R)) return rc;
+      return coop_finish(R, c->stream, evs);
+    };
+    if (ovl && !c->stream2) {
+      HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+      for (auto &x : c->ev2) HIPCHK(hipEventCreate(&x));
+    }
+    CoopRun pending;         // overlap: the cooperative launch in flight on stream2
+    bool have_pending = false;
+    int64_t j_chunk = 0;
+    for (int64_t b0 = 0; b0 < n; b0 += chunk, ++j_chunk) {
       const int64_t cnt = std::min(chunk, n - b0);
+      const int par = ovl ? (int)(j_chunk & 1) : 0;  // state buffer of this chunk
+      // overlap: the buffer is free once the cooperative pass of the chunk before last has finished
+      if (ovl && j_chunk >= 2) HIPCHK(hipStreamWaitEvent(c->stream, c->ev2[3 + par], 0));
       AlnArgs B = A;
       B.n = cnt;
       B.off = A.off + b0;
@@ -1531,8 +1618,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.early2_iters = c->gap_early2_iters;
       G.early2_entries = c->gap_early2_entries;
       if (resume) {
-        G.rdump = c->d_rdump.as<uint4>();
-        G.rd_next = c->d_roff.as<unsigned long long>() + n;
+        G.rdump = (par ? c->d_rdump2 : c->d_rdump).as<uint4>();
+        G.rd_next = c->d_roff.as<unsigned long long>() + n + 2 * par;
         G.rd_cap = rd_cap;
         G.roff = c->d_roff.as<uint64_t>() + b0;
         G.hpop = c->d_hpop.as<uint32_t>() + b0;
@@ -1592,8 +1679,27 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                 "seed widths %.3f candidate %.3f; exact steps %.3f (unique interval %.3f) (%.3g live lane-iterations)\n",
                 pf[11] / li, pf[12] / li, pf[13] / li, pf[14] / li, pf[15] / li, pf[17] / li, pf[18] / li, (double)pf[16]);
       }
-      if (resume_states)
+      if (resume_states && !ovl)
         if (int rc = coop_resumed(b0, cnt)) return rc;
+      if (resume_states && ovl) {
+        // the previous chunk's cooperative pass (stream2) is waited for and its results taken, then
+        // this chunk's is launched there; the next chunk's first pass (stream 1, next iteration) then
+        // fills the chip as its waves retire
+        if (have_pending) {
+          hipEvent_t evs[4] = {c->ev2[0], c->ev2[1], c->ev2[2], c->ev2[3 + pending.p]};
+          if (int rc = coop_finish(pending, c->stream2, evs)) return rc;
+          have_pending = false;
+        }
+        hipEvent_t evs[4] = {c->ev2[0], c->ev2[1], c->ev2[2], c->ev2[3 + par]};
+        if (int rc = coop_launch(b0, cnt, par, c->stream2, evs, true, pending)) return rc;
+        have_pending = true;
+      }
+    }
+    if (have_pending) {
+      hipEvent_t evs[4] = {c->ev2[0], c->ev2[1], c->ev2[2], c->ev2[3 + pending.p]};
+      if (int rc = coop_finish(pending, c->stream2, evs)) return rc;
+      have_pending = false;
+      HIPCHK(hipStreamSynchronize(c->stream2));
     }
   }
   // first pass, in chunks of lanes_per_chunk reads
@@ -1669,9 +1775,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     c->stats.n_heavy += (s_ & ST_HEAVY) != 0;
   }
   if (resume_states) {
-    unsigned long long rs[2] = {0, 0};
-    HIPCHK(hipMemcpy(rs, c->d_roff.as<unsigned long long>() + n, 16, hipMemcpyDeviceToHost));
-    c->stats.n_resumed = (int64_t)rs[1];
+    unsigned long long rs[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpy(rs, c->d_roff.as<unsigned long long>() + n, 32, hipMemcpyDeviceToHost));
+    c->stats.n_resumed = (int64_t)(rs[1] + rs[3]);  // states stored in either buffer
     c->stats.n_heavy += res_ok;  // handed on and resolved by the per-chunk cooperative launches
     c->stats.n_coop += res_ok;
     c->stats.ms_coop += res_ms;
