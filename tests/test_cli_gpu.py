@@ -197,3 +197,29 @@ def test_cli_gpu_parse_carry_overflow(golden_dir, sai_manifest, tmp_path):
     got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path,
                       {"IBWA_ALN_SUBBATCH": "500", "IBWA_FQ_PIECE_BYTES": "20000", "IBWA_FQ_CARRY_BYTES": "4096"}, "c.sai")
     assert oracle.sai_body_equal(got, gold)
+
+
+def test_cli_gpu_parse_more_than_2_24_records(golden_dir, tmp_path):
+    """One parsed block holding more than 2^24 records: the device scan packs each
+    record's kept-read rank and code offset into one 64-bit key (fastq.hip KeptKey), 32 bits each
+    -- a block is < 4 GiB, so neither half can wrap.  17 M tiny records (20 bp, empty headers, 46 B
+    each: one 780 MB piece) aligned with -n 0 from the GPU parse == the host readers' .sai."""
+    import numpy as np
+    n, L = (1 << 24) + 300_000, 20
+    rng = np.random.default_rng(5)
+    rec = np.empty((n, 2 + L + 1 + 2 + L + 1), dtype=np.uint8)
+    rec[:, 0] = ord("@")
+    rec[:, 1] = ord("\n")
+    rec[:, 2:2 + L] = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, (n, L), dtype=np.uint8)]
+    rec[:, 2 + L] = ord("\n")
+    rec[:, 3 + L] = ord("+")
+    rec[:, 4 + L] = ord("\n")
+    rec[:, 5 + L:5 + 2 * L] = ord("I")
+    rec[:, 5 + 2 * L] = ord("\n")
+    fq = tmp_path / "tiny.fq"
+    rec.tofile(str(fq))
+    del rec
+    host = run_cli_env(["-n", "0"], golden_dir, str(fq), tmp_path, {"IBWA_ALN_GPU_PARSE": "0"}, "host.sai")
+    dev = run_cli_env(["-n", "0"], golden_dir, str(fq), tmp_path, {"IBWA_FQ_PIECE_BYTES": str(1 << 30)}, "dev.sai")
+    assert len(host) > 64 + 4 * n
+    assert dev[64:] == host[64:]
