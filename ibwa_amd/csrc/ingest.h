@@ -81,7 +81,10 @@ class FastqGpu {
     const uint64_t fs = std::max<uint64_t>((fsize_ + 4095) / 4096 * 4096, 4096);
     piece_ = std::max<uint64_t>(piece_bytes, 4096);
     carry_ = std::min<uint64_t>(std::max<uint64_t>(carry_bytes, 4096), fs);
-    chunk_ = std::min<uint64_t>(piece_ * G_, fs);
+    // regions of equal size (at most piece_bytes per GPU): the last groups then hold as many reads as
+    // the others, so the lanes finish together instead of one short group running alone at the end
+    const uint64_t per = piece_ * G_, n_reg = (fs + per - 1) / per;
+    chunk_ = std::min<uint64_t>(per, ((fs + n_reg - 1) / n_reg + 4095) / 4096 * 4096);
     for (auto &b : buf_) {
       void *p = nullptr;
       if (ibwa_host_alloc(carry_ + chunk_ + 64, &p)) { ok_ = false; return; }
