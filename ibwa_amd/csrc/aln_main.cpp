@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <chrono>
@@ -440,7 +441,9 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         ing.push_back(x);
       }
     const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
-    const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)1 << 30;
+    // 2 GiB per GPU (~8 M reads of 100 bp): fewer, larger groups than 1 GiB pieces (align phase 6.21
+    // -> 5.96 s at 50 M reads, profiles/r05_e2e_b.json); 3 GiB pieces need ~274 GB at 2 lanes
+    const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
     const uint64_t carry = cm && atoll(cm) > 0 ? (uint64_t)atoll(cm) : (uint64_t)256 << 20;
     fg.reset(new FastqGpu(fq_dev, ing, n_gpus, opt.mode, opt.trim_qual, kSub, piece, carry,
                           [opt](int max_len) { return batch_key(opt, max_len); }));
@@ -671,10 +674,6 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   if (out != stdout) fclose(out);
   int64_t dev_now = 0, dev_peak = 0;
   ibwa_device_bytes(&dev_now, &dev_peak);
-  for (int l = n_lanes - 1; l >= 1; --l)  // lanes sharing the index first
-    for (auto *x : lctx[l]) ibwa_ctx_destroy(x);
-  for (auto *x : ctx) ibwa_ctx_destroy(x);
-  if (have < 0) return 1;
   ph.print("ibwa-amd aln");
   fprintf(stderr, "[ibwa-amd aln] device memory: peak %.1f GB of engine buffers on %d GPU(s) (%d context(s) per GPU, "
                   "index shared)\n", dev_peak / 1e9, n_gpus, n_lanes);
@@ -693,5 +692,16 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     fprintf(stderr, "[ibwa-amd aln] input parse: %lld reads in %.2f s on %d host threads = %.2f M reads/s (%.3f M per thread)\n",
             (long long)tot_seqs, parse_s, nt, tot_seqs / parse_s / 1e6, tot_seqs / parse_s / 1e6 / nt);
   }
-  return 0;
+  // Every record is written and every kernel has finished: the process ends here.  Tearing down the
+  // contexts, the ingest slots and the pinned buffers one by one only hands back what the driver and
+  // the OS reclaim at exit anyway (IBWA_ALN_CLEAN_EXIT=1 does it, for leak checkers).
+  if (env_int("IBWA_ALN_CLEAN_EXIT", 0) == 0) {
+    fflush(stdout);
+    fflush(stderr);
+    _exit(have < 0 ? 1 : 0);
+  }
+  for (int l = n_lanes - 1; l >= 1; --l)  // lanes sharing the index first
+    for (auto *x : lctx[l]) ibwa_ctx_destroy(x);
+  for (auto *x : ctx) ibwa_ctx_destroy(x);
+  return have < 0 ? 1 : 0;
 }

@@ -249,7 +249,10 @@ struct ibwa_ctx {
   int gap_coop = 1;
   // overlap each first-pass chunk's cooperative pass over its resumed reads with the next chunk's
   // first pass (two streams, two resume-state buffers), in at least gap_overlap_chunks chunks
-  int gap_overlap = 1;
+  // Off by default: at 50 M reads 4 overlapped chunks took 5 541 ms per step against 5 345 ms for 3
+  // sequential ones (profiles/r05_sweep_overlap.jsonl: the chunks' extra first-pass tails and the
+  // pass's own k_width cost more than the hidden cooperative-pass tails gain)
+  int gap_overlap = 0;
   int gap_overlap_chunks = 4;
   int64_t gap_overlap_min = 8 << 20;  // reads per chunk at least (a smaller launch is mostly tail)
   int gap_lw = 1;                    // first pass with its widths in LDS (gapped.hip LW) when they fit
