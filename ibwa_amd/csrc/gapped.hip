@@ -199,6 +199,9 @@ template <bool WIDE, bool PROF, bool LW, int NBL>
 __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long *counter) {
   static_assert(!(WIDE && LW), "the LDS-width variant is a first-pass kernel");
   using E = Ent<WIDE>;
+  // gap_shadow positions per iteration (st 5): 16 in the LDS-width first pass (the hot kernel), 8
+  // elsewhere (one block register set: the other variants are at their register limit)
+  constexpr int SHW = LW ? 16 : 8;
   using H = typename E::Head;
   constexpr bool REUSE = WIDE;
   constexpr uint32_t NILH = E::NIL;
@@ -352,21 +355,26 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     }
     return false;
   };
-  auto end_read = [&](uint32_t stat) __attribute__((always_inline)) {
+  // (the room for its na hits was reserved at pos, and its first four hits hb.v3, v2, v1, v0 loaded,
+  // in the iteration's round trip: see `ending` below)
+  auto end_read = [&](uint32_t stat, uint32_t na, unsigned long long pos, const Blk &hb) __attribute__((always_inline)) {
     const bool pl_ = pleader();
-    int na = stat ? 0 : n_aln;
     KArgs *ka = args();
     if (na) {
-      const unsigned long long pos = atomicAdd(ka->aln_next, (unsigned long long)na);
       if (pos + (unsigned long long)na > ka->aln_total) {
         stat |= ST_ALN_OVERFLOW;
         na = 0;
       } else {
-        for (int j = 0; j < na; ++j) {
-          uint4 h = ent1[P0 - 1 - j];
-          h.w &= 0xFFFFu;  // the hit's last_diff_pos rides in bits 16-31 (resume states replay gap_shadow)
+        // the hit's last_diff_pos rides in bits 16-31 (resume states replay gap_shadow): masked off
+        auto put = [&](uint32_t j, uint4 h) __attribute__((always_inline)) {
+          h.w &= 0xFFFFu;
           ka->aln[pos + j] = h;
-        }
+        };
+        put(0, hb.v3);
+        if (na > 1) put(1, hb.v2);
+        if (na > 2) put(2, hb.v1);
+        if (na > 3) put(3, hb.v0);
+        for (uint32_t j = 4; j < na; ++j) put(j, ent1[P0 - 1 - j]);
         ka->aln_off[ro] = pos;
       }
     }
@@ -465,7 +473,6 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     uint64_t t_top = pnow();
     if (PROF && t_rest) pf3 += t_top - t_rest;
     // ------------------------------------------------ retire reads that ended last iteration
-    if (st == 3) end_read(end_stat);
     // the search state of a claimed read whose length, max_diff and N count are set: the two roots
     // (bwtgap.c:126-127: strand 0 then strand 1, both score 0 -> C = strand 1)
     auto start_read = [&]() __attribute__((always_inline)) {
@@ -735,8 +742,15 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     // a shadowing lane loads 16 width positions of its hit's strand into the block registers
     const bool shd = st == 5;
     const uint4 *shp = reinterpret_cast<const uint4 *>((sh_a ? W1 : W0) + sh_q);
-    load_blk(shd ? shp : obq, shd ? 0u : ql, qrun || shd, bl);
-    load_blk(shd ? shp + 4 : obq, shd ? 0u : qk - 1, (qrun && !qkneg && !qshare) || shd, bk);
+    // a lane whose read ended last iteration (st 3) reserves its hits' room in the output stream and
+    // loads its first four hits (the last static slots) in this same round trip; the consume step
+    // writes them (end_read) -- the wave no longer waits on the atomic and then on the hit loads
+    const bool ending = st == 3;
+    const uint32_t na_end = ending && !end_stat ? (uint32_t)n_aln : 0u;
+    unsigned long long e_pos = 0;
+    if (na_end) e_pos = atomicAdd(args()->aln_next, (unsigned long long)na_end);
+    load_blk(shd ? shp : na_end ? ent1 + (P0 - 4) : obq, (shd || na_end) ? 0u : ql, qrun || shd || na_end, bl);
+    load_blk(shd ? shp + 4 : obq, shd ? 0u : qk - 1, (qrun && !qkneg && !qshare) || (shd && SHW > 8), bk);
     // width bounds of strand a at positions i-2, i-1 and the seed pair
     const uint2 *Wa = a ? W1 : W0;
     const uint2 *SWa = a ? SW1 : SW0;
@@ -826,6 +840,10 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
       st = 3;
       continue;
     }
+    if (ending) {
+      end_read(end_stat, na_end, e_pos, bl);
+      continue;
+    }
     if (shd) {
       // ---- gap_shadow (bwtgap.c:81-91) of positions sh_q .. sh_q + 15 (< ldp) of strand sh_a: the
       // hit's interval size is taken off every width above it, and a width equal to it becomes the
@@ -836,7 +854,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
       const int ldp_ = (int)sh_ldp;
       const uint4 wq[8] = {bl.v0, bl.v1, bl.v2, bl.v3, bk.v0, bk.v1, bk.v2, bk.v3};
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
+      for (int u = 0; u < SHW; ++u) {
         const int pp = sh_q + u;
         const uint4 &h = wq[u >> 1];
         uint2 w = (u & 1) ? make_uint2(h.z, h.w) : make_uint2(h.x, h.y);
@@ -863,7 +881,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
           cell = (cell & ~(0x8u << sh)) | ((sh_prevx == w.x ? 1u : 0u) << 3 << sh);
         }
       }
-      sh_q += 16;
+      sh_q += SHW;
       if (sh_q > ldp_) st = 1;  // every position up to ldp seen: back to popping
       continue;
     }
