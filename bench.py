@@ -433,6 +433,22 @@ def e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns):
         out["fastq_bytes"] = os.path.getsize(fq)
         out["fastq_write_s"] = time.perf_counter() - t
         sai = os.path.join(d, "reads.sai")
+        import re
+        # parse-only first (IBWA_ALN_PARSE_ONLY: the file is read and parsed into groups, nothing is
+        # aligned; no arena): the ingest rate of one process
+        r = subprocess.run([CLI, "aln", *args.aln.split(), "-f", sai, pre, fq], stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE, timeout=600,
+                           env=dict(os.environ, IBWA_ALN_TIMES="1", IBWA_ALN_PARSE_ONLY="1", IBWA_ARENA_GB="0"))
+        err = r.stderr.decode(errors="replace")
+        m_ = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s parsing ahead", err)
+        m2 = re.search(r"parse only: (\d+) reads, ([\d.]+) s parsing", err)
+        if r.returncode == 0 and m_ and m2:
+            out["parse_only"] = {"records": int(m_.group(1)), "producer_s": float(m_.group(2)),
+                                 "records_per_s": int(m_.group(1)) / max(float(m_.group(2)), 1e-3),
+                                 "consumer_wait_s": float(m2.group(2)),
+                                 "note": "GPU parse of the whole file with nothing aligned: producer_s = the parse "
+                                         "calls' wall time (file reads overlapped); consumer_wait_s = the time the "
+                                         "group loop waited for parsed groups"}
         env = dict(os.environ, IBWA_ALN_TIMES="1")
         t = time.perf_counter()
         r = subprocess.run([CLI, "aln", *args.aln.split(), "-f", sai, pre, fq], stdout=subprocess.DEVNULL,
@@ -441,7 +457,6 @@ def e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns):
         err = r.stderr.decode(errors="replace")
         if r.returncode != 0:
             raise RuntimeError(f"ibwa-amd aln failed ({r.returncode}): {err[-800:]}")
-        import re
         phases = {}
         for ln in err.splitlines():
             if "wall s:" in ln:
