@@ -39,6 +39,7 @@ using ibwa_cli::FastqBulk;
 using ibwa_cli::FastqGpu;
 using ibwa_cli::SeqReader;
 
+const auto g_proc_t0 = std::chrono::steady_clock::now();  // process start (static initialisation)
 const int kBatch = 0x40000;  // bwtaln.c:193
 // A GPU run takes up to kGroup consecutive batches whose batch-level options (bwtaln.c:86-93: the
 // max_diff of the batch's longest read, which clamps max_gapo and sizes the stack) are the same,
@@ -370,6 +371,8 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   }
   if (n_gpus < 1) n_gpus = 1;
   ibwa_sam::Phases ph;
+  ph.t0 = g_proc_t0;
+  ph.mark("startup");  // process start to here: loading, option parsing, opening the input
   // GPU slice g runs on device g mod (visible devices): more slices than devices rehearse the
   // multi-GPU path on fewer GPUs (index replication, the slice split, the ordered writer)
   int n_dev = 0;
@@ -416,6 +419,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         fprintf(stderr, "[ibwa-amd aln] arena on GPU %d: %.1f GiB reserved in %.0f ms\n", d, want_gb[d], ms[d]);
     }
   }
+  ph.mark("device arena");  // HIP start-up, and the wait for memory a previous process released
   // FASTQ parsed on the GPUs: n_lanes + 3 ingest contexts per GPU (their own streams and buffers;
   // ingest.h's slots); the first region is read and parsed while the index loads
   std::vector<ibwa_ctx_t *> ing;
@@ -672,6 +676,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     return 1;
   }
   if (out != stdout) fclose(out);
+  ph.mark("last records written");
   int64_t dev_now = 0, dev_peak = 0;
   ibwa_device_bytes(&dev_now, &dev_peak);
   ph.print("ibwa-amd aln");

@@ -1308,7 +1308,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     // only its slowest reads still run, so fewer (and balanced) launches waste less -- but no more
     // reads than an earlier run's resume states per read let the state buffer hold (150 bp at 2 %:
     // 3 chunks of 6.7 M instead of 2 of 10 M, whose overflowing states start over: 5160 -> 4972 ms
-    // per 20 M reads, profiles/r04_sweep_mem150.jsonl)
+    // per 20 M reads in the round-4 footprint sweep)
     // LDS: bucket heads + free slots + page table per lane, the page bitmap per workgroup
     const uint32_t LG = 13, P0 = c->gap_cap1;
     const int max_pages = (int)std::min<uint32_t>(7, (65536u - P0) >> LG);
@@ -1811,7 +1811,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       // shared by 8x fewer concurrent waves each round (the pool is taken page by page, so each of
       // them can grow into the room the others leave): a read whose stack outgrew its share of a
       // busy pool is still resolved cooperatively, instead of by the sequential wide kernel (at
-      // coop_pool_gb=10, 150 bp reads at 2 %: minutes, r04_sweep_mem150)
+      // coop_pool_gb=10, 150 bp reads at 2 %: minutes; now 1.07x the 16 GiB time, r05_sweep_mem150.jsonl)
       const int full_blocks = c->n_cus * c->coop_waves_per_cu;
       const int blocks = (int)std::min<int64_t>(std::max(1, full_blocks >> (3 * round)), lanes);
       const uint32_t freecap = 4096, hcap = 4096;
