@@ -385,16 +385,29 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   // IBWA_ARENA_GB: its size per GPU (0: none); default: the free memory less a margin, at most
   // kArenaMaxGb.
   const int n_used = std::min(n_gpus, n_dev);
+  const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
+  const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
+  // 2 GiB per GPU (~8 M reads of 100 bp): fewer, larger groups than 1 GiB pieces (align phase 6.21
+  // -> 5.96 s at 50 M reads, profiles/r05_e2e_b.json); 3 GiB pieces need ~274 GB at 2 lanes
+  const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
   {
-    // the default arena follows the inputs: the index structures (bit planes, relaid-out BWT, K-mer
-    // tables: ~17x the two .bwt files at GRCh37 size), the ingest slots and the lanes' search scratch
-    // (both grow with the reads a group holds: ~16x the FASTQ bytes at 100 bp, capped at kArenaMaxGb)
+    // The default arena follows the inputs, from what round 5 measured of the engine's buffers
+    // (profiles/r05_e2e_b.json, r05_bench_v1.json extra.e2e, r05_pipe_full_v1.json; 221.6 GB for
+    // 100 bp reads in 2 GiB pieces, 170.7 GB in 1 GiB pieces, 174.5 GB for 150 bp in 2 GiB pieces,
+    // all at 2 lanes): the index structures (bit planes, relaid-out BWT, K-mer tables: ~17x the two
+    // .bwt files at GRCh37 size), per lane ~46 GB of search pools (smaller for a small batch) plus
+    // ~18x the FASTQ bytes a group holds, and per ingest slot ~2.5x the piece.  At most kArenaMaxGb.
     auto fbytes = [](const std::string &f) -> double {
       struct stat st;
       return stat(f.c_str(), &st) == 0 ? (double)st.st_size : 0.0;
     };
-    const double need_gb = (24.0 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) +
-                            16.0 * (fq_path ? fbytes(fq_path) : 0.0)) / (1u << 30) + 2.0;
+    const double GiB = (double)(1u << 30);
+    const bool gz = fq_path && !FastqGpu::usable(fq_path) && strcmp(fq_path, "-") != 0;
+    // FASTQ bytes of one GPU's group: a piece of the file, or (host readers) up to kGroup batches
+    const double fq = fq_path ? fbytes(fq_path) * (gz ? 4.0 : 1.0) : 0.0;
+    const double grp = std::min(fq / n_gpus, fq_dev ? (double)piece : (double)kGroup * kSub * 300.0) / GiB;
+    const double need_gb = 24.0 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
+                           n_lanes * (std::min(46.0, 92.0 * grp) + 18.0 * grp) + (n_lanes + 3) * 2.5 * grp + 2.0;
     const char *ag = getenv("IBWA_ARENA_GB");
     std::vector<std::thread> th;
     std::vector<int> rc(n_used, 0);
@@ -432,7 +445,6 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       for (auto *x : v) ibwa_ctx_destroy(x);
     }
   } destroy_ing{ing, fg};
-  const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
   if (fq_dev) {
     // one slot per group a lane can hold and the group being launched, and two more parsed ahead:
     // a parse waits for launch boundaries of the searches (their grids hold every CU), so with one
@@ -444,10 +456,6 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         if (ibwa_ctx_create(g % n_dev, &x)) return die("ibwa_ctx_create (ingest)");
         ing.push_back(x);
       }
-    const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
-    // 2 GiB per GPU (~8 M reads of 100 bp): fewer, larger groups than 1 GiB pieces (align phase 6.21
-    // -> 5.96 s at 50 M reads, profiles/r05_e2e_b.json); 3 GiB pieces need ~274 GB at 2 lanes
-    const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
     const uint64_t carry = cm && atoll(cm) > 0 ? (uint64_t)atoll(cm) : (uint64_t)256 << 20;
     fg.reset(new FastqGpu(fq_dev, ing, n_gpus, opt.mode, opt.trim_qual, kSub, piece, carry,
                           [opt](int max_len) { return batch_key(opt, max_len); }));
