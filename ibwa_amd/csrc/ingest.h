@@ -205,6 +205,13 @@ class FastqGpu {
       }
       cv_.notify_all();
     }
+    // every region is parsed (its bytes went to the GPUs with its parse): the pinned buffers are
+    // given back now, while the alignment goes on, instead of at exit (unpinning GBs takes time)
+    if (reader_.joinable()) reader_.join();
+    for (char *&b : buf_) {
+      ibwa_host_free(b);
+      b = nullptr;
+    }
     std::lock_guard<std::mutex> lk(mu_);
     finished_ = true;
     cv_.notify_all();
