@@ -449,11 +449,14 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     // one slot per group a lane can hold and the group being launched, and two more parsed ahead:
     // a parse waits for launch boundaries of the searches (their grids hold every CU), so with one
     // slot ahead the launching thread still waited (6.9 s of waits at 50 M reads, r04_e2e_50m_v2)
+    // (the producer parses one region at a time, so a GPU's slots share one parse scratch: only the
+    // kept reads stay per slot)
     const int n_slots = n_lanes + 3;
     for (int sl = 0; sl < n_slots; ++sl)
       for (int g = 0; g < n_gpus; ++g) {
         ibwa_ctx_t *x = nullptr;
         if (ibwa_ctx_create(g % n_dev, &x)) return die("ibwa_ctx_create (ingest)");
+        if (sl > 0 && ibwa_fq_share_scratch(x, ing[g])) return die("ibwa_fq_share_scratch");
         ing.push_back(x);
       }
     const uint64_t carry = cm && atoll(cm) > 0 ? (uint64_t)atoll(cm) : (uint64_t)256 << 20;

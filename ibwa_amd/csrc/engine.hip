@@ -66,6 +66,7 @@ struct Arena {
   char *base = nullptr;
   size_t size = 0, used = 0, peak = 0;
   std::map<size_t, size_t> free_;  // offset -> bytes
+  const bool trace = getenv("IBWA_ARENA_TRACE") != nullptr;  // every carve and release, on stderr
   void *alloc(size_t n) {
     n = (n + 4095) & ~(size_t)4095;
     std::lock_guard<std::mutex> lk(mu);
@@ -76,6 +77,7 @@ struct Arena {
       if (rest) free_[off + n] = rest;
       used += n;
       peak = std::max(peak, used);
+      if (trace) fprintf(stderr, "[ibwa_amd arena] +%.3f GB at %.3f GB: used %.3f GB\n", n / 1e9, off / 1e9, used / 1e9);
       return base + off;
     }
     return nullptr;
@@ -88,6 +90,7 @@ struct Arena {
     std::lock_guard<std::mutex> lk(mu);
     size_t off = (size_t)(static_cast<char *>(p) - base);
     used -= n;
+    if (trace) fprintf(stderr, "[ibwa_amd arena] -%.3f GB at %.3f GB: used %.3f GB\n", n / 1e9, off / 1e9, used / 1e9);
     auto nx = free_.lower_bound(off);
     if (nx != free_.end() && off + n == nx->first) {  // merge with the next free range
       n += nx->second;
@@ -169,6 +172,22 @@ struct DBuf {
     return b;
   }
   template <class T> T *as() const { return (T *)p; }
+};
+
+// A FASTQ parse's device scratch (ibwa_fq_parse): the raw block, its line table, per-record lengths
+// and scan keys.  Only the kept reads' codes, offsets and lengths outlive a parse, so the ingest
+// contexts of one device that never parse at the same time share one scratch (ibwa_fq_share_scratch).
+struct FqScratch {
+  int refs = 1;
+  const void *last = nullptr;  // the context whose block the line table holds (ibwa_fq_offset)
+  DBuf raw, tile, nl, cnt, len, L, key, tmp;
+  uint32_t *hinit = nullptr;  // pinned: the parse counters' initial values, then zeros for the padding
+  void unref() {
+    if (--refs > 0) return;
+    for (DBuf *b : {&raw, &tile, &nl, &cnt, &len, &L, &key, &tmp}) b->release();
+    if (hinit) (void)hipHostFree(hinit);
+    delete this;
+  }
 };
 
 }  // namespace
@@ -313,10 +332,10 @@ struct ibwa_ctx {
   int n_borrowers = 0;
   bool destroy_pending = false;  // destroyed while borrowed: freed with its last borrower
   // FASTQ ingest (fastq.hip, ibwa_fq_parse): the last parsed block and its kept reads
-  DBuf fq_raw, fq_tile, fq_nl, fq_cnt, fq_len, fq_L, fq_key, fq_codes, fq_offk, fq_lenk, fq_tmp;
+  DBuf fq_codes, fq_offk, fq_lenk;  // the last parsed block's kept reads (ibwa_batch_stage_fq's views)
+  FqScratch *fqs = nullptr;          // parse scratch, own or shared (ibwa_fq_share_scratch)
   int64_t fq_kept = 0;
   double fq_ms = 0;  // device time of the last parse (H2D copy + kernels), HIP events
-  uint32_t *fq_hinit = nullptr;  // pinned: the parse counters' initial values, then zeros for the padding
 };
 
 namespace {
@@ -580,15 +599,14 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
                   &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1], &c->c_dir, &c->c_free, &c->c_hits,
                   &c->c_next, &c->c_pool, &c->c_proot, &c->c_pstore, &c->c_recb, &c->c_stg, &c->d_cw, &c->d_feat,
                   &c->d_hpop, &c->d_ordi, &c->d_ordids, &c->d_ordk, &c->d_ordtmp, &c->d_ptabg, &c->d_rdump, &c->d_roff,
-                  &c->d_selst, &c->d_seltmp, &c->d_rdump2, &c->c_wbuf, &c->c_nN, &c->fq_L, &c->fq_cnt, &c->fq_codes, &c->fq_key, &c->fq_len, &c->fq_lenk,
-                  &c->fq_nl, &c->fq_offk, &c->fq_raw, &c->fq_tile, &c->fq_tmp})
+                  &c->d_selst, &c->d_seltmp, &c->d_rdump2, &c->c_wbuf, &c->c_nN, &c->fq_codes, &c->fq_lenk, &c->fq_offk})
     b->release();
+  if (c->fqs) c->fqs->unref();
   for (auto &b : c->sw) b.release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
   for (auto &x : c->ev2)
     if (x) (void)hipEventDestroy(x);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
-  if (c->fq_hinit) (void)hipHostFree(c->fq_hinit);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1015,53 +1033,57 @@ int ibwa_fq_parse(ibwa_ctx_t *c, const void *raw, uint64_t nbytes, int mode, int
   // simply ends earlier (the caller parses on from *consumed)
   const uint64_t cap_lines = std::min<uint64_t>(nbytes / 12 + 64, 0xFFFFFF00ull);
   const uint64_t max_rec = cap_lines / 4 + 1, n_tiles = padded / 16384;
-  if (int rc = c->fq_raw.ensure(padded)) return rc;
-  if (int rc = c->fq_tile.ensure(n_tiles * 8 + 8)) return rc;
-  if (int rc = c->fq_nl.ensure(cap_lines * 4)) return rc;
-  if (int rc = c->fq_cnt.ensure(16)) return rc;
-  if (int rc = c->fq_len.ensure(max_rec * 4)) return rc;
-  if (int rc = c->fq_L.ensure(max_rec * 4)) return rc;
-  if (int rc = c->fq_key.ensure(max_rec * 8)) return rc;
-  if (int rc = c->fq_codes.ensure(nbytes + 16)) return rc;
+  if (!c->fqs) c->fqs = new FqScratch();
+  FqScratch &S = *c->fqs;
+  S.last = nullptr;
+  if (int rc = S.raw.ensure(padded)) return rc;
+  if (int rc = S.tile.ensure(n_tiles * 8 + 8)) return rc;
+  if (int rc = S.nl.ensure(cap_lines * 4)) return rc;
+  if (int rc = S.cnt.ensure(16)) return rc;
+  if (int rc = S.len.ensure(max_rec * 4)) return rc;
+  if (int rc = S.L.ensure(max_rec * 4)) return rc;
+  if (int rc = S.key.ensure(max_rec * 8)) return rc;
+  // the kept reads' codes: at most half the block (a strict record of L bases takes 2 L + 4 bytes)
+  if (int rc = c->fq_codes.ensure(nbytes / 2 + 16)) return rc;
   if (int rc = c->fq_offk.ensure(max_rec * 8)) return rc;
   if (int rc = c->fq_lenk.ensure(max_rec * 4)) return rc;
   FqBufs B;
-  B.raw = c->fq_raw.as<uint8_t>();
-  B.tile_cnt = c->fq_tile.as<uint32_t>();
+  B.raw = S.raw.as<uint8_t>();
+  B.tile_cnt = S.tile.as<uint32_t>();
   B.tile_base = B.tile_cnt + n_tiles;
-  B.nl = c->fq_nl.as<uint32_t>();
+  B.nl = S.nl.as<uint32_t>();
   B.cap_lines = (uint32_t)cap_lines;
-  B.n_lines = c->fq_cnt.as<uint32_t>();
+  B.n_lines = S.cnt.as<uint32_t>();
   B.bad = B.n_lines + 1;
-  B.rec_len = c->fq_len.as<int32_t>();
-  B.rec_L = c->fq_L.as<uint32_t>();
-  B.rec_key = c->fq_key.as<uint64_t>();
+  B.rec_len = S.len.as<int32_t>();
+  B.rec_L = S.L.as<uint32_t>();
+  B.rec_key = S.key.as<uint64_t>();
   B.codes = c->fq_codes.as<uint8_t>();
   B.offk = c->fq_offk.as<uint64_t>();
   B.lenk = c->fq_lenk.as<uint32_t>();
   const FqOpt o{(int)((unsigned)mode >> 24), trim_qual, (mode & IBWA_MODE_IL13) ? 1 : 0};
   size_t tb = 0;
   HIPCHK(fq_parse_launch(B, nbytes, o, nullptr, &tb, c->stream));
-  if (int rc = c->fq_tmp.ensure(tb + 256)) return rc;
+  if (int rc = S.tmp.ensure(tb + 256)) return rc;
   HIPCHK(hipEventRecord(c->ev[6], c->stream));
   // the padding and the counters' initial values come from pinned host memory (copy engine), not
   // from memsets (kernels)
-  if (!c->fq_hinit) {
+  if (!S.hinit) {
     void *h = nullptr;
     HIPCHK(hipHostMalloc(&h, 8 + 2 * FQ_PAD_MAX, 0));
     memset(h, 0, 8 + 2 * FQ_PAD_MAX);
     static_cast<uint32_t *>(h)[1] = 0xFFFFFFFFu;
-    c->fq_hinit = static_cast<uint32_t *>(h);
+    S.hinit = static_cast<uint32_t *>(h);
   }
-  HIPCHK(hipMemcpyAsync(c->fq_raw.p, raw, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(S.raw.p, raw, nbytes, hipMemcpyHostToDevice, c->stream));
   if (padded - nbytes <= 2 * FQ_PAD_MAX)
-    HIPCHK(hipMemcpyAsync(c->fq_raw.as<uint8_t>() + nbytes, c->fq_hinit + 2, padded - nbytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(S.raw.as<uint8_t>() + nbytes, S.hinit + 2, padded - nbytes, hipMemcpyHostToDevice, c->stream));
   else
-    HIPCHK(hipMemsetAsync(c->fq_raw.as<uint8_t>() + nbytes, 0, padded - nbytes, c->stream));
-  HIPCHK(fq_parse_launch(B, nbytes, o, c->fq_tmp.p, &tb, c->stream, c->fq_hinit));
+    HIPCHK(hipMemsetAsync(S.raw.as<uint8_t>() + nbytes, 0, padded - nbytes, c->stream));
+  HIPCHK(fq_parse_launch(B, nbytes, o, S.tmp.p, &tb, c->stream, S.hinit));
   HIPCHK(hipEventRecord(c->ev[7], c->stream));
   uint32_t cnt[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(cnt, c->fq_cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(cnt, S.cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
@@ -1075,16 +1097,34 @@ int ibwa_fq_parse(ibwa_ctx_t *c, const void *raw, uint64_t nbytes, int mode, int
   }
   if (n == 0) return 0;
   uint32_t last_nl = 0;
-  HIPCHK(hipMemcpy(&last_nl, c->fq_nl.as<uint32_t>() + 4 * n - 1, 4, hipMemcpyDeviceToHost));
-  if (rec_len) HIPCHK(hipMemcpy(rec_len, c->fq_len.p, n * 4, hipMemcpyDeviceToHost));
-  if (rec_L) HIPCHK(hipMemcpy(rec_L, c->fq_L.p, n * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&last_nl, S.nl.as<uint32_t>() + 4 * n - 1, 4, hipMemcpyDeviceToHost));
+  if (rec_len) HIPCHK(hipMemcpy(rec_len, S.len.p, n * 4, hipMemcpyDeviceToHost));
+  if (rec_L) HIPCHK(hipMemcpy(rec_L, S.L.p, n * 4, hipMemcpyDeviceToHost));
   uint64_t key = 0;
   int32_t ll = 0;
-  HIPCHK(hipMemcpy(&key, c->fq_key.as<uint64_t>() + n - 1, 8, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(&ll, c->fq_len.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&key, S.key.as<uint64_t>() + n - 1, 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&ll, S.len.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost));
   c->fq_kept = (int64_t)(key >> 32) + (ll >= 0 ? 1 : 0);
+  S.last = c;
   *n_rec = (int64_t)n;
   *consumed = (uint64_t)last_nl + 1;
+  return 0;
+}
+
+int ibwa_fq_share_scratch(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
+  if (!dst || !src || dst == src) return fail(IBWA_EINVAL, "fq_share_scratch: bad arguments");
+  if (dst->device != src->device)
+    return fail(IBWA_EINVAL, "fq_share_scratch: contexts on devices %d and %d", dst->device, src->device);
+  ibwa_ctx *s = const_cast<ibwa_ctx *>(src);
+  HIPCHK(enter(s));
+  if (!s->fqs) s->fqs = new FqScratch();
+  if (dst->fqs == s->fqs) return 0;
+  if (dst->fqs) {
+    HIPCHK(enter(dst));
+    dst->fqs->unref();
+  }
+  dst->fqs = s->fqs;
+  ++dst->fqs->refs;
   return 0;
 }
 
@@ -1093,8 +1133,10 @@ int ibwa_fq_offset(const ibwa_ctx_t *c, int64_t r, uint64_t *off) {
   *off = 0;
   if (r == 0) return 0;
   HIPCHK(enter(c));
+  if (!c->fqs || !c->fqs->nl.p || c->fqs->last != c)
+    return fail(IBWA_EINVAL, "fq_offset: this context's block is not the last one parsed in its scratch");
   uint32_t x = 0;
-  HIPCHK(hipMemcpy(&x, c->fq_nl.as<uint32_t>() + 4 * r - 1, 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&x, c->fqs->nl.as<uint32_t>() + 4 * r - 1, 4, hipMemcpyDeviceToHost));
   *off = (uint64_t)x + 1;
   return 0;
 }

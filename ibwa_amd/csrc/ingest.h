@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -77,6 +78,16 @@ class FastqGpu {
     fd_ = open(fn, O_RDONLY);
     struct stat st;
     fsize_ = fd_ >= 0 && fstat(fd_, &st) == 0 ? (uint64_t)st.st_size : 0;
+    // The file is mapped (IBWA_FQ_MMAP, default 1) and each region handed to the parse where it lies:
+    // no pinned buffers (pinning 4.5 GB took ~1 s and unpinning it ~0.5 s at exit -- or, freed while
+    // the searches ran, slowed them: profiles/r05_exit.jsonl, r05_e2e_d.json), no carry copies (a
+    // region's unfinished batch is simply where the next region starts).  A reader thread faults the
+    // next region's pages in while the current one is parsed.
+    const char *mv = getenv("IBWA_FQ_MMAP");
+    if (fd_ >= 0 && fsize_ > 0 && !(mv && !strcmp(mv, "0"))) {
+      void *m = mmap(nullptr, fsize_, PROT_READ, MAP_PRIVATE, fd_, 0);
+      if (m != MAP_FAILED) map_ = static_cast<const char *>(m);
+    }
     // pinned buffers no larger than the file needs (a small input must not pin GBs)
     const uint64_t fs = std::max<uint64_t>((fsize_ + 4095) / 4096 * 4096, 4096);
     piece_ = std::max<uint64_t>(piece_bytes, 4096);
@@ -86,6 +97,7 @@ class FastqGpu {
     const uint64_t per = piece_ * G_, n_reg = (fs + per - 1) / per;
     chunk_ = std::min<uint64_t>(per, ((fs + n_reg - 1) / n_reg + 4095) / 4096 * 4096);
     for (auto &b : buf_) {
+      if (map_) break;
       void *p = nullptr;
       if (ibwa_host_alloc(carry_ + chunk_ + 64, &p)) { ok_ = false; return; }
       b = static_cast<char *>(p);
@@ -104,6 +116,7 @@ class FastqGpu {
     if (producer_.joinable()) producer_.join();
     if (reader_.joinable()) reader_.join();
     for (char *b : buf_) ibwa_host_free(b);
+    if (map_) munmap(const_cast<char *>(map_), fsize_);
     if (fd_ >= 0) close(fd_);
   }
   bool ok() const { return ok_; }
@@ -149,7 +162,8 @@ class FastqGpu {
   bool stop_ = false, finished_ = false;
   int fd_ = -1;
   uint64_t fsize_ = 0, piece_ = 0, carry_ = 0, chunk_ = 0;
-  char *buf_[2] = {nullptr, nullptr};
+  char *buf_[2] = {nullptr, nullptr};  // pinned region buffers (IBWA_FQ_MMAP=0)
+  const char *map_ = nullptr;         // the mapped file
   bool ok_ = false, handoff_ = false;
   uint64_t handoff_off_ = 0;
   int cur_ = 0;                 // buffer of the region being parsed
@@ -205,22 +219,34 @@ class FastqGpu {
       }
       cv_.notify_all();
     }
-    // every region is parsed (its bytes went to the GPUs with its parse): the pinned buffers are
-    // given back now, while the alignment goes on, instead of at exit (unpinning GBs takes time)
-    if (reader_.joinable()) reader_.join();
-    for (char *&b : buf_) {
-      ibwa_host_free(b);
-      b = nullptr;
-    }
     std::lock_guard<std::mutex> lk(mu_);
     finished_ = true;
     cv_.notify_all();
   }
 
-  // chunk at file offset next_off_ into buf_[b] + carry_, by several threads
+  // chunk at file offset next_off_ into buf_[b] + carry_ (mapped file: its pages faulted in), by
+  // several threads
   void start_read(int b) {
     const uint64_t off = next_off_, want = off < fsize_ ? std::min<uint64_t>(chunk_, fsize_ - off) : 0;
     next_off_ = off + want;
+    if (map_) {
+      got_[b] = want;
+      reader_ = std::thread([this, off, want]() {
+        const uint64_t pg = 4096, lo = off / pg * pg, hi = std::min<uint64_t>(fsize_, (off + want + pg - 1) / pg * pg);
+        const int nt = std::max(1, std::min<int>(ibwa_sam::host_threads(), (int)((hi - lo) >> 26) + 1));
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t)
+          th.emplace_back([&, t]() {
+            const uint64_t a = lo + (hi - lo) * t / nt / pg * pg, e = t + 1 == nt ? hi : lo + (hi - lo) * (t + 1) / nt / pg * pg;
+            if (e <= a) return;
+            if (madvise(const_cast<char *>(map_) + a, e - a, 22 /* MADV_POPULATE_READ */) == 0) return;
+            volatile char sink = 0;  // older kernels: touch one byte per page
+            for (uint64_t q = a; q < e; q += pg) sink = sink + map_[q];
+          });
+        for (auto &x : th) x.join();
+      });
+      return;
+    }
     char *dst = buf_[b] + carry_;
     reader_ = std::thread([this, b, off, want, dst]() {
       const int nt = std::max(1, std::min<int>(ibwa_sam::host_threads(), (int)(want >> 24) + 1));
@@ -256,7 +282,7 @@ class FastqGpu {
     reader_.join();
     const uint64_t got = got_[cur_];
     const bool eof = next_off_ >= fsize_;
-    char *const base = buf_[cur_] + carry_ - tail_;
+    const char *const base = map_ ? map_ + tail_file_off_ : buf_[cur_] + carry_ - tail_;
     const uint64_t n = tail_ + got;
     // the next chunk is read into the other buffer, behind its carry room, while this region is
     // parsed and aligned (that buffer's previous region went to the GPUs with its parse)
@@ -420,9 +446,15 @@ class FastqGpu {
       handoff_off_ = file_rewind;
       return HANDOFF;
     }
-    // the next region: the carried bytes in front of the next chunk, read meanwhile
+    // the next region: the carried bytes in front of the next chunk, read meanwhile (mapped file:
+    // already there; the page tables of what this region consumed are dropped)
     const int nb = cur_ ^ 1;
-    memcpy(buf_[nb] + carry_ - carry, base + rewind, carry);
+    if (map_) {
+      const uint64_t pg = 4096, a = tail_file_off_ / pg * pg, e = file_rewind / pg * pg;
+      if (e > a) madvise(const_cast<char *>(map_) + a, e - a, MADV_DONTNEED);
+    } else {
+      memcpy(buf_[nb] + carry_ - carry, base + rewind, carry);
+    }
     tail_ = carry;
     tail_file_off_ = file_rewind;
     cur_ = nb;

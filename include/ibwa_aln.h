@@ -144,8 +144,13 @@ int ibwa_batch_stage(ibwa_ctx_t *ctx, int64_t n_seqs, const uint8_t *seq, const 
  */
 int ibwa_fq_parse(ibwa_ctx_t *ctx, const void *raw, uint64_t nbytes, int mode, int trim_qual, int64_t *n_rec,
                   uint64_t *consumed, int *not_strict, int32_t *rec_len, uint32_t *rec_L, int64_t cap);
-/* byte offset (in the block) of record r of the last ibwa_fq_parse (r <= its n_rec) */
+/* byte offset (in the block) of record r of the last ibwa_fq_parse (r <= its n_rec); IBWA_EINVAL once
+ * another context sharing the parse scratch has parsed since */
 int ibwa_fq_offset(const ibwa_ctx_t *ctx, int64_t r, uint64_t *off);
+/* dst's parses use src's parse scratch (the raw block, line table, per-record arrays: ~1.7x the
+ * block; same device).  Only the kept reads (~0.75x the block) stay per context.  The contexts'
+ * ibwa_fq_parse calls must not overlap (each returns with its device work done). */
+int ibwa_fq_share_scratch(ibwa_ctx_t *dst, const ibwa_ctx_t *src);
 /* kept reads and device time (H2D copy + kernels, ms) of the last ibwa_fq_parse */
 int ibwa_fq_stats(const ibwa_ctx_t *ctx, int64_t *kept, double *ms);
 /* ibwa_batch_stage from src's last parsed block (same device): its kept reads [first, first + n),

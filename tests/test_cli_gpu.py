@@ -184,9 +184,12 @@ def test_cli_gpu_parse_equals_host(golden_dir, argv, shape, tmp_path):
     host = run_cli_env(argv, golden_dir, str(fq), tmp_path, dict(env, IBWA_ALN_GPU_PARSE="0"), "host.sai")
     ser = run_cli_env(argv, golden_dir, str(fq), tmp_path, dict(env, IBWA_ALN_SERIAL_READ="1"), "ser.sai")
     assert len(host) > 64 and host[64:] == ser[64:]
-    for extra, piece in (([], "1000000000"), ([], "40000"), (["-G", "2"], "30000")):
-        dev = run_cli_env(argv + extra, golden_dir, str(fq), tmp_path, dict(env, IBWA_FQ_PIECE_BYTES=piece), "dev.sai")
-        assert dev[64:] == host[64:], (extra, piece)
+    # IBWA_FQ_MMAP: regions parsed where the mapped file holds them (default) or read into pinned buffers
+    for extra, piece, mm in (([], "1000000000", "1"), ([], "40000", "1"), ([], "40000", "0"), (["-G", "2"], "30000", "1"),
+                             (["-G", "2"], "30000", "0")):
+        dev = run_cli_env(argv + extra, golden_dir, str(fq), tmp_path,
+                          dict(env, IBWA_FQ_PIECE_BYTES=piece, IBWA_FQ_MMAP=mm), "dev.sai")
+        assert dev[64:] == host[64:], (extra, piece, mm)
 
 
 def test_cli_gpu_parse_carry_overflow(golden_dir, sai_manifest, tmp_path):
@@ -194,9 +197,11 @@ def test_cli_gpu_parse_carry_overflow(golden_dir, sai_manifest, tmp_path):
     still the reference's."""
     m = sai_manifest["r100.default"]
     gold = open(os.path.join(golden_dir, "r100.default.sai"), "rb").read()
-    got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path,
-                      {"IBWA_ALN_SUBBATCH": "500", "IBWA_FQ_PIECE_BYTES": "20000", "IBWA_FQ_CARRY_BYTES": "4096"}, "c.sai")
-    assert oracle.sai_body_equal(got, gold)
+    for mm in ("1", "0"):
+        got = run_cli_env(m["argv"], golden_dir, m["reads"], tmp_path,
+                          {"IBWA_ALN_SUBBATCH": "500", "IBWA_FQ_PIECE_BYTES": "20000", "IBWA_FQ_CARRY_BYTES": "4096",
+                           "IBWA_FQ_MMAP": mm}, "c.sai")
+        assert oracle.sai_body_equal(got, gold), mm
 
 
 def test_cli_gpu_parse_more_than_2_24_records(golden_dir, tmp_path):

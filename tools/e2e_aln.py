@@ -78,12 +78,15 @@ def write_fastq(path, reads, first=0, count=None):
             f.write(buf.tobytes())
 
 
-def run(argv, timeout=1800, env=None):
+def run(argv, timeout=1800, env=None, save_stderr=None):
     t = time.perf_counter()
     r = subprocess.run(argv, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout,
                        env=dict(os.environ, IBWA_ALN_TIMES="1", **(env or {})))
     dt = time.perf_counter() - t
     err = r.stderr.decode(errors="replace")
+    if save_stderr:
+        with open(save_stderr, "w") as f:
+            f.write(err)
     if r.returncode != 0:
         raise RuntimeError(f"{argv[:2]} failed ({r.returncode}): {err[-1500:]}")
     phases = {}
@@ -156,6 +159,9 @@ def main():
     ap.add_argument("--host-parse-run", type=int, default=1, help="also align with the host parse and compare the .sai")
     ap.add_argument("--variants", default="", help="JSON list of {name: {ENV: value}}: extra aln runs of the same FASTQ "
                                                    "with these environment settings (.sai compared with the first run)")
+    ap.add_argument("--prof", default="", help="directory: one more aln run of the FASTQ under rocprofv3 --kernel-trace "
+                                               "--stats (the GPU's busy time inside the align phase)")
+    ap.add_argument("--arena-trace", default="", help="file: one more aln run with IBWA_ARENA_TRACE=1, its stderr")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
@@ -226,6 +232,23 @@ def main():
                     os.unlink(vsai)
                     c["runs"].append(r_)
             c["parse_only"] = parse
+            if a.arena_trace:
+                tsai = os.path.join(tmp, f"c{cid}_t.sai")
+                wall, ph = run([CLI, "aln"] + opts + ["-f", tsai, P, fq], env={"IBWA_ARENA_TRACE": "1"},
+                               save_stderr=a.arena_trace)
+                c["arena_trace_run"] = {"wall_s": wall, "phases_s": ph, "file": a.arena_trace}
+                os.unlink(tsai)
+            if a.prof:
+                psai = os.path.join(tmp, f"c{cid}_p.sai")
+                # a clean exit: the profiler writes its trace from exit handlers, which the CLI's fast
+                # _exit skips
+                wall, ph = run(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", a.prof,
+                                "-o", f"c{cid}_aln", "--", CLI, "aln"] + opts + ["-f", psai, P, fq],
+                               env={"IBWA_ALN_CLEAN_EXIT": "1"})
+                c["prof_run"] = {"wall_s": wall, "phases_s": ph, "dir": a.prof,
+                                 "sai_equal_first_run": open(psai, "rb").read() == open(sai, "rb").read()}
+                log(f"{name}: profiled aln run: {wall:.1f} s wall, phases {ph}")
+                os.unlink(psai)
             if a.host_parse_run:
                 hsai = os.path.join(tmp, f"c{cid}_h.sai")
                 wall, ph = run([CLI, "aln"] + opts + ["-f", hsai, P, fq], env={"IBWA_ALN_GPU_PARSE": "0"})
