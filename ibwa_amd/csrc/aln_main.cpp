@@ -467,9 +467,28 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       return 1;
     }
   }
+  // IBWA_CTX_OPTS="key=value,...": engine options (ibwa_ctx_set_option) for every aligning context --
+  // measurement and tuning (e.g. kmer_k=14,coop_pool_gb=10)
+  auto ctx_opts = [](ibwa_ctx_t *x) -> int {
+    const char *e = getenv("IBWA_CTX_OPTS");
+    if (!e) return 0;
+    std::string all(e);
+    size_t p = 0;
+    while (p < all.size()) {
+      const size_t q = std::min(all.find(',', p), all.size());
+      const std::string kv = all.substr(p, q - p);
+      const size_t eq = kv.find('=');
+      if (eq != std::string::npos && ibwa_ctx_set_option(x, kv.substr(0, eq).c_str(), atol(kv.c_str() + eq + 1))) {
+        fprintf(stderr, "[ibwa-amd aln] IBWA_CTX_OPTS: %s: %s\n", kv.c_str(), ibwa_last_error());
+        return 1;
+      }
+      p = q + 1;
+    }
+    return 0;
+  };
   std::vector<ibwa_ctx_t *> ctx(n_gpus, nullptr);
   for (int g = 0; g < n_gpus; ++g) {
-    if (ibwa_ctx_create(g % n_dev, &ctx[g])) return die("ibwa_ctx_create");
+    if (ibwa_ctx_create(g % n_dev, &ctx[g]) || ctx_opts(ctx[g])) return die("ibwa_ctx_create");
     if (g == 0) {
       if (ibwa_ctx_load_bwt_file(ctx[0], 0, (prefix + ".bwt").c_str())) return die("load .bwt");
       if (ibwa_ctx_load_bwt_file(ctx[0], 1, (prefix + ".rbwt").c_str())) return die("load .rbwt");
@@ -535,7 +554,8 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   for (int l = 1; l < n_lanes; ++l)
     for (int g = 0; g < n_gpus; ++g) {
       ibwa_ctx_t *x = nullptr;
-      if (ibwa_ctx_create(g % n_dev, &x) || ibwa_ctx_share_index(x, ctx[g])) return die("a second context on the GPU");
+      if (ibwa_ctx_create(g % n_dev, &x) || ctx_opts(x) || ibwa_ctx_share_index(x, ctx[g]))
+        return die("a second context on the GPU");
       lctx[l].push_back(x);
     }
   struct Job {
