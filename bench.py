@@ -467,6 +467,9 @@ def e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns):
                 out["gpu_parse"] = {"records": int(m_.group(1)), "producer_s": float(m_.group(2)),
                                     "device_ms": int(m_.group(3)),
                                     "records_per_s": int(m_.group(1)) / max(float(m_.group(2)), 1e-3)}
+            m_ = re.search(r"exiting at ([\d.]+) s", ln)
+            if m_:  # the process's own clock at its end (the rest of the wall is start-up and exit)
+                out["process_clock_at_exit_s"] = float(m_.group(1))
             m_ = re.search(r"arena on GPU 0: ([\d.]+) GB, peak use ([\d.]+) GB", ln)
             if m_:
                 out["arena_gb"], out["arena_peak_use_gb"] = float(m_.group(1)), float(m_.group(2))

@@ -650,20 +650,46 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       return 1;
     }
     writer = std::thread([out, &write_failed, naln = std::move(J.naln), aln = std::move(J.aln)]() {
+      // per slice: the records serialised by up to 8 threads (each a contiguous range of reads, at
+      // its byte offset), then one write -- the last group's write is on the wall clock
       for (size_t g = 0; g < naln.size(); ++g) {
-        const ibwa_aln1_t *p = aln[g];
-        size_t bytes = 0;
-        for (int32_t k : naln[g]) bytes += 4 + (size_t)k * sizeof(ibwa_aln1_t);
-        std::vector<char> buf(bytes);
-        char *w = buf.data();
-        for (int32_t k : naln[g]) {
-          memcpy(w, &k, 4);
-          w += 4;
-          if (k) memcpy(w, p, (size_t)k * sizeof(ibwa_aln1_t));
-          w += (size_t)k * sizeof(ibwa_aln1_t);
-          p += k;
+        const std::vector<int32_t> &na = naln[g];
+        const int64_t n = (int64_t)na.size();
+        const int T = (int)std::max<int64_t>(1, std::min<int64_t>(8, n >> 16));
+        std::vector<size_t> bo(T + 1, 0), ho(T + 1, 0);  // per range: its first byte / first hit
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+          th.emplace_back([&, t]() {
+            size_t b = 0, h = 0;
+            for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
+              b += 4 + (size_t)na[r] * sizeof(ibwa_aln1_t);
+              h += (size_t)na[r];
+            }
+            bo[t + 1] = b;
+            ho[t + 1] = h;
+          });
+        for (auto &x : th) x.join();
+        th.clear();
+        for (int t = 0; t < T; ++t) {
+          bo[t + 1] += bo[t];
+          ho[t + 1] += ho[t];
         }
-        if (bytes && fwrite(buf.data(), 1, bytes, out) != bytes) write_failed = true;
+        std::unique_ptr<char[]> buf(new char[std::max<size_t>(bo[T], 1)]);  // not zero-filled: every byte is written
+        for (int t = 0; t < T; ++t)
+          th.emplace_back([&, t]() {
+            char *w = buf.get() + bo[t];
+            const ibwa_aln1_t *p = aln[g] + ho[t];
+            for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
+              const int32_t k = na[r];
+              memcpy(w, &k, 4);
+              w += 4;
+              if (k) memcpy(w, p, (size_t)k * sizeof(ibwa_aln1_t));
+              w += (size_t)k * sizeof(ibwa_aln1_t);
+              p += k;
+            }
+          });
+        for (auto &x : th) x.join();
+        if (bo[T] && fwrite(buf.get(), 1, bo[T], out) != bo[T]) write_failed = true;
         ibwa_free(aln[g]);
       }
     });
@@ -732,6 +758,9 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   // contexts, the ingest slots and the pinned buffers one by one only hands back what the driver and
   // the OS reclaim at exit anyway (IBWA_ALN_CLEAN_EXIT=1 does it, for leak checkers).
   if (env_int("IBWA_ALN_CLEAN_EXIT", 0) == 0) {
+    if (kTimes)  // the process's own clock at its end: the rest of a timed wall is start-up and exit
+      fprintf(stderr, "[ibwa-amd aln] exiting at %.3f s\n",
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - g_proc_t0).count());
     fflush(stdout);
     fflush(stderr);
     _exit(have < 0 ? 1 : 0);

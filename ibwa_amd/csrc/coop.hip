@@ -1506,9 +1506,9 @@ __global__ void __launch_bounds__(64) k_coop_roots(CoopArgs A, unsigned long lon
 
 hipError_t launch_coop_roots(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st) {
   if (g.n <= 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  hipError_t e = zero_async(d_counter, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(g.pstore_next, 0, sizeof(unsigned long long), st);
+  e = zero_async(g.pstore_next, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_coop_roots, dim3(blocks), dim3(64), 0, st, g, d_counter);
   return hipGetLastError();
@@ -1518,9 +1518,9 @@ hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blo
   if (g.n <= 0) return hipSuccess;
   for (int c = 0; c < 5; ++c)  // the kernel takes L2 from ix[0] for both strands
     if (g.ix[0].L2[c] != g.ix[1].L2[c]) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  hipError_t e = zero_async(d_counter, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(g.pool_next, 0, sizeof(uint32_t), st);
+  e = zero_async(g.pool_next, sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   if (g.prof) hipLaunchKernelGGL(k_coop<true>, dim3(blocks), dim3(64), 0, st, g, d_counter);
   else hipLaunchKernelGGL(k_coop<false>, dim3(blocks), dim3(64), 0, st, g, d_counter);

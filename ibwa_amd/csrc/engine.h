@@ -278,6 +278,9 @@ hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1
                         int blocks, hipEvent_t ev_mid, const uint32_t *const jump[6], hipStream_t st);
 uint64_t occ64_blocks(uint32_t seq_len);
 hipError_t build_occ64(const IndexView &ix, uint4 *out, hipStream_t st);
+// bytes of zeros to device memory on stream st by the copy engine (from pinned host zeros): a
+// hipMemsetAsync is a kernel, which waits for CUs that another context's persistent grid holds
+hipError_t zero_async(void *p, size_t bytes, hipStream_t st);
 uint32_t exact_record_stride(int max_len);
 hipError_t launch_occ4(const IndexView &ix, int64_t n, const uint32_t *k, uint32_t *cnt, hipStream_t st);
 hipError_t build_strand(const uint8_t *T, uint64_t n, uint4 *out_blocks, uint32_t *primary, uint32_t totals[4],

@@ -110,6 +110,28 @@ thread_local hipStream_t g_stream = nullptr;  // the stream of the context this 
 constexpr int MAX_DEV = 64;
 Arena g_arena[MAX_DEV];
 
+}  // namespace
+
+namespace ibwa {
+hipError_t zero_async(void *p, size_t bytes, hipStream_t st) {
+  constexpr size_t kZ = 64u << 20;
+  static std::once_flag once;
+  static void *zeros = nullptr;
+  std::call_once(once, []() {
+    if (hipHostMalloc(&zeros, kZ, hipHostMallocDefault) != hipSuccess) zeros = nullptr;
+    else memset(zeros, 0, kZ);
+  });
+  if (!zeros) return hipMemsetAsync(p, 0, bytes, st);
+  for (size_t o = 0; o < bytes; o += kZ) {
+    hipError_t e = hipMemcpyAsync(static_cast<char *>(p) + o, zeros, std::min(kZ, bytes - o), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+}  // namespace ibwa
+
+namespace {
+
 Arena *arena_here() {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEV) return nullptr;
@@ -1420,9 +1442,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         if (int rc = c->d_rdump2.ensure(rd_cap * 16)) return rc;
       c->stats.resume_records_cap = (int64_t)rd_cap;
       if (int rc = c->d_roff.ensure(((uint64_t)n + 4) * 8)) return rc;
-      HIPCHK(hipMemsetAsync(c->d_roff.p, 0, ((uint64_t)n + 4) * 8, c->stream));
+      HIPCHK(zero_async(c->d_roff.p, ((uint64_t)n + 4) * 8, c->stream));
       if (int rc = c->d_hpop.ensure(((uint64_t)n + 1) * 4)) return rc;
-      HIPCHK(hipMemsetAsync(c->d_hpop.p, 0, ((uint64_t)n + 1) * 4, c->stream));
+      HIPCHK(zero_async(c->d_hpop.p, ((uint64_t)n + 1) * 4, c->stream));
       resume_states = true;
       c->hpop_valid = true;
     }
@@ -1439,7 +1461,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     if (int rc = c->d_naln.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
     if (int rc = c->d_status.ensure(std::max<int64_t>(n, 1) * 4)) return rc;
     if (int rc = c->d_counter.ensure(64)) return rc;
-    HIPCHK(hipMemsetAsync(c->d_counter.as<unsigned long long>() + 1, 0, 8, c->stream));
+    HIPCHK(zero_async(c->d_counter.as<unsigned long long>() + 1, 8, c->stream));
     // The reads of chunk [b0, b0 + cnt) that left a resume state go through the cooperative pass right
     // after their chunk's first pass, so the state buffer holds one chunk's states at a time: a read
     // it resolves is done (status 0), one it hands on starts over in the passes below.
@@ -1606,7 +1628,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       c->stats.resume_records += (int64_t)used;
       c->stats.resume_records_peak = std::max<int64_t>(c->stats.resume_records_peak, (int64_t)used);
       if (R.cnt >= 65536) c->resume_need = std::max(c->resume_need, (double)used / (double)R.cnt);
-      HIPCHK(hipMemsetAsync(rdn, 0, 8, st));
+      HIPCHK(zero_async(rdn, 8, st));
       HIPCHK(hipEventRecord(evs[3], st));  // the state buffer may be written again
       return 0;
     };
@@ -2162,7 +2184,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
           if (int rc = c->d_iters.ensure(lanes * 4)) return rc;
           G.iters = c->d_iters.as<uint32_t>();
         }
-        HIPCHK(hipMemsetAsync(G.aln_next, 0, 8, c->stream));
+        HIPCHK(zero_async(G.aln_next, 8, c->stream));
         // one heavy read per wave: an iteration then costs only that read's path
         const int blk = 64;
         G.lanes_per_wave = 1;

@@ -349,7 +349,7 @@ hipError_t launch_exact(const AlnArgs &a, const uint4 *o64_0, const uint4 *o64_1
                      rec, stride, K, comp, in_cap);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  e = zero_async(d_counter, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
   if (ev_mid && (e = hipEventRecord(ev_mid, st)) != hipSuccess) return e;  // pack | search boundary
   ExactArgs x;

@@ -1284,7 +1284,7 @@ hipError_t launch_gapped(const GapArgs &g, unsigned long long *d_counter, int bl
   for (int c = 0; c < 5; ++c)  // the kernel takes L2 and seq_len from ix[0] for both strands
     if (g.ix[0].L2[c] != g.ix[1].L2[c]) return hipErrorInvalidValue;
   if (g.ix[0].seq_len != g.ix[1].seq_len) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  hipError_t e = zero_async(d_counter, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
   const bool lw = !wide && g.cw != nullptr;
   const size_t lds = gapped_lds_bytes(g.o.n_stacks, block, wide, g.max_pages, g.pages_per_block, g.lanes_per_wave,

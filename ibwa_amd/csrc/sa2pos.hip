@@ -203,11 +203,11 @@ hipError_t derive_sampled_sa(const IndexView &ix, uint32_t intv, uint32_t *sa_s,
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // sink: node 0
-  e = hipMemsetAsync(nx, 0, 4, st);
-  if (e == hipSuccess) e = hipMemsetAsync(rk, 0, 4, st);
+  e = zero_async(nx, 4, st);
+  if (e == hipSuccess) e = zero_async(rk, 4, st);
   bool done = false;
   for (int round = 0; e == hipSuccess && !done && round < 40; ++round) {
-    e = hipMemsetAsync(active, 0, 4, st);
+    e = zero_async(active, 4, st);
     if (e != hipSuccess) break;
     hipLaunchKernelGGL(k_sa_jump, dim3(g), dim3(256), 0, st, n_nodes, nx, rk, nx2, rk2, active);
     e = hipGetLastError();

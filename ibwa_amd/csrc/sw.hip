@@ -523,7 +523,7 @@ hipError_t launch_pack_cigar(const uint32_t *cig, int cap, const int32_t *n_ciga
 
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), st);
+  hipError_t e = zero_async(d_counter, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_sw, dim3(blocks), dim3(256), 0, st, a, d_counter);
   return hipGetLastError();
