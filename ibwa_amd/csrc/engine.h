@@ -237,6 +237,7 @@ struct SwArgs {
   int stop_after;                 // diagnostics: 1 after the forward pass, 2 after the reverse pass
   int global_band;                // > 0: aln_global_core alone with this band (and gap_end), no local passes
   int gap_end;
+  int4 *st, *st2;                 // per pair, between the passes: (score_f, end_i, end_j, -), (start_i, start_j, score_r, path?)
 };
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st);
 // row p's n_cigar[p] CIGAR words (at cig + p * cap) to out + first[p]
