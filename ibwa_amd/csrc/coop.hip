@@ -1306,6 +1306,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     if (lane == 0) {
       A.n_aln[ro] = na;
       A.status[r] = status;  // per launch read: the host collects the reads to re-run from it
+      if (A.fix_status) {
+        if (status == 0u) A.fix_status[rr] = 0u;
+        else A.fix_roff[rr] = 0u;
+      }
       if (A.iters) A.iters[r] = n_iter;
     }
     __syncthreads();

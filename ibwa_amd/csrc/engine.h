@@ -172,6 +172,10 @@ struct CoopArgs {
   uint64_t pstore_cap;       // pstore capacity (entries)
   const uint4 *rdump;        // first-pass search states (GapArgs::rdump), roff[read] 1 + offset, 0: none
   const uint64_t *roff;
+  // resume_fixup folded in (non-null): as a read ends, fix_status[id] = 0 where it was resolved, else
+  // fix_roff[id] = 0 -- no kernel after the launch that would wait for CUs another grid holds
+  uint32_t *fix_status;
+  uint64_t *fix_roff;
   // >= 0: the widths and N counts are the first pass's own, of read (id - wb_base) of its chunk (right
   // after it: its gap_shadow updates are in them, so a resumed read does not replay them); -1: per
   // launch read (k_width run for this launch)
@@ -237,7 +241,6 @@ struct SwArgs {
   int stop_after;                 // diagnostics: 1 after the forward pass, 2 after the reverse pass
   int global_band;                // > 0: aln_global_core alone with this band (and gap_end), no local passes
   int gap_end;
-  int4 *st, *st2;                 // per pair, between the passes: (score_f, end_i, end_j, -), (start_i, start_j, score_r, path?)
 };
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st);
 // row p's n_cigar[p] CIGAR words (at cig + p * cap) to out + first[p]

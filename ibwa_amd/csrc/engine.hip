@@ -347,7 +347,7 @@ struct ibwa_ctx {
   int kmer_K = 0;   // K of the built tables
   bool kmer_valid = false;
   ibwa_run_stats_t stats = {};
-  DBuf sw[17];  // sw_batch's buffers (kept between calls)
+  DBuf sw[15];  // sw_batch's buffers (kept between calls)
   // ibwa_ctx_share_index: the context whose index structures this one borrows, and how many
   // contexts borrow this one's; neither side may rebuild or replace them while shared
   ibwa_ctx *share_src = nullptr;
@@ -1588,10 +1588,10 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       }
       HIPCHK(hipEventRecord(evs[2], st));
       // its own claim counter: the first pass of the next chunk claims with d_counter[0] meanwhile
+      K.fix_status = c->d_status.as<uint32_t>();  // resume_fixup, as each read ends
+      K.fix_roff = c->d_roff.as<uint64_t>();
       HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>() + (own_widths ? 6 : 0), blocks, st));
       HIPCHK(hipEventRecord(evs[1], st));
-      HIPCHK(resume_fixup(c->r_status.as<uint32_t>(), ids, lanes, c->d_status.as<uint32_t>(), c->d_roff.as<uint64_t>(),
-                          st));
       return 0;
     };
     // Finish part (after the launch's kernels): the reads it resolved, the state buffer's use, and the
@@ -2415,7 +2415,7 @@ int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1,
   // scratch cost more than the kernel on a sampe batch)
   DBuf &s1 = c->sw[0], &s2 = c->sw[1], &o1 = c->sw[2], &o2 = c->sw[3], &l1 = c->sw[4], &l2 = c->sw[5], &sc = c->sw[6],
        &pl = c->sw[7], &nc = c->sw[8], &en = c->sw[9], &cg = c->sw[10], &scr = c->sw[11], &tbb = c->sw[12],
-       &cf = c->sw[13], &cc = c->sw[14], &t1 = c->sw[15], &t2 = c->sw[16];
+       &cf = c->sw[13], &cc = c->sw[14];
   auto release = [&]() {};
   const uint64_t wpl = sw_words_per_lane(max1, max2), tpl = sw_tb_per_lane(max1, max2);
   const uint64_t per_wave = (wpl * 4 + tpl) * 64;
@@ -2428,7 +2428,7 @@ int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1,
       (rc = l1.ensure(n * 4)) || (rc = l2.ensure(n * 4)) || (rc = sc.ensure(n * 4)) || (rc = pl.ensure(n * 4)) ||
       (rc = nc.ensure(n * 4)) || (rc = en.ensure(n * 16)) || (rc = cg.ensure((uint64_t)n * cap * 4)) ||
       (rc = scr.ensure((uint64_t)blocks * 4 * wpl * 4 * 64)) || (rc = tbb.ensure((uint64_t)blocks * 4 * tpl * 64)) ||
-      (rc = c->d_counter.ensure(64)) || (rc = cf.ensure(n * 8)) || (rc = t1.ensure(n * 16)) || (rc = t2.ensure(n * 16))) {
+      (rc = c->d_counter.ensure(64)) || (rc = cf.ensure(n * 8))) {
     release();
     return rc;
   }
@@ -2456,8 +2456,6 @@ int sw_batch(ibwa_ctx_t *c, int64_t n, const uint8_t *ref, const uint64_t *off1,
   A.stop_after = c->sw_stop_after;
   A.global_band = global_band;
   A.gap_end = gap_end;
-  A.st = t1.as<int4>();
-  A.st2 = t2.as<int4>();
   if (!rc) {
     chk(hipEventRecord(c->ev[0], c->stream), "event");
     chk(launch_sw(A, c->d_counter.as<unsigned long long>(), blocks, c->stream), "k_sw");

@@ -4,7 +4,7 @@
 // followed by aln_global_core (stdaln.c:345-525, gap_end = -1) for the path and
 // aln_path2cigar32 (stdaln.c:1010-1040) for the CIGAR.
 //
-// One alignment per lane, persistent grids with per-wave claiming, one kernel per pass.  The forward
+// One alignment per lane, persistent grid with per-wave claiming.  The forward
 // pass and the global fill are strip-mined (a strip's columns of the row above in
 // registers, one boundary per row through scratch); the reverse pass walks its
 // lane-major eh row by aligned 32-word blocks (whole 128 B lines); all three are branch free per cell.
@@ -34,15 +34,6 @@ __host__ __device__ inline uint32_t sw_tb_width(int max_len1) { return (uint32_t
 #define IBWA_SW_RB 32
 #endif
 constexpr int RB = IBWA_SW_RB;
-// the forward and path kernels held to 3 waves per SIMD (<= 168 VGPRs; 0: the compiler's choice)
-#ifndef IBWA_SW_WPE
-#define IBWA_SW_WPE 3
-#endif
-#if IBWA_SW_WPE > 0
-#define SW_WPE __attribute__((amdgpu_waves_per_eu(IBWA_SW_WPE)))
-#else
-#define SW_WPE
-#endif
 static_assert(RB == 16 || RB == 32, "reverse-pass block of 16 or 32 words");
 // the reverse pass's eh row per lane: eh[0 .. l1+1] in whole blocks
 __host__ __device__ inline uint32_t sw_eh_words(int max_len1) { return (uint32_t)((max_len1 + 2 + RB - 1) / RB * RB); }
@@ -325,241 +316,184 @@ __device__ __forceinline__ void fwd_strip(const Lane &L, uint32_t eREF, uint32_t
 
 }  // namespace
 
-// The three passes run as three kernels over all pairs (k_sw_fwd, k_sw_rev, k_sw_path): each gets
-// the occupancy its own registers allow (the fused kernel ran all three at the forward pass's and
-// the global fill's 210 VGPRs: 2 waves per SIMD for the memory-bound reverse pass), and the state
-// between them is 8 words per pair (SwArgs::st).  One pair per lane, claimed per wave.
-struct SwLanes {
+__global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counter) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // lane-minor elements: ref4[(l1+31)/32*4], the forward pass's strip boundaries H / F per row, the
+  // global fill's (M, I, D) per row; lane-major: eh[0..l1+1] (sw_words_per_lane in total)
+  const uint32_t eREF = 0, eBH = eREF + (A.max_len1 + 31) / 32 * 4, eBF = eBH + A.max_len2 + 1;
+  const uint32_t eB = eBF + A.max_len2 + 1;  // the global fill's (M, I, D) per row at a strip's end
+  const uint32_t nminor = eB + 3 * (A.max_len2 + 1);
+  const uint32_t t_w = sw_tb_width(A.max_len1);
+  const uint32_t eEH = 0, nmajor = sw_eh_words(A.max_len1);
   Lane L;
-  uint32_t eREF, eBH, eBF, eB, t_w, eEH;
-  __device__ SwLanes(const SwArgs &A, int lane, uint64_t wave) {
-    // lane-minor elements: ref4[(l1+31)/32*4], the forward pass's strip boundaries H / F per row,
-    // the global fill's (M, I, D) per row; lane-major: eh[0..l1+1] (sw_words_per_lane in total)
-    eREF = 0;
-    eBH = eREF + (A.max_len1 + 31) / 32 * 4;
-    eBF = eBH + A.max_len2 + 1;
-    eB = eBF + A.max_len2 + 1;  // the global fill's (M, I, D) per row at a strip's end
-    const uint32_t nminor = eB + 3 * (A.max_len2 + 1);
-    t_w = sw_tb_width(A.max_len1);
-    eEH = 0;
-    const uint32_t nmajor = sw_eh_words(A.max_len1);
-    L.w = A.scratch + wave * A.words_per_lane * 64;
-    L.wv = L.w + (uint64_t)nminor * 64 + (uint64_t)lane * nmajor;
-    L.tb = A.tb + wave * A.tb_per_lane * 64;
-    L.lane = lane;
-  }
-};
-
-// the next pair of this lane (-1: none left), claimed 64 at a time by the wave
-__device__ __forceinline__ int64_t sw_claim(const SwArgs &A, unsigned long long *counter, int lane) {
-  int64_t base = 0;
-  if (lane == 0) base = (int64_t)atomicAdd(counter, 64ull);
-  base = __shfl(base, 0);
-  if (base >= A.n) return -2;
-  const int64_t p = base + lane;
-  return p < A.n ? p : -1;
-}
-
-// the read's codes packed 8 per word (the forward and reverse passes' column codes)
-__device__ __forceinline__ void pack_ref(const Lane &L, uint32_t eREF, const uint8_t *a, int n1) {
-  for (int w = 0; w < (n1 + 31) / 32 * 4; ++w) {
-    uint32_t x = 0;
-    for (int k = 0; k < 8 && w * 8 + k < n1; ++k) x |= (uint32_t)a[w * 8 + k] << (4 * k);
-    L.u(eREF + w) = x;
-  }
-}
-
-// ---- forward pass (stdaln.c:579-631): row j over seq2, columns i over seq1.  Strip-mined: STRIP
-// columns at a time for all rows, the strip's H / E of the row above in registers; between strips
-// only (H[j][i0-1], F) per row goes through scratch (fwd_strip).  Writes the outputs of a pair that
-// ends here (no path) and st[p] = (score_f, end_i, end_j) for the reverse pass.
-__global__ void __launch_bounds__(256) SW_WPE k_sw_fwd(SwArgs A, unsigned long long *counter) {
-  const int lane = threadIdx.x & 63;
-  const SwLanes S(A, lane, ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  L.w = A.scratch + wave * A.words_per_lane * 64;
+  L.wv = L.w + (uint64_t)nminor * 64 + (uint64_t)lane * nmajor;
+  L.tb = A.tb + wave * A.tb_per_lane * 64;
+  L.lane = lane;
+  int64_t cur = 0, cend = 0;
   for (;;) {
-    const int64_t p = sw_claim(A, counter, lane);
-    if (p == -2) break;
-    if (p < 0) continue;
-    const int n1 = (int)A.len1[p], n2 = (int)A.len2[p];
-    int score = -1, score_f = 0, end_i = 0, end_j = 0;
-    if (A.global_band <= 0 && n1 > 0 && n2 > 0) {
-      const uint8_t *a = A.seq1 + A.off1[p];
-      const uint8_t *b = A.seq2 + A.off2[p];
-      pack_ref(S.L, S.eREF, a, n1);
-      for (int i0 = 1; i0 <= n1; i0 += STRIP) {
-        if (n1 - i0 + 1 >= STRIP)
-          fwd_strip<false>(S.L, S.eREF, S.eBH, S.eBF, b, n1, n2, i0, score_f, end_i, end_j);
-        else
-          fwd_strip<true>(S.L, S.eREF, S.eBH, S.eBF, b, n1, n2, i0, score_f, end_i, end_j);
-      }
-      score = score_f;
+    // one pair per lane, claimed per wave
+    if (cur >= cend) {
+      int64_t base = 0;
+      if (lane == 0) base = (int64_t)atomicAdd(counter, 64ull);
+      base = __shfl(base, 0);
+      if (base >= A.n) break;
+      cur = base;
+      cend = base + 64 < A.n ? base + 64 : A.n;
     }
-    A.st[p] = make_int4(score_f, end_i, end_j, 0);
-    if (A.global_band <= 0) {
-      A.score[p] = score;
-      A.path_len[p] = 0;
-      A.n_cigar[p] = 0;
-      A.ends[p] = make_int4(0, 0, 0, 0);
-    }
-  }
-}
-
-// ---- reverse pass (stdaln.c:639-696) in the adaptive band, for the pairs whose forward score is
-// >= 1: the start (start_i, start_j) and score_r; st[p].w = 1 marks a pair for the path pass.
-__global__ void __launch_bounds__(256) k_sw_rev(SwArgs A, unsigned long long *counter) {
-  const int lane = threadIdx.x & 63;
-  const SwLanes S(A, lane, ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const Lane &L = S.L;
-  const uint32_t eREF = S.eREF, eEH = S.eEH;
-  for (;;) {
-    const int64_t p = sw_claim(A, counter, lane);
-    if (p == -2) break;
-    if (p < 0) continue;
-    const int4 f4 = A.st[p];
-    const int score_f = f4.x, end_i = f4.y, end_j = f4.z;
-    if (A.global_band > 0 || !(score_f >= 1 && end_i > 0 && end_j > 0) || A.stop_after == 1) continue;
-    const int n1 = (int)A.len1[p];
-    const uint8_t *a = A.seq1 + A.off1[p];
-    const uint8_t *b = A.seq2 + A.off2[p];
-    pack_ref(L, eREF, a, n1);
-    for (int i = 0; i <= end_i; ++i) L.v(eEH + i) = 0;
-    int score_r = sm(a[end_i - 1], b[end_j - 1]);
-    int start_i = end_i, start_j = end_j;
-    L.v(eEH + end_i) = (uint32_t)(QR + score_r) << 16;
-    int start = end_i - 1, end = end_i - 3;
-    if (end <= 0) end = 0;
-    for (int j = end_j - 1; j != 0; --j) {
-      const uint32_t cb = b[j - 1];
-      // the row's score profile: 6-bit field 6*ca = sm(cb, ca) + 32
-      const uint32_t rp = cb > 3 ? 19u * 0x1041041u : 13u * 0x41041u + (19u << 24) + (30u << (6 * cb));
-      int last_h = 0, f = 0, i = start;
-      bool found = false;
-      int nxt = (int)L.v(eEH + i + 1);  // eh[i+1] of the row below (old value)
-      // cells start, start-1, ..., end+1 (start > end >= 0 always) by aligned RB-word blocks of
-      // the eh row: block q = eh[RB q .. RB q + RB-1] is loaded (RB / 4 x 16 B) before its cells
-      // are updated (a cell writes eh[i+1] only, and cells go down, so every loaded value is
-      // still the row below's) and stored back whole: cells outside [end+1, i], or after the
-      // start was found, keep their word; cell RB q + RB-1 writes the next block's first word.
-      // The block's reference codes are packed words of eREF (8 per word: cell RB q + m reads
-      // a[RB q + m - 1]).
-      constexpr int RW = RB / 8;  // eREF words per block
-      while (i > end && !found) {
-        const int q = i / RB;
-        int blk[RB];
-#pragma unroll
-        for (int x = 0; x < RB / 4; ++x) {
-          const uint4 v = L.v4((uint32_t)q * (RB / 4) + x);
-          blk[4 * x] = (int)v.x; blk[4 * x + 1] = (int)v.y; blk[4 * x + 2] = (int)v.z; blk[4 * x + 3] = (int)v.w;
-        }
-        const uint32_t r0 = q > 0 ? L.u(eREF + RW * q - 1) : 0u;
-        uint32_t rw[RW];
-#pragma unroll
-        for (int x = 0; x < RW; ++x) rw[x] = L.u(eREF + RW * q + x);
-        uint32_t out[RB];
-        out[0] = (uint32_t)blk[0];
-        uint32_t top = 0;
-        bool top_act = false;
-        int ii = i;
-#pragma unroll
-        for (int m = RB - 1; m >= 0; --m) {
-          const int ik = RB * q + m;
-          const bool act = ik <= i && ik > end && !found;
-          const int nx = m == RB - 1 ? nxt : blk[m + 1];
-          const uint32_t code = m == 0 ? r0 >> 28 : (rw[(m - 1) >> 3] >> (4 * ((m - 1) & 7))) & 15u;
-          const uint32_t ca = (code < 4u ? code : 4u) * 6u;
-          const int hd = (nx >> 16) + (int)__builtin_amdgcn_ubfe(rp, ca, 6) - 32;
-          const int fn = max(f - R, last_h - QR);
-          const bool lp = last_h > 0;
-          const int fc = lp ? fn : f, fm = lp ? fn : 0;
-          const int above = blk[m] >> 16, e_old = nx & 0xffff;
-          const int e = max(max(e_old - R, above - QR), 0);
-          const int h = max(max(hd, fm), e);  // >= 0: e is
-          const uint32_t val = (uint32_t)last_h << 16 | (uint32_t)e;
-          if (m < RB - 1) {
-            out[m + 1] = act ? val : (uint32_t)blk[m + 1];
-          } else {
-            top = val;
-            top_act = act;
-          }
-          const bool upd = act && score_r < h;
-          if (act) {
-            f = fc;
-            last_h = h;
-          }
-          if (upd) {
-            score_r = h;
-            start_i = ik;
-            start_j = j;
-          }
-          found = found || (upd && h - QR == score_f);  // the start: stop here (j = 1; break)
-          if (act && !found) ii = ik - 1;
-        }
-#pragma unroll
-        for (int x = 0; x < RB / 4; ++x)
-          L.v4((uint32_t)q * (RB / 4) + x) = make_uint4(out[4 * x], out[4 * x + 1], out[4 * x + 2], out[4 * x + 3]);
-        if (top_act) L.v(eEH + (uint32_t)(RB * q + RB)) = top;
-        nxt = blk[0];
-        i = ii;
-      }
-      if (found) j = 1;
-      L.v(eEH + i + 1) = (uint32_t)last_h << 16;
-      if (((int)L.v(eEH + start) >> 16) <= QR) --start;
-      if (start <= 0) start = 0;
-      end = start_i - (start_j - j) - (score_r + (start_j - j) * MAXSC) / R - 1;
-      if (end <= 0) end = 0;
-    }
-    score_r -= QR;
-    A.st2[p] = make_int4(start_i, start_j, score_r, A.stop_after == 2 ? 0 : 1);
-  }
-}
-
-// ---- the path (stdaln.c:723-745): banded global alignment from the start to the end, band
-// doubling from 50, then the CIGAR reversed and the coordinates; or (global_band > 0)
-// aln_global_core alone over whole sequences (bwa_refine_gapped, bwase.c:198).
-__global__ void __launch_bounds__(256) SW_WPE k_sw_path(SwArgs A, unsigned long long *counter) {
-  const int lane = threadIdx.x & 63;
-  const SwLanes S(A, lane, ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  for (;;) {
-    const int64_t p = sw_claim(A, counter, lane);
-    if (p == -2) break;
-    if (p < 0) continue;
+    const int64_t p = cur + lane;
+    cur = cend;
+    if (p >= cend) continue;
     const int n1 = (int)A.len1[p], n2 = (int)A.len2[p];
     const uint8_t *a = A.seq1 + A.off1[p];
     const uint8_t *b = A.seq2 + A.off2[p];
     uint32_t *cig = A.cigar + (uint64_t)p * A.cigar_cap;
-    int score = 0, path_len = 0, n_cig = 0, s_i = 0, s_j = 0, e_i = 0, e_j = 0;
+    int score = -1, path_len = 0, n_cig = 0, s_i = 0, s_j = 0, e_i = 0, e_j = 0;
     if (A.global_band > 0) {
+      // aln_global_core alone (bwa_refine_gapped, bwase.c:198): whole sequences, one band
+      score = 0;
       if (n1 > 0 && n2 > 0) {
         int si = 0, sj = 0;
-        score = global_fill(S.L, S.eB, 0, S.t_w, a, n1, b, n2, A.global_band, A.gap_end, cig, A.cigar_cap, n_cig,
-                            path_len, si, sj);
+        score = global_fill(L, eB, 0, t_w, a, n1, b, n2, A.global_band, A.gap_end, cig,
+                            A.cigar_cap, n_cig, path_len, si, sj);
+        for (int k = 0; k < n_cig / 2; ++k) {
+          const uint32_t t = cig[k];
+          cig[k] = cig[n_cig - 1 - k];
+          cig[n_cig - 1 - k] = t;
+        }
         s_i = si; s_j = sj; e_i = n1; e_j = n2;
       }
-    } else {
-      const int4 f4 = A.st[p];
-      if (!(f4.x >= 1 && f4.y > 0 && f4.z > 0) || A.stop_after == 1) continue;
-      const int4 r4 = A.st2[p];
-      if (!r4.w) continue;
-      const int score_f = f4.x, end_i = f4.y, end_j = f4.z, start_i = r4.x, start_j = r4.y, score_r = r4.z;
-      const int span = ((end_i - start_i > end_j - start_j) ? end_i - start_i : end_j - start_j) + 1;
-      const int n1s = end_i - start_i + 1, n2s = end_j - start_j + 1;
-      int score_g = 0, si = 0, sj = 0;
-      for (int bw = BAND;; bw <<= 1) {
-        score_g = global_fill(S.L, S.eB, 0, S.t_w, a + start_i - 1, n1s, b + start_j - 1, n2s, bw, -1, cig,
-                              A.cigar_cap, n_cig, path_len, si, sj);
-        if (score_g == score_r || score_f == score_g) break;
-        if (bw > span) break;
+    } else if (n1 > 0 && n2 > 0) {
+      // ---- forward pass (stdaln.c:579-631): row j over seq2, columns i over seq1.
+      // Strip-mined: STRIP columns at a time for all rows, the strip's H / E of the row
+      // above in registers; between strips only (H[j][i0-1], F) per row goes through
+      // scratch (fwd_strip).
+      for (int w = 0; w < (n1 + 31) / 32 * 4; ++w) {
+        uint32_t x = 0;
+        for (int k = 0; k < 8 && w * 8 + k < n1; ++k) x |= (uint32_t)a[w * 8 + k] << (4 * k);
+        L.u(eREF + w) = x;
       }
-      score = (score_r > score_g && score_f > score_g) ? -1 : score_g;
-      s_i = si + start_i - 1; s_j = sj + start_j - 1;
-      e_i = n1s + start_i - 1; e_j = n2s + start_j - 1;
+      int score_f = 0, end_i = 0, end_j = 0;
+      for (int i0 = 1; i0 <= n1; i0 += STRIP) {
+        if (n1 - i0 + 1 >= STRIP)
+          fwd_strip<false>(L, eREF, eBH, eBF, b, n1, n2, i0, score_f, end_i, end_j);
+        else
+          fwd_strip<true>(L, eREF, eBH, eBF, b, n1, n2, i0, score_f, end_i, end_j);
+      }
+      score = score_f;
+      if (score_f >= 1 && end_i > 0 && end_j > 0 && A.stop_after != 1) {
+        // ---- reverse pass (stdaln.c:639-696) in the adaptive band
+        for (int i = 0; i <= end_i; ++i) L.v(eEH + i) = 0;
+        int score_r = sm(a[end_i - 1], b[end_j - 1]);
+        int start_i = end_i, start_j = end_j;
+        L.v(eEH + end_i) = (uint32_t)(QR + score_r) << 16;
+        int start = end_i - 1, end = end_i - 3;
+        if (end <= 0) end = 0;
+        for (int j = end_j - 1; j != 0; --j) {
+          const uint32_t cb = b[j - 1];
+          // the row's score profile: 6-bit field 6*ca = sm(cb, ca) + 32
+          const uint32_t rp = cb > 3 ? 19u * 0x1041041u : 13u * 0x41041u + (19u << 24) + (30u << (6 * cb));
+          int last_h = 0, f = 0, i = start;
+          bool found = false;
+          int nxt = (int)L.v(eEH + i + 1);  // eh[i+1] of the row below (old value)
+          // cells start, start-1, ..., end+1 (start > end >= 0 always) by aligned RB-word blocks of
+          // the eh row: block q = eh[RB q .. RB q + RB-1] is loaded (RB / 4 x 16 B) before its cells
+          // are updated (a cell writes eh[i+1] only, and cells go down, so every loaded value is
+          // still the row below's) and stored back whole: cells outside [end+1, i], or after the
+          // start was found, keep their word; cell RB q + RB-1 writes the next block's first word.
+          // The block's reference codes are packed words of the forward pass's eREF (8 per word:
+          // cell RB q + m reads a[RB q + m - 1]).
+          constexpr int RW = RB / 8;  // eREF words per block
+          while (i > end && !found) {
+            const int q = i / RB;
+            int blk[RB];
+#pragma unroll
+            for (int x = 0; x < RB / 4; ++x) {
+              const uint4 v = L.v4((uint32_t)q * (RB / 4) + x);
+              blk[4 * x] = (int)v.x; blk[4 * x + 1] = (int)v.y; blk[4 * x + 2] = (int)v.z; blk[4 * x + 3] = (int)v.w;
+            }
+            const uint32_t r0 = q > 0 ? L.u(eREF + RW * q - 1) : 0u;
+            uint32_t rw[RW];
+#pragma unroll
+            for (int x = 0; x < RW; ++x) rw[x] = L.u(eREF + RW * q + x);
+            uint32_t out[RB];
+            out[0] = (uint32_t)blk[0];
+            uint32_t top = 0;
+            bool top_act = false;
+            int ii = i;
+#pragma unroll
+            for (int m = RB - 1; m >= 0; --m) {
+              const int ik = RB * q + m;
+              const bool act = ik <= i && ik > end && !found;
+              const int nx = m == RB - 1 ? nxt : blk[m + 1];
+              const uint32_t code = m == 0 ? r0 >> 28 : (rw[(m - 1) >> 3] >> (4 * ((m - 1) & 7))) & 15u;
+              const uint32_t ca = (code < 4u ? code : 4u) * 6u;
+              const int hd = (nx >> 16) + (int)__builtin_amdgcn_ubfe(rp, ca, 6) - 32;
+              const int fn = max(f - R, last_h - QR);
+              const bool lp = last_h > 0;
+              const int fc = lp ? fn : f, fm = lp ? fn : 0;
+              const int above = blk[m] >> 16, e_old = nx & 0xffff;
+              const int e = max(max(e_old - R, above - QR), 0);
+              const int h = max(max(hd, fm), e);  // >= 0: e is
+              const uint32_t val = (uint32_t)last_h << 16 | (uint32_t)e;
+              if (m < RB - 1) {
+                out[m + 1] = act ? val : (uint32_t)blk[m + 1];
+              } else {
+                top = val;
+                top_act = act;
+              }
+              const bool upd = act && score_r < h;
+              if (act) {
+                f = fc;
+                last_h = h;
+              }
+              if (upd) {
+                score_r = h;
+                start_i = ik;
+                start_j = j;
+              }
+              found = found || (upd && h - QR == score_f);  // the start: stop here (j = 1; break)
+              if (act && !found) ii = ik - 1;
+            }
+#pragma unroll
+            for (int x = 0; x < RB / 4; ++x)
+              L.v4((uint32_t)q * (RB / 4) + x) = make_uint4(out[4 * x], out[4 * x + 1], out[4 * x + 2], out[4 * x + 3]);
+            if (top_act) L.v(eEH + (uint32_t)(RB * q + RB)) = top;
+            nxt = blk[0];
+            i = ii;
+          }
+          if (found) j = 1;
+          L.v(eEH + i + 1) = (uint32_t)last_h << 16;
+          if (((int)L.v(eEH + start) >> 16) <= QR) --start;
+          if (start <= 0) start = 0;
+          end = start_i - (start_j - j) - (score_r + (start_j - j) * MAXSC) / R - 1;
+          if (end <= 0) end = 0;
+        }
+        score_r -= QR;
+        if (A.stop_after == 2) goto done;
+        // ---- path by banded global alignment, band doubling from 50 (stdaln.c:723-745)
+        const int span = ((end_i - start_i > end_j - start_j) ? end_i - start_i : end_j - start_j) + 1;
+        const int n1s = end_i - start_i + 1, n2s = end_j - start_j + 1;
+        int score_g = 0, si = 0, sj = 0;
+        for (int bw = BAND;; bw <<= 1) {
+          score_g = global_fill(L, eB, 0, t_w, a + start_i - 1, n1s, b + start_j - 1, n2s,
+                                bw, -1, cig, A.cigar_cap, n_cig, path_len, si, sj);
+          if (score_g == score_r || score_f == score_g) break;
+          if (bw > span) break;
+        }
+        score = (score_r > score_g && score_f > score_g) ? -1 : score_g;
+        // reverse the CIGAR (traced end -> start) and convert the coordinates
+        for (int k = 0; k < n_cig / 2; ++k) {
+          const uint32_t t = cig[k];
+          cig[k] = cig[n_cig - 1 - k];
+          cig[n_cig - 1 - k] = t;
+        }
+        s_i = si + start_i - 1; s_j = sj + start_j - 1;
+        e_i = n1s + start_i - 1; e_j = n2s + start_j - 1;
+      }
     }
-    // the CIGAR was traced end -> start
-    for (int k = 0; k < n_cig / 2; ++k) {
-      const uint32_t t = cig[k];
-      cig[k] = cig[n_cig - 1 - k];
-      cig[n_cig - 1 - k] = t;
-    }
+  done:
     A.score[p] = score;
     A.path_len[p] = path_len;
     A.n_cigar[p] = n_cig;
@@ -589,18 +523,9 @@ hipError_t launch_pack_cigar(const uint32_t *cig, int cap, const int32_t *n_ciga
 
 hipError_t launch_sw(const SwArgs &a, unsigned long long *d_counter, int blocks, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
-  // one claim counter per pass (d_counter[0..2])
-  hipError_t e = zero_async(d_counter, 3 * sizeof(unsigned long long), st);
+  hipError_t e = zero_async(d_counter, sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
-  if (a.global_band <= 0) {
-    hipLaunchKernelGGL(k_sw_fwd, dim3(blocks), dim3(256), 0, st, a, d_counter);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (a.stop_after == 1) return hipSuccess;
-    hipLaunchKernelGGL(k_sw_rev, dim3(blocks), dim3(256), 0, st, a, d_counter + 1);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (a.stop_after == 2) return hipSuccess;
-  }
-  hipLaunchKernelGGL(k_sw_path, dim3(blocks), dim3(256), 0, st, a, d_counter + 2);
+  hipLaunchKernelGGL(k_sw, dim3(blocks), dim3(256), 0, st, a, d_counter);
   return hipGetLastError();
 }
 
