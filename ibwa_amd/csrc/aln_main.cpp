@@ -558,10 +558,26 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         return die("a second context on the GPU");
       lctx[l].push_back(x);
     }
+  // a slice's .sai records (ibwa_batch_fetch_sai), in buffers that go round: slice thread -> writer
+  // -> pool (no allocation or page faults per group once the pool holds a buffer per slice in flight)
+  struct SaiBuf {
+    std::unique_ptr<char[]> p;
+    uint64_t cap = 0, bytes = 0;
+  };
+  std::mutex pool_mu;
+  std::vector<SaiBuf> pool;
+  auto take_buf = [&]() {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    SaiBuf b;
+    if (!pool.empty()) {
+      b = std::move(pool.back());
+      pool.pop_back();
+    }
+    return b;
+  };
   struct Job {
     Group b;
-    std::vector<std::vector<int32_t>> naln;
-    std::vector<ibwa_aln1_t *> aln;
+    std::vector<SaiBuf> sai;
     std::vector<int> rc;
     std::vector<std::thread> th;
     std::chrono::steady_clock::time_point t0;
@@ -578,8 +594,8 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   } join_jobs{jobs};
   auto launch = [&](Job &J, std::vector<ibwa_ctx_t *> &cx) {
     const int64_t n = J.b.n();
-    J.naln.assign(n_gpus, {});
-    J.aln.assign(n_gpus, nullptr);
+    J.sai.clear();
+    J.sai.resize(n_gpus);
     J.rc.assign(n_gpus, 0);
     J.th.clear();
     J.t0 = std::chrono::steady_clock::now();
@@ -595,11 +611,10 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         stage_ms[g] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s0).count();
       }
     for (int g = 0; g < n_gpus; ++g) {
-      J.th.emplace_back([&J, &cx, &opt, g, n, per, sms = stage_ms[g]]() {
+      J.th.emplace_back([&J, &cx, &opt, &take_buf, g, n, per, sms = stage_ms[g]]() {
         const Group &cur = J.b;
         int64_t b = std::min<int64_t>(n, g * per), e = std::min<int64_t>(n, b + per);
         if (cur.dev) b = 0, e = cur.dg.count[g];
-        J.naln[g].resize(e - b);
         int64_t tot = 0;
         auto c0 = std::chrono::steady_clock::now();
         int rc = J.rc[g];
@@ -616,7 +631,18 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         auto c1 = std::chrono::steady_clock::now();
         if (!rc) rc = ibwa_batch_run(cx[g], &opt, cur.max_len());
         auto c2 = std::chrono::steady_clock::now();
-        if (!rc) rc = ibwa_batch_fetch(cx[g], J.naln[g].data(), &J.aln[g], &tot);
+        if (!rc) {  // the records serialised straight into a pooled buffer (grown when too small)
+          SaiBuf sb = take_buf();
+          uint64_t need = 0;
+          rc = ibwa_batch_fetch_sai(cx[g], sb.p.get(), sb.cap, &need, &tot);
+          if (!rc && need > sb.cap) {
+            sb.cap = need + need / 8;
+            sb.p.reset(new char[sb.cap]);
+            rc = ibwa_batch_fetch_sai(cx[g], sb.p.get(), sb.cap, &need, &tot);
+          }
+          sb.bytes = need;
+          J.sai[g] = std::move(sb);
+        }
         auto c3 = std::chrono::steady_clock::now();
         J.rc[g] = rc;
         if (kTimes) {
@@ -649,48 +675,11 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       fprintf(stderr, "[ibwa-amd aln] write failed\n");
       return 1;
     }
-    writer = std::thread([out, &write_failed, naln = std::move(J.naln), aln = std::move(J.aln)]() {
-      // per slice: the records serialised by up to 8 threads (each a contiguous range of reads, at
-      // its byte offset), then one write -- the last group's write is on the wall clock
-      for (size_t g = 0; g < naln.size(); ++g) {
-        const std::vector<int32_t> &na = naln[g];
-        const int64_t n = (int64_t)na.size();
-        const int T = (int)std::max<int64_t>(1, std::min<int64_t>(8, n >> 16));
-        std::vector<size_t> bo(T + 1, 0), ho(T + 1, 0);  // per range: its first byte / first hit
-        std::vector<std::thread> th;
-        for (int t = 0; t < T; ++t)
-          th.emplace_back([&, t]() {
-            size_t b = 0, h = 0;
-            for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
-              b += 4 + (size_t)na[r] * sizeof(ibwa_aln1_t);
-              h += (size_t)na[r];
-            }
-            bo[t + 1] = b;
-            ho[t + 1] = h;
-          });
-        for (auto &x : th) x.join();
-        th.clear();
-        for (int t = 0; t < T; ++t) {
-          bo[t + 1] += bo[t];
-          ho[t + 1] += ho[t];
-        }
-        std::unique_ptr<char[]> buf(new char[std::max<size_t>(bo[T], 1)]);  // not zero-filled: every byte is written
-        for (int t = 0; t < T; ++t)
-          th.emplace_back([&, t]() {
-            char *w = buf.get() + bo[t];
-            const ibwa_aln1_t *p = aln[g] + ho[t];
-            for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
-              const int32_t k = na[r];
-              memcpy(w, &k, 4);
-              w += 4;
-              if (k) memcpy(w, p, (size_t)k * sizeof(ibwa_aln1_t));
-              w += (size_t)k * sizeof(ibwa_aln1_t);
-              p += k;
-            }
-          });
-        for (auto &x : th) x.join();
-        if (bo[T] && fwrite(buf.get(), 1, bo[T], out) != bo[T]) write_failed = true;
-        ibwa_free(aln[g]);
+    writer = std::thread([out, &write_failed, &pool_mu, &pool, sai = std::move(J.sai)]() mutable {
+      for (auto &b : sai) {
+        if (b.bytes && fwrite(b.p.get(), 1, b.bytes, out) != b.bytes) write_failed = true;
+        std::lock_guard<std::mutex> lk(pool_mu);
+        pool.push_back(std::move(b));
       }
     });
     fprintf(stderr, "0.00 sec\n");

@@ -341,6 +341,8 @@ struct ibwa_ctx {
   std::vector<uint8_t> retry_pass;  // per retry_ids entry: 1 coop, 2 wide, 3 general kernels
   std::vector<int64_t> resumed_ids; // reads the cooperative pass resolved from a resume state (retry_info pass 4)
   bool naln_on_host = true;  // h_naln mirrors d_naln
+  bool fetched = false;       // the batch's results are on the host (fetch_to_host; a run resets it)
+  std::vector<int32_t> h_cnt;  // per read its hits, patches included (fetch_to_host)
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
   int kmer_k = -1;  // requested K (-1: auto from the genome size, 0: off)
@@ -1254,6 +1256,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   if (!c->loaded[0] || !c->loaded[1]) return fail(IBWA_ENOINDEX, "load both .bwt and .rbwt first");
   if (c->ix[0].seq_len != c->ix[1].seq_len) return fail(IBWA_EINVAL, ".bwt and .rbwt lengths differ");
   if (int rc = check_opt(opt)) return rc;
+  c->fetched = false;
   HIPCHK(enter(c));
   memset(&c->stats, 0, sizeof(c->stats));
   g_alloc_ms = 0;
@@ -2303,10 +2306,12 @@ int ibwa_batch_diag(const ibwa_ctx_t *c, int what, void *out, uint64_t cap_bytes
   return 0;
 }
 
-int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total) {
+// the batch's results to the host once (h_naln / h_aoff / h_aln), and per read its hit count with
+// the wide / general passes' patches in (c->h_cnt)
+static int fetch_to_host(ibwa_ctx_t *c) {
+  if (c->fetched) return 0;
   const int64_t n = c->n;
   const uint32_t cap = c->aln_cap_used;
-  // first-pass hits: per-read slots (n x cap), or the hit stream + per-read offsets
   const uint64_t n_slots = c->stream_out ? c->stream_len : (uint64_t)n * cap;
   c->h_aln.resize(std::max<uint64_t>(n_slots, 1));
   if (n) {
@@ -2323,10 +2328,69 @@ int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *
     if (n_slots) HIPCHK(hipMemcpyAsync(c->h_aln.data(), c->d_aln.p, n_slots * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }
-  // patch in the reads the wide / general passes resolved (the first and cooperative passes wrote
+  c->h_cnt.assign(c->h_naln.begin(), c->h_naln.begin() + n);
+  for (size_t j = 0; j < c->patch_ids.size(); ++j) c->h_cnt[c->patch_ids[j]] = (int32_t)c->patch_alns[j].size();
+  c->fetched = true;
+  return 0;
+}
+
+int ibwa_batch_fetch_sai(ibwa_ctx_t *c, void *dst, uint64_t cap_bytes, uint64_t *bytes, int64_t *n_total) {
+  if (!c || !bytes) return fail(IBWA_EINVAL, "fetch_sai: bad arguments");
+  if (int rc = fetch_to_host(c)) return rc;
+  const int64_t n = c->n;
+  const uint32_t cap = c->aln_cap_used;
+  const int32_t *cnt = c->h_cnt.data();
+  // per range of reads (one per host thread): its bytes and hits, then the ranges' offsets
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(16, n >> 16));
+  std::vector<uint64_t> bo(T + 1, 0), ho(T + 1, 0);
+  auto ranges = [&](auto &&fn) {
+    if (T == 1) { fn(0); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(fn, t);
+    for (auto &x : th) x.join();
+  };
+  ranges([&](int t) {
+    uint64_t h = 0;
+    for (int64_t i = n * t / T; i < n * (t + 1) / T; ++i) h += (uint64_t)cnt[i];
+    ho[t + 1] = h;
+    bo[t + 1] = h * 16 + (uint64_t)(n * (t + 1) / T - n * t / T) * 4;
+  });
+  for (int t = 0; t < T; ++t) {
+    bo[t + 1] += bo[t];
+    ho[t + 1] += ho[t];
+  }
+  *bytes = bo[T];
+  if (n_total) *n_total = (int64_t)ho[T];
+  if (!dst || cap_bytes < bo[T]) return 0;
+  ranges([&](int t) {
+    char *w = static_cast<char *>(dst) + bo[t];
+    const int64_t lo = n * t / T;
+    size_t rj = std::lower_bound(c->patch_ids.begin(), c->patch_ids.end(), lo) - c->patch_ids.begin();
+    for (int64_t i = lo; i < n * (t + 1) / T; ++i) {
+      const int32_t k = cnt[i];
+      const uint4 *src;
+      if (rj < c->patch_ids.size() && c->patch_ids[rj] == i) {
+        src = c->patch_alns[rj].data();
+        ++rj;
+      } else {
+        src = c->h_aln.data() + (c->stream_out ? (k ? c->h_aoff[i] : 0) : (uint64_t)i * cap);
+      }
+      memcpy(w, &k, 4);
+      if (k) memcpy(w + 4, src, (size_t)k * 16);
+      w += 4 + (size_t)k * 16;
+    }
+  });
+  return 0;
+}
+
+int ibwa_batch_fetch(ibwa_ctx_t *c, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total) {
+  const int64_t n = c->n;
+  const uint32_t cap = c->aln_cap_used;
+  // first-pass hits (per-read slots n x cap, or the hit stream + per-read offsets) to the host, with
+  // the reads the wide / general passes resolved patched in (the first and cooperative passes wrote
   // theirs into d_naln / d_aln)
-  std::vector<int32_t> cnt(c->h_naln.begin(), c->h_naln.end());
-  for (size_t j = 0; j < c->patch_ids.size(); ++j) cnt[c->patch_ids[j]] = (int32_t)c->patch_alns[j].size();
+  if (int rc = fetch_to_host(c)) return rc;
+  const std::vector<int32_t> &cnt = c->h_cnt;
   std::vector<int64_t> at(n + 1, 0);  // output offset of read i
   for (int64_t i = 0; i < n; ++i) at[i + 1] = at[i] + cnt[i];
   const int64_t tot = at[n];

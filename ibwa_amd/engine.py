@@ -88,6 +88,7 @@ CAPI = {
     "ibwa_fq_stats": (_i, [_vp, c.POINTER(c.c_int64), c.POINTER(c.c_double)]),
     "ibwa_fq_offset": (_i, [_vp, c.c_int64, c.POINTER(c.c_uint64)]),
     "ibwa_fq_share_scratch": (_i, [_vp, _vp]),
+    "ibwa_batch_fetch_sai": (_i, [_vp, _vp, c.c_uint64, c.POINTER(c.c_uint64), c.POINTER(c.c_int64)]),
     "ibwa_batch_stage_fq": (_i, [_vp, _vp, c.c_int64, c.c_int64, _i]),
     "ibwa_host_alloc": (_i, [c.c_uint64, c.POINTER(_vp)]),
     "ibwa_host_free": (_i, [_vp]),
@@ -251,6 +252,14 @@ class Engine:
         buf = c.string_at(ptr.value, tot.value * 16)
         lib().ibwa_free(ptr)
         return n_aln, np.frombuffer(buf, dtype=ALN_DTYPE).copy()
+
+    def fetch_sai(self):
+        """The batch's .sai records (ibwa_batch_fetch_sai): per read int32 n_aln + n_aln records."""
+        need = c.c_uint64()
+        _chk(lib().ibwa_batch_fetch_sai(self.h, None, 0, c.byref(need), None))
+        buf = c.create_string_buffer(max(need.value, 1))
+        _chk(lib().ibwa_batch_fetch_sai(self.h, buf, need.value, c.byref(need), None))
+        return buf.raw[:need.value]
 
     def retry_info(self):
         """(read ids, pass) of the reads the last run's first pass handed on; pass 1 = coop,

@@ -162,6 +162,11 @@ int ibwa_host_alloc(uint64_t bytes, void **p);
 int ibwa_host_free(void *p);
 int ibwa_batch_run(ibwa_ctx_t *ctx, const ibwa_gap_opt_t *opt, int batch_max_len);
 int ibwa_batch_fetch(ibwa_ctx_t *ctx, int32_t *n_aln, ibwa_aln1_t **aln, int64_t *n_total);
+/* The batch's .sai records (bwtaln.c:227-231: per read its int n_aln, then n_aln bwt_aln1_t), in
+ * input order, serialised by host threads straight into the caller's buffer.  *bytes = their size;
+ * with dst == NULL or cap < *bytes nothing is written (call again with a buffer that large: the
+ * device results are copied back once per batch).  *n_total = the hits (may be NULL). */
+int ibwa_batch_fetch_sai(ibwa_ctx_t *ctx, void *dst, uint64_t cap, uint64_t *bytes, int64_t *n_total);
 
 /*
  * ibwa_ctx_prepare: the per-index device structures the first ibwa_batch_run with

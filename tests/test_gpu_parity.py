@@ -55,6 +55,29 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path, gappe
     assert not bad, bad
 
 
+def test_fetch_sai_equals_fetch(golden_dir, sai_manifest, gpu_engine):
+    """ibwa_batch_fetch_sai (the CLI's writer input: records serialised by host threads into the
+    caller's buffer) == the .sai body built from ibwa_batch_fetch, == the reference's golden; a buffer
+    too small is left untouched and reports the size."""
+    import ctypes as c
+    for key in ("r100.default", "mixed.N", "r150.m50"):
+        m = sai_manifest[key]
+        opt, _ = oracle.parse_aln_args(m["argv"])
+        recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+        seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+        gpu_engine.stage(seqs, offs, lens)
+        gpu_engine.run(_eopt(opt))
+        body = gpu_engine.fetch_sai()
+        n_aln, alns = gpu_engine.fetch()
+        assert body == oracle.sai_bytes(opt, n_aln, alns)[64:], key
+        exp = open(os.path.join(golden_dir, key + ".sai"), "rb").read()
+        assert body == exp[64:], key
+        small = c.create_string_buffer(b"\x5a" * 16, 16)
+        need = c.c_uint64()
+        assert E.lib().ibwa_batch_fetch_sai(gpu_engine.h, small, 16, c.byref(need), None) == 0
+        assert need.value == len(body) and small.raw == b"\x5a" * 16
+
+
 @pytest.mark.parametrize("width_jump", [0, 2])
 def test_sai_goldens_width_jump(golden_dir, sai_manifest, gpu_engine, width_jump):
     """k_width with (2: SA / text derived from the loaded BWT) and without (0) one-row steps from
