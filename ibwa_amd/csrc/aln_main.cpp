@@ -392,11 +392,13 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
   {
     // The default arena follows the inputs, from what round 5 measured of the engine's buffers
-    // (profiles/r05_e2e_b.json, r05_bench_v1.json extra.e2e, r05_pipe_full_v1.json; 221.6 GB for
-    // 100 bp reads in 2 GiB pieces, 170.7 GB in 1 GiB pieces, 174.5 GB for 150 bp in 2 GiB pieces,
-    // all at 2 lanes): the index structures (bit planes, relaid-out BWT, K-mer tables: ~17x the two
-    // .bwt files at GRCh37 size), per lane ~46 GB of search pools (smaller for a small batch) plus
-    // ~18x the FASTQ bytes a group holds, and per ingest slot ~2.5x the piece.  At most kArenaMaxGb.
+    // (IBWA_ARENA_TRACE=1 lists every carve: profiles/r05_arena_trace.log, 100 bp reads in 2 GiB
+    // pieces, 2 lanes): the index structures (relaid-out BWT, bit planes, K-mer tables of K <= 14:
+    // ~7.4x the two .bwt files at GRCh37 size); per lane ~22.6 GB per GiB of FASTQ its group holds
+    // (resume states 12.5, widths 8.7, compressed widths and per-read arrays 1.4) plus ~32 GB that
+    // do not grow with the group (first-pass slots 12.9, page pools 4.8, cooperative pool 10.7 --
+    // 17.2 above 128 bp -- and staging 3.2; fewer for a small group, whose grids are smaller); the
+    // ingest scratch ~1.7x a piece and per ingest slot ~0.75x a piece.  At most kArenaMaxGb.
     auto fbytes = [](const std::string &f) -> double {
       struct stat st;
       return stat(f.c_str(), &st) == 0 ? (double)st.st_size : 0.0;
@@ -406,8 +408,8 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     // FASTQ bytes of one GPU's group: a piece of the file, or (host readers) up to kGroup batches
     const double fq = fq_path ? fbytes(fq_path) * (gz ? 4.0 : 1.0) : 0.0;
     const double grp = std::min(fq / n_gpus, fq_dev ? (double)piece : (double)kGroup * kSub * 300.0) / GiB;
-    const double need_gb = 24.0 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
-                           n_lanes * (std::min(46.0, 92.0 * grp) + 18.0 * grp) + (n_lanes + 3) * 2.5 * grp + 2.0;
+    const double need_gb = 8.0 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
+                           n_lanes * (std::min(36.0, 72.0 * grp) + 23.0 * grp) + 1.7 * grp + (n_lanes + 3) * 0.8 * grp + 2.0;
     const char *ag = getenv("IBWA_ARENA_GB");
     std::vector<std::thread> th;
     std::vector<int> rc(n_used, 0);

@@ -204,11 +204,55 @@ struct FqScratch {
   const void *last = nullptr;  // the context whose block the line table holds (ibwa_fq_offset)
   DBuf raw, tile, nl, cnt, len, L, key, tmp;
   uint32_t *hinit = nullptr;  // pinned: the parse counters' initial values, then zeros for the padding
+  // a block in pageable memory (the CLI's mapped file) goes to the device through two pinned
+  // staging chunks, filled by host threads: left to the HIP runtime, a pageable copy locks the
+  // file's pages, and unlocking GBs of them cost ~0.3 s at process exit (profiles/r05_e2e_g.json)
+  static constexpr size_t kStage = 64u << 20;
+  char *stage[2] = {nullptr, nullptr};
+  hipEvent_t sev[2] = {nullptr, nullptr};
   void unref() {
     if (--refs > 0) return;
     for (DBuf *b : {&raw, &tile, &nl, &cnt, &len, &L, &key, &tmp}) b->release();
     if (hinit) (void)hipHostFree(hinit);
+    for (int i = 0; i < 2; ++i) {
+      if (stage[i]) (void)hipHostFree(stage[i]);
+      if (sev[i]) (void)hipEventDestroy(sev[i]);
+    }
     delete this;
+  }
+  // src[0, n) to device dst on stream st
+  hipError_t h2d(void *dst, const void *src, size_t n, hipStream_t st) {
+    hipPointerAttribute_t at;
+    const bool pinned = hipPointerGetAttributes(&at, src) == hipSuccess;
+    (void)hipGetLastError();  // an unregistered pointer is not an error here
+    if (pinned || n < (8u << 20)) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+    for (int i = 0; i < 2; ++i) {
+      if (!stage[i]) {
+        void *p = nullptr;
+        if (hipError_t e = hipHostMalloc(&p, kStage, hipHostMallocDefault)) return e;
+        stage[i] = static_cast<char *>(p);
+      }
+      if (!sev[i])
+        if (hipError_t e = hipEventCreateWithFlags(&sev[i], hipEventDisableTiming)) return e;
+    }
+    const char *s = static_cast<const char *>(src);
+    for (size_t o = 0, k = 0; o < n; o += kStage, ++k) {
+      const int b = (int)(k & 1);
+      const size_t len = std::min(kStage, n - o);
+      if (k >= 2)
+        if (hipError_t e = hipEventSynchronize(sev[b])) return e;  // its previous chunk has left
+      const int T = 8;
+      std::thread th[T];
+      for (int t = 0; t < T; ++t)
+        th[t] = std::thread([&, t]() {
+          const size_t a = len * t / T, z = len * (t + 1) / T;
+          memcpy(stage[b] + a, s + o + a, z - a);
+        });
+      for (auto &x : th) x.join();
+      if (hipError_t e = hipMemcpyAsync(static_cast<char *>(dst) + o, stage[b], len, hipMemcpyHostToDevice, st)) return e;
+      if (hipError_t e = hipEventRecord(sev[b], st)) return e;
+    }
+    return hipSuccess;
   }
 };
 
@@ -323,7 +367,10 @@ struct ibwa_ctx {
   DBuf d_hpop;           // per read: first-pass pops before its resume state (0: none; ibwa_batch_diag 2)
   bool hpop_valid = false;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
-  int coop_pool_gb = 16;             // bucket page pool
+  // bucket page pool, GiB (0: by read length -- 10 up to 128 bp, 16 above: at 100 bp 10 GiB costs
+  // nothing, 5 322 vs 5 316 ms per 50 M-read step; at 150 bp / 2 % it cost 7 %, profiles/r05_sweep_mem*.jsonl)
+  int coop_pool_gb = 0;
+  uint64_t pool_bytes(int max_len) const { return (uint64_t)(coop_pool_gb ? coop_pool_gb : max_len <= 128 ? 10 : 16) << 30; }
   uint32_t coop_pool_pages = 0;      // tests: the pool in pages (0: by coop_pool_gb)
   DBuf c_stg, c_dir, c_free, c_pool, c_hits, c_next, c_recb, c_proot, c_pstore;
   bool stream_out = false;           // d_aln is a hit stream indexed by d_aoff
@@ -396,7 +443,9 @@ int ensure_kmer(ibwa_ctx *c) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     K = 1;
-    while (K < 15 && (1ull << (2 * (K + 1))) <= 2ull * c->ix[0].seq_len &&
+    // at most 14: K = 15 tables (2 x 8.6 GB at GRCh37 size) bought nothing over 14 (2 x 2.1 GB):
+    // 5 311 vs 5 316 ms per 50 M-read step, profiles/r05_sweep_mem.jsonl
+    while (K < 14 && (1ull << (2 * (K + 1))) <= 2ull * c->ix[0].seq_len &&
            2ull * 8ull * (1ull << (2 * (K + 1))) <= (uint64_t)(0.4 * (double)free_b))
       ++K;
   }
@@ -682,7 +731,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_overlap_chunks" && value >= 2 && value <= 64) c->gap_overlap_chunks = (int)value;
   else if (k == "gap_overlap_min" && value >= 1) c->gap_overlap_min = value;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
-  else if (k == "coop_pool_gb" && value > 0 && value <= 256) c->coop_pool_gb = (int)value;
+  else if (k == "coop_pool_gb" && value >= 0 && value <= 256) c->coop_pool_gb = (int)value;
   else if (k == "coop_stg_room" && value >= 1 && value <= 4) c->coop_stg_room = (int)value;
   else if (k == "coop_pool_pages" && value >= 0 && value <= (1l << 24)) c->coop_pool_pages = (uint32_t)value;
   else if (k == "gap_resume_recs" && value >= 1 && value <= 65536) c->gap_resume_recs = (uint32_t)value;
@@ -1099,7 +1148,7 @@ int ibwa_fq_parse(ibwa_ctx_t *c, const void *raw, uint64_t nbytes, int mode, int
     static_cast<uint32_t *>(h)[1] = 0xFFFFFFFFu;
     S.hinit = static_cast<uint32_t *>(h);
   }
-  HIPCHK(hipMemcpyAsync(S.raw.p, raw, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(S.h2d(S.raw.p, raw, nbytes, c->stream));
   if (padded - nbytes <= 2 * FQ_PAD_MAX)
     HIPCHK(hipMemcpyAsync(S.raw.as<uint8_t>() + nbytes, S.hinit + 2, padded - nbytes, hipMemcpyHostToDevice, c->stream));
   else
@@ -1506,8 +1555,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       const int blocks = (int)std::min<int64_t>(full_blocks, lanes);
       const uint32_t freecap = 4096, hcap = 4096;
       const uint64_t pool_bytes = std::min<uint64_t>(
-          (uint64_t)c->coop_pool_gb << 30,
-          std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
+          c->pool_bytes(max_len), std::max<uint64_t>(1ull << 30, c->pool_bytes(max_len) / full_blocks * blocks));
       const uint32_t pool_pages = c->coop_pool_pages ? c->coop_pool_pages : (uint32_t)(pool_bytes / (COOP_PG * 16ull));
       R.pool_pages = pool_pages;
       if (int rc = c->c_stg.ensure((uint64_t)blocks * 64 * 16 << stg_log2)) return rc;
@@ -1883,9 +1931,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       const int blocks = (int)std::min<int64_t>(std::max(1, full_blocks >> (3 * round)), lanes);
       const uint32_t freecap = 4096, hcap = 4096;
       const uint64_t pool_bytes =
-          round ? (uint64_t)c->coop_pool_gb << 30
-                : std::min<uint64_t>((uint64_t)c->coop_pool_gb << 30,
-                                     std::max<uint64_t>(1ull << 30, ((uint64_t)c->coop_pool_gb << 30) / full_blocks * blocks));
+          round ? c->pool_bytes(max_len)
+                : std::min<uint64_t>(c->pool_bytes(max_len),
+                                     std::max<uint64_t>(1ull << 30, c->pool_bytes(max_len) / full_blocks * blocks));
       const uint32_t pool_pages = c->coop_pool_pages ? c->coop_pool_pages : (uint32_t)(pool_bytes / (COOP_PG * 16ull));
       if (int rc = c->d_ids.ensure(lanes * 8)) return rc;
       if (int rc = c->d_wbuf.ensure(lanes * A.wstride * 8)) return rc;

@@ -165,7 +165,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     defaults = {"gap_cap1": 8192, "gap_pages_per_block": 384, "exact_path": 1, "gapped_v2": 1, "exact_jump": 1,
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
-                "gap_resume_entries": 300, "coop_pool_gb": 16, "gap_tail_lanes": 16, "gap_tail_iters": 200,
+                "gap_resume_entries": 300, "coop_pool_gb": 0, "gap_tail_lanes": 16, "gap_tail_iters": 200,
                 "gap_lw_min_waves": 8, "coop_pool_pages": 0, "gap_overlap_min": 8 << 20, "gap_overlap_chunks": 4,
                 "gap_overlap": 0}
     try:
