@@ -105,6 +105,9 @@ def run(argv, timeout=1800, env=None, save_stderr=None):
         if m:
             log("  cli:", ln.strip())
             phases["gpu parse"] = {"records": int(m.group(1)), "producer_s": float(m.group(2)), "device_ms": int(m.group(3))}
+        m = re.search(r"exit probe: (.*) ([\d.]+) ms", ln)
+        if m:
+            phases.setdefault("exit probe ms", {})[m.group(1)] = float(m.group(2))
         m = re.search(r"exiting at ([\d.]+) s", ln)
         if m:
             phases["exiting at"] = float(m.group(1))
