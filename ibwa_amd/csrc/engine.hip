@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -2356,11 +2357,23 @@ int ibwa_batch_diag(const ibwa_ctx_t *c, int what, void *out, uint64_t cap_bytes
 
 // the batch's results to the host once (h_naln / h_aoff / h_aln), and per read its hit count with
 // the wide / general passes' patches in (c->h_cnt)
+// huge pages for a large host array (fewer faults, and fewer page tables to tear down at exit)
+static void advise_huge(const void *p, size_t bytes) {
+  const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+  const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(uintptr_t)((2u << 20) - 1);
+  if (e > a) (void)madvise(reinterpret_cast<void *>(a), e - a, MADV_HUGEPAGE);
+}
+
 static int fetch_to_host(ibwa_ctx_t *c) {
   if (c->fetched) return 0;
   const int64_t n = c->n;
   const uint32_t cap = c->aln_cap_used;
   const uint64_t n_slots = c->stream_out ? c->stream_len : (uint64_t)n * cap;
+  if (c->h_aln.capacity() < n_slots) {
+    std::vector<uint4>().swap(c->h_aln);
+    c->h_aln.reserve(n_slots + n_slots / 8);  // not touched yet: huge pages advised first
+    advise_huge(c->h_aln.data(), c->h_aln.capacity() * sizeof(uint4));
+  }
   c->h_aln.resize(std::max<uint64_t>(n_slots, 1));
   if (n) {
     HIPCHK(enter(c));

@@ -116,7 +116,7 @@ class FastqGpu {
     if (producer_.joinable()) producer_.join();
     if (reader_.joinable()) reader_.join();
     for (char *b : buf_) ibwa_host_free(b);
-    if (map_) munmap(const_cast<char *>(map_), fsize_);
+    if (map_ && map_lo_ < fsize_) munmap(const_cast<char *>(map_) + map_lo_, fsize_ - map_lo_);
     if (fd_ >= 0) close(fd_);
   }
   bool ok() const { return ok_; }
@@ -164,6 +164,7 @@ class FastqGpu {
   uint64_t fsize_ = 0, piece_ = 0, carry_ = 0, chunk_ = 0;
   char *buf_[2] = {nullptr, nullptr};  // pinned region buffers (IBWA_FQ_MMAP=0)
   const char *map_ = nullptr;         // the mapped file
+  uint64_t map_lo_ = 0;               // ... still mapped from this offset on (consumed regions are unmapped)
   bool ok_ = false, handoff_ = false;
   uint64_t handoff_off_ = 0;
   int cur_ = 0;                 // buffer of the region being parsed
@@ -451,7 +452,14 @@ class FastqGpu {
     const int nb = cur_ ^ 1;
     if (map_) {
       const uint64_t pg = 4096, a = tail_file_off_ / pg * pg, e = file_rewind / pg * pg;
-      if (e > a) madvise(const_cast<char *>(map_) + a, e - a, MADV_DONTNEED);
+      // unmapped, not only dropped: the page tables of 12 GB of mapping cost ~0.1 s at exit
+      // (profiles/r05_e2e_i.json, IBWA_ALN_EXIT_PROBE)
+      if (e > a && a == map_lo_) {
+        munmap(const_cast<char *>(map_) + a, e - a);
+        map_lo_ = e;
+      } else if (e > a) {
+        madvise(const_cast<char *>(map_) + a, e - a, MADV_DONTNEED);
+      }
     } else {
       memcpy(buf_[nb] + carry_ - carry, base + rewind, carry);
     }
