@@ -365,6 +365,7 @@ struct ibwa_ctx {
   DBuf d_cw, d_ptabg;
   DBuf d_rdump, d_roff;
   DBuf d_rdump2, c_wbuf, c_nN;  // gap_overlap: the second state buffer; the overlapped pass's own widths / N counts  // resume states (GapArgs::rdump) and per-read offsets
+  DBuf d_wbuf2, d_nN2, d_cw2;   // gap_overlap 1: the width rows of odd chunks (double-buffered)
   DBuf d_hpop;           // per read: first-pass pops before its resume state (0: none; ibwa_batch_diag 2)
   bool hpop_valid = false;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
@@ -673,7 +674,8 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
                   &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1], &c->c_dir, &c->c_free, &c->c_hits,
                   &c->c_next, &c->c_pool, &c->c_proot, &c->c_pstore, &c->c_recb, &c->c_stg, &c->d_cw, &c->d_feat,
                   &c->d_hpop, &c->d_ordi, &c->d_ordids, &c->d_ordk, &c->d_ordtmp, &c->d_ptabg, &c->d_rdump, &c->d_roff,
-                  &c->d_selst, &c->d_seltmp, &c->d_rdump2, &c->c_wbuf, &c->c_nN, &c->fq_codes, &c->fq_lenk, &c->fq_offk})
+                  &c->d_selst, &c->d_seltmp, &c->d_rdump2, &c->c_wbuf, &c->c_nN, &c->fq_codes, &c->fq_lenk, &c->fq_offk,
+                  &c->d_wbuf2, &c->d_nN2, &c->d_cw2})
     b->release();
   if (c->fqs) c->fqs->unref();
   for (auto &b : c->sw) b.release();
@@ -728,7 +730,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "diag") c->diag = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
-  else if (k == "gap_overlap") c->gap_overlap = value != 0;
+  else if (k == "gap_overlap" && value >= 0 && value <= 2) c->gap_overlap = (int)value;
   else if (k == "gap_overlap_chunks" && value >= 2 && value <= 64) c->gap_overlap_chunks = (int)value;
   else if (k == "gap_overlap_min" && value >= 1) c->gap_overlap_min = value;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
@@ -1482,6 +1484,16 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (int rc = c->d_cw.ensure(chunk * (uint64_t)cw_words * 4)) return rc;
       if (int rc = c->d_ptabg.ensure(lanes * GAP_MAX_PAGES * 2)) return rc;
     }
+    // gap_overlap 1: odd chunks' width rows in a second set, so chunk j's cooperative pass reads its
+    // own first pass's rows (gap_shadow updates included) while chunk j+1's k_width writes the other
+    // set; gap_overlap 2: one set, the overlapped pass runs its own k_width and replays gap_shadow
+    const bool dbl = ovl && c->gap_overlap == 1;
+    if (dbl) {
+      if (int rc = c->d_wbuf2.ensure(chunk * A.wstride * 8)) return rc;
+      if (int rc = c->d_nN2.ensure(chunk * 2 + 2)) return rc;
+      if (lw)
+        if (int rc = c->d_cw2.ensure(chunk * (uint64_t)cw_words * 4)) return rc;
+    }
     // resume states of the early hand-offs: per read 1 + the state's offset (0: none), then per state
     // buffer its fill counter and the count of states stored
     uint64_t rd_cap = 0;
@@ -1602,9 +1614,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         K.wb_base = -1;
         K.nN = c->c_nN.as<uint16_t>();
       } else {
-        K.wbuf = c->d_wbuf.as<uint2>();
+        K.wbuf = (dbl && p ? c->d_wbuf2 : c->d_wbuf).as<uint2>();
         K.wb_base = b0;
-        K.nN = c->d_nN.as<uint16_t>();
+        K.nN = (dbl && p ? c->d_nN2 : c->d_nN).as<uint16_t>();
       }
       K.stg = c->c_stg.as<uint4>();
       K.stg_log2 = stg_log2;
@@ -1706,11 +1718,13 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       B.n = cnt;
       B.off = A.off + b0;
       B.len = A.len + b0;
-      B.wbuf = c->d_wbuf.as<uint2>();
-      B.nN = c->d_nN.as<uint16_t>();
+      B.wbuf = (dbl && par ? c->d_wbuf2 : c->d_wbuf).as<uint2>();
+      B.nN = (dbl && par ? c->d_nN2 : c->d_nN).as<uint16_t>();
       GapArgs G = gap_args(c, A, o, b0, cnt);
+      G.wbuf = B.wbuf;
+      G.nN = B.nN;
       if (lw) {
-        B.cw = c->d_cw.as<uint32_t>();
+        B.cw = (dbl && par ? c->d_cw2 : c->d_cw).as<uint32_t>();
         B.cw_words = cw_words;
         B.cw_rw = cw_rw;
         G.cw = B.cw;
@@ -1810,7 +1824,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
           have_pending = false;
         }
         hipEvent_t evs[4] = {c->ev2[0], c->ev2[1], c->ev2[2], c->ev2[3 + par]};
-        if (int rc = coop_launch(b0, cnt, par, c->stream2, evs, true, pending)) return rc;
+        if (int rc = coop_launch(b0, cnt, par, c->stream2, evs, !dbl, pending)) return rc;
         have_pending = true;
       }
     }

@@ -142,20 +142,22 @@ def test_exact_reads_round_trip(mid_genome):
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "coop_pool_pages": 256}),
     ([], 100, 0.01, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4, "gap_resume": 0}),
     # each chunk's cooperative pass over its resumed reads on a second stream while the next chunk's
-    # first pass runs (gap_overlap: two state buffers; the pass recomputes its reads' widths and
-    # replays gap_shadow from the states), in 3 chunks, under several options and a state buffer too
-    # small for some states
+    # first pass runs (two state buffers; gap_overlap 1: two sets of width rows, the pass reads its
+    # chunk's own; 2: the pass recomputes its reads' widths and replays gap_shadow from the states),
+    # in 3-4 chunks, under several options and a state buffer too small for some states
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 5_000,
                              "gap_overlap_chunks": 3}),
-    ([], 150, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 2_000,
+    ([], 150, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 2, "gap_overlap_min": 2_000,
                              "gap_overlap_chunks": 3}),
     (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4,
                                                            "gap_overlap": 1, "gap_overlap_min": 2_000,
                                                            "gap_overlap_chunks": 3}),
-    (["-m", "300"], 100, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 2_000,
+    (["-m", "300"], 100, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 2, "gap_overlap_min": 2_000,
                                         "gap_overlap_chunks": 3}),
-    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 5_000,
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 2, "gap_overlap_min": 5_000,
                              "gap_overlap_chunks": 3, "gap_resume_records": 8_000}),
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 5_000,
+                             "gap_overlap_chunks": 4, "gap_resume_records": 8_000}),
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 5_000,
                              "gap_overlap_chunks": 4, "coop_pool_gb": 1})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
