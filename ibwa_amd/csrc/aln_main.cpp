@@ -19,6 +19,7 @@
 #include <zlib.h>
 
 #include <chrono>
+#include <cmath>
 #include <functional>
 #include <algorithm>
 #include <string>
@@ -392,25 +393,46 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   // -> 5.96 s at 50 M reads, profiles/r05_e2e_b.json); 3 GiB pieces need ~274 GB at 2 lanes
   const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
   {
-    // The default arena follows the inputs, from what round 5 measured of the engine's buffers
-    // (IBWA_ARENA_TRACE=1 lists every carve: profiles/r05_arena_trace.log, 100 bp reads in 2 GiB
-    // pieces, 2 lanes): the index structures (relaid-out BWT, bit planes, K-mer tables of K <= 14:
-    // ~7.4x the two .bwt files at GRCh37 size); per lane ~22.6 GB per GiB of FASTQ its group holds
-    // (resume states 12.5, widths 8.7, compressed widths and per-read arrays 1.4) plus ~32 GB that
-    // do not grow with the group (first-pass slots 12.9, page pools 4.8, cooperative pool 10.7 --
-    // 17.2 above 128 bp -- and staging 3.2; fewer for a small group, whose grids are smaller); the
-    // ingest scratch ~1.7x a piece and per ingest slot ~0.75x a piece.  At most kArenaMaxGb.
+    // The default arena follows the inputs, calibrated on what round 5 measured (GiB; IBWA_ARENA_TRACE=1
+    // lists every carve, profiles/r05_arena_trace.log): the index structures (relaid-out BWT, bit
+    // planes, K-mer tables of K <= 14: ~7.5x the two .bwt files); per lane a part that does not grow
+    // with its group (first-pass slots, page pools, cooperative pool and staging: ~30, ~36 above
+    // 128 bp with the larger pool; less for a small group, whose grids are smaller) plus a part per
+    // GiB of FASTQ the group holds (resume states, width rows, per-read arrays: ~21.5 at 100 bp; ~16
+    // at 150 bp -- fewer reads per GiB -- plus room for the resume states to grow after the first
+    // group); the ingest scratch ~1.7x and each ingest slot ~0.8x a region's piece.  Measured peaks:
+    // 169 GiB at 100 bp in 1.94 GiB groups (r05_e2e_h.json), 147 GiB at 150 bp in 1.58 GiB groups
+    // (r05_pipe_full_v2.json).  An arena larger than the need makes the next process wait for the
+    // driver to wipe it (~33 GB/s).  At most kArenaMaxGb.
     auto fbytes = [](const std::string &f) -> double {
       struct stat st;
       return stat(f.c_str(), &st) == 0 ? (double)st.st_size : 0.0;
     };
     const double GiB = (double)(1u << 30);
     const bool gz = fq_path && !FastqGpu::usable(fq_path) && strcmp(fq_path, "-") != 0;
-    // FASTQ bytes of one GPU's group: a piece of the file, or (host readers) up to kGroup batches
+    // FASTQ bytes of one GPU's group: a region's piece (equal regions of at most `piece` per GPU, as
+    // FastqGpu cuts them), or (host readers) up to kGroup batches
     const double fq = fq_path ? fbytes(fq_path) * (gz ? 4.0 : 1.0) : 0.0;
-    const double grp = std::min(fq / n_gpus, fq_dev ? (double)piece : (double)kGroup * kSub * 300.0) / GiB;
-    const double need_gb = 8.0 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
-                           n_lanes * (std::min(36.0, 72.0 * grp) + 23.0 * grp) + 1.7 * grp + (n_lanes + 3) * 0.8 * grp + 2.0;
+    double grp_b = (double)kGroup * kSub * 300.0;
+    if (fq_dev) {
+      const double per = (double)piece * n_gpus, n_reg = std::max(1.0, std::ceil(fq / per));
+      grp_b = std::min(per, fq / n_reg) / n_gpus;
+    }
+    const double grp = std::min(fq / n_gpus, grp_b) / GiB;
+    // the read length from the first record (plain FASTQ): longer reads take the larger pool
+    int first_len = 0;
+    if (fq_path && !gz && strcmp(fq_path, "-") != 0)
+      if (FILE *f = fopen(fq_path, "rb")) {
+        char line[4096];
+        if (fgets(line, sizeof line, f) && line[0] == '@' && fgets(line, sizeof line, f))
+          first_len = (int)strcspn(line, "\r\n");
+        fclose(f);
+      }
+    const bool long_reads = first_len == 0 || first_len > 128;
+    const double fixed = long_reads ? 36.0 : 30.0, per_gib = long_reads ? 20.0 : 21.5;
+    const double need_gb = 7.5 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
+                           n_lanes * (std::min(fixed, 2.0 * fixed * grp) + per_gib * grp) + 1.7 * grp +
+                           (n_lanes + 3) * 0.8 * grp + 2.0;
     const char *ag = getenv("IBWA_ARENA_GB");
     std::vector<std::thread> th;
     std::vector<int> rc(n_used, 0);
