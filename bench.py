@@ -540,7 +540,7 @@ def sw_leg(eng, refs, reads, do_cpu, steps=3):
     out["value"] = n / (out["full_kernel_ms"] * 1e-3)
     out["unit"] = "alignments/s"
     # the VALU work per alignment measured by SQ_INSTS_VALU on this workload shape (the latest
-    # profiles/*_sw_pmc.json, tools/r03_sw_pmc.sh) over the live kernel time: whole k_sw
+    # profiles/*_sw_pmc.json, tools/sessions/r03_sw_pmc.sh) over the live kernel time: whole k_sw
     # Only a counter file of this build (its build_id) and of this workload shape counts; otherwise the
     # forward-pass estimate below stands in.
     import glob

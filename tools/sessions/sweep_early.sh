@@ -1,7 +1,7 @@
 #!/bin/bash
 # Sweep engine options on the gapped bench (one step after one warm-up, no CPU legs).
-# usage: tools/sweep_early.sh <reads> "<key=val,key=val...>" ...   (an empty config is the default)
-#   e.g. tools/sweep_early.sh 10000000 "" "gap_early_iters=2000,gap_early_entries=500" "gap_reads_per_chunk=16777216"
+# usage: tools/sessions/sweep_early.sh <reads> "<key=val,key=val...>" ...   (an empty config is the default)
+#   e.g. tools/sessions/sweep_early.sh 10000000 "" "gap_early_iters=2000,gap_early_entries=500" "gap_reads_per_chunk=16777216"
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
