@@ -1651,10 +1651,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         HIPCHK(launch_width(B, c->block, st));
       }
       HIPCHK(hipEventRecord(evs[2], st));
-      // its own claim counter: the first pass of the next chunk claims with d_counter[0] meanwhile
       K.fix_status = c->d_status.as<uint32_t>();  // resume_fixup, as each read ends
       K.fix_roff = c->d_roff.as<uint64_t>();
-      HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>() + (own_widths ? 6 : 0), blocks, st));
+      // overlapped (stream2): its own claim counter -- the first pass of the next chunk claims with
+      // d_counter[0] meanwhile (sharing it lost and duplicated reads at 50 M reads, r05_sweep_ovl2.jsonl)
+      HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>() + (st != c->stream ? 6 : 0), blocks, st));
       HIPCHK(hipEventRecord(evs[1], st));
       return 0;
     };
