@@ -1381,17 +1381,46 @@ int sampe_main(int argc, char *argv[]) {
   // GPU, and (-R) its .remap table when it has one
   S.dbs.db.resize(count);
   S.cache.resize(count);
+  // the host side (.ann / .amb / .pac, .remap tables) on a thread while the GPU takes the indexes
+  std::vector<int> host_ok(count, 0);
+  std::thread host_side([&]() {
+    for (int d = 0; d < count; ++d) {
+      RefDb &r = S.dbs.db[d];
+      if (!bns_restore(prefixes[d], r.bns)) return;
+      host_ok[d] = 1;
+      if (S.popt.remapping)  // seq_restore (dbset.c:81-101)
+        r.remap = load_remappings(prefixes[d] + ".remap", r.bns.n_seqs, r.mappings);
+      host_ok[d] = 2;
+    }
+  });
+  int gpu_rc = 0;
+  for (int d = 0; d < count && !gpu_rc; ++d) {
+    const std::string &prefix = prefixes[d];
+    ibwa_ctx_t *cx = nullptr;
+    if (ibwa_ctx_create(0, &cx)) { gpu_rc = 1; break; }
+    S.ctx.push_back(cx);
+    if (ibwa_ctx_load_bwt_file(cx, 0, (prefix + ".bwt").c_str()) || ibwa_ctx_load_bwt_file(cx, 1, (prefix + ".rbwt").c_str()))
+      gpu_rc = 2;
+    else if (ibwa_ctx_load_sa_file(cx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(cx, 1, (prefix + ".rsa").c_str()))
+      gpu_rc = 3;
+    else if (ibwa_ctx_expand_sa(cx))
+      gpu_rc = 4;
+  }
+  host_side.join();
+  if (gpu_rc == 1) return die("ibwa_ctx_create");
+  if (gpu_rc == 2) return die("load .bwt / .rbwt");
+  if (gpu_rc == 3) return die("load .sa / .rsa");
+  if (gpu_rc == 4) return die("expand SA");
   for (int d = 0; d < count; ++d) {
     RefDb &r = S.dbs.db[d];
     const std::string &prefix = prefixes[d];
-    if (!bns_restore(prefix, r.bns)) {
+    if (host_ok[d] < 1) {
       fprintf(stderr, "[ibwa-amd sampe] cannot read %s.ann / .amb / .pac\n", prefix.c_str());
       return 1;
     }
     r.offset = S.dbs.l_pac;
     S.dbs.l_pac += (uint64_t)r.bns.l_pac;
-    if (S.popt.remapping) {  // seq_restore (dbset.c:81-101)
-      r.remap = load_remappings(prefix + ".remap", r.bns.n_seqs, r.mappings);
+    if (S.popt.remapping) {
       if (r.remap < 0) {
         fprintf(stderr, "Fatal error loading sequence mappings from %s\n", (prefix + ".remap").c_str());
         return 1;
@@ -1399,14 +1428,6 @@ int sampe_main(int argc, char *argv[]) {
         fprintf(stderr, " - Remapping enabled for sequence %s\n", prefix.c_str());
       }
     }
-    ibwa_ctx_t *cx = nullptr;
-    if (ibwa_ctx_create(0, &cx)) return die("ibwa_ctx_create");
-    S.ctx.push_back(cx);
-    if (ibwa_ctx_load_bwt_file(cx, 0, (prefix + ".bwt").c_str()) || ibwa_ctx_load_bwt_file(cx, 1, (prefix + ".rbwt").c_str()))
-      return die("load .bwt / .rbwt");
-    if (ibwa_ctx_load_sa_file(cx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(cx, 1, (prefix + ".rsa").c_str()))
-      return die("load .sa / .rsa");
-    if (ibwa_ctx_expand_sa(cx)) return die("expand SA");
   }
   S.rnd.seed((long)S.dbs.db[0].bns.seed);  // srand48(dbs->db[0]->bns->bns->seed), bwape.c:471
   S.rg_id = rg_id.empty() ? nullptr : rg_id.c_str();

@@ -19,6 +19,7 @@
 
 #include <memory>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -40,19 +41,28 @@ int run_samse(Reader &rd, FILE *fp_sa, const ibwa_gap_opt_t &opt, const std::str
   Dbs dbs;  // samse: a set of one reference (dbset_restore, dbset.c:135)
   dbs.db.resize(1);
   Bns &b = dbs.db[0].bns;
-  if (!bns_restore(prefix, b)) {
+  // the host's .ann / .amb / .pac on a thread while the GPU takes the index
+  bool b_ok = false;
+  std::thread host_side([&]() { b_ok = bns_restore(prefix, b); });
+  ibwa_ctx_t *ctx = nullptr;
+  int gpu_rc = ibwa_ctx_create(0, &ctx) ? 1 : 0;
+  if (!gpu_rc && (ibwa_ctx_load_bwt_file(ctx, 0, (prefix + ".bwt").c_str()) ||
+                  ibwa_ctx_load_bwt_file(ctx, 1, (prefix + ".rbwt").c_str())))
+    gpu_rc = 2;
+  if (!gpu_rc && (ibwa_ctx_load_sa_file(ctx, 0, (prefix + ".sa").c_str()) ||
+                  ibwa_ctx_load_sa_file(ctx, 1, (prefix + ".rsa").c_str())))
+    gpu_rc = 3;
+  if (!gpu_rc && ibwa_ctx_expand_sa(ctx)) gpu_rc = 4;
+  host_side.join();
+  if (gpu_rc == 1) return die("ibwa_ctx_create");
+  if (gpu_rc == 2) return die("load .bwt / .rbwt");
+  if (gpu_rc == 3) return die("load .sa / .rsa");
+  if (gpu_rc == 4) return die("expand SA");
+  if (!b_ok) {
     fprintf(stderr, "[ibwa-amd samse] cannot read %s.ann / .amb / .pac\n", prefix.c_str());
     return 1;
   }
   dbs.l_pac = (uint64_t)b.l_pac;
-  ibwa_ctx_t *ctx = nullptr;
-  if (ibwa_ctx_create(0, &ctx)) return die("ibwa_ctx_create");
-  if (ibwa_ctx_load_bwt_file(ctx, 0, (prefix + ".bwt").c_str()) ||
-      ibwa_ctx_load_bwt_file(ctx, 1, (prefix + ".rbwt").c_str()))
-    return die("load .bwt / .rbwt");
-  if (ibwa_ctx_load_sa_file(ctx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(ctx, 1, (prefix + ".rsa").c_str()))
-    return die("load .sa / .rsa");
-  if (ibwa_ctx_expand_sa(ctx)) return die("expand SA");
   Drand48 rnd;
   rnd.seed((long)b.seed);  // srand48(bns->seed), bwase.c:662
   Out o{out, {}};
