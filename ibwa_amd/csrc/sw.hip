@@ -384,7 +384,9 @@ __global__ void __launch_bounds__(256) k_sw(SwArgs A, unsigned long long *counte
       score = score_f;
       if (score_f >= 1 && end_i > 0 && end_j > 0 && A.stop_after != 1) {
         // ---- reverse pass (stdaln.c:639-696) in the adaptive band
-        for (int i = 0; i <= end_i; ++i) L.v(eEH + i) = 0;
+        // eh[0 .. end_i] = 0 by 16 B stores (up to 3 words past end_i as well: whole blocks of the
+        // row, never read by a cell -- a cell i <= start < end_i reads eh[i] and eh[i + 1] only)
+        for (int q = 0; q <= end_i / 4; ++q) L.v4((uint32_t)q) = make_uint4(0u, 0u, 0u, 0u);
         int score_r = sm(a[end_i - 1], b[end_j - 1]);
         int start_i = end_i, start_j = end_j;
         L.v(eEH + end_i) = (uint32_t)(QR + score_r) << 16;
