@@ -474,15 +474,17 @@ def e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns):
             if m_:
                 out["arena_gb"], out["arena_peak_use_gb"] = float(m_.group(1)), float(m_.group(2))
         load = phases.get("load index", 0.0)
-        arena = phases.get("device arena", 0.0)
+        # the device arena's phase; until round 5 it also held the GPU runtime's start-up, now its own
+        arena = phases.get("device arena", 0.0) + phases.get("gpu runtime start", 0.0)
         out.update({"wall_s": wall, "phases_s": phases, "value": n / max(wall - load - arena, 1e-9), "unit": "reads/s",
                     "value_excl_index_load_only": n / max(wall - load, 1e-9),
                     "value_incl_setup": n / wall,
                     "note": "wall clock of the child process (start-up, FASTQ parse, alignment, .sai writes, exit); "
                             "`value` excludes its 'load index' phase (.bwt/.rbwt read and relaid out on the GPU) and "
-                            "its 'device arena' phase (HIP start-up and the one device reservation, which here waits "
-                            "for the driver to wipe the ~220 GB this bench process released just before: a few ms "
-                            "on a fresh box, tools/alloc_bench.cpp); value_incl_setup counts everything"})
+                            "its 'gpu runtime start' and 'device arena' phases (HIP start-up and the one device "
+                            "reservation, which here waits for the driver to take back the ~200 GB this bench process "
+                            "released just before: a few ms on a fresh box, tools/alloc_bench.cpp); "
+                            "value_incl_setup counts everything"})
         t = time.perf_counter()
         first_bad = L.ibwa_sai_diff(sai.encode(), n, np.ascontiguousarray(n_aln, dtype=np.int32).ctypes.data,
                                     np.ascontiguousarray(alns).ctypes.data)

@@ -390,20 +390,10 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
   const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
   // 2 GiB per GPU (~8 M reads of 100 bp): fewer, larger groups than 1 GiB pieces (align phase 6.12-6.2
-  // vs 5.71-5.79 s at 50 M reads, profiles/r05_e2e_i.json); 2.5 and 3 GiB measured no faster.  An
-  // input that 2 GiB pieces would cut into at most one group per lane (10 M reads of 150 bp: two
-  // 1.7 GB groups) is cut into two groups per lane instead: the lanes run their groups side by side
-  // either way, and the smaller groups keep the process under ~144 GB, so that a second `aln` run
-  // right after it (the other end of a pair) finds clean memory instead of waiting seconds for the
-  // driver to wipe what this one used (profiles/r05_pipe_full_v2.json: 5.98 s)
-  uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
-  if (!(pm && atoll(pm) > 0) && fq_dev) {
-    struct stat st;
-    const uint64_t fs = stat(fq_dev, &st) == 0 ? (uint64_t)st.st_size : 0;
-    const uint64_t per_lane = (uint64_t)n_lanes * (uint64_t)n_gpus;
-    if (fs > 0 && fs <= piece * per_lane)
-      piece = std::max<uint64_t>((uint64_t)256 << 20, (fs + 2 * per_lane - 1) / (2 * per_lane));
-  }
+  // vs 5.71-5.79 s at 50 M reads, profiles/r05_e2e_i.json); 2.5 and 3 GiB measured no faster.  (Cutting
+  // a small input into two groups per lane kept a 10 M-read 150 bp run at 131 instead of 157 GB but
+  // cost 6 % of its align phase, and the next process waited as long: r05_pipe_full_v3.json.)
+  const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
   {
     // The default arena follows the inputs, calibrated on what round 5 measured (GiB; IBWA_ARENA_TRACE=1
     // lists every carve, profiles/r05_arena_trace.log): the index structures (relaid-out BWT, bit
@@ -449,6 +439,11 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     std::vector<std::thread> th;
     std::vector<int> rc(n_used, 0);
     std::vector<double> want_gb(n_used, 0.0), ms(n_used, 0.0);
+    {  // HIP start-up (device enumeration, the driver's process state) apart from the reservation
+      uint64_t fr = 0, tot = 0;
+      (void)ibwa_device_memory(0, &fr, &tot);
+      ph.mark("gpu runtime start");
+    }
     for (int d = 0; d < n_used; ++d)
       th.emplace_back([&, d]() {
         const auto t0 = std::chrono::steady_clock::now();
