@@ -632,22 +632,41 @@ inline int approx_mapQ(const Read &p, int mm) {
 
 // bwa_cal_md1 (bwase.c:243-295)
 inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, const Dbs &b, int *nm_out) {
+  // the reference bases of a CIGAR run are extracted at once (extract(x, n) == n one-base extracts:
+  // both stop at l_pac and cross references the same way), the numbers formatted in place
   std::string str;
-  char buf[32];
+  str.reserve(32);
+  auto put_int = [&str](int v) {
+    char t[12];
+    char *e = t + sizeof t, *q = e;
+    unsigned u = (unsigned)v;
+    do {
+      *--q = (char)('0' + u % 10);
+      u /= 10;
+    } while (u);
+    str.append(q, (size_t)(e - q));
+  };
+  thread_local std::vector<uint8_t> rb;
   uint64_t x = pos, y = 0;
   const uint64_t l_pac = b.l_pac;
   int u = 0, nm = 0;
   uint8_t c = 0;
+  auto run = [&](uint64_t at, int l) -> int {  // the bases of [at, at + l) before l_pac, into rb
+    if ((int)rb.size() < l) rb.resize((size_t)l);
+    if (at >= l_pac || l <= 0) return 0;
+    const uint64_t n = std::min<uint64_t>((uint64_t)l, l_pac - at);
+    return (int)extract(b, at, (uint32_t)n, rb.data());
+  };
   if (s.has_cigar) {
     for (uint32_t cg : s.cigar) {
       const int l = (int)cig_len(cg);
       const uint32_t op = cig_op(cg);
       if (op == FROM_M) {
-        for (int z = 0; z < l && x + z < l_pac; ++z) {
-          extract(b, x + z, 1, &c);
+        const int n = run(x, l);
+        for (int z = 0; z < n; ++z) {
+          c = rb[z];
           if (c > 3 || seq[y + z] > 3 || c != seq[y + z]) {
-            snprintf(buf, sizeof buf, "%d", u);
-            str += buf;
+            put_int(u);
             str += "ACGTN"[c];
             ++nm;
             u = 0;
@@ -660,11 +679,11 @@ inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, cons
         y += l;
         if (op == FROM_I) nm += l;
       } else if (op == FROM_D) {
-        snprintf(buf, sizeof buf, "%d", u);
-        str += buf;
+        put_int(u);
         str += '^';
-        for (int z = 0; z < l && x + z < l_pac; ++z) {
-          extract(b, x + z, 1, &c);
+        const int n = run(x, l);
+        for (int z = 0; z < n; ++z) {
+          c = rb[z];
           str += "ACGT"[c];
         }
         u = 0;
@@ -672,11 +691,12 @@ inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, cons
       }
     }
   } else {
+    // past l_pac nothing is extracted: c keeps the last base's value (as the reference)
+    const int n = run(x, s.len);
     for (int z = 0; z < s.len; ++z) {
-      extract(b, x + z, 1, &c);  // past l_pac nothing is written: c keeps its value (as the reference)
+      if (z < n) c = rb[z];
       if (c > 3 || seq[y + z] > 3 || c != seq[y + z]) {
-        snprintf(buf, sizeof buf, "%d", u);
-        str += buf;
+        put_int(u);
         str += "ACGTN"[c];
         ++nm;
         u = 0;
@@ -685,8 +705,7 @@ inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, cons
       }
     }
   }
-  snprintf(buf, sizeof buf, "%d", u);
-  str += buf;
+  put_int(u);
   *nm_out = nm;
   return str;
 }
