@@ -906,13 +906,16 @@ inline int refine_gapped(ibwa_ctx_t *ctx, const Dbs &b, std::vector<Read *> &rea
     if (ibwa_global_batch(ctx, m, rbuf.data(), roff.data(), rlen.data(), qbuf.data(), qoff.data(), qlen.data(), 50, 5,
                           sc.data(), pl.data(), nc.data(), &c32, &tc))
       return -1;
-    int64_t q0 = 0;
-    for (int64_t k = 0; k < m; ++k) {
-      Refine &j = jobs[k];
-      if (j.q) refine_finish(b, j, c32 + q0, nc[k], j.s->len, &j.q->pos, j.q->cigar, &j.q->has_cigar);
-      else refine_finish(b, j, c32 + q0, nc[k], j.s->len, &j.s->pos, j.s->cigar, &j.s->has_cigar);
-      q0 += nc[k];
-    }
+    // the fix-ups on the host threads (each job writes its own read's or multi hit's fields)
+    std::vector<int64_t> q0(m + 1, 0);
+    for (int64_t k = 0; k < m; ++k) q0[k + 1] = q0[k] + nc[k];
+    parallel_chunks(m, [&](int64_t lo, int64_t hi, int) {
+      for (int64_t k = lo; k < hi; ++k) {
+        Refine &j = jobs[k];
+        if (j.q) refine_finish(b, j, c32 + q0[k], nc[k], j.s->len, &j.q->pos, j.q->cigar, &j.q->has_cigar);
+        else refine_finish(b, j, c32 + q0[k], nc[k], j.s->len, &j.s->pos, j.s->cigar, &j.s->has_cigar);
+      }
+    });
     ibwa_free(c32);
   }
   parallel_chunks((int64_t)reads.size(), [&](int64_t lo, int64_t hi, int) {
