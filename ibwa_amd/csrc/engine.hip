@@ -86,6 +86,12 @@ struct Arena {
   bool owns(const void *p) const {
     return base && static_cast<const char *>(p) >= base && static_cast<const char *>(p) < base + size;
   }
+  char *released_base = nullptr;  // ibwa_release: the range handed back (buffers in it are dropped)
+  size_t released_size = 0;
+  bool was_released(const void *p) const {
+    return released_base && static_cast<const char *>(p) >= released_base &&
+           static_cast<const char *>(p) < released_base + released_size;
+  }
   void release(void *p, size_t n) {
     n = (n + 4095) & ~(size_t)4095;
     std::lock_guard<std::mutex> lk(mu);
@@ -166,6 +172,11 @@ struct DBuf {
     return 0;
   }
   static void free_dev(void *q, size_t n) {
+    for (Arena &a : g_arena)
+      if (a.was_released(q)) {  // its arena was handed back (ibwa_release): nothing left to free
+        dev_bytes_add(-(int64_t)n);
+        return;
+      }
     for (Arena &a : g_arena)
       if (a.owns(q)) {
         // the range may still be used by work queued on the owning context's stream (the API call
@@ -615,6 +626,24 @@ int ibwa_reserve(int device, uint64_t bytes) {
   a.base = static_cast<char *>(p);
   a.size = want;
   a.free_[0] = want;
+  return 0;
+}
+
+int ibwa_release(int device) {
+  if (device < 0 || device >= MAX_DEV) return fail(IBWA_EINVAL, "device %d out of range", device);
+  Arena &a = g_arena[device];
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (!a.base) return 0;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipFree(a.base));
+  // the range is gone: buffers still pointing into it are neither used nor freed again (free_dev
+  // finds no owning arena and skips pointers that were carved: released_ marks them)
+  a.released_base = a.base;
+  a.released_size = a.size;
+  a.base = nullptr;
+  a.size = a.used = 0;
+  a.free_.clear();
   return 0;
 }
 

@@ -88,6 +88,7 @@ CAPI = {
     "ibwa_fq_stats": (_i, [_vp, c.POINTER(c.c_int64), c.POINTER(c.c_double)]),
     "ibwa_fq_offset": (_i, [_vp, c.c_int64, c.POINTER(c.c_uint64)]),
     "ibwa_fq_share_scratch": (_i, [_vp, _vp]),
+    "ibwa_release": (_i, [_i]),
     "ibwa_batch_fetch_sai": (_i, [_vp, _vp, c.c_uint64, c.POINTER(c.c_uint64), c.POINTER(c.c_int64)]),
     "ibwa_batch_stage_fq": (_i, [_vp, _vp, c.c_int64, c.c_int64, _i]),
     "ibwa_host_alloc": (_i, [c.c_uint64, c.POINTER(_vp)]),

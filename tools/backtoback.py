@@ -30,6 +30,9 @@ def aln(env, out):
         sys.exit(f"aln failed: {err[-1000:]}")
     ph = {}
     for ln in err.splitlines():
+        m = re.search(r"arenas released in ([\d.]+) ms", ln)
+        if m:
+            ph["release_ms"] = float(m.group(1))
         if "wall s:" in ln:
             for name, v in re.findall(r"([a-z][a-z .()]*?) (\d+\.\d+)", ln.split("wall s:", 1)[1]):
                 ph[name.strip()] = float(v)
@@ -39,7 +42,7 @@ def aln(env, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--arena-gb", default="118")
-    ap.add_argument("--cases", default="fast,clean,sleep2,fast")
+    ap.add_argument("--cases", default="fast,clean,sleep2,release,fast")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
     base = {"IBWA_ARENA_GB": a.arena_gb}
@@ -47,6 +50,8 @@ def main():
         first = dict(base)
         if case == "clean":
             first["IBWA_ALN_CLEAN_EXIT"] = "1"
+        if case == "release":
+            first["IBWA_ALN_RELEASE"] = "1"
         w1, p1 = aln(first, os.path.join(tmp, "a.sai"))
         if case == "sleep2":
             time.sleep(2.0)
