@@ -390,10 +390,22 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
   const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
   // 2 GiB per GPU (~8 M reads of 100 bp): fewer, larger groups than 1 GiB pieces (align phase 6.12-6.2
-  // vs 5.71-5.79 s at 50 M reads, profiles/r05_e2e_i.json); 2.5 and 3 GiB measured no faster.  (Cutting
-  // a small input into two groups per lane kept a 10 M-read 150 bp run at 131 instead of 157 GB but
-  // cost 6 % of its align phase, and the next process waited as long: r05_pipe_full_v3.json.)
-  const uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
+  // vs 5.71-5.79 s at 50 M reads, profiles/r05_e2e_i.json); 2.5 and 3 GiB measured no faster.  An
+  // input that 2 GiB pieces would cut into at most one group per lane (10 M reads of 150 bp: two
+  // 1.7 GB groups) is cut into two groups per lane instead: the lanes run their groups side by side
+  // either way, and the process stays under ~128 GiB (124 vs 146 GiB for that input, align +6 %,
+  // r05_pipe_full_v{2,3}.json) -- so that both ends of a pair can be aligned at once on one GPU.
+  // (Back to back, the second process waits for the driver to wipe the first one's memory whatever
+  // its size: the wipe runs on the copy engine that also clears the new allocation,
+  // profiles/r05_b2b*.jsonl.)
+  uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
+  if (!(pm && atoll(pm) > 0) && fq_dev) {
+    struct stat st;
+    const uint64_t fs = stat(fq_dev, &st) == 0 ? (uint64_t)st.st_size : 0;
+    const uint64_t per_lane = (uint64_t)n_lanes * (uint64_t)n_gpus;
+    if (fs > 0 && fs <= piece * per_lane)
+      piece = std::max<uint64_t>((uint64_t)256 << 20, (fs + 2 * per_lane - 1) / (2 * per_lane));
+  }
   {
     // The default arena follows the inputs, calibrated on what round 5 measured (GiB; IBWA_ARENA_TRACE=1
     // lists every carve, profiles/r05_arena_trace.log): the index structures (relaid-out BWT, bit

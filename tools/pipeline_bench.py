@@ -49,6 +49,24 @@ def run(argv, stdout=None, timeout=1200):
     return dt
 
 
+def run_both(argvs, timeout=1200):
+    """Both commands at once (the two ends' aln on one GPU); wall of the pair and of each."""
+    t = time.perf_counter()
+    ps = [subprocess.Popen(a, stderr=subprocess.PIPE) for a in argvs]
+    walls, errs = [], []
+    for p_ in ps:
+        _, err = p_.communicate(timeout=timeout)
+        walls.append(time.perf_counter() - t)
+        errs.append(err.decode(errors="replace"))
+        if p_.returncode != 0:
+            raise RuntimeError(f"failed ({p_.returncode}): {errs[-1][-1500:]}")
+    for a, err in zip(argvs, errs):
+        for ln in err.splitlines():
+            if "wall s:" in ln or "[ibwa-amd aln]" in ln:
+                log(f"  {os.path.basename(a[0])} {a[1]} (concurrent): {ln}")
+    return time.perf_counter() - t, walls
+
+
 def write_fasta(path, ascii_, lens):
     with open(path, "wb") as f:
         o = 0
@@ -124,6 +142,7 @@ def main():
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--sub", type=float, default=0.02)
     ap.add_argument("--threads", type=int, default=bench.host_threads())
+    ap.add_argument("--concurrent-ends", type=int, default=1, help="also align the two ends at once (one GPU)")
     ap.add_argument("--out", default="")
     ap.add_argument("--diag", action="store_true", help="only run `aln` on the sample's end 2 with IBWA_VERBOSE")
     a = ap.parse_args()
@@ -162,10 +181,22 @@ def main():
     # ---- ibwa-amd over all pairs
     sai = [os.path.join(tmp, f"r{e}.sai") for e in (1, 2)]
     res["aln_s"] = [run([CLI, "aln", "-f", sai[e], P, fq[e]]) for e in (0, 1)]
+    if a.concurrent_ends:
+        # both ends' aln at once on the one GPU (each process under ~128 GiB): no process waits for
+        # the memory the other one released; the .sai must equal the sequential runs'
+        time.sleep(8.0)  # the sequential runs' memory wiped first
+        csai = [os.path.join(tmp, f"c{e}.sai") for e in (1, 2)]
+        pair_s, walls = run_both([[CLI, "aln", "-f", csai[e], P, fq[e]] for e in (0, 1)])
+        same = all(open(csai[e], "rb").read() == open(sai[e], "rb").read() for e in (0, 1))
+        res["aln_concurrent"] = {"pair_wall_s": pair_s, "walls_s": walls, "sai_equal_sequential": same}
+        log(f"ibwa-amd: both ends' aln at once: {pair_s:.2f} s for the pair (sequential {sum(res['aln_s']):.2f} s), "
+            f".sai equal {same}")
     res["sampe_s"] = run([CLI, "sampe", "-R", "-f", os.path.join(tmp, "pe.sam"), P, sai[0], sai[1], fq[0], fq[1]])
     res["samse_s"] = run([CLI, "samse", "-f", os.path.join(tmp, "se.sam"), P, sai[0], fq[0]])
     tot = sum(res["aln_s"]) + res["sampe_s"]
     res["pairs_per_s_aln_sampe"] = a.pairs / tot
+    if "aln_concurrent" in res:
+        res["pairs_per_s_aln_concurrent_sampe"] = a.pairs / (res["aln_concurrent"]["pair_wall_s"] + res["sampe_s"])
     log(f"ibwa-amd: aln {res['aln_s'][0]:.2f} + {res['aln_s'][1]:.2f} s, sampe -R {res['sampe_s']:.2f} s, "
         f"samse {res['samse_s']:.2f} s -> {res['pairs_per_s_aln_sampe']:.0f} pairs/s (aln x2 + sampe, files in/out)")
     # ---- the sample: ibwa-amd and the reference, SAM compared
