@@ -181,22 +181,22 @@ def main():
     # ---- ibwa-amd over all pairs
     sai = [os.path.join(tmp, f"r{e}.sai") for e in (1, 2)]
     res["aln_s"] = [run([CLI, "aln", "-f", sai[e], P, fq[e]]) for e in (0, 1)]
+    res["sampe_s"] = run([CLI, "sampe", "-R", "-f", os.path.join(tmp, "pe.sam"), P, sai[0], sai[1], fq[0], fq[1]])
+    res["samse_s"] = run([CLI, "samse", "-f", os.path.join(tmp, "se.sam"), P, sai[0], fq[0]])
     if a.concurrent_ends:
         # both ends' aln at once on the one GPU (each process under ~128 GiB): no process waits for
         # the memory the other one released; the .sai must equal the sequential runs'
-        time.sleep(8.0)  # the sequential runs' memory wiped first
+        time.sleep(8.0)  # the earlier runs' memory wiped first (the next GPU process waits for it)
         csai = [os.path.join(tmp, f"c{e}.sai") for e in (1, 2)]
         pair_s, walls = run_both([[CLI, "aln", "-f", csai[e], P, fq[e]] for e in (0, 1)])
         same = all(open(csai[e], "rb").read() == open(sai[e], "rb").read() for e in (0, 1))
         res["aln_concurrent"] = {"pair_wall_s": pair_s, "walls_s": walls, "sai_equal_sequential": same}
         log(f"ibwa-amd: both ends' aln at once: {pair_s:.2f} s for the pair (sequential {sum(res['aln_s']):.2f} s), "
             f".sai equal {same}")
-    res["sampe_s"] = run([CLI, "sampe", "-R", "-f", os.path.join(tmp, "pe.sam"), P, sai[0], sai[1], fq[0], fq[1]])
-    res["samse_s"] = run([CLI, "samse", "-f", os.path.join(tmp, "se.sam"), P, sai[0], fq[0]])
+        time.sleep(8.0)  # their memory wiped before the sample's runs below
     tot = sum(res["aln_s"]) + res["sampe_s"]
     res["pairs_per_s_aln_sampe"] = a.pairs / tot
-    if "aln_concurrent" in res:
-        res["pairs_per_s_aln_concurrent_sampe"] = a.pairs / (res["aln_concurrent"]["pair_wall_s"] + res["sampe_s"])
+
     log(f"ibwa-amd: aln {res['aln_s'][0]:.2f} + {res['aln_s'][1]:.2f} s, sampe -R {res['sampe_s']:.2f} s, "
         f"samse {res['samse_s']:.2f} s -> {res['pairs_per_s_aln_sampe']:.0f} pairs/s (aln x2 + sampe, files in/out)")
     # ---- the sample: ibwa-amd and the reference, SAM compared
