@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -97,20 +98,40 @@ struct Background {
   ~Background() { wait(); }
 };
 // wall-clock seconds per named phase, printed to stderr at the end of a command
+// (IBWA_PHASE_CPU=1: also the process's CPU seconds, all threads, per phase -- a worker's own only
+// when it is the only one running)
 struct Phases {
-  std::vector<std::pair<const char *, double>> acc;
+  std::vector<std::pair<const char *, double>> acc, cpu;
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  double c0 = cpu_now();
+  static double cpu_now() {
+    timespec ts;
+    clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+  }
+  static void add(std::vector<std::pair<const char *, double>> &v, const char *name, double dt) {
+    for (auto &a : v)
+      if (!strcmp(a.first, name)) { a.second += dt; return; }
+    v.push_back({name, dt});
+  }
   void mark(const char *name) {
     const auto t = std::chrono::steady_clock::now();
-    const double dt = std::chrono::duration<double>(t - t0).count();
+    add(acc, name, std::chrono::duration<double>(t - t0).count());
     t0 = t;
-    for (auto &a : acc)
-      if (!strcmp(a.first, name)) { a.second += dt; return; }
-    acc.push_back({name, dt});
+    static const bool want_cpu = getenv("IBWA_PHASE_CPU") != nullptr;
+    if (want_cpu) {
+      const double c = cpu_now();
+      add(cpu, name, c - c0);
+      c0 = c;
+    }
   }
   void print(const char *who) const {
     fprintf(stderr, "[%s] wall s:", who);
     for (auto &a : acc) fprintf(stderr, " %s %.2f", a.first, a.second);
+    fprintf(stderr, "\n");
+    if (cpu.empty()) return;
+    fprintf(stderr, "[%s] cpu s:", who);
+    for (auto &a : cpu) fprintf(stderr, " %s %.2f", a.first, a.second);
     fprintf(stderr, "\n");
   }
 };

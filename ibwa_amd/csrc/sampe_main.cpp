@@ -23,6 +23,14 @@
 // CIGAR of gapped hits, and the SAM prints the projected position with ZR:Z: the original.
 // Without -R the reference's select_sai_ibwa never sees a successful remap status and leaves every
 // read unmapped ("Failed to select primary alignment"); that is reproduced.
+//
+// `-G N` shards the batch loop (bwape.c:476-536) over N workers, worker w on GPU w mod the visible
+// devices (several on one device share its index): a worker takes the next batch of 0x40000 pairs
+// in file order and runs it whole.  What the reference carries from batch to batch is settled in
+// that order when the batch is taken -- the drand48 draws of its hit choice and the first use of each
+// wide interval (whose strand and read length the cached positions keep) -- or waited for: a batch
+// whose insert size cannot be inferred takes the previous batch's (bwape.c:410-411), and the SAM is
+// written batch by batch in file order.  The output does not depend on N.
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -31,7 +39,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -418,21 +429,56 @@ struct Source {
 };
 
 // ---------------------------------------------------------------- the batch loop (bwa_sai2sam_pe_core)
+// One shard of the batch loop (-G): its GPU contexts, one per reference, and what its batches work
+// in, kept from batch to batch.
+struct Worker {
+  std::vector<ibwa_ctx_t *> ctx;  // per reference: its index, SA -> coordinate
+  // bwtcache (bwtcache.c:27-45), one per reference: positions of an interval of >= 1000 rows, keyed
+  // by (k, l) only, computed with the strand and read length of the interval's first use in the run
+  std::vector<std::unordered_map<uint64_t, std::vector<uint64_t>>> cache;
+  // every pair's positions, per host thread; kept across batches (a batch holds ~10 M positions,
+  // 0.5 GB: allocating, faulting in and freeing that each batch cost about as much as filling it)
+  std::vector<std::vector<Position>> pstore;
+  std::unique_ptr<ibwa_ref_seq_t[]> sw_ref[2];  // paired_sw's bwa_seq_t mirrors per end (capacity kept)
+  std::unique_ptr<uint8_t[]> sw_rev[2];
+  size_t sw_ref_cap[2] = {0, 0}, sw_rev_cap[2] = {0, 0};
+  Phases ph;
+};
+
+// A batch of pairs (bwa_read_seq twice, bwape.c:466-468) with its .sai records and what its place
+// in the file settles: the drand48 decisions and the first uses of its wide intervals.
+struct Batch {
+  int64_t idx = 0;
+  std::vector<Read> seqs[2];
+  std::vector<Aln> flat[2];       // every read's alignments, one flat array per end
+  std::vector<size_t> offs[2];    // read i's at flat[offs[i] .. offs[i + 1])
+  std::vector<int> midx;          // select_rng per (pair, end) at 2 i + j: the main alignment
+  std::vector<double> rcache;     // and the draw that picks its row
+  // per reference: each interval of >= kMinHashWidth rows the batch uses -> (strand << 32 | read
+  // length) of its first use in the run (the cached positions are computed with those)
+  std::vector<std::unordered_map<uint64_t, uint64_t>> wide;
+};
+
 struct Sampe {
   Dbs dbs;
-  std::vector<ibwa_ctx_t *> ctx;  // one per reference (its index, SA -> coordinate)
+  std::vector<Worker> W;  // -G workers (at least one)
   std::vector<std::vector<const char *>> sai_fn;  // per reference: end 1, end 2
   PeOpt popt;
   ibwa_gap_opt_t gopt[2];
   std::vector<FILE *> fp_sai[2];  // per end, per reference
   std::vector<ibwa_aln1_t> sai_tmp[2];  // per end (the ends are read on two threads)
   Drand48 rnd;
-  Isize last_ii;
-  // bwtcache (bwtcache.c:27-45), one per reference: positions of an interval of >= 1000 rows,
-  // keyed by (k, l) only
-  std::vector<std::unordered_map<uint64_t, std::vector<uint64_t>>> cache;
+  // per reference: each wide interval's first use so far (in batch order, when a batch is taken)
+  std::vector<std::unordered_map<uint64_t, uint64_t>> first_use;
   const char *rg_id = nullptr;
-  Phases ph;
+  // batch-to-batch order between the workers: the insert size each batch settled on (for the next
+  // batch's fallback), the next batch to print, a failure anywhere
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<int64_t, Isize> ii_done;
+  int64_t printed = 0;
+  long tot = 0;
+  bool failed = false;
 
   int max_diff_of(const Read &r) const {
     return gopt[1].fnr > 0.0 ? ibwa_cal_maxdiff(r.len, 0.02, gopt[1].fnr) : gopt[1].max_diff;
@@ -509,8 +555,9 @@ struct Sampe {
   }
 
   // SA rows -> positions (bwtdb_sa2seq, dbset.c:240-246), one launch per reference
-  int sa2pos(const std::vector<int> &db, const std::vector<uint8_t> &st, const std::vector<uint32_t> &k,
+  int sa2pos(Worker &w, const std::vector<int> &db, const std::vector<uint8_t> &st, const std::vector<uint32_t> &k,
              const std::vector<uint32_t> &len, std::vector<uint64_t> &pos) {
+    const std::vector<ibwa_ctx_t *> &ctx = w.ctx;
     pos.assign(k.size(), 0);
     if (ctx.size() == 1) {  // one reference: the lists as they are
       if (!k.empty() && ibwa_sa2pos(ctx[0], (int64_t)k.size(), st.data(), k.data(), len.data(), dbs.db[0].offset, pos.data()))
@@ -611,33 +658,28 @@ struct Sampe {
 
   // The next batch of 0x40000 pairs (bwa_read_seq twice, bwape.c:466-468) and its .sai records,
   // end 1 and end 2 on two threads, in the background: the first batch while the index loads, each
-  // later one while the batch before it is processed.
-  std::vector<Read> nxt[2];
+  // later one while the batches before it are processed.
+  Batch nb;
+  size_t batch_pairs = 0x40000;  // IBWA_SAMPE_BATCH: other sizes are for tests (the SAM depends on it)
   double rd_s[2][2] = {{0, 0}, {0, 0}};  // per end: seconds reading reads, reading .sai records
-  std::vector<std::vector<Position>> pstore_;  // batch()'s per-thread position stores (capacity kept)
-  std::unique_ptr<ibwa_ref_seq_t[]> sw_ref_[2];  // paired_sw's bwa_seq_t mirrors per end (capacity kept)
-  std::unique_ptr<uint8_t[]> sw_rev_[2];
-  size_t sw_ref_cap_[2] = {0, 0}, sw_rev_cap_[2] = {0, 0};
-  std::vector<Aln> nflat[2];
-  std::vector<size_t> noff[2];
   bool nxt_ok[2] = {true, true};
   Background reader;
   void read_next(Source *src) {
     auto rd = [this, src](int j) {
       const auto t0 = std::chrono::steady_clock::now();
-      nxt[j].reserve(0x40000);
-      src[j].take(nxt[j], 0x40000, std::max(1, host_threads() / 2));
+      nb.seqs[j].reserve(batch_pairs);
+      src[j].take(nb.seqs[j], batch_pairs, std::max(1, host_threads() / 2));
       const auto t1 = std::chrono::steady_clock::now();
       // alngrp_create per read, in read order (saiset.c:45-76)
-      const size_t n = nxt[j].size();
-      nflat[j].clear();
-      nflat[j].reserve(n + n / 4);
-      noff[j].assign(n + 1, 0);
+      const size_t n = nb.seqs[j].size();
+      nb.flat[j].clear();
+      nb.flat[j].reserve(n + n / 4);
+      nb.offs[j].assign(n + 1, 0);
       nxt_ok[j] = true;
       for (size_t i = 0; i < n && nxt_ok[j]; ++i) {
-        noff[j][i] = nflat[j].size();
-        nxt_ok[j] = read_alns((int)j, nflat[j]);
-        noff[j][i + 1] = nflat[j].size();
+        nb.offs[j][i] = nb.flat[j].size();
+        nxt_ok[j] = read_alns((int)j, nb.flat[j]);
+        nb.offs[j][i + 1] = nb.flat[j].size();
       }
       const auto t2 = std::chrono::steady_clock::now();
       rd_s[j][0] += std::chrono::duration<double>(t1 - t0).count();
@@ -651,40 +693,148 @@ struct Sampe {
     reader.start([this, src]() { read_next(src); });
   }
 
+  // The next batch in file order into b (its buffers swapped with the reader's for reuse), with the
+  // decisions the reference makes in batch order; one worker at a time.  1: a batch, 0: the end, -1:
+  // an error.
+  int take(Source *src, Worker &w, Batch &b, int64_t idx) {
+    reader.wait();
+    for (int j = 0; j < 2; ++j) {
+      b.seqs[j].swap(nb.seqs[j]);
+      b.flat[j].swap(nb.flat[j]);
+      b.offs[j].swap(nb.offs[j]);
+    }
+    w.ph.mark("read (wait)");
+    if (b.seqs[0].empty()) return 0;
+    if (!nxt_ok[0] || !nxt_ok[1]) return -1;
+    start_reading(src);
+    static const bool sync_read = getenv("IBWA_SAMPE_SYNC_READ") != nullptr;  // measurement: no overlap
+    if (sync_read) {
+      reader.wait();
+      w.ph.mark("read (next batch, not overlapped)");
+    }
+    if (b.seqs[1].size() != b.seqs[0].size()) {
+      fprintf(stderr, "[ibwa-amd sampe] the two read files hold different numbers of reads\n");
+      return -1;
+    }
+    b.idx = idx;
+    const int n = (int)b.seqs[0].size();
+    auto span = [&b](int j, int i) { return AlnSpan{b.flat[j].data() + b.offs[j][i], b.offs[j][i + 1] - b.offs[j][i]}; };
+    b.midx.resize(2 * (size_t)n);
+    b.rcache.resize(2 * (size_t)n);
+    for (int i = 0; i < n; ++i)  // the drand48 stream, in pair order
+      for (int j = 0; j < 2; ++j) select_rng(span(j, i), b.midx[2 * i + j], b.rcache[2 * i + j]);
+    w.ph.mark("hit choice: drand48");
+    b.wide.resize(dbs.db.size());
+    for (auto &m : b.wide) m.clear();
+    if (popt.remapping) {  // the wide intervals' first uses in (pair, end, alignment) order
+      for (int i = 0; i < n; ++i)
+        for (int j = 0; j < 2; ++j)
+          for (const Aln &al : span(j, i)) {
+            const ibwa_aln1_t &a = al.aln;
+            if (a.l - a.k + 1 < kMinHashWidth) continue;
+            const uint64_t key = (uint64_t)a.k << 32 | a.l;
+            const uint64_t use = (uint64_t)a.a << 32 | (uint32_t)b.seqs[j][i].len;
+            b.wide[al.dbidx].emplace(key, first_use[al.dbidx].emplace(key, use).first->second);
+          }
+      w.ph.mark("rows: first uses");
+    }
+    return 1;
+  }
+
+  // the batch-to-batch waits: false when a worker failed
+  bool wait_ii(int64_t idx, Isize &ii) {
+    if (idx < 0) {
+      ii = Isize();
+      return true;
+    }
+    std::unique_lock<std::mutex> l(mu);
+    cv.wait(l, [&] { return failed || ii_done.count(idx) != 0; });
+    if (failed) return false;
+    ii = ii_done[idx];
+    return true;
+  }
+  void publish_ii(int64_t idx, const Isize &ii) {
+    std::lock_guard<std::mutex> l(mu);
+    ii_done[idx] = ii;  // kept: a slower worker's batch idx + 1 may ask for it late
+    cv.notify_all();
+  }
+  bool wait_turn(int64_t idx) {
+    std::unique_lock<std::mutex> l(mu);
+    cv.wait(l, [&] { return failed || printed == idx; });
+    return !failed;
+  }
+  void end_turn(int n) {
+    std::lock_guard<std::mutex> l(mu);
+    tot += n;
+    fprintf(stderr, "[bwa_sai2sam_pe_core] %ld sequences have been processed.\n", tot);
+    ++printed;
+    cv.notify_all();
+  }
+  void fail() {
+    std::lock_guard<std::mutex> l(mu);
+    failed = true;
+    cv.notify_all();
+  }
+
   int run(Source src[2], FILE *out) {
     Out o{out, {}};
-    long tot = 0;
-    std::vector<Read> seqs[2];
-    std::vector<Aln> flat[2];
-    std::vector<size_t> offs[2];
-    for (;;) {
-      reader.wait();
-      for (int j = 0; j < 2; ++j) {
-        seqs[j].swap(nxt[j]);
-        flat[j].swap(nflat[j]);
-        offs[j].swap(noff[j]);
+    std::mutex take_mu;
+    bool end = false;
+    int64_t n_taken = 0;
+    std::vector<int> rcs(W.size(), 0);
+    auto work = [&](int wi) {
+      Worker &w = W[wi];
+      Batch b;  // buffers kept from batch to batch
+      for (;;) {
+        {
+          std::lock_guard<std::mutex> l(take_mu);
+          if (end) return;
+          {
+            std::lock_guard<std::mutex> l2(mu);
+            if (failed) return;
+          }
+          const int t = take(src, w, b, n_taken);
+          if (t == 0) {
+            end = true;
+            return;
+          }
+          if (t < 0) {
+            rcs[wi] = 1;
+            end = true;
+            fail();
+            return;
+          }
+          ++n_taken;
+        }
+        if (int rc = batch(w, b, o)) {
+          rcs[wi] = rc;
+          fail();
+          return;
+        }
       }
-      ph.mark("read (wait)");
-      if (seqs[0].empty()) break;
-      if (!nxt_ok[0] || !nxt_ok[1]) return 1;
-      start_reading(src);
-      if (seqs[1].size() != seqs[0].size()) {
-        fprintf(stderr, "[ibwa-amd sampe] the two read files hold different numbers of reads\n");
-        return 1;
-      }
-      const int n = (int)seqs[0].size();
-      tot += n;
-      if (int rc = batch(seqs, flat, offs, n, o)) return rc;
-      fprintf(stderr, "[bwa_sai2sam_pe_core] %ld sequences have been processed.\n", tot);
-    }
+    };
+    std::vector<std::thread> th;
+    for (size_t wi = 1; wi < W.size(); ++wi) th.emplace_back(work, (int)wi);
+    work(0);
+    for (auto &t : th) t.join();
+    for (int rc : rcs)
+      if (rc) return rc;
     o.flush();
-    ph.print("ibwa-amd sampe");
+    for (size_t wi = 0; wi < W.size(); ++wi) {
+      char who[48];
+      if (W.size() == 1) snprintf(who, sizeof who, "ibwa-amd sampe");
+      else snprintf(who, sizeof who, "ibwa-amd sampe worker %zu", wi);
+      W[wi].ph.print(who);
+    }
     fprintf(stderr, "[ibwa-amd sampe] read-ahead thread s: end 1 reads %.2f .sai %.2f, end 2 reads %.2f .sai %.2f\n",
             rd_s[0][0], rd_s[0][1], rd_s[1][0], rd_s[1][1]);
     return 0;
   }
 
-  int batch(std::vector<Read> seqs[2], std::vector<Aln> aflat[2], std::vector<size_t> aoff[2], int n, Out &o) {
+  int batch(Worker &wk, Batch &bt, Out &o) {
+    Phases &ph = wk.ph;
+    std::vector<Read> *seqs = bt.seqs;
+    const int n = (int)seqs[0].size();
     // every read's alignments in one flat array per end (alns[j][i] slices it), read with the batch
     std::vector<AlnSpan> alns[2];
     // ---- SE (bwa_cal_pac_pos_pe, bwape.c:366-385): hit choice in pair order (the drand48 stream),
@@ -698,14 +848,12 @@ struct Sampe {
     }
     for (int j = 0; j < 2; ++j) {
       alns[j].resize(n);
-      for (int i = 0; i < n; ++i) alns[j][i] = AlnSpan{aflat[j].data() + aoff[j][i], aoff[j][i + 1] - aoff[j][i]};
+      for (int i = 0; i < n; ++i)
+        alns[j][i] = AlnSpan{bt.flat[j].data() + bt.offs[j][i], bt.offs[j][i + 1] - bt.offs[j][i]};
     }
     {
-      std::vector<int> midx(2 * (size_t)n);
-      std::vector<double> rcache(2 * (size_t)n);
-      for (int i = 0; i < n; ++i)  // the drand48 stream, in pair order
-        for (int j = 0; j < 2; ++j) select_rng(alns[j][i], midx[2 * i + j], rcache[2 * i + j]);
-      ph.mark("hit choice: drand48");
+      const std::vector<int> &midx = bt.midx;  // the drand48 decisions, made when the batch was taken
+      const std::vector<double> &rcache = bt.rcache;
       parallel_ordered(n, [&](int64_t lo, int64_t hi_, int) {
         for (int64_t i = lo; i < hi_; ++i)
           for (int j = 0; j < 2; ++j) {
@@ -750,7 +898,7 @@ struct Sampe {
     }
     ph.mark("hit choice: row lists");
     std::vector<uint64_t> pos;
-    if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
+    if (int rc = sa2pos(wk, hd, hs, hk, hl, pos)) return rc;
     ph.mark("sa2pos: kernel");
     std::vector<uint8_t> ok(hi.size(), 0);
     auto remap_main = [&](size_t t) {
@@ -791,7 +939,7 @@ struct Sampe {
           }
         }
         std::vector<uint64_t> p1;
-        if (int rc = sa2pos(d1, s1, k1, l1, p1)) return rc;
+        if (int rc = sa2pos(wk, d1, s1, k1, l1, p1)) return rc;
         parallel_ordered((int64_t)(f1 - f0), [&](int64_t lo, int64_t hi_, int) {
           for (int64_t u = lo; u < hi_; ++u) {
             const size_t t = fail[f0 + u];
@@ -826,12 +974,17 @@ struct Sampe {
     // ---- insert size
     Isize ii;
     infer_isize(seqs[0], seqs[1], ii, popt.ap_prior, (int64_t)dbs.l_pac);
-    if (ii.avg < 0.0 && last_ii.avg > 0.0) ii = last_ii;
+    if (ii.avg < 0.0) {  // the previous batch's, as it ended up (bwape.c:410-411)
+      Isize last_ii;
+      if (!wait_ii(bt.idx - 1, last_ii)) return 1;
+      if (last_ii.avg > 0.0) ii = last_ii;
+    }
     if (popt.force_isize) {
       fprintf(stderr, "[bwa_cal_pac_pos_pe] discard insert size estimate as user's request.\n");
       ii.low = ii.high = 0;
       ii.avg = ii.std = -1.0;
     }
+    publish_ii(bt.idx, ii);
     ph.mark("isize");
     // ---- every row of every interval (compute_seq_coords_and_counts): one SA->pos launch per
     // reference.  Rows of intervals narrower than kMinHashWidth are computed per (read, alignment);
@@ -891,21 +1044,22 @@ struct Sampe {
             const uint32_t w = a.l - a.k + 1;
             if (w < kMinHashWidth) continue;
             const uint64_t key = (uint64_t)a.k << 32 | a.l;
-            if (cache[al.dbidx].count(key)) continue;
+            if (wk.cache[al.dbidx].count(key)) continue;
             fill.push_back({{al.dbidx, key}, (int64_t)hk.size()});
-            cache[al.dbidx][key];  // reserve: later uses in this batch share it
+            wk.cache[al.dbidx][key];  // reserve: later uses in this batch share it
+            const uint64_t use = bt.wide[al.dbidx].at(key);  // the run's first use: its strand, read length
             for (uint32_t r = 0; r < w; ++r) {
-              hd.push_back(al.dbidx); hs.push_back((uint8_t)a.a); hk.push_back(a.k + r);
-              hl.push_back((uint32_t)seqs[j][i].len);
+              hd.push_back(al.dbidx); hs.push_back((uint8_t)(use >> 32)); hk.push_back(a.k + r);
+              hl.push_back((uint32_t)use);
             }
           }
     }
     ph.mark("rows");
-    if (int rc = sa2pos(hd, hs, hk, hl, pos)) return rc;
+    if (int rc = sa2pos(wk, hd, hs, hk, hl, pos)) return rc;
     ph.mark("rows: sa2pos kernel");
     for (auto &f : fill) {
       const uint32_t k = (uint32_t)(f.first.second >> 32), l = (uint32_t)f.first.second;
-      cache[f.first.first][f.first.second].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
+      wk.cache[f.first.first][f.first.second].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
     }
     ph.mark("rows: cache");
     // ---- select_sai_multi's rows that the -R pass did not compute (no -R, or a cached interval):
@@ -934,7 +1088,7 @@ struct Sampe {
           }
         }
       }
-      if (int rc = sa2pos(hd, hs, hk, hl, mpos)) return rc;
+      if (int rc = sa2pos(wk, hd, hs, hk, hl, mpos)) return rc;
     }
     ph.mark("multi rows");
     // ---- PE (bwa_cal_pac_pos_pe_thread, bwape.c:238-297) on the host threads, in three passes so
@@ -942,9 +1096,7 @@ struct Sampe {
     // shared array holds there: (A) every pair's positions, counts and sort; (B) each pair's nearest
     // earlier pair with more positions; (C) the pairing itself and select_sai_multi.
     const int nth = host_threads();
-    // every pair's positions, per host thread; kept across batches (a batch holds ~10 M positions,
-    // 0.5 GB: allocating, faulting in and freeing that each batch cost about as much as filling it)
-    std::vector<std::vector<Position>> &pstore = pstore_;
+    std::vector<std::vector<Position>> &pstore = wk.pstore;  // every pair's positions, per host thread
     pstore.resize(std::max<size_t>(pstore.size(), (size_t)nth));
     for (auto &v : pstore) v.clear();
     std::vector<uint32_t> pcnt(n, 0);
@@ -984,7 +1136,7 @@ struct Sampe {
               min_score = std::min(min_score, a.score);
               const uint32_t w = a.l - a.k + 1;
               const int64_t slot = aslot[row0[j][i] + (int64_t)k];
-              const uint64_t *pp = slot < 0 ? cache[d].find((uint64_t)a.k << 32 | a.l)->second.data() : pos.data() + slot;
+              const uint64_t *pp = slot < 0 ? wk.cache[d].find((uint64_t)a.k << 32 | a.l)->second.data() : pos.data() + slot;
               for (uint32_t r = 0; r < w; ++r) {
                 const uint64_t x = pp[r];
                 if (x < rdb.offset || x >= rdb.offset + (uint64_t)rdb.bns.l_pac) continue;
@@ -1131,13 +1283,13 @@ struct Sampe {
     fprintf(stderr, "[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);
     ph.mark("pairing");
     // ---- mate rescue (bwa_paired_sw) over the concatenated references
-    if (int rc = paired_sw(seqs, n, ii)) return rc;
+    if (int rc = paired_sw(wk, seqs, n, ii)) return rc;
     ph.mark("paired SW");
     // ---- refine gapped alignments of both ends, MD/NM, trimmed reads; then remap()
     std::vector<Read *> rp;
     for (int j = 0; j < 2; ++j)
       for (Read &r : seqs[j]) rp.push_back(&r);
-    if (int rc = refine_gapped(ctx[0], dbs, rp)) return rc == 1 ? 1 : die("global alignment");
+    if (int rc = refine_gapped(wk.ctx[0], dbs, rp)) return rc == 1 ? 1 : die("global alignment");
     ph.mark("refine");
     for (int j = 0; j < 2; ++j)
       parallel_ordered(n, [&](int64_t lo, int64_t hi_, int) {
@@ -1152,7 +1304,9 @@ struct Sampe {
         }
       }, 0, 4096);
     ph.mark("remap after refine");
-    // ---- print: with -R the remapped (primary) coordinates, the original ones as ZR
+    // ---- print: with -R the remapped (primary) coordinates, the original ones as ZR; batch by batch
+    // in file order
+    if (!wait_turn(bt.idx)) return 1;
     print_parallel(o, n, [&](Out &ob, int64_t i) {
       Read *p[2] = {&seqs[0][i], &seqs[1][i]};
       if (p[0]->bc[0] || p[1]->bc[0]) {
@@ -1169,8 +1323,8 @@ struct Sampe {
       print_sam1(ob, dbs, *p[0], p[1], gopt[1].mode, gopt[1].max_top2, rg_id);
       print_sam1(ob, dbs, *p[1], p[0], gopt[1].mode, gopt[1].max_top2, rg_id);
     });
+    end_turn(n);
     ph.mark("print");
-    last_ii = ii;
     return 0;
   }
 
@@ -1211,12 +1365,14 @@ struct Sampe {
   }
 
   // bwa_paired_sw through the C-ABI (compat.cpp) on bwa_seq_t mirrors of the batch
-  int paired_sw(std::vector<Read> seqs[2], int n, const Isize &ii) {
+  int paired_sw(Worker &wk, std::vector<Read> seqs[2], int n, const Isize &ii) {
+    Phases &ph = wk.ph;
     if (!popt.is_sw || ii.avg < 0.0) return 0;
     // the mirrors are filled in parallel below, in buffers kept across batches (allocating, faulting
     // in and freeing a batch's worth each time cost ~25 ms per batch)
-    std::unique_ptr<ibwa_ref_seq_t[]> *ref = sw_ref_;
-    std::unique_ptr<uint8_t[]> *rev = sw_rev_;
+    std::unique_ptr<ibwa_ref_seq_t[]> *ref = wk.sw_ref;
+    std::unique_ptr<uint8_t[]> *rev = wk.sw_rev;
+    size_t *sw_ref_cap_ = wk.sw_ref_cap, *sw_rev_cap_ = wk.sw_rev_cap;
     for (int j = 0; j < 2; ++j) {
       if (sw_ref_cap_[j] < (size_t)std::max(n, 1)) {
         sw_ref_cap_[j] = (size_t)std::max(n, 1);
@@ -1269,7 +1425,7 @@ struct Sampe {
       offs.push_back(r.offset);
       lens.push_back((uint64_t)r.bns.l_pac);
     }
-    if (ibwa_paired_sw_dbs(ctx[0], n, sp, &po, &ri, (int)pacs.size(), pacs.data(), offs.data(), lens.data(), n_tot,
+    if (ibwa_paired_sw_dbs(wk.ctx[0], n, sp, &po, &ri, (int)pacs.size(), pacs.data(), offs.data(), lens.data(), n_tot,
                            n_mapped))
       return die("paired SW");
     ph.mark("paired SW: windows+SW+fix-up");
@@ -1313,8 +1469,9 @@ int sampe_main(int argc, char *argv[]) {
   int c;
   const char *fn_out = nullptr;
   std::string rg_line, rg_id;
+  int n_workers = 1;
   optind = 1;
-  while ((c = getopt(argc, argv, "a:o:sPn:N:c:f:ARr:t:")) >= 0) {  // bwa_sai2sam_pe (bwape.c:583-610)
+  while ((c = getopt(argc, argv, "a:o:sPn:N:c:f:ARr:t:G:")) >= 0) {  // bwa_sai2sam_pe (bwape.c:583-610) + -G
     switch (c) {
       case 'r':
         if (!set_rg(optarg, rg_line, rg_id)) {
@@ -1333,11 +1490,12 @@ int sampe_main(int argc, char *argv[]) {
       case 'f': fn_out = optarg; break;
       case 'A': S.popt.force_isize = 1; break;
       case 'R': S.popt.remapping = 1; break;
+      case 'G': n_workers = atoi(optarg); break;
       default: return 1;
     }
   }
   if (optind + 5 > argc) {
-    fprintf(stderr, "Usage: ibwa-amd sampe [-a INT] [-o INT] [-n INT] [-N INT] [-c FLOAT] [-f out.sam] [-r RG] [-sAR]\n"
+    fprintf(stderr, "Usage: ibwa-amd sampe [-a INT] [-o INT] [-n INT] [-N INT] [-c FLOAT] [-f out.sam] [-r RG] [-G INT] [-sAR]\n"
                     "                      <prefix> <in1.sai> <in2.sai> <in1.fq> <in2.fq> [<prefix2> <in1.sai> <in2.sai> ...]\n");
     return 1;
   }
@@ -1376,12 +1534,20 @@ int sampe_main(int argc, char *argv[]) {
       return 1;
     }
   }
+  if (const char *e = getenv("IBWA_SAMPE_BATCH")) S.batch_pairs = (size_t)std::max(1L, atol(e));
   S.start_reading(src);
   // dbset_restore (dbset.c:135-176): references at cumulative offsets, each with its index on the
   // GPU, and (-R) its .remap table when it has one
   S.dbs.db.resize(count);
-  S.cache.resize(count);
-  // the host side (.ann / .amb / .pac, .remap tables) on a thread while the GPU takes the indexes
+  if (n_workers < 1) n_workers = 1;
+  S.W.resize(n_workers);
+  for (Worker &w : S.W) w.cache.resize(count);
+  S.first_use.resize(count);
+  int n_dev = 0;
+  if (ibwa_device_count(&n_dev) || n_dev < 1) return die("no HIP device");
+  if (n_workers > n_dev)
+    fprintf(stderr, "[ibwa-amd sampe] -G %d on %d visible device(s): worker w runs on device w mod %d\n", n_workers, n_dev, n_dev);
+  // the host side (.ann / .amb / .pac, .remap tables) on a thread while the GPUs take the indexes
   std::vector<int> host_ok(count, 0);
   std::thread host_side([&]() {
     for (int d = 0; d < count; ++d) {
@@ -1393,24 +1559,46 @@ int sampe_main(int argc, char *argv[]) {
       host_ok[d] = 2;
     }
   });
-  int gpu_rc = 0;
-  for (int d = 0; d < count && !gpu_rc; ++d) {
-    const std::string &prefix = prefixes[d];
-    ibwa_ctx_t *cx = nullptr;
-    if (ibwa_ctx_create(0, &cx)) { gpu_rc = 1; break; }
-    S.ctx.push_back(cx);
-    if (ibwa_ctx_load_bwt_file(cx, 0, (prefix + ".bwt").c_str()) || ibwa_ctx_load_bwt_file(cx, 1, (prefix + ".rbwt").c_str()))
-      gpu_rc = 2;
-    else if (ibwa_ctx_load_sa_file(cx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(cx, 1, (prefix + ".rsa").c_str()))
-      gpu_rc = 3;
-    else if (ibwa_ctx_expand_sa(cx))
-      gpu_rc = 4;
+  // the first worker on each device loads the indexes there (the devices in parallel); the others
+  // share them
+  const int n_load = std::min(n_workers, n_dev);
+  std::vector<int> gpu_rcs(n_load, 0);
+  auto load = [&](int w) {
+    int &rc = gpu_rcs[w];
+    for (int d = 0; d < count && !rc; ++d) {
+      const std::string &prefix = prefixes[d];
+      ibwa_ctx_t *cx = nullptr;
+      if (ibwa_ctx_create(w, &cx)) { rc = 1; break; }
+      S.W[w].ctx.push_back(cx);
+      if (ibwa_ctx_load_bwt_file(cx, 0, (prefix + ".bwt").c_str()) || ibwa_ctx_load_bwt_file(cx, 1, (prefix + ".rbwt").c_str()))
+        rc = 2;
+      else if (ibwa_ctx_load_sa_file(cx, 0, (prefix + ".sa").c_str()) || ibwa_ctx_load_sa_file(cx, 1, (prefix + ".rsa").c_str()))
+        rc = 3;
+      else if (ibwa_ctx_expand_sa(cx))
+        rc = 4;
+    }
+  };
+  {
+    std::vector<std::thread> lt;
+    for (int w = 1; w < n_load; ++w) lt.emplace_back(load, w);
+    load(0);
+    for (auto &t : lt) t.join();
   }
+  int gpu_rc = 0;
+  for (int x : gpu_rcs) gpu_rc = gpu_rc ? gpu_rc : x;
+  for (int w = n_load; w < n_workers && !gpu_rc; ++w)
+    for (int d = 0; d < count && !gpu_rc; ++d) {
+      ibwa_ctx_t *cx = nullptr;
+      if (ibwa_ctx_create(w % n_dev, &cx)) { gpu_rc = 1; break; }
+      S.W[w].ctx.push_back(cx);
+      if (ibwa_ctx_share_index(cx, S.W[w % n_dev].ctx[d])) gpu_rc = 5;
+    }
   host_side.join();
   if (gpu_rc == 1) return die("ibwa_ctx_create");
   if (gpu_rc == 2) return die("load .bwt / .rbwt");
   if (gpu_rc == 3) return die("load .sa / .rsa");
   if (gpu_rc == 4) return die("expand SA");
+  if (gpu_rc == 5) return die("share index");
   for (int d = 0; d < count; ++d) {
     RefDb &r = S.dbs.db[d];
     const std::string &prefix = prefixes[d];
@@ -1446,12 +1634,13 @@ int sampe_main(int argc, char *argv[]) {
   head += "@PG\tID:bwa\tPN:bwa\tVN:ibwa-amd\n";
   fwrite(head.data(), 1, head.size(), out);
   Source *sp = src;
-  S.ph.mark("load index (first batch read meanwhile)");
+  S.W[0].ph.mark("load index (first batch read meanwhile)");
   const int rc = S.run(sp, out);
   S.reader.wait();  // a batch read ahead on an error return
   for (int j = 0; j < 2; ++j)
     for (FILE *fp : S.fp_sai[j]) fclose(fp);
   if (out != stdout) fclose(out);
-  for (ibwa_ctx_t *cx : S.ctx) ibwa_ctx_destroy(cx);
+  for (size_t w = S.W.size(); w-- > 0;)  // the sharing contexts before the ones they borrow from
+    for (ibwa_ctx_t *cx : S.W[w].ctx) ibwa_ctx_destroy(cx);
   return rc;
 }

@@ -155,3 +155,49 @@ def test_sampe_bulk_reader_equals_serial(golden_dir, aln_opts, tmp_path):
         outs.append(_body(out.read_text()))
     assert len(outs[0]) > 1000
     assert outs[0] == outs[1]
+
+
+def _sampe(argv, args, out, env=None):
+    r = subprocess.run([CLI, "sampe"] + argv + ["-f", str(out)] + args, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr[-2000:]
+    return out.read_text(), r.stderr
+
+
+@pytest.mark.parametrize("key", sorted(MANIFEST))
+def test_sampe_two_workers_match_reference(golden_dir, key, tmp_path):
+    """`sampe -G 2` on one GPU (sampe_main.cpp Worker: the second worker's contexts share the first's
+    index): the reference's SAM, byte for byte except @PG."""
+    m = MANIFEST[key]
+    g = lambda x: os.path.join(golden_dir, x)  # noqa: E731
+    got, _ = _sampe(m["argv"] + ["-G", "2"], [g(m.get("prefix", "g1m")), *map(g, m["sai"]), *map(g, m["reads"])],
+                    tmp_path / "out.sam")
+    assert _body(got) == _body(gzip.open(g(m["sam"]), "rt").read())
+
+
+def test_sampe_workers_equal_one_worker_on_small_batches(golden_dir, tmp_path):
+    """The batch loop sharded over -G 2 / -G 3 workers (bwape.c:476-536 batch by batch) writes what
+    one worker writes, on batches of 29 pairs (IBWA_SAMPE_BATCH) so that every worker takes many:
+    the drand48 draws taken in batch order, the wide intervals' cached positions computed with their
+    first use in the run (tandem: intervals of >= 1000 rows), the previous batch's insert size where a
+    batch has too few good pairs (bwape.c:410-411), SAM in file order; one reference and two."""
+    g = lambda x: os.path.join(golden_dir, x)  # noqa: E731
+    env = {"IBWA_SAMPE_BATCH": "29"}
+    cases = [(MANIFEST[k]["argv"], [g(MANIFEST[k].get("prefix", "g1m")), *map(g, MANIFEST[k]["sai"]),
+                                    *map(g, MANIFEST[k]["reads"])])
+             for k in ("pe100.default", "pe100.noR", "pe100.n5N20", "tandem.R", "tandemt.R.t3", "pe150.default")]
+    for k in ("remap.R", "remap.noR"):
+        m = REMAP[k]
+        args = [g(m["prefixes"][0]), *map(g, m["sai"][0]), *map(g, m["reads"])]
+        for pre, sai in zip(m["prefixes"][1:], m["sai"][1:]):
+            args += [g(pre), *map(g, sai)]
+        cases.append((m["argv"], args))
+    fell_back = False
+    for argv, args in cases:
+        one, err = _sampe(argv + ["-G", "1"], args, tmp_path / "g1.sam", env)
+        fell_back = fell_back or "too few good pairs" in err
+        assert len(one.splitlines()) > 100
+        for n in ("2", "3"):
+            got, _ = _sampe(argv + ["-G", n], args, tmp_path / f"g{n}.sam", env)
+            assert got == one, (argv, n)
+    assert fell_back  # some batch took the previous batch's insert size

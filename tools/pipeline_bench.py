@@ -37,14 +37,18 @@ def log(*a):
     print("[pipeline]", *a, file=sys.stderr, flush=True)
 
 
+LAST_ERR = [""]
+
+
 def run(argv, stdout=None, timeout=1200):
     t = time.perf_counter()
     r = subprocess.run(argv, stdout=stdout, stderr=subprocess.PIPE, timeout=timeout)
     dt = time.perf_counter() - t
+    LAST_ERR[0] = r.stderr.decode(errors="replace")
     if r.returncode != 0:
         raise RuntimeError(f"{argv[:2]} failed ({r.returncode}): {r.stderr.decode()[-1500:]}")
     for ln in r.stderr.decode(errors="replace").splitlines():
-        if "wall s:" in ln or "[ibwa-amd aln]" in ln or "hipMalloc" in ln or "coop pass" in ln or "retry" in ln or "batch of" in ln or "paired_sw]" in ln or "read-ahead" in ln:
+        if "wall s:" in ln or "cpu s:" in ln or "[ibwa-amd aln]" in ln or "hipMalloc" in ln or "coop pass" in ln or "retry" in ln or "batch of" in ln or "paired_sw]" in ln or "read-ahead" in ln:
             log(f"  {os.path.basename(argv[0])} {argv[1]}: {ln}")
     return dt
 
@@ -129,6 +133,23 @@ def write_fastq(path, reads, tag, end, first=0, count=None):
             f.write(b"".join(b"@%s%d/%d\n%s\n+\n%s\n" % (tag, i, end, reads[i].tobytes(), qual) for i in range(s, e)))
 
 
+def load_s(err):
+    """sampe's index load (with the first batch read meanwhile), from its phase line."""
+    for ln in err.splitlines():
+        if "wall s:" in ln and "load index" in ln:
+            return float(ln.split("meanwhile)")[1].split()[0])
+    return None
+
+
+def file_digest(path):
+    import hashlib
+    h = hashlib.sha1()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 24), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
 def sam_body(path):
     with open(path, "rb") as f:
         return [ln for ln in f.read().split(b"\n") if ln and not ln.startswith(b"@PG")]
@@ -143,6 +164,7 @@ def main():
     ap.add_argument("--sub", type=float, default=0.02)
     ap.add_argument("--threads", type=int, default=bench.host_threads())
     ap.add_argument("--concurrent-ends", type=int, default=1, help="also align the two ends at once (one GPU)")
+    ap.add_argument("--sampe-workers", default="1,2", help="sampe -R -G values to time (the first is sampe_s)")
     ap.add_argument("--out", default="")
     ap.add_argument("--diag", action="store_true", help="only run `aln` on the sample's end 2 with IBWA_VERBOSE")
     a = ap.parse_args()
@@ -181,7 +203,22 @@ def main():
     # ---- ibwa-amd over all pairs
     sai = [os.path.join(tmp, f"r{e}.sai") for e in (1, 2)]
     res["aln_s"] = [run([CLI, "aln", "-f", sai[e], P, fq[e]]) for e in (0, 1)]
-    res["sampe_s"] = run([CLI, "sampe", "-R", "-f", os.path.join(tmp, "pe.sam"), P, sai[0], sai[1], fq[0], fq[1]])
+    res["sampe_workers"] = {}
+    for k, g in enumerate(a.sampe_workers.split(",")):
+        pe = os.path.join(tmp, "pe.sam" if k == 0 else f"pe.G{g}.sam")
+        dt = run([CLI, "sampe", "-R", "-G", g, "-f", pe, P, sai[0], sai[1], fq[0], fq[1]])
+        ld = load_s(LAST_ERR[0])
+        w = {"wall_s": dt, "load_s": ld, "pairs_per_s_excl_load": a.pairs / (dt - ld) if ld is not None else None}
+        if k == 0:
+            res["sampe_s"] = dt
+            ref_digest = file_digest(pe)
+        else:
+            w["sam_equal_first"] = file_digest(pe) == ref_digest
+            os.unlink(pe)
+        res["sampe_workers"][g] = w
+        log(f"ibwa-amd sampe -R -G {g}: {dt:.2f} s (index load {ld} s) -> "
+            f"{w['pairs_per_s_excl_load'] or 0:.0f} pairs/s excluding the load" +
+            (f", SAM equal -G {a.sampe_workers.split(',')[0]}: {w['sam_equal_first']}" if k else ""))
     res["samse_s"] = run([CLI, "samse", "-f", os.path.join(tmp, "se.sam"), P, sai[0], fq[0]])
     if a.concurrent_ends:
         # both ends' aln at once on the one GPU (each process under ~128 GiB): no process waits for
