@@ -429,6 +429,15 @@ struct Source {
 };
 
 // ---------------------------------------------------------------- the batch loop (bwa_sai2sam_pe_core)
+// a host thread's buffers for the positions pass
+struct PosScratch {
+  PosArr arr;
+  std::vector<std::pair<uint64_t, int>> ps;
+  std::vector<PosKey> pk;
+  std::vector<uint64_t> kk, tk;
+  std::vector<uint32_t> ki, tv;
+};
+
 // One shard of the batch loop (-G): its GPU contexts, one per reference, and what its batches work
 // in, kept from batch to batch.
 struct Worker {
@@ -439,6 +448,7 @@ struct Worker {
   // every pair's positions, per host thread; kept across batches (a batch holds ~10 M positions,
   // 0.5 GB: allocating, faulting in and freeing that each batch cost about as much as filling it)
   std::vector<std::vector<Position>> pstore;
+  std::vector<PosScratch> pscr;  // per host thread
   std::unique_ptr<ibwa_ref_seq_t[]> sw_ref[2];  // paired_sw's bwa_seq_t mirrors per end (capacity kept)
   std::unique_ptr<uint8_t[]> sw_rev[2];
   size_t sw_ref_cap[2] = {0, 0}, sw_rev_cap[2] = {0, 0};
@@ -1109,13 +1119,16 @@ struct Sampe {
     auto now_ns = []() {
       return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
     };
+    wk.pscr.resize(std::max(wk.pscr.size(), (size_t)nth));
     parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
-      PosArr arr;
-      std::vector<std::pair<uint64_t, int>> ps;
-      std::vector<PosKey> pk;
-      std::vector<Position> tmp;
-      std::vector<uint64_t> kk, tk;
-      std::vector<uint32_t> ki, tv;
+      // this host thread's scratch, kept across chunks and batches (a pair of a repeat holds up to
+      // ~160 k positions: fresh buffers per chunk were page-faulted in again and again)
+      PosScratch &sc = wk.pscr[th];
+      PosArr &arr = sc.arr;
+      std::vector<std::pair<uint64_t, int>> &ps = sc.ps;
+      std::vector<PosKey> &pk = sc.pk;
+      std::vector<uint64_t> &kk = sc.kk, &tk = sc.tk;
+      std::vector<uint32_t> &ki = sc.ki, &tv = sc.tv;
       int64_t a_pos = 0, a_cnt = 0, a_sort = 0;
       for (int64_t i = lo; i < hi_; ++i) {
         Read *p[2] = {&seqs[0][i], &seqs[1][i]};
@@ -1186,25 +1199,29 @@ struct Sampe {
         const bool m0 = p[0]->type == TYPE_UNIQUE || p[0]->type == TYPE_REPEAT;
         const bool m1 = p[1]->type == TYPE_UNIQUE || p[1]->type == TYPE_REPEAT;
         paired[i] = m0 && m1;
+        // the pair's positions go to this thread's store, sorted for find_optimal_pair when paired:
+        // gathered there in sorted order through a permutation when one is computed
+        std::vector<Position> &st = pstore[th];
+        const uint32_t *perm = nullptr;
         if (paired[i]) {  // find_optimal_pair's sort
           bool done = false;
           if (arr.n > 256 && fit32) {
             // no two positions with the same (remapped position, position): then the sorted order is
-            // unique and a radix sort gives the introsort's; with such ties the introsort decides
+            // unique and a radix sort gives the introsort's; with such ties the introsort decides.
+            // Without remapping (every remapped position == its position) the key is the position
+            // alone: the same order and the same ties, in half the radix passes.
+            bool plain = true;
+            for (size_t t = 0; t < arr.n && plain; ++t) plain = arr.a[t].remapped_pos == arr.a[t].pos;
             kk.resize(arr.n);
             ki.resize(arr.n);
             for (size_t t = 0; t < arr.n; ++t) {
-              kk[t] = arr.a[t].remapped_pos << 32 | arr.a[t].pos;
+              kk[t] = plain ? arr.a[t].pos : arr.a[t].remapped_pos << 32 | arr.a[t].pos;
               ki[t] = (uint32_t)t;
             }
             radix_sort_u64(arr.n, kk.data(), ki.data(), tk, tv);
             done = true;
             for (size_t t = 1; t < arr.n && done; ++t) done = kk[t] != kk[t - 1];
-            if (done) {
-              tmp.resize(arr.n);
-              for (size_t t = 0; t < arr.n; ++t) tmp[t] = arr.a[ki[t]];
-              std::copy(tmp.begin(), tmp.end(), arr.a.begin());
-            }
+            if (done) perm = ki.data();
           }
           if (done) {
           } else if (arr.n > 32) {
@@ -1215,18 +1232,23 @@ struct Sampe {
             ks_introsort(arr.n, pk.data(), [](const PosKey &a, const PosKey &b) {
               return a.rp == b.rp ? a.p < b.p : a.rp < b.rp;
             });
-            tmp.resize(arr.n);
-            for (size_t t = 0; t < arr.n; ++t) tmp[t] = arr.a[pk[t].idx];
-            std::copy(tmp.begin(), tmp.end(), arr.a.begin());
+            ki.resize(arr.n);
+            for (size_t t = 0; t < arr.n; ++t) ki[t] = pk[t].idx;
+            perm = ki.data();
           } else {
             ks_introsort(arr.n, arr.a.data(), position_lt);
           }
         }
         if (pstats) a_sort += now_ns() - t0;
         pth[i] = th;
-        poff[i] = pstore[th].size();
+        poff[i] = st.size();
         pcnt[i] = (uint32_t)arr.n;
-        pstore[th].insert(pstore[th].end(), arr.a.begin(), arr.a.begin() + arr.n);
+        if (perm) {
+          if (st.capacity() < st.size() + arr.n) st.reserve(std::max(st.size() + arr.n, 2 * st.capacity()));
+          for (size_t t = 0; t < arr.n; ++t) st.push_back(arr.a[perm[t]]);
+        } else {
+          st.insert(st.end(), arr.a.begin(), arr.a.begin() + arr.n);
+        }
       }
       t_pos += a_pos;
       t_cnt += a_cnt;
