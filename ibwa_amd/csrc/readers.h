@@ -185,7 +185,6 @@ struct FastqBulk {
 
   // bytes of the record at p (> 0), 0 when the data ends inside it, -1 when it is not strict
   static int64_t rec_at(const char *p, const char *e, bool at_eof, const char *base, Rec &r) {
-    const uint8_t *cls = SeqReader::seq_class();
     if (p >= e) return 0;
     if (*p != '@') return -1;
     const char *h = (const char *)memchr(p, '\n', (size_t)(e - p));
@@ -195,8 +194,14 @@ struct FastqBulk {
     if (!se) return at_eof ? -1 : 0;
     const int64_t L = se - sq;
     if (L < 1 || L > (1 << 24)) return -1;
-    for (const char *x = sq; x < se; ++x)
-      if (cls[(uint8_t)*x] != 1) return -1;
+    // no exit per byte: the checks run branch-free over the line (and vectorise).  seq_class() == 1
+    // is isgraph() in the C locale, 33..126, but for '>', '+' and '@'
+    uint8_t bad = 0;
+    for (const char *x = sq; x < se; ++x) {
+      const uint8_t c = (uint8_t)*x;
+      bad |= (uint8_t)((c < 33) | (c > 126) | (c == '>') | (c == '+') | (c == '@'));
+    }
+    if (bad) return -1;
     const char *pl = se + 1;
     if (pl >= e) return at_eof ? -1 : 0;
     if (*pl != '+') return -1;
@@ -204,10 +209,12 @@ struct FastqBulk {
     if (!pe) return at_eof ? -1 : 0;
     const char *u = pe + 1;
     if (e - u < L + 1) return at_eof ? -1 : 0;
+    uint8_t qbad = 0;
     for (int64_t k = 0; k < L; ++k) {
       const uint8_t c = (uint8_t)u[k];
-      if (c < 33 || c > 127) return -1;
+      qbad |= (uint8_t)((c < 33) | (c > 127));
     }
+    if (qbad) return -1;
     if (u[L] != '\n') return -1;
     r.h = (uint64_t)(p - base);
     r.s = (uint64_t)(sq - base);

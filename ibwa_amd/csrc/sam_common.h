@@ -532,15 +532,30 @@ inline bool rec_to_read(const char *base, const ibwa_cli::FastqBulk::Rec &r, int
   const int n = L - l_bc;
   p.full_len = p.clip_len = p.len = n;
   p.seq.resize(n);
-  for (int i = 0; i < n; ++i) p.seq[i] = nt4[(unsigned char)s[l_bc + i]];
   p.qual.resize(n);
-  for (int i = 0; i < n; ++i) p.qual[i] = qv(l_bc + i);
+  p.rseq.resize(n);
+  uint8_t *sq = p.seq.data(), *rs = p.rseq.data();
+  const char *src = s + l_bc;
+  if (is_64) {
+    for (int i = 0; i < n; ++i) p.qual[i] = qv(l_bc + i);
+  } else {
+    memcpy(&p.qual[0], q + l_bc, (size_t)n);
+  }
   p.has_qual = true;
-  if (trim_qual >= 1) trim_read(trim_qual, p);
-  p.rseq.assign(n, 0);
-  for (int i = 0; i < p.len; ++i) {
-    const uint8_t c = p.seq[p.len - 1 - i];
-    p.rseq[i] = is_comp && c < 4 ? 3 - c : c;
+  if (trim_qual >= 1) {
+    for (int i = 0; i < n; ++i) sq[i] = nt4[(unsigned char)src[i]];
+    trim_read(trim_qual, p);
+    memset(rs, 0, (size_t)n);
+    for (int i = 0; i < p.len; ++i) {
+      const uint8_t c = sq[p.len - 1 - i];
+      rs[i] = is_comp && c < 4 ? 3 - c : c;
+    }
+  } else {  // untrimmed: the codes and their reverse complement in one pass
+    for (int i = 0; i < n; ++i) {
+      const uint8_t c = nt4[(unsigned char)src[i]];
+      sq[i] = c;
+      rs[n - 1 - i] = is_comp && c < 4 ? 3 - c : c;
+    }
   }
   // kseq's name: the header up to its first white space; then /[12]$ trimmed
   const char *h = base + r.h + 1, *e = h;
