@@ -210,10 +210,29 @@ inline bool bns_restore(const std::string &prefix, Bns &b) {
 
 inline uint8_t pac_at(const Bns &b, uint64_t x) { return (b.pac[x >> 2] >> ((~x & 3) << 1)) & 3; }  // bns_pac
 
+// codes [x, x + n) of a 2-bit packed sequence (base x at bits 7-6 of byte x / 4 down to bits 1-0):
+// pac_at base by base, a whole byte's four codes at once where x is byte-aligned
+inline void unpack_pac(const uint8_t *pac, uint64_t x, uint64_t n, uint8_t *out) {
+  static const struct Lut {
+    uint32_t w[256];
+    Lut() {
+      for (int b = 0; b < 256; ++b) {
+        const uint8_t c[4] = {(uint8_t)(b >> 6 & 3), (uint8_t)(b >> 4 & 3), (uint8_t)(b >> 2 & 3), (uint8_t)(b & 3)};
+        memcpy(&w[b], c, 4);
+      }
+    }
+  } lut;
+  uint64_t t = 0;
+  for (; t < n && (x & 3); ++t, ++x) *out++ = (pac[x >> 2] >> ((~x & 3) << 1)) & 3;
+  for (const uint8_t *q = pac + (x >> 2); t + 4 <= n; t += 4, x += 4, out += 4) memcpy(out, &lut.w[*q++], 4);
+  for (; t < n; ++t, ++x) *out++ = (pac[x >> 2] >> ((~x & 3) << 1)) & 3;
+}
+
 // dbset_extract_sequence (dbset.c:306-325), one database at offset 0
 inline uint32_t extract(const Bns &b, uint64_t beg, uint32_t len, uint8_t *out) {
-  uint32_t t = 0;
-  while (t < len && beg < (uint64_t)b.l_pac) out[t++] = pac_at(b, beg++);
+  if (beg >= (uint64_t)b.l_pac) return 0;
+  const uint32_t t = (uint32_t)std::min<uint64_t>(len, (uint64_t)b.l_pac - beg);
+  unpack_pac(b.pac.data(), beg, t, out);
   return t;
 }
 
@@ -298,7 +317,12 @@ inline uint32_t extract(const Dbs &d, uint64_t beg, uint32_t len, uint8_t *out) 
     const int idx = d.coord2idx((int64_t)beg);
     const RefDb &r = d.db[idx];
     uint64_t pos = beg - r.offset;
-    while (pos < (uint64_t)r.bns.l_pac && total < len) out[total++] = pac_at(r.bns, pos++);
+    if (pos < (uint64_t)r.bns.l_pac) {
+      const uint64_t k = std::min<uint64_t>(len - total, (uint64_t)r.bns.l_pac - pos);
+      unpack_pac(r.bns.pac.data(), pos, k, out + total);
+      total += (uint32_t)k;
+      pos += k;
+    }
     beg = pos + r.offset;
   }
   return total;
