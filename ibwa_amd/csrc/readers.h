@@ -61,14 +61,14 @@ struct SeqReader {
   }
   // byte classes for the sequence scan: 0 skipped (not isgraph), 1 kept, 2 ends the sequence
   static const uint8_t *seq_class() {
-    static uint8_t t[256];
-    static bool init = false;
-    if (!init) {
-      for (int c = 0; c < 256; ++c) t[c] = isgraph(c) ? 1 : 0;
-      t[(int)'>'] = t[(int)'+'] = t[(int)'@'] = 2;
-      init = true;
-    }
-    return t;
+    static const struct Tab {  // built once, thread-safely (readers run on several threads)
+      uint8_t t[256];
+      Tab() {
+        for (int c = 0; c < 256; ++c) t[c] = isgraph(c) ? 1 : 0;
+        t[(int)'>'] = t[(int)'+'] = t[(int)'@'] = 2;
+      }
+    } tab;
+    return tab.t;
   }
   // returns seq length, -1 at EOF, -2 on a truncated quality string.  Byte-for-byte the loops of
   // kseq_read, run over the buffer in bulk (runs of kept bytes are appended at once).
