@@ -26,6 +26,8 @@ Extra JSON fields (rank 0, N=1):
   extra.exact_leg -- configs[1] (10M reads, -n 0) on the same index, with its own roofline
   extra.e2e     -- the same reads end to end through the CLI (`ibwa-amd aln`: FASTQ file in, .sai out,
                    index load excluded), .sai == the timed step's hits for every read
+  extra.e2e_gz  -- the same reads as BGZF-compressed FASTQ through the CLI (inflated on the host
+                   threads, parsed on the GPU), .sai == the timed step's hits for every read
   extra.sw_leg  -- k_sw on 200k mate-rescue pairs (510 bp window x 150 bp read, configs[4]'s SW
                    shape) from the same genome: alignments/s, GCUPS over the forward cells, the
                    forward pass alone (engine option sw_stop=1) against its VALU roofline
@@ -399,7 +401,12 @@ def e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns):
     two overlapped lanes, records written in input order (bwa_aln_core, bwtaln.c:173-241).  The
     bench's engine is closed first (the CLI needs the HBM).  Reported: the CLI's wall clock, its
     phases (index load, with the device arena reserved meanwhile; align), reads/s with and without
-    them, and parity: the CLI's .sai must equal the timed step's hits for every read."""
+    them, and parity: the CLI's .sai must equal the timed step's hits for every read.
+
+    With --e2e-gz (default on) the same reads also go in as a BGZF-compressed FASTQ (`reads.fq.gz`,
+    deflate level 1 as `bgzip -l 1`, binned qualities in runs so that it compresses like real FASTQ;
+    qualities do not enter the search without -q): members inflated on the host threads (gzsrc.h),
+    records parsed on the GPU.  Returned under "gz" (bench.py puts it in extra.e2e_gz)."""
     import subprocess
     import tempfile
     from ibwa_amd import _native
@@ -429,67 +436,98 @@ def e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns):
         del pos, strand
         if L.ibwa_synth_write_fastq(fq.encode(), raw.ctypes.data, 0, n, args.read_len, threads) != 0:
             raise RuntimeError(f"cannot write {fq}")
-        del raw
         out["fastq_bytes"] = os.path.getsize(fq)
         out["fastq_write_s"] = time.perf_counter() - t
-        sai = os.path.join(d, "reads.sai")
+        fqz = None
+        gz = {}
+        if args.e2e_gz:
+            t = time.perf_counter()
+            fqz = os.path.join(d, "reads.fq.gz")
+            if L.ibwa_synth_write_fastq_gz(fqz.encode(), raw.ctypes.data, 0, n, args.read_len, threads, 1, 0, 1) != 0:
+                raise RuntimeError(f"cannot write {fqz}")
+            gz = {"workload": f"configs[2] end to end from compressed input: the same {n} x {args.read_len} bp reads "
+                              f"as BGZF FASTQ (deflate level 1, binned qualities) -> .sai, `ibwa-amd aln` (defaults), "
+                              f"one GPU",
+                  "gz_bytes": os.path.getsize(fqz), "gz_write_s": time.perf_counter() - t}
+        del raw
         import re
-        # parse-only first (IBWA_ALN_PARSE_ONLY: the file is read and parsed into groups, nothing is
-        # aligned; no arena): the ingest rate of one process
-        r = subprocess.run([CLI, "aln", *args.aln.split(), "-f", sai, pre, fq], stdout=subprocess.DEVNULL,
-                           stderr=subprocess.PIPE, timeout=600,
-                           env=dict(os.environ, IBWA_ALN_TIMES="1", IBWA_ALN_PARSE_ONLY="1", IBWA_ARENA_GB="0"))
-        err = r.stderr.decode(errors="replace")
-        m_ = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s parsing ahead", err)
-        m2 = re.search(r"parse only: (\d+) reads, ([\d.]+) s parsing", err)
-        if r.returncode == 0 and m_ and m2:
-            out["parse_only"] = {"records": int(m_.group(1)), "producer_s": float(m_.group(2)),
-                                 "records_per_s": int(m_.group(1)) / max(float(m_.group(2)), 1e-3),
-                                 "consumer_wait_s": float(m2.group(2)),
-                                 "note": "GPU parse of the whole file with nothing aligned: producer_s = the parse "
-                                         "calls' wall time (file reads overlapped); consumer_wait_s = the time the "
-                                         "group loop waited for parsed groups"}
-        env = dict(os.environ, IBWA_ALN_TIMES="1")
-        t = time.perf_counter()
-        r = subprocess.run([CLI, "aln", *args.aln.split(), "-f", sai, pre, fq], stdout=subprocess.DEVNULL,
-                           stderr=subprocess.PIPE, env=env, timeout=900)
-        wall = time.perf_counter() - t
-        err = r.stderr.decode(errors="replace")
-        if r.returncode != 0:
-            raise RuntimeError(f"ibwa-amd aln failed ({r.returncode}): {err[-800:]}")
-        phases = {}
-        for ln in err.splitlines():
-            if "wall s:" in ln:
-                for name, v in re.findall(r"([a-z][a-z .()]*?) (\d+\.\d+)", ln.split("wall s:", 1)[1]):
-                    phases[name.strip()] = float(v)
-            m_ = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s parsing ahead.*\((\d+) ms of device", ln)
-            if m_:
-                out["gpu_parse"] = {"records": int(m_.group(1)), "producer_s": float(m_.group(2)),
-                                    "device_ms": int(m_.group(3)),
-                                    "records_per_s": int(m_.group(1)) / max(float(m_.group(2)), 1e-3)}
-            m_ = re.search(r"exiting at ([\d.]+) s", ln)
-            if m_:  # the process's own clock at its end (the rest of the wall is start-up and exit)
-                out["process_clock_at_exit_s"] = float(m_.group(1))
-            m_ = re.search(r"arena on GPU 0: ([\d.]+) GB, peak use ([\d.]+) GB", ln)
-            if m_:
-                out["arena_gb"], out["arena_peak_use_gb"] = float(m_.group(1)), float(m_.group(2))
-        load = phases.get("load index", 0.0)
-        # the device arena's phase; until round 5 it also held the GPU runtime's start-up, now its own
-        arena = phases.get("device arena", 0.0) + phases.get("gpu runtime start", 0.0)
-        out.update({"wall_s": wall, "phases_s": phases, "value": n / max(wall - load - arena, 1e-9), "unit": "reads/s",
-                    "value_excl_index_load_only": n / max(wall - load, 1e-9),
-                    "value_incl_setup": n / wall,
-                    "note": "wall clock of the child process (start-up, FASTQ parse, alignment, .sai writes, exit); "
-                            "`value` excludes its 'load index' phase (.bwt/.rbwt read and relaid out on the GPU) and "
-                            "its 'gpu runtime start' and 'device arena' phases (HIP start-up and the one device "
-                            "reservation, which here waits for the driver to take back the ~200 GB this bench process "
-                            "released just before: a few ms on a fresh box, tools/alloc_bench.cpp); "
-                            "value_incl_setup counts everything"})
-        t = time.perf_counter()
-        first_bad = L.ibwa_sai_diff(sai.encode(), n, np.ascontiguousarray(n_aln, dtype=np.int32).ctypes.data,
-                                    np.ascontiguousarray(alns).ctypes.data)
-        out["parity"] = {"reads": n, "sai_equals_timed_step_hits": first_bad == -1,
-                         "first_differing_read": int(first_bad), "check_s": time.perf_counter() - t}
+
+        def run(path, res):
+            sai = os.path.join(d, "reads.sai")
+            # parse-only first (IBWA_ALN_PARSE_ONLY: the file is read (and inflated) and parsed into groups,
+            # nothing is aligned; no arena): the ingest rate of one process
+            r = subprocess.run([CLI, "aln", *args.aln.split(), "-f", sai, pre, path], stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, timeout=600,
+                               env=dict(os.environ, IBWA_ALN_TIMES="1", IBWA_ALN_PARSE_ONLY="1", IBWA_ARENA_GB="0"))
+            err = r.stderr.decode(errors="replace")
+            m_ = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s parsing ahead", err)
+            m2 = re.search(r"parse only: (\d+) reads, ([\d.]+) s parsing", err)
+            m3 = re.search(r"inflated on (\d+) host threads: ([\d.]+) GB in ([\d.]+) s", err)
+            if r.returncode == 0 and m_ and m2:
+                res["parse_only"] = {"records": int(m_.group(1)), "producer_s": float(m_.group(2)),
+                                     "records_per_s": int(m_.group(1)) / max(float(m2.group(2)), 1e-3),
+                                     "consumer_wait_s": float(m2.group(2)),
+                                     "note": "the whole file read, inflated if compressed, and parsed on the GPU with "
+                                             "nothing aligned: producer_s = the parse calls' wall time; "
+                                             "consumer_wait_s = the time the group loop waited for parsed groups "
+                                             "(records_per_s = records / consumer_wait_s)"}
+                if m3:
+                    res["parse_only"]["inflate"] = {"threads": int(m3.group(1)), "gb": float(m3.group(2)),
+                                                    "reader_thread_s": float(m3.group(3))}
+            env = dict(os.environ, IBWA_ALN_TIMES="1")
+            t = time.perf_counter()
+            r = subprocess.run([CLI, "aln", *args.aln.split(), "-f", sai, pre, path], stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, env=env, timeout=900)
+            wall = time.perf_counter() - t
+            err = r.stderr.decode(errors="replace")
+            if r.returncode != 0:
+                raise RuntimeError(f"ibwa-amd aln failed ({r.returncode}): {err[-800:]}")
+            phases = {}
+            for ln in err.splitlines():
+                if "wall s:" in ln:
+                    for name, v in re.findall(r"([a-z][a-z .()]*?) (\d+\.\d+)", ln.split("wall s:", 1)[1]):
+                        phases[name.strip()] = float(v)
+                m_ = re.search(r"input parsed on the GPUs: (\d+) records, ([\d.]+) s parsing ahead.*\((\d+) ms of device", ln)
+                if m_:
+                    res["gpu_parse"] = {"records": int(m_.group(1)), "producer_s": float(m_.group(2)),
+                                        "device_ms": int(m_.group(3)),
+                                        "records_per_s": int(m_.group(1)) / max(float(m_.group(2)), 1e-3)}
+                m_ = re.search(r"inflated on (\d+) host threads: ([\d.]+) GB in ([\d.]+) s", ln)
+                if m_:
+                    res["inflate"] = {"threads": int(m_.group(1)), "gb": float(m_.group(2)),
+                                      "reader_thread_s": float(m_.group(3))}
+                m_ = re.search(r"exiting at ([\d.]+) s", ln)
+                if m_:  # the process's own clock at its end (the rest of the wall is start-up and exit)
+                    res["process_clock_at_exit_s"] = float(m_.group(1))
+                m_ = re.search(r"arena on GPU 0: ([\d.]+) GB, peak use ([\d.]+) GB", ln)
+                if m_:
+                    res["arena_gb"], res["arena_peak_use_gb"] = float(m_.group(1)), float(m_.group(2))
+            load = phases.get("load index", 0.0)
+            # the device arena's phase; until round 5 it also held the GPU runtime's start-up, now its own
+            arena = phases.get("device arena", 0.0) + phases.get("gpu runtime start", 0.0)
+            res.update({"wall_s": wall, "phases_s": phases, "value": n / max(wall - load - arena, 1e-9),
+                        "unit": "reads/s", "value_excl_index_load_only": n / max(wall - load, 1e-9),
+                        "value_incl_setup": n / wall,
+                        "note": "wall clock of the child process (start-up, input read / inflated and parsed, "
+                                "alignment, .sai writes, exit); `value` excludes its 'load index' phase (.bwt/.rbwt "
+                                "read and relaid out on the GPU) and its 'gpu runtime start' and 'device arena' phases "
+                                "(HIP start-up and the one device reservation, which waits for the driver to take "
+                                "back the memory the previous process released); value_incl_setup counts everything"})
+            t = time.perf_counter()
+            first_bad = L.ibwa_sai_diff(sai.encode(), n, np.ascontiguousarray(n_aln, dtype=np.int32).ctypes.data,
+                                        np.ascontiguousarray(alns).ctypes.data)
+            res["parity"] = {"reads": n, "sai_equals_timed_step_hits": first_bad == -1,
+                             "first_differing_read": int(first_bad), "check_s": time.perf_counter() - t}
+            os.unlink(sai)
+
+        run(fq, out)
+        if fqz:
+            os.unlink(fq)  # page cache for the next file
+            try:
+                run(fqz, gz)
+            except Exception as e:  # the uncompressed leg's result stands
+                gz["error"] = repr(e)[:500]
+            out["gz"] = gz
         return out
     finally:
         subprocess.run(["rm", "-rf", d])
@@ -605,6 +643,8 @@ def main():
     ap.add_argument("--sa2pos", type=int, default=1, help="also time SA->coordinate of every read's first hit")
     ap.add_argument("--e2e-leg", type=int, default=1, help="also run the CLI end to end on the same reads as a "
                                                           "FASTQ file (extra.e2e)")
+    ap.add_argument("--e2e-gz", type=int, default=1, help="also run the CLI on the same reads as BGZF FASTQ "
+                                                         "(extra.e2e_gz)")
     ap.add_argument("--sw-leg", type=int, default=200_000, help="SW mate-rescue pairs for extra.sw_leg (0: off)")
     ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
     ap.add_argument("--shards", type=int, default=1,
@@ -865,6 +905,8 @@ def main():
         if args.e2e_leg and world == 1 and not exact_cfg and n_aln is not None and os.path.exists(CLI):
             # last: it closes the engine (the CLI process needs the HBM)
             leg("e2e", lambda: e2e_leg(eng, ascii_, lens, args, threads, n_aln, alns))
+            if isinstance(extra.get("e2e"), dict) and "gz" in extra["e2e"]:
+                extra["e2e_gz"] = extra["e2e"].pop("gz")
         result["extra"] = extra
         print(json.dumps(result), flush=True)
     eng.close()

@@ -87,6 +87,9 @@ def declare_host_helpers(L):
     L.ibwa_pack_nt4_mt.argtypes = [c.c_void_p, c.c_uint64, c.c_void_p, c.c_int]
     L.ibwa_synth_write_fastq.restype = c.c_int
     L.ibwa_synth_write_fastq.argtypes = [c.c_char_p, c.c_void_p, c.c_uint64, c.c_uint64, c.c_int, c.c_int]
+    L.ibwa_synth_write_fastq_gz.restype = c.c_int
+    L.ibwa_synth_write_fastq_gz.argtypes = [c.c_char_p, c.c_void_p, c.c_uint64, c.c_uint64, c.c_int, c.c_int, c.c_int,
+                                            c.c_int, c.c_int]
     L.ibwa_sai_diff.restype = c.c_int64
     L.ibwa_sai_diff.argtypes = [c.c_char_p, c.c_uint64, c.c_void_p, c.c_void_p]
     L.ibwa_encode_reads_fixed.restype = None

@@ -398,10 +398,22 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   // (Back to back, the second process waits for the driver to wipe the first one's memory whatever
   // its size: the wipe runs on the copy engine that also clears the new allocation,
   // profiles/r05_b2b*.jsonl.)
+  // FASTQ bytes of the input: the file's size, or for gzip the inflated size GzSource estimates from
+  // its first members
+  auto fastq_bytes = [](const char *path) -> double {
+    struct stat st;
+    if (!path || stat(path, &st) != 0) return 0.0;
+    if (FastqGpu::is_gzip(path)) {
+      ibwa_cli::GzSource g;
+      if (g.open(path)) return (double)g.size_hint();
+      return 4.0 * (double)st.st_size;
+    }
+    return (double)st.st_size;
+  };
+  const double in_bytes = fastq_bytes(fq_path && strcmp(fq_path, "-") ? fq_path : nullptr);
   uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
   if (!(pm && atoll(pm) > 0) && fq_dev) {
-    struct stat st;
-    const uint64_t fs = stat(fq_dev, &st) == 0 ? (uint64_t)st.st_size : 0;
+    const uint64_t fs = (uint64_t)in_bytes;
     const uint64_t per_lane = (uint64_t)n_lanes * (uint64_t)n_gpus;
     if (fs > 0 && fs <= piece * per_lane)
       piece = std::max<uint64_t>((uint64_t)256 << 20, (fs + 2 * per_lane - 1) / (2 * per_lane));
@@ -423,10 +435,9 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       return stat(f.c_str(), &st) == 0 ? (double)st.st_size : 0.0;
     };
     const double GiB = (double)(1u << 30);
-    const bool gz = fq_path && !FastqGpu::usable(fq_path) && strcmp(fq_path, "-") != 0;
     // FASTQ bytes of one GPU's group: a region's piece (equal regions of at most `piece` per GPU, as
     // FastqGpu cuts them), or (host readers) up to kGroup batches
-    const double fq = fq_path ? fbytes(fq_path) * (gz ? 4.0 : 1.0) : 0.0;
+    const double fq = in_bytes;
     double grp_b = (double)kGroup * kSub * 300.0;
     if (fq_dev) {
       const double per = (double)piece * n_gpus, n_reg = std::max(1.0, std::ceil(fq / per));
@@ -435,12 +446,12 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     const double grp = std::min(fq / n_gpus, grp_b) / GiB;
     // the read length from the first record (plain FASTQ): longer reads take the larger pool
     int first_len = 0;
-    if (fq_path && !gz && strcmp(fq_path, "-") != 0)
-      if (FILE *f = fopen(fq_path, "rb")) {
+    if (fq_path && strcmp(fq_path, "-") != 0)
+      if (gzFile f = gzopen(fq_path, "rb")) {  // (plain files are read as they are)
         char line[4096];
-        if (fgets(line, sizeof line, f) && line[0] == '@' && fgets(line, sizeof line, f))
+        if (gzgets(f, line, sizeof line) && line[0] == '@' && gzgets(f, line, sizeof line))
           first_len = (int)strcspn(line, "\r\n");
-        fclose(f);
+        gzclose(f);
       }
     const bool long_reads = first_len == 0 || first_len > 128;
     const double fixed = long_reads ? 36.0 : 30.0, per_gib = long_reads ? 20.0 : 21.5;
@@ -566,7 +577,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
         if (fg->handoff()) {  // the host readers from the first batch the device path did not take
           fprintf(stderr, "[ibwa-amd aln] the host readers take over at byte %llu\n",
                   (unsigned long long)fg->handoff_offset());
-          if (gzseek(rd.fp, (z_off_t)fg->handoff_offset(), SEEK_SET) < 0) r = -1;
+          if (!rd.in.seek(fg->handoff_offset())) r = -1;
         } else {
           dev_done = true;  // the input ended on the GPU path
         }
@@ -801,6 +812,10 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     fprintf(stderr, "[ibwa-amd aln] input parsed on the GPUs: %lld records, %.2f s parsing ahead of the alignment (%.0f ms "
                     "of device time: H2D copies + kernels)%s\n",
             (long long)fg->records(), fg->parse_s(), fg->dev_ms(), fg->handoff() ? "; the host readers took the rest" : "");
+    if (fg->gzip())
+      fprintf(stderr, "[ibwa-amd aln] %s input inflated on %d host threads: %.3f GB in %.2f s of the reader thread "
+                      "(ahead of the parse)\n",
+              fg->bgzf() ? "BGZF" : "gzip", ibwa_cli::gz_threads(), fg->input_bytes() / 1e9, fg->inflate_s());
   }
   if (parse_s > 0) {
     const int nt = fb ? ibwa_sam::host_threads() : 1;

@@ -29,7 +29,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <memory>
 #include <deque>
 #include <functional>
 #include <mutex>
@@ -37,6 +39,7 @@
 #include <thread>
 #include <vector>
 
+#include "gzsrc.h"
 #include "ibwa_aln.h"
 #include "readers.h"
 #include "sam_common.h"
@@ -54,17 +57,23 @@ struct DevGroup {
 
 class FastqGpu {
  public:
-  // true when `fn` is a regular, uncompressed file this path can take
+  // true when `fn` is a regular file this path can take: uncompressed, or gzip (inflated on the host
+  // threads by GzSource, the parse on the GPUs) unless IBWA_GZ_PARALLEL=0
   static bool usable(const char *fn) {
     if (!strcmp(fn, "-")) return false;
     struct stat st;
     if (stat(fn, &st) != 0 || !S_ISREG(st.st_mode)) return false;
+    if (!is_gzip(fn)) return true;
+    const char *pe = getenv("IBWA_GZ_PARALLEL");
+    return !(pe && atoi(pe) == 0);
+  }
+  static bool is_gzip(const char *fn) {
     FILE *f = fopen(fn, "rb");
     if (!f) return false;
     unsigned char m[2] = {0, 0};
     const size_t got = fread(m, 1, 2, f);
     fclose(f);
-    return !(got == 2 && m[0] == 0x1f && m[1] == 0x8b);  // gzip: the host readers inflate it
+    return got == 2 && m[0] == 0x1f && m[1] == 0x8b;
   }
 
   // ing: n_slots x G ingest contexts, slot-major (ing[slot * G + g] on GPU g); key_of(max_len): the
@@ -78,13 +87,21 @@ class FastqGpu {
     fd_ = open(fn, O_RDONLY);
     struct stat st;
     fsize_ = fd_ >= 0 && fstat(fd_, &st) == 0 ? (uint64_t)st.st_size : 0;
+    // gzip: the reader thread inflates each region (GzSource, on all host threads for BGZF and
+    // multi-member files) into pageable buffers; offsets are then offsets of the inflated stream, and
+    // the size an estimate until the stream ends
+    if (fd_ >= 0 && is_gzip(fn)) {
+      src_.reset(new GzSource);
+      if (!src_->open(fn)) { ok_ = false; return; }
+      fsize_ = src_->size_hint();
+    }
     // The file is mapped (IBWA_FQ_MMAP, default 1) and each region handed to the parse where it lies:
     // no pinned buffers (pinning 4.5 GB took ~1 s and unpinning it ~0.5 s at exit -- or, freed while
     // the searches ran, slowed them: profiles/r05_exit.jsonl, r05_e2e_d.json), no carry copies (a
     // region's unfinished batch is simply where the next region starts).  A reader thread faults the
     // next region's pages in while the current one is parsed.
     const char *mv = getenv("IBWA_FQ_MMAP");
-    if (fd_ >= 0 && fsize_ > 0 && !(mv && !strcmp(mv, "0"))) {
+    if (fd_ >= 0 && fsize_ > 0 && !src_ && !(mv && !strcmp(mv, "0"))) {
       void *m = mmap(nullptr, fsize_, PROT_READ, MAP_PRIVATE, fd_, 0);
       if (m != MAP_FAILED) map_ = static_cast<const char *>(m);
     }
@@ -99,7 +116,16 @@ class FastqGpu {
     for (auto &b : buf_) {
       if (map_) break;
       void *p = nullptr;
-      if (ibwa_host_alloc(carry_ + chunk_ + 64, &p)) { ok_ = false; return; }
+      if (src_) {  // pageable, huge pages (ibwa_fq_parse stages pageable blocks through pinned chunks)
+        const uint64_t sz = (carry_ + chunk_ + 64 + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+        p = aligned_alloc(2u << 20, sz);
+        if (!p) { ok_ = false; return; }
+        madvise(p, sz, MADV_HUGEPAGE);
+        pageable_ = true;
+      } else if (ibwa_host_alloc(carry_ + chunk_ + 64, &p)) {
+        ok_ = false;
+        return;
+      }
       b = static_cast<char *>(p);
     }
     ok_ = fd_ >= 0 && n_slots_ >= 1;
@@ -115,7 +141,10 @@ class FastqGpu {
     cv_.notify_all();
     if (producer_.joinable()) producer_.join();
     if (reader_.joinable()) reader_.join();
-    for (char *b : buf_) ibwa_host_free(b);
+    for (char *b : buf_) {
+      if (pageable_) free(b);
+      else ibwa_host_free(b);
+    }
     if (map_ && map_lo_ < fsize_) munmap(const_cast<char *>(map_) + map_lo_, fsize_ - map_lo_);
     if (fd_ >= 0) close(fd_);
   }
@@ -124,6 +153,10 @@ class FastqGpu {
   bool handoff() const { return handoff_; }
   uint64_t handoff_offset() const { return handoff_off_; }
   double parse_s() const { return parse_s_; }
+  double inflate_s() const { return inflate_s_; }  // reader-thread time inflating gzip input
+  bool gzip() const { return src_ != nullptr; }
+  bool bgzf() const { return src_ && src_->bgzf(); }
+  uint64_t input_bytes() const { return src_ ? src_->offset() : fsize_; }
   double dev_ms() const { return dev_ms_; }
   int64_t records() const { return n_records_; }
   // GPU g's ingest context of a group
@@ -164,6 +197,10 @@ class FastqGpu {
   uint64_t fsize_ = 0, piece_ = 0, carry_ = 0, chunk_ = 0;
   char *buf_[2] = {nullptr, nullptr};  // pinned region buffers (IBWA_FQ_MMAP=0)
   const char *map_ = nullptr;         // the mapped file
+  std::unique_ptr<GzSource> src_;     // gzip input: the inflated stream
+  bool pageable_ = false;             // buf_ from aligned_alloc (gzip), else pinned
+  bool src_end_[2] = {false, false};  // per buffer: the stream ended with it (src_)
+  bool src_stop_[2] = {false, false}; // ... or stopped at a problem gzread must see (src_)
   uint64_t map_lo_ = 0;               // ... still mapped from this offset on (consumed regions are unmapped)
   bool ok_ = false, handoff_ = false;
   uint64_t handoff_off_ = 0;
@@ -182,7 +219,7 @@ class FastqGpu {
     std::vector<uint32_t> L;
   };
   std::vector<Piece> pc_;  // per GPU, reused by every region
-  double parse_s_ = 0, dev_ms_ = 0;
+  double parse_s_ = 0, dev_ms_ = 0, inflate_s_ = 0;
   int64_t n_records_ = 0;
 
   // regions in turn, each into a slot whose previous region has been released
@@ -228,6 +265,18 @@ class FastqGpu {
   // chunk at file offset next_off_ into buf_[b] + carry_ (mapped file: its pages faulted in), by
   // several threads
   void start_read(int b) {
+    if (src_) {  // the next chunk of the inflated stream
+      char *dst = buf_[b] + carry_;
+      reader_ = std::thread([this, b, dst]() {
+        const auto t0 = std::chrono::steady_clock::now();
+        got_[b] = src_->read(reinterpret_cast<uint8_t *>(dst), chunk_);
+        next_off_ += got_[b];
+        src_stop_[b] = src_->failed();
+        src_end_[b] = src_->eof() || src_->failed();
+        inflate_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      });
+      return;
+    }
     const uint64_t off = next_off_, want = off < fsize_ ? std::min<uint64_t>(chunk_, fsize_ - off) : 0;
     next_off_ = off + want;
     if (map_) {
@@ -282,14 +331,21 @@ class FastqGpu {
     auto key_of = key_of_;
     reader_.join();
     const uint64_t got = got_[cur_];
-    const bool eof = next_off_ >= fsize_;
+    // gzip input that stopped at a problem (src_stop): its bytes so far are parsed as not the end of
+    // the input, and the host readers take over at the first batch not complete
+    const bool src_stop = src_ && src_stop_[cur_];
+    const bool eof = src_ ? src_end_[cur_] && !src_stop : next_off_ >= fsize_;
     const char *const base = map_ ? map_ + tail_file_off_ : buf_[cur_] + carry_ - tail_;
     const uint64_t n = tail_ + got;
     // the next chunk is read into the other buffer, behind its carry room, while this region is
     // parsed and aligned (that buffer's previous region went to the GPUs with its parse)
-    if (!eof) start_read(cur_ ^ 1);
+    if (!eof && !src_stop) start_read(cur_ ^ 1);
     groups_.clear();
-    if (n == 0) return END;
+    if (n == 0) {
+      if (!src_stop) return END;
+      handoff_off_ = tail_file_off_;
+      return HANDOFF;
+    }
     // pieces: one per GPU, split at strict record starts (readers.h FastqBulk::rec_at)
     const int G = (int)ing_.size();
     std::vector<uint64_t> cut(G + 1, n);
@@ -438,7 +494,7 @@ class FastqGpu {
     n_records_ += recs;
     const uint64_t file_rewind = tail_file_off_ + rewind;
     if (input_end) return END;
-    if (strict_stop || eof) {  // a record the host readers must see (not strict, truncated, ...)
+    if (strict_stop || eof || src_stop) {  // a record the host readers must see (not strict, truncated, ...)
       handoff_off_ = file_rewind;
       return HANDOFF;
     }

@@ -1,5 +1,7 @@
 // readers.h -- read input of the CLI commands (aln_main.cpp, samse_main.cpp): FASTQ/FASTA
-// (.gz) with kseq_read's record semantics and unaligned BAM with bwa_read_bam's selection.
+// (.gz) with kseq_read's record semantics and unaligned BAM with bwa_read_bam's selection.  Bytes
+// come from a ByteStream (gzsrc.h): gzip files inflated on all host threads ahead of the parse,
+// anything else through gzread as the reference reads it.
 #pragma once
 #include <ctype.h>
 #include <stdint.h>
@@ -13,11 +15,13 @@
 #include <string>
 #include <vector>
 
+#include "gzsrc.h"
+
 namespace ibwa_cli {
 
-// Buffered gz reader with the record semantics of kseq_read (kseq.h:156-195).
+// Buffered reader with the record semantics of kseq_read (kseq.h:156-195).
 struct SeqReader {
-  gzFile fp = nullptr;
+  ByteStream in;
   std::vector<char> buf = std::vector<char>(1 << 20);
   int begin = 0, end = 0;
   bool eof = false;
@@ -28,14 +32,7 @@ struct SeqReader {
   bool keep_comment = false, comment_alloc = false;
   std::string comment;
 
-  bool open(const char *fn) {
-    fp = strcmp(fn, "-") ? gzopen(fn, "r") : gzdopen(fileno(stdin), "r");
-    if (fp) gzbuffer(fp, 1 << 20);
-    return fp != nullptr;
-  }
-  ~SeqReader() {
-    if (fp) gzclose(fp);
-  }
+  bool open(const char *fn) { return in.open(fn); }
   int getc_() {
     if (!fill()) return -1;
     return (unsigned char)buf[begin++];
@@ -54,7 +51,7 @@ struct SeqReader {
       return true;
     }
     if (eof) return false;
-    end = gzread(fp, buf.data(), (unsigned)buf.size());
+    end = (int)in.read(buf.data(), buf.size());
     begin = 0;
     if (end <= 0) { eof = true; end = 0; return false; }
     return true;
@@ -240,7 +237,7 @@ struct FastqBulk {
     if (eof) return;
     while (end < blk.cap) {
       const size_t want = std::min<size_t>(blk.cap - end, (size_t)1 << 26);
-      const int got = gzread(rd.fp, blk.data() + end, (unsigned)want);
+      const int64_t got = rd.in.read(blk.data() + end, want);
       if (got <= 0) { eof = true; break; }
       end += (size_t)got;
     }
@@ -324,22 +321,21 @@ struct FastqBulk {
   }
 };
 
-// BAM input: bam_header_read / bam_read1 (bamlite.c:34-116) over gzread (a BGZF file is a
-// series of gzip members), and the record selection and decoding of bwa_read_bam
+// BAM input: bam_header_read / bam_read1 (bamlite.c:34-116) over the inflated BGZF stream (a BGZF
+// file is a series of gzip members: ByteStream inflates them on all threads), and the record
+// selection and decoding of bwa_read_bam
 // (bwaseqio.c:89-143): `which` bit 1 = read 1, 2 = read 2, 4 = neither (bwtaln.c:159-171);
 // 4-bit bases -> A/C/G/T/N, reverse-strand records reverse-complemented back, qualities
 // +33 capped at 126.  The record is handed on as FASTQ-like strings.
 struct BamReader {
-  gzFile fp = nullptr;
+  ByteStream in;
   int which = 7;
   std::string name, seq, qual;
   std::vector<uint8_t> data;
-  bool readn(void *p, int n) { return gzread(fp, p, (unsigned)n) == n; }
+  bool readn(void *p, int n) { return in.read(p, (uint64_t)n) == n; }
   bool open(const char *fn, int w) {
     which = w;
-    fp = strcmp(fn, "-") ? gzopen(fn, "r") : gzdopen(fileno(stdin), "r");
-    if (!fp) return false;
-    gzbuffer(fp, 1 << 20);
+    if (!in.open(fn)) return false;
     char magic[4];
     if (!readn(magic, 4) || memcmp(magic, "BAM\1", 4) != 0) {
       fprintf(stderr, "[bam_header_read] invalid BAM binary header (this is not a BAM file).\n");
@@ -359,9 +355,6 @@ struct BamReader {
     }
     return true;
   }
-  ~BamReader() {
-    if (fp) gzclose(fp);
-  }
   int last = 0;  // what the last read() returned
   // seq length of the next selected record, -1 at EOF, -2 on a truncated or corrupt record
   int read() { return last = read_record(); }
@@ -369,7 +362,7 @@ struct BamReader {
     static const char nt16[] = "NACNGNNNTNNNNNNN";  // bam_nt16_nt4_table (bwaseqio.c:11) as bases
     for (;;) {
       int32_t block_len = 0;
-      const int got = gzread(fp, &block_len, 4);
+      const int64_t got = in.read(&block_len, 4);
       if (got == 0) return -1;
       if (got != 4 || block_len < 32) return -2;
       uint32_t x[8];

@@ -19,6 +19,7 @@
 #include <vector>
 #include <thread>
 #include <algorithm>
+#include <zlib.h>
 
 namespace {
 
@@ -408,6 +409,139 @@ int ibwa_synth_write_fastq(const char *path, const char *seqs, uint64_t first, u
   for (auto &x : th) x.join();
   const bool ok = fclose(f) == 0 && std::find(bad.begin(), bad.end(), 1) == bad.end();
   return ok ? 0 : -1;
+}
+
+// The same records gzip-compressed, for the compressed-input legs (bench extra.e2e_gz, tests):
+// kind 0 BGZF (SAM spec §4.1: members of <= 65 280 input bytes with the 'BC' extra subfield, the
+// empty EOF member last), kind 1 plain gzip members of ~4 MiB input each (no BC field: a reader has
+// to find them), kind 2 one member.  qual_mode 0: 'I' as ibwa_synth_write_fastq; 1: binned
+// qualities in runs (four bins, NovaSeq-like), so the file compresses like real FASTQ (~4x rather
+// than ~7x).  Members are deflated on n_threads threads at `level`.
+int ibwa_synth_write_fastq_gz(const char *path, const char *seqs, uint64_t first, uint64_t n, int len,
+                              int n_threads, int qual_mode, int kind, int level) {
+  if (n_threads < 1) n_threads = 1;
+  FILE *f = fopen(path, "wb");
+  if (!f) return -1;
+  const uint64_t rec = 12 + 1 + (uint64_t)len + 3 + (uint64_t)len + 1;
+  const uint64_t mem_in = kind == 0 ? 65280 : (4u << 20);
+  auto record = [&](char *w, uint64_t r) {
+    uint64_t id = first + r;
+    w[0] = '@';
+    w[1] = 'r';
+    for (int d = 11; d >= 2; --d, id /= 10) w[d] = (char)('0' + id % 10);
+    w[12] = '\n';
+    memcpy(w + 13, seqs + r * (uint64_t)len, len);
+    memcpy(w + 13 + len, "\n+\n", 3);
+    if (qual_mode == 0) {
+      memset(w + 16 + len, 'I', len);
+    } else {
+      static const char bins[4] = {'F', ':', ',', '#'};
+      int b = 0;
+      for (int i = 0; i < len; ++i) {
+        const uint64_t x = draw(0x51, first + r, (uint64_t)i);
+        if ((x & 7) == 0) {  // a bin change every ~8 bases: mostly F, then :, then , and #
+          const uint32_t u = (uint32_t)(x >> 8) % 100;
+          b = u < 78 ? 0 : u < 92 ? 1 : u < 98 ? 2 : 3;
+        }
+        w[16 + len + i] = bins[b];
+      }
+    }
+    w[16 + 2 * len] = '\n';
+  };
+  // one member from in[0..k): gzip header (+ 'BC' for BGZF), raw deflate, CRC-32, ISIZE
+  auto member = [&](const char *in, uint64_t k, std::vector<unsigned char> &out) -> bool {
+    z_stream zs{};
+    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    const size_t h0 = out.size(), hl = kind == 0 ? 18 : 10;
+    const size_t bound = deflateBound(&zs, (uLong)k);
+    out.resize(h0 + hl + bound + 8);
+    unsigned char *h = out.data() + h0;
+    memset(h, 0, hl);
+    h[0] = 0x1f; h[1] = 0x8b; h[2] = 8; h[9] = 0xff;
+    if (kind == 0) { h[3] = 4; h[10] = 6; h[12] = 'B'; h[13] = 'C'; h[14] = 2; }
+    zs.next_in = (Bytef *)in;
+    zs.avail_in = (uInt)k;
+    zs.next_out = h + hl;
+    zs.avail_out = (uInt)bound;
+    const int r = deflate(&zs, Z_FINISH);
+    const size_t clen = bound - zs.avail_out;
+    deflateEnd(&zs);
+    if (r != Z_STREAM_END) return false;
+    const uint32_t crc = (uint32_t)crc32(0, (const Bytef *)in, (uInt)k), isz = (uint32_t)k;
+    unsigned char *t = h + hl + clen;
+    for (int i = 0; i < 4; ++i) { t[i] = (unsigned char)(crc >> (8 * i)); t[4 + i] = (unsigned char)(isz >> (8 * i)); }
+    if (kind == 0) {
+      const uint32_t bs = (uint32_t)(hl + clen + 8 - 1);
+      if (bs > 0xffff) return false;
+      h[16] = (unsigned char)bs; h[17] = (unsigned char)(bs >> 8);
+    }
+    out.resize(h0 + hl + clen + 8);
+    return true;
+  };
+  if (kind == 2) {  // one member, deflated as a stream
+    z_stream zs{};
+    if (deflateInit2(&zs, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) { fclose(f); return -1; }
+    const uint64_t step = 1u << 14;
+    std::vector<char> text(step * rec);
+    std::vector<unsigned char> out(1u << 22);
+    bool ok = true;
+    for (uint64_t a = 0; ok && a <= n; a += step) {
+      const uint64_t b = std::min(n, a + step);
+      for (uint64_t r = a; r < b; ++r) record(text.data() + (r - a) * rec, r);
+      zs.next_in = (Bytef *)text.data();
+      zs.avail_in = (uInt)((b - a) * rec);
+      const int fl = b == n ? Z_FINISH : Z_NO_FLUSH;
+      int r = Z_OK;
+      do {
+        zs.next_out = out.data();
+        zs.avail_out = (uInt)out.size();
+        r = deflate(&zs, fl);
+        const size_t k = out.size() - zs.avail_out;
+        if (r == Z_STREAM_ERROR || (k && fwrite(out.data(), 1, k, f) != k)) ok = false;
+      } while (ok && (zs.avail_out == 0 || (fl == Z_FINISH && r != Z_STREAM_END)));
+      if (b == n) break;
+    }
+    deflateEnd(&zs);
+    return fclose(f) == 0 && ok ? 0 : -1;
+  }
+  // thread t compresses records [lo, hi) into its own buffer; the buffers are written in order
+  std::vector<std::vector<unsigned char>> outb(n_threads);
+  std::vector<int> bad(n_threads, 0);
+  auto work = [&](int t) {
+    const uint64_t lo = n * t / n_threads, hi = n * (t + 1) / n_threads;
+    std::vector<char> text;
+    text.reserve(mem_in + rec);
+    std::vector<char> one(rec);
+    std::vector<unsigned char> &out = outb[t];
+    out.reserve((size_t)((hi - lo) * rec / 3));
+    for (uint64_t r = lo; r < hi; ++r) {
+      record(one.data(), r);
+      // members split inside records (a member boundary is not a record boundary in general)
+      uint64_t o = 0;
+      while (o < rec) {
+        const uint64_t k = std::min<uint64_t>(rec - o, mem_in - text.size());
+        text.insert(text.end(), one.data() + o, one.data() + o + k);
+        o += k;
+        if (text.size() == mem_in) {
+          if (!member(text.data(), text.size(), out)) { bad[t] = 1; return; }
+          text.clear();
+        }
+      }
+    }
+    if (!text.empty() && !member(text.data(), text.size(), out)) bad[t] = 1;
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < n_threads; ++t) th.emplace_back(work, t);
+  for (auto &x : th) x.join();
+  bool ok = std::find(bad.begin(), bad.end(), 1) == bad.end();
+  for (auto &b : outb)
+    if (ok && !b.empty() && fwrite(b.data(), 1, b.size(), f) != b.size()) ok = false;
+  if (ok && kind == 0) {  // the BGZF end-of-file marker
+    static const unsigned char eofb[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C',
+                                           2, 0, 0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    ok = fwrite(eofb, 1, sizeof eofb, f) == sizeof eofb;
+  }
+  return fclose(f) == 0 && ok ? 0 : -1;
 }
 
 // A .sai file (bwtaln.c:192, :227-231: 64 B header, then per read int32 n_aln and n_aln 16 B

@@ -201,3 +201,24 @@ def test_sampe_workers_equal_one_worker_on_small_batches(golden_dir, tmp_path):
             got, _ = _sampe(argv + ["-G", n], args, tmp_path / f"g{n}.sam", env)
             assert got == one, (argv, n)
     assert fell_back  # some batch took the previous batch's insert size
+
+
+def test_sampe_gzip_reads(golden_dir, tmp_path):
+    """sampe reading both ends as compressed FASTQ -- end 1 BGZF, end 2 plain multi-member gzip, both
+    inflated on the host threads (gzsrc.h) -- gives the reference's SAM on the uncompressed files."""
+    from tests import gz_util as G
+    key = sorted(MANIFEST)[0]
+    m = MANIFEST[key]
+    reads = []
+    for j, x in enumerate(m["reads"]):
+        data = open(os.path.join(golden_dir, x), "rb").read()
+        p = tmp_path / f"r{j}.fq.gz"
+        p.write_bytes(G.bgzf(data, block=9000) if j == 0 else G.multi(data, 5, 1, 30_000))
+        reads.append(str(p))
+    out = tmp_path / "out.sam"
+    r = subprocess.run([CLI, "sampe"] + m["argv"] + ["-f", str(out), os.path.join(golden_dir, m.get("prefix", "g1m")),
+                                                     *[os.path.join(golden_dir, x) for x in m["sai"]], *reads],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = _body(gzip.open(os.path.join(golden_dir, m["sam"]), "rt").read())
+    assert _body(out.read_text()) == want

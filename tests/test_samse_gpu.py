@@ -71,3 +71,22 @@ def test_samse_bulk_reader_equals_serial(golden_dir, aln_opts, tmp_path):
         outs.append(_body(out.read_text()))
     assert len(outs[0]) > 1000
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("shape", ["bgzf", "multi"])
+def test_samse_gzip_reads(golden_dir, shape, tmp_path):
+    """samse reading its FASTQ as BGZF / multi-member gzip (inflated on the host threads, gzsrc.h): the
+    SAM equals the reference's on the uncompressed file."""
+    from tests import gz_util as G
+    key = next(k for k in sorted(MANIFEST) if MANIFEST[k]["reads"].endswith(".fq") and "-B" not in MANIFEST[k]["argv"])
+    m = MANIFEST[key]
+    data = open(os.path.join(golden_dir, m["reads"]), "rb").read()
+    gz = tmp_path / "r.fq.gz"
+    gz.write_bytes(G.bgzf(data, block=7000) if shape == "bgzf" else G.multi(data, 4, 1, 20_000))
+    out = tmp_path / "out.sam"
+    r = subprocess.run([CLI, "samse"] + m["argv"] + ["-f", str(out), os.path.join(golden_dir, m.get("prefix", "g1m")),
+                                                     os.path.join(golden_dir, m["sai"]), str(gz)],
+                       capture_output=True, text=True, timeout=120, env=dict(os.environ, IBWA_GZ_THREADS="4"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = _body(gzip.open(os.path.join(golden_dir, m["sam"]), "rt").read())
+    assert _body(out.read_text()) == want
