@@ -846,16 +846,6 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     for (auto *x : ctx) ibwa_ctx_destroy(x);
     lap("index contexts");
   }
-  // IBWA_ALN_RELEASE=1 (measurement): the device arenas handed back before the process ends.  It
-  // made a process started right after this one wait 3.5-5.2 s for the driver's wipe, where one
-  // after a plain exit often did not (profiles/r05_b2b_rel*.jsonl), so the default is the plain exit
-  if (env_int("IBWA_ALN_RELEASE", 0)) {
-    const auto t = std::chrono::steady_clock::now();
-    for (int d = 0; d < n_used; ++d) (void)ibwa_release(d);
-    if (kTimes)
-      fprintf(stderr, "[ibwa-amd aln] arenas released in %.0f ms\n",
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
-  }
   if (env_int("IBWA_ALN_CLEAN_EXIT", 0) == 0 || env_int("IBWA_ALN_EXIT_PROBE", 0)) {
     if (kTimes)  // the process's own clock at its end: the rest of a timed wall is start-up and exit
       fprintf(stderr, "[ibwa-amd aln] exiting at %.3f s\n",

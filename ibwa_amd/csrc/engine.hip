@@ -86,12 +86,6 @@ struct Arena {
   bool owns(const void *p) const {
     return base && static_cast<const char *>(p) >= base && static_cast<const char *>(p) < base + size;
   }
-  char *released_base = nullptr;  // ibwa_release: the range handed back (buffers in it are dropped)
-  size_t released_size = 0;
-  bool was_released(const void *p) const {
-    return released_base && static_cast<const char *>(p) >= released_base &&
-           static_cast<const char *>(p) < released_base + released_size;
-  }
   void release(void *p, size_t n) {
     n = (n + 4095) & ~(size_t)4095;
     std::lock_guard<std::mutex> lk(mu);
@@ -172,11 +166,6 @@ struct DBuf {
     return 0;
   }
   static void free_dev(void *q, size_t n) {
-    for (Arena &a : g_arena)
-      if (a.was_released(q)) {  // its arena was handed back (ibwa_release): nothing left to free
-        dev_bytes_add(-(int64_t)n);
-        return;
-      }
     for (Arena &a : g_arena)
       if (a.owns(q)) {
         // the range may still be used by work queued on the owning context's stream (the API call
@@ -634,13 +623,13 @@ int ibwa_release(int device) {
   Arena &a = g_arena[device];
   std::lock_guard<std::mutex> lk(a.mu);
   if (!a.base) return 0;
+  // a buffer still carved from it belongs to a context that may use it again: the contexts go first
+  if (a.used > 0)
+    return fail(IBWA_EINVAL, "device %d's arena still holds %zu bytes of context buffers (destroy the contexts first)",
+                device, a.used);
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipFree(a.base));
-  // the range is gone: buffers still pointing into it are neither used nor freed again (free_dev
-  // finds no owning arena and skips pointers that were carved: released_ marks them)
-  a.released_base = a.base;
-  a.released_size = a.size;
   a.base = nullptr;
   a.size = a.used = 0;
   a.free_.clear();
@@ -691,12 +680,13 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   // last of them is destroyed: its index buffers are theirs too
   if (c->n_borrowers > 0) {
     c->destroy_pending = true;
+    g_stream = nullptr;
     return;
   }
-  if (ibwa_ctx *src = c->share_src) {
-    c->share_src = nullptr;
-    if (--src->n_borrowers == 0 && src->destroy_pending) ibwa_ctx_destroy(src);
-  }
+  // the context whose index this one borrowed is destroyed after this one's own buffers are released
+  // (their arena release synchronises this context's stream, g_stream)
+  ibwa_ctx *src = c->share_src;
+  c->share_src = nullptr;
   for (DBuf *b : {&c->h2p_in, &c->h2p_out, &c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
                   &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
@@ -714,6 +704,8 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   (void)hipStreamDestroy(c->stream);
   delete c;
+  g_stream = nullptr;  // not left naming a destroyed stream
+  if (src && --src->n_borrowers == 0 && src->destroy_pending) ibwa_ctx_destroy(src);
 }
 
 int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {

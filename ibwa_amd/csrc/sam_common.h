@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include <algorithm>
@@ -53,6 +54,25 @@ inline std::string *&msg_sink() {
   static thread_local std::string *sink = nullptr;
   return sink;
 }
+// The stderr of one sampe batch (-G workers): collected while a worker runs the batch and printed
+// when its SAM is written, in file order -- the reference's sequential order of batch messages
+inline std::string *&batch_log() {
+  static thread_local std::string *log = nullptr;
+  return log;
+}
+inline void emit(const char *s) {
+  if (std::string *b = batch_log()) b->append(s);
+  else fputs(s, stderr);
+}
+inline void elog(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+inline void elog(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  emit(buf);
+}
 inline void msg(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 inline void msg(const char *fmt, ...) {
   char buf[1024];
@@ -61,7 +81,7 @@ inline void msg(const char *fmt, ...) {
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
   if (std::string *s = msg_sink()) s->append(buf);
-  else fputs(buf, stderr);
+  else emit(buf);
 }
 // f(begin, end, thread) over [0, n) in chunks of `grain` claimed dynamically by the host threads
 // (a few costly items do not hold one thread's whole share back), with msg() output kept in the
@@ -88,7 +108,7 @@ inline void parallel_ordered(int64_t n, const std::function<void(int64_t, int64_
   work(0);
   for (auto &x : th) x.join();
   for (const std::string &x : out)
-    if (!x.empty()) fputs(x.c_str(), stderr);
+    if (!x.empty()) emit(x.c_str());
 }
 // a thread joined when it goes out of scope (the next batch's parser, on every return path)
 struct Background {
@@ -158,13 +178,36 @@ struct Amb {
   int64_t offset = 0;
   int32_t len = 0;
 };
+// 2 MiB-aligned memory advised for transparent huge pages before it is first touched: the .pac is
+// read at random (MD/NM, refinement and mate-rescue windows), and with 4 KiB pages most of those
+// reads also miss the TLB
+template <class T>
+struct HugeAlloc {
+  using value_type = T;
+  HugeAlloc() = default;
+  template <class U>
+  HugeAlloc(const HugeAlloc<U> &) {}
+  T *allocate(size_t n) {
+    const size_t huge = (size_t)2 << 20, bytes = (n * sizeof(T) + huge - 1) / huge * huge;
+    void *p = aligned_alloc(huge, bytes);
+    if (!p) throw std::bad_alloc();
+    madvise(p, bytes, MADV_HUGEPAGE);
+    return static_cast<T *>(p);
+  }
+  void deallocate(T *p, size_t) { free(p); }
+  template <class U>
+  bool operator==(const HugeAlloc<U> &) const { return true; }
+  template <class U>
+  bool operator!=(const HugeAlloc<U> &) const { return false; }
+};
+
 struct Bns {
   int64_t l_pac = 0;
   int32_t n_seqs = 0;
   uint32_t seed = 0;
   std::vector<Ann> anns;
   std::vector<Amb> ambs;
-  std::vector<uint8_t> pac;  // seq_load_pac (dbset.c:103-108): l_pac / 4 + 1 bytes
+  std::vector<uint8_t, HugeAlloc<uint8_t>> pac;  // seq_load_pac (dbset.c:103-108): l_pac / 4 + 1 bytes
 };
 
 // bns_restore_core (bntseq.c:88-140) + seq_load_pac

@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -163,6 +164,7 @@ struct PairCtx {
   const PeOpt *opt;
   const Isize *ii;
   int s_mm;
+  const int *pen;  // pairing_aux's insert-size penalty per l <= ii->high_bayesian (with ii->high)
   const ibwa_aln1_t &al(const Position &x) const {
     // a position left by an earlier pair (PosView) may index past this pair's alignments: the
     // reference reads whatever lies there; here a zero record
@@ -192,7 +194,7 @@ void pairing_aux(const PairCtx &c, Pint &pi, const Position &u, const Position &
       ((c.ii->high && l <= c.ii->high_bayesian) || (c.ii->high == 0 && l <= (uint32_t)c.opt->max_isize))) {
     uint64_t s = (uint64_t)(int64_t)(c.al(v).score + c.al(u).score);
     s *= 10;
-    if (c.ii->high) s += (int)(-4.343 * log(.5 * erfc(M_SQRT1_2 * fabs(l - c.ii->avg) / c.ii->std)) + .499);
+    if (c.ii->high) s += c.pen[l];  // (int)(-4.343 * log(.5 * erfc(M_SQRT1_2 * |l - avg| / std)) + .499)
     s = s << 32 | (uint32_t)hash_64(u.remapped_pos << 32 | v.remapped_pos);
     if (s >> 32 == pi.o_score >> 32) {
       pi.o_n += n_optimal;
@@ -346,10 +348,10 @@ int infer_isize(const std::vector<Read> &s0, const std::vector<Read> &s1, Isize 
     else ++n_rej;
     max_len = std::max(max_len, std::max(p[0]->len, p[1]->len));
   }
-  fprintf(stderr, "[infer_isize]  total rejected pairs: %d\n", n_rej);
+  elog("[infer_isize]  total rejected pairs: %d\n", n_rej);
   const int tot = (int)isizes.size();
   if (tot < 20) {
-    fprintf(stderr, "[infer_isize] fail to infer insert size: too few good pairs\n");
+    elog("[infer_isize] fail to infer insert size: too few good pairs\n");
     return -1;
   }
   {  // sorted by counting (every kept size is < 100000): the order the sums below need
@@ -382,18 +384,18 @@ int infer_isize(const std::vector<Read> &s0, const std::vector<Read> &s1, Isize 
     if (isizes[i] > ii.high_bayesian) ++n_ap;
   ii.ap_prior = .01 * (n_ap + .01) / tot;
   if (ii.ap_prior < ap_prior) ii.ap_prior = ap_prior;
-  fprintf(stderr, "[infer_isize] (25, 50, 75) percentile: (%d, %d, %d)\n", p25, p50, p75);
+  elog("[infer_isize] (25, 50, 75) percentile: (%d, %d, %d)\n", p25, p50, p75);
   if (std::isnan(ii.std) || p75 > 100000) {
     ii.low = ii.high = ii.high_bayesian = 0;
     ii.avg = ii.std = -1.0;
-    fprintf(stderr, "[infer_isize] fail to infer insert size: weird pairing\n");
+    elog("[infer_isize] fail to infer insert size: weird pairing\n");
     return -1;
   }
   for (y = 1.0; y < 10.0; y += 0.01)
     if (.5 * erfc(y / M_SQRT2) < ap_prior / L * (y * ii.std + ii.avg)) break;
   ii.high_bayesian = (uint32_t)(y * ii.std + ii.avg + .499);
-  fprintf(stderr, "[infer_isize] inferred external isize from %d pairs: %.3lf +/- %.3lf\n", n, ii.avg, ii.std);
-  fprintf(stderr, "[infer_isize] inferred maximum insert size: %u (%.2lf sigma)\n", ii.high_bayesian, y);
+  elog("[infer_isize] inferred external isize from %d pairs: %.3lf +/- %.3lf\n", n, ii.avg, ii.std);
+  elog("[infer_isize] inferred maximum insert size: %u (%.2lf sigma)\n", ii.high_bayesian, y);
   return 0;
 }
 
@@ -442,9 +444,6 @@ struct PosScratch {
 // in, kept from batch to batch.
 struct Worker {
   std::vector<ibwa_ctx_t *> ctx;  // per reference: its index, SA -> coordinate
-  // bwtcache (bwtcache.c:27-45), one per reference: positions of an interval of >= 1000 rows, keyed
-  // by (k, l) only, computed with the strand and read length of the interval's first use in the run
-  std::vector<std::unordered_map<uint64_t, std::vector<uint64_t>>> cache;
   // every pair's positions, per host thread; kept across batches (a batch holds ~10 M positions,
   // 0.5 GB: allocating, faulting in and freeing that each batch cost about as much as filling it)
   std::vector<std::vector<Position>> pstore;
@@ -467,9 +466,16 @@ struct Batch {
   // per reference: each interval of >= kMinHashWidth rows the batch uses -> (strand << 32 | read
   // length) of its first use in the run (the cached positions are computed with those)
   std::vector<std::unordered_map<uint64_t, uint64_t>> wide;
+  bool ok[2] = {true, true};  // the .sai records were read whole
 };
 
 struct Sampe {
+  // bwtcache (bwtcache.c:27-45), one per reference and shared by the -G workers: positions of an
+  // interval of >= 1000 rows, keyed by (k, l) only, computed with the strand and read length of the
+  // interval's first use in the run (Batch::wide settles those in file order, so every worker that
+  // computes an interval gets the same positions)
+  std::vector<std::unordered_map<uint64_t, std::shared_ptr<const std::vector<uint64_t>>>> wide_cache;
+  std::mutex wide_mu;
   Dbs dbs;
   std::vector<Worker> W;  // -G workers (at least one)
   std::vector<std::vector<const char *>> sai_fn;  // per reference: end 1, end 2
@@ -666,16 +672,21 @@ struct Sampe {
     return true;
   }
 
-  // The next batch of 0x40000 pairs (bwa_read_seq twice, bwape.c:466-468) and its .sai records,
-  // end 1 and end 2 on two threads, in the background: the first batch while the index loads, each
-  // later one while the batches before it are processed.
-  Batch nb;
+  // The batches of 0x40000 pairs (bwa_read_seq twice, bwape.c:466-468) with their .sai records, end
+  // 1 and end 2 on two threads, read ahead by a reader thread into a queue of up to `depth` batches:
+  // the first ones while the index loads, later ones while the batches before them are processed
+  // (with several workers one batch ahead left a worker waiting whenever two finished close together).
   size_t batch_pairs = 0x40000;  // IBWA_SAMPE_BATCH: other sizes are for tests (the SAM depends on it)
+  size_t depth = 2;              // IBWA_SAMPE_READ_AHEAD
   double rd_s[2][2] = {{0, 0}, {0, 0}};  // per end: seconds reading reads, reading .sai records
-  bool nxt_ok[2] = {true, true};
-  Background reader;
-  void read_next(Source *src) {
-    auto rd = [this, src](int j) {
+  std::mutex rq_mu;
+  std::condition_variable rq_cv;
+  std::deque<std::unique_ptr<Batch>> ready;  // read, in file order; an empty or failed one ends it
+  std::vector<std::unique_ptr<Batch>> spare;  // taken and done: buffers for the reader to refill
+  bool stop_reading = false;
+  std::thread reader;
+  void read_into(Source *src, Batch &nb) {
+    auto rd = [this, src, &nb](int j) {
       const auto t0 = std::chrono::steady_clock::now();
       nb.seqs[j].reserve(batch_pairs);
       src[j].take(nb.seqs[j], batch_pairs, std::max(1, host_threads() / 2));
@@ -685,10 +696,10 @@ struct Sampe {
       nb.flat[j].clear();
       nb.flat[j].reserve(n + n / 4);
       nb.offs[j].assign(n + 1, 0);
-      nxt_ok[j] = true;
-      for (size_t i = 0; i < n && nxt_ok[j]; ++i) {
+      nb.ok[j] = true;
+      for (size_t i = 0; i < n && nb.ok[j]; ++i) {
         nb.offs[j][i] = nb.flat[j].size();
-        nxt_ok[j] = read_alns((int)j, nb.flat[j]);
+        nb.ok[j] = read_alns((int)j, nb.flat[j]);
         nb.offs[j][i + 1] = nb.flat[j].size();
       }
       const auto t2 = std::chrono::steady_clock::now();
@@ -700,28 +711,58 @@ struct Sampe {
     t1.join();
   }
   void start_reading(Source *src) {
-    reader.start([this, src]() { read_next(src); });
+    reader = std::thread([this, src]() {
+      for (;;) {
+        std::unique_ptr<Batch> nb;
+        {
+          std::unique_lock<std::mutex> l(rq_mu);
+          rq_cv.wait(l, [&] { return stop_reading || ready.size() < depth; });
+          if (stop_reading) return;
+          if (!spare.empty()) {
+            nb = std::move(spare.back());
+            spare.pop_back();
+          } else {
+            nb.reset(new Batch);
+          }
+        }
+        read_into(src, *nb);
+        const bool last = nb->seqs[0].empty() || !nb->ok[0] || !nb->ok[1];
+        {
+          std::lock_guard<std::mutex> l(rq_mu);
+          ready.push_back(std::move(nb));
+        }
+        rq_cv.notify_all();
+        if (last) return;
+      }
+    });
+  }
+  ~Sampe() { stop_reader(); }
+  void stop_reader() {
+    {
+      std::lock_guard<std::mutex> l(rq_mu);
+      stop_reading = true;
+    }
+    rq_cv.notify_all();
+    if (reader.joinable()) reader.join();
   }
 
-  // The next batch in file order into b (its buffers swapped with the reader's for reuse), with the
+  // The next batch in file order into b (b's previous batch goes back to the reader), with the
   // decisions the reference makes in batch order; one worker at a time.  1: a batch, 0: the end, -1:
   // an error.
-  int take(Source *src, Worker &w, Batch &b, int64_t idx) {
-    reader.wait();
-    for (int j = 0; j < 2; ++j) {
-      b.seqs[j].swap(nb.seqs[j]);
-      b.flat[j].swap(nb.flat[j]);
-      b.offs[j].swap(nb.offs[j]);
+  int take(Worker &w, std::unique_ptr<Batch> &bp, int64_t idx) {
+    {
+      std::unique_lock<std::mutex> l(rq_mu);
+      if (bp) spare.push_back(std::move(bp));
+      rq_cv.wait(l, [&] { return !ready.empty(); });
+      const Batch &f = *ready.front();
+      if (f.seqs[0].empty()) return 0;  // left in the queue: the end for every worker
+      if (!f.ok[0] || !f.ok[1]) return -1;
+      bp = std::move(ready.front());
+      ready.pop_front();
     }
+    rq_cv.notify_all();
     w.ph.mark("read (wait)");
-    if (b.seqs[0].empty()) return 0;
-    if (!nxt_ok[0] || !nxt_ok[1]) return -1;
-    start_reading(src);
-    static const bool sync_read = getenv("IBWA_SAMPE_SYNC_READ") != nullptr;  // measurement: no overlap
-    if (sync_read) {
-      reader.wait();
-      w.ph.mark("read (next batch, not overlapped)");
-    }
+    Batch &b = *bp;
     if (b.seqs[1].size() != b.seqs[0].size()) {
       fprintf(stderr, "[ibwa-amd sampe] the two read files hold different numbers of reads\n");
       return -1;
@@ -776,6 +817,10 @@ struct Sampe {
   void end_turn(int n) {
     std::lock_guard<std::mutex> l(mu);
     tot += n;
+    if (std::string *b = batch_log()) {  // the batch's messages, in file order with the SAM
+      fputs(b->c_str(), stderr);
+      b->clear();
+    }
     fprintf(stderr, "[bwa_sai2sam_pe_core] %ld sequences have been processed.\n", tot);
     ++printed;
     cv.notify_all();
@@ -786,7 +831,7 @@ struct Sampe {
     cv.notify_all();
   }
 
-  int run(Source src[2], FILE *out) {
+  int run(FILE *out) {
     Out o{out, {}};
     std::mutex take_mu;
     bool end = false;
@@ -794,7 +839,7 @@ struct Sampe {
     std::vector<int> rcs(W.size(), 0);
     auto work = [&](int wi) {
       Worker &w = W[wi];
-      Batch b;  // buffers kept from batch to batch
+      std::unique_ptr<Batch> b;  // the batch in hand (its buffers go back to the reader)
       for (;;) {
         {
           std::lock_guard<std::mutex> l(take_mu);
@@ -803,7 +848,7 @@ struct Sampe {
             std::lock_guard<std::mutex> l2(mu);
             if (failed) return;
           }
-          const int t = take(src, w, b, n_taken);
+          const int t = take(w, b, n_taken);
           if (t == 0) {
             end = true;
             return;
@@ -816,7 +861,12 @@ struct Sampe {
           }
           ++n_taken;
         }
-        if (int rc = batch(w, b, o)) {
+        std::string log;  // this batch's stderr, printed with its SAM (end_turn)
+        batch_log() = &log;
+        const int brc = batch(w, *b, o);
+        batch_log() = nullptr;
+        if (!log.empty()) fputs(log.c_str(), stderr);  // an error return: what the batch said so far
+        if (int rc = brc) {
           rcs[wi] = rc;
           fail();
           return;
@@ -827,6 +877,7 @@ struct Sampe {
     for (size_t wi = 1; wi < W.size(); ++wi) th.emplace_back(work, (int)wi);
     work(0);
     for (auto &t : th) t.join();
+    stop_reader();
     for (int rc : rcs)
       if (rc) return rc;
     o.flush();
@@ -880,31 +931,28 @@ struct Sampe {
     std::vector<uint32_t> hk, hl;
     std::vector<int> hi;  // (pair, end) as 2 i + j
     {
-      // the chosen hits in (pair, end) order: counts per block of pairs, then filled in place
-      const int64_t nb = (n + 4095) / 4096;
-      std::vector<int64_t> c0(nb + 1, 0);
-      parallel_chunks(nb, [&](int64_t lo, int64_t hi_, int) {
-        for (int64_t b = lo; b < hi_; ++b) {
-          int64_t c = 0;
-          for (int64_t i = b * 4096; i < std::min<int64_t>(n, (b + 1) * 4096); ++i) c += chosen[0][i] + chosen[1][i];
-          c0[b + 1] = c;
-        }
-      });
-      for (int64_t b = 0; b < nb; ++b) c0[b + 1] += c0[b];
-      hd.resize(c0[nb]); hs.resize(c0[nb]); hk.resize(c0[nb]); hl.resize(c0[nb]); hi.resize(c0[nb]);
-      parallel_chunks(nb, [&](int64_t lo, int64_t hi_, int) {
-        for (int64_t b = lo; b < hi_; ++b) {
-          int64_t o = c0[b];
-          for (int64_t i = b * 4096; i < std::min<int64_t>(n, (b + 1) * 4096); ++i)
-            for (int j = 0; j < 2; ++j)
-              if (chosen[j][i]) {
-                const Read &p = seqs[j][i];
-                hd[o] = alns[j][i][pick[j][i].main_idx].dbidx;
-                hs[o] = (uint8_t)p.strand; hk[o] = p.sa; hl[o] = (uint32_t)p.len;
-                hi[o++] = (int)(2 * i + j);
-              }
-        }
-      });
+      // the chosen hits in (pair, end) order: counts per thread's range of pairs, then filled in place
+      // (parallel_chunks splits [0, n) the same way both times)
+      const int nt = host_threads();
+      std::vector<int64_t> c0(nt + 1, 0);
+      parallel_chunks(n, [&](int64_t lo, int64_t hi_, int t) {
+        int64_t c = 0;
+        for (int64_t i = lo; i < hi_; ++i) c += chosen[0][i] + chosen[1][i];
+        c0[t + 1] = c;
+      }, nt);
+      for (int t = 0; t < nt; ++t) c0[t + 1] += c0[t];
+      hd.resize(c0[nt]); hs.resize(c0[nt]); hk.resize(c0[nt]); hl.resize(c0[nt]); hi.resize(c0[nt]);
+      parallel_chunks(n, [&](int64_t lo, int64_t hi_, int t) {
+        int64_t o = c0[t];
+        for (int64_t i = lo; i < hi_; ++i)
+          for (int j = 0; j < 2; ++j)
+            if (chosen[j][i]) {
+              const Read &p = seqs[j][i];
+              hd[o] = alns[j][i][pick[j][i].main_idx].dbidx;
+              hs[o] = (uint8_t)p.strand; hk[o] = p.sa; hl[o] = (uint32_t)p.len;
+              hi[o++] = (int)(2 * i + j);
+            }
+      }, nt);
     }
     ph.mark("hit choice: row lists");
     std::vector<uint64_t> pos;
@@ -990,7 +1038,7 @@ struct Sampe {
       if (last_ii.avg > 0.0) ii = last_ii;
     }
     if (popt.force_isize) {
-      fprintf(stderr, "[bwa_cal_pac_pos_pe] discard insert size estimate as user's request.\n");
+      elog("[bwa_cal_pac_pos_pe] discard insert size estimate as user's request.\n");
       ii.low = ii.high = 0;
       ii.avg = ii.std = -1.0;
     }
@@ -1004,6 +1052,8 @@ struct Sampe {
     std::vector<int64_t> aslot;    // per alignment: first row in rows (-1: cached)
     hd.clear(); hs.clear(); hk.clear(); hl.clear();
     std::vector<std::pair<std::pair<int, uint64_t>, int64_t>> fill;  // new cache keys -> first row
+    // this batch's wide intervals (per reference) -> their positions in the shared cache
+    std::vector<std::unordered_map<uint64_t, std::shared_ptr<const std::vector<uint64_t>>>> bc(wide_cache.size());
     if (popt.remapping) {
       // alignment slots in (pair, end, alignment) order; the narrow intervals' rows at offsets from
       // per-pair counts, filled on the host threads; then the wide ones in pair order (the first use
@@ -1054,9 +1104,17 @@ struct Sampe {
             const uint32_t w = a.l - a.k + 1;
             if (w < kMinHashWidth) continue;
             const uint64_t key = (uint64_t)a.k << 32 | a.l;
-            if (wk.cache[al.dbidx].count(key)) continue;
+            if (bc[al.dbidx].count(key)) continue;
+            {
+              std::lock_guard<std::mutex> l(wide_mu);
+              auto it = wide_cache[al.dbidx].find(key);
+              if (it != wide_cache[al.dbidx].end()) {
+                bc[al.dbidx][key] = it->second;
+                continue;
+              }
+            }
             fill.push_back({{al.dbidx, key}, (int64_t)hk.size()});
-            wk.cache[al.dbidx][key];  // reserve: later uses in this batch share it
+            bc[al.dbidx][key];  // reserve: later uses in this batch share it
             const uint64_t use = bt.wide[al.dbidx].at(key);  // the run's first use: its strand, read length
             for (uint32_t r = 0; r < w; ++r) {
               hd.push_back(al.dbidx); hs.push_back((uint8_t)(use >> 32)); hk.push_back(a.k + r);
@@ -1069,7 +1127,11 @@ struct Sampe {
     ph.mark("rows: sa2pos kernel");
     for (auto &f : fill) {
       const uint32_t k = (uint32_t)(f.first.second >> 32), l = (uint32_t)f.first.second;
-      wk.cache[f.first.first][f.first.second].assign(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
+      auto v = std::make_shared<const std::vector<uint64_t>>(pos.begin() + f.second, pos.begin() + f.second + (l - k + 1));
+      std::lock_guard<std::mutex> lk(wide_mu);
+      // a worker that missed the same interval meanwhile computed the same positions (the first use
+      // fixes strand and length): the first one stored is kept
+      bc[f.first.first][f.first.second] = wide_cache[f.first.first].emplace(f.first.second, std::move(v)).first->second;
     }
     ph.mark("rows: cache");
     // ---- select_sai_multi's rows that the -R pass did not compute (no -R, or a cached interval):
@@ -1149,7 +1211,7 @@ struct Sampe {
               min_score = std::min(min_score, a.score);
               const uint32_t w = a.l - a.k + 1;
               const int64_t slot = aslot[row0[j][i] + (int64_t)k];
-              const uint64_t *pp = slot < 0 ? wk.cache[d].find((uint64_t)a.k << 32 | a.l)->second.data() : pos.data() + slot;
+              const uint64_t *pp = slot < 0 ? bc[d].find((uint64_t)a.k << 32 | a.l)->second->data() : pos.data() + slot;
               for (uint32_t r = 0; r < w; ++r) {
                 const uint64_t x = pp[r];
                 if (x < rdb.offset || x >= rdb.offset + (uint64_t)rdb.bns.l_pac) continue;
@@ -1276,16 +1338,23 @@ struct Sampe {
     if (getenv("IBWA_SAMPE_STATS")) {
       uint64_t tot = 0, mx = 0;
       for (int i = 0; i < n; ++i) { tot += pcnt[i]; mx = std::max<uint64_t>(mx, pcnt[i]); }
-      fprintf(stderr, "[ibwa-amd sampe] batch of %d pairs: %llu positions (max %llu per pair), %zu rows computed; "
+      elog("[ibwa-amd sampe] batch of %d pairs: %llu positions (max %llu per pair), %zu rows computed; "
               "positions pass thread-ms: rows %.0f, c1/c2 %.0f, sort %.0f\n", n, (unsigned long long)tot,
               (unsigned long long)mx, pos.size(), t_pos * 1e-6, t_cnt * 1e-6, t_sort * 1e-6);
+    }
+    // pairing_aux's penalty depends on l alone: once per batch for every l it can be asked for
+    std::vector<int> pen;
+    if (ii.high) {
+      pen.resize((size_t)ii.high_bayesian + 1);
+      for (uint32_t l = 0; l <= ii.high_bayesian; ++l)
+        pen[l] = (int)(-4.343 * log(.5 * erfc(M_SQRT1_2 * fabs(l - ii.avg) / ii.std)) + .499);
     }
     std::vector<int> chg(nth, 0);
     parallel_ordered(n, [&](int64_t lo, int64_t hi_, int th) {
       for (int64_t i = lo; i < hi_; ++i) {
         Read *p[2] = {&seqs[0][i], &seqs[1][i]};
         if (paired[i]) {
-          PairCtx c{{p[0], p[1]}, {&alns[0][i], &alns[1][i]}, &popt, &ii, gopt[1].s_mm};
+          PairCtx c{{p[0], p[1]}, {&alns[0][i], &alns[1][i]}, &popt, &ii, gopt[1].s_mm, pen.data()};
           chg[th] += find_optimal_pair(c, PosView(parr.data(), pcnt.data(), pg.data(), i));
         }
         if (popt.N_multi || popt.n_multi) {
@@ -1302,7 +1371,7 @@ struct Sampe {
     }, nth);
     int cnt_chg = 0;
     for (int x : chg) cnt_chg += x;
-    fprintf(stderr, "[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);
+    elog("[bwa_sai2sam_pe_core] changing coordinates of %d alignments.\n", cnt_chg);
     ph.mark("pairing");
     // ---- mate rescue (bwa_paired_sw) over the concatenated references
     if (int rc = paired_sw(wk, seqs, n, ii)) return rc;
@@ -1451,9 +1520,9 @@ struct Sampe {
                            n_mapped))
       return die("paired SW");
     ph.mark("paired SW: windows+SW+fix-up");
-    fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 singletons are mated.\n", (unsigned long long)n_mapped[1],
+    elog("[bwa_paired_sw] %llu out of %llu Q17 singletons are mated.\n", (unsigned long long)n_mapped[1],
             (unsigned long long)n_tot[1]);
-    fprintf(stderr, "[bwa_paired_sw] %llu out of %llu Q17 discordant pairs are fixed.\n", (unsigned long long)n_mapped[0],
+    elog("[bwa_paired_sw] %llu out of %llu Q17 discordant pairs are fixed.\n", (unsigned long long)n_mapped[0],
             (unsigned long long)n_tot[0]);
     for (int j = 0; j < 2; ++j) {
       parallel_chunks(n, [&](int64_t lo, int64_t hi, int) {
@@ -1557,13 +1626,14 @@ int sampe_main(int argc, char *argv[]) {
     }
   }
   if (const char *e = getenv("IBWA_SAMPE_BATCH")) S.batch_pairs = (size_t)std::max(1L, atol(e));
+  if (const char *e = getenv("IBWA_SAMPE_READ_AHEAD")) S.depth = (size_t)std::max(1L, atol(e));
   S.start_reading(src);
   // dbset_restore (dbset.c:135-176): references at cumulative offsets, each with its index on the
   // GPU, and (-R) its .remap table when it has one
   S.dbs.db.resize(count);
   if (n_workers < 1) n_workers = 1;
   S.W.resize(n_workers);
-  for (Worker &w : S.W) w.cache.resize(count);
+  S.wide_cache.resize(count);
   S.first_use.resize(count);
   int n_dev = 0;
   if (ibwa_device_count(&n_dev) || n_dev < 1) return die("no HIP device");
@@ -1655,10 +1725,9 @@ int sampe_main(int argc, char *argv[]) {
   if (!rg_line.empty()) head += rg_line + "\n";
   head += "@PG\tID:bwa\tPN:bwa\tVN:ibwa-amd\n";
   fwrite(head.data(), 1, head.size(), out);
-  Source *sp = src;
   S.W[0].ph.mark("load index (first batch read meanwhile)");
-  const int rc = S.run(sp, out);
-  S.reader.wait();  // a batch read ahead on an error return
+  const int rc = S.run(out);
+  S.stop_reader();  // batches read ahead on an error return
   for (int j = 0; j < 2; ++j)
     for (FILE *fp : S.fp_sai[j]) fclose(fp);
   if (out != stdout) fclose(out);

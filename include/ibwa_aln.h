@@ -80,14 +80,14 @@ int ibwa_device_bytes(int64_t *now, int64_t *peak);
  * 139: gap_init_stack / gap_destroy_stack per thread) with memory taken once per process.  A
  * hipMalloc right after another process released much of the HBM waits for the driver to wipe it;
  * reserving the arena while the index loads pays that once, overlapped.  IBWA_EINVAL if the device
- * already has one (the arena lives until the process exits). */
+ * already has one (the arena lives until the process exits or ibwa_release). */
 int ibwa_reserve(int device, uint64_t bytes);
 /* Hand the arena of `device` back to the driver now, e.g. before a long host-only phase.  The
  * driver wipes freed memory on the copy engine (~33 GB/s) and an allocation made meanwhile -- by
  * any process -- waits behind that wipe: handing a large arena back right before exit made the next
- * process wait 3.5-5.2 s where an exit holding it often did not (profiles/r05_b2b_rel*.jsonl).  Every
- * buffer carved from it becomes invalid: call it after the last use of the device's contexts
- * (destroying them afterwards is allowed and frees nothing twice). */
+ * process wait 3.5-5.2 s where an exit holding it often did not (profiles/r05_b2b_rel*.jsonl).  The
+ * contexts that carved buffers from it are destroyed first: IBWA_EINVAL while any buffer is still
+ * carved.  Afterwards ibwa_reserve may reserve a new arena. */
 int ibwa_release(int device);
 /* Free and total device memory of `device` (hipMemGetInfo), for sizing an arena. */
 int ibwa_device_memory(int device, uint64_t *free_b, uint64_t *total_b);

@@ -81,6 +81,7 @@ def lib():
         L.or_set_width_touches.argtypes = [c.c_void_p]
         L.or_set_touch_split.argtypes = [c.c_void_p, c.c_void_p]
         L.or_push_kinds.argtypes = [c.c_void_p]
+        L.or_depth_hist.argtypes = [c.c_void_p]
         L.or_exact_touches.argtypes = [c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p, c.c_void_p,
                                        c.c_int, c.c_int, c.c_int, c.c_void_p]
         L.or_aln_local_core.restype = c.c_int
@@ -348,6 +349,21 @@ def push_kinds(reset=False):
         L.or_push_kinds_reset()
     n = len(PUSH_KINDS)
     return {k: (int(out[i]), int(out[n + i]), int(out[2 * n + i])) for i, k in enumerate(PUSH_KINDS)}
+
+
+DEP_N = 64
+
+
+def depth_hist(reset=False):
+    """Instrumentation: by depth d (BWT steps from the root; the last bin holds d >= DEP_N - 1) the
+    expansions (one bwt_2occ4 each), the pops and the exact-tail steps (one bwt_2occ each) of the
+    restated bwt_match_gap calls since the last push_kinds(reset=True) (or this call's reset)."""
+    L = lib()
+    out = np.zeros(3 * DEP_N, dtype=np.uint64)
+    L.or_depth_hist(out.ctypes.data)
+    if reset:
+        L.or_push_kinds_reset()
+    return {"expansions": out[:DEP_N].copy(), "pops": out[DEP_N:2 * DEP_N].copy(), "tail_steps": out[2 * DEP_N:].copy()}
 
 
 def exact_touches(bwt0, bwt1, seqs, offs, lens, mode, K=0, jump=False):

@@ -284,12 +284,17 @@ typedef struct {
 	int phantom; /* instrumentation: can never be expanded (see gs_push) */
 	int mc;      /* instrumentation: a match child (popped right after its parent's expansion) */
 	int kind;    /* instrumentation: what pushed it (OR_K_*) */
+	int dep;     /* instrumentation: BWT steps from the root (the length of the node's reference string) */
 } entry_t;
 
 /* instrumentation: pushes / pops / expansions by kind of entry, summed over all searches since the
  * last or_push_kinds_reset (relaxed atomics; diagnostics for the GPU stack design) */
 enum { OR_K_ROOT, OR_K_INS_OPEN, OR_K_DEL_OPEN, OR_K_INS_EXT, OR_K_DEL_EXT, OR_K_MISMATCH, OR_K_MATCH, OR_K_N };
 static uint64_t g_kind_push[OR_K_N], g_kind_pop[OR_K_N], g_kind_exp[OR_K_N];
+/* instrumentation: by depth (OR_DEP_N - 1 = that or deeper) the expansions (one bwt_2occ4 each), the pops
+ * and the exact-tail steps (one bwt_2occ each) -- where the search's rank queries fall (tools/depth_stats.py) */
+#define OR_DEP_N 64
+static uint64_t g_dep_exp[OR_DEP_N], g_dep_pop[OR_DEP_N], g_dep_tail[OR_DEP_N];
 static int g_kinds_on; /* counting is off until the first reset: shared counters would serialise the threads */
 void or_push_kinds_reset(void)
 {
@@ -297,7 +302,20 @@ void or_push_kinds_reset(void)
 	memset(g_kind_push, 0, sizeof g_kind_push);
 	memset(g_kind_pop, 0, sizeof g_kind_pop);
 	memset(g_kind_exp, 0, sizeof g_kind_exp);
+	memset(g_dep_exp, 0, sizeof g_dep_exp);
+	memset(g_dep_pop, 0, sizeof g_dep_pop);
+	memset(g_dep_tail, 0, sizeof g_dep_tail);
 }
+void or_depth_hist(uint64_t out[3 * OR_DEP_N])
+{
+	int i;
+	for (i = 0; i < OR_DEP_N; ++i) {
+		out[i] = __atomic_load_n(&g_dep_exp[i], __ATOMIC_RELAXED);
+		out[OR_DEP_N + i] = __atomic_load_n(&g_dep_pop[i], __ATOMIC_RELAXED);
+		out[2 * OR_DEP_N + i] = __atomic_load_n(&g_dep_tail[i], __ATOMIC_RELAXED);
+	}
+}
+static inline int dep_bin(int d) { return d < OR_DEP_N - 1 ? d : OR_DEP_N - 1; }
 void or_push_kinds(uint64_t out[3 * OR_K_N])
 {
 	int i;
@@ -320,6 +338,7 @@ typedef struct {
 	 * rounds = sum over windows of W consecutive chains of one level of the longest chain */
 	uint32_t chains, rounds, next_mc, ch_len, win_n, win_max, win_level;
 	int next_kind; /* instrumentation: kind of the next push (OR_K_*) */
+	int next_dep;  /* instrumentation: depth of the next push */
 	uint32_t *chl, chl_n, chl_m; /* chain (length << 11 | level) in pop order, when stats are on */
 	uint64_t *hset; uint32_t hcap, hn; /* distinct (a,i,k,l) expansions, when stats are on */
 	uint32_t split_pop, touch_at_split; /* touches counted before pop number split_pop + 1 (0: off) */
@@ -423,6 +442,7 @@ static void gs_push(gstack_t *s, int a, int i, uint32_t k, uint32_t l, int n_mm,
 	p->last_diff_pos = ldp;
 	p->mc = s->next_mc; s->next_mc = 0;
 	p->kind = s->next_kind; s->next_kind = OR_K_MISMATCH;
+	p->dep = s->next_dep;
 	if (g_kinds_on) __atomic_add_fetch(&g_kind_push[p->kind], 1, __ATOMIC_RELAXED);
 	p->score = score & 0x7ff; /* info = score<<21 keeps 11 bits */
 	/* phantom: more diffs than the (non-increasing) max_diff allows, or a score the
@@ -442,7 +462,10 @@ static void gs_pop(gstack_t *s, entry_t *e)
 	bucket_t *q = s->b + s->best;
 	++s->pops;
 	*e = q->e[q->n - 1];
-	if (g_kinds_on) __atomic_add_fetch(&g_kind_pop[e->kind], 1, __ATOMIC_RELAXED);
+	if (g_kinds_on) {
+		__atomic_add_fetch(&g_kind_pop[e->kind], 1, __ATOMIC_RELAXED);
+		__atomic_add_fetch(&g_dep_pop[dep_bin(e->dep)], 1, __ATOMIC_RELAXED);
+	}
 	if (!e->phantom) --s->n_real;
 	if (!e->mc && s->hset) { /* a chain starts: record the previous one */
 		if (s->chains) {
@@ -507,6 +530,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 	stack->score_cap = 0x7fffffff;
 	stack->gape = (opt->mode & OR_MODE_GAPE) != 0;
 	stack->next_kind = OR_K_ROOT;
+	stack->next_dep = 0;
 	gs_push(stack, 0, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
 	stack->next_kind = OR_K_ROOT;
 	gs_push(stack, 1, len, 0, bwts[0]->seq_len, 0, 0, 0, ST_M, 0, opt);
@@ -543,9 +567,12 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 		else if (m == 0 && (e.state == ST_M || (opt->mode & OR_MODE_GAPE) || e.n_gape == opt->max_gape)) {
 			++stack->tails;
 			{
-				uint32_t ts0 = stack->tail_steps;
+				uint32_t ts0 = stack->tail_steps, q;
 				hit = match_exact_alt_n(bwt, i, str, &k, &l, t, &stack->tail_steps) != 0;
 				stack->ch_len += stack->tail_steps - ts0;
+				if (g_kinds_on)
+					for (q = 0; q < stack->tail_steps - ts0; ++q)
+						__atomic_add_fetch(&g_dep_tail[dep_bin(e.dep + (int)q)], 1, __ATOMIC_RELAXED);
 			}
 			if (!hit) continue;
 		}
@@ -585,7 +612,10 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 
 		--i;
 		++stack->expansions;
-		if (g_kinds_on) __atomic_add_fetch(&g_kind_exp[e.kind], 1, __ATOMIC_RELAXED);
+		if (g_kinds_on) {
+			__atomic_add_fetch(&g_kind_exp[e.kind], 1, __ATOMIC_RELAXED);
+			__atomic_add_fetch(&g_dep_exp[dep_bin(e.dep)], 1, __ATOMIC_RELAXED);
+		}
 		gs_note_exp(stack, a, i, k, l);
 		twoocc4_t(bwt, k - 1, l, ck, cl, t);
 		occ = l - k + 1;
@@ -604,16 +634,19 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 			if (e.state == ST_M) {
 				if (e.n_gapo < opt->max_gapo) {
 					stack->next_kind = OR_K_INS_OPEN;
+					stack->next_dep = e.dep;
 					gs_push(stack, a, i, k, l, e.n_mm, e.n_gapo + 1, e.n_gape, ST_I, i, opt);
 					for (j = 0; j != 4; ++j) {
 						uint32_t kk = bwt->L2[j] + ck[j] + 1, ll = bwt->L2[j] + cl[j];
 						stack->next_kind = OR_K_DEL_OPEN;
+						stack->next_dep = e.dep + 1;
 						if (kk <= ll) gs_push(stack, a, i + 1, kk, ll, e.n_mm, e.n_gapo + 1, e.n_gape, ST_D, i + 1, opt);
 					}
 				}
 			} else if (e.state == ST_I) {
 				if (e.n_gape < opt->max_gape) {
 					stack->next_kind = OR_K_INS_EXT;
+					stack->next_dep = e.dep;
 					gs_push(stack, a, i, k, l, e.n_mm, e.n_gapo, e.n_gape + 1, ST_I, i, opt);
 				}
 			} else if (e.state == ST_D) {
@@ -622,6 +655,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 						for (j = 0; j != 4; ++j) {
 							uint32_t kk = bwt->L2[j] + ck[j] + 1, ll = bwt->L2[j] + cl[j];
 							stack->next_kind = OR_K_DEL_EXT;
+							stack->next_dep = e.dep + 1;
 							if (kk <= ll) gs_push(stack, a, i + 1, kk, ll, e.n_mm, e.n_gapo, e.n_gape + 1, ST_D, i + 1, opt);
 						}
 					}
@@ -635,6 +669,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 				uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
 				stack->next_mc = !is_mm;
 				stack->next_kind = is_mm ? OR_K_MISMATCH : OR_K_MATCH;
+				stack->next_dep = e.dep + 1;
 				if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm + is_mm, e.n_gapo, e.n_gape, ST_M,
 				                      is_mm ? i : e.last_diff_pos, opt);
 			}
@@ -643,6 +678,7 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 			uint32_t kk = bwt->L2[c] + ck[c] + 1, ll = bwt->L2[c] + cl[c];
 			stack->next_mc = 1;
 			stack->next_kind = OR_K_MATCH;
+			stack->next_dep = e.dep + 1;
 			if (kk <= ll) gs_push(stack, a, i, kk, ll, e.n_mm, e.n_gapo, e.n_gape, ST_M, e.last_diff_pos, opt);
 		}
 	}

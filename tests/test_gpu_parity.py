@@ -286,3 +286,51 @@ def test_shared_index_is_frozen(golden_dir, sai_manifest):
     n2, a2 = src.aln(seqs, offs, lens, _eopt(opt))
     assert (n2 == n_aln).all() and a2.tobytes() == alns.tobytes()
     src.close()
+
+
+_ARENA_SCRIPT = r"""
+import ctypes, os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import oracle
+from ibwa_amd import engine as E
+L = E.lib()
+gold = sys.argv[2]
+recs = oracle.read_fastq_records(os.path.join(gold, "reads_r100.fq"))[:300]
+opt, _ = oracle.parse_aln_args([])
+seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+assert L.ibwa_reserve(0, 4 << 30) == 0, L.ibwa_last_error()
+def run():
+    eng = E.Engine(0)
+    eng.load_index_files(os.path.join(gold, "g1m"))
+    n_aln, alns = eng.aln(seqs, offs, lens, E.default_opt())
+    return eng, n_aln, alns
+eng, n1, a1 = run()
+used = ctypes.c_uint64()
+L.ibwa_arena_stats(0, None, ctypes.byref(used), None)
+assert used.value > 0
+# buffers are still carved: the arena cannot go
+assert L.ibwa_release(0) != 0 and b"destroy the contexts" in L.ibwa_last_error()
+eng.close()
+assert L.ibwa_release(0) == 0, L.ibwa_last_error()
+# a new arena after the release, and the same hits from contexts carved from it
+assert L.ibwa_reserve(0, 4 << 30) == 0, L.ibwa_last_error()
+eng, n2, a2 = run()
+assert (n1 == n2).all() and a1.tobytes() == a2.tobytes()
+eng.close()
+assert L.ibwa_release(0) == 0, L.ibwa_last_error()
+print("arena ok")
+"""
+
+
+def test_arena_release_refused_while_carved(golden_dir, tmp_path):
+    """ibwa_release: refused while a context still holds buffers carved from the arena
+    (they would point into freed HBM), allowed once the contexts are destroyed; a new arena can then be
+    reserved and gives the same hits.  Its own process: the arena is process-wide."""
+    import subprocess
+    import sys
+    s = tmp_path / "arena.py"
+    s.write_text(_ARENA_SCRIPT)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, str(s), root, golden_dir], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "arena ok" in r.stdout, r.stderr[-3000:]

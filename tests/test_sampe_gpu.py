@@ -197,9 +197,9 @@ def test_sampe_workers_equal_one_worker_on_small_batches(golden_dir, tmp_path):
         one, err = _sampe(argv + ["-G", "1"], args, tmp_path / "g1.sam", env)
         fell_back = fell_back or "too few good pairs" in err
         assert len(one.splitlines()) > 100
-        for n in ("2", "3"):
-            got, _ = _sampe(argv + ["-G", n], args, tmp_path / f"g{n}.sam", env)
-            assert got == one, (argv, n)
+        for n, ahead in (("2", "2"), ("3", "5"), ("2", "1")):  # IBWA_SAMPE_READ_AHEAD: batches read ahead
+            got, _ = _sampe(argv + ["-G", n], args, tmp_path / f"g{n}.sam", dict(env, IBWA_SAMPE_READ_AHEAD=ahead))
+            assert got == one, (argv, n, ahead)
     assert fell_back  # some batch took the previous batch's insert size
 
 
