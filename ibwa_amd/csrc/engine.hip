@@ -263,10 +263,6 @@ struct ibwa_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
-  // the cooperative pass over a chunk's resumed reads, overlapped with the next chunk's first pass
-  // (gap_overlap): its own stream and events, created at the first such run
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev2[6] = {};
   // index
   DBuf idx[2];
   IndexView ix[2] = {};
@@ -333,14 +329,6 @@ struct ibwa_ctx {
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
   int gap_coop = 1;
-  // overlap each first-pass chunk's cooperative pass over its resumed reads with the next chunk's
-  // first pass (two streams, two resume-state buffers), in at least gap_overlap_chunks chunks
-  // Off by default: at 50 M reads 4 overlapped chunks took 5 541 ms per step against 5 345 ms for 3
-  // sequential ones (profiles/r05_sweep_overlap.jsonl: the chunks' extra first-pass tails and the
-  // pass's own k_width cost more than the hidden cooperative-pass tails gain)
-  int gap_overlap = 0;
-  int gap_overlap_chunks = 4;
-  int64_t gap_overlap_min = 8 << 20;  // reads per chunk at least (a smaller launch is mostly tail)
   int gap_lw = 1;                    // first pass with its widths in LDS (gapped.hip LW) when they fit
   int gap_lw_min_waves = 8;          // ... in a workgroup size that keeps at least this many waves per CU
   int gap_resume = 1;                // early hand-offs leave their search state for the coop pass (LW)
@@ -364,8 +352,6 @@ struct ibwa_ctx {
   uint32_t gap_resume_cap1 = 4096;   // first-pass static slots per lane when states are left (<= gap_cap1)
   DBuf d_cw, d_ptabg;
   DBuf d_rdump, d_roff;
-  DBuf d_rdump2, c_wbuf, c_nN;  // gap_overlap: the second state buffer; the overlapped pass's own widths / N counts  // resume states (GapArgs::rdump) and per-read offsets
-  DBuf d_wbuf2, d_nN2, d_cw2;   // gap_overlap 1: the width rows of odd chunks (double-buffered)
   DBuf d_hpop;           // per read: first-pass pops before its resume state (0: none; ibwa_batch_diag 2)
   bool hpop_valid = false;
   int coop_waves_per_cu = 12;        // 13.3 KiB of LDS and 168 VGPRs per wave (3 waves per SIMD)
@@ -693,15 +679,11 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
                   &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1], &c->c_dir, &c->c_free, &c->c_hits,
                   &c->c_next, &c->c_pool, &c->c_proot, &c->c_pstore, &c->c_recb, &c->c_stg, &c->d_cw, &c->d_feat,
                   &c->d_hpop, &c->d_ordi, &c->d_ordids, &c->d_ordk, &c->d_ordtmp, &c->d_ptabg, &c->d_rdump, &c->d_roff,
-                  &c->d_selst, &c->d_seltmp, &c->d_rdump2, &c->c_wbuf, &c->c_nN, &c->fq_codes, &c->fq_lenk, &c->fq_offk,
-                  &c->d_wbuf2, &c->d_nN2, &c->d_cw2})
+                  &c->d_selst, &c->d_seltmp, &c->fq_codes, &c->fq_lenk, &c->fq_offk})
     b->release();
   if (c->fqs) c->fqs->unref();
   for (auto &b : c->sw) b.release();
   for (auto &x : c->ev) (void)hipEventDestroy(x);
-  for (auto &x : c->ev2)
-    if (x) (void)hipEventDestroy(x);
-  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   (void)hipStreamDestroy(c->stream);
   delete c;
   g_stream = nullptr;  // not left naming a destroyed stream
@@ -751,9 +733,6 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "diag") c->diag = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
-  else if (k == "gap_overlap" && value >= 0 && value <= 2) c->gap_overlap = (int)value;
-  else if (k == "gap_overlap_chunks" && value >= 2 && value <= 64) c->gap_overlap_chunks = (int)value;
-  else if (k == "gap_overlap_min" && value >= 1) c->gap_overlap_min = value;
   else if (k == "coop_waves_per_cu" && value > 0 && value <= 16) c->coop_waves_per_cu = (int)value;
   else if (k == "coop_pool_gb" && value >= 0 && value <= 256) c->coop_pool_gb = (int)value;
   else if (k == "coop_stg_room" && value >= 1 && value <= 4) c->coop_stg_room = (int)value;
@@ -1480,17 +1459,12 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     const int per_cu = std::max<int>(
         1, std::min<int>(c->gap_blocks_per_cu * 256 / block, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
     const bool resume = lw && c->gap_resume && c->gap_coop && max_len <= COOP_MAXLEN && o.n_stacks <= COOP_NSTK;
-    // Overlap (gap_overlap): chunk j's cooperative pass over its resumed reads runs on a second
-    // stream while chunk j+1's first pass runs -- the first pass fills the tail of the cooperative
-    // pass (its longest heavy reads) instead of the chip idling in it.  It needs two state buffers,
-    // so the chunks are smaller (at least gap_overlap_chunks of them); batches too small to gain are
-    // not split.
-    const int64_t ovl_chunks = std::min<int64_t>(c->gap_overlap_chunks, n / std::max<int64_t>(c->gap_overlap_min, 1));
-    const bool ovl = resume && c->gap_overlap && ovl_chunks >= 2;
+    // (Round 5 also overlapped a chunk's cooperative pass with the next chunk's first pass on a
+    // second stream; measured 3-10 % slower at 50 M reads in both of its variants, it was removed in
+    // round 6: DESIGN §4.4.1.)
     int64_t per_chunk = c->gap_reads_per_chunk;
-    if (ovl) per_chunk = std::min<int64_t>(per_chunk, (n + ovl_chunks - 1) / ovl_chunks);
-    if (c->resume_need > 0)
-      per_chunk = std::max<int64_t>(65536, std::min<int64_t>(per_chunk, (int64_t)((double)(((uint64_t)c->gap_resume_gb << 30) / 16) /
+    if (c->resume_need > 0)  // (the state buffer's bound no lower than 65 536 reads; gap_reads_per_chunk may be)
+      per_chunk = std::min<int64_t>(per_chunk, std::max<int64_t>(65536, (int64_t)((double)(((uint64_t)c->gap_resume_gb << 30) / 16) /
                                                                                    (1.15 * c->resume_need))));
     const int64_t n_chunks = (std::max<int64_t>(n, 1) + per_chunk - 1) / per_chunk;
     const int64_t chunk = (std::max<int64_t>(n, 1) + n_chunks - 1) / n_chunks;
@@ -1505,16 +1479,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (int rc = c->d_cw.ensure(chunk * (uint64_t)cw_words * 4)) return rc;
       if (int rc = c->d_ptabg.ensure(lanes * GAP_MAX_PAGES * 2)) return rc;
     }
-    // gap_overlap 1: odd chunks' width rows in a second set, so chunk j's cooperative pass reads its
-    // own first pass's rows (gap_shadow updates included) while chunk j+1's k_width writes the other
-    // set; gap_overlap 2: one set, the overlapped pass runs its own k_width and replays gap_shadow
-    const bool dbl = ovl && c->gap_overlap == 1;
-    if (dbl) {
-      if (int rc = c->d_wbuf2.ensure(chunk * A.wstride * 8)) return rc;
-      if (int rc = c->d_nN2.ensure(chunk * 2 + 2)) return rc;
-      if (lw)
-        if (int rc = c->d_cw2.ensure(chunk * (uint64_t)cw_words * 4)) return rc;
-    }
     // resume states of the early hand-offs: per read 1 + the state's offset (0: none), then per state
     // buffer its fill counter and the count of states stored
     uint64_t rd_cap = 0;
@@ -1524,8 +1488,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       rd_cap = std::min<uint64_t>(((uint64_t)c->gap_resume_gb << 30) / 16, (uint64_t)((double)chunk * per_read) + (1u << 16));
       if (c->gap_resume_records > 0) rd_cap = (uint64_t)c->gap_resume_records;
       if (int rc = c->d_rdump.ensure(rd_cap * 16)) return rc;
-      if (ovl)
-        if (int rc = c->d_rdump2.ensure(rd_cap * 16)) return rc;
       c->stats.resume_records_cap = (int64_t)rd_cap;
       if (int rc = c->d_roff.ensure(((uint64_t)n + 4) * 8)) return rc;
       HIPCHK(zero_async(c->d_roff.p, ((uint64_t)n + 4) * 8, c->stream));
@@ -1551,23 +1513,18 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     // The reads of chunk [b0, b0 + cnt) that left a resume state go through the cooperative pass right
     // after their chunk's first pass, so the state buffer holds one chunk's states at a time: a read
     // it resolves is done (status 0), one it hands on starts over in the passes below.
-    // Launch part: select the resumed reads of chunk [b0, b0 + cnt) (state buffer p), order them
-    // largest stack first, then k_coop on stream st.  Without overlap the widths and N counts are the
-    // chunk's own first-pass rows, still in place (their gap_shadow updates included); with overlap the
-    // next chunk's k_width overwrites those rows, so the pass runs its own k_width over the selected
-    // reads (c_wbuf, c_nN) and replays gap_shadow hit by hit from the states (wb_base < 0).
+    // Launch part: select the resumed reads of chunk [b0, b0 + cnt), order them largest stack first,
+    // then k_coop on stream st.  The widths and N counts are the chunk's own first-pass rows, still in
+    // place (their gap_shadow updates included).
     struct CoopRun {
       int64_t lanes = 0, b0 = 0, cnt = 0;
-      int p = 0;
       uint32_t pool_pages = 0;
       const int64_t *ids = nullptr;
     };
-    auto coop_launch = [&](int64_t b0, int64_t cnt, int p, hipStream_t st, hipEvent_t *evs, bool own_widths,
-                           CoopRun &R) -> int {
+    auto coop_launch = [&](int64_t b0, int64_t cnt, hipStream_t st, hipEvent_t *evs, CoopRun &R) -> int {
       R = CoopRun();
       R.b0 = b0;
       R.cnt = cnt;
-      R.p = p;
       size_t tb = 0;
       HIPCHK(select_resumed(c->d_roff.as<uint64_t>(), b0, cnt, c->d_status.as<uint32_t>(), nullptr, nullptr, nullptr,
                             nullptr, &tb, st));
@@ -1628,17 +1585,9 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.maxdiff_tab = A.maxdiff_tab;
       K.wstride = A.wstride;
       K.wlen1 = A.wlen1;
-      if (own_widths) {
-        if (int rc = c->c_wbuf.ensure((uint64_t)lanes * A.wstride * 8)) return rc;
-        if (int rc = c->c_nN.ensure((uint64_t)lanes * 2 + 2)) return rc;
-        K.wbuf = c->c_wbuf.as<uint2>();
-        K.wb_base = -1;
-        K.nN = c->c_nN.as<uint16_t>();
-      } else {
-        K.wbuf = (dbl && p ? c->d_wbuf2 : c->d_wbuf).as<uint2>();
-        K.wb_base = b0;
-        K.nN = (dbl && p ? c->d_nN2 : c->d_nN).as<uint16_t>();
-      }
+      K.wbuf = c->d_wbuf.as<uint2>();
+      K.wb_base = b0;
+      K.nN = c->d_nN.as<uint16_t>();
       K.stg = c->c_stg.as<uint4>();
       K.stg_log2 = stg_log2;
       K.dir = c->c_dir.as<uint32_t>();
@@ -1649,7 +1598,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.pool_next = c->c_next.as<uint32_t>();
       K.hits = c->c_hits.as<uint4>();
       K.recb = c->c_recb.as<uint4>();
-      K.rdump = (p ? c->d_rdump2 : c->d_rdump).as<uint4>();
+      K.rdump = c->d_rdump.as<uint4>();
       K.roff = c->d_roff.as<uint64_t>();
       K.hcap = hcap;
       K.max_iters = 1u << 24;
@@ -1661,29 +1610,17 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.status = c->r_status.as<uint32_t>();
       K.o = o;
       HIPCHK(hipEventRecord(evs[0], st));
-      if (own_widths) {
-        AlnArgs B = A;
-        B.ids = ids;
-        B.n = lanes;
-        B.wbuf = c->c_wbuf.as<uint2>();
-        B.nN = c->c_nN.as<uint16_t>();
-        B.cw = nullptr;  // the cooperative pass reads the full widths
-        B.feat = nullptr;
-        HIPCHK(launch_width(B, c->block, st));
-      }
       HIPCHK(hipEventRecord(evs[2], st));
       K.fix_status = c->d_status.as<uint32_t>();  // resume_fixup, as each read ends
       K.fix_roff = c->d_roff.as<uint64_t>();
-      // overlapped (stream2): its own claim counter -- the first pass of the next chunk claims with
-      // d_counter[0] meanwhile (sharing it lost and duplicated reads at 50 M reads, r05_sweep_ovl2.jsonl)
-      HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>() + (st != c->stream ? 6 : 0), blocks, st));
+      HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, st));
       HIPCHK(hipEventRecord(evs[1], st));
       return 0;
     };
     // Finish part (after the launch's kernels): the reads it resolved, the state buffer's use, and the
     // buffer's fill counter back to 0 for the chunk after next.
     auto coop_finish = [&](CoopRun &R, hipStream_t st, hipEvent_t *evs) -> int {
-      unsigned long long *rdn = c->d_roff.as<unsigned long long>() + n + 2 * R.p;
+      unsigned long long *rdn = c->d_roff.as<unsigned long long>() + n;
       if (R.lanes > 0) {
         HIPCHK(hipEventSynchronize(evs[1]));
         note_coop_pages(c, R.pool_pages);
@@ -1721,32 +1658,22 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
     auto coop_resumed = [&](int64_t b0, int64_t cnt) -> int {
       CoopRun R;
       hipEvent_t evs[4] = {c->ev[3], c->ev[4], c->ev[5], c->ev[6]};
-      if (int rc = coop_launch(b0, cnt, 0, c->stream, evs, false, R)) return rc;
+      if (int rc = coop_launch(b0, cnt, c->stream, evs, R)) return rc;
       return coop_finish(R, c->stream, evs);
     };
-    if (ovl && !c->stream2) {
-      HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-      for (auto &x : c->ev2) HIPCHK(hipEventCreate(&x));
-    }
-    CoopRun pending;         // overlap: the cooperative launch in flight on stream2
-    bool have_pending = false;
-    int64_t j_chunk = 0;
-    for (int64_t b0 = 0; b0 < n; b0 += chunk, ++j_chunk) {
+    for (int64_t b0 = 0; b0 < n; b0 += chunk) {
       const int64_t cnt = std::min(chunk, n - b0);
-      const int par = ovl ? (int)(j_chunk & 1) : 0;  // state buffer of this chunk
-      // overlap: the buffer is free once the cooperative pass of the chunk before last has finished
-      if (ovl && j_chunk >= 2) HIPCHK(hipStreamWaitEvent(c->stream, c->ev2[3 + par], 0));
       AlnArgs B = A;
       B.n = cnt;
       B.off = A.off + b0;
       B.len = A.len + b0;
-      B.wbuf = (dbl && par ? c->d_wbuf2 : c->d_wbuf).as<uint2>();
-      B.nN = (dbl && par ? c->d_nN2 : c->d_nN).as<uint16_t>();
+      B.wbuf = c->d_wbuf.as<uint2>();
+      B.nN = c->d_nN.as<uint16_t>();
       GapArgs G = gap_args(c, A, o, b0, cnt);
       G.wbuf = B.wbuf;
       G.nN = B.nN;
       if (lw) {
-        B.cw = (dbl && par ? c->d_cw2 : c->d_cw).as<uint32_t>();
+        B.cw = c->d_cw.as<uint32_t>();
         B.cw_words = cw_words;
         B.cw_rw = cw_rw;
         G.cw = B.cw;
@@ -1773,8 +1700,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.early2_iters = c->gap_early2_iters;
       G.early2_entries = c->gap_early2_entries;
       if (resume) {
-        G.rdump = (par ? c->d_rdump2 : c->d_rdump).as<uint4>();
-        G.rd_next = c->d_roff.as<unsigned long long>() + n + 2 * par;
+        G.rdump = c->d_rdump.as<uint4>();
+        G.rd_next = c->d_roff.as<unsigned long long>() + n;
         G.rd_cap = rd_cap;
         G.roff = c->d_roff.as<uint64_t>() + b0;
         G.hpop = c->d_hpop.as<uint32_t>() + b0;
@@ -1834,27 +1761,8 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
                 "seed widths %.3f candidate %.3f; exact steps %.3f (unique interval %.3f) (%.3g live lane-iterations)\n",
                 pf[11] / li, pf[12] / li, pf[13] / li, pf[14] / li, pf[15] / li, pf[17] / li, pf[18] / li, (double)pf[16]);
       }
-      if (resume_states && !ovl)
+      if (resume_states)
         if (int rc = coop_resumed(b0, cnt)) return rc;
-      if (resume_states && ovl) {
-        // the previous chunk's cooperative pass (stream2) is waited for and its results taken, then
-        // this chunk's is launched there; the next chunk's first pass (stream 1, next iteration) then
-        // fills the chip as its waves retire
-        if (have_pending) {
-          hipEvent_t evs[4] = {c->ev2[0], c->ev2[1], c->ev2[2], c->ev2[3 + pending.p]};
-          if (int rc = coop_finish(pending, c->stream2, evs)) return rc;
-          have_pending = false;
-        }
-        hipEvent_t evs[4] = {c->ev2[0], c->ev2[1], c->ev2[2], c->ev2[3 + par]};
-        if (int rc = coop_launch(b0, cnt, par, c->stream2, evs, !dbl, pending)) return rc;
-        have_pending = true;
-      }
-    }
-    if (have_pending) {
-      hipEvent_t evs[4] = {c->ev2[0], c->ev2[1], c->ev2[2], c->ev2[3 + pending.p]};
-      if (int rc = coop_finish(pending, c->stream2, evs)) return rc;
-      have_pending = false;
-      HIPCHK(hipStreamSynchronize(c->stream2));
     }
   }
   // first pass, in chunks of lanes_per_chunk reads

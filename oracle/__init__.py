@@ -359,11 +359,14 @@ def depth_hist(reset=False):
     expansions (one bwt_2occ4 each), the pops and the exact-tail steps (one bwt_2occ each) of the
     restated bwt_match_gap calls since the last push_kinds(reset=True) (or this call's reset)."""
     L = lib()
-    out = np.zeros(3 * DEP_N, dtype=np.uint64)
+    out = np.zeros(4 * DEP_N + 3, dtype=np.uint64)
     L.or_depth_hist(out.ctypes.data)
     if reset:
         L.or_push_kinds_reset()
-    return {"expansions": out[:DEP_N].copy(), "pops": out[DEP_N:2 * DEP_N].copy(), "tail_steps": out[2 * DEP_N:].copy()}
+    return {"expansions": out[:DEP_N].copy(), "pops": out[DEP_N:2 * DEP_N].copy(),
+            "tail_steps": out[2 * DEP_N:3 * DEP_N].copy(), "match_child_pops": out[3 * DEP_N:4 * DEP_N].copy(),
+            "unique_pops": int(out[4 * DEP_N]), "unique_match_child_pops": int(out[4 * DEP_N + 1]),
+            "unique_tail_steps": int(out[4 * DEP_N + 2])}
 
 
 def exact_touches(bwt0, bwt1, seqs, offs, lens, mode, K=0, jump=False):

@@ -295,6 +295,10 @@ static uint64_t g_kind_push[OR_K_N], g_kind_pop[OR_K_N], g_kind_exp[OR_K_N];
  * and the exact-tail steps (one bwt_2occ each) -- where the search's rank queries fall (tools/depth_stats.py) */
 #define OR_DEP_N 64
 static uint64_t g_dep_exp[OR_DEP_N], g_dep_pop[OR_DEP_N], g_dep_tail[OR_DEP_N];
+/* pops of match children by depth (popped right after their parent's expansion: a chain of them is what
+ * a table of the shallow intervals could fetch ahead), pops at a one-row interval and match-child pops
+ * at one (a chain that follows the text) */
+static uint64_t g_dep_mcpop[OR_DEP_N], g_uniq_pop, g_uniq_mcpop, g_uniq_tail;
 static int g_kinds_on; /* counting is off until the first reset: shared counters would serialise the threads */
 void or_push_kinds_reset(void)
 {
@@ -305,15 +309,21 @@ void or_push_kinds_reset(void)
 	memset(g_dep_exp, 0, sizeof g_dep_exp);
 	memset(g_dep_pop, 0, sizeof g_dep_pop);
 	memset(g_dep_tail, 0, sizeof g_dep_tail);
+	memset(g_dep_mcpop, 0, sizeof g_dep_mcpop);
+	g_uniq_pop = g_uniq_mcpop = g_uniq_tail = 0;
 }
-void or_depth_hist(uint64_t out[3 * OR_DEP_N])
+void or_depth_hist(uint64_t out[4 * OR_DEP_N + 3])
 {
 	int i;
 	for (i = 0; i < OR_DEP_N; ++i) {
 		out[i] = __atomic_load_n(&g_dep_exp[i], __ATOMIC_RELAXED);
 		out[OR_DEP_N + i] = __atomic_load_n(&g_dep_pop[i], __ATOMIC_RELAXED);
 		out[2 * OR_DEP_N + i] = __atomic_load_n(&g_dep_tail[i], __ATOMIC_RELAXED);
+		out[3 * OR_DEP_N + i] = __atomic_load_n(&g_dep_mcpop[i], __ATOMIC_RELAXED);
 	}
+	out[4 * OR_DEP_N] = __atomic_load_n(&g_uniq_pop, __ATOMIC_RELAXED);
+	out[4 * OR_DEP_N + 1] = __atomic_load_n(&g_uniq_mcpop, __ATOMIC_RELAXED);
+	out[4 * OR_DEP_N + 2] = __atomic_load_n(&g_uniq_tail, __ATOMIC_RELAXED);
 }
 static inline int dep_bin(int d) { return d < OR_DEP_N - 1 ? d : OR_DEP_N - 1; }
 void or_push_kinds(uint64_t out[3 * OR_K_N])
@@ -465,6 +475,11 @@ static void gs_pop(gstack_t *s, entry_t *e)
 	if (g_kinds_on) {
 		__atomic_add_fetch(&g_kind_pop[e->kind], 1, __ATOMIC_RELAXED);
 		__atomic_add_fetch(&g_dep_pop[dep_bin(e->dep)], 1, __ATOMIC_RELAXED);
+		if (e->mc) __atomic_add_fetch(&g_dep_mcpop[dep_bin(e->dep)], 1, __ATOMIC_RELAXED);
+		if (e->k == e->l) {
+			__atomic_add_fetch(&g_uniq_pop, 1, __ATOMIC_RELAXED);
+			if (e->mc) __atomic_add_fetch(&g_uniq_mcpop, 1, __ATOMIC_RELAXED);
+		}
 	}
 	if (!e->phantom) --s->n_real;
 	if (!e->mc && s->hset) { /* a chain starts: record the previous one */
@@ -570,9 +585,11 @@ static void match_gap(const or_bwt_t *const bwts[2], int len, const uint8_t *seq
 				uint32_t ts0 = stack->tail_steps, q;
 				hit = match_exact_alt_n(bwt, i, str, &k, &l, t, &stack->tail_steps) != 0;
 				stack->ch_len += stack->tail_steps - ts0;
-				if (g_kinds_on)
+				if (g_kinds_on) {
 					for (q = 0; q < stack->tail_steps - ts0; ++q)
 						__atomic_add_fetch(&g_dep_tail[dep_bin(e.dep + (int)q)], 1, __ATOMIC_RELAXED);
+					if (e.k == e.l) __atomic_add_fetch(&g_uniq_tail, stack->tail_steps - ts0, __ATOMIC_RELAXED);
+				}
 			}
 			if (!hit) continue;
 		}

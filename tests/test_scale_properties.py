@@ -141,25 +141,18 @@ def test_exact_reads_round_trip(mid_genome):
     ([], 100, 0.02, 4_000, {"gap_iter_budget": 1, "coop_pool_pages": 48}),
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "coop_pool_pages": 256}),
     ([], 100, 0.01, 8_000, {"gap_early_iters": 20, "gap_early_entries": 4, "gap_resume": 0}),
-    # each chunk's cooperative pass over its resumed reads on a second stream while the next chunk's
-    # first pass runs (two state buffers; gap_overlap 1: two sets of width rows, the pass reads its
-    # chunk's own; 2: the pass recomputes its reads' widths and replays gap_shadow from the states),
-    # in 3-4 chunks, under several options and a state buffer too small for some states
-    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 5_000,
-                             "gap_overlap_chunks": 3}),
-    ([], 150, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 2, "gap_overlap_min": 2_000,
-                             "gap_overlap_chunks": 3}),
+    # several first-pass chunks, each followed by the cooperative pass over its resumed reads (the
+    # state buffer and its fill counter reused chunk after chunk), under several options and a state
+    # buffer too small for some states
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_reads_per_chunk": 10_000}),
+    ([], 150, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_reads_per_chunk": 4_000}),
     (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4,
-                                                           "gap_overlap": 1, "gap_overlap_min": 2_000,
-                                                           "gap_overlap_chunks": 3}),
-    (["-m", "300"], 100, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 2, "gap_overlap_min": 2_000,
-                                        "gap_overlap_chunks": 3}),
-    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 2, "gap_overlap_min": 5_000,
-                             "gap_overlap_chunks": 3, "gap_resume_records": 8_000}),
-    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 5_000,
-                             "gap_overlap_chunks": 4, "gap_resume_records": 8_000}),
-    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_overlap": 1, "gap_overlap_min": 5_000,
-                             "gap_overlap_chunks": 4, "coop_pool_gb": 1})])
+                                                           "gap_reads_per_chunk": 3_000}),
+    (["-m", "300"], 100, 0.02, 12_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_reads_per_chunk": 4_000}),
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_reads_per_chunk": 7_500,
+                             "gap_resume_records": 8_000}),
+    ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_reads_per_chunk": 7_500,
+                             "coop_pool_gb": 1})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
@@ -168,8 +161,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
                 "gap_resume_entries": 300, "coop_pool_gb": 0, "gap_tail_lanes": 16, "gap_tail_iters": 200,
-                "gap_lw_min_waves": 8, "coop_pool_pages": 0, "gap_overlap_min": 8 << 20, "gap_overlap_chunks": 4,
-                "gap_overlap": 0}
+                "gap_lw_min_waves": 8, "coop_pool_pages": 0, "gap_reads_per_chunk": 16 << 20}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)

@@ -49,6 +49,7 @@ def main():
         oracle.cal_sa_reg_gap(b0, b1, seq, off[sel], lns[sel], oopt, n_threads=th)
         h = oracle.depth_hist(reset=True)
         n = max(sel.size, 1)
+        uq = {k: h.pop(k) for k in ("unique_pops", "unique_match_child_pops", "unique_tail_steps")}
         trips = h["pops"].astype(np.float64) + h["tail_steps"]
         tot = trips.sum()
         cum = np.cumsum(trips) / max(tot, 1)
@@ -56,6 +57,13 @@ def main():
         out[tag] = {"n": int(sel.size),
                     "per_read": {k: round(float(v.sum()) / n, 1) for k, v in h.items()},
                     "round_trips_per_read": round(tot / n, 1),
+                    # pops of a match child at depth < K: popped right after the parent's expansion, so a
+                    # table of shallow intervals could have fetched them with the parent's round trip
+                    "frac_round_trips_match_child_below_depth": {
+                        K: round(float(h["match_child_pops"][:K].sum()) / max(tot, 1), 4) for K in (8, 10, 12, 13, 14, 16)},
+                    "frac_round_trips_unique": round((uq["unique_pops"] + uq["unique_tail_steps"]) / max(tot, 1), 4),
+                    "frac_round_trips_unique_match_child": round(uq["unique_match_child_pops"] / max(tot, 1), 4),
+                    "frac_round_trips_unique_tail": round(uq["unique_tail_steps"] / max(tot, 1), 4),
                     "frac_round_trips_below_depth": {K: round(float(cum[K - 1]), 4) for K in (8, 10, 12, 13, 14, 15, 16, 20)},
                     "frac_expansions_below_depth": {K: round(float(exp_cum[K - 1]), 4) for K in (8, 10, 12, 13, 14, 15, 16, 20)},
                     "hist": {k: [int(x) for x in v] for k, v in h.items()}}
