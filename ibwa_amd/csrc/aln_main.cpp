@@ -825,28 +825,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   // Every record is written and every kernel has finished: the process ends here.  Tearing down the
   // contexts, the ingest slots and the pinned buffers one by one only hands back what the driver and
   // the OS reclaim at exit anyway (IBWA_ALN_CLEAN_EXIT=1 does it, for leak checkers).
-  if (env_int("IBWA_ALN_EXIT_PROBE", 0)) {
-    // measurement: what the process's teardown costs, part by part, before the _exit below
-    auto t = std::chrono::steady_clock::now();
-    auto lap = [&](const char *what) {
-      const auto u = std::chrono::steady_clock::now();
-      fprintf(stderr, "[ibwa-amd aln] exit probe: %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(u - t).count());
-      t = u;
-    };
-    fg.reset();
-    lap("ingest (file mapping, threads)");
-    pool.clear();
-    lap("record buffers");
-    for (auto *x : ing) ibwa_ctx_destroy(x);
-    ing.clear();
-    lap("ingest contexts");
-    for (int l = n_lanes - 1; l >= 1; --l)
-      for (auto *x : lctx[l]) ibwa_ctx_destroy(x);
-    lap("lane contexts");
-    for (auto *x : ctx) ibwa_ctx_destroy(x);
-    lap("index contexts");
-  }
-  if (env_int("IBWA_ALN_CLEAN_EXIT", 0) == 0 || env_int("IBWA_ALN_EXIT_PROBE", 0)) {
+  if (env_int("IBWA_ALN_CLEAN_EXIT", 0) == 0) {
     if (kTimes)  // the process's own clock at its end: the rest of a timed wall is start-up and exit
       fprintf(stderr, "[ibwa-amd aln] exiting at %.3f s\n",
               std::chrono::duration<double>(std::chrono::steady_clock::now() - g_proc_t0).count());

@@ -112,8 +112,14 @@ struct GapArgs {
   uint32_t *hpop;            // optional: per read, the pops (bwtgap.c:129) made before its state was left
   uint32_t tail_lanes;       // resume also when no read is left to claim and <= tail_lanes of the wave
   uint32_t tail_iters;       //   are busy, for a read past tail_iters iterations (0: off)
+  // Level tables (LW first pass; kmer.hip build_level_tables): per BWT the SA interval of every string
+  // of length <= tab_k + 1.  A node at depth <= tab_k is stored by its string (x = code, y = LTAB_MARK |
+  // depth) and expanded from one 32 B load of its children's intervals instead of two Occ blocks.
+  const uint2 *ltab[2];
+  uint32_t tab_k;            // 0: off
   AlnOpt o;
 };
+constexpr uint32_t LTAB_MARK = 0xFFFFFF00u;  // y >= this: a node stored by its string (no l can be: seq_len < it)
 constexpr int RD_HDR = 2;  // resume state header: {entries, hits, lowest score, stack size}, {best_score, best_cnt, max_diff, pops}
 constexpr int GAP_RING = 16;      // bucket heads of the LDS-width variant: live scores span <= 16
 constexpr int GAP_MAX_PAGES = 8;  // page-table entries per lane (global table)
@@ -270,6 +276,10 @@ hipError_t derive_isa_text(const IndexView &ix, const uint32_t *full, uint32_t *
                            hipStream_t st);
 
 hipError_t build_kmer_table(const IndexView &ix, int K, uint2 *table, uint2 *tmp, hipStream_t st);
+// first index of level d of a level table: (4^d - 1) / 3 rounded up to a multiple of 4 (level d >= 1 then
+// starts 32 B-aligned, so a node's four children are one aligned 32 B load)
+__host__ __device__ inline uint64_t ltab_off(uint32_t d) { return d == 0 ? 0ull : ((1ull << (2 * d)) - 1) / 3 + 3; }
+hipError_t build_level_tables(const IndexView &ix, int levels, uint2 *t, hipStream_t st);
 
 hipError_t relayout_reference_bwt(const uint32_t *d_ref, uint64_t n_words, uint64_t n_blocks, uint4 *d_out,
                                   hipStream_t st);

@@ -380,6 +380,11 @@ struct ibwa_ctx {
   std::vector<int32_t> h_cnt;  // per read its hits, patches included (fetch_to_host)
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
+  // level tables of the LW first pass (GapArgs::ltab): strings of length <= gap_tab_k + 1 (0: off),
+  // built with the K-mer tables (ensure_kmer)
+  DBuf ltab[2];
+  int gap_tab_k = 0;
+  int ltab_K = 0;   // tab_k of the built level tables
   int kmer_k = -1;  // requested K (-1: auto from the genome size, 0: off)
   int kmer_K = 0;   // K of the built tables
   bool kmer_valid = false;
@@ -455,6 +460,15 @@ int ensure_kmer(ibwa_ctx *c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     tmp.release();
     c->kmer_K = K;
+  }
+  c->ltab_K = 0;
+  if (c->gap_tab_k > 0) {
+    for (int s = 0; s < 2; ++s) {
+      if (int rc = c->ltab[s].ensure(ltab_off((uint32_t)c->gap_tab_k + 2) * 8)) return rc;
+      hipError_t e = build_level_tables(c->ix[s], c->gap_tab_k + 1, c->ltab[s].as<uint2>(), c->stream);
+      if (e != hipSuccess) return fail(IBWA_EHIP, "level tables: %s", hipGetErrorString(e));
+    }
+    c->ltab_K = c->gap_tab_k;
   }
   c->kmer_valid = true;
   return 0;
@@ -675,7 +689,7 @@ void ibwa_ctx_destroy(ibwa_ctx_t *c) {
   c->share_src = nullptr;
   for (DBuf *b : {&c->h2p_in, &c->h2p_out, &c->idx[0], &c->idx[1], &c->d_seq, &c->d_off, &c->d_len, &c->d_wbuf, &c->d_heads, &c->d_ent,
                   &c->d_prev, &c->d_aln, &c->d_naln, &c->d_status, &c->d_tab, &c->d_ids, &c->r_aln, &c->r_naln,
-                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
+                  &c->r_status, &c->sa_s[0], &c->sa_s[1], &c->d_counter, &c->kt[0], &c->kt[1], &c->ltab[0], &c->ltab[1], &c->d_rec, &c->o64[0], &c->o64[1], &c->d_nN, &c->d_pool, &c->d_aoff, &c->r_aoff, &c->d_iters, &c->d_prof, &c->sa_full[0], &c->sa_full[1],
                   &c->isa_full[0], &c->isa_full[1], &c->txt2[0], &c->txt2[1], &c->c_dir, &c->c_free, &c->c_hits,
                   &c->c_next, &c->c_pool, &c->c_proot, &c->c_pstore, &c->c_recb, &c->c_stg, &c->d_cw, &c->d_feat,
                   &c->d_hpop, &c->d_ordi, &c->d_ordids, &c->d_ordk, &c->d_ordtmp, &c->d_ptabg, &c->d_rdump, &c->d_roff,
@@ -698,6 +712,13 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
       if (int rc = refuse_shared(c, "option kmer_k")) return rc;
     c->kmer_k = (int)value;
     c->kmer_valid = false;
+  }
+  else if (k == "gap_tab_k" && value >= 0 && value <= 13) {
+    if (value != c->gap_tab_k) {
+      if (int rc = refuse_shared(c, "option gap_tab_k")) return rc;
+      c->kmer_valid = false;  // built with the K-mer tables
+    }
+    c->gap_tab_k = (int)value;
   }
   else if (k == "exact_blocks" && value > 0) c->exact_blocks = (int)value;
   else if (k == "lanes_per_chunk" && value > 0) c->lanes_per_chunk = value;
@@ -837,11 +858,13 @@ int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   HIPCHK(enter(dst));
   HIPCHK(hipStreamSynchronize(src->stream));  // src's structures are complete
   for (int s = 0; s < 2; ++s) {
-    for (DBuf *b : {&dst->idx[s], &dst->o64[s], &dst->kt[s], &dst->sa_s[s], &dst->sa_full[s], &dst->isa_full[s], &dst->txt2[s]})
+    for (DBuf *b : {&dst->idx[s], &dst->o64[s], &dst->kt[s], &dst->ltab[s], &dst->sa_s[s], &dst->sa_full[s], &dst->isa_full[s],
+                    &dst->txt2[s]})
       b->release();
     dst->idx[s] = src->idx[s].borrow();
     dst->o64[s] = src->o64[s].borrow();
     dst->kt[s] = src->kt[s].borrow();
+    dst->ltab[s] = src->ltab[s].borrow();
     dst->sa_s[s] = src->sa_s[s].borrow();
     dst->sa_full[s] = src->sa_full[s].borrow();
     dst->isa_full[s] = src->isa_full[s].borrow();
@@ -853,6 +876,8 @@ int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   }
   dst->kmer_k = src->kmer_k;
   dst->kmer_K = src->kmer_K;
+  dst->gap_tab_k = src->gap_tab_k;
+  dst->ltab_K = src->ltab_K;
   dst->kmer_valid = src->kmer_valid;
   dst->sa_intv = src->sa_intv;
   dst->sa_expanded = src->sa_expanded;
@@ -1682,6 +1707,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         G.ptab_g = c->d_ptabg.as<uint16_t>();
       }
       G.ent = c->d_ent.as<uint4>();
+      if (lw && c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {
+        G.ltab[0] = c->ltab[0].as<uint2>();
+        G.ltab[1] = c->ltab[1].as<uint2>();
+        G.tab_k = (uint32_t)c->ltab_K;
+      }
       G.cap1 = P0r;
       G.hit_slots = std::min<uint32_t>(c->gap_hit_slots, P0r / 2);
       G.pool = c->d_pool.as<uint4>();

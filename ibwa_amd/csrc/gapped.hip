@@ -280,6 +280,10 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
   bool seeded = false;
   const uint8_t *s = nullptr;
   bool fastrd = false;  // the read's symbols are in LDS (rdl)
+  // LW level tables (GapArgs::ltab): this read's nodes at depth <= TK are stored by their string; a read
+  // so short that a hit could come at such a depth does not use them
+  const uint32_t TK = LW ? A.tab_k : 0u;
+  bool tabok = false;
   const uint2 *W0 = nullptr, *W1 = nullptr, *SW0 = nullptr, *SW1 = nullptr;
   BMask nonempty = {0u, 0u, 0u, 0u};
   uint4 C = make_uint4(0, 0, 0, 0);
@@ -431,6 +435,17 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
           uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
           if (ok0) e0 = *sp(s0);
           if (ok1) e1 = *sp(s1);
+          // an entry stored by its string leaves with its interval (the cooperative pass knows no strings)
+          auto by_interval = [&](uint4 &x) __attribute__((always_inline)) {
+            if (LW && TK > 0 && out && x.y >= LTAB_MARK) {
+              const uint2 *tb = ((x.w >> 28) & 1u) ? A.ltab[0] : A.ltab[1];
+              const uint2 iv = tb[ltab_off(x.y & 0xFFu) + x.x];
+              x.x = iv.x;
+              x.y = iv.y;
+            }
+          };
+          by_interval(e0);
+          by_interval(e1);
           auto live = [&](const uint4 &x, uint32_t slot) __attribute__((always_inline)) {
             const int sc = (int)(((x.w >> 16) & 31u) * (uint32_t)o.s_mm + ((x.w >> 21) & 7u) * (uint32_t)o.s_gapo +
                                  ((x.w >> 24) & 15u) * (uint32_t)o.s_gape);
@@ -482,8 +497,11 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
       n_aln = 0;
       status = 0;
       seeded = len > o.seed_len;
-      ent1[0] = E::make(0u, ixv0.seq_len, len, 0, NILH, 0, 0, 0, 0, STATE_M);
-      C = E::make(0u, ixv0.seq_len, len, 0, 0u, 0, 0, 0, 1, STATE_M);
+      // (a hit needs every read symbol consumed: depth >= len - the insertions, at most 7 + 15)
+      tabok = LW && TK > 0 && len > (int)TK + 24;
+      const uint32_t root_l = tabok ? LTAB_MARK : ixv0.seq_len;  // the root by its (empty) string
+      ent1[0] = E::make(0u, root_l, len, 0, NILH, 0, 0, 0, 0, STATE_M);
+      C = E::make(0u, root_l, len, 0, 0u, 0, 0, 0, 1, STATE_M);
       ent1[1] = C;
       // every bucket head starts empty (a pop that empties a bucket writes NIL back), so a
       // push reads its bucket's head without consulting the non-empty mask
@@ -736,6 +754,10 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     const uint4 *obq = st == 2 ? (xa ? A.o64[0] : A.o64[1]) : ob;
     const uint32_t qk = st == 2 ? xk : k, ql = st == 2 ? xl : l;
     const bool qrun = (srch && i > 0) || (st == 2 && xj >= 0) || do_mat;
+    // a node stored by its string: its children's intervals from the level table (one 32 B load),
+    // and for a deletion state its own interval (the max_del_occ test); no Occ blocks
+    const bool shq = LW && TK > 0 && st == 1 && qrun && e.y >= LTAB_MARK;
+    const uint32_t sdep = e.y & 0xFFu;
     const bool qkneg = qk == 0;
     const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
     Blk bk, bl;
@@ -749,8 +771,19 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     const uint32_t na_end = ending && !end_stat ? (uint32_t)n_aln : 0u;
     unsigned long long e_pos = 0;
     if (na_end) e_pos = atomicAdd(args()->aln_next, (unsigned long long)na_end);
-    load_blk(shd ? shp : na_end ? ent1 + (P0 - 4) : obq, (shd || na_end) ? 0u : ql, qrun || shd || na_end, bl);
-    load_blk(shd ? shp + 4 : obq, shd ? 0u : qk - 1, (qrun && !qkneg && !qshare) || (shd && SHW > 8), bk);
+    load_blk(shd ? shp : na_end ? ent1 + (P0 - 4) : obq, (shd || na_end) ? 0u : ql, (qrun && !shq) || shd || na_end, bl);
+    load_blk(shd ? shp + 4 : obq, shd ? 0u : qk - 1, (qrun && !qkneg && !qshare && !shq) || (shd && SHW > 8), bk);
+    if (shq) {
+      const uint2 *tb = a ? A.ltab[0] : A.ltab[1];
+      const uint4 *ch = reinterpret_cast<const uint4 *>(tb + ltab_off(sdep + 1) + ((uint64_t)e.x << 2));
+      bl.v0 = ch[0];
+      bl.v1 = ch[1];
+      if (state == STATE_D) {
+        const uint2 own = tb[ltab_off(sdep) + e.x];
+        bl.v2.x = own.x;
+        bl.v2.y = own.y;
+      }
+    }
     // width bounds of strand a at positions i-2, i-1 and the seed pair
     const uint2 *Wa = a ? W1 : W0;
     const uint2 *SWa = a ? SW1 : SW0;
@@ -889,7 +922,10 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     // this iteration's rank queries, all four symbols: the children intervals (KK[c], LL[c])
     // of (qk, ql) -- for the exact step, the exact first step and the expansion alike
     uint4 KK = make_uint4(0, 0, 0, 0), LL = make_uint4(0, 0, 0, 0);
-    if (qrun) {
+    if (shq) {
+      KK = make_uint4(bl.v0.x, bl.v0.z, bl.v1.x, bl.v1.z);
+      LL = make_uint4(bl.v0.y, bl.v0.w, bl.v1.y, bl.v1.w);
+    } else if (qrun) {
       const uint4 cl4 = occ4_of(bl, ql);
       const uint4 ck4 = qkneg ? make_uint4(0, 0, 0, 0)
                               : make_uint4(occ_of(qshare ? bl.v0 : bk.v0, qk - 1),
@@ -899,6 +935,13 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
       KK = make_uint4(ixv0.L2[0] + ck4.x + 1, ixv0.L2[1] + ck4.y + 1, ixv0.L2[2] + ck4.z + 1, ixv0.L2[3] + ck4.w + 1);
       LL = make_uint4(ixv0.L2[0] + cl4.x, ixv0.L2[1] + cl4.y, ixv0.L2[2] + cl4.z, ixv0.L2[3] + cl4.w);
     }
+
+    // the children of a node stored by its string are stored by theirs too while their depth is <= TK
+    const bool shch = shq && sdep + 1u <= TK;
+    auto cxk = [&](uint32_t c) __attribute__((always_inline)) -> uint32_t { return shch ? (e.x << 2 | c) : pick4(KK, c); };
+    auto cxl = [&](uint32_t c) __attribute__((always_inline)) -> uint32_t {
+      return shch ? (LTAB_MARK | (sdep + 1u)) : pick4(LL, c);
+    };
 
     if (st == 2) {
       // one step of bwt_match_exact_alt (bwt.c:240-247)
@@ -959,7 +1002,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
         bump = b_end;
       }
       const uint32_t g_prev = E::prev(e);
-      const uint4 del = E::make(pick4(KK, c), pick4(LL, c), i + 1, i + 1, C_slot, e_mm, e_go, e_ge, a, STATE_D);
+      const uint4 del = E::make(cxk(c), cxl(c), i + 1, i + 1, C_slot, e_mm, e_go, e_ge, a, STATE_D);
       const uint4 grp = dmr ? E::make(k, l, i, (int)dmr, g_prev, e_mm, e_go, e_ge, a, STATE_G)
                             : E::make(k, l, i, i, g_prev, e_mm, e_go, e_ge, a, STATE_I);
       lds_heads[hidx(C_b)] = (H)slot;
@@ -998,7 +1041,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
       // ---- expansion (bwtgap.c:200-258)
       const bool pl_ = pleader();
       const int ni = i - 1;
-      const uint32_t occ = l - k + 1;
+      const uint32_t occ = shq ? bl.v2.y - bl.v2.x + 1 : l - k + 1;  // (by string: its own interval, loaded for STATE_D)
       bool allow_diff = true, allow_M = true;
       if (ni > 0) {
         // width[ni-1] = position i-2, width[ni] = position i-1
@@ -1131,8 +1174,8 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
           for (int j = 0; j < 5; ++j) {
             if (vg & (1u << j)) {
               const uint32_t slot = slot_at(t++);
-              const uint32_t pk = j == 0 ? k : j == 1 ? KK.x : j == 2 ? KK.y : j == 3 ? KK.z : KK.w;
-              const uint32_t pl = j == 0 ? l : j == 1 ? LL.x : j == 2 ? LL.y : j == 3 ? LL.z : LL.w;
+              const uint32_t pk = j == 0 ? k : cxk((uint32_t)j - 1u);
+              const uint32_t pl = j == 0 ? l : cxl((uint32_t)j - 1u);
               const int pi = j == 0 ? ni : ni + 1;
               const bool grp = j == 0 && dmask;
               last = E::make(pk, pl, pi, grp ? (int)dmask : pi, link, e_mm, n_gapo, n_gape, a,
@@ -1156,7 +1199,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
             if (vmm & (1u << j)) {
               const uint32_t slot = slot_at(t++);
               const uint32_t c = (csym + (uint32_t)j - 4u) & 3u;
-              last = E::make(pick4(KK, c), pick4(LL, c), ni, ni, link, e_mm + 1, e_go, e_ge, a, STATE_M);
+              last = E::make(cxk(c), cxl(c), ni, ni, link, e_mm + 1, e_go, e_ge, a, STATE_M);
               *slot_ptr(slot) = last;
               link = slot;
             }
@@ -1169,7 +1212,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
         if (has_match_ch) {
           const uint32_t slot = slot_at(t++);
           const uint32_t hd = hB;
-          const uint4 ne = E::make(pick4(KK, csym), pick4(LL, csym), ni, ldp, hd, e_mm, e_go, e_ge, a, STATE_M);
+          const uint4 ne = E::make(cxk(csym), cxl(csym), ni, ldp, hd, e_mm, e_go, e_ge, a, STATE_M);
           lds_heads[hidx(sc_base)] = (H)slot;
           if ((cfl & 6u) == 6u) *slot_ptr(D_slot) = D;
           D = C;

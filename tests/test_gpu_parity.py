@@ -55,6 +55,26 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path, gappe
     assert not bad, bad
 
 
+@pytest.mark.parametrize("tab_k", [12, 6])
+def test_sai_goldens_level_tables(golden_dir, sai_manifest, gpu_engine, tab_k):
+    """The first pass with its shallow nodes stored by their strings and expanded from the level
+    tables (GapArgs::ltab, gap_tab_k): every golden .sai of the option matrix, bit for bit."""
+    gpu_engine.set_option("gap_tab_k", tab_k)
+    bad = []
+    try:
+        for key, m in sorted(sai_manifest.items()):
+            opt, _ = oracle.parse_aln_args(m["argv"])
+            recs = oracle.read_fastq_records(os.path.join(golden_dir, m["reads"]))
+            seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+            n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+            got = oracle.sai_bytes(opt, n_aln, alns)
+            if not oracle.sai_body_equal(got, open(os.path.join(golden_dir, key + ".sai"), "rb").read()):
+                bad.append(key)
+    finally:
+        gpu_engine.set_option("gap_tab_k", 0)
+    assert not bad, bad
+
+
 def test_fetch_sai_equals_fetch(golden_dir, sai_manifest, gpu_engine):
     """ibwa_batch_fetch_sai (the CLI's writer input: records serialised by host threads into the
     caller's buffer) == the .sai body built from ibwa_batch_fetch, == the reference's golden; a buffer

@@ -152,7 +152,18 @@ def test_exact_reads_round_trip(mid_genome):
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_reads_per_chunk": 7_500,
                              "gap_resume_records": 8_000}),
     ([], 100, 0.01, 30_000, {"gap_resume_iters": 20, "gap_resume_entries": 4, "gap_reads_per_chunk": 7_500,
-                             "coop_pool_gb": 1})])
+                             "coop_pool_gb": 1}),
+    # the first pass with its shallow nodes stored by their strings (level tables, gap_tab_k): alone,
+    # with resume states that carry such entries to the cooperative pass (converted to intervals), with
+    # gaps, seeds, long deletions, 150 bp, and every read leaving its state in the launch's tail
+    ([], 100, 0.01, 30_000, {"gap_tab_k": 12}),
+    ([], 100, 0.02, 20_000, {"gap_tab_k": 12, "gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-n", "3", "-o", "2", "-e", "3"], 100, 0.02, 8_000, {"gap_tab_k": 10, "gap_resume_iters": 20,
+                                                          "gap_resume_entries": 4}),
+    (["-l", "20", "-k", "1"], 100, 0.02, 8_000, {"gap_tab_k": 8, "gap_resume_iters": 20, "gap_resume_entries": 4}),
+    (["-L", "-d", "30"], 100, 0.02, 8_000, {"gap_tab_k": 11, "gap_resume_iters": 20, "gap_resume_entries": 4}),
+    ([], 150, 0.02, 8_000, {"gap_tab_k": 13, "gap_resume_iters": 20, "gap_resume_entries": 4}),
+    ([], 100, 0.01, 30_000, {"gap_tab_k": 12, "gap_tail_lanes": 64, "gap_tail_iters": 5})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
     seq, off, lns, _, _ = reads(ascii_, lens, 5 + n, n, ln, sub, 0.05)
@@ -161,7 +172,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
                 "gap_resume_entries": 300, "coop_pool_gb": 0, "gap_tail_lanes": 16, "gap_tail_iters": 200,
-                "gap_lw_min_waves": 8, "coop_pool_pages": 0, "gap_reads_per_chunk": 16 << 20}
+                "gap_lw_min_waves": 8, "coop_pool_pages": 0, "gap_reads_per_chunk": 16 << 20, "gap_tab_k": 0}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)

@@ -111,6 +111,10 @@ def run(argv, timeout=1800, env=None, save_stderr=None):
         m = re.search(r"exiting at ([\d.]+) s", ln)
         if m:
             phases["exiting at"] = float(m.group(1))
+        m = re.search(r"arena on GPU 0: ([\d.]+) GB, peak use ([\d.]+) GB", ln)
+        if m:
+            log("  cli:", ln.strip())
+            phases["arena_gb"], phases["arena_peak_use_gb"] = float(m.group(1)), float(m.group(2))
         m = re.search(r"device memory: peak ([\d.]+) GB", ln)
         if m:
             log("  cli:", ln.strip())
