@@ -455,7 +455,13 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       }
     const bool long_reads = first_len == 0 || first_len > 128;
     const double fixed = long_reads ? 36.0 : 30.0, per_gib = long_reads ? 20.0 : 21.5;
-    const double need_gb = 7.5 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
+    // the first pass's level tables (engine gap_tab_k, auto): 2 x 8 B x ((4^(K+2) - 1) / 3) for the K that
+    // strings of length K + 1 still mostly occur at (5.7 GB for a GRCh37-sized genome)
+    const double seq_len = 4.0 * fbytes(prefix + ".bwt");
+    int tab_k = 0;
+    while (tab_k < 13 && std::ldexp(1.0, 2 * (tab_k + 1)) <= seq_len) ++tab_k;
+    const double ltab_gb = tab_k ? 2.0 * 8.0 * (std::ldexp(1.0, 2 * (tab_k + 2)) / 3.0) / GiB : 0.0;
+    const double need_gb = ltab_gb + 7.5 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
                            n_lanes * (std::min(fixed, 2.0 * fixed * grp) + per_gib * grp) + 1.7 * grp +
                            (n_lanes + 3) * 0.8 * grp + 2.0;
     const char *ag = getenv("IBWA_ARENA_GB");

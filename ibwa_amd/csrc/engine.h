@@ -186,6 +186,10 @@ struct CoopArgs {
   // after it: its gap_shadow updates are in them, so a resumed read does not replay them); -1: per
   // launch read (k_width run for this launch)
   int64_t wb_base;
+  // level tables of the first pass (GapArgs::ltab, tab_k): nodes at depth <= tab_k stored by their
+  // strings (resume states hand them on so), expanded and stepped from the tables; 0: off
+  const uint2 *ltab[2];
+  uint32_t tab_k;
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);

@@ -380,10 +380,12 @@ struct ibwa_ctx {
   std::vector<int32_t> h_cnt;  // per read its hits, patches included (fetch_to_host)
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
-  // level tables of the LW first pass (GapArgs::ltab): strings of length <= gap_tab_k + 1 (0: off),
-  // built with the K-mer tables (ensure_kmer)
+  // level tables of the LW first pass (GapArgs::ltab): strings of length <= gap_tab_k + 1 (0: off;
+  // -1: auto, floor(log4(n)) up to 13 -- 2 x 2.9 GB at GRCh37 size), built with the K-mer tables
+  // (ensure_kmer).  Measured at 50 M reads (profiles/r06_sweep_tab.jsonl, hits identical): k_gapped
+  // 2 476 ms per step without, 2 149 / 2 027 / 1 947 ms with K = 10 / 12 / 13.
   DBuf ltab[2];
-  int gap_tab_k = 0;
+  int gap_tab_k = -1;
   int ltab_K = 0;   // tab_k of the built level tables
   int kmer_k = -1;  // requested K (-1: auto from the genome size, 0: off)
   int kmer_K = 0;   // K of the built tables
@@ -462,13 +464,18 @@ int ensure_kmer(ibwa_ctx *c) {
     c->kmer_K = K;
   }
   c->ltab_K = 0;
-  if (c->gap_tab_k > 0) {
+  int TK = c->gap_tab_k;
+  if (TK < 0) {  // auto: as deep as strings of that length still mostly occur, at most 13
+    TK = 0;
+    while (TK < 13 && (1ull << (2 * (TK + 1))) <= (uint64_t)c->ix[0].seq_len) ++TK;
+  }
+  if (TK > 0 && c->ix[0].seq_len < LTAB_MARK) {
     for (int s = 0; s < 2; ++s) {
-      if (int rc = c->ltab[s].ensure(ltab_off((uint32_t)c->gap_tab_k + 2) * 8)) return rc;
-      hipError_t e = build_level_tables(c->ix[s], c->gap_tab_k + 1, c->ltab[s].as<uint2>(), c->stream);
+      if (int rc = c->ltab[s].ensure(ltab_off((uint32_t)TK + 2) * 8)) return rc;
+      hipError_t e = build_level_tables(c->ix[s], TK + 1, c->ltab[s].as<uint2>(), c->stream);
       if (e != hipSuccess) return fail(IBWA_EHIP, "level tables: %s", hipGetErrorString(e));
     }
-    c->ltab_K = c->gap_tab_k;
+    c->ltab_K = TK;
   }
   c->kmer_valid = true;
   return 0;
@@ -713,7 +720,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
     c->kmer_k = (int)value;
     c->kmer_valid = false;
   }
-  else if (k == "gap_tab_k" && value >= 0 && value <= 13) {
+  else if (k == "gap_tab_k" && value >= -1 && value <= 14) {
     if (value != c->gap_tab_k) {
       if (int rc = refuse_shared(c, "option gap_tab_k")) return rc;
       c->kmer_valid = false;  // built with the K-mer tables
@@ -1636,6 +1643,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.o = o;
       HIPCHK(hipEventRecord(evs[0], st));
       HIPCHK(hipEventRecord(evs[2], st));
+      if (c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // the first pass's states carry string-stored nodes
+        K.ltab[0] = c->ltab[0].as<uint2>();
+        K.ltab[1] = c->ltab[1].as<uint2>();
+        K.tab_k = (uint32_t)c->ltab_K;
+      }
       K.fix_status = c->d_status.as<uint32_t>();  // resume_fixup, as each read ends
       K.fix_roff = c->d_roff.as<uint64_t>();
       HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, st));
@@ -1997,6 +2009,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (resume_states) {
         K.rdump = c->d_rdump.as<uint4>();
         K.roff = c->d_roff.as<uint64_t>();
+        if (c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // states may carry string-stored nodes
+          K.ltab[0] = c->ltab[0].as<uint2>();
+          K.ltab[1] = c->ltab[1].as<uint2>();
+          K.tab_k = (uint32_t)c->ltab_K;
+        }
       }
       if (c->coop_roots) {
         K.proot = c->c_proot.as<uint4>();

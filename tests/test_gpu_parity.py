@@ -55,10 +55,11 @@ def test_sai_goldens_gpu(golden_dir, sai_manifest, gpu_engine, exact_path, gappe
     assert not bad, bad
 
 
-@pytest.mark.parametrize("tab_k", [12, 6])
+@pytest.mark.parametrize("tab_k", [12, 6, 0])
 def test_sai_goldens_level_tables(golden_dir, sai_manifest, gpu_engine, tab_k):
     """The first pass with its shallow nodes stored by their strings and expanded from the level
-    tables (GapArgs::ltab, gap_tab_k): every golden .sai of the option matrix, bit for bit."""
+    tables (GapArgs::ltab, gap_tab_k; 0: off, every node by its interval): every golden .sai of the
+    option matrix, bit for bit."""
     gpu_engine.set_option("gap_tab_k", tab_k)
     bad = []
     try:
@@ -71,7 +72,7 @@ def test_sai_goldens_level_tables(golden_dir, sai_manifest, gpu_engine, tab_k):
             if not oracle.sai_body_equal(got, open(os.path.join(golden_dir, key + ".sai"), "rb").read()):
                 bad.append(key)
     finally:
-        gpu_engine.set_option("gap_tab_k", 0)
+        gpu_engine.set_option("gap_tab_k", -1)
     assert not bad, bad
 
 

@@ -172,7 +172,7 @@ def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
                 "gap_iter_budget": 8000, "gap_coop": 1, "coop_roots": 1, "gap_early_iters": 3000,
                 "gap_early_entries": 1000, "gap_resume": 1, "gap_resume_records": 0, "gap_resume_iters": 2000,
                 "gap_resume_entries": 300, "coop_pool_gb": 0, "gap_tail_lanes": 16, "gap_tail_iters": 200,
-                "gap_lw_min_waves": 8, "coop_pool_pages": 0, "gap_reads_per_chunk": 16 << 20, "gap_tab_k": 0}
+                "gap_lw_min_waves": 8, "coop_pool_pages": 0, "gap_reads_per_chunk": 16 << 20, "gap_tab_k": -1}
     try:
         for k, v in tune.items():
             eng.set_option(k, v)
