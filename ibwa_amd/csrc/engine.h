@@ -117,6 +117,7 @@ struct GapArgs {
   // depth) and expanded from one 32 B load of its children's intervals instead of two Occ blocks.
   const uint2 *ltab[2];
   uint32_t tab_k;            // 0: off
+  uint32_t keep_coded;       // resume states keep string-stored entries (the cooperative pass has the tables)
   AlnOpt o;
 };
 constexpr uint32_t LTAB_MARK = 0xFFFFFF00u;  // y >= this: a node stored by its string (no l can be: seq_len < it)

@@ -386,6 +386,8 @@ struct ibwa_ctx {
   // 2 476 ms per step without, 2 149 / 2 027 / 1 947 ms with K = 10 / 12 / 13.
   DBuf ltab[2];
   int gap_tab_k = -1;
+  int coop_tab = 1;  // the cooperative pass expands string-stored nodes from the tables too (0: the
+                     // first pass hands its states on with intervals)
   int ltab_K = 0;   // tab_k of the built level tables
   int kmer_k = -1;  // requested K (-1: auto from the genome size, 0: off)
   int kmer_K = 0;   // K of the built tables
@@ -720,6 +722,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
     c->kmer_k = (int)value;
     c->kmer_valid = false;
   }
+  else if (k == "coop_tab" && (value == 0 || value == 1)) c->coop_tab = (int)value;
   else if (k == "gap_tab_k" && value >= -1 && value <= 14) {
     if (value != c->gap_tab_k) {
       if (int rc = refuse_shared(c, "option gap_tab_k")) return rc;
@@ -1643,7 +1646,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.o = o;
       HIPCHK(hipEventRecord(evs[0], st));
       HIPCHK(hipEventRecord(evs[2], st));
-      if (c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // the first pass's states carry string-stored nodes
+      if (c->coop_tab && c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // the first pass's states carry string-stored nodes
         K.ltab[0] = c->ltab[0].as<uint2>();
         K.ltab[1] = c->ltab[1].as<uint2>();
         K.tab_k = (uint32_t)c->ltab_K;
@@ -1723,6 +1726,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         G.ltab[0] = c->ltab[0].as<uint2>();
         G.ltab[1] = c->ltab[1].as<uint2>();
         G.tab_k = (uint32_t)c->ltab_K;
+        G.keep_coded = c->coop_tab ? 1u : 0u;
       }
       G.cap1 = P0r;
       G.hit_slots = std::min<uint32_t>(c->gap_hit_slots, P0r / 2);
@@ -2009,7 +2013,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (resume_states) {
         K.rdump = c->d_rdump.as<uint4>();
         K.roff = c->d_roff.as<uint64_t>();
-        if (c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // states may carry string-stored nodes
+        if (c->coop_tab && c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // states may carry string-stored nodes
           K.ltab[0] = c->ltab[0].as<uint2>();
           K.ltab[1] = c->ltab[1].as<uint2>();
           K.tab_k = (uint32_t)c->ltab_K;

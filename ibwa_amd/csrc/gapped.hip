@@ -435,7 +435,18 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
           uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
           if (ok0) e0 = *sp(s0);
           if (ok1) e1 = *sp(s1);
-          // (entries stored by their strings leave as they are: the cooperative pass has the same tables)
+          // entries stored by their strings leave as they are when the cooperative pass has the same tables
+          // (GapArgs::keep_coded), else with their intervals
+          auto by_interval = [&](uint4 &x) __attribute__((always_inline)) {
+            if (LW && TK > 0 && out && !A.keep_coded && x.y >= LTAB_MARK) {
+              const uint2 *tb = ((x.w >> 28) & 1u) ? A.ltab[0] : A.ltab[1];
+              const uint2 iv = tb[ltab_off(x.y & 0xFFu) + x.x];
+              x.x = iv.x;
+              x.y = iv.y;
+            }
+          };
+          by_interval(e0);
+          by_interval(e1);
           auto live = [&](const uint4 &x, uint32_t slot) __attribute__((always_inline)) {
             const int sc = (int)(((x.w >> 16) & 31u) * (uint32_t)o.s_mm + ((x.w >> 21) & 7u) * (uint32_t)o.s_gapo +
                                  ((x.w >> 24) & 15u) * (uint32_t)o.s_gape);
