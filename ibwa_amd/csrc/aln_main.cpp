@@ -418,6 +418,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     if (fs > 0 && fs <= piece * per_lane)
       piece = std::max<uint64_t>((uint64_t)256 << 20, (fs + 2 * per_lane - 1) / (2 * per_lane));
   }
+  int cli_tab_k = 0;  // the level tables' K, pinned on the aligning contexts (the arena counts them)
   {
     // The default arena follows the inputs, calibrated on what round 5 measured (GiB; IBWA_ARENA_TRACE=1
     // lists every carve, profiles/r05_arena_trace.log): the index structures (relaid-out BWT, bit
@@ -455,11 +456,14 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
       }
     const bool long_reads = first_len == 0 || first_len > 128;
     const double fixed = long_reads ? 36.0 : 30.0, per_gib = long_reads ? 20.0 : 21.5;
-    // the first pass's level tables (engine gap_tab_k, auto): 2 x 8 B x ((4^(K+2) - 1) / 3) for the K that
-    // strings of length K + 1 still mostly occur at (5.7 GB for a GRCh37-sized genome)
+    // the first pass's level tables (engine gap_tab_k): 2 x 8 B x ((4^(K+2) - 1) / 3) for the K that
+    // strings of length K + 1 still mostly occur at, at most 13 (5.7 GB for a GRCh37-sized genome; the
+    // engine's auto rule would take 14 -- 23 GB, -5 % k_gapped -- where HBM has room: here the CLI
+    // keeps its footprint)
     const double seq_len = 4.0 * fbytes(prefix + ".bwt");
     int tab_k = 0;
     while (tab_k < 13 && std::ldexp(1.0, 2 * (tab_k + 1)) <= seq_len) ++tab_k;
+    cli_tab_k = tab_k;
     const double ltab_gb = tab_k ? 2.0 * 8.0 * (std::ldexp(1.0, 2 * (tab_k + 2)) / 3.0) / GiB : 0.0;
     const double need_gb = ltab_gb + 7.5 * (fbytes(prefix + ".bwt") + fbytes(prefix + ".rbwt")) / GiB +
                            n_lanes * (std::min(fixed, 2.0 * fixed * grp) + per_gib * grp) + 1.7 * grp +
@@ -549,7 +553,9 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   };
   std::vector<ibwa_ctx_t *> ctx(n_gpus, nullptr);
   for (int g = 0; g < n_gpus; ++g) {
-    if (ibwa_ctx_create(g % n_dev, &ctx[g]) || ctx_opts(ctx[g])) return die("ibwa_ctx_create");
+    if (ibwa_ctx_create(g % n_dev, &ctx[g]) || ibwa_ctx_set_option(ctx[g], "gap_tab_k", cli_tab_k) ||
+        ctx_opts(ctx[g]))
+      return die("ibwa_ctx_create");
     if (g == 0) {
       if (ibwa_ctx_load_bwt_file(ctx[0], 0, (prefix + ".bwt").c_str())) return die("load .bwt");
       if (ibwa_ctx_load_bwt_file(ctx[0], 1, (prefix + ".rbwt").c_str())) return die("load .rbwt");

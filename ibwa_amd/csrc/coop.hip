@@ -264,7 +264,7 @@ constexpr uint32_t GRP_FAIL = 0xFFFFFFF0u;
 __device__ __noinline__ uint2 expand_groups(uint4 *pool, const uint4 *o0, const uint4 *o1, uint4 L2, uint32_t *dir_s,
                                             uint32_t *dirc0, uint32_t *freel, uint32_t n_free, uint32_t freecap,
                                             uint32_t *pool_next, uint32_t pool_pages, uint32_t N, uint32_t old_np,
-                                            int lane, const uint2 *lt0, const uint2 *lt1, uint32_t TK) {
+                                            int lane) {
   auto ent_at = [&](uint32_t j) -> uint4 {
     return pool[((uint64_t)dirc0[j >> COOP_PG_LOG2] << COOP_PG_LOG2) + (j & (COOP_PG - 1))];
   };
@@ -313,26 +313,12 @@ __device__ __noinline__ uint2 expand_groups(uint4 *pool, const uint4 *o0, const 
       // the insertion child: the group itself, its deletions spelled out
       put(vo, make_uint4(e.x, e.y, gi | gi << 10, (e.w & ~(3u << 25)) | (uint32_t)STATE_I << 25));
       uint32_t r = 1;
-      // a group stored by its string (level tables): its deletions from the table, by their strings
-      // while their depth is <= TK
-      const bool coded = TK > 0 && e.y >= LTAB_MARK;
-      const uint32_t dep = e.y & 0xFFu;
       for (uint32_t cc = 0; cc < 4; ++cc) {
         if (dm & (1u << cc)) {
-          uint32_t dk, dl;
-          if (coded && dep + 1u <= TK) {
-            dk = e.x << 2 | cc;
-            dl = LTAB_MARK | (dep + 1u);
-          } else if (coded) {
-            const uint2 iv = ((e.w >> 24) & 1u ? lt0 : lt1)[ltab_off(dep + 1u) + ((uint64_t)e.x << 2) + cc];
-            dk = iv.x;
-            dl = iv.y;
-          } else {
-            const uint32_t l2 = pick4(L2, cc);
-            dl = l2 + occ_of(ob[(size_t)(e.y >> 6) * 4 + cc], e.y);
-            dk = l2 + 1u;
-            if (e.x != 0) dk += occ_of(ob[(size_t)((e.x - 1) >> 6) * 4 + cc], e.x - 1);
-          }
+          const uint32_t l2 = pick4(L2, cc);
+          const uint32_t dl = l2 + occ_of(ob[(size_t)(e.y >> 6) * 4 + cc], e.y);
+          uint32_t dk = l2 + 1u;
+          if (e.x != 0) dk += occ_of(ob[(size_t)((e.x - 1) >> 6) * 4 + cc], e.x - 1);
           put(vo + r, make_uint4(dk, dl, (gi + 1) | (gi + 1) << 10, (e.w & ~(3u << 25)) | (uint32_t)STATE_D << 25));
           ++r;
         }
@@ -587,10 +573,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     } else {
       // ---------------------------------------------- per-read setup
       const bool seeded = len > o.seed_len;
-      // nodes stored by their strings (level tables) reach this pass in resume states; a read so short
-      // that a hit could come at such a depth never has any (the first pass's rule)
-      const uint32_t TK = A.tab_k;
-      const bool tabok = TK > 0 && len > (int)TK + 24;
       // a first-pass search state to resume from (GapArgs::rdump), 1 + its offset
       const uint64_t rof = A.roff ? A.roff[rr] : 0ull;
       // level 0 done by k_coop_roots: the records of its two chains (A.proot[2 r], [2 r + 1])
@@ -691,8 +673,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             // the level holds gap groups: spell them out first
             const uint2 g = expand_groups(A.pool, A.o64[0], A.o64[1],
                                           make_uint4(ixv0.L2[0], ixv0.L2[1], ixv0.L2[2], ixv0.L2[3]), dir + s * MAXP,
-                                          S.dirc[0], freel, n_free, A.freecap, A.pool_next, A.pool_pages, N, S.np[s], lane,
-                                          A.ltab[0], A.ltab[1], A.tab_k);
+                                          S.dirc[0], freel, n_free, A.freecap, A.pool_next, A.pool_pages, N, S.np[s], lane);
             n_free = g.y;
             if (g.x >= GRP_FAIL) {
               status = ST_STACK_OVERFLOW | (g.x & 15u) << 8;
@@ -1136,22 +1117,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           const bool qkneg = qk == 0;
           const bool qshare = !qkneg && ((qk - 1) >> 6) == (ql >> 6);
           const uint32_t tsym = tail ? sym_of(a, i) : 0u;
-          // a node stored by its string: its children's intervals (an expansion: 32 B; a tail step: the
-          // tail symbol's 8 B) and for a deletion state its own interval from the level table
-          const bool coded = tabok && (exp || tail) && l >= LTAB_MARK;
-          const uint32_t cdep = l & 0xFFu;
           // One set of load registers: a lane fetches its chain's entry (bl.v0), takes an exact-tail
           // step (the tail symbol's Occ words of both rows: bl.v0, bk.v0) or expands (both whole
           // blocks) -- never two of these, so the round trip holds 8 uint4s, not 14
           Blk bk, bl;
           {
             const bool fetch = lst == L_FETCH;
-            const bool kld = (exp || tail) && !qkneg && !qshare && !coded;
+            const bool kld = (exp || tail) && !qkneg && !qshare;
             const uint4 *pl = fetch ? A.pool + (((uint64_t)ent_page << COOP_PG_LOG2) + ent_off)
                                     : ob + ((size_t)(ql >> 6) * 4 + tsym);
             const uint4 *pk = ob + ((size_t)((qk - 1) >> 6) * 4 + tsym);
-            if (fetch || ((exp || tail) && !coded)) bl.v0 = pl[0];
-            if (exp && !coded) {
+            if (fetch || exp || tail) bl.v0 = pl[0];
+            if (exp) {
               bl.v1 = pl[1];
               bl.v2 = pl[2];
               bl.v3 = pl[3];
@@ -1161,22 +1138,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               bk.v1 = pk[1];
               bk.v2 = pk[2];
               bk.v3 = pk[3];
-            }
-            if (coded) {
-              const uint2 *tb = (a ? A.ltab[0] : A.ltab[1]) + ltab_off(cdep + 1u) + ((uint64_t)qk << 2);
-              if (exp) {
-                bl.v0 = reinterpret_cast<const uint4 *>(tb)[0];
-                bl.v1 = reinterpret_cast<const uint4 *>(tb)[1];
-                if (((ew >> 25) & 3u) == (uint32_t)STATE_D) {
-                  const uint2 own = (a ? A.ltab[0] : A.ltab[1])[ltab_off(cdep) + qk];
-                  bl.v2.x = own.x;
-                  bl.v2.y = own.y;
-                }
-              } else {
-                const uint2 t2 = tb[tsym];
-                bl.v0.x = t2.x;
-                bl.v0.y = t2.y;
-              }
             }
           }
 
@@ -1191,12 +1152,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             if (qshare) tvk = tvl;
             const uint32_t ok = qkneg ? 0u : occ_of(tvk, qk - 1), ol = occ_of(tvl, ql);
             const uint32_t base = l2of(ix, tsym);
-            k = coded ? tvl.x : base + ok + 1;
-            l = coded ? tvl.y : base + ol;
-            if (k <= l && coded && cdep + 1u <= TK) {  // still by its string
-              k = qk << 2 | tsym;
-              l = LTAB_MARK | (cdep + 1u);
-            }
+            k = base + ok + 1;
+            l = base + ol;
             if (k > l) {
               end_chain(false, 0, 0);
             } else if (--i < 0) {
@@ -1212,10 +1169,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             const int e_mm = (int)(ew & 0xffu), e_go = (int)((ew >> 8) & 0xffu), e_ge = (int)((ew >> 16) & 0xffu);
             const int state = (int)((ew >> 25) & 3u);
             uint4 KK, LL;
-            if (coded) {
-              KK = make_uint4(bl.v0.x, bl.v0.z, bl.v1.x, bl.v1.z);
-              LL = make_uint4(bl.v0.y, bl.v0.w, bl.v1.y, bl.v1.w);
-            } else {
+            {
               const uint4 cl4 = make_uint4(occ_of(bl.v0, ql), occ_of(bl.v1, ql), occ_of(bl.v2, ql), occ_of(bl.v3, ql));
               const uint4 ck4 = qkneg ? make_uint4(0, 0, 0, 0)
                                       : make_uint4(occ_of(bk.v0, qk - 1), occ_of(bk.v1, qk - 1), occ_of(bk.v2, qk - 1),
@@ -1232,9 +1186,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
             }
             const int ni = i - 1;
             const uint32_t csym = sym_of(a, ni);
-            const uint32_t occ = coded ? bl.v2.y - bl.v2.x + 1 : l - k + 1;
-            // children of a node stored by its string are stored by theirs while their depth is <= TK
-            const bool cch = coded && cdep + 1u <= TK;
+            const uint32_t occ = l - k + 1;
             bool allow_diff = true, allow_M = true;
             if (ni > 0) {
               const uint2 w_im2 = make_uint2(S.Ww[a][ni - 1], S.Wb[a][ni - 1]),
@@ -1279,8 +1231,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               vm &= vm - 1;
               const bool is_ins = j == 0, is_del = j - 1 < 4, is_sym = j >= 5;
               const uint32_t cc = is_del ? j - 1 : (csym + j - 4) & 3;
-              const uint32_t pk = is_ins ? k : cch ? (k << 2 | cc) : pick4(KK, cc);
-              const uint32_t pl = is_ins ? l : cch ? (LTAB_MARK | (cdep + 1u)) : pick4(LL, cc);
+              const uint32_t pk = is_ins ? k : pick4(KK, cc);
+              const uint32_t pl = is_ins ? l : pick4(LL, cc);
               const bool open = !is_sym && state == STATE_M;
               const int n_mm = e_mm + (is_sym ? 1 : 0);  // staged symbol children are mismatches
               const int n_gapo = e_go + (open ? 1 : 0), n_gape = e_ge + (!is_sym && !open ? 1 : 0);
@@ -1295,9 +1247,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               if (grp) cnt2 = (cnt2 + ((uint32_t)__builtin_popcount(gdm) << 16)) | 1u << (28 + q);
             }
             if (match) {
-              const uint32_t mk = pick4(KK, csym), ml = pick4(LL, csym);
-              k = cch ? (k << 2 | csym) : mk;
-              l = cch ? (LTAB_MARK | (cdep + 1u)) : ml;
+              k = pick4(KK, csym);
+              l = pick4(LL, csym);
               i = ni;
               ew = (ew & ~(3u << 25)) | (uint32_t)STATE_M << 25;
               pop_node();

@@ -116,8 +116,7 @@ struct GapArgs {
   // of length <= tab_k + 1.  A node at depth <= tab_k is stored by its string (x = code, y = LTAB_MARK |
   // depth) and expanded from one 32 B load of its children's intervals instead of two Occ blocks.
   const uint2 *ltab[2];
-  uint32_t tab_k;            // 0: off
-  uint32_t keep_coded;       // resume states keep string-stored entries (the cooperative pass has the tables)
+  uint32_t tab_k;            // 0: off (resume states leave with intervals: the cooperative pass has no tables)
   AlnOpt o;
 };
 constexpr uint32_t LTAB_MARK = 0xFFFFFF00u;  // y >= this: a node stored by its string (no l can be: seq_len < it)
@@ -187,10 +186,6 @@ struct CoopArgs {
   // after it: its gap_shadow updates are in them, so a resumed read does not replay them); -1: per
   // launch read (k_width run for this launch)
   int64_t wb_base;
-  // level tables of the first pass (GapArgs::ltab, tab_k): nodes at depth <= tab_k stored by their
-  // strings (resume states hand them on so), expanded and stepped from the tables; 0: off
-  const uint2 *ltab[2];
-  uint32_t tab_k;
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);

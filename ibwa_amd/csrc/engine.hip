@@ -381,13 +381,12 @@ struct ibwa_ctx {
   // K-mer interval tables for the exact-match path (kmer.hip)
   DBuf kt[2], o64[2];
   // level tables of the LW first pass (GapArgs::ltab): strings of length <= gap_tab_k + 1 (0: off;
-  // -1: auto, floor(log4(n)) up to 13 -- 2 x 2.9 GB at GRCh37 size), built with the K-mer tables
+  // -1: auto, floor(log4(n)) up to 13 -- 2 x 2.9 GB at GRCh37 size -- or 14 with room, ensure_kmer),
+  // built with the K-mer tables
   // (ensure_kmer).  Measured at 50 M reads (profiles/r06_sweep_tab.jsonl, hits identical): k_gapped
   // 2 476 ms per step without, 2 149 / 2 027 / 1 947 ms with K = 10 / 12 / 13.
   DBuf ltab[2];
   int gap_tab_k = -1;
-  int coop_tab = 1;  // the cooperative pass expands string-stored nodes from the tables too (0: the
-                     // first pass hands its states on with intervals)
   int ltab_K = 0;   // tab_k of the built level tables
   int kmer_k = -1;  // requested K (-1: auto from the genome size, 0: off)
   int kmer_K = 0;   // K of the built tables
@@ -467,9 +466,17 @@ int ensure_kmer(ibwa_ctx *c) {
   }
   c->ltab_K = 0;
   int TK = c->gap_tab_k;
-  if (TK < 0) {  // auto: as deep as strings of that length still mostly occur, at most 13
+  if (TK < 0) {
+    // auto: as deep as strings of that length still mostly occur, at most 13 (2 x 2.9 GB at GRCh37
+    // size); 14 (2 x 11.5 GB) when both tables take at most 15 % of the free HBM: k_gapped 1 935 ->
+    // 1 844 ms per 50 M-read step (profiles/r06_sweep_tab2.jsonl).  The CLI pins its K (aln_main.cpp).
     TK = 0;
     while (TK < 13 && (1ull << (2 * (TK + 1))) <= (uint64_t)c->ix[0].seq_len) ++TK;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    if (TK == 13 && (1ull << 30) <= (uint64_t)c->ix[0].seq_len &&
+        2.0 * 8.0 * (double)ltab_off(16) <= 0.15 * (double)free_b)
+      TK = 14;
   }
   if (TK > 0 && c->ix[0].seq_len < LTAB_MARK) {
     for (int s = 0; s < 2; ++s) {
@@ -722,7 +729,6 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
     c->kmer_k = (int)value;
     c->kmer_valid = false;
   }
-  else if (k == "coop_tab" && (value == 0 || value == 1)) c->coop_tab = (int)value;
   else if (k == "gap_tab_k" && value >= -1 && value <= 14) {
     if (value != c->gap_tab_k) {
       if (int rc = refuse_shared(c, "option gap_tab_k")) return rc;
@@ -1646,11 +1652,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.o = o;
       HIPCHK(hipEventRecord(evs[0], st));
       HIPCHK(hipEventRecord(evs[2], st));
-      if (c->coop_tab && c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // the first pass's states carry string-stored nodes
-        K.ltab[0] = c->ltab[0].as<uint2>();
-        K.ltab[1] = c->ltab[1].as<uint2>();
-        K.tab_k = (uint32_t)c->ltab_K;
-      }
       K.fix_status = c->d_status.as<uint32_t>();  // resume_fixup, as each read ends
       K.fix_roff = c->d_roff.as<uint64_t>();
       HIPCHK(launch_coop(K, c->d_counter.as<unsigned long long>(), blocks, st));
@@ -1726,7 +1727,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
         G.ltab[0] = c->ltab[0].as<uint2>();
         G.ltab[1] = c->ltab[1].as<uint2>();
         G.tab_k = (uint32_t)c->ltab_K;
-        G.keep_coded = c->coop_tab ? 1u : 0u;
       }
       G.cap1 = P0r;
       G.hit_slots = std::min<uint32_t>(c->gap_hit_slots, P0r / 2);
@@ -2013,11 +2013,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (resume_states) {
         K.rdump = c->d_rdump.as<uint4>();
         K.roff = c->d_roff.as<uint64_t>();
-        if (c->coop_tab && c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // states may carry string-stored nodes
-          K.ltab[0] = c->ltab[0].as<uint2>();
-          K.ltab[1] = c->ltab[1].as<uint2>();
-          K.tab_k = (uint32_t)c->ltab_K;
-        }
       }
       if (c->coop_roots) {
         K.proot = c->c_proot.as<uint4>();

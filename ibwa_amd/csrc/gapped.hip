@@ -435,10 +435,10 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
           uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
           if (ok0) e0 = *sp(s0);
           if (ok1) e1 = *sp(s1);
-          // entries stored by their strings leave as they are when the cooperative pass has the same tables
-          // (GapArgs::keep_coded), else with their intervals
+          // entries stored by their strings leave with their intervals (the cooperative pass expands from
+          // Occ blocks: tables there measured no faster, profiles/r06_sweep_tab2.jsonl)
           auto by_interval = [&](uint4 &x) __attribute__((always_inline)) {
-            if (LW && TK > 0 && out && !A.keep_coded && x.y >= LTAB_MARK) {
+            if (LW && TK > 0 && out && x.y >= LTAB_MARK) {
               const uint2 *tb = ((x.w >> 28) & 1u) ? A.ltab[0] : A.ltab[1];
               const uint2 iv = tb[ltab_off(x.y & 0xFFu) + x.x];
               x.x = iv.x;
