@@ -243,12 +243,50 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
                                            uint2 *wa, uint2 *wb, uint32_t *lw = nullptr, RecOut *rec = nullptr,
                                            uint32_t clamp = 0, int nb = 4, uint32_t *rd = nullptr,
                                            const uint32_t *sa0 = nullptr, const uint32_t *sa1 = nullptr,
-                                           const uint32_t *tx0 = nullptr, const uint32_t *tx1 = nullptr) {
+                                           const uint32_t *tx0 = nullptr, const uint32_t *tx1 = nullptr,
+                                           const uint2 *lta = nullptr, const uint2 *ltb = nullptr, int tdep = 0) {
   WChain A{0u, ixa.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u};
   WChain B{0u, ixb.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u};
   uint32_t lwa = 0, lwb = 0;  // sum of log2(width) over the positions (diagnostics)
   uint32_t pa = 0, pb = 0;    // previous positions' widths (record)
-  for (int base = 0; base < L; base += 16) {
+  // The first min(L, tdep) steps of both chains from the level tables (AlnArgs::ltab): the interval
+  // after d symbols is the table entry of their string, so those steps' loads are independent -- one
+  // round trip for all of them instead of a chain of dependent Occ steps.  A chain takes table steps
+  // up to its first N or empty interval (the steps from there reset it as before).
+  constexpr int TMAX = 15;
+  uint2 ta[TMAX], tb[TMAX];
+  int da = 0, db = 0;
+  if (tdep > 0) {
+    const int D = L < tdep ? L : tdep;
+    uint32_t xa = 0, xb = 0;
+    int dn = D;  // steps before the first N
+#pragma unroll
+    for (int d = 0; d < TMAX; ++d) {
+      ta[d] = tb[d] = make_uint2(1u, 0u);
+      if (d < dn) {
+        const uint32_t ca = s[d];
+        if (ca > 3) {
+          dn = d;
+        } else {
+          const uint32_t cb = strand_base(ca, 1, comp);
+          xa = xa << 2 | ca;
+          xb = xb << 2 | cb;
+          ta[d] = lta[ltab_off((uint32_t)d + 1u) + xa];
+          tb[d] = ltb[ltab_off((uint32_t)d + 1u) + xb];
+        }
+      }
+    }
+    // the nonempty prefix (the intervals along a string only narrow)
+#pragma unroll
+    for (int d = 0; d < TMAX; ++d) {
+      da += (d < dn && ta[d].x <= ta[d].y) ? 1 : 0;
+      db += (d < dn && tb[d].x <= tb[d].y) ? 1 : 0;
+    }
+  }
+  // one block of 16 steps; the first block (the only one with table steps) peeled so that the table
+  // registers are dead before the others
+  auto block = [&](int base, auto first) __attribute__((always_inline)) {
+    constexpr bool FIRST = decltype(first)::value;
     uint2 ba[16], bb[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
@@ -256,11 +294,24 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
       if (i < L) {
         uint32_t ca = s[i];
         uint32_t cb = strand_base(ca, 1, comp);
+        const bool tA = FIRST && t < TMAX && t < da, tB = FIRST && t < TMAX && t < db;
         WLoad xa, xb;
-        wchain_load(ixa, sa0, tx0, A, ca, xa);
-        wchain_load(ixb, sa1, tx1, B, cb, xb);
-        wchain_step(ixa, sa0 != nullptr, A, ca, xa);
-        wchain_step(ixb, sa1 != nullptr, B, cb, xb);
+        if (!tA) wchain_load(ixa, sa0, tx0, A, ca, xa);
+        if (!tB) wchain_load(ixb, sa1, tx1, B, cb, xb);
+        if (FIRST && t < TMAX && tA) {
+          A.k = ta[t < TMAX ? t : 0].x;
+          A.l = ta[t < TMAX ? t : 0].y;
+          if (t == da - 1 && sa0 != nullptr && A.k == A.l) A.mode = 1;  // as an Occ step to one row would
+        } else {
+          wchain_step(ixa, sa0 != nullptr, A, ca, xa);
+        }
+        if (FIRST && t < TMAX && tB) {
+          B.k = tb[t < TMAX ? t : 0].x;
+          B.l = tb[t < TMAX ? t : 0].y;
+          if (t == db - 1 && sa1 != nullptr && B.k == B.l) B.mode = 1;
+        } else {
+          wchain_step(ixb, sa1 != nullptr, B, cb, xb);
+        }
         ba[t] = make_uint2(A.l - A.k + 1, A.bid);
         lwa += 31 - __builtin_clz(A.l - A.k + 1);
         bb[t] = make_uint2(B.l - B.k + 1, B.bid);
@@ -285,7 +336,9 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
         }
       if (rd) rd[base >> 4] = x;
     }
-  }
+  };
+  if (L > 0) block(0, std::true_type{});
+  for (int base = 16; base < L; base += 16) block(base, std::false_type{});
   wa[L] = make_uint2(0u, A.bid + 1);
   wb[L] = make_uint2(0u, B.bid + 1);
   if (rec) rec->put(rec_byte(wa[L], wb[L], pa, pb, L == 0, clamp, nb));
@@ -305,6 +358,7 @@ __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
   const uint8_t *s = A.seq + A.off[r];
   const bool comp = A.o.mode & MODE_COMPREAD;
   const uint32_t *sa0 = A.jsa[0], *sa1 = A.jsa[1], *tx0 = A.jtxt[0], *tx1 = A.jtxt[1];
+  const int tdep = A.ltab[0] ? (int)min(A.tab_k + 1u, 15u) : 0;  // leading steps from the level tables
   uint2 *w0 = A.wbuf + (uint64_t)lane * A.wstride;
   uint2 *w1 = w0 + A.wlen1;
   uint2 *sw0 = w1 + A.wlen1;
@@ -333,18 +387,20 @@ __global__ void __launch_bounds__(256) k_width(AlnArgs A) {
     const int md = A.o.fnr_pos ? (int)A.maxdiff_tab[L] : A.o.max_diff;
     rec[0] = (uint32_t)L | (nN < 255u ? nN : 255u) << 16 | (uint32_t)md << 24;
     RecOut ro{rec + 1 + A.cw_rw, 0u, 0u};
-    width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, &ro, (uint32_t)md + 1u, 4, rec + 1, sa0, sa1, tx0, tx1);
+    width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, &ro, (uint32_t)md + 1u, 4, rec + 1, sa0, sa1, tx0, tx1,
+               A.ltab[0], A.ltab[1], tdep);
     while (ro.off < A.wlen1) ro.put(0u);  // positions past this read's length
     if (L > A.o.seed_len)
       width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1, nullptr, &ro,
-                 (uint32_t)A.o.max_seed_diff + 1u, 3, nullptr, sa0, sa1, tx0, tx1);
+                 (uint32_t)A.o.max_seed_diff + 1u, 3, nullptr, sa0, sa1, tx0, tx1, A.ltab[0], A.ltab[1], tdep);
     ro.flush();
     return;
   }
-  width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, nullptr, 0, 4, nullptr, sa0, sa1, tx0, tx1);
+  width_pair(A.ix[0], A.ix[1], L, s, comp, w0, w1, nullptr, nullptr, 0, 4, nullptr, sa0, sa1, tx0, tx1, A.ltab[0],
+             A.ltab[1], tdep);
   if (L > A.o.seed_len)
     width_pair(A.ix[0], A.ix[1], A.o.seed_len, s + (L - A.o.seed_len), comp, sw0, sw1, nullptr, nullptr, 0, 4,
-               nullptr, sa0, sa1, tx0, tx1);
+               nullptr, sa0, sa1, tx0, tx1, A.ltab[0], A.ltab[1], tdep);
 }
 
 __device__ __forceinline__ int int_log2(uint32_t v) {  // bwtgap.c:93-102

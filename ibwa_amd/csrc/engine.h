@@ -55,6 +55,10 @@ struct AlnArgs {
   // path's jump); nullptr: every step reads the Occ blocks
   const uint32_t *jsa[2];
   const uint32_t *jtxt[2];
+  // the first pass's level tables (GapArgs::ltab): k_width takes a chain's first min(len, tab_k + 1,
+  // 15) steps from them; nullptr: off
+  const uint2 *ltab[2];
+  uint32_t tab_k;
   AlnOpt o;
 };
 

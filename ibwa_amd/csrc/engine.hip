@@ -299,6 +299,7 @@ struct ibwa_ctx {
   bool jump_derived = false;  // jump arrays derived from a loaded BWT (ensure_jump), not built here
   int jump_derive = 1;        // option: derive them for a loaded index when HBM allows
   int exact_jump = 1;
+  int width_tab = 1;           // option: k_width's first steps from the level tables (first pass)
   int width_jump = 1;         // option: k_width steps one-row intervals from the text (2: derive SA / text for it)
   uint32_t sa_intv = 0;
   bool sa_loaded[2] = {false, false};  // sa_s[s] holds a sampled SA of the resident index
@@ -767,6 +768,7 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "exact_jump") c->exact_jump = value != 0;
   else if (k == "jump_derive") c->jump_derive = value != 0;
   else if (k == "width_jump" && value >= 0 && value <= 2) c->width_jump = (int)value;
+  else if (k == "width_tab" && (value == 0 || value == 1)) c->width_tab = (int)value;
   else if (k == "diag") c->diag = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
@@ -902,6 +904,7 @@ int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   dst->jump_derive = src->jump_derive;
   dst->exact_jump = src->exact_jump;
   dst->width_jump = src->width_jump;
+  dst->width_tab = src->width_tab;
   dst->share_src = const_cast<ibwa_ctx *>(src);
   ++dst->share_src->n_borrowers;
   return 0;
@@ -1464,6 +1467,11 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
   if (v2) {
     if (int rc = ensure_kmer(c)) return rc;
     c->stats.path = 2;
+    if (c->width_tab && c->ltab_K > 0 && c->ix[0].seq_len < LTAB_MARK) {  // k_width's leading steps
+      A.ltab[0] = c->ltab[0].as<uint2>();
+      A.ltab[1] = c->ltab[1].as<uint2>();
+      A.tab_k = (uint32_t)c->ltab_K;
+    }
     // equal chunks of at most gap_reads_per_chunk reads: every launch ends with a tail in which
     // only its slowest reads still run, so fewer (and balanced) launches waste less -- but no more
     // reads than an earlier run's resume states per read let the state buffer hold (150 bp at 2 %:

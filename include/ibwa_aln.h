@@ -228,7 +228,14 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "width_jump" (0/1/2, default 1) k_width steps one-row intervals from the 2-bit text
  *                                  (1: when those arrays are resident; 2: derive them for a
  *                                  gapped batch too; 0: Occ steps only) -- same widths
+ *   "width_tab" (0/1, default 1)   k_width takes a chain's first steps (up to gap_tab_k + 1) from
+ *                                  the level tables, one round trip for all -- same widths
  *   "kmer_k" (-1 auto, 0 off, 1..16) K-mer interval table length
+ *   "gap_tab_k" (-1 auto, 0 off, 1..14) level tables of the first pass: the SA interval of every
+ *                                  string of length <= K + 1 per strand; nodes at depth <= K are
+ *                                  stored by their strings and expanded from one 32 B load (auto:
+ *                                  floor(log4(n)) up to 13, 14 when both tables fit 15 % of the free
+ *                                  HBM; the CLI pins 13) -- same hits
  *   "exact_blocks", "lanes_per_chunk"
  *   "gapped_v2" (0/1, default 1)   persistent gapped-search kernel (else the general kernels)
  *   "gap_cap1", "gap_pages_per_block", "gap_hit_slots", "gap_blocks_per_cu", "gap_reads_per_chunk"
