@@ -829,7 +829,10 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
                       "(ahead of the parse)\n",
               fg->bgzf() ? "BGZF" : "gzip", ibwa_cli::gz_threads(), fg->input_bytes() / 1e9, fg->inflate_s());
   }
-  if (parse_s > 0) {
+  if (parse_s > 0 && fg && !fg->handoff()) {  // every record parsed on the GPUs: the time is waiting
+    fprintf(stderr, "[ibwa-amd aln] input: %lld reads parsed on the GPUs, %.2f s waited for parsed groups\n",
+            (long long)tot_seqs, parse_s);
+  } else if (parse_s > 0) {
     const int nt = fb ? ibwa_sam::host_threads() : 1;
     fprintf(stderr, "[ibwa-amd aln] input parse: %lld reads in %.2f s on %d host threads = %.2f M reads/s (%.3f M per thread)\n",
             (long long)tot_seqs, parse_s, nt, tot_seqs / parse_s / 1e6, tot_seqs / parse_s / 1e6 / nt);
