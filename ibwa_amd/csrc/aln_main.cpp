@@ -389,9 +389,12 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
   const int n_used = std::min(n_gpus, n_dev);
   const int n_lanes = std::max(1, std::min(4, env_int("IBWA_ALN_LANES", 2)));
   const char *pm = getenv("IBWA_FQ_PIECE_BYTES"), *cm = getenv("IBWA_FQ_CARRY_BYTES");
-  // 2 GiB per GPU (~8 M reads of 100 bp): fewer, larger groups than 1 GiB pieces (align phase 6.12-6.2
-  // vs 5.71-5.79 s at 50 M reads, profiles/r05_e2e_i.json); 2.5 and 3 GiB measured no faster.  An
-  // input that 2 GiB pieces would cut into at most one group per lane (10 M reads of 150 bp: two
+  // 1.5 GiB per GPU (~7 M reads of 100 bp): fewer, larger groups than 1 GiB pieces (align phase 6.12-6.2
+  // vs 5.71-5.79 s at 50 M reads with 2 GiB, profiles/r05_e2e_i.json; 2.5 and 3 GiB measured no
+  // faster); 1.5 GiB aligned as fast as 2 GiB (5.15 vs 5.18-5.36 s) with the arena's peak use 174 ->
+  // 160 GB (round 6, profiles/r06_e2e_mem.json: the resume states and width rows scale with the
+  // group; first-pass chunks capped at 4 M reads inside a group took 141 GB but +10 %).  An
+  // input that the pieces would cut into at most one group per lane (10 M reads of 150 bp: two
   // 1.7 GB groups) is cut into two groups per lane instead: the lanes run their groups side by side
   // either way, and the process stays under ~128 GiB (124 vs 146 GiB for that input, align +6 %,
   // r05_pipe_full_v{2,3}.json) -- so that both ends of a pair can be aligned at once on one GPU.
@@ -411,7 +414,7 @@ int run_aln(Reader &rd, FastqBulk *fb, const ibwa_gap_opt_t &opt, const std::str
     return (double)st.st_size;
   };
   const double in_bytes = fastq_bytes(fq_path && strcmp(fq_path, "-") ? fq_path : nullptr);
-  uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)2 << 30;
+  uint64_t piece = pm && atoll(pm) > 0 ? (uint64_t)atoll(pm) : (uint64_t)3 << 29;
   if (!(pm && atoll(pm) > 0) && fq_dev) {
     const uint64_t fs = (uint64_t)in_bytes;
     const uint64_t per_lane = (uint64_t)n_lanes * (uint64_t)n_gpus;

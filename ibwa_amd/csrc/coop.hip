@@ -72,9 +72,6 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 
 // lane states
 constexpr int L_IDLE = 0, L_FETCH = 1, L_EXP = 2, L_TAIL = 3;
-// an exact tail at a one-row interval (CoopArgs::jsa set): SA[k] wanted, then the read's remaining
-// symbols compared with the text before it, 16 per iteration (the ISA gives the final row)
-constexpr int L_TJ1 = 4, L_TJ2 = 5;
 // prologue chain records: the root chain ended in a hit / did not run (read not for this kernel)
 constexpr uint32_t PRO_HIT = 1, PRO_SKIP = 2;
 
@@ -344,8 +341,6 @@ struct Shm {
                       //  done (1) | stack growth before the chain's last pop << 1 (16 bits) |
                       //  deletions pending in its gap groups << 17}
   uint32_t dirc[4][MAXP];  // page ids of the level's bucket and of its (up to) three target buckets
-  uint8_t str[COOP_MAXLEN];  // bwa_seq_t.seq; strand 1 reads it complemented (COMPREAD); 16 B-aligned
-                             // (a tail jump reads 32 symbols as two 16 B words)
   uint32_t nb[NSTK];       // entries per bucket
   uint16_t np[NSTK];       // pages per bucket (<= MAXP)
   // width arrays (bwt_width_t {w, bid}) of strands 0 / 1 and the seed widths, split so that the
@@ -355,6 +350,7 @@ struct Shm {
   uint32_t SWw[2][COOP_SEEDMAX + 1];
   uint16_t Wb[2][COOP_MAXLEN + 2];
   uint16_t SWb[2][COOP_SEEDMAX + 1];
+  uint8_t str[COOP_MAXLEN];      // bwa_seq_t.seq; strand 1 reads it complemented (COMPREAD)
   uint32_t gm[NSTK / 32];        // buckets holding gap groups
   uint32_t gq;                   // target categories (bit q) that this level's commits gave gap groups
   uint32_t head[64];             // per-lane staging ring: first uncommitted slot
@@ -491,12 +487,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
   const int lane = threadIdx.x;
   const uint64_t wave = blockIdx.x;
   const AlnOpt o = A.o;
-  typedef const __attribute__((address_space(4))) CoopArgs KArgs;
-  auto args = [&]() __attribute__((always_inline)) -> KArgs * {
-    KArgs *p = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();  // A is the first kernel argument
-    asm volatile("" : "+s"(p));
-    return p;
-  };
   const bool comp = o.mode & MODE_COMPREAD;
   // read symbol x of strand a: strand 1 is the complement under COMPREAD
   auto sym_of = [&](int a, int x) __attribute__((always_inline)) -> uint32_t {
@@ -583,7 +573,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     } else {
       // ---------------------------------------------- per-read setup
       const bool seeded = len > o.seed_len;
-      const bool jok = A.jsa[0] != nullptr;  // one-row exact tails jump (SA, ISA and text resident)
       // a first-pass search state to resume from (GapArgs::rdump), 1 + its offset
       const uint64_t rof = A.roff ? A.roff[rr] : 0ull;
       // level 0 done by k_coop_roots: the records of its two chains (A.proot[2 r], [2 r + 1])
@@ -716,7 +705,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         // n_mm | n_gapo << 8 | n_gape << 16 | a << 24 | state << 25
         uint32_t ew = 0;
         uint32_t ent_page = 0, ent_off = 0;
-        uint32_t &tcj = ent_off;  // a tail jump's read symbols compared so far (L_TJ2: no entry fetched)
         // Entry window: lane x holds the entry of chain wh (wh = x mod 64), loaded with an earlier
         // iteration's round trip, so a chain claimed inside the window starts expanding in the
         // iteration that claims it instead of spending one on fetching its entry.
@@ -777,7 +765,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
           else if (m == 0 && (state == STATE_M || gape || e_ge == o.max_gape)) {             // :160
             --i;  // the tail's next symbol
             if (sym_of(a, i) > 3) end = 1;
-            else lst = jok && k == l ? L_TJ1 : L_TAIL;
+            else lst = L_TAIL;
           } else {
             lst = L_EXP;
           }
@@ -1151,19 +1139,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               bk.v2 = pk[2];
               bk.v3 = pk[3];
             }
-            // a tail jump's loads, in the same registers: SA[k]; or three text words from the read's
-            // next compared position (k holds the text position of read symbol 0) and, on the first
-            // compare, the ISA of that position -- the row the tail ends on
-            // (the pointers are re-read from the kernel-argument segment: live through the loop they
-            // took SGPRs, and the kernel's SGPR spills went into VGPR lanes -- 1 -> 14 VGPR spills)
-            if (lst == L_TJ1) bl.v0.x = (a ? args()->jsa[0] : args()->jsa[1])[qk];
-            if (lst == L_TJ2) {
-              const uint32_t *tx = a ? args()->jtxt[0] : args()->jtxt[1];
-              const uint32_t w = (qk + tcj) >> 4;
-              bl.v0.x = tx[w];
-              bl.v0.y = tx[w + 1];
-              if (tcj == 0) bl.v0.w = (a ? args()->jisa[0] : args()->jisa[1])[qk];
-            }
           }
 
           // ============================================ consume
@@ -1185,43 +1160,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
               end_chain(true, k, l);
             } else if (sym_of(a, i) > 3) {
               end_chain(false, 0, 0);
-            } else if (jok && k == l) {
-              lst = L_TJ1;
             }
-          } else if (lst == L_TJ1) {
-            // one row k with its suffix at q = SA[k]: a step by c stays on one row exactly when q > 0 and
-            // text[q - 1] == c (else the interval empties), so the tail's m = i + 1 symbols match exactly
-            // when text[q - m .. q - 1] spells read symbols 0 .. i (bwt.c:240-247 step by step)
-            const uint32_t q = bl.v0.x, m = (uint32_t)(i + 1);
-            if (q < m) {
-              end_chain(false, 0, 0);
-            } else {
-              k = q - m;
-              tcj = 0;
-              lst = L_TJ2;
-            }
-          } else if (lst == L_TJ2) {
-            if (tcj == 0) l = bl.v0.w;  // the row of text position k
-            // read symbols tcj .. tcj + 15 (bytes in LDS) packed 2 bits each; an N among them fails
-            const uint4 sb = *reinterpret_cast<const uint4 *>(&S.str[tcj]);
-            auto pk8 = [](uint32_t x) __attribute__((always_inline)) {
-              return (x & 3u) | ((x >> 6) & 0xCu) | ((x >> 12) & 0x30u) | ((x >> 18) & 0xC0u);
-            };
-            auto nb4 = [](uint32_t x) __attribute__((always_inline)) {
-              return ((x >> 2) & 1u) | ((x >> 9) & 2u) | ((x >> 16) & 4u) | ((x >> 23) & 8u);
-            };
-            uint32_t rd = pk8(sb.x) | pk8(sb.y) << 8 | pk8(sb.z) << 16 | pk8(sb.w) << 24;
-            const uint32_t nf = nb4(sb.x) | nb4(sb.y) << 4 | nb4(sb.z) << 8 | nb4(sb.w) << 12;
-            const int left = i + 1 - (int)tcj;
-            if (a && comp) rd = ~rd;
-            const uint32_t tpos = k + tcj, sh = 2 * (tpos & 15);
-            const uint32_t tw = sh ? (bl.v0.x >> sh) | (bl.v0.y << (32 - sh)) : bl.v0.x;
-            const uint32_t mask = left >= 16 ? 0xFFFFFFFFu : ((1u << (2 * left)) - 1u);
-            const uint32_t nmask = left >= 16 ? 0xFFFFu : ((1u << left) - 1u);
-            const bool fail = (nf & nmask) != 0u || ((tw ^ rd) & mask) != 0u;
-            tcj += 16;
-            // one end_chain call site here (two made the chain state spill)
-            if (fail || (int)tcj > i) end_chain(!fail, l, l);
           } else if (exp) {
             // ---- expansion (bwtgap.c:200-258); the match child continues the chain.  The same steps as
             // expand_node (k_coop_roots), kept inline: through the function this loop's registers

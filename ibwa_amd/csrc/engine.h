@@ -190,9 +190,6 @@ struct CoopArgs {
   // after it: its gap_shadow updates are in them, so a resumed read does not replay them); -1: per
   // launch read (k_width run for this launch)
   int64_t wb_base;
-  // the exact path's full SA, ISA and 2-bit text per strand (nullptr: not resident): an exact tail
-  // at a one-row interval jumps over its remaining symbols (k_exact's unique-interval jump)
-  const uint32_t *jsa[2], *jisa[2], *jtxt[2];
   AlnOpt o;
 };
 hipError_t launch_coop(const CoopArgs &g, unsigned long long *d_counter, int blocks, hipStream_t st);

@@ -300,7 +300,6 @@ struct ibwa_ctx {
   int jump_derive = 1;        // option: derive them for a loaded index when HBM allows
   int exact_jump = 1;
   int width_tab = 1;           // option: k_width's first steps from the level tables (first pass)
-  int coop_jump = 1;           // option: k_coop's one-row exact tails jump when SA / ISA / text are resident
   int width_jump = 1;         // option: k_width steps one-row intervals from the text (2: derive SA / text for it)
   uint32_t sa_intv = 0;
   bool sa_loaded[2] = {false, false};  // sa_s[s] holds a sampled SA of the resident index
@@ -490,15 +489,6 @@ int ensure_kmer(ibwa_ctx *c) {
   }
   c->kmer_valid = true;
   return 0;
-}
-// k_coop's one-row exact-tail jump (CoopArgs::jsa): when the full SA, ISA and text are resident
-void set_coop_jump(const ibwa_ctx *c, CoopArgs &K) {
-  if (!c->coop_jump || !c->jump_ready) return;
-  for (int s = 0; s < 2; ++s) {
-    K.jsa[s] = c->sa_full[s].as<uint32_t>();
-    K.jisa[s] = c->isa_full[s].as<uint32_t>();
-    K.jtxt[s] = c->txt2[s].as<uint32_t>();
-  }
 }
 // The exact path's unique-interval jump needs the full SA, the ISA and the 2-bit text of both
 // strands.  An index built here keeps them (ibwa_ctx_build_index); for an index loaded from .bwt
@@ -779,7 +769,6 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "jump_derive") c->jump_derive = value != 0;
   else if (k == "width_jump" && value >= 0 && value <= 2) c->width_jump = (int)value;
   else if (k == "width_tab" && (value == 0 || value == 1)) c->width_tab = (int)value;
-  else if (k == "coop_jump" && (value == 0 || value == 1)) c->coop_jump = (int)value;
   else if (k == "diag") c->diag = value != 0;
   else if (k == "sa_walk") c->sa_walk = value != 0;
   else if (k == "gap_coop") c->gap_coop = value != 0;
@@ -916,7 +905,6 @@ int ibwa_ctx_share_index(ibwa_ctx_t *dst, const ibwa_ctx_t *src) {
   dst->exact_jump = src->exact_jump;
   dst->width_jump = src->width_jump;
   dst->width_tab = src->width_tab;
-  dst->coop_jump = src->coop_jump;
   dst->share_src = const_cast<ibwa_ctx *>(src);
   ++dst->share_src->n_borrowers;
   return 0;
@@ -1637,7 +1625,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.ix[1] = c->ix[1];
       K.o64[0] = c->o64[0].as<uint4>();
       K.o64[1] = c->o64[1].as<uint4>();
-      set_coop_jump(c, K);
       K.seq = A.seq;
       K.off = A.off;
       K.len = A.len;
@@ -2010,7 +1997,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       K.ix[1] = c->ix[1];
       K.o64[0] = c->o64[0].as<uint4>();
       K.o64[1] = c->o64[1].as<uint4>();
-      set_coop_jump(c, K);
       K.seq = A.seq;
       K.off = A.off;
       K.len = A.len;

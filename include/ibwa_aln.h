@@ -231,9 +231,6 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "width_tab" (0/1, default 1)   k_width takes a chain's first steps (up to gap_tab_k + 1) from
  *                                  the level tables, one round trip for all -- same widths
  *   "kmer_k" (-1 auto, 0 off, 1..16) K-mer interval table length
- *   "coop_jump" (0/1, default 1)   the cooperative pass's exact tails at a one-row interval jump over
- *                                  their remaining symbols (SA, text compare, ISA) when the full SA /
- *                                  ISA / text are resident -- same hits
  *   "gap_tab_k" (-1 auto, 0 off, 1..14) level tables of the first pass: the SA interval of every
  *                                  string of length <= K + 1 per strand; nodes at depth <= K are
  *                                  stored by their strings and expanded from one 32 B load (auto:

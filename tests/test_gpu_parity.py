@@ -99,17 +99,15 @@ def test_fetch_sai_equals_fetch(golden_dir, sai_manifest, gpu_engine):
         assert need.value == len(body) and small.raw == b"\x5a" * 16
 
 
-@pytest.mark.parametrize("width_jump,width_tab,coop_jump", [(0, 1, 1), (2, 1, 1), (2, 1, 0), (1, 0, 1), (0, 0, 1)])
-def test_sai_goldens_width_jump(golden_dir, sai_manifest, gpu_engine, width_jump, width_tab, coop_jump):
-    """k_width with (2: SA / ISA / text derived from the loaded BWT) and without (0) one-row steps
-    from the text, with and without its leading steps from the level tables (width_tab): every
-    gapped golden, in the first pass and (budget 1) through the heavy-read pass -- which, with the
-    derived arrays, jumps its one-row exact tails (coop_jump 1) or steps them (0)."""
+@pytest.mark.parametrize("width_jump,width_tab", [(0, 1), (2, 1), (1, 0), (0, 0)])
+def test_sai_goldens_width_jump(golden_dir, sai_manifest, gpu_engine, width_jump, width_tab):
+    """k_width with (2: SA / text derived from the loaded BWT) and without (0) one-row steps from
+    the text, with and without its leading steps from the level tables (width_tab): every gapped
+    golden, in the first pass and (budget 1) through the heavy-read pass."""
     bad = []
     try:
         gpu_engine.set_option("width_jump", width_jump)
         gpu_engine.set_option("width_tab", width_tab)
-        gpu_engine.set_option("coop_jump", coop_jump)
         for budget in (8000, 1):
             gpu_engine.set_option("gap_iter_budget", budget)
             for key, m in sorted(sai_manifest.items()):
@@ -125,7 +123,6 @@ def test_sai_goldens_width_jump(golden_dir, sai_manifest, gpu_engine, width_jump
     finally:
         gpu_engine.set_option("width_jump", 1)
         gpu_engine.set_option("width_tab", 1)
-        gpu_engine.set_option("coop_jump", 1)
         gpu_engine.set_option("gap_iter_budget", 8000)
     assert not bad, bad
 

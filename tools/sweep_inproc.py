@@ -28,7 +28,7 @@ DEFAULTS = {"gap_early_iters": 3000, "gap_early_entries": 1000, "gap_iter_budget
             "gap_resume_iters": 2000, "gap_resume_entries": 300, "gap_tail_lanes": 16, "gap_tail_iters": 200,
             "gap_pages_per_block": 384, "gap_cap1": 8192, "gap_resume_ppb": 48, "gap_resume_cap1": 4096,
             "coop_pool_gb": 0, "gap_lw_min_waves": 8, "coop_waves_per_cu": 12,
-            "coop_stg_room": 1, "gap_resume_recs": 192, "kmer_k": -1, "gap_tab_k": -1, "width_tab": 1, "coop_jump": 1}
+            "coop_stg_room": 1, "gap_resume_recs": 192, "kmer_k": -1, "gap_tab_k": -1, "width_tab": 1}
 
 
 def main():
