@@ -178,36 +178,53 @@ __device__ __forceinline__ uint32_t rec_byte(uint2 a, uint2 b, uint32_t pa, uint
 // text: row k with k == l has the suffix at q = SA[k], BWT[k] = text[q-1], and stepping with c
 // stays on one row (suffix at q-1) exactly when q > 0 and text[q-1] == c; otherwise the interval
 // is empty and the reference resets it.  Mode 0: Occ steps; 1: the interval became one row at
-// the last step -- this step is an Occ step that also loads SA[k]; 2: text steps (suffix at t),
-// one 2-bit text word loaded per 16 steps.  Every mode issues its loads in the same round trip
-// as the other chain's and the other lanes' (the chains stay in lockstep).
+// the last step -- this step is an Occ step that also loads SA[k]; 2: text steps (suffix at t)
+// from a window of two 2-bit text words (32 symbols).  Every mode issues its loads in the same
+// round trip as the other chain's and the other lanes' (the chains stay in lockstep), and the text
+// windows are refilled at the 16-position blocks' first step (`refresh`), for the block's 16 steps at
+// once: text-mode lanes then load in the same steps, so the wave waits once per block for them
+// instead of at almost every step (a lane entering text mode inside a block loads its window then).
 struct WChain {
   uint32_t k, l, bid;
-  uint32_t mode, t, wi, w;  // text mode: suffix position, cached text word index and word
+  uint32_t mode, t, wi, w, w2;  // text mode: suffix position, window's first word index, its two words
 };
 
 struct WLoad {
   Fetch1 f;
-  uint32_t q, w;
+  uint32_t q, w, w2, wi;
   bool tl;
 };
 
+// text position p is in the chain's window
+__device__ __forceinline__ bool win_has(const WChain &h, uint32_t p) {
+  return h.wi != 0xFFFFFFFFu && p >= 16u * h.wi && p - 16u * h.wi < 32u;
+}
+
 // the step's loads (issued for both chains before either is consumed: one round trip)
 __device__ __forceinline__ void wchain_load(const IndexView &ix, const uint32_t *sa, const uint32_t *tx,
-                                            const WChain &h, uint32_t c, WLoad &x) {
+                                            const WChain &h, uint32_t c, WLoad &x, bool refresh) {
   fetch1(ix, h.k - 1, h.l, c & 3, c < 4 && h.mode != 2, x.f);
   x.q = 0;
   if (h.mode == 1) x.q = sa[h.k];
-  const uint32_t twi = (h.t - 1u) >> 4;
-  x.tl = h.mode == 2 && h.t > 0 && twi != h.wi;
+  // the next 16 steps read text positions p, p - 1, ..., p - 15 (p = t - 1): a window from word
+  // (p - 15) / 16 holds them all
+  const uint32_t p = h.t - 1u;
+  x.tl = h.mode == 2 && h.t > 0 && (!win_has(h, p) || (refresh && !win_has(h, p >= 15u ? p - 15u : 0u)));
+  x.wi = (p >= 15u ? p - 15u : 0u) >> 4;
   x.w = h.w;
-  if (x.tl) x.w = tx[twi];
+  x.w2 = h.w2;
+  if (x.tl) {
+    x.w = tx[x.wi];
+    x.w2 = tx[x.wi + 1];
+  }
 }
 
 __device__ __forceinline__ void wchain_step(const IndexView &ix, bool jump, WChain &h, uint32_t c, const WLoad &x) {
   if (h.mode == 2) {
-    if (x.tl) { h.w = x.w; h.wi = (h.t - 1u) >> 4; }
-    if (h.t > 0 && c < 4 && ((x.w >> (2 * ((h.t - 1u) & 15))) & 3u) == c) {
+    if (x.tl) { h.w = x.w; h.w2 = x.w2; h.wi = x.wi; }
+    const uint32_t p = h.t - 1u;
+    const uint32_t tw = p - 16u * h.wi < 16u ? h.w : h.w2;
+    if (h.t > 0 && c < 4 && ((tw >> (2 * (p & 15))) & 3u) == c) {
       --h.t;  // still one row: k == l stays, width 1
     } else {
       h.k = 0; h.l = ix.seq_len; ++h.bid; h.mode = 0;
@@ -245,8 +262,8 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
                                            const uint32_t *sa0 = nullptr, const uint32_t *sa1 = nullptr,
                                            const uint32_t *tx0 = nullptr, const uint32_t *tx1 = nullptr,
                                            const uint2 *lta = nullptr, const uint2 *ltb = nullptr, int tdep = 0) {
-  WChain A{0u, ixa.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u};
-  WChain B{0u, ixb.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u};
+  WChain A{0u, ixa.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u, 0u};
+  WChain B{0u, ixb.seq_len, 0u, 0u, 0u, 0xFFFFFFFFu, 0u, 0u};
   uint32_t lwa = 0, lwb = 0;  // sum of log2(width) over the positions (diagnostics)
   uint32_t pa = 0, pb = 0;    // previous positions' widths (record)
   // The first min(L, tdep) steps of both chains from the level tables (AlnArgs::ltab): the interval
@@ -296,8 +313,8 @@ __device__ __forceinline__ void width_pair(const IndexView ixa, const IndexView 
         uint32_t cb = strand_base(ca, 1, comp);
         const bool tA = FIRST && t < TMAX && t < da, tB = FIRST && t < TMAX && t < db;
         WLoad xa, xb;
-        if (!tA) wchain_load(ixa, sa0, tx0, A, ca, xa);
-        if (!tB) wchain_load(ixb, sa1, tx1, B, cb, xb);
+        if (!tA) wchain_load(ixa, sa0, tx0, A, ca, xa, t == 0);
+        if (!tB) wchain_load(ixb, sa1, tx1, B, cb, xb, t == 0);
         if (FIRST && t < TMAX && tA) {
           A.k = ta[t < TMAX ? t : 0].x;
           A.l = ta[t < TMAX ? t : 0].y;
