@@ -95,8 +95,6 @@ struct GapArgs {
   uint32_t max_iters;        // iteration budget per read (0: none); over it -> ST_HEAVY
   uint32_t early_iters;      // early hand-off: past this many iterations (0: off) a read whose
   uint32_t early_entries;    //   stack holds more than early_entries entries -> ST_HEAVY
-  uint32_t early2_iters;     // a second such rule (0: off), e.g. an earlier check with a larger stack
-  uint32_t early2_entries;
   int lanes_per_wave;        // reads a wave runs at once (64; 1 for heavy reads)
   int free_depth;            // LDS free-slot stack per read (wide kernel)
   // LDS-resident widths (first pass, when they fit): the k_width records (AlnArgs::cw) copied into

@@ -288,7 +288,6 @@ struct ibwa_ctx {
   std::vector<std::vector<uint4>> patch_alns;       // their hits (the coop pass writes into d_aln / d_naln)
   DBuf d_selst, d_seltmp;                           // statuses of the handed-on reads, select scratch
   DBuf d_ordk, d_ordi, d_ordids, d_ordtmp;          // the coop pass's order (largest first-pass stack first)
-  int coop_order = 1;                               // option
   int coop_roots = 1;                               // option: level 0 of the heavy reads by k_coop_roots
   uint32_t aln_cap_used = 0;
   // sampled suffix arrays kept by ibwa_ctx_build_index
@@ -325,7 +324,6 @@ struct ibwa_ctx {
   // early hand-off to the coop pass: a read past 3000 iterations whose stack holds > 1000 entries
   // (swept at 10M reads: 2.28 -> 2.14 s per step; budget 6000-16000 with it: within noise)
   uint32_t gap_early_iters = 3000, gap_early_entries = 1000;
-  uint32_t gap_early2_iters = 0, gap_early2_entries = 0;  // a second early hand-off rule (0: off)
   uint32_t gap_iter_budget = 8000;   // first-pass iterations per read before handing it to the coop pass (swept 1000-8000 at 50M reads: 8000 best)
   DBuf d_nN, d_pool, d_aoff, r_aoff, d_iters;
   // wave-cooperative heavy-read pass (coop.hip)
@@ -748,8 +746,6 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_iter_budget" && value >= 0) c->gap_iter_budget = (uint32_t)value;
   else if (k == "gap_early_iters" && value >= 0) c->gap_early_iters = (uint32_t)value;
   else if (k == "gap_early_entries" && value >= 0) c->gap_early_entries = (uint32_t)value;
-  else if (k == "gap_early2_iters" && value >= 0) c->gap_early2_iters = (uint32_t)value;
-  else if (k == "gap_early2_entries" && value >= 0) c->gap_early2_entries = (uint32_t)value;
   else if (k == "gap_lw" && (value == 0 || value == 1)) c->gap_lw = (int)value;
   else if (k == "gap_lw_min_waves" && value >= 1 && value <= 32) c->gap_lw_min_waves = (int)value;
   else if (k == "gap_resume" && (value == 0 || value == 1)) c->gap_resume = (int)value;
@@ -761,7 +757,6 @@ int ibwa_ctx_set_option(ibwa_ctx_t *c, const char *key, long value) {
   else if (k == "gap_tail_iters" && value >= 0) c->gap_tail_iters = (uint32_t)value;
   else if (k == "gap_resume_ppb" && value >= 1 && value <= 65536) c->gap_resume_ppb = (int)value;
   else if (k == "gap_resume_cap1" && value >= 16 && value <= 65536) c->gap_resume_cap1 = (uint32_t)value;
-  else if (k == "coop_order" && (value == 0 || value == 1)) c->coop_order = (int)value;
   else if (k == "coop_roots" && (value == 0 || value == 1)) c->coop_roots = (int)value;
   else if (k == "gap_stream_per_read" && value >= 0 && value <= 4096) c->gap_stream_per_read = (uint32_t)value;
   else if (k == "gap_stream_min" && value >= 1) c->gap_stream_min = (uint64_t)value;
@@ -1608,7 +1603,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       if (int rc = c->r_status.ensure(lanes * 4)) return rc;
       // largest first-pass stack first, as in the main cooperative pass below
       const int64_t *ids = c->d_ids.as<int64_t>();
-      if (c->coop_order && lanes > 1) {
+      if (lanes > 1) {
         size_t ob = 0;
         HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &ob, st));
         if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;
@@ -1751,8 +1746,6 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       G.max_iters = c->gap_iter_budget;
       G.early_iters = resume ? c->gap_resume_iters : c->gap_early_iters;
       G.early_entries = resume ? c->gap_resume_entries : c->gap_early_entries;
-      G.early2_iters = c->gap_early2_iters;
-      G.early2_entries = c->gap_early2_entries;
       if (resume) {
         G.rdump = c->d_rdump.as<uint4>();
         G.rd_next = c->d_roff.as<unsigned long long>() + n;
@@ -1968,7 +1961,7 @@ int ibwa_batch_run(ibwa_ctx_t *c, const ibwa_gap_opt_t *opt, int batch_max_len) 
       // which order resolves a read changes nothing in its results
       if (round) HIPCHK(hipMemcpy(c->d_ids.p, todo.data(), lanes * 8, hipMemcpyHostToDevice));
       const int64_t *coop_ids = c->d_ids.as<int64_t>();
-      if (!round && c->coop_order && lanes > 1) {
+      if (!round && lanes > 1) {
         size_t tb = 0;
         HIPCHK(order_heavy_first(nullptr, nullptr, lanes, nullptr, nullptr, nullptr, nullptr, &tb, c->stream));
         if (int rc = c->d_ordk.ensure(lanes * 8)) return rc;

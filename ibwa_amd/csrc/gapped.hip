@@ -637,8 +637,7 @@ __device__ __forceinline__ void gapped_body(const GapArgs &A, unsigned long long
     // leave their states for the cooperative pass instead of holding the wave (and the launch) open
     const bool tail = LW && A.rdump && A.tail_lanes && !more && (uint32_t)__popcll(__ballot(st != 0)) <= A.tail_lanes &&
                       n_iter > A.tail_iters;
-    if ((over_budget || tail || (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries) ||
-         (A.early2_iters && n_iter > A.early2_iters && n_entries > (int)A.early2_entries)) &&
+    if ((over_budget || tail || (A.early_iters && n_iter > A.early_iters && n_entries > (int)A.early_entries)) &&
         (st == 1 || st == 2)) {
       if (LW && A.rdump && !over_budget && st == 1) {
         // resume: the read leaves its search state at this pop (below)

@@ -1040,6 +1040,10 @@ struct Out {
   FILE *fp;
   std::string b;
   std::thread w;  // print_parallel's write-behind of a batch's lines
+  // print_parallel's per-thread line buffers, handed back by the writer with their capacity: a batch's
+  // lines go into memory the previous batch already faulted in (a fresh ~0.2 GB per batch, allocated,
+  // faulted in and freed, cost about as much as formatting into it)
+  std::vector<std::string> spare;
   void wait() {
     if (w.joinable()) w.join();
   }
@@ -1052,6 +1056,17 @@ struct Out {
   Out &s(const char *x) { b += x; return *this; }
   Out &s(const std::string &x) { b += x; return *this; }
   Out &c(char x) { b += x; return *this; }
+  // n bases of s as letters (codes 0-4), or the reverse complement of s[0, n)
+  Out &bases(const uint8_t *q, int n, bool rc) {
+    const size_t o0 = b.size();
+    b.resize(o0 + (size_t)(n > 0 ? n : 0));
+    char *w = &b[o0];
+    if (!rc)
+      for (int k = 0; k < n; ++k) w[k] = "ACGTN"[q[k]];
+    else
+      for (int k = 0; k < n; ++k) w[k] = "TGCAN"[q[n - 1 - k]];
+    return *this;
+  }
   Out &i(long long v) {  // %lld
     char t[24];
     char *e = t + sizeof t, *q = e;
@@ -1124,10 +1139,7 @@ inline void print_sam1(Out &o, const Dbs &d, Read &p, const Read *mate, int mode
     } else {
       o.s("\t*\t0\t0\t");
     }
-    if (p.strand == 0)
-      for (int k = 0; k < p.full_len; ++k) o.c("ACGTN"[p.seq[k]]);
-    else
-      for (int k = 0; k < p.full_len; ++k) o.c("TGCAN"[p.seq[p.full_len - 1 - k]]);
+    o.bases(p.seq.data(), p.full_len, p.strand != 0);
     o.c('\t');
     if (p.has_qual) {
       if (p.strand) std::reverse(p.qual.begin(), p.qual.begin() + std::min<size_t>(p.len, p.qual.size()));
@@ -1180,7 +1192,7 @@ inline void print_sam1(Out &o, const Dbs &d, Read &p, const Read *mate, int mode
     int flag = p.extra_flag | SAM_FSU;
     if (mate && mate->type == TYPE_NO_MATCH) flag |= SAM_FMU;
     o.s(p.name).c('\t').i(flag).s("\t*\t0\t0\t*\t*\t0\t0\t");
-    for (int k = 0; k < p.len; ++k) o.c("ACGTN"[s[k]]);
+    o.bases(s.data(), p.len, false);
     o.c('\t');
     if (p.has_qual) {
       if (p.strand) std::reverse(p.qual.begin(), p.qual.begin() + std::min<size_t>(p.len, p.qual.size()));
@@ -1197,18 +1209,24 @@ inline void print_sam1(Out &o, const Dbs &d, Read &p, const Read *mate, int mode
 
 // SAM lines of items [0, n) formatted on host threads into per-chunk buffers, written in order
 inline void print_parallel(Out &o, int64_t n, const std::function<void(Out &, int64_t)> &fmt) {
-  o.flush();
+  o.flush();  // (joins the previous batch's writer: o.spare holds its buffers)
   const int nt = host_threads();
-  std::vector<std::string> bufs(nt);
+  std::vector<std::string> bufs = std::move(o.spare);
+  o.spare.clear();
+  bufs.resize(nt);
+  for (auto &x : bufs) x.clear();  // (a small batch leaves some unused: none may write old lines)
   parallel_chunks(n, [&](int64_t lo, int64_t hi, int t) {
-    Out ob{nullptr, {}};
+    Out ob{nullptr, std::move(bufs[t])};
     for (int64_t i = lo; i < hi; ++i) fmt(ob, i);
-    bufs[t].swap(ob.b);
+    bufs[t] = std::move(ob.b);
   }, nt);
-  // written while the next batch is worked on (Out::flush / the next call / ~Out wait for it)
-  o.w = std::thread([fp = o.fp, bufs = std::move(bufs)]() {
+  // written while the next batch is worked on (Out::flush / the next call / ~Out wait for it), then
+  // handed back for the next batch
+  Out *op = &o;
+  o.w = std::thread([op, fp = o.fp, bufs = std::move(bufs)]() mutable {
     for (auto &x : bufs)
       if (!x.empty()) fwrite(x.data(), 1, x.size(), fp);
+    op->spare = std::move(bufs);
   });
 }
 

@@ -247,7 +247,6 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *   "gap_iter_budget" (8000)       first-pass iterations before a read goes to the cooperative pass
  *   "gap_early_iters", "gap_early_entries" (3000, 1000)
  *                                  earlier hand-off of a read whose stack holds that many entries
- *   "gap_early2_iters", "gap_early2_entries" (0, 0)  a second such rule (0: off)
  *   "gap_resume" (0/1, default 1), "gap_resume_gb" (48)  an early hand-off leaves the read's search
  *                                  state (at the next score-level boundary) for the cooperative pass,
  *                                  which resumes it instead of starting over; state buffer size cap

@@ -4,7 +4,7 @@ its index and the reads are built once, then every config runs one warm-up and -
 (same reads, same box), printing per-kernel times and the heavy-read count.  Each config's hits are
 compared with the first config's (bit-exact: options that only move work between passes must not
 change a single hit).
-usage: tools/sweep_inproc.py [--reads 50000000] [--steps 1] "" "gap_early2_iters=1000,gap_early2_entries=1000" ...
+usage: tools/sweep_inproc.py [--reads 50000000] [--steps 1] "" "gap_resume_iters=3000,gap_resume_entries=500" ...
 """
 import argparse
 import json
@@ -23,7 +23,7 @@ from ibwa_amd import engine as E  # noqa: E402
 
 # engine defaults of the options a config may set (engine.hip)
 DEFAULTS = {"gap_early_iters": 3000, "gap_early_entries": 1000, "gap_iter_budget": 8000,
-            "gap_early2_iters": 0, "gap_early2_entries": 0, "gap_resume": 1, "gap_resume_gb": 48,
+            "gap_resume": 1, "gap_resume_gb": 48,
             "coop_roots": 1, "gap_reads_per_chunk": 16 << 20,
             "gap_resume_iters": 2000, "gap_resume_entries": 300, "gap_tail_lanes": 16, "gap_tail_iters": 200,
             "gap_pages_per_block": 384, "gap_cap1": 8192, "gap_resume_ppb": 48, "gap_resume_cap1": 4096,
