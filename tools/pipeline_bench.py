@@ -53,10 +53,10 @@ def run(argv, stdout=None, timeout=1200):
     return dt
 
 
-def run_both(argvs, timeout=1200):
+def run_both(argvs, timeout=1200, env=None):
     """Both commands at once (the two ends' aln on one GPU); wall of the pair and of each."""
     t = time.perf_counter()
-    ps = [subprocess.Popen(a, stderr=subprocess.PIPE) for a in argvs]
+    ps = [subprocess.Popen(a, stderr=subprocess.PIPE, env=env) for a in argvs]
     walls, errs = [], []
     for p_ in ps:
         _, err = p_.communicate(timeout=timeout)
@@ -164,6 +164,9 @@ def main():
     ap.add_argument("--sub", type=float, default=0.02)
     ap.add_argument("--threads", type=int, default=bench.host_threads())
     ap.add_argument("--concurrent-ends", type=int, default=1, help="also align the two ends at once (one GPU)")
+    ap.add_argument("--concurrent-lanes", default="1,2",
+                    help="IBWA_ALN_LANES of each of the two processes aligning the ends at once (the first is "
+                         "the pipeline's: one lane each, the other process overlapping it; then the others)")
     ap.add_argument("--sampe-workers", default="1,2", help="sampe -R -G values to time (the first is sampe_s)")
     ap.add_argument("--out", default="")
     ap.add_argument("--diag", action="store_true", help="only run `aln` on the sample's end 2 with IBWA_VERBOSE")
@@ -207,10 +210,21 @@ def main():
     sai = [os.path.join(tmp, f"r{e}.sai") for e in (1, 2)]
     csai = [os.path.join(tmp, f"c{e}.sai") for e in (1, 2)]
     if a.concurrent_ends:
-        time.sleep(8.0)  # the index builder's memory wiped first (the next GPU process waits for it)
-        pair_s, walls = run_both([[CLI, "aln", "-f", csai[e], P, fq[e]] for e in (0, 1)])
-        res["aln_concurrent"] = {"pair_wall_s": pair_s, "walls_s": walls}
-        log(f"ibwa-amd: both ends' aln at once: {pair_s:.2f} s for the pair")
+        # one lane per process by default: the other end's process overlaps it as a second lane would,
+        # and the two arenas (~87 instead of ~139 GiB each for 10 M x 150 bp) leave the device room, so
+        # neither waits for the other's allocation
+        for li, lanes in enumerate(int(x) for x in a.concurrent_lanes.split(",")):
+            time.sleep(8.0)  # the previous GPU process's memory wiped first (the next one waits for it)
+            env = dict(os.environ, IBWA_ALN_LANES=str(lanes))
+            pair_s, walls = run_both([[CLI, "aln", "-f", csai[e], P, fq[e]] for e in (0, 1)], env=env)
+            if li == 0:
+                res["aln_concurrent"] = {"pair_wall_s": pair_s, "walls_s": walls, "lanes_per_process": lanes}
+                csai_first = [open(f_, "rb").read() for f_ in csai]
+            else:
+                res.setdefault("aln_concurrent_other_lanes", []).append(
+                    {"lanes_per_process": lanes, "pair_wall_s": pair_s, "walls_s": walls,
+                     "sai_equal_first": [open(f_, "rb").read() for f_ in csai] == csai_first})
+            log(f"ibwa-amd: both ends' aln at once, {lanes} lane(s) per process: {pair_s:.2f} s for the pair")
     time.sleep(8.0)  # their memory wiped before the sequential runs
     res["aln_s"] = [run([CLI, "aln", "-f", sai[e], P, fq[e]]) for e in (0, 1)]
     if a.concurrent_ends:
