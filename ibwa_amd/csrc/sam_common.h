@@ -736,10 +736,12 @@ inline int approx_mapQ(const Read &p, int mm) {
 // bwa_cal_md1 (bwase.c:243-295)
 inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, const Dbs &b, int *nm_out) {
   // the reference bases of a CIGAR run are extracted at once (extract(x, n) == n one-base extracts:
-  // both stop at l_pac and cross references the same way), the numbers formatted in place
-  std::string str;
-  str.reserve(32);
-  auto put_int = [&str](int v) {
+  // both stop at l_pac and cross references the same way), the numbers formatted in place; built in a
+  // per-thread buffer and returned as one string (most MD strings fit the string's inline storage:
+  // no allocation per read)
+  thread_local std::string str;
+  str.clear();
+  auto put_int = [](int v) {
     char t[12];
     char *e = t + sizeof t, *q = e;
     unsigned u = (unsigned)v;
@@ -810,7 +812,7 @@ inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, cons
   }
   put_int(u);
   *nm_out = nm;
-  return str;
+  return std::string(str);
 }
 
 // bwa_correct_trimmed (bwase.c:297-331)
