@@ -263,7 +263,14 @@ int ibwa_batch_stats(const ibwa_ctx_t *ctx, ibwa_run_stats_t *st);
  *                                  that run out of its pages run again in up to two more launches with
  *                                  the whole pool, then the wide kernel; "coop_pool_pages": the pool
  *                                  in pages, for tests)
- *   "coop_stg_room" (1)            its per-lane staging ring holds this many chains' children (1..4) */
+ *   "coop_stg_room" (1)            its per-lane staging ring holds this many chains' children (1..4)
+ *   "coop_roots" (0/1, default 1)  level 0 of the heavy reads one root chain per lane (k_coop_roots)
+ *   "gap_coop" (0/1, default 1)    the cooperative pass (0: heavy reads go to the wide kernel)
+ *   "sa_walk" (0/1, default 0)     SA -> coordinate by walking the sampled SA even when the full SA is
+ *                                  resident
+ *   Test and diagnostics hooks: "gap_stream_per_read" (4), "gap_stream_min" (1 << 20) the first
+ *   pass's hit-stream size; "gap_resume_records", "coop_pool_pages" buffer sizes in records / pages;
+ *   "diag" (0) per-read iterations and k_width features; "sw_stop" (0) stop k_sw after a pass. */
 int ibwa_ctx_set_option(ibwa_ctx_t *ctx, const char *key, long value);
 
 /* The sources this library was built from: the first 16 hex digits of the SHA-256 of the
