@@ -1204,6 +1204,11 @@ struct Sampe {
             ps.clear();
             int min_score = INT32_MAX;
             const AlnSpan &ag = alns[j][i];
+            // one alignment on a reference without a remapping table: its rows' positions are distinct
+            // (distinct suffixes) and unmoved, and all score the same -- c1 = the positions kept, c2 = 0,
+            // no sort (the repeats' long lists are mostly such ends)
+            const bool one = ag.size() == 1 && !dbs.db[ag[0].dbidx].remap;
+            size_t n_one = 0;
             for (size_t k = 0; k < ag.size(); ++k) {
               const ibwa_aln1_t &a = ag[k].aln;
               const int d = ag[k].dbidx;
@@ -1226,26 +1231,29 @@ struct Sampe {
                 if (!status) continue;
                 ap.idx_and_end = (uint32_t)k << 1 | (uint32_t)j;
                 arr.push(ap);
-                ps.push_back({ap.remapped_pos, a.score});
+                if (one) ++n_one;
+                else ps.push_back({ap.remapped_pos, a.score});
               }
             }
             const int64_t t1 = pstats ? now_ns() : 0;
             if (pstats) a_pos += t1 - t0;
             // c1 / c2 below need the positions grouped, each group's lowest score first: a sort
             // by (remapped position, score), on one 64-bit key when the values fit
-            bool sc20 = true;
-            for (const auto &x : ps) sc20 = sc20 && (unsigned)x.second < (1u << 20);
-            if (ps.size() > 256 && fit32 && sc20) {
-              kk.resize(ps.size());
-              for (size_t t = 0; t < ps.size(); ++t) kk[t] = ps[t].first << 20 | (uint64_t)(ps[t].second & 0xFFFFF);
-              radix_sort_u64(kk.size(), kk.data(), nullptr, tk, tv);
-              for (size_t t = 0; t < ps.size(); ++t) ps[t] = {kk[t] >> 20, (int)(kk[t] & 0xFFFFF)};
-            } else {
-              std::sort(ps.begin(), ps.end());
+            size_t c[2] = {n_one, 0};
+            if (!one) {
+              bool sc20 = true;
+              for (const auto &x : ps) sc20 = sc20 && (unsigned)x.second < (1u << 20);
+              if (ps.size() > 256 && fit32 && sc20) {
+                kk.resize(ps.size());
+                for (size_t t = 0; t < ps.size(); ++t) kk[t] = ps[t].first << 20 | (uint64_t)(ps[t].second & 0xFFFFF);
+                radix_sort_u64(kk.size(), kk.data(), nullptr, tk, tv);
+                for (size_t t = 0; t < ps.size(); ++t) ps[t] = {kk[t] >> 20, (int)(kk[t] & 0xFFFFF)};
+              } else {
+                std::sort(ps.begin(), ps.end());
+              }
+              for (size_t t = 0; t < ps.size(); ++t)
+                if (t == 0 || ps[t].first != ps[t - 1].first) ++c[ps[t].second == min_score ? 0 : 1];
             }
-            size_t c[2] = {0, 0};
-            for (size_t t = 0; t < ps.size(); ++t)
-              if (t == 0 || ps[t].first != ps[t - 1].first) ++c[ps[t].second == min_score ? 0 : 1];
             p[j]->c1 = (uint32_t)c[0] & 0xfffffffu;
             p[j]->c2 = (uint32_t)c[1] & 0xfffffffu;
             if (p[j]->c1 != 0) p[j]->type = p[j]->c1 > 1 ? TYPE_REPEAT : TYPE_UNIQUE;
