@@ -1488,7 +1488,11 @@ struct Sampe {
           Read &r = seqs[j][i];
           ibwa_ref_seq_t &t = ref[j][i];
           memset(&t, 0, sizeof t);
-          std::reverse_copy(r.seq.begin(), r.seq.begin() + r.len, rev[j].get() + ro[i]);  // bwa_seq_t.seq: reversed
+          // the sequences of pairs bwa_paired_sw looks at (bwasw.c:157-159: an end with mapQ >= 17, end 1
+          // not properly paired -- its first test, before any sequence is read); the others' are never read
+          const bool looked_at = (seqs[0][i].mapQ >= 17 || seqs[1][i].mapQ >= 17) && (seqs[0][i].extra_flag & SAM_FPP) == 0;
+          if (looked_at)
+            std::reverse_copy(r.seq.begin(), r.seq.begin() + r.len, rev[j].get() + ro[i]);  // bwa_seq_t.seq: reversed
           t.seq = rev[j].get() + ro[i];
           t.rseq = r.rseq.data();
           t.len = (uint32_t)r.len;
