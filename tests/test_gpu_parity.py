@@ -127,6 +127,54 @@ def test_sai_goldens_width_jump(golden_dir, sai_manifest, gpu_engine, width_jump
     assert not bad, bad
 
 
+def _edge_records(golden_dir, seed=7):
+    """Reads from the first and last bases of the golden reference (and its middle), forward and
+    reverse-complemented, exact and with one or two substitutions, 100 / 36 / 20 / 12 bp."""
+    codes, l_pac = oracle.read_pac(os.path.join(golden_dir, "g1m"))
+    rng = np.random.default_rng(seed)
+    recs = []
+    for L in (100, 36, 20, 12):
+        for start in (0, 1, 5, 17, l_pac // 2, l_pac - L - 3, l_pac - L):
+            ref = codes[start:start + L].astype(np.int64)
+            for nm in (0, 1, 2):
+                t = ref.copy()
+                for p in rng.choice(L, size=nm, replace=False):
+                    t[p] = (t[p] + 1 + rng.integers(3)) % 4
+                for rc in (False, True):
+                    u = 3 - t[::-1] if rc else t
+                    recs.append((f"e{len(recs)}", "".join("ACGT"[c] for c in u).encode(), b"I" * L))
+            # an N where k_width's table prefix reads (the read's last bases: bwa_seq_t.seq is reversed)
+            for q in (L - 1, L - 4, L - 15, L - 17):
+                if 0 <= q < L:
+                    u = bytearray("".join("ACGT"[c] for c in ref).encode())
+                    u[q] = ord("N")
+                    recs.append((f"e{len(recs)}", bytes(u), b"I" * L))
+    return recs
+
+
+@pytest.mark.parametrize("width_jump,budget", [(1, 8000), (2, 8000), (2, 1), (0, 1)])
+def test_reference_edge_reads(golden_dir, gpu_engine, width_jump, budget):
+    """Reads at the reference's ends: k_width's level-table prefix and its text windows as the
+    suffix position nears 0 (width_jump 2 derives the SA / text of the loaded index), the level
+    tables' short-read rule (12 / 20 bp reads keep intervals), in the first pass and (budget 1)
+    through the heavy-read pass -- hits equal to the oracle's."""
+    recs = _edge_records(golden_dir)
+    opt, _ = oracle.parse_aln_args([])
+    seqs, offs, lens = oracle.encode_reads(recs, opt.mode, opt.trim_qual)
+    try:
+        gpu_engine.set_option("width_jump", width_jump)
+        gpu_engine.set_option("gap_iter_budget", budget)
+        n_aln, alns = gpu_engine.aln(seqs, offs, lens, _eopt(opt))
+    finally:
+        gpu_engine.set_option("width_jump", 1)
+        gpu_engine.set_option("gap_iter_budget", 8000)
+    b0 = oracle.Bwt(os.path.join(golden_dir, "g1m.bwt"))
+    b1 = oracle.Bwt(os.path.join(golden_dir, "g1m.rbwt"))
+    rn, ra, _ = oracle.cal_sa_reg_gap(b0, b1, seqs, offs, lens, opt)
+    assert (n_aln == rn).all() and alns.tobytes() == ra.tobytes()
+    assert int(rn.sum()) > len(recs) // 2  # most of them align
+
+
 @pytest.mark.parametrize("coop", [1, 0])
 def test_sai_goldens_heavy_pass(golden_dir, sai_manifest, gpu_engine, coop):
     """An iteration budget of 1 hands every gapped read to the heavy-read pass: the
