@@ -163,6 +163,7 @@ def test_exact_reads_round_trip(mid_genome):
     (["-l", "20", "-k", "1"], 100, 0.02, 8_000, {"gap_tab_k": 8, "gap_resume_iters": 20, "gap_resume_entries": 4}),
     (["-L", "-d", "30"], 100, 0.02, 8_000, {"gap_tab_k": 11, "gap_resume_iters": 20, "gap_resume_entries": 4}),
     ([], 150, 0.02, 8_000, {"gap_tab_k": 13, "gap_resume_iters": 20, "gap_resume_entries": 4}),
+    ([], 100, 0.02, 8_000, {"gap_tab_k": 14, "gap_resume_iters": 20, "gap_resume_entries": 4}),
     ([], 100, 0.01, 30_000, {"gap_tab_k": 12, "gap_tail_lanes": 64, "gap_tail_iters": 5})])
 def test_gpu_equals_oracle(mid_genome, argv, ln, sub, n, tune):
     ascii_, lens, eng, b0, b1 = mid_genome
