@@ -762,23 +762,41 @@ inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, cons
     const uint64_t n = std::min<uint64_t>((uint64_t)l, l_pac - at);
     return (int)extract(b, at, (uint32_t)n, rb.data());
   };
+  // bases [0, n) of rb against seq[y, y + n): the mismatches into the MD string; eight equal bytes at a
+  // time are eight matches (extracted codes are 0-3, so equal bytes exclude an N); c ends as rb[n - 1]
+  auto md_run = [&](int n, uint64_t yy) {
+    int z = 0;
+    while (z < n) {
+      if (z + 8 <= n) {
+        uint64_t ra, sb;
+        memcpy(&ra, rb.data() + z, 8);
+        memcpy(&sb, seq + yy + z, 8);
+        if (ra == sb) {
+          u += 8;
+          z += 8;
+          continue;
+        }
+      }
+      c = rb[z];
+      if (c > 3 || seq[yy + z] > 3 || c != seq[yy + z]) {
+        put_int(u);
+        str += "ACGTN"[c];
+        ++nm;
+        u = 0;
+      } else {
+        ++u;
+      }
+      ++z;
+    }
+    if (n > 0) c = rb[n - 1];
+  };
   if (s.has_cigar) {
     for (uint32_t cg : s.cigar) {
       const int l = (int)cig_len(cg);
       const uint32_t op = cig_op(cg);
       if (op == FROM_M) {
         const int n = run(x, l);
-        for (int z = 0; z < n; ++z) {
-          c = rb[z];
-          if (c > 3 || seq[y + z] > 3 || c != seq[y + z]) {
-            put_int(u);
-            str += "ACGTN"[c];
-            ++nm;
-            u = 0;
-          } else {
-            ++u;
-          }
-        }
+        md_run(n, y);
         x += l; y += l;
       } else if (op == FROM_I || op == FROM_S) {
         y += l;
@@ -798,8 +816,8 @@ inline std::string cal_md1(const Read &s, uint64_t pos, const uint8_t *seq, cons
   } else {
     // past l_pac nothing is extracted: c keeps the last base's value (as the reference)
     const int n = run(x, s.len);
-    for (int z = 0; z < s.len; ++z) {
-      if (z < n) c = rb[z];
+    md_run(n, y);
+    for (int z = n; z < s.len; ++z) {
       if (c > 3 || seq[y + z] > 3 || c != seq[y + z]) {
         put_int(u);
         str += "ACGTN"[c];
