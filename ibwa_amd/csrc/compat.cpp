@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <thread>
@@ -493,8 +494,14 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
   for (int64_t j = 0, acc = 0; j < m; ++j) { cfirst[j] = acc; acc += ncig[j]; }
   const double prior_term = -4.343 * log(ii->ap_prior / l_pac);
   const int new_term = (int)(-4.343 * log(.5 * erfc(M_SQRT1_2 * 1.5) + .499));
-  int64_t j = 0;
-  for (int i = 0; i < n_seqs; ++i) {
+  // each pair's fix-up reads and writes only its own two reads: contiguous pair ranges on the host
+  // threads, the counts summed after
+  std::vector<uint64_t> nmap(2 * (size_t)nt, 0);
+  std::atomic<int> oom{0};
+  auto fix = [&](int t) {
+  const int i0 = (int)((int64_t)n_seqs * t / nt), i1 = (int)((int64_t)n_seqs * (t + 1) / nt);
+  int64_t j = std::lower_bound(cand.begin(), cand.end(), i0, [](const Cand &c, int v) { return c.pair < v; }) - cand.begin();
+  for (int i = i0; i < i1; ++i) {
     if (single[i] < 0) continue;
     ibwa_ref_seq_t *p[2] = {seqs[0] + i, seqs[1] + i};
     const uint32_t *cg[2] = {nullptr, nullptr};
@@ -535,7 +542,7 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
       k = 1, mapQ = p[0]->mapQ;
     }
     if (k < 0 || p[k]->pos == (uint64_t)bg[k]) continue;
-    ++n_mapped[single[i]];
+    ++nmap[2 * (size_t)t + (size_t)single[i]];
     ibwa_ref_seq_t *fx = p[k], *rf = p[1 - k];
     int tmp = (int)rf->mapQ - fx->mapQ / 2 - 8;
     if (tmp <= 0) tmp = 1;
@@ -546,7 +553,7 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
     if ((int)fx->seQ > mq_adjust[k]) fx->seQ = mq_adjust[k];
     free(fx->cigar);
     fx->cigar = (uint32_t *)malloc(sizeof(uint32_t) * nc[k]);
-    if (!fx->cigar) { ibwa_free(cig); return IBWA_EHIP; }
+    if (!fx->cigar) { oom = 1; return; }
     memcpy(fx->cigar, cg[k], sizeof(uint32_t) * nc[k]);
     fx->n_cigar = nc[k];
     // __set_fixed (bwasw.c:167-178)
@@ -561,7 +568,19 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
     fx->extra_flag |= IBWA_SAM_FPP;
     rf->extra_flag |= IBWA_SAM_FPP;
   }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(fix, t);
+    fix(0);
+    for (auto &x : th) x.join();
+  }
+  for (int t = 0; t < nt; ++t) {
+    n_mapped[0] += nmap[2 * (size_t)t];
+    n_mapped[1] += nmap[2 * (size_t)t + 1];
+  }
   ibwa_free(cig);
+  if (oom) return IBWA_EHIP;
   if (stats) {
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
