@@ -499,75 +499,75 @@ int paired_sw_core(ibwa_ctx_t *ctx, int n_seqs, ibwa_ref_seq_t *seqs[2], const i
   std::vector<uint64_t> nmap(2 * (size_t)nt, 0);
   std::atomic<int> oom{0};
   auto fix = [&](int t) {
-  const int i0 = (int)((int64_t)n_seqs * t / nt), i1 = (int)((int64_t)n_seqs * (t + 1) / nt);
-  int64_t j = std::lower_bound(cand.begin(), cand.end(), i0, [](const Cand &c, int v) { return c.pair < v; }) - cand.begin();
-  for (int i = i0; i < i1; ++i) {
-    if (single[i] < 0) continue;
-    ibwa_ref_seq_t *p[2] = {seqs[0] + i, seqs[1] + i};
-    const uint32_t *cg[2] = {nullptr, nullptr};
-    int nc[2] = {0, 0}, mq_adjust[2] = {255, 255};
-    int64_t bg[2] = {0, 0};
-    uint32_t ct[2] = {0, 0};
-    for (; j < m && cand[j].pair == i; ++j) {
-      const int k = cand[j].k;
-      bg[k] = beg[j];
-      if (!ncig[j]) continue;
-      cg[k] = cig + cfirst[j];
-      nc[k] = ncig[j];
-      ct[k] = cnt[j];
-      if (p[k]->type != IBWA_TYPE_NO_MATCH) {  // re-evaluate (bwasw.c:222-236)
-        int clip = 0;
-        if ((cg[k][0] >> 29) == 3) clip += cg[k][0] & 0x1fffffff;
-        if ((cg[k][nc[k] - 1] >> 29) == 3) clip += cg[k][nc[k] - 1] & 0x1fffffff;
-        int s_old = (int)((p[k]->n_mm * 9 + p[k]->n_gapo * 13 + p[k]->n_gape * 2) / 3. * 8. + .499);
-        int s_new = (int)(((ct[k] >> 16) * 9 + (ct[k] >> 8 & 0xff) * 13 + (ct[k] & 0xff) * 2 + clip * 3) / 3. * 8. + .499);
-        s_old += prior_term;
-        s_new += new_term;
-        if (s_old < s_new) {
-          mq_adjust[k] = s_new - s_old;
-          cg[k] = nullptr;
-          nc[k] = 0;
-        } else {
-          mq_adjust[k] = s_old - s_new;
+    const int i0 = (int)((int64_t)n_seqs * t / nt), i1 = (int)((int64_t)n_seqs * (t + 1) / nt);
+    int64_t j = std::lower_bound(cand.begin(), cand.end(), i0, [](const Cand &c, int v) { return c.pair < v; }) - cand.begin();
+    for (int i = i0; i < i1; ++i) {
+      if (single[i] < 0) continue;
+      ibwa_ref_seq_t *p[2] = {seqs[0] + i, seqs[1] + i};
+      const uint32_t *cg[2] = {nullptr, nullptr};
+      int nc[2] = {0, 0}, mq_adjust[2] = {255, 255};
+      int64_t bg[2] = {0, 0};
+      uint32_t ct[2] = {0, 0};
+      for (; j < m && cand[j].pair == i; ++j) {
+        const int k = cand[j].k;
+        bg[k] = beg[j];
+        if (!ncig[j]) continue;
+        cg[k] = cig + cfirst[j];
+        nc[k] = ncig[j];
+        ct[k] = cnt[j];
+        if (p[k]->type != IBWA_TYPE_NO_MATCH) {  // re-evaluate (bwasw.c:222-236)
+          int clip = 0;
+          if ((cg[k][0] >> 29) == 3) clip += cg[k][0] & 0x1fffffff;
+          if ((cg[k][nc[k] - 1] >> 29) == 3) clip += cg[k][nc[k] - 1] & 0x1fffffff;
+          int s_old = (int)((p[k]->n_mm * 9 + p[k]->n_gapo * 13 + p[k]->n_gape * 2) / 3. * 8. + .499);
+          int s_new = (int)(((ct[k] >> 16) * 9 + (ct[k] >> 8 & 0xff) * 13 + (ct[k] & 0xff) * 2 + clip * 3) / 3. * 8. + .499);
+          s_old += prior_term;
+          s_new += new_term;
+          if (s_old < s_new) {
+            mq_adjust[k] = s_new - s_old;
+            cg[k] = nullptr;
+            nc[k] = 0;
+          } else {
+            mq_adjust[k] = s_old - s_new;
+          }
         }
       }
+      int k = -1, mapQ = 0;
+      if (cg[0] && cg[1]) {
+        k = p[0]->mapQ < p[1]->mapQ ? 0 : 1;
+        mapQ = abs((int)p[1]->mapQ - (int)p[0]->mapQ);
+      } else if (cg[0]) {
+        k = 0, mapQ = p[1]->mapQ;
+      } else if (cg[1]) {
+        k = 1, mapQ = p[0]->mapQ;
+      }
+      if (k < 0 || p[k]->pos == (uint64_t)bg[k]) continue;
+      ++nmap[2 * (size_t)t + (size_t)single[i]];
+      ibwa_ref_seq_t *fx = p[k], *rf = p[1 - k];
+      int tmp = (int)rf->mapQ - fx->mapQ / 2 - 8;
+      if (tmp <= 0) tmp = 1;
+      if (mapQ > tmp) mapQ = tmp;
+      fx->mapQ = rf->mapQ = mapQ;
+      fx->seQ = rf->seQ = rf->seQ < (uint64_t)mapQ ? rf->seQ : (uint64_t)mapQ;
+      if ((int)fx->mapQ > mq_adjust[k]) fx->mapQ = mq_adjust[k];
+      if ((int)fx->seQ > mq_adjust[k]) fx->seQ = mq_adjust[k];
+      free(fx->cigar);
+      fx->cigar = (uint32_t *)malloc(sizeof(uint32_t) * nc[k]);
+      if (!fx->cigar) { oom = 1; return; }
+      memcpy(fx->cigar, cg[k], sizeof(uint32_t) * nc[k]);
+      fx->n_cigar = nc[k];
+      // __set_fixed (bwasw.c:167-178)
+      fx->type = IBWA_TYPE_MATESW;
+      fx->pos = fx->remapped_pos = (uint64_t)bg[k];
+      fx->dbidx = fx->remapped_dbidx = 0;
+      fx->seQ = rf->seQ;
+      fx->strand = std_pe ? 1 - rf->strand : rf->strand;
+      fx->n_mm = ct[k] >> 16;
+      fx->n_gapo = ct[k] >> 8 & 0xff;
+      fx->n_gape = ct[k] & 0xff;
+      fx->extra_flag |= IBWA_SAM_FPP;
+      rf->extra_flag |= IBWA_SAM_FPP;
     }
-    int k = -1, mapQ = 0;
-    if (cg[0] && cg[1]) {
-      k = p[0]->mapQ < p[1]->mapQ ? 0 : 1;
-      mapQ = abs((int)p[1]->mapQ - (int)p[0]->mapQ);
-    } else if (cg[0]) {
-      k = 0, mapQ = p[1]->mapQ;
-    } else if (cg[1]) {
-      k = 1, mapQ = p[0]->mapQ;
-    }
-    if (k < 0 || p[k]->pos == (uint64_t)bg[k]) continue;
-    ++nmap[2 * (size_t)t + (size_t)single[i]];
-    ibwa_ref_seq_t *fx = p[k], *rf = p[1 - k];
-    int tmp = (int)rf->mapQ - fx->mapQ / 2 - 8;
-    if (tmp <= 0) tmp = 1;
-    if (mapQ > tmp) mapQ = tmp;
-    fx->mapQ = rf->mapQ = mapQ;
-    fx->seQ = rf->seQ = rf->seQ < (uint64_t)mapQ ? rf->seQ : (uint64_t)mapQ;
-    if ((int)fx->mapQ > mq_adjust[k]) fx->mapQ = mq_adjust[k];
-    if ((int)fx->seQ > mq_adjust[k]) fx->seQ = mq_adjust[k];
-    free(fx->cigar);
-    fx->cigar = (uint32_t *)malloc(sizeof(uint32_t) * nc[k]);
-    if (!fx->cigar) { oom = 1; return; }
-    memcpy(fx->cigar, cg[k], sizeof(uint32_t) * nc[k]);
-    fx->n_cigar = nc[k];
-    // __set_fixed (bwasw.c:167-178)
-    fx->type = IBWA_TYPE_MATESW;
-    fx->pos = fx->remapped_pos = (uint64_t)bg[k];
-    fx->dbidx = fx->remapped_dbidx = 0;
-    fx->seQ = rf->seQ;
-    fx->strand = std_pe ? 1 - rf->strand : rf->strand;
-    fx->n_mm = ct[k] >> 16;
-    fx->n_gapo = ct[k] >> 8 & 0xff;
-    fx->n_gape = ct[k] & 0xff;
-    fx->extra_flag |= IBWA_SAM_FPP;
-    rf->extra_flag |= IBWA_SAM_FPP;
-  }
   };
   {
     std::vector<std::thread> th;
