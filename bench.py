@@ -873,6 +873,8 @@ def main():
                 pmc = pmc_traffic(kn, result["config"]["workload"])
                 pk[name] = {"algorithmic_bytes_per_step": ab, "kernel_ms_per_step": ms, "achieved": ach,
                             "frac": ach / HBM_PEAK_GBS, "touches_per_read": tt / args.reads,
+                            # the GPU side of the same count: HBM bytes (the PMC file's) in 64 B units per read
+                            "gpu_touches_per_read": pmc[0] / 64.0 / args.reads if pmc else None,
                             "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
                             "traffic_over_algorithmic": pmc[0] / ab if pmc and ab > 0 else None}
             ach = touches * 64.0 * args.reads / (k_ms * 1e-3) / 1e9
@@ -894,6 +896,9 @@ def main():
                                            "kernel_ms": k_ms, "touches_per_read": touches,
                                            "traffic": pmc[0] if pmc else None,
                                            "traffic_source": pmc[1] if pmc else None},
+                                  "touches_note": "touches_per_read: the reference's 64 B rank-query touches per read "
+                                                  "(oracle/ibwa_oracle.c counters on the sample); gpu_touches_per_read: "
+                                                  "the kernel's measured HBM bytes per read / 64 (traffic_source)",
                                   "touches_sample": f"first {ns_} reads ({int(resumed.sum())} of them resumed and "
                                                     f"{int(scratch.sum())} re-run by the cooperative pass), "
                                                     f"oracle/ibwa_oracle.c touch counter split at each resumed "
